@@ -1,0 +1,208 @@
+/*
+ * pinot_hip.h -- C ABI of libpinot_hip.so, the MI355X-native segment query hot path.
+ *
+ * Drop-in boundary. The reference's Java server keeps its operator surface and
+ * calls these entry points through Java 21 FFM (INTEGRATION.md shows the bindings):
+ *
+ *   phip_segment_load    <- ImmutableSegmentLoader.load
+ *                           (pinot-segment-local/.../indexsegment/immutable/ImmutableSegmentLoader.java:155-190,
+ *                           222-280): per column the forward index, dictionary and inverted index
+ *                           buffers that PhysicalColumnIndexContainer (…/segment/index/column/
+ *                           PhysicalColumnIndexContainer.java:44-68) maps, handed over as raw bytes
+ *                           (PinotDataBuffer.toDirectByteBuffer, pinot-segment-spi/.../memory/
+ *                           PinotDataBuffer.java:671-696) and pinned in HBM.
+ *   phip_segment_unload  <- IndexSegment.destroy
+ *   phip_query           <- InstancePlanMakerImplV2.makeInstancePlan
+ *                           (pinot-core/.../plan/maker/InstancePlanMakerImplV2.java:172-199) when the
+ *                           query option selects the GPU: one call replaces, for all segments of the
+ *                           query, FilterPlanNode/BaseFilterOperator.getTrues
+ *                           (pinot-core/.../operator/filter/BaseFilterOperator.java:85-93),
+ *                           AggregationOperator.getNextBlock (…/operator/query/AggregationOperator.java:63-80),
+ *                           GroupByOperator.getNextBlock (…/operator/query/GroupByOperator.java:100-140)
+ *                           and the CombineOperator merge (…/operator/combine/BaseSingleBlockCombineOperator.java:58-162).
+ *                           Results are the intermediate values AggregationResultsBlock /
+ *                           GroupByResultsBlock carry (…/operator/blocks/results/).
+ *   phip_filter_bitmap   <- BaseFilterOperator.getTrues / getBitmaps for one segment (doc-id set as
+ *                           64-doc bitmap words; the bit for doc d is bit d%64 of word d/64).
+ *
+ * Conventions: every function returns int32_t status (PHIP_OK = 0); on error the calling
+ * thread's message is available from phip_last_error(). Host buffers passed in are borrowed for
+ * the duration of the call only; the library owns all device memory. All entry points are
+ * thread-safe (per-device mutex). No HIP/torch types cross the boundary.
+ */
+#ifndef PINOT_HIP_H_
+#define PINOT_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+#define PHIP_EXTERN extern "C"
+#else
+#define PHIP_EXTERN extern
+#endif
+#define PHIP_API PHIP_EXTERN __attribute__((visibility("default")))
+
+/* ---- status ------------------------------------------------------------------------------ */
+#define PHIP_OK 0
+#define PHIP_ERR_INVALID 1     /* malformed descriptor / plan */
+#define PHIP_ERR_HIP 2         /* a HIP runtime call failed */
+#define PHIP_ERR_UNSUPPORTED 3 /* shape outside the GPU subset: caller falls back to the Java path */
+#define PHIP_ERR_NOT_FOUND 4   /* unknown segment handle or column */
+#define PHIP_ERR_NO_DEVICE 5   /* no usable GPU */
+
+/* ---- stored data types (FieldSpec.DataType, single-value) ---------------------------------- */
+#define PHIP_TYPE_INT 0
+#define PHIP_TYPE_LONG 1
+#define PHIP_TYPE_FLOAT 2
+#define PHIP_TYPE_DOUBLE 3
+#define PHIP_TYPE_STRING 4
+
+/* ---- forward index encodings -------------------------------------------------------------- */
+#define PHIP_FWD_FIXED_BIT 0 /* FixedBitSVForwardIndexWriter: ceil(N*b/8) BE bytes, MSB first */
+#define PHIP_FWD_SORTED 1    /* SortedIndexReaderImpl: card x (start,end) BE int32, inclusive */
+#define PHIP_FWD_RAW_CHUNK 2 /* BaseChunkForwardIndexWriter v2/v3, PASS_THROUGH fixed-width */
+
+typedef struct phip_column_desc {
+  const char *name;
+  int32_t data_type;      /* PHIP_TYPE_* */
+  int32_t fwd_kind;       /* PHIP_FWD_* */
+  int32_t cardinality;    /* dictionary length (0 for raw columns) */
+  int32_t bits_per_value; /* fixed-bit width: getNumBitsPerValue(card-1) */
+  int32_t string_width;   /* STRING dictionary: bytes per '\0'-padded entry */
+  int32_t reserved;
+  const uint8_t *forward;
+  uint64_t forward_bytes;
+  const uint8_t *dictionary; /* BE fixed-width sorted values (NULL for raw columns) */
+  uint64_t dictionary_bytes;
+  const uint8_t *inverted; /* (card+1) BE u32 offsets + portable Roaring bitmaps, or NULL */
+  uint64_t inverted_bytes;
+} phip_column_desc;
+
+typedef struct phip_segment_desc {
+  const char *name;
+  int32_t device;      /* device ordinal, -1 = current default device */
+  int32_t num_docs;
+  int32_t num_columns;
+  int32_t reserved;
+  const phip_column_desc *columns;
+} phip_segment_desc;
+
+/* ---- filter program ----------------------------------------------------------------------
+ * Per segment, a preorder tree: an AND/OR node is followed by its num_children subtrees; NOT by
+ * one subtree. Leaves carry the per-segment outcome of the reference's PredicateEvaluator
+ * (dictionary ids are per segment): RangePredicateEvaluatorFactory (dict-id range [lo,hi)),
+ * In/NotIn/Eq/NotEq evaluators (dict-id set), SortedIndexBasedFilterOperator (doc ranges) or
+ * InvertedIndexFilterOperator (dict ids whose bitmaps are OR-ed, complemented if exclusive). */
+#define PHIP_NODE_LEAF 0
+#define PHIP_NODE_AND 1
+#define PHIP_NODE_OR 2
+#define PHIP_NODE_NOT 3
+
+#define PHIP_LEAF_MATCH_ALL 0  /* predicate alwaysTrue for this segment */
+#define PHIP_LEAF_MATCH_NONE 1 /* predicate alwaysFalse for this segment */
+#define PHIP_LEAF_DICT_RANGE 2 /* scan forward index: lo <= dictId < hi */
+#define PHIP_LEAF_DICT_SET 3   /* scan forward index: dictId in ids (xor exclusive) */
+#define PHIP_LEAF_DOC_RANGES 4 /* ids = count x (startDoc, endDoc) inclusive, sorted, disjoint */
+#define PHIP_LEAF_INVERTED 5   /* OR of inverted-index bitmaps of ids (xor exclusive) */
+
+typedef struct phip_filter_node {
+  int32_t op;           /* PHIP_NODE_* */
+  int32_t num_children; /* AND/OR */
+  int32_t leaf_kind;    /* PHIP_LEAF_* */
+  int32_t column;       /* index into phip_query_desc.columns */
+  int32_t lo, hi;       /* DICT_RANGE */
+  int32_t exclusive;    /* DICT_SET / INVERTED */
+  int32_t count;        /* number of ids (DICT_SET/INVERTED) or of ranges (DOC_RANGES) */
+  const int32_t *ids;
+} phip_filter_node;
+
+/* ---- aggregations ------------------------------------------------------------------------- */
+#define PHIP_AGG_COUNT 0 /* CountAggregationFunction */
+#define PHIP_AGG_SUM 1   /* SumAggregationFunction (int64 exact for INT/LONG inputs, f64 otherwise) */
+#define PHIP_AGG_MIN 2   /* MinAggregationFunction (default +inf) */
+#define PHIP_AGG_MAX 3   /* MaxAggregationFunction (default -inf) */
+#define PHIP_AGG_HLL 4   /* DistinctCountHLLAggregationFunction: HyperLogLog(log2m) registers */
+
+#define PHIP_EXPR_COLUMN 0 /* a */
+#define PHIP_EXPR_ADD 1    /* a + b   (AdditionTransformFunction) */
+#define PHIP_EXPR_SUB 2    /* a - b   (SubtractionTransformFunction.java:99-124) */
+#define PHIP_EXPR_MUL 3    /* a * b   (MultiplicationTransformFunction.java:90-106) */
+
+typedef struct phip_aggregation {
+  int32_t function; /* PHIP_AGG_* */
+  int32_t expr;     /* PHIP_EXPR_* (ignored for COUNT) */
+  int32_t column_a; /* index into phip_query_desc.columns */
+  int32_t column_b;
+  int32_t log2m; /* HLL */
+  int32_t reserved;
+} phip_aggregation;
+
+typedef struct phip_query_desc {
+  int32_t num_columns;
+  int32_t num_segments;
+  const char *const *columns; /* column names; nodes/aggregations refer to them by index */
+  const uint64_t *segments;   /* handles from phip_segment_load */
+  const int32_t *filter_offsets;          /* [num_segments+1] into filter_nodes; empty = match all */
+  const phip_filter_node *filter_nodes;
+  int32_t num_aggregations;
+  int32_t num_group_by;
+  const phip_aggregation *aggregations;
+  const int32_t *group_by_columns; /* indices into columns */
+  int64_t num_groups_limit;        /* InstancePlanMakerImplV2 numGroupsLimit (default 100,000) */
+} phip_query_desc;
+
+/* ---- results ------------------------------------------------------------------------------
+ * Library-owned, valid until phip_result_free. For an aggregation-only query num_groups = 1.
+ * values[g*num_aggregations + a] holds SUM/MIN/MAX/COUNT as double (HLL: estimate);
+ * long_values[...] the exact int64 SUM (integral inputs) or COUNT.
+ * hll_registers: [num_groups][num_hll][1 << log2m] u8 in aggregation order of the HLL aggs.
+ * group_keys[g*num_group_by + k]: id in the query-global dictionary of group-by column k;
+ * phip_result_dictionary returns that dictionary's values. */
+typedef struct phip_result {
+  int64_t num_docs_scanned;
+  int64_t num_entries_scanned_in_filter;
+  int64_t num_entries_scanned_post_filter;
+  int64_t num_total_docs;
+  int32_t num_segments_processed;
+  int32_t num_segments_matched;
+  int32_t num_groups_limit_reached;
+  int32_t num_aggregations;
+  int64_t num_groups;
+  int32_t num_group_by;
+  int32_t num_hll;
+  const double *values;
+  const int64_t *long_values;
+  const uint8_t *hll_registers;
+  const int32_t *group_keys;
+  double scan_kernel_ms; /* device time of the fused filter/aggregate kernel(s) */
+  double device_ms;      /* device time of the whole query on the stream */
+} phip_result;
+
+typedef struct phip_dictionary_view {
+  int32_t data_type;
+  int32_t cardinality;
+  int32_t string_width;
+  int32_t reserved;
+  const void *values; /* LE int32/int64/float/double array, or card x string_width bytes */
+} phip_dictionary_view;
+
+/* ---- entry points -------------------------------------------------------------------------- */
+PHIP_API int32_t phip_init(const int32_t *devices, int32_t num_devices);
+PHIP_API int32_t phip_shutdown(void);
+PHIP_API int32_t phip_device_count(int32_t *out_count);
+PHIP_API const char *phip_last_error(void);
+PHIP_API const char *phip_version(void);
+
+PHIP_API int32_t phip_segment_load(const phip_segment_desc *desc, uint64_t *out_handle);
+PHIP_API int32_t phip_segment_unload(uint64_t handle);
+PHIP_API int32_t phip_segment_device_bytes(uint64_t handle, uint64_t *out_bytes);
+
+PHIP_API int32_t phip_query(const phip_query_desc *query, phip_result **out_result);
+PHIP_API int32_t phip_result_dictionary(const phip_result *result, int32_t group_by_index,
+                                        phip_dictionary_view *out_view);
+PHIP_API void phip_result_free(phip_result *result);
+
+/* Filter only, one segment: words_out receives ceil(num_docs/64) bitmap words. */
+PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *words_out, int64_t num_words);
+
+#endif /* PINOT_HIP_H_ */

@@ -1,0 +1,324 @@
+"""Reference-semantics CPU executor over Pinot segment encodings -- TEST INFRASTRUCTURE ONLY.
+
+Restates, per segment, what the reference's CPU server path computes:
+  * forward index decode     PinotDataBitSet.readInt (pinot-segment-local/.../io/util/PinotDataBitSet.java:74-96),
+                             SortedIndexReaderImpl (…/readers/sorted/SortedIndexReaderImpl.java:114-116),
+                             FixedByteChunkSVForwardIndexReader (…/readers/forward/FixedByteChunkSVForwardIndexReader.java:63-72)
+  * leaf operator choice     FilterOperatorUtils.DefaultImplementation (pinot-core/.../operator/filter/FilterOperatorUtils.java:98-131):
+                             sorted index -> doc ranges, inverted index -> OR of Roaring bitmaps
+                             (InvertedIndexFilterOperator.java:59-96), else a scan of values
+  * predicate semantics      on VALUES (dictionary value compared with the literal), an independent
+                             route from the product's dict-id ranges
+  * boolean algebra          AndDocIdSet / OrDocIdSet / NotDocIdSet as set algebra on doc masks
+  * aggregation              SumAggregationFunction.aggregate (:69-146): double per <=10,000-doc block then
+                             holder += block (DocIdSetPlanNode.java:29); Min/Max (+inf/-inf defaults);
+                             Count; DistinctCountHLL offers each matched dictionary value
+                             (DistinctCountHLLAggregationFunction.java:105-111,457-466)
+  * group-by                 keys = tuples of values; DoubleGroupByResultHolder adds per doc in doc order
+                             (…/groupby/DoubleGroupByResultHolder.java:94-98)
+Intermediate results use the product's results containers (plain data) so the same broker reduce
+renders both; exact integer sums are reported beside the double ones (``exact_sums``).
+"""
+import numpy as np
+
+from . import lib as _oracle_lib
+
+_BE = {0: ">i4", 1: ">i8", 2: ">f4", 3: ">f8"}
+_NATIVE = {0: np.int64, 1: np.int64, 2: np.float64, 3: np.float64}
+MAX_DOC_PER_CALL = 10_000
+
+
+class OracleSegment:
+    """Reads an ImmutableSegment's index bytes (never its source values)."""
+
+    def __init__(self, seg):
+        self.seg = seg
+        self.num_docs = seg.num_docs
+        self._ids = {}
+        self._vals = {}
+        self._dict = {}
+
+    def meta(self, c):
+        return self.seg.columns[c].metadata
+
+    def dictionary(self, c):
+        d = self._dict.get(c)
+        if d is None:
+            ci = self.seg.columns[c]
+            m = ci.metadata
+            if int(m.data_type) == 4:
+                w = m.string_width
+                d = np.array([ci.dictionary[i * w:(i + 1) * w].rstrip(b"\0").decode("utf-8")
+                              for i in range(m.cardinality)], dtype=object)
+            else:
+                d = np.frombuffer(ci.dictionary, dtype=_BE[int(m.data_type)]).astype(_NATIVE[int(m.data_type)])
+            self._dict[c] = d
+        return d
+
+    def dict_ids(self, c):
+        ids = self._ids.get(c)
+        if ids is None:
+            ci = self.seg.columns[c]
+            m = ci.metadata
+            L = _oracle_lib()
+            ids = np.empty(max(self.num_docs, 1), dtype=np.int32)
+            fwd = np.frombuffer(ci.forward, dtype=np.uint8)
+            if m.is_sorted:
+                rc = L.oracle_sorted_dict_ids(fwd.ctypes.data, m.cardinality, self.num_docs, ids.ctypes.data)
+                assert rc == 0, "bad sorted index"
+            else:
+                L.oracle_read_fixed_bit(fwd.ctypes.data, m.bits_per_element, 0, self.num_docs, ids.ctypes.data)
+            ids = ids[:self.num_docs]
+            self._ids[c] = ids
+        return ids
+
+    def values(self, c):
+        v = self._vals.get(c)
+        if v is None:
+            ci = self.seg.columns[c]
+            m = ci.metadata
+            if m.has_dictionary:
+                v = self.dictionary(c)[self.dict_ids(c)]
+            else:
+                v = _read_raw_chunk(ci.forward, int(m.data_type), self.num_docs)
+            self._vals[c] = v
+        return v
+
+    def inverted_docs(self, c, dict_id):
+        ci = self.seg.columns[c]
+        card = ci.metadata.cardinality
+        buf = np.frombuffer(ci.inverted, dtype=np.uint8)
+        offs = np.frombuffer(ci.inverted, dtype=">u4", count=card + 1).astype(np.int64)
+        hdr = (card + 1) * 4
+        o0, o1 = offs[dict_id] - offs[0] + hdr, offs[dict_id + 1] - offs[0] + hdr
+        out = np.empty(max(self.num_docs, 1), dtype=np.int32)
+        n = _oracle_lib().oracle_roaring_decode(buf[o0:o1].ctypes.data, int(o1 - o0), out.ctypes.data, len(out))
+        assert n >= 0, "bad roaring bitmap"
+        return out[:n]
+
+
+def _read_raw_chunk(buf, dtype, n):
+    h = np.frombuffer(buf, dtype=">i4", count=7)
+    version, num_chunks, per_chunk, entry, total, comp, data_hdr = [int(x) for x in h]
+    assert comp == 0 and total == n
+    osz = 4 if version == 2 else 8
+    offs = np.frombuffer(buf, dtype=">i4" if osz == 4 else ">i8", count=num_chunks, offset=data_hdr)
+    parts = []
+    for k in range(num_chunks):
+        docs = min(per_chunk, n - k * per_chunk)
+        parts.append(np.frombuffer(buf, dtype=_BE[dtype], count=docs, offset=int(offs[k])))
+    return np.concatenate(parts).astype(_NATIVE[dtype]) if parts else np.zeros(0, _NATIVE[dtype])
+
+
+# ----------------------------------------------------------------------------------- filter
+def _literal(m, lit):
+    if int(m.data_type) == 4:
+        return str(lit)
+    return lit
+
+
+def _pred_on_values(pred, vals, m):
+    t = pred.type
+    if t in ("EQ", "NOT_EQ", "IN", "NOT_IN"):
+        lits = [_literal(m, v) for v in pred.values]
+        hit = np.zeros(len(vals), dtype=bool)
+        for lv in lits:
+            hit |= (vals == lv)
+        return ~hit if t in ("NOT_EQ", "NOT_IN") else hit
+    ok = np.ones(len(vals), dtype=bool)
+    if pred.lower != "*":
+        lo = _literal(m, pred.lower)
+        ok &= (vals >= lo) if pred.lower_inclusive else (vals > lo)
+    if pred.upper != "*":
+        hi = _literal(m, pred.upper)
+        ok &= (vals <= hi) if pred.upper_inclusive else (vals < hi)
+    return ok
+
+
+def eval_filter(os_: OracleSegment, fc):
+    n = os_.num_docs
+    if fc is None:
+        return np.ones(n, dtype=bool)
+    if fc.type == "AND":
+        m = np.ones(n, dtype=bool)
+        for c in fc.children:
+            m &= eval_filter(os_, c)
+        return m
+    if fc.type == "OR":
+        m = np.zeros(n, dtype=bool)
+        for c in fc.children:
+            m |= eval_filter(os_, c)
+        return m
+    if fc.type == "NOT":
+        return ~eval_filter(os_, fc.children[0])
+    if fc.type == "CONSTANT":
+        return np.full(n, bool(fc.constant))
+    pred = fc.predicate
+    col = pred.column
+    m = os_.meta(col)
+    if m.has_dictionary and (m.is_sorted or (m.has_inverted_index and pred.type != "RANGE")):
+        dict_match = _pred_on_values(pred, os_.dictionary(col), m)
+        out = np.zeros(n, dtype=bool)
+        if m.is_sorted:
+            pairs = np.frombuffer(os_.seg.columns[col].forward, dtype=">i4").reshape(-1, 2)
+            for d in np.nonzero(dict_match)[0]:
+                out[pairs[d, 0]:pairs[d, 1] + 1] = True
+        else:
+            for d in np.nonzero(dict_match)[0]:
+                out[os_.inverted_docs(col, int(d))] = True
+        return out
+    return _pred_on_values(pred, os_.values(col), m)
+
+
+# ----------------------------------------------------------------------------------- expressions
+def _expr_values(os_, e, docs):
+    from pinot_amd.query.context import Function, Identifier, Literal
+    if isinstance(e, Identifier):
+        v = os_.values(e.name)[docs]
+        return v
+    if isinstance(e, Literal):
+        return np.full(len(docs), float(e.value))
+    if isinstance(e, Function):
+        if e.name == "cast":
+            v = _expr_values(os_, e.args[0], docs)
+            return v.astype(np.float64) if str(e.args[1].value).upper() in ("DOUBLE", "FLOAT") else v
+        a = _expr_values(os_, e.args[0], docs).astype(np.float64)
+        b = _expr_values(os_, e.args[1], docs).astype(np.float64)
+        if e.name == "times":
+            return 1.0 * a * b  # MultiplicationTransformFunction.java:90-106
+        if e.name == "minus":
+            return a - b
+        if e.name == "plus":
+            return a + b
+        if e.name == "divide":
+            return a / b
+    raise NotImplementedError(str(e))
+
+
+def _exact_values(os_, e, docs):
+    """Exact integer value of an INT/LONG-only expression, or None."""
+    from pinot_amd.query.context import Function, Identifier
+    if isinstance(e, Identifier):
+        if int(os_.meta(e.name).data_type) in (0, 1):
+            return os_.values(e.name)[docs].astype(object if False else np.int64)
+        return None
+    if isinstance(e, Function):
+        if e.name == "cast":
+            return _exact_values(os_, e.args[0], docs)
+        if e.name in ("times", "minus", "plus") and len(e.args) == 2:
+            a, b = _exact_values(os_, e.args[0], docs), _exact_values(os_, e.args[1], docs)
+            if a is None or b is None:
+                return None
+            return {"times": a * b, "minus": a - b, "plus": a + b}[e.name]
+    return None
+
+
+def _hll_registers(os_, col, docs, log2m):
+    L = _oracle_lib()
+    regs = np.zeros(1 << log2m, dtype=np.uint8)
+    m = os_.meta(col)
+    ids = np.unique(os_.dict_ids(col)[docs])
+    d = os_.dictionary(col)
+    t = int(m.data_type)
+    for i in ids.tolist():
+        v = d[i]
+        if t == 4:
+            b = v.encode("utf-8")
+            arr = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
+            x = L.oracle_murmur_hash_bytes(arr.ctypes.data, len(b), -1)
+        elif t in (0, 1):
+            x = L.oracle_murmur_hash_long(int(v))
+        elif t == 2:
+            x = L.oracle_murmur_hash_long(int(np.float32(v).view(np.int32)))
+        else:
+            x = L.oracle_murmur_hash_long(int(np.float64(v).view(np.int64)))
+        L.oracle_hll_offer_hashed(regs.ctypes.data, log2m, x)
+    return regs
+
+
+def _agg_segment(os_, ag, docs):
+    """Intermediate result of one aggregation over matched docs (ascending) of one segment."""
+    f = ag.function
+    if f == "count":
+        return len(docs), None
+    if f in ("distinctcounthll", "distinctcountrawhll"):
+        return _hll_registers(os_, ag.argument.name, docs, ag.log2m), None
+    vals = _expr_values(os_, ag.argument, docs).astype(np.float64)
+    if f == "sum":
+        s = _oracle_lib().oracle_block_sum_f64(np.ascontiguousarray(vals).ctypes.data, len(vals), MAX_DOC_PER_CALL)
+        ex = _exact_values(os_, ag.argument, docs)
+        return s, (int(ex.sum(dtype=np.int64)) if ex is not None else None)
+    if f == "min":
+        return (float(vals.min()) if len(vals) else float("inf")), None
+    if f == "max":
+        return (float(vals.max()) if len(vals) else float("-inf")), None
+    if f == "avg":
+        s = _oracle_lib().oracle_block_sum_f64(np.ascontiguousarray(vals).ctypes.data, len(vals), MAX_DOC_PER_CALL)
+        return (s, len(vals)), None
+    if f == "minmaxrange":
+        return ((float(vals.min()) if len(vals) else float("inf")),
+                (float(vals.max()) if len(vals) else float("-inf"))), None
+    raise NotImplementedError(f)
+
+
+def execute(query, segments):
+    """Server-side execution over ImmutableSegments -> (results block, exact_sums)."""
+    from pinot_amd.engine.results import (AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock,
+                                          merge_intermediate)
+    from pinot_amd.query.context import columns_of
+    stats = ExecutionStatistics()
+    projected = set()
+    for ag in query.aggregations:
+        if ag.argument is not None:
+            projected.update(columns_of(ag.argument))
+    for e in query.group_by:
+        projected.update(columns_of(e))
+    per_seg = []
+    for seg in segments:
+        os_ = OracleSegment(seg)
+        mask = eval_filter(os_, query.filter)
+        docs = np.nonzero(mask)[0]
+        stats.num_docs_scanned += len(docs)
+        stats.num_total_docs += seg.num_docs
+        stats.num_entries_scanned_post_filter += len(docs) * len(projected)
+        stats.num_segments_processed += 1
+        stats.num_segments_matched += int(len(docs) > 0)
+        per_seg.append((os_, docs))
+    if not query.group_by:
+        results, exact = None, None
+        for os_, docs in per_seg:
+            r = [_agg_segment(os_, ag, docs) for ag in query.aggregations]
+            vals = [x[0] for x in r]
+            exs = [x[1] for x in r]
+            if results is None:
+                results, exact = vals, exs
+            else:
+                results = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(query.aggregations, results, vals)]
+                exact = [(a + b) if a is not None and b is not None else None for a, b in zip(exact, exs)]
+        return AggregationResultsBlock(query.aggregations, results, stats), exact
+    groups, exact_groups = {}, {}
+    for os_, docs in per_seg:
+        if len(docs) == 0:
+            continue
+        keycols = [os_.values(e.name)[docs] for e in query.group_by]
+        keys = list(zip(*[k.tolist() for k in keycols]))
+        order = {}
+        for i, k in enumerate(keys):
+            order.setdefault(k, []).append(i)
+        for k, idx in order.items():
+            gdocs = docs[np.asarray(idx, dtype=np.int64)]
+            r = [_agg_segment(os_, ag, gdocs) for ag in query.aggregations]
+            vals = [x[0] for x in r]
+            exs = [x[1] for x in r]
+            if k in groups:
+                groups[k] = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(query.aggregations, groups[k], vals)]
+                exact_groups[k] = [(a + b) if a is not None and b is not None else None
+                                   for a, b in zip(exact_groups[k], exs)]
+            else:
+                groups[k] = vals
+                exact_groups[k] = exs
+    return GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats), exact_groups
+
+
+def filter_mask(query, segment):
+    return eval_filter(OracleSegment(segment), query.filter)

@@ -1,0 +1,135 @@
+"""ctypes binding of libpinot_hip.so (include/pinot_hip.h).
+
+This is the Python twin of the Java FFM binding shown in INTEGRATION.md. The product path has
+no CPU fallback: if the library cannot be loaded, or no GPU is present, calls raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpinot_hip.so")
+
+PHIP_OK = 0
+PHIP_ERR_INVALID = 1
+PHIP_ERR_HIP = 2
+PHIP_ERR_UNSUPPORTED = 3
+PHIP_ERR_NOT_FOUND = 4
+PHIP_ERR_NO_DEVICE = 5
+
+FWD_FIXED_BIT, FWD_SORTED, FWD_RAW_CHUNK = 0, 1, 2
+NODE_LEAF, NODE_AND, NODE_OR, NODE_NOT = 0, 1, 2, 3
+LEAF_MATCH_ALL, LEAF_MATCH_NONE, LEAF_DICT_RANGE, LEAF_DICT_SET, LEAF_DOC_RANGES, LEAF_INVERTED = range(6)
+AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_HLL = range(5)
+EXPR_COLUMN, EXPR_ADD, EXPR_SUB, EXPR_MUL = range(4)
+
+EXPORTED_SYMBOLS = (
+    "phip_init", "phip_shutdown", "phip_device_count", "phip_last_error", "phip_version",
+    "phip_segment_load", "phip_segment_unload", "phip_segment_device_bytes", "phip_query",
+    "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap",
+)
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class ColumnDesc(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data_type", ctypes.c_int32), ("fwd_kind", ctypes.c_int32),
+                ("cardinality", ctypes.c_int32), ("bits_per_value", ctypes.c_int32),
+                ("string_width", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("forward", ctypes.c_void_p), ("forward_bytes", ctypes.c_uint64),
+                ("dictionary", ctypes.c_void_p), ("dictionary_bytes", ctypes.c_uint64),
+                ("inverted", ctypes.c_void_p), ("inverted_bytes", ctypes.c_uint64)]
+
+
+class SegmentDesc(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("device", ctypes.c_int32), ("num_docs", ctypes.c_int32),
+                ("num_columns", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("columns", ctypes.POINTER(ColumnDesc))]
+
+
+class FilterNode(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("num_children", ctypes.c_int32), ("leaf_kind", ctypes.c_int32),
+                ("column", ctypes.c_int32), ("lo", ctypes.c_int32), ("hi", ctypes.c_int32),
+                ("exclusive", ctypes.c_int32), ("count", ctypes.c_int32),
+                ("ids", ctypes.POINTER(ctypes.c_int32))]
+
+
+class Aggregation(ctypes.Structure):
+    _fields_ = [("function", ctypes.c_int32), ("expr", ctypes.c_int32), ("column_a", ctypes.c_int32),
+                ("column_b", ctypes.c_int32), ("log2m", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class QueryDesc(ctypes.Structure):
+    _fields_ = [("num_columns", ctypes.c_int32), ("num_segments", ctypes.c_int32),
+                ("columns", ctypes.POINTER(ctypes.c_char_p)), ("segments", ctypes.POINTER(ctypes.c_uint64)),
+                ("filter_offsets", ctypes.POINTER(ctypes.c_int32)), ("filter_nodes", ctypes.POINTER(FilterNode)),
+                ("num_aggregations", ctypes.c_int32), ("num_group_by", ctypes.c_int32),
+                ("aggregations", ctypes.POINTER(Aggregation)), ("group_by_columns", ctypes.POINTER(ctypes.c_int32)),
+                ("num_groups_limit", ctypes.c_int64)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("num_docs_scanned", ctypes.c_int64), ("num_entries_scanned_in_filter", ctypes.c_int64),
+                ("num_entries_scanned_post_filter", ctypes.c_int64), ("num_total_docs", ctypes.c_int64),
+                ("num_segments_processed", ctypes.c_int32), ("num_segments_matched", ctypes.c_int32),
+                ("num_groups_limit_reached", ctypes.c_int32), ("num_aggregations", ctypes.c_int32),
+                ("num_groups", ctypes.c_int64), ("num_group_by", ctypes.c_int32), ("num_hll", ctypes.c_int32),
+                ("values", ctypes.POINTER(ctypes.c_double)), ("long_values", ctypes.POINTER(ctypes.c_int64)),
+                ("hll_registers", ctypes.POINTER(ctypes.c_uint8)), ("group_keys", ctypes.POINTER(ctypes.c_int32)),
+                ("scan_kernel_ms", ctypes.c_double), ("device_ms", ctypes.c_double)]
+
+
+class DictionaryView(ctypes.Structure):
+    _fields_ = [("data_type", ctypes.c_int32), ("cardinality", ctypes.c_int32), ("string_width", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("values", ctypes.c_void_p)]
+
+
+class PhipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"pinot_hip error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load libpinot_hip.so (fails loudly: there is no CPU fallback on the product path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    i32, u64, i64 = ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64
+    lib.phip_init.argtypes = [ctypes.POINTER(i32), i32]
+    lib.phip_init.restype = i32
+    lib.phip_shutdown.argtypes = []
+    lib.phip_shutdown.restype = i32
+    lib.phip_device_count.argtypes = [ctypes.POINTER(i32)]
+    lib.phip_device_count.restype = i32
+    lib.phip_last_error.argtypes = []
+    lib.phip_last_error.restype = ctypes.c_char_p
+    lib.phip_version.argtypes = []
+    lib.phip_version.restype = ctypes.c_char_p
+    lib.phip_segment_load.argtypes = [ctypes.POINTER(SegmentDesc), ctypes.POINTER(u64)]
+    lib.phip_segment_load.restype = i32
+    lib.phip_segment_unload.argtypes = [u64]
+    lib.phip_segment_unload.restype = i32
+    lib.phip_segment_device_bytes.argtypes = [u64, ctypes.POINTER(u64)]
+    lib.phip_segment_device_bytes.restype = i32
+    lib.phip_query.argtypes = [ctypes.POINTER(QueryDesc), ctypes.POINTER(ctypes.POINTER(Result))]
+    lib.phip_query.restype = i32
+    lib.phip_result_dictionary.argtypes = [ctypes.POINTER(Result), i32, ctypes.POINTER(DictionaryView)]
+    lib.phip_result_dictionary.restype = i32
+    lib.phip_result_free.argtypes = [ctypes.POINTER(Result)]
+    lib.phip_result_free.restype = None
+    lib.phip_filter_bitmap.argtypes = [ctypes.POINTER(QueryDesc), ctypes.POINTER(u64), i64]
+    lib.phip_filter_bitmap.restype = i32
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != PHIP_OK:
+        raise PhipError(rc, load().phip_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,106 @@
+// device.h -- structures shared by the host runtime (runtime.cpp) and the gfx950 kernels
+// (kernels.hip). Plain POD, identical layout on host and device.
+#pragma once
+#include <stdint.h>
+
+namespace phip {
+
+constexpr int kMaxQueryColumns = 16;  // distinct columns one query may reference
+constexpr int kMaxAggs = 8;           // aggregation slots per query
+constexpr int kMaxFilterDepth = 6;    // AND/OR/NOT nesting (host rejects deeper trees)
+constexpr int kWave = 64;             // CDNA wavefront
+constexpr int kBlock = 256;           // 4 waves per workgroup
+constexpr int kTileGroups = 64;       // 64-doc groups per wave tile: lane g owns group g's bitmap word
+constexpr int kTileDocs = kTileGroups * 64;  // 4096 docs per tile
+constexpr int kMaxHllRegs = 1 << 12;  // log2m <= 12 on the GPU path
+
+// Accumulator kinds of one aggregation slot.
+enum AccKind : int32_t {
+  ACC_COUNT = 0,    // int64 count
+  ACC_SUM_I64 = 1,  // exact int64 sum (INT/LONG inputs)
+  ACC_SUM_F64 = 2,  // double sum
+  ACC_MIN_F64 = 3,
+  ACC_MAX_F64 = 4,
+  ACC_HLL = 5,      // registers, per (group, hll slot)
+};
+
+// One column as seen by one segment of a query.
+struct DevCol {
+  const uint32_t *words;  // fixed-bit dict ids: u32 words holding the BE stream (bit 31 = first bit)
+  const void *dict;       // LE typed dictionary (INT/LONG/FLOAT/DOUBLE), null for STRING
+  const void *raw;        // LE raw values for no-dictionary columns
+  const int32_t *remap;   // segment dict id -> query-global id (group-by), null = identity
+  const uint32_t *hll;    // per dict id (register << 8) | rho, for DISTINCTCOUNTHLL
+  int32_t bits;
+  int32_t card;
+  int32_t type;      // PHIP_TYPE_*
+  int32_t has_dict;  // 1: dictionary-encoded; 0: raw
+};
+
+struct DevSeg {
+  int32_t num_docs;
+  int32_t tile_begin;  // first global tile index of this segment
+  int32_t node_begin;  // filter nodes [node_begin, node_end); empty = match all
+  int32_t node_end;
+  DevCol cols[kMaxQueryColumns];
+};
+
+struct DevNode {
+  int32_t op;           // PHIP_NODE_*
+  int32_t num_children;
+  int32_t leaf_kind;    // PHIP_LEAF_*
+  int32_t column;
+  int32_t lo, hi;
+  int32_t exclusive;
+  int32_t count;
+  int32_t next;         // index of the node after this subtree (preorder skip)
+  int32_t pad;
+  const void *aux;      // DICT_SET: u32 bitset over dict ids; DOC_RANGES: int32 pairs;
+                        // INVERTED: u64 doc bitmap words of the segment (materialised)
+};
+
+struct DevAgg {
+  int32_t acc;     // AccKind
+  int32_t expr;    // PHIP_EXPR_*
+  int32_t col_a;
+  int32_t col_b;
+  int32_t integral;  // expression evaluated in int64 (both inputs INT/LONG)
+  int32_t hll_slot;  // ACC_HLL: index among HLL aggs
+  int32_t log2m;
+  int32_t pad;
+};
+
+struct DevQuery {
+  const DevSeg *segs;
+  const DevNode *nodes;
+  int32_t num_segs;
+  int32_t total_tiles;
+  int32_t num_aggs;
+  int32_t num_hll;
+  DevAgg aggs[kMaxAggs];
+  // group-by
+  int32_t num_group_by;
+  int32_t gb_cols[4];
+  int64_t gb_stride[4];   // mixed radix, column 0 least significant
+  int64_t num_groups;     // dense key space size (0 = no group-by)
+  uint64_t *gb_table;     // [num_aggs][num_groups] 64-bit accumulators (int64 / f64 bits / ordered min-max)
+  uint64_t *gb_count;     // [num_groups] int64 doc counts
+  uint32_t *gb_hll;       // [num_hll][num_groups][1<<log2m]
+  // aggregation-only partials
+  uint64_t *partials;     // [num_blocks][num_aggs + 2] (slot num_aggs: matched docs, +1: entries scanned)
+  uint32_t *hll_regs;     // [num_hll][1<<log2m] (aggregation-only)
+  uint64_t *seg_matched;  // [num_segs] matched docs per segment
+  uint64_t *filter_out;   // optional: filter bitmap words of segment 0 (phip_filter_bitmap)
+};
+
+// One Roaring container of one selected dictionary id, OR-ed into a segment's dense doc words.
+struct RoaringTask {
+  const uint8_t *payload;
+  uint64_t *out_words;
+  int32_t key;   // high 16 bits of the doc ids: words [1024*key, 1024*key + 1024)
+  int32_t kind;  // 0 array (card x u16), 1 bitmap (1024 x u64 LE), 2 run (u16 nruns, (start, len-1) pairs)
+  int32_t card;  // array cardinality / number of runs
+  int32_t pad;
+};
+
+}  // namespace phip

@@ -1,0 +1,1355 @@
+// runtime.cpp -- host runtime of libpinot_hip.so: devices, HBM-resident segments, query executor,
+// and the C ABI declared in include/pinot_hip.h.
+//
+// Segment load (ImmutableSegmentLoader.load, pinot-segment-local/.../immutable/
+// ImmutableSegmentLoader.java:155-190,222-280) pins, per column, the forward index, the dictionary
+// and the inverted index in HBM in the layouts the kernels read (kernels.hip header). A query
+// (InstancePlanMakerImplV2.makeInstancePlan, pinot-core/.../plan/maker/InstancePlanMakerImplV2.java:172-199)
+// runs as: Roaring decode of inverted leaves -> one fused filter/aggregate (or group-by) launch over
+// all segments -> deterministic finalize -> one D2H copy; it replaces the per-segment operators and
+// the CombineOperator thread fan-out (BaseCombineOperator.java:98-143).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pinot_hip.h"
+#include "device.h"
+
+namespace phip {
+hipError_t launch_bswap32(uint32_t *p, int64_t n, hipStream_t s);
+hipError_t launch_bswap64(uint64_t *p, int64_t n, hipStream_t s);
+hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32_t *ids_tmp, int64_t n, int32_t bits,
+                                   uint32_t *words, int64_t nwords, hipStream_t s);
+hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
+hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream_t s);
+hipError_t launch_scan(const DevQuery &q, int nblocks, size_t lds_bytes, bool group_by, hipStream_t s);
+hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
+                                    uint64_t *out, hipStream_t s);
+hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_counts, int64_t nchunks,
+                              int64_t *offsets, hipStream_t s);
+hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *offsets, int64_t nchunks,
+                                int64_t *keys, hipStream_t s);
+hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs,
+                               const int32_t *kinds, const uint64_t *table, const uint64_t *counts,
+                               const uint32_t *hll, int32_t nhll, int32_t log2m, double *vals, int64_t *longs,
+                               uint8_t *hll_out, hipStream_t s);
+}  // namespace phip
+
+using namespace phip;
+
+// ================================================================================================
+// errors
+// ================================================================================================
+static thread_local std::string g_err;
+
+static int32_t fail(int32_t code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) return fail(PHIP_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+static inline uint32_t be32(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+static inline uint64_t be64(const uint8_t *p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+static inline uint32_t le32(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static inline uint16_t le16(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+
+static int num_bits_per_value(int32_t max_value) {  // PinotDataBitSet.getNumBitsPerValue (:61-72)
+  if (max_value <= 1) return 1;
+  int b = 0;
+  while (max_value > 0) {
+    b++;
+    max_value >>= 1;
+  }
+  return b;
+}
+
+static int type_width(int32_t t) {
+  switch (t) {
+    case PHIP_TYPE_INT:
+    case PHIP_TYPE_FLOAT: return 4;
+    case PHIP_TYPE_LONG:
+    case PHIP_TYPE_DOUBLE: return 8;
+    default: return 0;
+  }
+}
+
+// ================================================================================================
+// clearspring MurmurHash / HyperLogLog register index (stream-lib 2.9.8, pom.xml:1416-1418), as
+// DistinctCountHLLAggregationFunction offers dictionary values (…/function/DistinctCountHLLAggregationFunction.java:457-466)
+// ================================================================================================
+static int32_t murmur_hash_long(int64_t data) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = 0;
+  uint32_t k = (uint32_t)data * m;
+  k ^= k >> 24;
+  h ^= k * m;
+  k = (uint32_t)((uint64_t)data >> 32) * m;
+  k ^= k >> 24;
+  h *= m;
+  h ^= k * m;
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+static int32_t murmur_hash_bytes(const uint8_t *d, int32_t len, int32_t seed) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = (uint32_t)seed ^ (uint32_t)len;
+  int32_t n4 = len >> 2;
+  for (int32_t i = 0; i < n4; i++) {
+    uint32_t k = le32(d + 4 * i);
+    k *= m;
+    k ^= k >> 24;
+    k *= m;
+    h *= m;
+    h ^= k;
+  }
+  int32_t left = len - (n4 << 2);
+  if (left) {
+    if (left >= 3) h ^= (uint32_t)((int32_t)(int8_t)d[len - 3] << 16);
+    if (left >= 2) h ^= (uint32_t)((int32_t)(int8_t)d[len - 2] << 8);
+    h ^= (uint32_t)(int32_t)(int8_t)d[len - 1];
+    h *= m;
+  }
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+static uint32_t hll_index_rho(int32_t x, int log2m) {  // HyperLogLog.offerHashed
+  uint32_t ux = (uint32_t)x;
+  uint32_t j = ux >> (32 - log2m);
+  uint32_t w = (ux << log2m) | ((1u << (log2m - 1)) + 1u);
+  uint32_t r = (uint32_t)__builtin_clz(w) + 1u;
+  return (j << 8) | r;
+}
+
+// ================================================================================================
+// devices and segments
+// ================================================================================================
+struct Workspace {
+  struct Buf {
+    void *p = nullptr;
+    size_t cap = 0;
+  };
+  std::map<std::string, Buf> dev;
+  std::map<std::string, Buf> host;  // pinned
+
+  int32_t get(const std::string &name, size_t bytes, void **out) {
+    Buf &b = dev[name];
+    if (b.cap < bytes) {
+      if (b.p) (void)hipFree(b.p);
+      size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
+      HIP_TRY(hipMalloc(&b.p, cap));
+      b.cap = cap;
+    }
+    *out = b.p;
+    return PHIP_OK;
+  }
+  int32_t get_host(const std::string &name, size_t bytes, void **out) {
+    Buf &b = host[name];
+    if (b.cap < bytes) {
+      if (b.p) (void)hipHostFree(b.p);
+      size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
+      HIP_TRY(hipHostMalloc(&b.p, cap, hipHostMallocDefault));
+      b.cap = cap;
+    }
+    *out = b.p;
+    return PHIP_OK;
+  }
+  void release() {
+    for (auto &kv : dev)
+      if (kv.second.p) (void)hipFree(kv.second.p);
+    for (auto &kv : host)
+      if (kv.second.p) (void)hipHostFree(kv.second.p);
+    dev.clear();
+    host.clear();
+  }
+};
+
+struct Device {
+  int ordinal = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {};
+  std::mutex mu;
+  Workspace ws;
+  // query-global dictionary remaps for group-by (key: column + segment handles)
+  struct Remap {
+    std::vector<int32_t *> dev;  // per segment (nullptr = identity)
+    int32_t card = 0;
+    int32_t type = 0;
+    int32_t width = 0;
+    std::vector<uint8_t> values;  // LE typed or fixed-width strings
+  };
+  std::map<std::string, std::shared_ptr<Remap>> remaps;
+};
+
+struct Container {
+  int32_t key, kind, card;
+  uint64_t off;  // payload offset within the column's device blob
+};
+
+struct ColumnStore {
+  std::string name;
+  int32_t type = 0, fwd_kind = 0, card = 0, bits = 0, string_width = 0;
+  uint32_t *words = nullptr;  // fixed-bit dict ids (also synthesised for sorted columns)
+  void *dict = nullptr;       // LE typed dictionary (numeric)
+  void *raw = nullptr;        // LE raw values
+  std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
+  std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
+  std::map<int, uint32_t *> hll;      // per log2m
+  // inverted index
+  uint8_t *inv_blob = nullptr;
+  std::vector<int64_t> inv_begin;  // card+1 into inv_conts
+  std::vector<Container> inv_conts;
+};
+
+struct Segment {
+  uint64_t handle = 0;
+  int device = 0;
+  int32_t num_docs = 0;
+  std::string name;
+  std::vector<ColumnStore> cols;
+  std::unordered_map<std::string, int> by_name;
+  uint64_t device_bytes = 0;
+  std::vector<void *> allocations;
+};
+
+static std::mutex g_mu;  // guards the registries below
+static std::vector<std::unique_ptr<Device>> g_devices;
+static std::unordered_map<uint64_t, std::unique_ptr<Segment>> g_segments;
+static std::atomic<uint64_t> g_next_handle{1};
+
+static int32_t ensure_devices_locked() {
+  if (!g_devices.empty()) return PHIP_OK;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(PHIP_ERR_NO_DEVICE, "no HIP device available");
+  int cur = 0;
+  HIP_TRY(hipGetDevice(&cur));
+  auto d = std::make_unique<Device>();
+  d->ordinal = cur;
+  HIP_TRY(hipSetDevice(cur));
+  HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
+  g_devices.push_back(std::move(d));
+  return PHIP_OK;
+}
+
+static Device *find_device(int ordinal) {
+  for (auto &d : g_devices)
+    if (d->ordinal == ordinal) return d.get();
+  return nullptr;
+}
+
+// ================================================================================================
+// segment load
+// ================================================================================================
+static int32_t dev_alloc(Segment &s, size_t bytes, void **out) {
+  void *p = nullptr;
+  HIP_TRY(hipMalloc(&p, bytes == 0 ? 16 : bytes));
+  s.allocations.push_back(p);
+  s.device_bytes += bytes;
+  *out = p;
+  return PHIP_OK;
+}
+
+static int32_t parse_inverted(const phip_column_desc &c, ColumnStore &cs, Segment &seg, hipStream_t st) {
+  const uint8_t *b = c.inverted;
+  const uint64_t len = c.inverted_bytes;
+  const int32_t card = c.cardinality;
+  const uint64_t off_bytes = (uint64_t)(card + 1) * 4;
+  if (len < off_bytes) return fail(PHIP_ERR_INVALID, "column %s: inverted index too short", c.name);
+  // BitmapInvertedIndexReader.java:40-62: offsets are absolute or relative; normalise by the first
+  const uint64_t first = be32(b);
+  cs.inv_begin.assign(card + 1, 0);
+  for (int32_t d = 0; d < card; d++) {
+    uint64_t o0 = be32(b + 4 * d) - first, o1 = be32(b + 4 * (d + 1)) - first;
+    if (o1 < o0 || off_bytes + o1 > len) return fail(PHIP_ERR_INVALID, "column %s: bad bitmap offsets", c.name);
+    const uint8_t *bm = b + off_bytes + o0;
+    const uint64_t blen = o1 - o0;
+    cs.inv_begin[d] = (int64_t)cs.inv_conts.size();
+    if (blen < 8) return fail(PHIP_ERR_INVALID, "column %s: bitmap %d truncated", c.name, d);
+    uint32_t cookie = le32(bm);
+    uint64_t pos;
+    int32_t size;
+    bool has_run = false;
+    const uint8_t *runflags = nullptr;
+    if ((cookie & 0xFFFF) == 12347) {
+      has_run = true;
+      size = (int32_t)(cookie >> 16) + 1;
+      runflags = bm + 4;
+      pos = 4 + (uint64_t)(size + 7) / 8;
+    } else if (cookie == 12346) {
+      size = (int32_t)le32(bm + 4);
+      pos = 8;
+    } else {
+      return fail(PHIP_ERR_INVALID, "column %s: bitmap %d bad cookie %u", c.name, d, cookie);
+    }
+    const uint8_t *hdr = bm + pos;
+    pos += 4ull * size;
+    const bool has_off = !has_run || size >= 4;
+    const uint8_t *offs = bm + pos;
+    if (has_off) pos += 4ull * size;
+    if (pos > blen) return fail(PHIP_ERR_INVALID, "column %s: bitmap %d header overflow", c.name, d);
+    for (int32_t k = 0; k < size; k++) {
+      Container ct;
+      ct.key = le16(hdr + 4 * k);
+      int32_t ccard = (int32_t)le16(hdr + 4 * k + 2) + 1;
+      bool is_run = has_run && ((runflags[k >> 3] >> (k & 7)) & 1);
+      if (has_off) pos = le32(offs + 4 * k);
+      if (pos + 2 > blen) return fail(PHIP_ERR_INVALID, "column %s: bitmap %d container overflow", c.name, d);
+      uint64_t psize;
+      if (is_run) {
+        ct.kind = 2;
+        ct.card = le16(bm + pos);
+        psize = 2 + 4ull * ct.card;
+      } else if (ccard <= 4096) {
+        ct.kind = 0;
+        ct.card = ccard;
+        psize = 2ull * ccard;
+      } else {
+        ct.kind = 1;
+        ct.card = ccard;
+        psize = 8192;
+      }
+      if (pos + psize > blen) return fail(PHIP_ERR_INVALID, "column %s: bitmap %d payload overflow", c.name, d);
+      if ((int64_t)ct.key * 65536 >= (int64_t)seg.num_docs + 65536)
+        return fail(PHIP_ERR_INVALID, "column %s: bitmap %d key beyond numDocs", c.name, d);
+      ct.off = off_bytes + o0 + pos - off_bytes;  // relative to blob start (after offsets)
+      cs.inv_conts.push_back(ct);
+      pos += psize;
+    }
+  }
+  cs.inv_begin[card] = (int64_t)cs.inv_conts.size();
+  const uint64_t blob = len - off_bytes;
+  void *p;
+  int32_t rc = dev_alloc(seg, blob + 16, &p);
+  if (rc) return rc;
+  cs.inv_blob = (uint8_t *)p;
+  HIP_TRY(hipMemcpyAsync(cs.inv_blob, b + off_bytes, blob, hipMemcpyHostToDevice, st));
+  return PHIP_OK;
+}
+
+static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t st, std::vector<void *> &temps) {
+  ColumnStore cs;
+  if (!c.name) return fail(PHIP_ERR_INVALID, "column without name");
+  cs.name = c.name;
+  cs.type = c.data_type;
+  cs.fwd_kind = c.fwd_kind;
+  cs.card = c.cardinality;
+  cs.string_width = c.string_width;
+  const int64_t n = seg.num_docs;
+  if (c.data_type < PHIP_TYPE_INT || c.data_type > PHIP_TYPE_STRING)
+    return fail(PHIP_ERR_INVALID, "column %s: bad data type %d", c.name, c.data_type);
+  const bool dict = c.fwd_kind != PHIP_FWD_RAW_CHUNK;
+  if (dict) {
+    if (c.cardinality <= 0) return fail(PHIP_ERR_INVALID, "column %s: cardinality must be > 0", c.name);
+    const int w = c.data_type == PHIP_TYPE_STRING ? c.string_width : type_width(c.data_type);
+    if (w <= 0 || c.dictionary == nullptr || c.dictionary_bytes != (uint64_t)w * c.cardinality)
+      return fail(PHIP_ERR_INVALID, "column %s: dictionary size %llu != card %d x width %d", c.name,
+                  (unsigned long long)c.dictionary_bytes, c.cardinality, w);
+    cs.host_dict.assign(c.dictionary, c.dictionary + c.dictionary_bytes);
+    if (c.data_type != PHIP_TYPE_STRING) {
+      void *p;
+      int32_t rc = dev_alloc(seg, c.dictionary_bytes, &p);
+      if (rc) return rc;
+      HIP_TRY(hipMemcpyAsync(p, c.dictionary, c.dictionary_bytes, hipMemcpyHostToDevice, st));
+      if (w == 4) HIP_TRY(launch_bswap32((uint32_t *)p, c.cardinality, st));
+      else HIP_TRY(launch_bswap64((uint64_t *)p, c.cardinality, st));
+      cs.dict = p;
+    }
+    cs.bits = num_bits_per_value(c.cardinality - 1);
+    // padded word array: whole tiles + 4 guard words
+    const int64_t nwords = round_up(std::max<int64_t>(n, 1), kTileDocs) * cs.bits / 32 + 4;
+    void *wp;
+    int32_t rc = dev_alloc(seg, nwords * 4, &wp);
+    if (rc) return rc;
+    cs.words = (uint32_t *)wp;
+    HIP_TRY(hipMemsetAsync(cs.words, 0, nwords * 4, st));
+    if (c.fwd_kind == PHIP_FWD_FIXED_BIT) {
+      if (c.bits_per_value != cs.bits)
+        return fail(PHIP_ERR_INVALID, "column %s: bits %d != getNumBitsPerValue(card-1) = %d", c.name,
+                    c.bits_per_value, cs.bits);
+      const uint64_t need = (uint64_t)ceil_div(n * cs.bits, 8);
+      if (c.forward_bytes < need)
+        return fail(PHIP_ERR_INVALID, "column %s: forward index %llu bytes < %llu", c.name,
+                    (unsigned long long)c.forward_bytes, (unsigned long long)need);
+      HIP_TRY(hipMemcpyAsync(cs.words, c.forward, need, hipMemcpyHostToDevice, st));
+      HIP_TRY(launch_bswap32(cs.words, ceil_div(need, 4), st));
+    } else if (c.fwd_kind == PHIP_FWD_SORTED) {
+      if (c.forward_bytes != 8ull * c.cardinality)
+        return fail(PHIP_ERR_INVALID, "column %s: sorted index must be card x 8 bytes", c.name);
+      cs.sorted_pairs.resize(2 * (size_t)c.cardinality);
+      int64_t expect = 0;
+      for (int32_t d = 0; d < c.cardinality; d++) {
+        int32_t s = (int32_t)be32(c.forward + 8 * d), e = (int32_t)be32(c.forward + 8 * d + 4);
+        if (s != expect || e < s || e >= n)
+          return fail(PHIP_ERR_INVALID, "column %s: sorted ranges not contiguous at dict id %d", c.name, d);
+        expect = (int64_t)e + 1;
+        cs.sorted_pairs[2 * d] = s;
+        cs.sorted_pairs[2 * d + 1] = e;
+      }
+      if (expect != n) return fail(PHIP_ERR_INVALID, "column %s: sorted ranges do not cover numDocs", c.name);
+      void *pairs, *ids;
+      HIP_TRY(hipMalloc(&pairs, c.forward_bytes));
+      temps.push_back(pairs);
+      HIP_TRY(hipMalloc(&ids, std::max<int64_t>(n, 1) * 4));
+      temps.push_back(ids);
+      HIP_TRY(hipMemcpyAsync(pairs, c.forward, c.forward_bytes, hipMemcpyHostToDevice, st));
+      HIP_TRY(launch_sorted_to_packed((const uint32_t *)pairs, c.cardinality, (int32_t *)ids, n, cs.bits, cs.words,
+                                      ceil_div(n * cs.bits, 32), st));
+    } else {
+      return fail(PHIP_ERR_INVALID, "column %s: bad forward kind %d", c.name, c.fwd_kind);
+    }
+    if (c.inverted) {
+      int32_t rc2 = parse_inverted(c, cs, seg, st);
+      if (rc2) return rc2;
+    }
+  } else {
+    // raw fixed-width chunk forward index (BaseChunkForwardIndexWriter.java:40-160)
+    if (c.data_type == PHIP_TYPE_STRING) return fail(PHIP_ERR_UNSUPPORTED, "raw STRING columns are not on the GPU path");
+    const uint8_t *h = c.forward;
+    if (c.forward_bytes < 28) return fail(PHIP_ERR_INVALID, "column %s: chunk header truncated", c.name);
+    int32_t version = (int32_t)be32(h), num_chunks = (int32_t)be32(h + 4), per_chunk = (int32_t)be32(h + 8);
+    int32_t entry = (int32_t)be32(h + 12), total = (int32_t)be32(h + 16), comp = (int32_t)be32(h + 20);
+    int32_t data_hdr = (int32_t)be32(h + 24);
+    if (comp != 0) return fail(PHIP_ERR_UNSUPPORTED, "column %s: compressed chunks (type %d) are not on the GPU path", c.name, comp);
+    if (entry != type_width(c.data_type) || total != n || per_chunk <= 0 ||
+        num_chunks != ceil_div(n, per_chunk) || (version < 2 || version > 3))
+      return fail(PHIP_ERR_INVALID, "column %s: bad chunk header", c.name);
+    const int osz = version == 2 ? 4 : 8;
+    if ((uint64_t)data_hdr + (uint64_t)num_chunks * osz > c.forward_bytes)
+      return fail(PHIP_ERR_INVALID, "column %s: chunk offsets truncated", c.name);
+    void *p;
+    int32_t rc = dev_alloc(seg, (uint64_t)std::max<int64_t>(n, 1) * entry + 16, &p);
+    if (rc) return rc;
+    cs.raw = p;
+    for (int32_t k = 0; k < num_chunks; k++) {
+      uint64_t off = osz == 4 ? be32(h + data_hdr + 4 * k) : be64(h + data_hdr + 8 * k);
+      int64_t docs = std::min<int64_t>(per_chunk, n - (int64_t)k * per_chunk);
+      if (off + (uint64_t)docs * entry > c.forward_bytes) return fail(PHIP_ERR_INVALID, "column %s: chunk %d overflow", c.name, k);
+      HIP_TRY(hipMemcpyAsync((uint8_t *)p + (int64_t)k * per_chunk * entry, h + off, docs * entry,
+                             hipMemcpyHostToDevice, st));
+    }
+    if (entry == 4) HIP_TRY(launch_bswap32((uint32_t *)p, n, st));
+    else HIP_TRY(launch_bswap64((uint64_t *)p, n, st));
+  }
+  seg.by_name[cs.name] = (int)seg.cols.size();
+  seg.cols.push_back(std::move(cs));
+  return PHIP_OK;
+}
+
+// ================================================================================================
+// query execution
+// ================================================================================================
+namespace {
+
+struct Blob {  // host staging for one H2D copy; device address = base + offset
+  std::vector<uint8_t> data;
+  size_t add(const void *p, size_t n, size_t align = 16) {
+    size_t off = round_up((int64_t)data.size(), (int64_t)align);
+    data.resize(off + n);
+    if (n) memcpy(data.data() + off, p, n);
+    return off;
+  }
+  size_t reserve(size_t n, size_t align = 16) {
+    size_t off = round_up((int64_t)data.size(), (int64_t)align);
+    data.resize(off + n);
+    return off;
+  }
+};
+
+struct ResultImpl {
+  phip_result pub;
+  std::vector<double> values;
+  std::vector<int64_t> longs;
+  std::vector<uint8_t> hll;
+  std::vector<int32_t> keys;
+  std::vector<std::shared_ptr<Device::Remap>> dicts;
+};
+
+// validate a preorder subtree; returns index after it or -1
+int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, int depth, int ncols,
+                  std::vector<int> &next, std::string &err) {
+  if (idx >= end) {
+    err = "filter tree truncated";
+    return -1;
+  }
+  if (depth > kMaxFilterDepth) {
+    err = "filter tree deeper than supported";
+    return -1;
+  }
+  const phip_filter_node &n = nodes[idx];
+  int after;
+  switch (n.op) {
+    case PHIP_NODE_LEAF:
+      if (n.leaf_kind < PHIP_LEAF_MATCH_ALL || n.leaf_kind > PHIP_LEAF_INVERTED) {
+        err = "bad leaf kind";
+        return -1;
+      }
+      if (n.leaf_kind >= PHIP_LEAF_DICT_RANGE && n.leaf_kind != PHIP_LEAF_DOC_RANGES &&
+          (n.column < 0 || n.column >= ncols)) {
+        err = "leaf column out of range";
+        return -1;
+      }
+      if ((n.leaf_kind == PHIP_LEAF_DICT_SET || n.leaf_kind == PHIP_LEAF_INVERTED || n.leaf_kind == PHIP_LEAF_DOC_RANGES) &&
+          n.count > 0 && n.ids == nullptr) {
+        err = "leaf ids missing";
+        return -1;
+      }
+      after = idx + 1;
+      break;
+    case PHIP_NODE_NOT:
+      after = validate_tree(nodes, begin, end, idx + 1, depth + 1, ncols, next, err);
+      if (after < 0) return -1;
+      break;
+    case PHIP_NODE_AND:
+    case PHIP_NODE_OR: {
+      if (n.num_children < 1) {
+        err = "AND/OR without children";
+        return -1;
+      }
+      int c = idx + 1;
+      for (int k = 0; k < n.num_children; k++) {
+        c = validate_tree(nodes, begin, end, c, depth + 1, ncols, next, err);
+        if (c < 0) return -1;
+      }
+      after = c;
+      break;
+    }
+    default:
+      err = "bad node op";
+      return -1;
+  }
+  next[idx - begin] = after;
+  return after;
+}
+
+std::string dict_key(const ColumnStore &c) { return std::string((const char *)c.host_dict.data(), c.host_dict.size()); }
+
+// Query-global dictionary of one group-by column across the query's segments.
+int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
+                    const std::string &name, std::shared_ptr<Device::Remap> &out) {
+  std::string key = name;
+  for (auto *s : segs) key += ":" + std::to_string(s->handle);
+  auto it = dev.remaps.find(key);
+  if (it != dev.remaps.end()) {
+    out = it->second;
+    return PHIP_OK;
+  }
+  auto r = std::make_shared<Device::Remap>();
+  const ColumnStore &c0 = segs[0]->cols[colidx[0]];
+  r->type = c0.type;
+  bool identical = true;
+  int width = c0.type == PHIP_TYPE_STRING ? c0.string_width : type_width(c0.type);
+  for (size_t i = 0; i < segs.size(); i++) {
+    const ColumnStore &c = segs[i]->cols[colidx[i]];
+    if (c.fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s", name.c_str());
+    if (c.type != c0.type) return fail(PHIP_ERR_INVALID, "column %s has different types across segments", name.c_str());
+    if (c.host_dict != c0.host_dict) identical = false;
+    if (c.type == PHIP_TYPE_STRING) width = std::max(width, c.string_width);
+  }
+  r->width = c0.type == PHIP_TYPE_STRING ? width : 0;
+  auto to_le = [&](const ColumnStore &c, int32_t id, std::vector<uint8_t> &dst) {
+    if (c.type == PHIP_TYPE_STRING) {
+      size_t o = dst.size();
+      dst.resize(o + width, 0);
+      memcpy(dst.data() + o, c.host_dict.data() + (size_t)id * c.string_width, c.string_width);
+    } else {
+      int w = type_width(c.type);
+      const uint8_t *p = c.host_dict.data() + (size_t)id * w;
+      for (int b = w - 1; b >= 0; b--) dst.push_back(p[b]);
+    }
+  };
+  r->dev.assign(segs.size(), nullptr);
+  if (identical) {
+    r->card = c0.card;
+    for (int32_t id = 0; id < c0.card; id++) to_le(c0, id, r->values);
+  } else {
+    // merge: collect (value bytes in comparable form) and sort
+    // comparable form: strings as padded bytes (memcmp order == Java compareTo for '\0'-padded
+    // ASCII/BMP UTF-8), numbers via typed compare
+    struct V {
+      std::vector<uint8_t> le;
+    };
+    std::vector<std::vector<uint8_t>> all;
+    for (size_t i = 0; i < segs.size(); i++) {
+      const ColumnStore &c = segs[i]->cols[colidx[i]];
+      for (int32_t id = 0; id < c.card; id++) {
+        std::vector<uint8_t> v;
+        to_le(c, id, v);
+        all.push_back(std::move(v));
+      }
+    }
+    auto less = [&](const std::vector<uint8_t> &a, const std::vector<uint8_t> &b) {
+      switch (c0.type) {
+        case PHIP_TYPE_INT: {
+          int32_t x, y;
+          memcpy(&x, a.data(), 4);
+          memcpy(&y, b.data(), 4);
+          return x < y;
+        }
+        case PHIP_TYPE_LONG: {
+          int64_t x, y;
+          memcpy(&x, a.data(), 8);
+          memcpy(&y, b.data(), 8);
+          return x < y;
+        }
+        case PHIP_TYPE_FLOAT: {
+          float x, y;
+          memcpy(&x, a.data(), 4);
+          memcpy(&y, b.data(), 4);
+          return x < y;
+        }
+        case PHIP_TYPE_DOUBLE: {
+          double x, y;
+          memcpy(&x, a.data(), 8);
+          memcpy(&y, b.data(), 8);
+          return x < y;
+        }
+        default: return memcmp(a.data(), b.data(), a.size()) < 0;
+      }
+    };
+    std::sort(all.begin(), all.end(), less);
+    all.erase(std::unique(all.begin(), all.end()), all.end());
+    r->card = (int32_t)all.size();
+    for (auto &v : all) r->values.insert(r->values.end(), v.begin(), v.end());
+    for (size_t i = 0; i < segs.size(); i++) {
+      const ColumnStore &c = segs[i]->cols[colidx[i]];
+      std::vector<int32_t> m(c.card);
+      for (int32_t id = 0; id < c.card; id++) {
+        std::vector<uint8_t> v;
+        to_le(c, id, v);
+        m[id] = (int32_t)(std::lower_bound(all.begin(), all.end(), v, less) - all.begin());
+      }
+      void *p;
+      HIP_TRY(hipMalloc(&p, std::max<size_t>(m.size(), 1) * 4));
+      HIP_TRY(hipMemcpy(p, m.data(), m.size() * 4, hipMemcpyHostToDevice));
+      r->dev[i] = (int32_t *)p;
+    }
+  }
+  dev.remaps[key] = r;
+  out = r;
+  return PHIP_OK;
+}
+
+int32_t ensure_hll(ColumnStore &c, int log2m, uint32_t **out) {
+  auto it = c.hll.find(log2m);
+  if (it != c.hll.end()) {
+    *out = it->second;
+    return PHIP_OK;
+  }
+  std::vector<uint32_t> t(c.card);
+  for (int32_t id = 0; id < c.card; id++) {
+    int32_t x;
+    const uint8_t *p;
+    switch (c.type) {
+      case PHIP_TYPE_INT: p = c.host_dict.data() + 4 * id; x = murmur_hash_long((int64_t)(int32_t)be32(p)); break;
+      case PHIP_TYPE_LONG: p = c.host_dict.data() + 8 * id; x = murmur_hash_long((int64_t)be64(p)); break;
+      case PHIP_TYPE_FLOAT: p = c.host_dict.data() + 4 * id; x = murmur_hash_long((int64_t)(int32_t)be32(p)); break;
+      case PHIP_TYPE_DOUBLE: p = c.host_dict.data() + 8 * id; x = murmur_hash_long((int64_t)be64(p)); break;
+      default: {
+        p = c.host_dict.data() + (size_t)c.string_width * id;
+        int32_t len = c.string_width;
+        while (len > 0 && p[len - 1] == 0) len--;
+        x = murmur_hash_bytes(p, len, -1);
+      }
+    }
+    t[id] = hll_index_rho(x, log2m);
+  }
+  void *d;
+  HIP_TRY(hipMalloc(&d, std::max<size_t>(t.size(), 1) * 4));
+  HIP_TRY(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  c.hll[log2m] = (uint32_t *)d;
+  *out = (uint32_t *)d;
+  return PHIP_OK;
+}
+
+int acc_kind_for(const phip_aggregation &a, bool integral) {
+  switch (a.function) {
+    case PHIP_AGG_COUNT: return ACC_COUNT;
+    case PHIP_AGG_SUM: return integral ? ACC_SUM_I64 : ACC_SUM_F64;
+    case PHIP_AGG_MIN: return ACC_MIN_F64;
+    case PHIP_AGG_MAX: return ACC_MAX_F64;
+    default: return ACC_HLL;
+  }
+}
+
+}  // namespace
+
+static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uint64_t *filter_words,
+                         int64_t filter_nwords) {
+  if (!q || q->num_segments <= 0 || q->num_columns < 0 || q->num_columns > kMaxQueryColumns)
+    return fail(PHIP_ERR_INVALID, "query: need >=1 segment and <= %d columns", kMaxQueryColumns);
+  if (q->num_aggregations < 0 || q->num_aggregations > kMaxAggs)
+    return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d aggregations on the GPU path", kMaxAggs);
+  if (q->num_group_by < 0 || q->num_group_by > 4) return fail(PHIP_ERR_UNSUPPORTED, "query: at most 4 group-by columns");
+  if (q->num_segments > 1 && filter_words) return fail(PHIP_ERR_INVALID, "filter bitmap: one segment only");
+
+  std::vector<Segment *> segs(q->num_segments);
+  Device *dev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (int i = 0; i < q->num_segments; i++) {
+      auto it = g_segments.find(q->segments[i]);
+      if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle %llu", (unsigned long long)q->segments[i]);
+      segs[i] = it->second.get();
+      if (i > 0 && segs[i]->device != segs[0]->device)
+        return fail(PHIP_ERR_UNSUPPORTED, "segments of one query must reside on one device");
+    }
+    dev = find_device(segs[0]->device);
+  }
+  if (!dev) return fail(PHIP_ERR_NO_DEVICE, "device %d not initialised", segs[0]->device);
+  std::lock_guard<std::mutex> dlock(dev->mu);
+  HIP_TRY(hipSetDevice(dev->ordinal));
+  hipStream_t st = dev->stream;
+
+  const int nseg = q->num_segments, ncols = q->num_columns, naggs = q->num_aggregations;
+  // resolve columns
+  std::vector<std::vector<int>> colidx(nseg, std::vector<int>(ncols, -1));
+  for (int s = 0; s < nseg; s++)
+    for (int c = 0; c < ncols; c++) {
+      auto it = segs[s]->by_name.find(q->columns[c]);
+      if (it == segs[s]->by_name.end())
+        return fail(PHIP_ERR_NOT_FOUND, "segment %s has no column %s", segs[s]->name.c_str(), q->columns[c]);
+      colidx[s][c] = it->second;
+    }
+
+  // aggregations
+  DevQuery dq;
+  memset(&dq, 0, sizeof(dq));
+  dq.num_segs = nseg;
+  dq.num_aggs = naggs;
+  int nhll = 0, log2m = 0;
+  std::vector<int32_t> kinds(naggs + 2, ACC_COUNT);
+  std::vector<bool> projected(ncols, false);
+  for (int a = 0; a < naggs; a++) {
+    const phip_aggregation &ag = q->aggregations[a];
+    DevAgg &d = dq.aggs[a];
+    d.expr = ag.expr;
+    d.col_a = ag.column_a;
+    d.col_b = ag.column_b;
+    if (ag.function < PHIP_AGG_COUNT || ag.function > PHIP_AGG_HLL) return fail(PHIP_ERR_INVALID, "bad aggregation function");
+    if (ag.function != PHIP_AGG_COUNT) {
+      if (ag.column_a < 0 || ag.column_a >= ncols) return fail(PHIP_ERR_INVALID, "aggregation column out of range");
+      projected[ag.column_a] = true;
+      if (ag.expr != PHIP_EXPR_COLUMN) {
+        if (ag.function == PHIP_AGG_HLL) return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over expressions");
+        if (ag.column_b < 0 || ag.column_b >= ncols) return fail(PHIP_ERR_INVALID, "aggregation column out of range");
+        projected[ag.column_b] = true;
+      }
+    }
+    bool integral = true;
+    if (ag.function != PHIP_AGG_COUNT) {
+      for (int s = 0; s < nseg; s++) {
+        const ColumnStore &ca = segs[s]->cols[colidx[s][ag.column_a]];
+        if (!(ca.type == PHIP_TYPE_INT || ca.type == PHIP_TYPE_LONG)) integral = false;
+        if (ca.type == PHIP_TYPE_STRING && ag.function != PHIP_AGG_HLL)
+          return fail(PHIP_ERR_INVALID, "numeric aggregation over STRING column %s", ca.name.c_str());
+        if (ag.function == PHIP_AGG_HLL && ca.fwd_kind == PHIP_FWD_RAW_CHUNK)
+          return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over raw column %s", ca.name.c_str());
+        if (ag.expr != PHIP_EXPR_COLUMN) {
+          const ColumnStore &cb = segs[s]->cols[colidx[s][ag.column_b]];
+          if (!(cb.type == PHIP_TYPE_INT || cb.type == PHIP_TYPE_LONG)) integral = false;
+          if (cb.type == PHIP_TYPE_STRING) return fail(PHIP_ERR_INVALID, "numeric expression over STRING column");
+        }
+      }
+    }
+    d.integral = integral;
+    d.acc = acc_kind_for(ag, integral);
+    kinds[a] = d.acc;
+    if (d.acc == ACC_HLL) {
+      if (ag.log2m < 4 || ag.log2m > 12) return fail(PHIP_ERR_UNSUPPORTED, "log2m %d outside [4,12]", ag.log2m);
+      if (nhll > 0 && ag.log2m != log2m) return fail(PHIP_ERR_UNSUPPORTED, "all HLL aggregations must share log2m");
+      log2m = ag.log2m;
+      d.hll_slot = nhll++;
+      d.log2m = ag.log2m;
+    }
+  }
+  dq.num_hll = nhll;
+  for (int k = 0; k < q->num_group_by; k++) {
+    int c = q->group_by_columns[k];
+    if (c < 0 || c >= ncols) return fail(PHIP_ERR_INVALID, "group-by column out of range");
+    projected[c] = true;
+  }
+  int num_projected = 0;
+  for (bool p : projected) num_projected += p ? 1 : 0;
+
+  // group-by key space
+  const bool group_by = q->num_group_by > 0;
+  std::vector<std::shared_ptr<Device::Remap>> gb_dicts;
+  std::vector<std::vector<int32_t *>> gb_remap_dev;  // [k][seg]
+  if (group_by) {
+    dq.num_group_by = q->num_group_by;
+    int64_t stride = 1;
+    for (int k = 0; k < q->num_group_by; k++) {
+      int c = q->group_by_columns[k];
+      std::vector<int> ci(nseg);
+      for (int s = 0; s < nseg; s++) ci[s] = colidx[s][c];
+      std::shared_ptr<Device::Remap> r;
+      int32_t rc = build_remap(*dev, segs, ci, q->columns[c], r);
+      if (rc) return rc;
+      gb_dicts.push_back(r);
+      dq.gb_cols[k] = c;
+      dq.gb_stride[k] = stride;
+      stride *= r->card;
+      if (stride > (int64_t)1 << 26)
+        return fail(PHIP_ERR_UNSUPPORTED, "group-by key space %lld exceeds the dense table limit", (long long)stride);
+    }
+    dq.num_groups = stride;
+  }
+
+  // ---- staging blob: segments, nodes, leaf aux ------------------------------------------------
+  Blob blob;
+  const size_t segs_off = blob.reserve(sizeof(DevSeg) * nseg);
+  std::vector<DevNode> nodes;
+  struct AuxFix {
+    size_t node;
+    size_t off;
+  };
+  std::vector<AuxFix> aux_fix;      // node.aux = dev_base + off
+  struct InvLeaf {
+    size_t node;
+    int seg;
+    int col;
+    const phip_filter_node *src;
+  };
+  std::vector<InvLeaf> inv_leaves;
+  int64_t total_tiles = 0;
+  int64_t total_docs = 0;
+  std::vector<DevSeg> dsegs(nseg);
+  for (int s = 0; s < nseg; s++) {
+    Segment &sg = *segs[s];
+    DevSeg &ds = dsegs[s];
+    memset(&ds, 0, sizeof(ds));
+    ds.num_docs = sg.num_docs;
+    ds.tile_begin = (int32_t)total_tiles;
+    total_tiles += ceil_div(sg.num_docs, kTileDocs);
+    total_docs += sg.num_docs;
+    for (int c = 0; c < ncols; c++) {
+      ColumnStore &cs = sg.cols[colidx[s][c]];
+      DevCol &dc = ds.cols[c];
+      dc.words = cs.words;
+      dc.dict = cs.dict;
+      dc.raw = cs.raw;
+      dc.bits = cs.bits;
+      dc.card = cs.card;
+      dc.type = cs.type;
+      dc.has_dict = cs.fwd_kind != PHIP_FWD_RAW_CHUNK;
+    }
+    for (int a = 0; a < naggs; a++) {
+      if (dq.aggs[a].acc != ACC_HLL) continue;
+      ColumnStore &cs = sg.cols[colidx[s][dq.aggs[a].col_a]];
+      uint32_t *h;
+      int32_t rc = ensure_hll(cs, dq.aggs[a].log2m, &h);
+      if (rc) return rc;
+      ds.cols[dq.aggs[a].col_a].hll = h;
+    }
+    for (int k = 0; k < q->num_group_by; k++) ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
+    // filter program
+    const int nb = q->filter_offsets ? q->filter_offsets[s] : 0;
+    const int ne = q->filter_offsets ? q->filter_offsets[s + 1] : 0;
+    ds.node_begin = (int32_t)nodes.size();
+    if (ne > nb) {
+      std::vector<int> next(ne - nb);
+      std::string err;
+      int after = validate_tree(q->filter_nodes, nb, ne, nb, 0, ncols, next, err);
+      if (after < 0) return fail(PHIP_ERR_INVALID, "segment %d filter: %s", s, err.c_str());
+      if (after != ne) return fail(PHIP_ERR_INVALID, "segment %d filter: trailing nodes", s);
+      for (int i = nb; i < ne; i++) {
+        const phip_filter_node &fn = q->filter_nodes[i];
+        DevNode dn;
+        memset(&dn, 0, sizeof(dn));
+        dn.op = fn.op;
+        dn.num_children = fn.num_children;
+        dn.leaf_kind = fn.leaf_kind;
+        dn.column = fn.column;
+        dn.lo = fn.lo;
+        dn.hi = fn.hi;
+        dn.exclusive = fn.exclusive;
+        dn.count = fn.count;
+        dn.next = ds.node_begin + (next[i - nb] - nb);
+        const size_t ni = nodes.size();
+        if (fn.op == PHIP_NODE_LEAF) {
+          ColumnStore *cs = (fn.leaf_kind >= PHIP_LEAF_DICT_RANGE && fn.leaf_kind != PHIP_LEAF_DOC_RANGES)
+                                ? &sg.cols[colidx[s][fn.column]]
+                                : nullptr;
+          switch (fn.leaf_kind) {
+            case PHIP_LEAF_DICT_RANGE:
+              if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_INVALID, "dict leaf on raw column");
+              dn.lo = std::max(0, fn.lo);
+              dn.hi = std::min(cs->card, fn.hi);
+              if (dn.hi <= dn.lo) dn.leaf_kind = PHIP_LEAF_MATCH_NONE;
+              break;
+            case PHIP_LEAF_DICT_SET: {
+              if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_INVALID, "dict leaf on raw column");
+              std::vector<uint32_t> bits(ceil_div(cs->card, 32) + 1, 0);
+              for (int k = 0; k < fn.count; k++) {
+                int32_t id = fn.ids[k];
+                if (id < 0 || id >= cs->card) return fail(PHIP_ERR_INVALID, "dict id %d out of range", id);
+                bits[id >> 5] |= 1u << (id & 31);
+              }
+              aux_fix.push_back({ni, blob.add(bits.data(), bits.size() * 4)});
+              break;
+            }
+            case PHIP_LEAF_DOC_RANGES: {
+              int32_t prev = -1;
+              for (int k = 0; k < fn.count; k++) {
+                int32_t a0 = fn.ids[2 * k], a1 = fn.ids[2 * k + 1];
+                if (a0 <= prev || a1 < a0 || a1 >= sg.num_docs)
+                  return fail(PHIP_ERR_INVALID, "doc ranges must be sorted, disjoint and within numDocs");
+                prev = a1;
+              }
+              aux_fix.push_back({ni, blob.add(fn.ids, (size_t)fn.count * 8)});
+              break;
+            }
+            case PHIP_LEAF_INVERTED:
+              if (cs->inv_begin.empty()) return fail(PHIP_ERR_INVALID, "column %s has no inverted index", cs->name.c_str());
+              inv_leaves.push_back({ni, s, colidx[s][fn.column], &fn});
+              break;
+            default: break;
+          }
+        }
+        nodes.push_back(dn);
+      }
+    }
+    ds.node_end = (int32_t)nodes.size();
+  }
+  if (total_tiles > INT32_MAX / 2) return fail(PHIP_ERR_UNSUPPORTED, "too many tiles in one query");
+  dq.total_tiles = (int32_t)total_tiles;
+
+  // inverted leaves: dense doc words per leaf + roaring container tasks
+  std::vector<RoaringTask> tasks;
+  size_t inv_words_total = 0;
+  std::vector<size_t> inv_word_off(inv_leaves.size());
+  for (size_t i = 0; i < inv_leaves.size(); i++) {
+    const Segment &sg = *segs[inv_leaves[i].seg];
+    size_t nw = (size_t)std::max(round_up(sg.num_docs, 65536), round_up(sg.num_docs, kTileDocs)) / 64;
+    inv_word_off[i] = inv_words_total;
+    inv_words_total += nw;
+  }
+  void *inv_words = nullptr;
+  if (inv_words_total) {
+    int32_t rc = dev->ws.get("inv_words", inv_words_total * 8, &inv_words);
+    if (rc) return rc;
+  }
+  for (size_t i = 0; i < inv_leaves.size(); i++) {
+    const InvLeaf &L = inv_leaves[i];
+    const ColumnStore &cs = segs[L.seg]->cols[L.col];
+    uint64_t *words = (uint64_t *)inv_words + inv_word_off[i];
+    nodes[L.node].aux = words;
+    for (int k = 0; k < L.src->count; k++) {
+      int32_t id = L.src->ids[k];
+      if (id < 0 || id >= cs.card) return fail(PHIP_ERR_INVALID, "inverted dict id %d out of range", id);
+      for (int64_t ci = cs.inv_begin[id]; ci < cs.inv_begin[id + 1]; ci++) {
+        const Container &ct = cs.inv_conts[ci];
+        RoaringTask t;
+        t.payload = cs.inv_blob + ct.off + (ct.kind == 2 ? 0 : 0);
+        t.out_words = words;
+        t.key = ct.key;
+        t.kind = ct.kind;
+        t.card = ct.card;
+        t.pad = 0;
+        tasks.push_back(t);
+      }
+    }
+  }
+  const size_t tasks_off = tasks.empty() ? 0 : blob.add(tasks.data(), tasks.size() * sizeof(RoaringTask));
+  const size_t nodes_off = blob.add(nodes.data(), std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
+  const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
+
+  // device buffers
+  const int nslots = naggs + 2;
+  int dev_cus = 256;
+  int nblocks = (int)std::min<int64_t>(ceil_div(total_tiles, kBlock / 64), (int64_t)dev_cus * 8);
+  nblocks = std::max(nblocks, 1);
+  void *dblob;
+  int32_t rc = dev->ws.get("blob", blob.data.size() + 64, &dblob);
+  if (rc) return rc;
+  uint8_t *base = (uint8_t *)dblob;
+  for (auto &f : aux_fix) nodes[f.node].aux = base + f.off;
+  // rewrite nodes (aux pointers now final) and segments
+  memcpy(blob.data.data() + nodes_off, nodes.data(), nodes.size() * sizeof(DevNode));
+  memcpy(blob.data.data() + segs_off, dsegs.data(), sizeof(DevSeg) * nseg);
+  dq.segs = (const DevSeg *)(base + segs_off);
+  dq.nodes = (const DevNode *)(base + nodes_off);
+
+  void *partials, *finals, *seg_matched;
+  rc = dev->ws.get("partials", (size_t)nblocks * nslots * 8, &partials);
+  if (rc) return rc;
+  rc = dev->ws.get("finals", 64 * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
+  if (rc) return rc;
+  rc = dev->ws.get("seg_matched", (size_t)nseg * 8, &seg_matched);
+  if (rc) return rc;
+  dq.partials = (uint64_t *)partials;
+  dq.hll_regs = (uint32_t *)((uint8_t *)finals + 64 * 8);
+  dq.seg_matched = (uint64_t *)seg_matched;
+  if (filter_words) {
+    void *fo;
+    rc = dev->ws.get("filter_out", (size_t)filter_nwords * 8 + 4096 * 8, &fo);
+    if (rc) return rc;
+    dq.filter_out = (uint64_t *)fo;
+  }
+  if (group_by) {
+    void *tb, *cnt, *gh = nullptr;
+    rc = dev->ws.get("gb_table", (size_t)std::max(naggs, 1) * dq.num_groups * 8, &tb);
+    if (rc) return rc;
+    rc = dev->ws.get("gb_count", (size_t)dq.num_groups * 8, &cnt);
+    if (rc) return rc;
+    if (nhll) {
+      rc = dev->ws.get("gb_hll", (size_t)nhll * dq.num_groups * (1 << log2m) * 4, &gh);
+      if (rc) return rc;
+    }
+    dq.gb_table = (uint64_t *)tb;
+    dq.gb_count = (uint64_t *)cnt;
+    dq.gb_hll = (uint32_t *)gh;
+  }
+
+  // ---- launch ---------------------------------------------------------------------------------
+  HIP_TRY(hipEventRecord(dev->ev[0], st));
+  HIP_TRY(hipMemcpyAsync(dblob, blob.data.data(), blob.data.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)nseg * 8, st));
+  if (nhll && !group_by) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, (size_t)nhll * (1 << log2m) * 4, st));
+  if (inv_words_total) {
+    HIP_TRY(hipMemsetAsync(inv_words, 0, inv_words_total * 8, st));
+    HIP_TRY(launch_roaring_or((const RoaringTask *)(base + tasks_off), (int32_t)tasks.size(), st));
+  }
+  if (group_by) {
+    HIP_TRY(hipMemsetAsync(dq.gb_count, 0, (size_t)dq.num_groups * 8, st));
+    for (int a = 0; a < naggs; a++) {
+      uint64_t init = 0;
+      if (dq.aggs[a].acc == ACC_MIN_F64) init = ~0ull;  // ordered(+inf) < ~0: atomicMin from the top
+      if (dq.aggs[a].acc == ACC_MAX_F64) init = 0ull;
+      HIP_TRY(launch_fill_u64(dq.gb_table + (int64_t)a * dq.num_groups, dq.num_groups, init, st));
+    }
+    if (nhll) HIP_TRY(hipMemsetAsync(dq.gb_hll, 0, (size_t)nhll * dq.num_groups * (1 << log2m) * 4, st));
+  }
+  size_t lds = (size_t)round_up((int64_t)(group_by ? 0 : nhll * (1 << std::max(log2m, 0)) * 4), 16) +
+               (size_t)(kBlock / 64) * nslots * 8;
+  HIP_TRY(hipEventRecord(dev->ev[1], st));
+  HIP_TRY(launch_scan(dq, nblocks, lds, group_by, st));
+  HIP_TRY(hipEventRecord(dev->ev[2], st));
+  HIP_TRY(launch_finalize_partials((const uint64_t *)partials, nblocks, nslots, (const int32_t *)(base + kinds_off),
+                                   (uint64_t *)finals, st));
+
+  auto impl = std::make_unique<ResultImpl>();
+  phip_result &r = impl->pub;
+  memset(&r, 0, sizeof(r));
+  std::vector<uint64_t> fin(nslots);
+  std::vector<uint64_t> segm(nseg);
+  std::vector<uint32_t> hll_host;
+  HIP_TRY(hipMemcpyAsync(fin.data(), finals, nslots * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(segm.data(), seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
+  if (nhll && !group_by) {
+    hll_host.resize((size_t)nhll << log2m);
+    HIP_TRY(hipMemcpyAsync(hll_host.data(), dq.hll_regs, hll_host.size() * 4, hipMemcpyDeviceToHost, st));
+  }
+  if (filter_words)
+    HIP_TRY(hipMemcpyAsync(filter_words, dq.filter_out, (size_t)filter_nwords * 8, hipMemcpyDeviceToHost, st));
+
+  int64_t ngroups = 1;
+  if (group_by) {
+    const int64_t nchunks = ceil_div(dq.num_groups, 1024);
+    void *cc, *offs, *keys;
+    rc = dev->ws.get("gb_chunk_counts", (size_t)nchunks * 4, &cc);
+    if (rc) return rc;
+    rc = dev->ws.get("gb_offsets", (size_t)(nchunks + 1) * 8, &offs);
+    if (rc) return rc;
+    HIP_TRY(launch_group_count(dq.gb_count, dq.num_groups, (int32_t *)cc, nchunks, (int64_t *)offs, st));
+    int64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    ngroups = total;
+    rc = dev->ws.get("gb_keys", (size_t)std::max<int64_t>(ngroups, 1) * 8, &keys);
+    if (rc) return rc;
+    void *ov, *ol, *oh = nullptr;
+    rc = dev->ws.get("gb_out_vals", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ov);
+    if (rc) return rc;
+    rc = dev->ws.get("gb_out_longs", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ol);
+    if (rc) return rc;
+    if (nhll) {
+      rc = dev->ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * (1 << log2m), &oh);
+      if (rc) return rc;
+    }
+    HIP_TRY(launch_group_compact(dq.gb_count, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
+    HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, (const int32_t *)(base + kinds_off),
+                                dq.gb_table, dq.gb_count, dq.gb_hll, nhll, log2m, (double *)ov, (int64_t *)ol,
+                                (uint8_t *)oh, st));
+    std::vector<int64_t> hkeys(ngroups);
+    impl->values.resize(ngroups * naggs);
+    impl->longs.resize(ngroups * naggs);
+    impl->hll.resize((size_t)ngroups * nhll * (nhll ? (1 << log2m) : 0));
+    if (ngroups) {
+      HIP_TRY(hipMemcpyAsync(hkeys.data(), keys, ngroups * 8, hipMemcpyDeviceToHost, st));
+      if (naggs) {
+        HIP_TRY(hipMemcpyAsync(impl->values.data(), ov, ngroups * naggs * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(impl->longs.data(), ol, ngroups * naggs * 8, hipMemcpyDeviceToHost, st));
+      }
+      if (nhll) HIP_TRY(hipMemcpyAsync(impl->hll.data(), oh, impl->hll.size(), hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipEventRecord(dev->ev[3], st));
+    HIP_TRY(hipStreamSynchronize(st));
+    impl->keys.resize(ngroups * q->num_group_by);
+    for (int64_t g = 0; g < ngroups; g++) {
+      int64_t key = hkeys[g];
+      for (int k = 0; k < q->num_group_by; k++) {
+        impl->keys[g * q->num_group_by + k] = (int32_t)(key % gb_dicts[k]->card);
+        key /= gb_dicts[k]->card;
+      }
+    }
+    impl->dicts = gb_dicts;
+    if (q->num_groups_limit > 0 && ngroups > q->num_groups_limit) r.num_groups_limit_reached = 1;
+  } else {
+    HIP_TRY(hipEventRecord(dev->ev[3], st));
+    HIP_TRY(hipStreamSynchronize(st));
+    impl->values.resize(naggs);
+    impl->longs.resize(naggs);
+    impl->hll.resize((size_t)nhll << (nhll ? log2m : 0));
+    for (int a = 0; a < naggs; a++) {
+      uint64_t v = fin[a];
+      double d = 0.0;
+      int64_t l = 0;
+      switch (dq.aggs[a].acc) {
+        case ACC_COUNT:
+        case ACC_SUM_I64: l = (int64_t)v; d = (double)l; break;
+        default: memcpy(&d, &v, 8);
+      }
+      impl->values[a] = d;
+      impl->longs[a] = l;
+    }
+    for (size_t i = 0; i < hll_host.size(); i++) impl->hll[i] = (uint8_t)hll_host[i];
+  }
+  float t_all = 0.f, t_scan = 0.f;
+  HIP_TRY(hipEventElapsedTime(&t_all, dev->ev[0], dev->ev[3]));
+  HIP_TRY(hipEventElapsedTime(&t_scan, dev->ev[1], dev->ev[2]));
+
+  r.num_docs_scanned = (int64_t)fin[naggs];
+  r.num_entries_scanned_in_filter = (int64_t)fin[naggs + 1];
+  r.num_entries_scanned_post_filter = r.num_docs_scanned * num_projected;
+  r.num_total_docs = total_docs;
+  r.num_segments_processed = nseg;
+  for (int s = 0; s < nseg; s++) r.num_segments_matched += segm[s] ? 1 : 0;
+  r.num_aggregations = naggs;
+  r.num_groups = group_by ? ngroups : 1;
+  r.num_group_by = q->num_group_by;
+  r.num_hll = nhll;
+  r.values = impl->values.data();
+  r.long_values = impl->longs.data();
+  r.hll_registers = impl->hll.data();
+  r.group_keys = impl->keys.data();
+  r.scan_kernel_ms = t_scan;
+  r.device_ms = t_all;
+  if (out_result) {
+    *out_result = &impl.release()->pub;
+  }
+  return PHIP_OK;
+}
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+PHIP_API const char *phip_last_error(void) { return g_err.c_str(); }
+PHIP_API const char *phip_version(void) { return "pinot_hip 0.1.0 gfx950"; }
+
+PHIP_API int32_t phip_device_count(int32_t *out_count) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  if (out_count) *out_count = n;
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_init(const int32_t *devices, int32_t num_devices) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (!g_devices.empty()) return PHIP_OK;
+  if (!devices || num_devices <= 0) return ensure_devices_locked();
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(PHIP_ERR_NO_DEVICE, "no HIP device available");
+  for (int i = 0; i < num_devices; i++) {
+    if (devices[i] < 0 || devices[i] >= n) return fail(PHIP_ERR_INVALID, "device %d out of range", devices[i]);
+    auto d = std::make_unique<Device>();
+    d->ordinal = devices[i];
+    HIP_TRY(hipSetDevice(d->ordinal));
+    HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
+    g_devices.push_back(std::move(d));
+  }
+  return PHIP_OK;
+}
+
+static void free_segment(Segment &s) {
+  (void)hipSetDevice(s.device);
+  for (void *p : s.allocations) (void)hipFree(p);
+  for (auto &c : s.cols)
+    for (auto &kv : c.hll) (void)hipFree(kv.second);
+  s.allocations.clear();
+}
+
+PHIP_API int32_t phip_shutdown(void) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto &kv : g_segments) free_segment(*kv.second);
+  g_segments.clear();
+  for (auto &d : g_devices) {
+    std::lock_guard<std::mutex> dl(d->mu);
+    (void)hipSetDevice(d->ordinal);
+    d->ws.release();
+    for (auto &kv : d->remaps)
+      for (auto *p : kv.second->dev)
+        if (p) (void)hipFree(p);
+    d->remaps.clear();
+    for (auto &e : d->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(d->stream);
+  }
+  g_devices.clear();
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_segment_load(const phip_segment_desc *desc, uint64_t *out_handle) {
+  if (!desc || !out_handle) return fail(PHIP_ERR_INVALID, "null argument");
+  if (desc->num_docs < 0 || desc->num_columns < 0 || (desc->num_columns > 0 && !desc->columns))
+    return fail(PHIP_ERR_INVALID, "bad segment descriptor");
+  Device *dev;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    int32_t rc = ensure_devices_locked();
+    if (rc) return rc;
+    dev = desc->device >= 0 ? find_device(desc->device) : g_devices[0].get();
+    if (!dev) return fail(PHIP_ERR_NO_DEVICE, "device %d not initialised (call phip_init)", desc->device);
+  }
+  std::lock_guard<std::mutex> dl(dev->mu);
+  HIP_TRY(hipSetDevice(dev->ordinal));
+  auto seg = std::make_unique<Segment>();
+  seg->device = dev->ordinal;
+  seg->num_docs = desc->num_docs;
+  seg->name = desc->name ? desc->name : "";
+  std::vector<void *> temps;
+  int32_t rc = PHIP_OK;
+  for (int c = 0; c < desc->num_columns && rc == PHIP_OK; c++) {
+    if (desc->columns[c].name && seg->by_name.count(desc->columns[c].name)) {
+      rc = fail(PHIP_ERR_INVALID, "duplicate column %s", desc->columns[c].name);
+      break;
+    }
+    rc = load_column(desc->columns[c], *seg, dev->stream, temps);
+  }
+  hipError_t se = hipStreamSynchronize(dev->stream);
+  for (void *p : temps) (void)hipFree(p);
+  if (rc == PHIP_OK && se != hipSuccess) rc = fail(PHIP_ERR_HIP, "segment load: %s", hipGetErrorString(se));
+  if (rc != PHIP_OK) {
+    free_segment(*seg);
+    return rc;
+  }
+  seg->handle = g_next_handle++;
+  *out_handle = seg->handle;
+  std::lock_guard<std::mutex> g(g_mu);
+  g_segments[seg->handle] = std::move(seg);
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_segment_unload(uint64_t handle) {
+  std::unique_ptr<Segment> seg;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_segments.find(handle);
+    if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle %llu", (unsigned long long)handle);
+    seg = std::move(it->second);
+    g_segments.erase(it);
+  }
+  Device *dev = find_device(seg->device);
+  if (dev) {
+    std::lock_guard<std::mutex> dl(dev->mu);  // waits for in-flight queries on the device
+    (void)hipSetDevice(dev->ordinal);
+    (void)hipStreamSynchronize(dev->stream);
+    for (auto it = dev->remaps.begin(); it != dev->remaps.end();) {
+      if (it->first.find(":" + std::to_string(handle)) != std::string::npos) {
+        for (auto *p : it->second->dev)
+          if (p) (void)hipFree(p);
+        it = dev->remaps.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    free_segment(*seg);
+  } else {
+    free_segment(*seg);
+  }
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_segment_device_bytes(uint64_t handle, uint64_t *out_bytes) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_segments.find(handle);
+  if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle");
+  if (out_bytes) *out_bytes = it->second->device_bytes;
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_query(const phip_query_desc *query, phip_result **out_result) {
+  if (!out_result) return fail(PHIP_ERR_INVALID, "null result pointer");
+  *out_result = nullptr;
+  return run_query(query, out_result, nullptr, 0);
+}
+
+PHIP_API int32_t phip_result_dictionary(const phip_result *result, int32_t k, phip_dictionary_view *out) {
+  if (!result || !out) return fail(PHIP_ERR_INVALID, "null argument");
+  const ResultImpl *impl = reinterpret_cast<const ResultImpl *>(result);
+  if (k < 0 || k >= (int)impl->dicts.size()) return fail(PHIP_ERR_INVALID, "group-by index out of range");
+  const auto &d = impl->dicts[k];
+  out->data_type = d->type;
+  out->cardinality = d->card;
+  out->string_width = d->width;
+  out->reserved = 0;
+  out->values = d->values.data();
+  return PHIP_OK;
+}
+
+PHIP_API void phip_result_free(phip_result *result) {
+  if (result) delete reinterpret_cast<ResultImpl *>(result);
+}
+
+PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *words_out, int64_t num_words) {
+  if (!query || !words_out || query->num_segments != 1) return fail(PHIP_ERR_INVALID, "filter bitmap: one segment");
+  phip_query_desc q = *query;
+  q.num_aggregations = 0;
+  q.num_group_by = 0;
+  phip_result *r = nullptr;
+  int32_t rc;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_segments.find(query->segments[0]);
+    if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle");
+    if (num_words < ceil_div(it->second->num_docs, 64)) return fail(PHIP_ERR_INVALID, "words_out too small");
+  }
+  rc = run_query(&q, &r, words_out, num_words);
+  if (r) phip_result_free(r);
+  return rc;
+}
+
+}  // extern "C"

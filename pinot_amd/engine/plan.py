@@ -1,0 +1,457 @@
+"""GPU plan maker and operators (host mirror of the reference's operator surface).
+
+  GpuInstancePlanMaker   InstancePlanMakerImplV2 (pinot-core/.../plan/maker/InstancePlanMakerImplV2.java:172-308)
+                         selected when the query option ``useGpu`` is set; builds ONE combine-level
+                         GPU operator over all segments instead of per-segment plan nodes.
+  filter compilation     FilterPlanNode.constructPhysicalOperator (pinot-core/.../plan/FilterPlanNode.java:195-320):
+                         per segment, constant-folds always-true/false predicates, then picks the leaf
+                         like FilterOperatorUtils.DefaultImplementation (…/operator/filter/FilterOperatorUtils.java:98-131):
+                         sorted index > inverted index > scan.
+  GpuCombineOperator     replaces AggregationOperator / GroupByOperator per segment plus the
+                         CombineOperator merge (…/operator/combine/BaseSingleBlockCombineOperator.java:58-162)
+                         with one phip_query call.
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+
+from .. import _lib
+from ..query import predicate as predeval
+from ..query.context import (AggregationInfo, FilterContext, Function, Identifier, Literal, QueryContext,
+                             columns_of)
+from ..query.sql import parse
+from ..spi import DEFAULT_NUM_GROUPS_LIMIT, DataType
+from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock
+from .segment import GpuSegment
+
+
+class UnsupportedOnGpu(Exception):
+    """Query shape outside the GPU subset (the Java side would call super.makeInstancePlan)."""
+
+
+# ------------------------------------------------------------------------------ filter trees
+@dataclass
+class _Leaf:
+    kind: int
+    column: Optional[str] = None
+    lo: int = 0
+    hi: int = 0
+    exclusive: bool = False
+    ids: Optional[np.ndarray] = None  # int32
+
+
+@dataclass
+class _Node:
+    op: int
+    children: list = field(default_factory=list)
+
+
+_TRUE = _Leaf(_lib.LEAF_MATCH_ALL)
+_FALSE = _Leaf(_lib.LEAF_MATCH_NONE)
+
+
+def _is_const(n, which):
+    return isinstance(n, _Leaf) and n.kind == which.kind and n.column is None
+
+
+def _doc_ranges_for(seg: GpuSegment, column: str, ev: predeval.DictPredicateEvaluation) -> np.ndarray:
+    """Sorted column: matching dict ids -> merged inclusive doc ranges (SortedIndexBasedFilterOperator.java:52-132)."""
+    card = seg.column_metadata(column).cardinality
+    ids = ev.matching_dict_ids(card)
+    ranges = []
+    for d in ids:
+        s, e = seg.sorted_doc_range(column, d)
+        if ranges and ranges[-1][1] + 1 == s:
+            ranges[-1][1] = e
+        else:
+            ranges.append([s, e])
+    return np.asarray(ranges, dtype=np.int32).reshape(-1)
+
+
+def compile_predicate(seg: GpuSegment, pred) -> object:
+    column = pred.column
+    m = seg.column_metadata(column)
+    if not m.has_dictionary:
+        raise UnsupportedOnGpu(f"predicate on raw (no-dictionary) column {column}")
+    ev = predeval.evaluate(pred, seg.dictionary(column))
+    if ev.always_false:
+        return _FALSE
+    if ev.always_true:
+        return _TRUE
+    if m.is_sorted:
+        return _Leaf(_lib.LEAF_DOC_RANGES, column, ids=_doc_ranges_for(seg, column, ev))
+    if m.has_inverted_index and pred.type != "RANGE":
+        if ev.kind == "range":
+            ids = np.arange(ev.start, ev.end, dtype=np.int32)
+            return _Leaf(_lib.LEAF_INVERTED, column, ids=ids)
+        return _Leaf(_lib.LEAF_INVERTED, column, exclusive=ev.exclusive, ids=np.asarray(ev.ids, dtype=np.int32))
+    if ev.kind == "range":
+        return _Leaf(_lib.LEAF_DICT_RANGE, column, lo=ev.start, hi=ev.end)
+    return _Leaf(_lib.LEAF_DICT_SET, column, exclusive=ev.exclusive, ids=np.asarray(ev.ids, dtype=np.int32))
+
+
+def compile_filter(seg: GpuSegment, fc: Optional[FilterContext]):
+    """FilterContext -> leaf/node tree for one segment, constants folded (FilterPlanNode.java:197-229)."""
+    if fc is None:
+        return _TRUE
+    if fc.type == "PREDICATE":
+        return compile_predicate(seg, fc.predicate)
+    if fc.type == "CONSTANT":
+        return _TRUE if fc.constant else _FALSE
+    if fc.type == "NOT":
+        c = compile_filter(seg, fc.children[0])
+        if _is_const(c, _TRUE):
+            return _FALSE
+        if _is_const(c, _FALSE):
+            return _TRUE
+        if isinstance(c, _Leaf) and c.kind in (_lib.LEAF_DICT_SET, _lib.LEAF_INVERTED):
+            return _Leaf(c.kind, c.column, c.lo, c.hi, not c.exclusive, c.ids)
+        return _Node(_lib.NODE_NOT, [c])
+    kids = [compile_filter(seg, c) for c in fc.children]
+    if fc.type == "AND":
+        if any(_is_const(k, _FALSE) for k in kids):
+            return _FALSE
+        kids = [k for k in kids if not _is_const(k, _TRUE)]
+        if not kids:
+            return _TRUE
+        if len(kids) == 1:
+            return kids[0]
+        # evaluation order (FilterOperatorUtils :205-252): sorted < bitmap < scan
+        prio = {_lib.LEAF_DOC_RANGES: 0, _lib.LEAF_INVERTED: 1, _lib.LEAF_DICT_RANGE: 3, _lib.LEAF_DICT_SET: 3}
+        kids.sort(key=lambda k: prio.get(k.kind, 2) if isinstance(k, _Leaf) else (4 if k.op == _lib.NODE_AND else 5))
+        return _Node(_lib.NODE_AND, kids)
+    if fc.type == "OR":
+        if any(_is_const(k, _TRUE) for k in kids):
+            return _TRUE
+        kids = [k for k in kids if not _is_const(k, _FALSE)]
+        if not kids:
+            return _FALSE
+        if len(kids) == 1:
+            return kids[0]
+        return _Node(_lib.NODE_OR, kids)
+    raise ValueError(fc.type)
+
+
+def _flatten(tree, col_index, out, keep):
+    if isinstance(tree, _Leaf):
+        n = _lib.FilterNode()
+        n.op = _lib.NODE_LEAF
+        n.leaf_kind = tree.kind
+        n.column = col_index[tree.column] if tree.column is not None else -1
+        n.lo, n.hi = tree.lo, tree.hi
+        n.exclusive = int(tree.exclusive)
+        if tree.ids is not None:
+            ids = np.ascontiguousarray(tree.ids, dtype=np.int32)
+            keep.append(ids)
+            n.count = len(ids) // 2 if tree.kind == _lib.LEAF_DOC_RANGES else len(ids)
+            n.ids = ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        out.append(n)
+        return
+    n = _lib.FilterNode()
+    n.op = tree.op
+    n.num_children = len(tree.children)
+    out.append(n)
+    for c in tree.children:
+        _flatten(c, col_index, out, keep)
+
+
+def _leaf_columns(tree, acc):
+    if isinstance(tree, _Leaf):
+        if tree.column is not None and tree.column not in acc:
+            acc.append(tree.column)
+    else:
+        for c in tree.children:
+            _leaf_columns(c, acc)
+
+
+# ------------------------------------------------------------------------------ aggregations
+def _strip_cast(e):
+    while isinstance(e, Function) and e.name == "cast":
+        e = e.args[0]
+    return e
+
+
+def _gpu_expr(e):
+    """Aggregation argument -> (PHIP_EXPR_*, col_a, col_b)."""
+    e = _strip_cast(e)
+    if isinstance(e, Identifier):
+        return _lib.EXPR_COLUMN, e.name, None
+    if isinstance(e, Function) and e.name in ("times", "minus", "plus") and len(e.args) == 2:
+        a, b = _strip_cast(e.args[0]), _strip_cast(e.args[1])
+        if isinstance(a, Identifier) and isinstance(b, Identifier):
+            op = {"times": _lib.EXPR_MUL, "minus": _lib.EXPR_SUB, "plus": _lib.EXPR_ADD}[e.name]
+            return op, a.name, b.name
+    raise UnsupportedOnGpu(f"aggregation argument {e} is outside the GPU expression subset")
+
+
+def plan_aggregations(aggs: Sequence[AggregationInfo]):
+    """Query aggregations -> GPU primitives (deduplicated) + per-function slot mapping."""
+    prims = []  # (function, expr, col_a, col_b, log2m)
+    mapping = []
+
+    def slot(p):
+        if p not in prims:
+            prims.append(p)
+        return prims.index(p)
+
+    for ag in aggs:
+        f = ag.function
+        if f == "count":
+            mapping.append(("count", slot((_lib.AGG_COUNT, 0, None, None, 0))))
+            continue
+        expr = _gpu_expr(ag.argument)
+        if f == "sum":
+            mapping.append(("sum", slot((_lib.AGG_SUM,) + expr + (0,))))
+        elif f == "min":
+            mapping.append(("min", slot((_lib.AGG_MIN,) + expr + (0,))))
+        elif f == "max":
+            mapping.append(("max", slot((_lib.AGG_MAX,) + expr + (0,))))
+        elif f == "avg":
+            mapping.append(("avg", (slot((_lib.AGG_SUM,) + expr + (0,)), slot((_lib.AGG_COUNT, 0, None, None, 0)))))
+        elif f == "minmaxrange":
+            mapping.append(("minmaxrange", (slot((_lib.AGG_MIN,) + expr + (0,)), slot((_lib.AGG_MAX,) + expr + (0,)))))
+        elif f in ("distinctcounthll", "distinctcountrawhll"):
+            if expr[0] != _lib.EXPR_COLUMN:
+                raise UnsupportedOnGpu("DISTINCTCOUNTHLL over an expression")
+            mapping.append((f, slot((_lib.AGG_HLL,) + expr + (ag.log2m,))))
+        else:
+            raise UnsupportedOnGpu(f"aggregation {f} is not on the GPU path")
+    return prims, mapping
+
+
+# ------------------------------------------------------------------------------ operators
+class GpuCombineOperator:
+    """One operator over all segments of the query (the all-segment GPU variant of SURVEY.md §8b)."""
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
+        self.query = query
+        self.segments = list(segments)
+        self.num_groups_limit = num_groups_limit
+        for e in query.group_by:
+            if not isinstance(e, Identifier):
+                raise UnsupportedOnGpu(f"group-by expression {e}")
+        self.prims, self.mapping = plan_aggregations(query.aggregations)
+        self.trees = [compile_filter(s, query.filter) for s in self.segments]
+        cols = []
+        for t in self.trees:
+            _leaf_columns(t, cols)
+        for p in self.prims:
+            for c in (p[2], p[3]):
+                if c is not None and c not in cols:
+                    cols.append(c)
+        for e in query.group_by:
+            if e.name not in cols:
+                cols.append(e.name)
+        self.columns = cols
+        for s in self.segments:
+            for c in cols:
+                if not s.has_column(c):
+                    raise KeyError(f"segment {s.name} has no column {c}")
+
+    def _desc(self, keep):
+        col_index = {c: i for i, c in enumerate(self.columns)}
+        q = _lib.QueryDesc()
+        names = (ctypes.c_char_p * max(len(self.columns), 1))(*[c.encode() for c in self.columns])
+        keep.append(names)
+        q.num_columns = len(self.columns)
+        q.columns = names
+        handles = (ctypes.c_uint64 * len(self.segments))(*[s.handle for s in self.segments])
+        keep.append(handles)
+        q.num_segments = len(self.segments)
+        q.segments = handles
+        nodes = []
+        offsets = [0]
+        for t in self.trees:
+            if not _is_const(t, _TRUE):
+                _flatten(t, col_index, nodes, keep)
+            offsets.append(len(nodes))
+        offs = (ctypes.c_int32 * len(offsets))(*offsets)
+        keep.append(offs)
+        q.filter_offsets = offs
+        arr = (_lib.FilterNode * max(len(nodes), 1))(*nodes)
+        keep.append(arr)
+        q.filter_nodes = arr
+        aggs = (_lib.Aggregation * max(len(self.prims), 1))()
+        for i, (f, expr, ca, cb, log2m) in enumerate(self.prims):
+            aggs[i].function = f
+            aggs[i].expr = expr
+            aggs[i].column_a = col_index[ca] if ca is not None else -1
+            aggs[i].column_b = col_index[cb] if cb is not None else -1
+            aggs[i].log2m = log2m
+        keep.append(aggs)
+        q.num_aggregations = len(self.prims)
+        q.aggregations = aggs
+        gb = (ctypes.c_int32 * max(len(self.query.group_by), 1))(*[col_index[e.name] for e in self.query.group_by])
+        keep.append(gb)
+        q.num_group_by = len(self.query.group_by)
+        q.group_by_columns = gb
+        q.num_groups_limit = self.num_groups_limit
+        return q
+
+    def filter_bitmap(self) -> np.ndarray:
+        """BaseFilterOperator.getTrues for a single segment, as 64-doc bitmap words."""
+        if len(self.segments) != 1:
+            raise ValueError("filter_bitmap takes one segment")
+        keep = []
+        q = self._desc(keep)
+        nwords = (self.segments[0].num_docs + 63) // 64
+        out = np.zeros(max(nwords, 1), dtype=np.uint64)
+        _lib.check(_lib.load().phip_filter_bitmap(ctypes.byref(q), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                                  len(out)))
+        return out[:nwords]
+
+    def run_raw(self):
+        keep = []
+        q = self._desc(keep)
+        res = ctypes.POINTER(_lib.Result)()
+        _lib.check(_lib.load().phip_query(ctypes.byref(q), ctypes.byref(res)))
+        return res
+
+    # -- NonScanBasedAggregationOperator (AggregationPlanNode.java:107-118, isFitForNonScanBasedPlan :165-190)
+    _NON_SCAN = ("count", "min", "max", "minmaxrange", "distinctcounthll", "distinctcountrawhll")
+
+    def _non_scan_fit(self):
+        if self.query.group_by or not all(_is_const(t, _TRUE) for t in self.trees):
+            return False
+        for ag in self.query.aggregations:
+            if ag.function not in self._NON_SCAN:
+                return False
+            if ag.function == "count":
+                continue
+            if not isinstance(ag.argument, Identifier):
+                return False
+            for s in self.segments:
+                if not s.column_metadata(ag.argument.name).has_dictionary:
+                    return False
+        return True
+
+    def _non_scan_block(self):
+        from . import hll
+        results = None
+        stats = ExecutionStatistics()
+        for s in self.segments:
+            seg_res = []
+            for ag in self.query.aggregations:
+                if ag.function == "count":
+                    seg_res.append(s.num_docs)
+                    continue
+                d = s.dictionary(ag.argument.name)
+                if ag.function == "min":
+                    seg_res.append(float(d.get(0)))
+                elif ag.function == "max":
+                    seg_res.append(float(d.get(len(d) - 1)))
+                elif ag.function == "minmaxrange":
+                    seg_res.append((float(d.get(0)), float(d.get(len(d) - 1))))
+                else:
+                    seg_res.append(hll.registers_of_hashes(hll.hash_values(d.values, d.data_type), ag.log2m))
+            if results is None:
+                results = seg_res
+            else:
+                from .results import merge_intermediate
+                results = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(self.query.aggregations, results, seg_res)]
+            stats.merge(ExecutionStatistics(s.num_docs, 0, 0, s.num_docs, 1, 1 if s.num_docs else 0))
+        return AggregationResultsBlock(self.query.aggregations, results, stats)
+
+    def next_block(self):
+        if self._non_scan_fit():
+            return self._non_scan_block()
+        lib = _lib.load()
+        res = self.run_raw()
+        try:
+            r = res.contents
+            stats = ExecutionStatistics(r.num_docs_scanned, r.num_entries_scanned_in_filter,
+                                        r.num_entries_scanned_post_filter, r.num_total_docs,
+                                        r.num_segments_processed, r.num_segments_matched)
+            na = r.num_aggregations
+            ng = r.num_groups
+            m = 1 << max([p[4] for p in self.prims if p[0] == _lib.AGG_HLL] + [0])
+            vals = np.ctypeslib.as_array(r.values, shape=(max(ng * na, 1),))[:ng * na].reshape(ng, na).copy() if na else np.zeros((ng, 0))
+            longs = np.ctypeslib.as_array(r.long_values, shape=(max(ng * na, 1),))[:ng * na].reshape(ng, na).copy() if na else np.zeros((ng, 0), np.int64)
+            hll = None
+            if r.num_hll:
+                hll = np.ctypeslib.as_array(r.hll_registers, shape=(ng * r.num_hll * m,)).reshape(ng, r.num_hll, m).copy()
+            hll_slot = {}
+            for i, p in enumerate(self.prims):
+                if p[0] == _lib.AGG_HLL:
+                    hll_slot[i] = len(hll_slot)
+            integral = self._integral_sums()
+
+            def prim_value(g, i):
+                f = self.prims[i][0]
+                if f == _lib.AGG_COUNT:
+                    return int(longs[g, i])
+                if f == _lib.AGG_SUM:
+                    return int(longs[g, i]) if integral[i] else float(vals[g, i])
+                if f in (_lib.AGG_MIN, _lib.AGG_MAX):
+                    return float(vals[g, i])
+                return hll[g, hll_slot[i]].copy()
+
+            def intermediates(g):
+                out = []
+                for f, s in self.mapping:
+                    if f in ("avg", "minmaxrange"):
+                        out.append((prim_value(g, s[0]), prim_value(g, s[1])))
+                    else:
+                        out.append(prim_value(g, s))
+                return out
+
+            if not self.query.group_by:
+                blk = AggregationResultsBlock(self.query.aggregations, intermediates(0), stats)
+            else:
+                nk = r.num_group_by
+                keys = np.ctypeslib.as_array(r.group_keys, shape=(max(ng * nk, 1),))[:ng * nk].reshape(ng, nk) if ng else np.zeros((0, nk), np.int32)
+                dicts = []
+                for k in range(nk):
+                    dv = _lib.DictionaryView()
+                    _lib.check(lib.phip_result_dictionary(res, k, ctypes.byref(dv)))
+                    dicts.append(_dictionary_values(dv))
+                groups = {}
+                for g in range(ng):
+                    key = tuple(dicts[k][keys[g, k]] for k in range(nk))
+                    groups[key] = intermediates(g)
+                blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
+                                          bool(r.num_groups_limit_reached))
+            blk.device_ms = r.device_ms
+            blk.scan_kernel_ms = r.scan_kernel_ms
+            return blk
+        finally:
+            lib.phip_result_free(res)
+
+    def _integral_sums(self):
+        out = {}
+        for i, p in enumerate(self.prims):
+            if p[0] != _lib.AGG_SUM:
+                continue
+            ok = True
+            for s in self.segments:
+                for c in (p[2], p[3]):
+                    if c is not None and not s.column_metadata(c).data_type.is_integral:
+                        ok = False
+            out[i] = ok
+        return out
+
+
+def _dictionary_values(dv):
+    card = dv.cardinality
+    t = DataType(dv.data_type)
+    if t == DataType.STRING:
+        w = dv.string_width
+        raw = ctypes.string_at(dv.values, card * w)
+        return [raw[i * w:(i + 1) * w].rstrip(b"\0").decode("utf-8") for i in range(card)]
+    dt = {DataType.INT: np.int32, DataType.LONG: np.int64, DataType.FLOAT: np.float32, DataType.DOUBLE: np.float64}[t]
+    arr = np.ctypeslib.as_array(ctypes.cast(dv.values, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(card,))
+    return [x.item() for x in arr]
+
+
+class GpuInstancePlanMaker:
+    """``pinot.server.query.executor.plan.maker.class`` plug-in."""
+
+    def __init__(self, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT):
+        self.num_groups_limit = num_groups_limit
+
+    def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]) -> GpuCombineOperator:
+        if isinstance(query, str):
+            query = parse(query)
+        return GpuCombineOperator(query, segments, self.num_groups_limit)

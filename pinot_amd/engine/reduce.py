@@ -1,0 +1,143 @@
+"""Broker-side reduce of server results blocks into a result table.
+
+Mirrors what the reference tests observe through BrokerReduceService (pinot-core/.../query/reduce/):
+AggregationDataTableReducer / GroupByDataTableReducer merge intermediates across server responses
+(AggregationFunction.merge), extract final results (extractFinalResult), apply ORDER BY / LIMIT, and
+name columns by alias or by the canonical expression. ``broker_response`` mirrors
+BaseQueriesTest.getBrokerResponse (pinot-core/src/test/java/org/apache/pinot/queries/BaseQueriesTest.java:207-247):
+the server response is reduced as if it came from an OFFLINE and a REALTIME server.
+"""
+import math
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+
+from ..query.context import Function, Identifier, Literal, QueryContext, SUPPORTED_AGGREGATIONS
+from ..spi import DEFAULT_HYPERLOGLOG_LOG2M
+from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock, merge_intermediate
+
+
+def hll_cardinality(regs: np.ndarray) -> int:
+    """clearspring HyperLogLog.cardinality() (stream-lib 2.9.8; DistinctCountHLLAggregationFunction.java:362-365)."""
+    m = len(regs)
+    log2m = m.bit_length() - 1
+    if log2m == 4:
+        alpha_mm = 0.673 * m * m
+    elif log2m == 5:
+        alpha_mm = 0.697 * m * m
+    elif log2m == 6:
+        alpha_mm = 0.709 * m * m
+    else:
+        alpha_mm = (0.7213 / (1 + 1.079 / m)) * m * m
+    s = 0.0
+    zeros = 0
+    for r in regs.tolist():
+        s += 1.0 / (1 << r)
+        zeros += r == 0
+    est = alpha_mm * (1.0 / s)
+    if est <= 2.5 * m:
+        return int(math.floor(m * math.log(m / zeros) + 0.5))
+    return int(math.floor(est + 0.5))
+
+
+def final_result(function: str, v):
+    """AggregationFunction.extractFinalResult."""
+    if function == "count":
+        return int(v)
+    if function == "sum":
+        return float(v)
+    if function in ("min", "max"):
+        return float(v)
+    if function == "avg":
+        s, c = v
+        return float(s) / c if c else float("-inf")
+    if function == "minmaxrange":
+        return float(v[1]) - float(v[0])
+    if function in ("distinctcounthll", "distinctcountrawhll"):
+        return hll_cardinality(v)
+    raise NotImplementedError(function)
+
+
+@dataclass
+class ResultTable:
+    columns: List[str]
+    rows: List[list]
+    stats: ExecutionStatistics = field(default_factory=ExecutionStatistics)
+    num_groups_limit_reached: bool = False
+
+
+def _agg_index(query: QueryContext, expr):
+    for i, a in enumerate(query.aggregations):
+        if isinstance(expr, Function) and expr.name == a.function:
+            if a.function == "count" or (expr.args and expr.args[0] == a.argument):
+                return i
+    return None
+
+
+def _column_name(expr, alias):
+    if alias:
+        return alias
+    if isinstance(expr, Function) and expr.name == "count":
+        return "count(*)"
+    return str(expr)
+
+
+def reduce_blocks(query: QueryContext, blocks) -> ResultTable:
+    stats = ExecutionStatistics()
+    for b in blocks:
+        stats.merge(b.stats)
+    names = [_column_name(e, a) for e, a in query.select]
+    if not query.group_by:
+        merged = None
+        for b in blocks:
+            if merged is None:
+                merged = list(b.results)
+            else:
+                merged = [merge_intermediate(a.function, x, y) for a, x, y in zip(query.aggregations, merged, b.results)]
+        finals = [final_result(a.function, v) for a, v in zip(query.aggregations, merged)]
+        row = []
+        for e, _ in query.select:
+            i = _agg_index(query, e)
+            if i is None:
+                raise NotImplementedError(f"post-aggregation expression {e}")
+            row.append(finals[i])
+        return ResultTable(names, [row], stats)
+
+    groups = {}
+    limit_reached = False
+    for b in blocks:
+        limit_reached |= b.num_groups_limit_reached
+        for k, v in b.groups.items():
+            if k in groups:
+                groups[k] = [merge_intermediate(a.function, x, y) for a, x, y in zip(query.aggregations, groups[k], v)]
+            else:
+                groups[k] = list(v)
+    gb_index = {str(e): i for i, e in enumerate(query.group_by)}
+    records = []
+    for k, v in groups.items():
+        finals = [final_result(a.function, x) for a, x in zip(query.aggregations, v)]
+        records.append((k, finals))
+
+    def value_of(expr, rec):
+        k, finals = rec
+        if str(expr) in gb_index:
+            return k[gb_index[str(expr)]]
+        i = _agg_index(query, expr)
+        if i is None:
+            raise NotImplementedError(f"order-by/select expression {expr}")
+        return finals[i]
+
+    for ob in reversed(query.order_by):
+        records.sort(key=lambda rec: value_of(ob.expression, rec), reverse=not ob.ascending)
+    records = records[:query.limit]
+    rows = [[value_of(e, rec) for e, _ in query.select] for rec in records]
+    return ResultTable(names, rows, stats, limit_reached)
+
+
+def broker_response(plan_maker, query, segments) -> ResultTable:
+    """BaseQueriesTest.getBrokerResponse: server over ``segments``, reduced as OFFLINE + REALTIME."""
+    from ..query.sql import parse
+    qc = parse(query) if isinstance(query, str) else query
+    block = plan_maker.make_instance_plan(qc, segments).next_block()
+    return reduce_blocks(qc, [block, block])

@@ -1,0 +1,71 @@
+"""Results blocks and execution statistics (the output contract of the hot path).
+
+  AggregationResultsBlock  pinot-core/.../operator/blocks/results/AggregationResultsBlock.java:54-155
+  GroupByResultsBlock      pinot-core/.../operator/blocks/results/GroupByResultsBlock.java:68-106
+  ExecutionStatistics      pinot-core/.../operator/ExecutionStatistics.java:42-45
+
+Intermediate results follow each function's intermediate type:
+  count -> int, sum -> float (int when every input is INT/LONG: exact), min/max ->
+  float, avg -> (sum, count), minmaxrange -> (min, max), distinctcounthll -> uint8 registers.
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+
+@dataclass
+class ExecutionStatistics:
+    num_docs_scanned: int = 0
+    num_entries_scanned_in_filter: int = 0
+    num_entries_scanned_post_filter: int = 0
+    num_total_docs: int = 0
+    num_segments_processed: int = 0
+    num_segments_matched: int = 0
+
+    def merge(self, o: "ExecutionStatistics"):
+        self.num_docs_scanned += o.num_docs_scanned
+        self.num_entries_scanned_in_filter += o.num_entries_scanned_in_filter
+        self.num_entries_scanned_post_filter += o.num_entries_scanned_post_filter
+        self.num_total_docs += o.num_total_docs
+        self.num_segments_processed += o.num_segments_processed
+        self.num_segments_matched += o.num_segments_matched
+
+
+@dataclass
+class AggregationResultsBlock:
+    aggregations: list                 # AggregationInfo per function
+    results: List[object]              # intermediate result per function
+    stats: ExecutionStatistics = field(default_factory=ExecutionStatistics)
+    device_ms: float = 0.0
+    scan_kernel_ms: float = 0.0
+
+
+@dataclass
+class GroupByResultsBlock:
+    aggregations: list
+    group_by: list                     # group-by expressions
+    groups: Dict[Tuple, List[object]]  # key values tuple -> intermediates
+    stats: ExecutionStatistics = field(default_factory=ExecutionStatistics)
+    num_groups_limit_reached: bool = False
+    device_ms: float = 0.0
+    scan_kernel_ms: float = 0.0
+
+
+def merge_intermediate(function: str, a, b):
+    """AggregationFunction.merge for the functions on the path."""
+    if function == "count":
+        return a + b
+    if function == "sum":
+        return a + b
+    if function == "min":
+        return min(a, b)
+    if function == "max":
+        return max(a, b)
+    if function == "avg":
+        return (a[0] + b[0], a[1] + b[1])
+    if function == "minmaxrange":
+        return (min(a[0], b[0]), max(a[1], b[1]))
+    if function in ("distinctcounthll", "distinctcountrawhll"):
+        return np.maximum(a, b)
+    raise NotImplementedError(function)

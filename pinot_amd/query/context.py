@@ -1,0 +1,162 @@
+"""Query context types (host side).
+
+Mirrors the shapes the reference's server consumes (all in pinot-common / pinot-core, used as
+inputs to the hot path, not rebuilt):
+  ExpressionContext      pinot-common/.../request/context/ExpressionContext.java
+  FilterContext          pinot-common/.../request/context/FilterContext.java:37-39 (AND/OR/NOT/PREDICATE/CONSTANT)
+  Predicate.Type         pinot-common/.../request/context/predicate/Predicate.java:30-42
+  RangePredicate         pinot-common/.../request/context/predicate/RangePredicate.java:38-143
+  QueryContext           pinot-core/.../query/request/context/QueryContext.java:74-757
+"""
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple, Union
+
+
+# ----------------------------------------------------------------------------- expressions
+@dataclass(frozen=True)
+class Identifier:
+    name: str
+
+    def __str__(self):
+        return self.name
+
+
+@dataclass(frozen=True)
+class Literal:
+    value: Union[int, float, str]
+
+    def __str__(self):
+        return repr(self.value) if isinstance(self.value, str) else str(self.value)
+
+
+@dataclass(frozen=True)
+class Function:
+    name: str  # lower-case canonical name
+    args: Tuple["Expression", ...]
+
+    def __str__(self):
+        return f"{self.name}({','.join(str(a) for a in self.args)})"
+
+
+Expression = Union[Identifier, Literal, Function]
+
+
+def columns_of(expr) -> List[str]:
+    if isinstance(expr, Identifier):
+        return [expr.name]
+    if isinstance(expr, Function):
+        out = []
+        for a in expr.args:
+            for c in columns_of(a):
+                if c not in out:
+                    out.append(c)
+        return out
+    return []
+
+
+# ----------------------------------------------------------------------------- predicates
+class PredicateType:
+    EQ = "EQ"
+    NOT_EQ = "NOT_EQ"
+    IN = "IN"
+    NOT_IN = "NOT_IN"
+    RANGE = "RANGE"
+
+
+UNBOUNDED = "*"  # RangePredicate.UNBOUNDED
+
+
+@dataclass(frozen=True)
+class Predicate:
+    type: str
+    lhs: Expression
+    values: Tuple = ()                 # EQ/NOT_EQ: (v,), IN/NOT_IN: (v1, ...)
+    lower: object = UNBOUNDED          # RANGE
+    upper: object = UNBOUNDED
+    lower_inclusive: bool = False
+    upper_inclusive: bool = False
+
+    @property
+    def column(self) -> str:
+        if not isinstance(self.lhs, Identifier):
+            raise NotImplementedError("predicates on expressions are out of scope")
+        return self.lhs.name
+
+
+@dataclass(frozen=True)
+class FilterContext:
+    type: str  # AND / OR / NOT / PREDICATE / CONSTANT
+    children: Tuple["FilterContext", ...] = ()
+    predicate: Optional[Predicate] = None
+    constant: Optional[bool] = None
+
+    @staticmethod
+    def AND(*children):
+        return FilterContext("AND", tuple(children))
+
+    @staticmethod
+    def OR(*children):
+        return FilterContext("OR", tuple(children))
+
+    @staticmethod
+    def NOT(child):
+        return FilterContext("NOT", (child,))
+
+    @staticmethod
+    def PRED(p: Predicate):
+        return FilterContext("PREDICATE", predicate=p)
+
+    def columns(self) -> List[str]:
+        if self.type == "PREDICATE":
+            return [self.predicate.column]
+        out = []
+        for c in self.children:
+            for x in c.columns():
+                if x not in out:
+                    out.append(x)
+        return out
+
+
+# ----------------------------------------------------------------------------- aggregations
+SUPPORTED_AGGREGATIONS = ("count", "sum", "min", "max", "avg", "minmaxrange", "distinctcounthll",
+                          "distinctcountrawhll", "distinctcount")
+
+
+@dataclass(frozen=True)
+class AggregationInfo:
+    function: str           # canonical lower-case name, e.g. "sum"
+    argument: Optional[Expression]  # None for COUNT(*)
+    log2m: int = 8
+
+    @property
+    def result_column_name(self) -> str:
+        """AggregationFunction.getResultColumnName(): lower-case function name + argument."""
+        if self.function == "count":
+            return "count(*)"
+        return f"{self.function}({self.argument})"
+
+
+@dataclass
+class OrderByExpression:
+    expression: Expression
+    ascending: bool = True
+
+
+@dataclass
+class QueryContext:
+    table: str
+    select: List[Tuple[Expression, Optional[str]]]
+    aggregations: List[AggregationInfo]
+    filter: Optional[FilterContext]
+    group_by: List[Expression]
+    order_by: List[OrderByExpression] = field(default_factory=list)
+    limit: int = 10
+    options: dict = field(default_factory=dict)
+
+    @property
+    def is_aggregation(self) -> bool:
+        return bool(self.aggregations) and not self.group_by
+
+    @property
+    def is_group_by(self) -> bool:
+        return bool(self.group_by)

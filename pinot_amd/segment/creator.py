@@ -1,0 +1,176 @@
+"""Immutable segment writer for the encodings the hot path reads.
+
+Produces, per column, the same index buffers Pinot's segment creator writes (and its loader
+maps), so the C-ABI receives exactly what ``ImmutableSegmentLoader`` would hand it:
+
+* dictionary     sorted distinct values, big-endian fixed width
+                 (SegmentDictionaryCreator; read by BaseImmutableDictionary.java:124-246;
+                 strings padded with '\\0' to the longest UTF-8 length)
+* forward index  - unsorted dict column: bit-packed dict ids, MSB-first big-endian,
+                   ceil(N*b/8) bytes, b = getNumBitsPerValue(card-1)
+                   (FixedBitSVForwardIndexWriter.java:39-50, PinotDataBitSet.java:61-72,
+                   SegmentColumnarIndexCreator.java:589)
+                 - sorted dict column: card x (startDocId, endDocId) BE int32, inclusive
+                   (SortedIndexReaderImpl.java:114-116)
+                 - raw (no-dictionary) fixed-width column: chunk format v2/v3 PASS_THROUGH
+                   (BaseChunkForwardIndexWriter.java:40-160)
+* inverted index (card+1) BE u32 absolute offsets + portable Roaring bitmaps
+                 (BitmapInvertedIndexWriter.java:35-156)
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .. import spi
+from ..spi import DataType
+from . import roaring
+
+
+@dataclass
+class ColumnMetadata:
+    name: str
+    data_type: DataType
+    total_docs: int
+    cardinality: int
+    bits_per_element: int
+    is_sorted: bool
+    has_dictionary: bool
+    has_inverted_index: bool
+    string_width: int = 0  # bytes per padded STRING dictionary entry
+
+
+@dataclass
+class ColumnIndexes:
+    metadata: ColumnMetadata
+    forward: bytes
+    dictionary: Optional[bytes] = None
+    inverted: Optional[bytes] = None
+
+
+@dataclass
+class ImmutableSegment:
+    name: str
+    num_docs: int
+    columns: Dict[str, ColumnIndexes] = field(default_factory=dict)
+
+    def column_names(self) -> List[str]:
+        return list(self.columns.keys())
+
+
+def pack_bits(dict_ids: np.ndarray, bits: int) -> bytes:
+    """MSB-first big-endian packing (FixedBitIntReaderWriter.writeInt semantics)."""
+    ids = np.asarray(dict_ids, dtype=np.uint32)
+    n = len(ids)
+    if n == 0:
+        return b""
+    be = ids.astype(">u4").view(np.uint8).reshape(n, 4)
+    allbits = np.unpackbits(be, axis=1)[:, 32 - bits:]
+    packed = np.packbits(allbits.reshape(-1))
+    nbytes = (n * bits + 7) // 8
+    assert len(packed) == nbytes
+    return packed.tobytes()
+
+
+def _encode_dictionary(sorted_vals, dt: DataType):
+    if dt == DataType.STRING:
+        enc = [s.encode("utf-8") for s in sorted_vals]
+        width = max([len(e) for e in enc] + [1])
+        buf = b"".join(e + b"\0" * (width - len(e)) for e in enc)
+        return buf, width
+    return np.asarray(sorted_vals, dtype=dt.numpy_be).tobytes(), 0
+
+
+def _sorted_unique(values: np.ndarray, dt: DataType):
+    if dt == DataType.STRING:
+        # Java String.compareTo order == code point order for BMP text
+        uniq = sorted(set(values.tolist()))
+        index = {v: i for i, v in enumerate(uniq)}
+        ids = np.fromiter((index[v] for v in values.tolist()), dtype=np.int32, count=len(values))
+        return uniq, ids
+    uniq, ids = np.unique(values, return_inverse=True)
+    return uniq, ids.astype(np.int32)
+
+
+def _chunk_forward(values: np.ndarray, dt: DataType, docs_per_chunk: int = 1000, version: int = 3) -> bytes:
+    """Fixed-byte chunk forward index, PASS_THROUGH (compression type 0)."""
+    n = len(values)
+    entry = np.dtype(dt.numpy_be).itemsize
+    num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
+    off_size = 4 if version == 2 else 8
+    header_size = 7 * 4 + num_chunks * off_size
+    header = np.array([version, num_chunks, docs_per_chunk, entry, n, 0, 7 * 4], dtype=">i4").tobytes()
+    data = np.asarray(values, dtype=dt.numpy_be).tobytes()
+    offsets = []
+    pos = header_size
+    for c in range(num_chunks):
+        offsets.append(pos)
+        pos += min(docs_per_chunk, n - c * docs_per_chunk) * entry
+    offs = np.asarray(offsets, dtype=">i4" if version == 2 else ">i8").tobytes()
+    return header + offs + data
+
+
+class SegmentCreator:
+    """Builds an ImmutableSegment from column arrays (``SegmentIndexCreationDriverImpl`` role)."""
+
+    def __init__(self, name: str, inverted_index_columns: Sequence[str] = (),
+                 no_dictionary_columns: Sequence[str] = (), run_optimize_bitmaps: bool = True):
+        self.name = name
+        self.inverted = set(inverted_index_columns)
+        self.raw = set(no_dictionary_columns)
+        self.run_optimize = run_optimize_bitmaps
+        self._cols = []
+
+    def add_column(self, name: str, data_type: DataType, values):
+        if data_type == DataType.STRING:
+            arr = np.asarray(values, dtype=np.str_)
+        else:
+            arr = np.asarray(values, dtype=data_type.numpy)
+        self._cols.append((name, data_type, arr))
+        return self
+
+    def build(self) -> ImmutableSegment:
+        if not self._cols:
+            raise ValueError("no columns")
+        n = len(self._cols[0][2])
+        seg = ImmutableSegment(self.name, n)
+        for name, dt, vals in self._cols:
+            if len(vals) != n:
+                raise ValueError(f"column {name}: {len(vals)} values, expected {n}")
+            seg.columns[name] = self._build_column(name, dt, vals, n)
+        return seg
+
+    def _build_column(self, name, dt, vals, n) -> ColumnIndexes:
+        if name in self.raw:
+            if dt == DataType.STRING:
+                raise NotImplementedError("raw STRING forward index is out of scope")
+            meta = ColumnMetadata(name, dt, n, 0, 0, False, False, False)
+            return ColumnIndexes(meta, _chunk_forward(vals, dt))
+        uniq, ids = _sorted_unique(vals, dt)
+        card = len(uniq)
+        dict_bytes, width = _encode_dictionary(uniq, dt)
+        is_sorted = bool(n == 0 or np.all(np.diff(ids) >= 0))
+        bits = spi.num_bits_per_value(card - 1)
+        if is_sorted:
+            starts = np.searchsorted(ids, np.arange(card), side="left")
+            ends = np.searchsorted(ids, np.arange(card), side="right") - 1
+            pairs = np.empty(2 * card, dtype=">i4")
+            pairs[0::2] = starts
+            pairs[1::2] = ends
+            fwd = pairs.tobytes()
+        else:
+            fwd = pack_bits(ids, bits)
+        inv = None
+        if name in self.inverted and not is_sorted:
+            order = np.argsort(ids, kind="stable")
+            bounds = np.searchsorted(ids[order], np.arange(card + 1), side="left")
+            bitmaps = [roaring.serialize(order[bounds[d]:bounds[d + 1]], self.run_optimize) for d in range(card)]
+            offsets = np.empty(card + 1, dtype=np.int64)
+            pos = (card + 1) * 4
+            for d, bm in enumerate(bitmaps):
+                offsets[d] = pos
+                pos += len(bm)
+            offsets[card] = pos
+            inv = offsets.astype(">u4").tobytes() + b"".join(bitmaps)
+        meta = ColumnMetadata(name, dt, n, card, bits, is_sorted, True, inv is not None, width)
+        return ColumnIndexes(meta, fwd, dict_bytes, inv)

@@ -1,0 +1,58 @@
+"""Data types and constants shared by the host mirror and the C-ABI.
+
+Mirrors ``FieldSpec.DataType`` (pinot-spi/src/main/java/org/apache/pinot/spi/data/FieldSpec.java)
+restricted to the single-value stored types on the hot path, and the numeric codes used by
+``include/pinot_hip.h`` (PHIP_TYPE_*).
+"""
+import enum
+
+import numpy as np
+
+
+class DataType(enum.IntEnum):
+    # values == PHIP_TYPE_* in include/pinot_hip.h
+    INT = 0
+    LONG = 1
+    FLOAT = 2
+    DOUBLE = 3
+    STRING = 4
+
+    @property
+    def numpy_be(self):
+        return {DataType.INT: ">i4", DataType.LONG: ">i8", DataType.FLOAT: ">f4",
+                DataType.DOUBLE: ">f8"}[self]
+
+    @property
+    def numpy(self):
+        return {DataType.INT: np.int32, DataType.LONG: np.int64, DataType.FLOAT: np.float32,
+                DataType.DOUBLE: np.float64, DataType.STRING: np.str_}[self]
+
+    @property
+    def is_numeric(self):
+        return self != DataType.STRING
+
+    @property
+    def is_integral(self):
+        return self in (DataType.INT, DataType.LONG)
+
+
+class FieldType(enum.Enum):
+    DIMENSION = "DIMENSION"
+    METRIC = "METRIC"
+    DATE_TIME = "DATE_TIME"
+
+
+# pinot-core/src/main/java/org/apache/pinot/core/plan/DocIdSetPlanNode.java:29
+MAX_DOC_PER_CALL = 10_000
+# pinot-core/.../plan/maker/InstancePlanMakerImplV2.java:74,78
+DEFAULT_MAX_INITIAL_RESULT_HOLDER_CAPACITY = 10_000
+DEFAULT_NUM_GROUPS_LIMIT = 100_000
+# pinot-spi/src/main/java/org/apache/pinot/spi/utils/CommonConstants.java:117
+DEFAULT_HYPERLOGLOG_LOG2M = 8
+
+
+def num_bits_per_value(max_value: int) -> int:
+    """``PinotDataBitSet.getNumBitsPerValue`` (pinot-segment-local/.../io/util/PinotDataBitSet.java:61-72)."""
+    if max_value <= 1:
+        return 1
+    return int(max_value).bit_length()
