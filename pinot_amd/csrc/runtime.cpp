@@ -982,7 +982,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     }
   }
   const size_t tasks_off = tasks.empty() ? 0 : blob.add(tasks.data(), tasks.size() * sizeof(RoaringTask));
-  const size_t nodes_off = blob.add(nodes.data(), std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
+  const size_t nodes_off = blob.reserve(std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
   const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
 
   // device buffers

@@ -303,8 +303,11 @@ class GpuCombineOperator:
         return out[:nwords]
 
     def run_raw(self):
-        keep = []
-        q = self._desc(keep)
+        # the descriptor is built once per operator and reused (plan reuse across executions)
+        if getattr(self, "_cached", None) is None:
+            keep = []
+            self._cached = (self._desc(keep), keep)
+        q = self._cached[0]
         res = ctypes.POINTER(_lib.Result)()
         _lib.check(_lib.load().phip_query(ctypes.byref(q), ctypes.byref(res)))
         return res

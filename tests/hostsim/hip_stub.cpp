@@ -1,0 +1,59 @@
+// Host-only HIP stand-in used to run libpinot_hip's host runtime (runtime.cpp) under AddressSanitizer
+// on a machine without a GPU: device memory is host memory, copies are memcpy, kernels are no-ops
+// that zero their outputs. Test tooling only -- catches host-side bugs (descriptor building,
+// staging, result assembly); device results are meaningless here.
+#include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <cstring>
+#include <cstdint>
+
+extern "C" {
+hipError_t hipGetDeviceCount(int *n) { *n = 1; return hipSuccess; }
+hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
+hipError_t hipSetDevice(int) { return hipSuccess; }
+hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) { *s = (hipStream_t)0x1; return hipSuccess; }
+hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipEventCreate(hipEvent_t *e) { *e = (hipEvent_t)0x1; return hipSuccess; }
+hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventElapsedTime(float *ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+hipError_t hipMalloc(void **p, size_t n) { *p = calloc(1, n ? n : 1); return hipSuccess; }
+hipError_t hipFree(void *p) { free(p); return hipSuccess; }
+hipError_t hipHostMalloc(void **p, size_t n, unsigned) { *p = calloc(1, n ? n : 1); return hipSuccess; }
+hipError_t hipHostFree(void *p) { free(p); return hipSuccess; }
+hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t) { memmove(d, s, n); return hipSuccess; }
+hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) { memmove(d, s, n); return hipSuccess; }
+hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t) { memset(d, v, n); return hipSuccess; }
+hipError_t hipGetLastError(void) { return hipSuccess; }
+const char *hipGetErrorString(hipError_t) { return "stub"; }
+}
+
+#include "../../pinot_amd/csrc/device.h"
+namespace phip {
+hipError_t launch_bswap32(uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_bswap64(uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }
+hipError_t launch_roaring_or(const RoaringTask *, int32_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_scan(const DevQuery &q, int nblocks, size_t, bool, hipStream_t) {
+  memset(q.partials, 0, (size_t)nblocks * (q.num_aggs + 2) * 8);
+  if (q.num_groups > 0) q.gb_count[0] = 1;  // one non-empty group
+  return hipSuccess;
+}
+hipError_t launch_finalize_partials(const uint64_t *, int, int nslots, const int32_t *, uint64_t *out, hipStream_t) {
+  memset(out, 0, nslots * 8); return hipSuccess;
+}
+hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *cc, int64_t nchunks, int64_t *offs, hipStream_t) {
+  int64_t s = 0;
+  for (int64_t c = 0; c < nchunks; c++) { offs[c] = s; int32_t k = 0; for (int64_t i = c * 1024; i < n && i < (c + 1) * 1024; i++) k += counts[i] != 0; cc[c] = k; s += k; }
+  offs[nchunks] = s; return hipSuccess;
+}
+hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *, int64_t, int64_t *keys, hipStream_t) {
+  int64_t o = 0; for (int64_t i = 0; i < n; i++) if (counts[i]) keys[o++] = i; return hipSuccess;
+}
+hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t naggs, const int32_t *, const uint64_t *, const uint64_t *,
+                               const uint32_t *, int32_t nhll, int32_t log2m, double *v, int64_t *l, uint8_t *h, hipStream_t) {
+  memset(v, 0, ng * naggs * 8); memset(l, 0, ng * naggs * 8); if (nhll) memset(h, 0, ng * nhll * (1 << log2m)); return hipSuccess;
+}
+}  // namespace phip

@@ -1,0 +1,54 @@
+"""Drives every host-side path of libpinot_hip (runtime.cpp) against the HIP stand-in under ASan."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from pinot_amd import _lib  # noqa: E402
+
+_lib.LIB_PATH = sys.argv[1]
+from pinot_amd.engine.plan import GpuInstancePlanMaker  # noqa: E402
+from pinot_amd.engine.reduce import broker_response  # noqa: E402
+from pinot_amd.engine.segment import GpuSegment  # noqa: E402
+from pinot_amd.query.sql import parse  # noqa: E402
+from pinot_amd.segment.creator import SegmentCreator  # noqa: E402
+from pinot_amd.spi import DataType  # noqa: E402
+from tests import fixtures  # noqa: E402
+
+pm = GpuInstancePlanMaker()
+segs = {n: GpuSegment(fixtures.segment_for(n)) for n in ("test_data_sv", "fast_filtered_count")}
+for case in fixtures.expected()["queries"]:
+    s = segs[case["data"]]
+    broker_response(pm, case["query"], [s, s])
+    qc = parse(case["query"])
+    pm.make_instance_plan(qc, [s]).filter_bitmap()
+for c in fixtures.expected()["docsets"]:
+    g = GpuSegment(fixtures.docset_segment(c["sets"], c["num_docs"]))
+    for p in ("s", "t"):
+        q = parse("SELECT COUNT(*) FROM t WHERE " + fixtures.docset_filter(c["op"], len(c["sets"]), p))
+        pm.make_instance_plan(q, [g]).filter_bitmap()
+    g.destroy()
+rng = np.random.default_rng(0)
+raws = []
+for k in range(3):
+    n = 5000 + k
+    c = SegmentCreator(f"s{k}", no_dictionary_columns=["r"], inverted_index_columns=["h"])
+    c.add_column("g", DataType.STRING, np.array([f"k{x}" for x in rng.integers(k, 40 + k, n)]))
+    c.add_column("h", DataType.INT, rng.integers(0, 7 + k, n))
+    c.add_column("m", DataType.LONG, rng.integers(-10 ** 12, 10 ** 12, n))
+    c.add_column("d", DataType.DOUBLE, rng.random(n))
+    c.add_column("r", DataType.LONG, rng.integers(0, 100, n))
+    raws.append(c.build())
+gs = [GpuSegment(r) for r in raws]
+for q in ("SELECT g, h, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTHLL(m) FROM t WHERE h <> 3 "
+          "GROUP BY g, h LIMIT 100000",
+          "SELECT SUM(r), AVG(d), DISTINCTCOUNTHLL(g) FROM t WHERE h IN (1, 2) OR m > 0",
+          "SELECT COUNT(*) FROM t WHERE NOT (h = 1 AND (g = 'k3' OR d < 0.5))"):
+    pm.make_instance_plan(parse(q), gs).next_block()
+for g in gs:
+    g.destroy()
+for s in segs.values():
+    s.destroy()
+print("HOSTSIM OK")
