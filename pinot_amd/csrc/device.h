@@ -7,11 +7,13 @@ namespace phip {
 
 constexpr int kMaxQueryColumns = 16;  // distinct columns one query may reference
 constexpr int kMaxAggs = 8;           // aggregation slots per query
-constexpr int kMaxFilterDepth = 6;    // AND/OR/NOT nesting (host rejects deeper trees)
+constexpr int kMaxFilterStack = 6;    // postfix evaluation stack depth (host rejects deeper programs)
 constexpr int kWave = 64;             // CDNA wavefront
 constexpr int kBlock = 256;           // 4 waves per workgroup
-constexpr int kTileGroups = 64;       // 64-doc groups per wave tile: lane g owns group g's bitmap word
-constexpr int kTileDocs = kTileGroups * 64;  // 4096 docs per tile
+constexpr int kTileGroups = 32;       // 64-doc groups per wave tile: lane g (< 32) owns group g's bitmap word
+constexpr int kTileDocs = kTileGroups * 64;  // 2048 docs per tile
+constexpr int kMaxStage = 16;         // LDS-staged sources (columns / inverted leaves) per segment
+constexpr int kStagePad = 16;         // guard bytes before and after every staged region
 constexpr int kMaxHllRegs = 1 << 12;  // log2m <= 12 on the GPU path
 
 // Accumulator kinds of one aggregation slot.
@@ -35,6 +37,17 @@ struct DevCol {
   int32_t card;
   int32_t type;      // PHIP_TYPE_*
   int32_t has_dict;  // 1: dictionary-encoded; 0: raw
+  int32_t lds_off;   // byte offset of this column's tile region in the wave's stage buffer, -1 = not staged
+  int32_t pad;
+};
+
+// One source the wave copies into its LDS stage buffer for every tile (LDS-DMA, 1 KiB per
+// wave-instruction): a fixed-bit column (256*b bytes per 2048-doc tile) or the dense doc words of an
+// inverted leaf (256 bytes per tile).
+struct StageSrc {
+  const uint8_t *base;  // tile t starts at base + t * bytes
+  int32_t bytes;        // per tile, multiple of 16
+  int32_t lds_off;      // region offset in the stage buffer
 };
 
 struct DevSeg {
@@ -42,6 +55,9 @@ struct DevSeg {
   int32_t tile_begin;  // first global tile index of this segment
   int32_t node_begin;  // filter nodes [node_begin, node_end); empty = match all
   int32_t node_end;
+  int32_t num_stage;
+  int32_t pad[3];
+  StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
 };
 
@@ -53,8 +69,8 @@ struct DevNode {
   int32_t lo, hi;
   int32_t exclusive;
   int32_t count;
-  int32_t next;         // index of the node after this subtree (preorder skip)
-  int32_t pad;
+  int32_t next;         // unused on device (programs are postfix)
+  int32_t lds_off;      // staged region of the leaf's column / inverted words, -1 = not staged
   const void *aux;      // DICT_SET: u32 bitset over dict ids; DOC_RANGES: int32 pairs;
                         // INVERTED: u64 doc bitmap words of the segment (materialised)
 };
@@ -77,6 +93,8 @@ struct DevQuery {
   int32_t total_tiles;
   int32_t num_aggs;
   int32_t num_hll;
+  int32_t stage_stride;  // bytes of one stage buffer (max over segments)
+  int32_t nbuf;          // 1 or 2 stage buffers per wave (double buffering)
   DevAgg aggs[kMaxAggs];
   // group-by
   int32_t num_group_by;

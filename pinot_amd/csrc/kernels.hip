@@ -25,6 +25,14 @@
 
 namespace phip {
 
+// Query metadata (segments, columns, filter programs) is read through the constant address space so
+// that it compiles to scalar loads (lgkmcnt): vector loads would be counted in vmcnt and every wait on
+// them would also wait for the LDS-DMA prefetch of the next tile.
+#define PHIP_CAS __attribute__((address_space(4)))
+typedef const PHIP_CAS DevSeg cseg_t;
+typedef const PHIP_CAS DevNode cnode_t;
+typedef const PHIP_CAS DevCol ccol_t;
+
 // ------------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------------
@@ -61,7 +69,7 @@ __host__ __device__ inline double f64_unordered(uint64_t u) {
   return x.d;
 }
 
-__device__ __forceinline__ int64_t dict_i64(const DevCol &c, uint32_t id) {
+__device__ __forceinline__ int64_t dict_i64(ccol_t &c, uint32_t id) {
   switch (c.type) {
     case PHIP_TYPE_INT: return ((const int32_t *)c.dict)[id];
     case PHIP_TYPE_LONG: return ((const int64_t *)c.dict)[id];
@@ -69,7 +77,7 @@ __device__ __forceinline__ int64_t dict_i64(const DevCol &c, uint32_t id) {
     default: return (int64_t)((const double *)c.dict)[id];
   }
 }
-__device__ __forceinline__ double dict_f64(const DevCol &c, uint32_t id) {
+__device__ __forceinline__ double dict_f64(ccol_t &c, uint32_t id) {
   switch (c.type) {
     case PHIP_TYPE_INT: return (double)((const int32_t *)c.dict)[id];
     case PHIP_TYPE_LONG: return (double)((const int64_t *)c.dict)[id];
@@ -77,7 +85,7 @@ __device__ __forceinline__ double dict_f64(const DevCol &c, uint32_t id) {
     default: return ((const double *)c.dict)[id];
   }
 }
-__device__ __forceinline__ int64_t raw_i64(const DevCol &c, int32_t doc) {
+__device__ __forceinline__ int64_t raw_i64(ccol_t &c, int32_t doc) {
   switch (c.type) {
     case PHIP_TYPE_INT: return ((const int32_t *)c.raw)[doc];
     case PHIP_TYPE_LONG: return ((const int64_t *)c.raw)[doc];
@@ -85,7 +93,7 @@ __device__ __forceinline__ int64_t raw_i64(const DevCol &c, int32_t doc) {
     default: return (int64_t)((const double *)c.raw)[doc];
   }
 }
-__device__ __forceinline__ double raw_f64(const DevCol &c, int32_t doc) {
+__device__ __forceinline__ double raw_f64(ccol_t &c, int32_t doc) {
   switch (c.type) {
     case PHIP_TYPE_INT: return (double)((const int32_t *)c.raw)[doc];
     case PHIP_TYPE_LONG: return (double)((const int64_t *)c.raw)[doc];
@@ -96,13 +104,53 @@ __device__ __forceinline__ double raw_f64(const DevCol &c, int32_t doc) {
 
 // Per-tile context of one wave.
 struct Tile {
-  int32_t doc0;      // first doc of the tile within the segment
-  uint32_t scanned;  // entries scanned in filter (lane 0 accumulates)
+  int32_t doc0;            // first doc of the tile within the segment
+  int32_t tile_in_seg;     // tile index within the segment
+  uint32_t scanned;        // entries scanned in filter (lane-uniform)
+  const uint8_t *stage;    // this wave's LDS stage buffer holding the tile's staged regions
 };
 
-__device__ __forceinline__ uint32_t col_dict_id(const DevCol &c, const Tile &t, uint32_t doc_in_tile) {
+typedef __attribute__((address_space(1))) const void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// Issue the LDS-DMA copies of one tile's staged regions (global_load_lds_dwordx4, 1 KiB per
+// wave-instruction, no VGPR round trip). Completion is awaited with s_waitcnt vmcnt(0).
+__device__ __forceinline__ void stage_tile(cseg_t &seg, int32_t tile_in_seg, uint8_t *buf) {
+  const int lane = lane_id();
+  for (int i = 0; i < seg.num_stage; i++) {
+    const uint8_t *sbase = seg.stage[i].base;
+    const int32_t sbytes = seg.stage[i].bytes;
+    const int32_t soff = seg.stage[i].lds_off;
+    const uint8_t *g = sbase + (int64_t)tile_in_seg * sbytes;
+    uint8_t *l = buf + soff;
+    for (int c = 0; c < sbytes; c += 1024) {
+      if (c + lane * 16 < sbytes)
+        __builtin_amdgcn_global_load_lds((gvoid_t *)(g + c + lane * 16), (lvoid_t *)(l + c), 16, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void wait_stage() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Window of 32 stream bits starting at bit p of a staged region (u32 words, bit 31 first).
+// q = floor((p-1)/32) may be -1 (reads the guard word before the region); s in [0, 31].
+__device__ __forceinline__ uint32_t window_at(const uint32_t *w, int32_t p) {
+  const int32_t q = (p - 1) >> 5;
+  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
+  return __builtin_amdgcn_alignbit(w[q], w[q + 1], s);
+}
+
+__device__ __forceinline__ uint32_t col_dict_id_global(ccol_t &c, const Tile &t, uint32_t dit) {
   const uint32_t *w = c.words + (uint64_t)(t.doc0 >> 5) * (uint32_t)c.bits;
-  return decode_bits(w, doc_in_tile * (uint32_t)c.bits, (uint32_t)c.bits);
+  return decode_bits(w, dit * (uint32_t)c.bits, (uint32_t)c.bits);
+}
+
+__device__ __forceinline__ uint32_t col_dict_id(ccol_t &c, const Tile &t, uint32_t dit) {
+  if (c.lds_off >= 0) {
+    const uint32_t *w = (const uint32_t *)(t.stage + c.lds_off);
+    return window_at(w, (int32_t)(dit * (uint32_t)c.bits)) >> (32 - c.bits);
+  }
+  return col_dict_id_global(c, t, dit);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -113,8 +161,8 @@ __device__ __forceinline__ uint64_t span_mask(int lo, int hi) {  // bits lo..hi 
   return upto & ~((1ull << lo) - 1);
 }
 
-__device__ __noinline__ uint64_t eval_leaf(const DevSeg *__restrict__ seg, const DevNode *__restrict__ n,
-                                           uint64_t care, Tile *t) {
+__device__ __forceinline__ uint64_t eval_leaf(cseg_t *__restrict__ seg, cnode_t *__restrict__ n,
+                                              uint64_t care, Tile *t) {
   const int lane = lane_id();
   const int kind = n->leaf_kind;
   if (kind == PHIP_LEAF_MATCH_ALL) return care;
@@ -123,8 +171,7 @@ __device__ __noinline__ uint64_t eval_leaf(const DevSeg *__restrict__ seg, const
     const int32_t *r = (const int32_t *)n->aux;
     const int32_t cnt = n->count;
     const int32_t tile_end = t->doc0 + kTileDocs - 1;
-    // first range that may intersect the tile (ranges sorted & disjoint)
-    int a = 0, b = cnt;
+    int a = 0, b = cnt;  // first range that may intersect the tile (ranges sorted & disjoint)
     while (a < b) {
       int mid = (a + b) >> 1;
       if (r[2 * mid + 1] < t->doc0) a = mid + 1; else b = mid;
@@ -140,90 +187,136 @@ __device__ __noinline__ uint64_t eval_leaf(const DevSeg *__restrict__ seg, const
     return care & m;
   }
   if (kind == PHIP_LEAF_INVERTED) {
-    const uint64_t *w = (const uint64_t *)n->aux;
-    uint64_t m = care ? w[(t->doc0 >> 6) + lane] : 0ull;
+    uint64_t m;
+    if (n->lds_off >= 0) {
+      m = lane < kTileGroups ? ((const uint64_t *)(t->stage + n->lds_off))[lane] : 0ull;
+    } else {
+      const uint64_t *w = (const uint64_t *)n->aux;
+      m = care ? w[(t->doc0 >> 6) + lane] : 0ull;
+    }
     if (n->exclusive) m = ~m;
     return care & m;
   }
-  // DICT_RANGE / DICT_SET: scan the bit-packed forward index, lanes = docs.
-  const DevCol &c = seg->cols[n->column];
-  const uint32_t bits = (uint32_t)c.bits;
-  const uint32_t *__restrict__ w = c.words + (uint64_t)(t->doc0 >> 5) * bits;
-  const uint32_t lo = (uint32_t)n->lo;
-  const uint32_t span = (uint32_t)(n->hi - n->lo);
+  // DICT_RANGE / DICT_SET on the bit-packed forward index: lanes = docs, one ballot per 64-doc group.
+  ccol_t &c = seg->cols[n->column];
+  const int32_t bits = c.bits;
+  const bool is_range = kind == PHIP_LEAF_DICT_RANGE;
   const uint32_t *__restrict__ set = (const uint32_t *)n->aux;
   const bool excl = n->exclusive != 0;
-  const bool is_range = kind == PHIP_LEAF_DICT_RANGE;
-  uint64_t need = ballot(care != 0);
   uint64_t res = 0;
-  uint32_t scanned = 0;
+  t->scanned += (uint32_t)__popcll(__ballot(care != 0)) * 64u;
+  if (n->lds_off >= 0) {
+    const uint32_t *w = (const uint32_t *)(t->stage + n->lds_off);
+    // Range test on the MSB-aligned window: lo <= v < hi  <=>  (win - lo<<k) < (hi-lo)<<k, k = 32-b
+    const uint32_t LO = (uint32_t)n->lo << (32 - bits);
+    const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - bits);
+    const int32_t p0 = lane * bits;
+#pragma unroll 8
+    for (int g = 0; g < kTileGroups; g++) {
+      const uint32_t win = window_at(w + g * 2 * bits, p0);
+      bool pass;
+      if (is_range) {
+        pass = (win - LO) < SPAN;
+      } else {
+        const uint32_t v = win >> (32 - bits);
+        pass = (((set[v >> 5] >> (v & 31)) & 1u) != 0) != excl;
+      }
+      const uint64_t m = ballot(pass);
+      res = (lane == g) ? m : res;
+    }
+    return res & care;
+  }
+  // not staged (LDS budget exceeded): decode from HBM
+  const uint32_t *__restrict__ w = c.words + (uint64_t)(t->doc0 >> 5) * (uint32_t)bits;
+  const uint32_t lo = (uint32_t)n->lo;
+  const uint32_t span = (uint32_t)(n->hi - n->lo);
+  uint64_t need = ballot(care != 0);
   while (need) {
     const int g = __builtin_ctzll(need);
     need &= need - 1;
-    const uint64_t cg = readlane64(care, g);
-    const uint32_t v = decode_bits(w, (uint32_t)(g * 64 + lane) * bits, bits);
+    const uint32_t v = decode_bits(w, (uint32_t)(g * 64 + lane) * (uint32_t)bits, (uint32_t)bits);
     bool pass;
     if (is_range) {
       pass = (v - lo) < span;
     } else {
       pass = (((set[v >> 5] >> (v & 31)) & 1u) != 0) != excl;
     }
-    const uint64_t m = ballot(pass) & cg;
+    const uint64_t m = ballot(pass);
     if (lane == g) res = m;
-    scanned += __popcll(cg);
   }
-  t->scanned += scanned;
-  return res;
+  return res & care;
 }
 
-template <int D>
-__device__ uint64_t eval_node(const DevSeg *__restrict__ seg, const DevNode *__restrict__ nodes, int idx,
-                              uint64_t care, Tile *t) {
-  const DevNode *n = nodes + idx;
-  const int op = n->op;
-  if (op == PHIP_NODE_LEAF) return eval_leaf(seg, n, care, t);
-  if constexpr (D >= kMaxFilterDepth) {
-    return 0;  // host rejects deeper trees
-  } else {
-    if (op == PHIP_NODE_NOT) {
-      uint64_t r = eval_node<D + 1>(seg, nodes, idx + 1, care, t);
-      return care & ~r;
-    }
-    const int nc = n->num_children;
-    int c = idx + 1;
-    if (op == PHIP_NODE_AND) {
-      uint64_t acc = care;
-      for (int k = 0; k < nc; k++) {
-        if (ballot(acc != 0) == 0) break;
-        acc = eval_node<D + 1>(seg, nodes, c, acc, t);
-        c = nodes[c].next;
+// Filter program: the segment's tree in postfix order (runtime.cpp converts the preorder ABI tree),
+// evaluated once per tile over per-lane group words with a small uniform-indexed register stack.
+// Leaves see every valid doc of the tile; AND/OR/NOT combine 64-doc words (AndDocIdSet / OrDocIdSet /
+// NotDocIdSet semantics: NOT complements within [0, numDocs)).
+#define PHIP_PUSH(v)                  \
+  do {                                \
+    const uint64_t _v = (v);          \
+    switch (sp) {                     \
+      case 0: s0 = _v; break;         \
+      case 1: s1 = _v; break;         \
+      case 2: s2 = _v; break;         \
+      case 3: s3 = _v; break;         \
+      case 4: s4 = _v; break;         \
+      default: s5 = _v; break;        \
+    }                                 \
+    sp++;                             \
+  } while (0)
+#define PHIP_POP(dst)                 \
+  do {                                \
+    sp--;                             \
+    switch (sp) {                     \
+      case 0: dst = s0; break;        \
+      case 1: dst = s1; break;        \
+      case 2: dst = s2; break;        \
+      case 3: dst = s3; break;        \
+      case 4: dst = s4; break;        \
+      default: dst = s5; break;       \
+    }                                 \
+  } while (0)
+
+__device__ __forceinline__ uint64_t eval_filter(cseg_t &seg, cnode_t *__restrict__ nodes, uint64_t valid,
+                                                Tile &t) {
+  uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
+  int sp = 0;
+  for (int i = seg.node_begin; i < seg.node_end; i++) {
+    cnode_t *n = nodes + i;
+    const int op = n->op;
+    if (op == PHIP_NODE_LEAF) {
+      PHIP_PUSH(eval_leaf(&seg, n, valid, &t));
+    } else if (op == PHIP_NODE_NOT) {
+      uint64_t v;
+      PHIP_POP(v);
+      PHIP_PUSH(valid & ~v);
+    } else {
+      uint64_t v, w;
+      PHIP_POP(v);
+      for (int k = 1; k < n->num_children; k++) {
+        PHIP_POP(w);
+        v = (op == PHIP_NODE_AND) ? (v & w) : (v | w);
       }
-      return acc;
+      PHIP_PUSH(v);
     }
-    // OR
-    uint64_t acc = 0;
-    for (int k = 0; k < nc; k++) {
-      uint64_t rem = care & ~acc;
-      if (ballot(rem != 0) == 0) break;
-      acc |= eval_node<D + 1>(seg, nodes, c, rem, t);
-      c = nodes[c].next;
-    }
-    return acc;
   }
+  uint64_t r;
+  PHIP_POP(r);
+  return r;
 }
 
 // ------------------------------------------------------------------------------------------------
 // aggregation expression values for one doc
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t col_i64(const DevCol &c, const Tile &t, uint32_t dit) {
+__device__ __forceinline__ int64_t col_i64(ccol_t &c, const Tile &t, uint32_t dit) {
   if (c.has_dict) return dict_i64(c, col_dict_id(c, t, dit));
   return raw_i64(c, t.doc0 + (int32_t)dit);
 }
-__device__ __forceinline__ double col_f64(const DevCol &c, const Tile &t, uint32_t dit) {
+__device__ __forceinline__ double col_f64(ccol_t &c, const Tile &t, uint32_t dit) {
   if (c.has_dict) return dict_f64(c, col_dict_id(c, t, dit));
   return raw_f64(c, t.doc0 + (int32_t)dit);
 }
-__device__ __forceinline__ int64_t expr_i64(const DevSeg &s, const DevAgg &a, const Tile &t, uint32_t dit) {
+__device__ __forceinline__ int64_t expr_i64(cseg_t &s, const DevAgg &a, const Tile &t, uint32_t dit) {
   int64_t x = col_i64(s.cols[a.col_a], t, dit);
   if (a.expr == PHIP_EXPR_COLUMN) return x;
   int64_t y = col_i64(s.cols[a.col_b], t, dit);
@@ -231,7 +324,7 @@ __device__ __forceinline__ int64_t expr_i64(const DevSeg &s, const DevAgg &a, co
   if (a.expr == PHIP_EXPR_SUB) return x - y;
   return x * y;
 }
-__device__ __forceinline__ double expr_f64(const DevSeg &s, const DevAgg &a, const Tile &t, uint32_t dit) {
+__device__ __forceinline__ double expr_f64(cseg_t &s, const DevAgg &a, const Tile &t, uint32_t dit) {
   double x = col_f64(s.cols[a.col_a], t, dit);
   if (a.expr == PHIP_EXPR_COLUMN) return x;
   double y = col_f64(s.cols[a.col_b], t, dit);
@@ -266,134 +359,172 @@ __device__ __forceinline__ uint64_t acc_init(int kind) {
 
 // ------------------------------------------------------------------------------------------------
 // fused filter + aggregate / group-by kernel
+//   per wave: tiles of 2048 docs, grid-stride; every tile's staged regions (filter columns, value
+//   columns, inverted-leaf words) arrive by LDS-DMA, double-buffered: tile i+stride is in flight while
+//   tile i is evaluated from LDS.
+// LDS: [HLL registers (aggregation-only)] [wave partials] [4 waves x nbuf x stage_stride]
 // ------------------------------------------------------------------------------------------------
-template <bool kGroupBy>
+template <int NA, bool kGroupBy>
 __global__ __launch_bounds__(kBlock) void scan_kernel(DevQuery q) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
-  const int wave = threadIdx.x >> 6;
+  // wave-uniform by construction; readfirstlane tells the compiler, so every value derived from the
+  // tile index (segment, offsets, metadata addresses) lives in SGPRs and metadata loads are scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int waves_total = gridDim.x * (kBlock / 64);
   const int gwave = blockIdx.x * (kBlock / 64) + wave;
+  const int nslots = q.num_aggs + 2;
 
-  // LDS: HLL registers of this block (aggregation-only), then wave partials.
   uint32_t *hll_lds = (uint32_t *)smem;
   int hll_words = 0;
   if (!kGroupBy && q.num_hll > 0) {
     hll_words = q.num_hll << q.aggs[0].log2m;  // all HLL aggs share log2m (host enforces)
     for (int i = threadIdx.x; i < hll_words; i += kBlock) hll_lds[i] = 0;
   }
+  const int part_off = (hll_words * 4 + 15) & ~15;
+  uint64_t *wave_part = (uint64_t *)(smem + part_off);
+  uint8_t *stage_base = smem + part_off + ((kBlock / 64) * nslots * 8 + 15 & ~15) +
+                        (size_t)wave * q.nbuf * q.stage_stride;
   __syncthreads();
 
-  uint64_t acc[kMaxAggs];
+  uint64_t acc[NA];
 #pragma unroll
-  for (int a = 0; a < kMaxAggs; a++) acc[a] = (a < q.num_aggs) ? acc_init(q.aggs[a].acc) : 0;
+  for (int a = 0; a < NA; a++) acc[a] = (a < q.num_aggs) ? acc_init(q.aggs[a].acc) : 0;
   uint64_t matched = 0;
   uint32_t scanned = 0;
 
-  for (int tile = gwave; tile < q.total_tiles; tile += waves_total) {
-    // segment of this tile (uniform binary search over tile_begin)
+  cseg_t *segs = (cseg_t *)q.segs;
+  cnode_t *nodes = (cnode_t *)q.nodes;
+  auto seg_of = [&](int tile) {
     int lo = 0, hi = q.num_segs - 1;
     while (lo < hi) {
       int mid = (lo + hi + 1) >> 1;
-      if (q.segs[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
+      if (segs[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
     }
-    const DevSeg &seg = q.segs[lo];
+    return lo;
+  };
+
+  int cur = 0;
+  int tile = gwave;
+  if (tile < q.total_tiles) {
+    const int s0 = seg_of(tile);
+    stage_tile(segs[s0], tile - segs[s0].tile_begin, stage_base);
+  }
+  for (; tile < q.total_tiles; tile += waves_total) {
+    const int si = __builtin_amdgcn_readfirstlane(seg_of(tile));
+    cseg_t &seg = segs[si];
     Tile t;
-    t.doc0 = (tile - seg.tile_begin) * kTileDocs;
+    t.tile_in_seg = tile - seg.tile_begin;
+    t.doc0 = t.tile_in_seg * kTileDocs;
     t.scanned = 0;
+    t.stage = stage_base + cur * q.stage_stride;
+    wait_stage();  // this tile's regions have landed
+    const int next = tile + waves_total;
+    if (q.nbuf == 2 && next < q.total_tiles) {
+      const int sn = seg_of(next);
+      stage_tile(segs[sn], next - segs[sn].tile_begin, stage_base + (cur ^ 1) * q.stage_stride);
+    }
+
     // valid docs of group = lane
     const int32_t gdoc0 = t.doc0 + lane * 64;
     const int32_t rem = seg.num_docs - gdoc0;
-    uint64_t mask = rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1));
-    if (seg.node_end > seg.node_begin) mask = eval_node<0>(&seg, q.nodes, seg.node_begin, mask, &t);
+    uint64_t mask = (lane >= kTileGroups) ? 0ull : (rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1)));
+    if (seg.node_end > seg.node_begin) mask = eval_filter(seg, nodes, mask, t);
     scanned += t.scanned;
     matched += __popcll(mask);
     {
       uint64_t tm = wave_reduce_u64_add((uint64_t)__popcll(mask));
-      if (lane == 0 && tm) atomicAdd((unsigned long long *)&q.seg_matched[lo], (unsigned long long)tm);
+      if (lane == 0 && tm) atomicAdd((unsigned long long *)&q.seg_matched[si], (unsigned long long)tm);
     }
-    if (q.filter_out != nullptr && gdoc0 < seg.num_docs) q.filter_out[(t.doc0 >> 6) + lane] = mask;
+    if (q.filter_out != nullptr && lane < kTileGroups && gdoc0 < seg.num_docs)
+      q.filter_out[(t.doc0 >> 6) + lane] = mask;
 
-    if (q.num_aggs == 0 && !kGroupBy) continue;
-    uint64_t groups = ballot(mask != 0);
-    while (groups) {
-      const int g = __builtin_ctzll(groups);
-      groups &= groups - 1;
-      const uint64_t m = readlane64(mask, g);
-      if (!((m >> lane) & 1)) continue;
-      const uint32_t dit = (uint32_t)(g * 64 + lane);
-      if constexpr (kGroupBy) {
-        int64_t key = 0;
-        for (int k = 0; k < q.num_group_by; k++) {
-          const DevCol &c = seg.cols[q.gb_cols[k]];
-          uint32_t id = col_dict_id(c, t, dit);
-          int32_t gid = c.remap ? c.remap[id] : (int32_t)id;
-          key += (int64_t)gid * q.gb_stride[k];
-        }
-        atomicAdd((unsigned long long *)&q.gb_count[key], 1ull);
-#pragma unroll
-        for (int a = 0; a < kMaxAggs; a++) {
-          if (a >= q.num_aggs) break;
-          const DevAgg &ag = q.aggs[a];
-          uint64_t *slot = q.gb_table + (int64_t)a * q.num_groups + key;
-          switch (ag.acc) {
-            case ACC_COUNT: break;  // == gb_count
-            case ACC_SUM_I64:
-              atomicAdd((unsigned long long *)slot, (unsigned long long)expr_i64(seg, ag, t, dit));
-              break;
-            case ACC_SUM_F64: atomicAdd((double *)slot, expr_f64(seg, ag, t, dit)); break;
-            case ACC_MIN_F64:
-              atomicMin((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
-              break;
-            case ACC_MAX_F64:
-              atomicMax((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
-              break;
-            case ACC_HLL: {
-              const DevCol &c = seg.cols[ag.col_a];
-              uint32_t h = c.hll[col_dict_id(c, t, dit)];
-              uint32_t *regs = q.gb_hll + ((int64_t)ag.hll_slot * q.num_groups + key) * (1 << ag.log2m);
-              atomicMax(&regs[h >> 8], (uint32_t)(h & 0xff));
-              break;
+    if (q.num_aggs > 0 || kGroupBy) {
+      uint64_t groups = ballot(mask != 0);
+      while (groups) {
+        const int g = __builtin_ctzll(groups);
+        groups &= groups - 1;
+        const uint64_t m = readlane64(mask, g);
+        if ((m >> lane) & 1) {
+          const uint32_t dit = (uint32_t)(g * 64 + lane);
+          if constexpr (kGroupBy) {
+            int64_t key = 0;
+            for (int k = 0; k < q.num_group_by; k++) {
+              ccol_t &c = seg.cols[q.gb_cols[k]];
+              uint32_t id = col_dict_id(c, t, dit);
+              int32_t gid = c.remap ? c.remap[id] : (int32_t)id;
+              key += (int64_t)gid * q.gb_stride[k];
             }
-          }
-        }
-      } else {
+            atomicAdd((unsigned long long *)&q.gb_count[key], 1ull);
 #pragma unroll
-        for (int a = 0; a < kMaxAggs; a++) {
-          if (a >= q.num_aggs) break;
-          const DevAgg &ag = q.aggs[a];
-          switch (ag.acc) {
-            case ACC_COUNT: acc[a] += 1; break;
-            case ACC_SUM_I64: acc[a] += (uint64_t)expr_i64(seg, ag, t, dit); break;
-            case ACC_SUM_F64:
-              acc[a] = (uint64_t)__double_as_longlong(__longlong_as_double((long long)acc[a]) +
-                                                      expr_f64(seg, ag, t, dit));
-              break;
-            case ACC_MIN_F64:
-              acc[a] = (uint64_t)__double_as_longlong(
-                  fmin(__longlong_as_double((long long)acc[a]), expr_f64(seg, ag, t, dit)));
-              break;
-            case ACC_MAX_F64:
-              acc[a] = (uint64_t)__double_as_longlong(
-                  fmax(__longlong_as_double((long long)acc[a]), expr_f64(seg, ag, t, dit)));
-              break;
-            case ACC_HLL: {
-              const DevCol &c = seg.cols[ag.col_a];
-              uint32_t h = c.hll[col_dict_id(c, t, dit)];
-              atomicMax(&hll_lds[(ag.hll_slot << ag.log2m) + (h >> 8)], (uint32_t)(h & 0xff));
-              break;
+            for (int a = 0; a < NA; a++) {
+              if (a >= q.num_aggs) break;
+              const DevAgg &ag = q.aggs[a];
+              uint64_t *slot = q.gb_table + (int64_t)a * q.num_groups + key;
+              switch (ag.acc) {
+                case ACC_COUNT: break;  // == gb_count
+                case ACC_SUM_I64:
+                  atomicAdd((unsigned long long *)slot, (unsigned long long)expr_i64(seg, ag, t, dit));
+                  break;
+                case ACC_SUM_F64: atomicAdd((double *)slot, expr_f64(seg, ag, t, dit)); break;
+                case ACC_MIN_F64:
+                  atomicMin((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
+                  break;
+                case ACC_MAX_F64:
+                  atomicMax((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
+                  break;
+                case ACC_HLL: {
+                  ccol_t &c = seg.cols[ag.col_a];
+                  uint32_t h = c.hll[col_dict_id(c, t, dit)];
+                  uint32_t *regs = q.gb_hll + ((int64_t)ag.hll_slot * q.num_groups + key) * (1 << ag.log2m);
+                  atomicMax(&regs[h >> 8], (uint32_t)(h & 0xff));
+                  break;
+                }
+              }
+            }
+          } else {
+#pragma unroll
+            for (int a = 0; a < NA; a++) {
+              if (a >= q.num_aggs) break;
+              const DevAgg &ag = q.aggs[a];
+              switch (ag.acc) {
+                case ACC_COUNT: acc[a] += 1; break;
+                case ACC_SUM_I64: acc[a] += (uint64_t)expr_i64(seg, ag, t, dit); break;
+                case ACC_SUM_F64:
+                  acc[a] = (uint64_t)__double_as_longlong(__longlong_as_double((long long)acc[a]) +
+                                                          expr_f64(seg, ag, t, dit));
+                  break;
+                case ACC_MIN_F64:
+                  acc[a] = (uint64_t)__double_as_longlong(
+                      fmin(__longlong_as_double((long long)acc[a]), expr_f64(seg, ag, t, dit)));
+                  break;
+                case ACC_MAX_F64:
+                  acc[a] = (uint64_t)__double_as_longlong(
+                      fmax(__longlong_as_double((long long)acc[a]), expr_f64(seg, ag, t, dit)));
+                  break;
+                case ACC_HLL: {
+                  ccol_t &c = seg.cols[ag.col_a];
+                  uint32_t h = c.hll[col_dict_id(c, t, dit)];
+                  atomicMax(&hll_lds[(ag.hll_slot << ag.log2m) + (h >> 8)], (uint32_t)(h & 0xff));
+                  break;
+                }
+              }
             }
           }
         }
       }
     }
+    if (q.nbuf == 1 && next < q.total_tiles) {
+      const int sn = seg_of(next);
+      stage_tile(segs[sn], next - segs[sn].tile_begin, stage_base);
+    }
+    cur ^= (q.nbuf == 2) ? 1 : 0;
   }
+  wait_stage();
 
-  // ---- block reduction of the aggregation-only partials -------------------------------------
-  const int nslots = q.num_aggs + 2;
-  uint64_t *wave_part = (uint64_t *)(smem + ((hll_words * 4 + 15) & ~15));
+  // ---- block reduction of the partials ---------------------------------------------------------
 #pragma unroll
-  for (int a = 0; a < kMaxAggs; a++) {
+  for (int a = 0; a < NA; a++) {
     if (a >= q.num_aggs) break;
     const int kind = q.aggs[a].acc;
     uint64_t v;
@@ -406,10 +537,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DevQuery q) {
   }
   {
     uint64_t m = wave_reduce_u64_add(matched);
-    uint64_t s = wave_reduce_u64_add((uint64_t)scanned);
     if (lane == 0) {
       wave_part[wave * nslots + q.num_aggs] = m;
-      wave_part[wave * nslots + q.num_aggs + 1] = s;
+      wave_part[wave * nslots + q.num_aggs + 1] = scanned;
     }
   }
   __syncthreads();
@@ -438,14 +568,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DevQuery q) {
   }
 }
 
-// Deterministic reduction of per-block partials (fixed order) -> out[nslots].
+// Deterministic reduction of per-block partials -> out[nslots]: one wave per slot, lane-strided over
+// blocks in a fixed order, then a fixed shuffle tree (bitwise reproducible run to run).
 __global__ void finalize_partials_kernel(const uint64_t *__restrict__ partials, int nblocks, int nslots,
                                          const int32_t *__restrict__ kinds, uint64_t *__restrict__ out) {
-  const int a = threadIdx.x;
+  const int a = blockIdx.x;
+  const int lane = threadIdx.x;
   if (a >= nslots) return;
   const int kind = kinds[a];
-  uint64_t v = partials[a];
-  for (int b = 1; b < nblocks; b++) {
+  const bool fp = kind == ACC_SUM_F64 || kind == ACC_MIN_F64 || kind == ACC_MAX_F64;
+  uint64_t v = fp ? acc_init(kind) : 0;
+  for (int b = lane; b < nblocks; b += 64) {
     uint64_t x = partials[(int64_t)b * nslots + a];
     if (kind == ACC_SUM_F64) {
       v = (uint64_t)__double_as_longlong(__longlong_as_double((long long)v) + __longlong_as_double((long long)x));
@@ -457,7 +590,12 @@ __global__ void finalize_partials_kernel(const uint64_t *__restrict__ partials, 
       v += x;
     }
   }
-  out[a] = v;
+  if (fp) {
+    v = (uint64_t)__double_as_longlong(wave_reduce_f64(__longlong_as_double((long long)v), kind));
+  } else {
+    v = wave_reduce_u64_add(v);
+  }
+  if (lane == 0) out[a] = v;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -666,17 +804,39 @@ hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream
   roaring_or_kernel<<<ntasks < 8192 ? ntasks : 8192, kBlock, 0, s>>>(tasks, ntasks);
   return hipGetLastError();
 }
-hipError_t launch_scan(const DevQuery &q, int nblocks, size_t lds_bytes, bool group_by, hipStream_t s) {
+template <int NA>
+static void launch_scan_na(const DevQuery &q, int nblocks, size_t lds, bool group_by, hipStream_t s) {
   if (group_by) {
-    scan_kernel<true><<<nblocks, kBlock, lds_bytes, s>>>(q);
+    scan_kernel<NA, true><<<nblocks, kBlock, lds, s>>>(q);
   } else {
-    scan_kernel<false><<<nblocks, kBlock, lds_bytes, s>>>(q);
+    scan_kernel<NA, false><<<nblocks, kBlock, lds, s>>>(q);
   }
+}
+
+hipError_t launch_scan(const DevQuery &q, int nblocks, size_t lds_bytes, bool group_by, hipStream_t s) {
+  if (lds_bytes > 65536) {
+    static bool configured = false;  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
+    if (!configured) {
+      hipFuncSetAttribute((const void *)scan_kernel<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipFuncSetAttribute((const void *)scan_kernel<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipFuncSetAttribute((const void *)scan_kernel<4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipFuncSetAttribute((const void *)scan_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipFuncSetAttribute((const void *)scan_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipFuncSetAttribute((const void *)scan_kernel<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipFuncSetAttribute((const void *)scan_kernel<4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipFuncSetAttribute((const void *)scan_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      configured = true;
+    }
+  }
+  if (q.num_aggs <= 1) launch_scan_na<1>(q, nblocks, lds_bytes, group_by, s);
+  else if (q.num_aggs <= 2) launch_scan_na<2>(q, nblocks, lds_bytes, group_by, s);
+  else if (q.num_aggs <= 4) launch_scan_na<4>(q, nblocks, lds_bytes, group_by, s);
+  else launch_scan_na<8>(q, nblocks, lds_bytes, group_by, s);
   return hipGetLastError();
 }
 hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
                                     uint64_t *out, hipStream_t s) {
-  finalize_partials_kernel<<<1, 64, 0, s>>>(partials, nblocks, nslots, kinds, out);
+  finalize_partials_kernel<<<nslots, 64, 0, s>>>(partials, nblocks, nslots, kinds, out);
   return hipGetLastError();
 }
 hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_counts, int64_t nchunks,

@@ -196,6 +196,7 @@ struct Workspace {
 
 struct Device {
   int ordinal = 0;
+  int num_cus = 256;
   hipStream_t stream = nullptr;
   hipEvent_t ev[4] = {};
   std::mutex mu;
@@ -256,6 +257,7 @@ static int32_t ensure_devices_locked() {
   auto d = std::make_unique<Device>();
   d->ordinal = cur;
   HIP_TRY(hipSetDevice(cur));
+  HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, cur));
   HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
   g_devices.push_back(std::move(d));
@@ -502,7 +504,7 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
     err = "filter tree truncated";
     return -1;
   }
-  if (depth > kMaxFilterDepth) {
+  if (depth > 64) {
     err = "filter tree deeper than supported";
     return -1;
   }
@@ -863,6 +865,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       dc.card = cs.card;
       dc.type = cs.type;
       dc.has_dict = cs.fwd_kind != PHIP_FWD_RAW_CHUNK;
+      dc.lds_off = -1;
     }
     for (int a = 0; a < naggs; a++) {
       if (dq.aggs[a].acc != ACC_HLL) continue;
@@ -883,7 +886,34 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       int after = validate_tree(q->filter_nodes, nb, ne, nb, 0, ncols, next, err);
       if (after < 0) return fail(PHIP_ERR_INVALID, "segment %d filter: %s", s, err.c_str());
       if (after != ne) return fail(PHIP_ERR_INVALID, "segment %d filter: trailing nodes", s);
-      for (int i = nb; i < ne; i++) {
+      // postfix order for the device (kernels.hip: eval_filter), checking the stack depth
+      std::vector<int> order;
+      {
+        std::vector<std::pair<int, int>> st{{nb, 0}};  // (node, children emitted)
+        while (!st.empty()) {
+          auto &top = st.back();
+          const phip_filter_node &fn = q->filter_nodes[top.first];
+          const int nkids = fn.op == PHIP_NODE_LEAF ? 0 : (fn.op == PHIP_NODE_NOT ? 1 : fn.num_children);
+          if (top.second < nkids) {
+            int c = top.first + 1;
+            for (int k = 0; k < top.second; k++) c = next[c - nb];
+            top.second++;
+            st.push_back({c, 0});
+          } else {
+            order.push_back(top.first);
+            st.pop_back();
+          }
+        }
+        int sp = 0, maxsp = 0;
+        for (int i : order) {
+          const phip_filter_node &fn = q->filter_nodes[i];
+          if (fn.op == PHIP_NODE_LEAF) sp++;
+          else if (fn.op != PHIP_NODE_NOT) sp -= fn.num_children - 1;
+          maxsp = std::max(maxsp, sp);
+        }
+        if (maxsp > kMaxFilterStack) return fail(PHIP_ERR_UNSUPPORTED, "segment %d filter needs stack depth %d", s, maxsp);
+      }
+      for (int i : order) {
         const phip_filter_node &fn = q->filter_nodes[i];
         DevNode dn;
         memset(&dn, 0, sizeof(dn));
@@ -896,6 +926,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
         dn.exclusive = fn.exclusive;
         dn.count = fn.count;
         dn.next = ds.node_begin + (next[i - nb] - nb);
+        dn.lds_off = -1;
         const size_t ni = nodes.size();
         if (fn.op == PHIP_NODE_LEAF) {
           ColumnStore *cs = (fn.leaf_kind >= PHIP_LEAF_DICT_RANGE && fn.leaf_kind != PHIP_LEAF_DOC_RANGES)
@@ -907,6 +938,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
               dn.lo = std::max(0, fn.lo);
               dn.hi = std::min(cs->card, fn.hi);
               if (dn.hi <= dn.lo) dn.leaf_kind = PHIP_LEAF_MATCH_NONE;
+              else if (dn.lo == 0 && dn.hi == cs->card) dn.leaf_kind = PHIP_LEAF_MATCH_ALL;
               break;
             case PHIP_LEAF_DICT_SET: {
               if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_INVALID, "dict leaf on raw column");
@@ -982,13 +1014,64 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     }
   }
   const size_t tasks_off = tasks.empty() ? 0 : blob.add(tasks.data(), tasks.size() * sizeof(RoaringTask));
+
+  // ---- LDS staging layout per segment (kernels.hip: stage_tile) --------------------------------
+  // Every wave copies, per 2048-doc tile, the fixed-bit words of the filter columns, then of the value
+  // columns, and the dense words of inverted leaves into its LDS stage buffer. Regions are padded by
+  // kStagePad bytes on both sides (window_at reads one word before / after).
+  const int64_t kStageBudget = 36 * 1024;  // bytes per wave and buffer
+  int32_t stage_stride = 0;
+  for (int s = 0; s < nseg; s++) {
+    DevSeg &ds = dsegs[s];
+    int32_t off = 0;
+    ds.num_stage = 0;
+    auto add_col = [&](int c) -> bool {
+      DevCol &dc = ds.cols[c];
+      if (!dc.has_dict || dc.words == nullptr) return false;
+      if (dc.lds_off >= 0) return true;
+      const int32_t bytes = 256 * dc.bits;
+      if (ds.num_stage >= kMaxStage || off + bytes + 2 * kStagePad > kStageBudget) return false;
+      dc.lds_off = off + kStagePad;
+      ds.stage[ds.num_stage++] = {(const uint8_t *)dc.words, bytes, dc.lds_off};
+      off += bytes + 2 * kStagePad;
+      return true;
+    };
+    for (int i = ds.node_begin; i < ds.node_end; i++) {
+      DevNode &dn = nodes[i];
+      if (dn.op != PHIP_NODE_LEAF) continue;
+      if (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || dn.leaf_kind == PHIP_LEAF_DICT_SET) {
+        if (add_col(dn.column)) dn.lds_off = ds.cols[dn.column].lds_off;
+      } else if (dn.leaf_kind == PHIP_LEAF_INVERTED && dn.aux != nullptr) {
+        if (ds.num_stage < kMaxStage && off + 256 + 2 * kStagePad <= kStageBudget) {
+          dn.lds_off = off + kStagePad;
+          ds.stage[ds.num_stage++] = {(const uint8_t *)dn.aux, 256, dn.lds_off};
+          off += 256 + 2 * kStagePad;
+        }
+      }
+    }
+    for (int a = 0; a < naggs; a++) {
+      if (dq.aggs[a].acc == ACC_COUNT) continue;
+      add_col(dq.aggs[a].col_a);
+      if (dq.aggs[a].expr != PHIP_EXPR_COLUMN) add_col(dq.aggs[a].col_b);
+    }
+    for (int k = 0; k < q->num_group_by; k++) add_col(q->group_by_columns[k]);
+    stage_stride = std::max(stage_stride, off);
+  }
+  stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
+  const size_t lds_fixed = (size_t)round_up((int64_t)(group_by ? 0 : nhll * (1 << std::max(log2m, 0)) * 4), 16) +
+                           (size_t)round_up((int64_t)(kBlock / 64) * (naggs + 2) * 8, 16);
+  int nbuf = (lds_fixed + (size_t)(kBlock / 64) * 2 * stage_stride <= 80 * 1024) ? 2 : 1;
+  const size_t lds = lds_fixed + (size_t)(kBlock / 64) * nbuf * stage_stride;
+  if (lds > 160 * 1024) return fail(PHIP_ERR_UNSUPPORTED, "query needs %zu bytes of LDS", lds);
+  dq.stage_stride = stage_stride;
+  dq.nbuf = nbuf;
   const size_t nodes_off = blob.reserve(std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
   const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
 
   // device buffers
   const int nslots = naggs + 2;
-  int dev_cus = 256;
-  int nblocks = (int)std::min<int64_t>(ceil_div(total_tiles, kBlock / 64), (int64_t)dev_cus * 8);
+  const int blocks_per_cu = std::max(1, std::min<int>(8, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
+  int nblocks = (int)std::min<int64_t>(ceil_div(total_tiles, kBlock / 64), (int64_t)dev->num_cus * blocks_per_cu);
   nblocks = std::max(nblocks, 1);
   void *dblob;
   int32_t rc = dev->ws.get("blob", blob.data.size() + 64, &dblob);
@@ -1051,8 +1134,6 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     }
     if (nhll) HIP_TRY(hipMemsetAsync(dq.gb_hll, 0, (size_t)nhll * dq.num_groups * (1 << log2m) * 4, st));
   }
-  size_t lds = (size_t)round_up((int64_t)(group_by ? 0 : nhll * (1 << std::max(log2m, 0)) * 4), 16) +
-               (size_t)(kBlock / 64) * nslots * 8;
   HIP_TRY(hipEventRecord(dev->ev[1], st));
   HIP_TRY(launch_scan(dq, nblocks, lds, group_by, st));
   HIP_TRY(hipEventRecord(dev->ev[2], st));
@@ -1198,6 +1279,7 @@ PHIP_API int32_t phip_init(const int32_t *devices, int32_t num_devices) {
     auto d = std::make_unique<Device>();
     d->ordinal = devices[i];
     HIP_TRY(hipSetDevice(d->ordinal));
+    HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, d->ordinal));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
     g_devices.push_back(std::move(d));
