@@ -10,10 +10,12 @@ constexpr int kMaxAggs = 8;           // aggregation slots per query
 constexpr int kMaxFilterStack = 6;    // postfix evaluation stack depth (host rejects deeper programs)
 constexpr int kWave = 64;             // CDNA wavefront
 constexpr int kBlock = 256;           // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kTileGroups = 32;       // 64-doc groups per wave tile: lane g (< 32) owns group g's bitmap word
 constexpr int kTileDocs = kTileGroups * 64;  // 2048 docs per tile
-constexpr int kMaxStage = 16;         // LDS-staged sources (columns / inverted leaves) per segment
+constexpr int kMaxStage = 12;         // LDS-staged filter sources (scan columns / inverted leaves) per segment
 constexpr int kStagePad = 16;         // guard bytes before and after every staged region
+constexpr int kListBytes = kTileDocs * 2;  // per-wave compacted list of matched doc offsets (u16)
 constexpr int kMaxHllRegs = 1 << 12;  // log2m <= 12 on the GPU path
 
 // Accumulator kinds of one aggregation slot.
@@ -25,6 +27,11 @@ enum AccKind : int32_t {
   ACC_MAX_F64 = 4,
   ACC_HLL = 5,      // registers, per (group, hll slot)
 };
+
+// Device filter-program opcodes (postfix; AND/OR are binary and applied incrementally, so a child
+// can be skipped once the running value decides the node: AndDocIdSet / OrDocIdSet short-circuit).
+enum DevOp : int32_t { DOP_LEAF = 0, DOP_AND = 1, DOP_OR = 2, DOP_NOT = 3 };
+enum SkipKind : int32_t { SKIP_NONE = 0, SKIP_IF_NONE = 1, SKIP_IF_ALL = 2 };
 
 // One column as seen by one segment of a query.
 struct DevCol {
@@ -42,37 +49,48 @@ struct DevCol {
 };
 
 // One source the wave copies into its LDS stage buffer for every tile (LDS-DMA, 1 KiB per
-// wave-instruction): a fixed-bit column (256*b bytes per 2048-doc tile) or the dense doc words of an
-// inverted leaf (256 bytes per tile).
+// wave-instruction): a fixed-bit filter column (256*b bytes per 2048-doc tile) or the dense doc words of
+// an inverted leaf (256 bytes per tile).
 struct StageSrc {
   const uint8_t *base;  // tile t starts at base + t * bytes
   int32_t bytes;        // per tile, multiple of 16
   int32_t lds_off;      // region offset in the stage buffer
 };
 
+// One segment with work in this query. Its tiles [tile0, tile0 + num_work) are global work items
+// [work_begin, work_begin + num_work): tiles outside the candidate doc range of a sorted-index leaf
+// under the root AND are never visited (SortedIndexBasedFilterOperator prunes them on the CPU too).
 struct DevSeg {
   int32_t num_docs;
-  int32_t tile_begin;  // first global tile index of this segment
+  int32_t work_begin;
+  int32_t tile0;
+  int32_t num_work;
   int32_t node_begin;  // filter nodes [node_begin, node_end); empty = match all
   int32_t node_end;
   int32_t num_stage;
-  int32_t pad[3];
+  int32_t seg_index;   // index into the query's segment list (seg_matched)
+  int32_t num_dma;     // LDS-DMA wave-instructions per tile (sum of ceil(stage bytes / 1 KiB))
+  int32_t pad;
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
 };
 
 struct DevNode {
-  int32_t op;           // PHIP_NODE_*
-  int32_t num_children;
-  int32_t leaf_kind;    // PHIP_LEAF_*
+  int32_t op;         // DevOp
+  int32_t leaf_kind;  // PHIP_LEAF_*
   int32_t column;
-  int32_t lo, hi;
+  int32_t lo, hi;     // DICT_RANGE [lo, hi)
   int32_t exclusive;
   int32_t count;
-  int32_t next;         // unused on device (programs are postfix)
-  int32_t lds_off;      // staged region of the leaf's column / inverted words, -1 = not staged
-  const void *aux;      // DICT_SET: u32 bitset over dict ids; DOC_RANGES: int32 pairs;
-                        // INVERTED: u64 doc bitmap words of the segment (materialised)
+  int32_t skip_to;    // first node after the enclosing child's AND/OR when the short-circuit holds
+  int32_t skip_kind;  // SkipKind
+  int32_t lds_off;    // staged region of the leaf's column / inverted words, -1 = not staged
+  int32_t bits;       // scan leaves: bits per value of the column
+  int32_t small_set;  // DICT_SET with card <= 64: membership in set_mask
+  int32_t pad;
+  uint64_t set_mask;
+  const void *aux;    // DICT_SET: u32 bitset over dict ids; DOC_RANGES: int32 pairs;
+                      // INVERTED: u64 doc bitmap words of the segment (materialised)
 };
 
 struct DevAgg {
@@ -90,11 +108,13 @@ struct DevQuery {
   const DevSeg *segs;
   const DevNode *nodes;
   int32_t num_segs;
-  int32_t total_tiles;
+  int32_t total_work;
   int32_t num_aggs;
   int32_t num_hll;
   int32_t stage_stride;  // bytes of one stage buffer (max over segments)
-  int32_t nbuf;          // 1 or 2 stage buffers per wave (double buffering)
+  int32_t nbuf;          // stage buffers per wave (2: the next tile's DMA overlaps this tile)
+  int32_t need_docs;     // 1 if any aggregation / group-by reads per-doc values (else COUNT only)
+  int32_t pad0;
   DevAgg aggs[kMaxAggs];
   // group-by
   int32_t num_group_by;
@@ -107,7 +127,7 @@ struct DevQuery {
   // aggregation-only partials
   uint64_t *partials;     // [num_blocks][num_aggs + 2] (slot num_aggs: matched docs, +1: entries scanned)
   uint32_t *hll_regs;     // [num_hll][1<<log2m] (aggregation-only)
-  uint64_t *seg_matched;  // [num_segs] matched docs per segment
+  uint64_t *seg_matched;  // [num query segments] matched docs per segment
   uint64_t *filter_out;   // optional: filter bitmap words of segment 0 (phip_filter_bitmap)
 };
 

@@ -4,20 +4,23 @@
 //   * fixed-bit dict-id forward index: u32 words, word k = BE bytes [4k, 4k+4) read as a big-endian
 //     integer, so bit 31 of word k is stream bit 32k (FixedBitIntReader's MSB-first order,
 //     pinot-segment-local/.../io/reader/impl/FixedBitIntReader.java:121-178). Doc d's id is bits
-//     [d*b, d*b+b). A 64-doc group occupies exactly 2b words, a 4096-doc tile 128b words.
+//     [d*b, d*b+b). A 64-doc group occupies exactly 2b words, a 2048-doc tile 64b words (256b bytes).
 //   * dictionaries: LE typed arrays; raw columns: LE values.
 //
-// Execution model of the fused scan kernel (K1+K2+K5..K8 of SURVEY.md §2.4):
-//   one wave = one tile of 64 groups x 64 docs. Leaves are evaluated with lanes = docs: each
-//   lane decodes its doc's dict id and tests the predicate; __ballot returns the 64-doc bitmap word
-//   of that group directly (SVScanDocIdIterator + PredicateEvaluator.applySV,
-//   pinot-core/.../dociditerators/SVScanDocIdIterator.java:75-142). The word is parked in lane g
-//   (lane g owns group g), so the boolean algebra of the filter tree (AndDocIdSet / OrDocIdSet /
-//   NotDocIdSet) is per-lane u64 arithmetic, evaluated once per tile with "care" masks: a child of
-//   an AND only decodes groups whose running AND is non-zero (the applyAnd candidate-doc semantics of
-//   ScanBasedDocIdIterator.applyAnd, SVScanDocIdIterator.java:114-142), a child of an OR only those
-//   not already true. Aggregation then revisits the groups with a non-zero final word, lanes = docs,
-//   with inactive lanes masked.
+// Execution model of the fused scan kernel (K1+K2+K5..K8 of SURVEY.md §2.4): one wave owns one
+// 2048-doc tile at a time (32 groups x 64 docs), grid-striding over a work list of tiles that the host
+// has already pruned with the sorted-index leaves.
+//   1. Filter: the tile's bytes of every scanned column arrive in LDS by LDS-DMA (double-buffered:
+//      tile i+1 is in flight while tile i is evaluated). Leaves are evaluated with lanes = docs: each
+//      lane decodes its doc's dict id and tests the predicate; the 64-lane ballot IS the group's 64-doc
+//      bitmap word (SVScanDocIdIterator + PredicateEvaluator.applySV,
+//      pinot-core/.../dociditerators/SVScanDocIdIterator.java:75-142), kept by lane g. The filter program (postfix, binary AND/OR with short-circuit skips) then combines
+//      per-lane u64 words (AndDocIdSet / OrDocIdSet / NotDocIdSet).
+//   2. Compaction: the matched docs of the tile become a u16 list in LDS (mbcnt ranks per group).
+//   3. Projection + aggregation with lanes = matched docs (late materialisation, as DataFetcher reads
+//      only the matched doc ids, pinot-core/.../common/DataFetcher.java:335-386): value / group-key
+//      columns are decoded from LDS when staged, else straight from HBM, dictionaries gathered, and the
+//      values folded into per-lane accumulators or group tables.
 #include <hip/hip_runtime.h>
 
 #include "../../include/pinot_hip.h"
@@ -26,8 +29,7 @@
 namespace phip {
 
 // Query metadata (segments, columns, filter programs) is read through the constant address space so
-// that it compiles to scalar loads (lgkmcnt): vector loads would be counted in vmcnt and every wait on
-// them would also wait for the LDS-DMA prefetch of the next tile.
+// that it compiles to scalar loads (lgkmcnt), never counted in vmcnt.
 #define PHIP_CAS __attribute__((address_space(4)))
 typedef const PHIP_CAS DevSeg cseg_t;
 typedef const PHIP_CAS DevNode cnode_t;
@@ -46,12 +48,24 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// rank of this lane among the set bits of m below it
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Bits [off, off+bits) of the MSB-first stream held in words (u32, bit 31 first).
-__device__ __forceinline__ uint32_t decode_bits(const uint32_t *__restrict__ words, uint32_t off,
-                                                uint32_t bits) {
+__device__ __forceinline__ uint32_t decode_bits(const uint32_t *__restrict__ words, uint64_t off, uint32_t bits) {
   const uint32_t *p = words + (off >> 5);
   uint64_t win = ((uint64_t)p[0] << 32) | (uint64_t)p[1];
   return (uint32_t)((win << (off & 31)) >> (64 - bits));
+}
+
+// Window of 32 stream bits starting at bit p of a staged region (u32 words, bit 31 first).
+// q = floor((p-1)/32) may be -1 (reads the guard word before the region); s in [0, 31].
+__device__ __forceinline__ uint32_t window_at(const uint32_t *w, int32_t p) {
+  const int32_t q = (p - 1) >> 5;
+  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
+  return __builtin_amdgcn_alignbit(w[q], w[q + 1], s);
 }
 
 // Order-preserving map double <-> u64 (for atomicMin/atomicMax on the group table).
@@ -68,6 +82,8 @@ __host__ __device__ inline double f64_unordered(uint64_t u) {
   x.u = u;
   return x.d;
 }
+__device__ __forceinline__ double as_f64(uint64_t u) { return __longlong_as_double((long long)u); }
+__device__ __forceinline__ uint64_t as_u64(double d) { return (uint64_t)__double_as_longlong(d); }
 
 __device__ __forceinline__ int64_t dict_i64(ccol_t &c, uint32_t id) {
   switch (c.type) {
@@ -102,212 +118,284 @@ __device__ __forceinline__ double raw_f64(ccol_t &c, int32_t doc) {
   }
 }
 
-// Per-tile context of one wave.
-struct Tile {
-  int32_t doc0;            // first doc of the tile within the segment
-  int32_t tile_in_seg;     // tile index within the segment
-  uint32_t scanned;        // entries scanned in filter (lane-uniform)
-  const uint8_t *stage;    // this wave's LDS stage buffer holding the tile's staged regions
-};
+// ------------------------------------------------------------------------------------------------
+// LDS-DMA staging. The copy is issued through inline asm so that hipcc does not see an LDS write in
+// flight: it would otherwise put s_waitcnt vmcnt(0) in front of the first ds_read of the CURRENT
+// tile and drain the prefetch of the next one. Completion is awaited by wait_vmcnt(n) below.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
 
-typedef __attribute__((address_space(1))) const void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
+__device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
 
-// Issue the LDS-DMA copies of one tile's staged regions (global_load_lds_dwordx4, 1 KiB per
-// wave-instruction, no VGPR round trip). Completion is awaited with s_waitcnt vmcnt(0).
+// Issue the LDS-DMA copies of one tile's staged regions (1 KiB per wave-instruction).
 __device__ __forceinline__ void stage_tile(cseg_t &seg, int32_t tile_in_seg, uint8_t *buf) {
   const int lane = lane_id();
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(buf));
   for (int i = 0; i < seg.num_stage; i++) {
-    const uint8_t *sbase = seg.stage[i].base;
     const int32_t sbytes = seg.stage[i].bytes;
-    const int32_t soff = seg.stage[i].lds_off;
-    const uint8_t *g = sbase + (int64_t)tile_in_seg * sbytes;
-    uint8_t *l = buf + soff;
+    const uint8_t *g = seg.stage[i].base + (int64_t)tile_in_seg * sbytes + lane * 16;
+    const uint32_t l = lbase + (uint32_t)seg.stage[i].lds_off;
     for (int c = 0; c < sbytes; c += 1024) {
-      if (c + lane * 16 < sbytes)
-        __builtin_amdgcn_global_load_lds((gvoid_t *)(g + c + lane * 16), (lvoid_t *)(l + c), 16, 0, 0);
+      if (c + lane * 16 < sbytes) dma16(g + c, l + (uint32_t)c);
     }
   }
 }
 
-__device__ __forceinline__ void wait_stage() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Window of 32 stream bits starting at bit p of a staged region (u32 words, bit 31 first).
-// q = floor((p-1)/32) may be -1 (reads the guard word before the region); s in [0, 31].
-__device__ __forceinline__ uint32_t window_at(const uint32_t *w, int32_t p) {
-  const int32_t q = (p - 1) >> 5;
-  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
-  return __builtin_amdgcn_alignbit(w[q], w[q + 1], s);
-}
-
-__device__ __forceinline__ uint32_t col_dict_id_global(ccol_t &c, const Tile &t, uint32_t dit) {
-  const uint32_t *w = c.words + (uint64_t)(t.doc0 >> 5) * (uint32_t)c.bits;
-  return decode_bits(w, dit * (uint32_t)c.bits, (uint32_t)c.bits);
-}
-
-__device__ __forceinline__ uint32_t col_dict_id(ccol_t &c, const Tile &t, uint32_t dit) {
-  if (c.lds_off >= 0) {
-    const uint32_t *w = (const uint32_t *)(t.stage + c.lds_off);
-    return window_at(w, (int32_t)(dit * (uint32_t)c.bits)) >> (32 - c.bits);
+// s_waitcnt vmcnt(n) for a wave-uniform n (vmcnt takes an immediate).
+#define PHIP_VM(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    PHIP_VM(1) PHIP_VM(2) PHIP_VM(3) PHIP_VM(4) PHIP_VM(5) PHIP_VM(6) PHIP_VM(7) PHIP_VM(8) PHIP_VM(9)
+    PHIP_VM(10) PHIP_VM(11) PHIP_VM(12) PHIP_VM(13) PHIP_VM(14) PHIP_VM(15) PHIP_VM(16) PHIP_VM(17)
+    PHIP_VM(18) PHIP_VM(19) PHIP_VM(20) PHIP_VM(21) PHIP_VM(22) PHIP_VM(23) PHIP_VM(24) PHIP_VM(25)
+    PHIP_VM(26) PHIP_VM(27) PHIP_VM(28) PHIP_VM(29) PHIP_VM(30) PHIP_VM(31) PHIP_VM(32) PHIP_VM(33)
+    PHIP_VM(34) PHIP_VM(35) PHIP_VM(36) PHIP_VM(37) PHIP_VM(38) PHIP_VM(39) PHIP_VM(40) PHIP_VM(41)
+    PHIP_VM(42) PHIP_VM(43) PHIP_VM(44) PHIP_VM(45) PHIP_VM(46) PHIP_VM(47) PHIP_VM(48) PHIP_VM(49)
+    PHIP_VM(50) PHIP_VM(51) PHIP_VM(52) PHIP_VM(53) PHIP_VM(54) PHIP_VM(55) PHIP_VM(56) PHIP_VM(57)
+    PHIP_VM(58) PHIP_VM(59) PHIP_VM(60) PHIP_VM(61) PHIP_VM(62) PHIP_VM(63)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
-  return col_dict_id_global(c, t, dit);
 }
+#undef PHIP_VM
+
+// Per-tile context of one wave.
+struct Tile {
+  int32_t doc0;          // first doc of the tile within the segment
+  int32_t valid_docs;    // docs of the tile inside the segment (1..2048)
+  const uint8_t *stage;  // this wave's LDS stage buffer holding the tile's staged regions
+};
 
 // ------------------------------------------------------------------------------------------------
-// filter leaves
+// filter leaves. A tile's doc set is held lane-major: lane l owns a 32-bit word whose bit (31-g)
+// is doc g*64 + l of the tile. Leaves decode with lanes = docs of one 64-doc group at a time and
+// shift the predicate bit into the lane's word (the group loop is ~4 VALU per 64 docs), and the
+// boolean algebra of the filter tree is one VALU op per lane on u32 words.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t span_mask(int lo, int hi) {  // bits lo..hi inclusive, 0<=lo<=hi<=63
-  uint64_t upto = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
-  return upto & ~((1ull << lo) - 1);
+// Group loop of one scan leaf: lane l decodes doc g*64 + l from the staged words (2B words per group).
+// B is runtime: a width-templated switch measured 143 VGPRs (hipcc hoists the cases' common LDS
+// reads above the switch) against 69 for one width; the runtime form costs one address add per group.
+#define PHIP_GROUP_LOOP(PASS_EXPR)                                             \
+  const int lane = lane_id();                                                  \
+  const int32_t p = lane * B;                                                  \
+  const int32_t q = (p - 1) >> 5;                                              \
+  const uint32_t s = (uint32_t)(32 * (q + 1) - p);                             \
+  const uint32_t *wl = w + q;                                                  \
+  const int32_t gstride = 2 * B;                                               \
+  uint32_t r = 0;                                                              \
+  _Pragma("unroll 8") for (int g = 0; g < kTileGroups; g++) {                  \
+    const uint32_t win = __builtin_amdgcn_alignbit(wl[0], wl[1], s);           \
+    wl += gstride;                                                             \
+    r = r + r + (uint32_t)(PASS_EXPR);                                         \
+  }                                                                            \
+  return r;
+
+// RangePredicateEvaluator on dict ids: lo <= v < hi  <=>  (win - lo<<k) < (hi-lo)<<k with k = 32-B
+// (the low k bits of the window belong to the next doc and never carry into the comparison).
+__device__ __forceinline__ uint32_t scan_range(const uint32_t *w, int B, uint32_t LO, uint32_t SPAN) {
+  PHIP_GROUP_LOOP((win - LO) < SPAN)
 }
 
-__device__ __forceinline__ uint64_t eval_leaf(cseg_t *__restrict__ seg, cnode_t *__restrict__ n,
-                                              uint64_t care, Tile *t) {
+// IN / NOT IN / EQ / NEQ on a column with card <= 64: membership in a 64-bit mask (the host
+// complements it for exclusive predicates).
+__device__ __forceinline__ uint32_t scan_small_set(const uint32_t *w, int B, uint64_t set) {
+  const uint32_t k = 32 - B;
+  PHIP_GROUP_LOOP(((set >> (win >> k)) & 1ull) != 0)
+}
+
+// IN / NOT IN on a larger dictionary: bitset over dict ids in HBM (L1/L2 resident).
+__device__ __forceinline__ uint32_t scan_big_set(const uint32_t *w, int B, const uint32_t *__restrict__ set, bool excl) {
+  const uint32_t k = 32 - B;
+  PHIP_GROUP_LOOP(((((set[(win >> k) >> 5] >> ((win >> k) & 31)) & 1u) != 0) != excl))
+}
+
+// bits [lo, hi] (inclusive, 0 <= lo <= hi <= 31) of a u32
+__device__ __forceinline__ uint32_t span32(int lo, int hi) {
+  const uint32_t upto = (hi == 31) ? ~0u : ((1u << (hi + 1)) - 1u);
+  return upto & ~((1u << lo) - 1u);
+}
+
+// Lane-major word of the doc range [s, e] (tile-relative, inclusive, clamped to the tile).
+__device__ __forceinline__ uint32_t range_word(int32_t s, int32_t e, int lane) {
+  // groups g with s <= g*64 + lane <= e
+  const int32_t g_lo = max(0, (s - lane + 63) >> 6);
+  const int32_t g_hi = min(kTileGroups - 1, (e - lane) >= 0 ? (e - lane) >> 6 : -1);
+  if (g_lo > g_hi) return 0u;
+  return span32(31 - g_hi, 31 - g_lo);
+}
+
+// One leaf over the tile; `valid` = lane-major docs of the tile inside the segment.
+__device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__ n, uint32_t valid, const Tile &t,
+                                              uint32_t &scanned) {
   const int lane = lane_id();
   const int kind = n->leaf_kind;
-  if (kind == PHIP_LEAF_MATCH_ALL) return care;
+  if (kind == PHIP_LEAF_MATCH_ALL) return valid;
   if (kind == PHIP_LEAF_MATCH_NONE) return 0;
   if (kind == PHIP_LEAF_DOC_RANGES) {
-    const int32_t *r = (const int32_t *)n->aux;
+    // SortedIndexBasedFilterOperator: inclusive doc ranges, sorted and disjoint
+    const int32_t *rg = (const int32_t *)n->aux;
     const int32_t cnt = n->count;
-    const int32_t tile_end = t->doc0 + kTileDocs - 1;
-    int a = 0, b = cnt;  // first range that may intersect the tile (ranges sorted & disjoint)
+    const int32_t tile_end = t.doc0 + kTileDocs - 1;
+    int a = 0, b = cnt;  // first range that may intersect the tile
     while (a < b) {
       int mid = (a + b) >> 1;
-      if (r[2 * mid + 1] < t->doc0) a = mid + 1; else b = mid;
+      if (rg[2 * mid + 1] < t.doc0) a = mid + 1; else b = mid;
     }
-    const int32_t d0 = t->doc0 + lane * 64;
-    uint64_t m = 0;
+    uint32_t m = 0;
     for (int i = a; i < cnt; i++) {
-      int32_t s = r[2 * i], e = r[2 * i + 1];
+      const int32_t s = rg[2 * i], e = rg[2 * i + 1];
       if (s > tile_end) break;
-      int lo = max(s, d0), hi = min(e, d0 + 63);
-      if (lo <= hi) m |= span_mask(lo - d0, hi - d0);
+      m |= range_word(max(s, t.doc0) - t.doc0, min(e, tile_end) - t.doc0, lane);
     }
-    return care & m;
+    return valid & m;
   }
   if (kind == PHIP_LEAF_INVERTED) {
-    uint64_t m;
-    if (n->lds_off >= 0) {
-      m = lane < kTileGroups ? ((const uint64_t *)(t->stage + n->lds_off))[lane] : 0ull;
-    } else {
-      const uint64_t *w = (const uint64_t *)n->aux;
-      m = care ? w[(t->doc0 >> 6) + lane] : 0ull;
-    }
-    if (n->exclusive) m = ~m;
-    return care & m;
-  }
-  // DICT_RANGE / DICT_SET on the bit-packed forward index: lanes = docs, one ballot per 64-doc group.
-  ccol_t &c = seg->cols[n->column];
-  const int32_t bits = c.bits;
-  const bool is_range = kind == PHIP_LEAF_DICT_RANGE;
-  const uint32_t *__restrict__ set = (const uint32_t *)n->aux;
-  const bool excl = n->exclusive != 0;
-  uint64_t res = 0;
-  t->scanned += (uint32_t)__popcll(__ballot(care != 0)) * 64u;
-  if (n->lds_off >= 0) {
-    const uint32_t *w = (const uint32_t *)(t->stage + n->lds_off);
-    // Range test on the MSB-aligned window: lo <= v < hi  <=>  (win - lo<<k) < (hi-lo)<<k, k = 32-b
-    const uint32_t LO = (uint32_t)n->lo << (32 - bits);
-    const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - bits);
-    const int32_t p0 = lane * bits;
+    // dense u64 doc words (bit d%64 of word d/64), transposed into the lane-major form
+    const uint64_t *w = n->lds_off >= 0 ? (const uint64_t *)(t.stage + n->lds_off)
+                                        : (const uint64_t *)n->aux + (t.doc0 >> 6);
+    uint32_t r = 0;
 #pragma unroll 8
-    for (int g = 0; g < kTileGroups; g++) {
-      const uint32_t win = window_at(w + g * 2 * bits, p0);
-      bool pass;
-      if (is_range) {
-        pass = (win - LO) < SPAN;
-      } else {
-        const uint32_t v = win >> (32 - bits);
-        pass = (((set[v >> 5] >> (v & 31)) & 1u) != 0) != excl;
-      }
-      const uint64_t m = ballot(pass);
-      res = (lane == g) ? m : res;
+    for (int g = 0; g < kTileGroups; g++) r = r + r + (uint32_t)((w[g] >> lane) & 1ull);
+    if (n->exclusive) r = ~r;
+    return valid & r;
+  }
+  // DICT_RANGE / DICT_SET on the bit-packed forward index
+  scanned += (uint32_t)t.valid_docs;
+  const int32_t B = n->bits;
+  if (n->lds_off >= 0) {
+    const uint32_t *w = (const uint32_t *)(t.stage + n->lds_off);
+    uint32_t r;
+    if (kind == PHIP_LEAF_DICT_RANGE) {
+      const uint32_t LO = (uint32_t)n->lo << (32 - B);
+      const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - B);
+      r = scan_range(w, B, LO, SPAN);
+    } else if (n->small_set) {
+      r = scan_small_set(w, B, n->set_mask);
+    } else {
+      r = scan_big_set(w, B, (const uint32_t *)n->aux, n->exclusive != 0);
     }
-    return res & care;
+    return r & valid;
   }
   // not staged (LDS budget exceeded): decode from HBM
-  const uint32_t *__restrict__ w = c.words + (uint64_t)(t->doc0 >> 5) * (uint32_t)bits;
+  ccol_t &c = seg.cols[n->column];
+  const bool is_range = kind == PHIP_LEAF_DICT_RANGE;
+  const uint32_t *__restrict__ set = (const uint32_t *)n->aux;
   const uint32_t lo = (uint32_t)n->lo;
   const uint32_t span = (uint32_t)(n->hi - n->lo);
-  uint64_t need = ballot(care != 0);
-  while (need) {
-    const int g = __builtin_ctzll(need);
-    need &= need - 1;
-    const uint32_t v = decode_bits(w, (uint32_t)(g * 64 + lane) * (uint32_t)bits, (uint32_t)bits);
+  const bool excl = n->exclusive != 0;
+  const int32_t last = t.valid_docs - 1;
+  uint32_t r = 0;
+  for (int g = 0; g < kTileGroups; g++) {
+    const int32_t dit = min(g * 64 + lane, last);
+    const uint32_t v = decode_bits(c.words, (uint64_t)(uint32_t)(t.doc0 + dit) * (uint32_t)B, (uint32_t)B);
     bool pass;
     if (is_range) {
       pass = (v - lo) < span;
+    } else if (n->small_set) {
+      pass = ((n->set_mask >> v) & 1ull) != 0;
     } else {
       pass = (((set[v >> 5] >> (v & 31)) & 1u) != 0) != excl;
     }
-    const uint64_t m = ballot(pass);
-    if (lane == g) res = m;
+    r = r + r + (uint32_t)pass;
   }
-  return res & care;
+  return r & valid;
 }
 
-// Filter program: the segment's tree in postfix order (runtime.cpp converts the preorder ABI tree),
-// evaluated once per tile over per-lane group words with a small uniform-indexed register stack.
-// Leaves see every valid doc of the tile; AND/OR/NOT combine 64-doc words (AndDocIdSet / OrDocIdSet /
-// NotDocIdSet semantics: NOT complements within [0, numDocs)).
-#define PHIP_PUSH(v)                  \
-  do {                                \
-    const uint64_t _v = (v);          \
-    switch (sp) {                     \
-      case 0: s0 = _v; break;         \
-      case 1: s1 = _v; break;         \
-      case 2: s2 = _v; break;         \
-      case 3: s3 = _v; break;         \
-      case 4: s4 = _v; break;         \
-      default: s5 = _v; break;        \
-    }                                 \
-    sp++;                             \
+// Filter program: the segment's tree in postfix order with binary AND/OR (runtime.cpp converts the
+// preorder ABI tree), evaluated once per tile over lane-major words with a small register stack.
+// The first leaf of the j-th (j >= 2) child of an AND / OR carries a skip: when the running value of
+// the node is already all-false (AND) / all-valid (OR) for the tile, the child is not evaluated.
+#define PHIP_PUSH(v)           \
+  do {                         \
+    const uint32_t _v = (v);   \
+    switch (sp) {              \
+      case 0: s0 = _v; break;  \
+      case 1: s1 = _v; break;  \
+      case 2: s2 = _v; break;  \
+      case 3: s3 = _v; break;  \
+      case 4: s4 = _v; break;  \
+      default: s5 = _v; break; \
+    }                          \
+    sp++;                      \
   } while (0)
-#define PHIP_POP(dst)                 \
-  do {                                \
-    sp--;                             \
-    switch (sp) {                     \
-      case 0: dst = s0; break;        \
-      case 1: dst = s1; break;        \
-      case 2: dst = s2; break;        \
-      case 3: dst = s3; break;        \
-      case 4: dst = s4; break;        \
-      default: dst = s5; break;       \
-    }                                 \
+#define PHIP_TOP(dst)             \
+  do {                            \
+    switch (sp - 1) {             \
+      case 0: dst = s0; break;    \
+      case 1: dst = s1; break;    \
+      case 2: dst = s2; break;    \
+      case 3: dst = s3; break;    \
+      case 4: dst = s4; break;    \
+      default: dst = s5; break;   \
+    }                             \
+  } while (0)
+#define PHIP_POP(dst) \
+  do {                \
+    PHIP_TOP(dst);    \
+    sp--;             \
   } while (0)
 
-__device__ __forceinline__ uint64_t eval_filter(cseg_t &seg, cnode_t *__restrict__ nodes, uint64_t valid,
-                                                Tile &t) {
-  uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
+__device__ __forceinline__ uint32_t eval_filter(cseg_t &seg, cnode_t *__restrict__ nodes, uint32_t valid,
+                                                const Tile &t, uint32_t &scanned) {
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
   int sp = 0;
-  for (int i = seg.node_begin; i < seg.node_end; i++) {
+  int i = seg.node_begin;
+  const int end = seg.node_end;
+  while (i < end) {
     cnode_t *n = nodes + i;
     const int op = n->op;
-    if (op == PHIP_NODE_LEAF) {
-      PHIP_PUSH(eval_leaf(&seg, n, valid, &t));
-    } else if (op == PHIP_NODE_NOT) {
-      uint64_t v;
+    if (op == DOP_LEAF) {
+      const int sk = n->skip_kind;
+      if (sk != SKIP_NONE) {
+        uint32_t top;
+        PHIP_TOP(top);
+        const bool decided = (sk == SKIP_IF_NONE) ? (ballot(top != 0) == 0) : (ballot(top != valid) == 0);
+        if (decided) {
+          i = n->skip_to;
+          continue;
+        }
+      }
+      PHIP_PUSH(eval_leaf(seg, n, valid, t, scanned));
+    } else if (op == DOP_NOT) {
+      uint32_t v;
       PHIP_POP(v);
       PHIP_PUSH(valid & ~v);
     } else {
-      uint64_t v, w;
+      uint32_t v, w;
       PHIP_POP(v);
-      for (int k = 1; k < n->num_children; k++) {
-        PHIP_POP(w);
-        v = (op == PHIP_NODE_AND) ? (v & w) : (v | w);
-      }
-      PHIP_PUSH(v);
+      PHIP_POP(w);
+      PHIP_PUSH(op == DOP_AND ? (v & w) : (v | w));
     }
+    i++;
   }
-  uint64_t r;
+  uint32_t r;
   PHIP_POP(r);
   return r;
 }
 
 // ------------------------------------------------------------------------------------------------
-// aggregation expression values for one doc
+// per-doc projection (lanes = matched docs; dit = doc offset within the tile)
 // ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t col_dict_id(ccol_t &c, const Tile &t, uint32_t dit) {
+  if (c.lds_off >= 0) {
+    const uint32_t *w = (const uint32_t *)(t.stage + c.lds_off);
+    return window_at(w, (int32_t)(dit * (uint32_t)c.bits)) >> (32 - c.bits);
+  }
+  return decode_bits(c.words, (uint64_t)(uint32_t)(t.doc0 + (int32_t)dit) * (uint32_t)c.bits, (uint32_t)c.bits);
+}
 __device__ __forceinline__ int64_t col_i64(ccol_t &c, const Tile &t, uint32_t dit) {
   if (c.has_dict) return dict_i64(c, col_dict_id(c, t, dit));
   return raw_i64(c, t.doc0 + (int32_t)dit);
@@ -341,6 +429,10 @@ __device__ __forceinline__ uint64_t wave_reduce_u64_add(uint64_t v) {
   }
   return v;
 }
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
+  return __builtin_amdgcn_readfirstlane(v);
+}
 __device__ __forceinline__ double wave_reduce_f64(double v, int kind) {
   for (int o = 32; o > 0; o >>= 1) {
     double w = __shfl_xor(v, o);
@@ -352,28 +444,112 @@ __device__ __forceinline__ double wave_reduce_f64(double v, int kind) {
 }
 
 __device__ __forceinline__ uint64_t acc_init(int kind) {
-  if (kind == ACC_MIN_F64) return (uint64_t)__double_as_longlong(__builtin_huge_val());
-  if (kind == ACC_MAX_F64) return (uint64_t)__double_as_longlong(-__builtin_huge_val());
+  if (kind == ACC_MIN_F64) return as_u64(__builtin_huge_val());
+  if (kind == ACC_MAX_F64) return as_u64(-__builtin_huge_val());
   return 0;  // counts, int sums, f64 +0.0
+}
+
+__device__ __forceinline__ uint64_t acc_combine(int kind, uint64_t a, uint64_t b) {
+  if (kind == ACC_SUM_F64) return as_u64(as_f64(a) + as_f64(b));
+  if (kind == ACC_MIN_F64) return as_u64(fmin(as_f64(a), as_f64(b)));
+  if (kind == ACC_MAX_F64) return as_u64(fmax(as_f64(a), as_f64(b)));
+  return a + b;
+}
+
+// Aggregation-only: fold one chunk of matched docs into per-lane accumulators (inactive lanes add
+// the identity; their dit = 0 is a valid doc so every load stays in bounds).
+template <int NA>
+__device__ __forceinline__ void agg_docs(const DevQuery &q, cseg_t &seg, const Tile &t, uint32_t dit, bool act,
+                                         uint64_t (&acc)[NA], uint32_t *hll_lds) {
+#pragma unroll
+  for (int a = 0; a < NA; a++) {
+    if (a >= q.num_aggs) break;
+    const DevAgg &ag = q.aggs[a];
+    switch (ag.acc) {
+      case ACC_COUNT: break;  // per tile
+      case ACC_SUM_I64: {
+        const int64_t v = expr_i64(seg, ag, t, dit);
+        acc[a] += act ? (uint64_t)v : 0ull;
+        break;
+      }
+      case ACC_SUM_F64: {
+        const double v = expr_f64(seg, ag, t, dit);
+        acc[a] = as_u64(as_f64(acc[a]) + (act ? v : 0.0));
+        break;
+      }
+      case ACC_MIN_F64: {
+        const double v = expr_f64(seg, ag, t, dit);
+        acc[a] = as_u64(fmin(as_f64(acc[a]), act ? v : __builtin_huge_val()));
+        break;
+      }
+      case ACC_MAX_F64: {
+        const double v = expr_f64(seg, ag, t, dit);
+        acc[a] = as_u64(fmax(as_f64(acc[a]), act ? v : -__builtin_huge_val()));
+        break;
+      }
+      case ACC_HLL: {
+        ccol_t &c = seg.cols[ag.col_a];
+        const uint32_t h = c.hll[col_dict_id(c, t, dit)];
+        if (act) atomicMax(&hll_lds[(ag.hll_slot << ag.log2m) + (h >> 8)], h & 0xffu);
+        break;
+      }
+    }
+  }
+}
+
+// Group-by: dense mixed-radix key over query-global dict ids (DictionaryBasedGroupKeyGenerator,
+// column 0 least significant), then global-atomic updates of the group tables.
+__device__ __forceinline__ void group_docs(const DevQuery &q, cseg_t &seg, const Tile &t, uint32_t dit, bool act) {
+  int64_t key = 0;
+  for (int k = 0; k < q.num_group_by; k++) {
+    ccol_t &c = seg.cols[q.gb_cols[k]];
+    const uint32_t id = col_dict_id(c, t, dit);
+    const int32_t gid = c.remap ? c.remap[id] : (int32_t)id;
+    key += (int64_t)gid * q.gb_stride[k];
+  }
+  if (!act) return;
+  atomicAdd((unsigned long long *)&q.gb_count[key], 1ull);
+#pragma unroll
+  for (int a = 0; a < kMaxAggs; a++) {
+    if (a >= q.num_aggs) break;
+    const DevAgg &ag = q.aggs[a];
+    uint64_t *slot = q.gb_table + (int64_t)a * q.num_groups + key;
+    switch (ag.acc) {
+      case ACC_COUNT: break;  // == gb_count
+      case ACC_SUM_I64: atomicAdd((unsigned long long *)slot, (unsigned long long)expr_i64(seg, ag, t, dit)); break;
+      case ACC_SUM_F64: atomicAdd((double *)slot, expr_f64(seg, ag, t, dit)); break;
+      case ACC_MIN_F64:
+        atomicMin((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
+        break;
+      case ACC_MAX_F64:
+        atomicMax((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
+        break;
+      case ACC_HLL: {
+        ccol_t &c = seg.cols[ag.col_a];
+        const uint32_t h = c.hll[col_dict_id(c, t, dit)];
+        uint32_t *regs = q.gb_hll + ((int64_t)ag.hll_slot * q.num_groups + key) * (1 << ag.log2m);
+        atomicMax(&regs[h >> 8], h & 0xffu);
+        break;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
 // fused filter + aggregate / group-by kernel
-//   per wave: tiles of 2048 docs, grid-stride; every tile's staged regions (filter columns, value
-//   columns, inverted-leaf words) arrive by LDS-DMA, double-buffered: tile i+stride is in flight while
-//   tile i is evaluated from LDS.
-// LDS: [HLL registers (aggregation-only)] [wave partials] [4 waves x nbuf x stage_stride]
+// LDS: [HLL registers (aggregation-only)] [wave partials] [per wave: match list | nbuf x stage]
 // ------------------------------------------------------------------------------------------------
 template <int NA, bool kGroupBy>
 __global__ __launch_bounds__(kBlock) void scan_kernel(DevQuery q) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   // wave-uniform by construction; readfirstlane tells the compiler, so every value derived from the
-  // tile index (segment, offsets, metadata addresses) lives in SGPRs and metadata loads are scalar
+  // work index (segment, offsets, metadata addresses) lives in SGPRs and metadata loads are scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int waves_total = gridDim.x * (kBlock / 64);
-  const int gwave = blockIdx.x * (kBlock / 64) + wave;
-  const int nslots = q.num_aggs + 2;
+  const int waves_total = gridDim.x * kWavesPerBlock;
+  const int gwave = blockIdx.x * kWavesPerBlock + wave;
+  const int naggs = q.num_aggs;
+  const int nslots = naggs + 2;
 
   uint32_t *hll_lds = (uint32_t *)smem;
   int hll_words = 0;
@@ -383,182 +559,143 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DevQuery q) {
   }
   const int part_off = (hll_words * 4 + 15) & ~15;
   uint64_t *wave_part = (uint64_t *)(smem + part_off);
-  uint8_t *stage_base = smem + part_off + ((kBlock / 64) * nslots * 8 + 15 & ~15) +
-                        (size_t)wave * q.nbuf * q.stage_stride;
+  uint8_t *wave_base = smem + part_off + ((kWavesPerBlock * nslots * 8 + 15) & ~15) +
+                       (size_t)wave * (kListBytes + q.nbuf * q.stage_stride);
+  uint16_t *list = (uint16_t *)wave_base;
+  uint8_t *stage_base = wave_base + kListBytes;
   __syncthreads();
 
   uint64_t acc[NA];
 #pragma unroll
-  for (int a = 0; a < NA; a++) acc[a] = (a < q.num_aggs) ? acc_init(q.aggs[a].acc) : 0;
-  uint64_t matched = 0;
+  for (int a = 0; a < NA; a++) acc[a] = (a < naggs) ? acc_init(q.aggs[a].acc) : 0;
+  uint64_t matched = 0;  // wave-uniform
   uint32_t scanned = 0;
+  uint64_t seg_acc = 0;
+  int seg_acc_idx = -1;
+  uint64_t count_acc = 0;  // COUNT slots: matched docs (wave-uniform)
 
   cseg_t *segs = (cseg_t *)q.segs;
   cnode_t *nodes = (cnode_t *)q.nodes;
-  auto seg_of = [&](int tile) {
-    int lo = 0, hi = q.num_segs - 1;
-    while (lo < hi) {
-      int mid = (lo + hi + 1) >> 1;
-      if (segs[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-  };
-
+  int si = 0, sn = 0;  // segment of the current / the prefetched work item (monotone)
   int cur = 0;
-  int tile = gwave;
-  if (tile < q.total_tiles) {
-    const int s0 = seg_of(tile);
-    stage_tile(segs[s0], tile - segs[s0].tile_begin, stage_base);
+  int work = gwave;
+  if (work < q.total_work) {
+    while (sn + 1 < q.num_segs && segs[sn + 1].work_begin <= work) sn++;
+    stage_tile(segs[sn], segs[sn].tile0 + (work - segs[sn].work_begin), stage_base);
   }
-  for (; tile < q.total_tiles; tile += waves_total) {
-    const int si = __builtin_amdgcn_readfirstlane(seg_of(tile));
+  for (; work < q.total_work; work += waves_total) {
+    while (si + 1 < q.num_segs && segs[si + 1].work_begin <= work) si++;
     cseg_t &seg = segs[si];
     Tile t;
-    t.tile_in_seg = tile - seg.tile_begin;
-    t.doc0 = t.tile_in_seg * kTileDocs;
-    t.scanned = 0;
+    const int32_t tile_in_seg = seg.tile0 + (work - seg.work_begin);
+    t.doc0 = tile_in_seg * kTileDocs;
+    t.valid_docs = min(kTileDocs, seg.num_docs - t.doc0);
     t.stage = stage_base + cur * q.stage_stride;
-    wait_stage();  // this tile's regions have landed
-    const int next = tile + waves_total;
-    if (q.nbuf == 2 && next < q.total_tiles) {
-      const int sn = seg_of(next);
-      stage_tile(segs[sn], next - segs[sn].tile_begin, stage_base + (cur ^ 1) * q.stage_stride);
+    // prefetch the next work item into the other buffer, then wait only for this tile's copies
+    const int next = work + waves_total;
+    int in_flight = 0;
+    if (q.nbuf == 2 && next < q.total_work) {
+      while (sn + 1 < q.num_segs && segs[sn + 1].work_begin <= next) sn++;
+      stage_tile(segs[sn], segs[sn].tile0 + (next - segs[sn].work_begin), stage_base + (cur ^ 1) * q.stage_stride);
+      in_flight = segs[sn].num_dma;
+    }
+    wait_vmcnt(in_flight);
+
+    if (si != seg_acc_idx) {
+      if (seg_acc_idx >= 0 && seg_acc != 0 && lane == 0)
+        atomicAdd((unsigned long long *)&q.seg_matched[segs[seg_acc_idx].seg_index], (unsigned long long)seg_acc);
+      seg_acc = 0;
+      seg_acc_idx = si;
     }
 
-    // valid docs of group = lane
-    const int32_t gdoc0 = t.doc0 + lane * 64;
-    const int32_t rem = seg.num_docs - gdoc0;
-    uint64_t mask = (lane >= kTileGroups) ? 0ull : (rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1)));
-    if (seg.node_end > seg.node_begin) mask = eval_filter(seg, nodes, mask, t);
-    scanned += t.scanned;
-    matched += __popcll(mask);
-    {
-      uint64_t tm = wave_reduce_u64_add((uint64_t)__popcll(mask));
-      if (lane == 0 && tm) atomicAdd((unsigned long long *)&q.seg_matched[si], (unsigned long long)tm);
+    // docs of the tile inside the segment, lane-major: bit (31-g) of lane l is doc g*64 + l
+    const int32_t ngrp = min(kTileGroups, max(0, (t.valid_docs - lane + 63) >> 6));
+    const uint32_t valid = ngrp == 0 ? 0u : (~0u << (32 - ngrp));
+    uint32_t mask = valid;
+    if (seg.node_end > seg.node_begin) mask = eval_filter(seg, nodes, valid, t, scanned);
+    if (q.filter_out != nullptr) {  // 64-doc bitmap words (phip_filter_bitmap)
+      uint64_t my = 0;
+      for (int g = 0; g < kTileGroups; g++) {
+        const uint64_t wg = ballot((mask >> (31 - g)) & 1u);
+        if (lane == g) my = wg;
+      }
+      if (lane < kTileGroups && lane * 64 < t.valid_docs) q.filter_out[(t.doc0 >> 6) + lane] = my;
     }
-    if (q.filter_out != nullptr && lane < kTileGroups && gdoc0 < seg.num_docs)
-      q.filter_out[(t.doc0 >> 6) + lane] = mask;
 
-    if (q.num_aggs > 0 || kGroupBy) {
-      uint64_t groups = ballot(mask != 0);
-      while (groups) {
-        const int g = __builtin_ctzll(groups);
-        groups &= groups - 1;
-        const uint64_t m = readlane64(mask, g);
-        if ((m >> lane) & 1) {
-          const uint32_t dit = (uint32_t)(g * 64 + lane);
-          if constexpr (kGroupBy) {
-            int64_t key = 0;
-            for (int k = 0; k < q.num_group_by; k++) {
-              ccol_t &c = seg.cols[q.gb_cols[k]];
-              uint32_t id = col_dict_id(c, t, dit);
-              int32_t gid = c.remap ? c.remap[id] : (int32_t)id;
-              key += (int64_t)gid * q.gb_stride[k];
-            }
-            atomicAdd((unsigned long long *)&q.gb_count[key], 1ull);
-#pragma unroll
-            for (int a = 0; a < NA; a++) {
-              if (a >= q.num_aggs) break;
-              const DevAgg &ag = q.aggs[a];
-              uint64_t *slot = q.gb_table + (int64_t)a * q.num_groups + key;
-              switch (ag.acc) {
-                case ACC_COUNT: break;  // == gb_count
-                case ACC_SUM_I64:
-                  atomicAdd((unsigned long long *)slot, (unsigned long long)expr_i64(seg, ag, t, dit));
-                  break;
-                case ACC_SUM_F64: atomicAdd((double *)slot, expr_f64(seg, ag, t, dit)); break;
-                case ACC_MIN_F64:
-                  atomicMin((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
-                  break;
-                case ACC_MAX_F64:
-                  atomicMax((unsigned long long *)slot, (unsigned long long)f64_ordered(expr_f64(seg, ag, t, dit)));
-                  break;
-                case ACC_HLL: {
-                  ccol_t &c = seg.cols[ag.col_a];
-                  uint32_t h = c.hll[col_dict_id(c, t, dit)];
-                  uint32_t *regs = q.gb_hll + ((int64_t)ag.hll_slot * q.num_groups + key) * (1 << ag.log2m);
-                  atomicMax(&regs[h >> 8], (uint32_t)(h & 0xff));
-                  break;
-                }
-              }
-            }
-          } else {
-#pragma unroll
-            for (int a = 0; a < NA; a++) {
-              if (a >= q.num_aggs) break;
-              const DevAgg &ag = q.aggs[a];
-              switch (ag.acc) {
-                case ACC_COUNT: acc[a] += 1; break;
-                case ACC_SUM_I64: acc[a] += (uint64_t)expr_i64(seg, ag, t, dit); break;
-                case ACC_SUM_F64:
-                  acc[a] = (uint64_t)__double_as_longlong(__longlong_as_double((long long)acc[a]) +
-                                                          expr_f64(seg, ag, t, dit));
-                  break;
-                case ACC_MIN_F64:
-                  acc[a] = (uint64_t)__double_as_longlong(
-                      fmin(__longlong_as_double((long long)acc[a]), expr_f64(seg, ag, t, dit)));
-                  break;
-                case ACC_MAX_F64:
-                  acc[a] = (uint64_t)__double_as_longlong(
-                      fmax(__longlong_as_double((long long)acc[a]), expr_f64(seg, ag, t, dit)));
-                  break;
-                case ACC_HLL: {
-                  ccol_t &c = seg.cols[ag.col_a];
-                  uint32_t h = c.hll[col_dict_id(c, t, dit)];
-                  atomicMax(&hll_lds[(ag.hll_slot << ag.log2m) + (h >> 8)], (uint32_t)(h & 0xff));
-                  break;
-                }
-              }
-            }
-          }
+    int nm = 0;
+    if (q.need_docs) {
+      auto do_chunk = [&](uint32_t dit, bool act) {
+        if constexpr (kGroupBy) {
+          group_docs(q, seg, t, dit, act);
+        } else {
+          agg_docs<NA>(q, seg, t, dit, act, acc, hll_lds);
+        }
+      };
+      if (ballot(mask != valid) == 0) {
+        // every doc of the tile matched: the list is the identity
+        nm = t.valid_docs;
+        for (int c = 0; c < nm; c += 64) {
+          const bool act = c + lane < nm;
+          do_chunk(act ? (uint32_t)(c + lane) : 0u, act);
+        }
+      } else {
+        // compaction of the matched docs into the wave's list (ascending doc order)
+        uint32_t any = wave_or32(mask);
+        while (any) {
+          const int bit = 31 - __builtin_clz(any);
+          any &= ~(1u << bit);
+          const bool b = (mask >> bit) & 1u;
+          const uint64_t m = ballot(b);
+          if (b) list[nm + mbcnt64(m)] = (uint16_t)((31 - bit) * 64 + lane);
+          nm += __popcll(m);
+        }
+        for (int c = 0; c < nm; c += 64) {
+          const bool act = c + lane < nm;
+          do_chunk(act ? (uint32_t)list[c + lane] : 0u, act);
         }
       }
+    } else {
+      nm = (int)wave_reduce_u64_add((uint64_t)__popc(mask));
+      nm = __builtin_amdgcn_readfirstlane(nm);
     }
-    if (q.nbuf == 1 && next < q.total_tiles) {
-      const int sn = seg_of(next);
-      stage_tile(segs[sn], next - segs[sn].tile_begin, stage_base);
-    }
+    matched += (uint64_t)nm;
+    seg_acc += (uint64_t)nm;
     cur ^= (q.nbuf == 2) ? 1 : 0;
+    if (q.nbuf == 1 && next < q.total_work) {
+      while (sn + 1 < q.num_segs && segs[sn + 1].work_begin <= next) sn++;
+      stage_tile(segs[sn], segs[sn].tile0 + (next - segs[sn].work_begin), stage_base);
+    }
   }
-  wait_stage();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (seg_acc_idx >= 0 && seg_acc != 0 && lane == 0)
+    atomicAdd((unsigned long long *)&q.seg_matched[segs[seg_acc_idx].seg_index], (unsigned long long)seg_acc);
+  count_acc = matched;
 
   // ---- block reduction of the partials ---------------------------------------------------------
 #pragma unroll
   for (int a = 0; a < NA; a++) {
-    if (a >= q.num_aggs) break;
+    if (a >= naggs) break;
     const int kind = q.aggs[a].acc;
     uint64_t v;
-    if (kind == ACC_COUNT || kind == ACC_SUM_I64 || kind == ACC_HLL) {
+    if (kind == ACC_COUNT) {
+      v = count_acc;
+    } else if (kind == ACC_SUM_I64 || kind == ACC_HLL) {
       v = wave_reduce_u64_add(acc[a]);
     } else {
-      v = (uint64_t)__double_as_longlong(wave_reduce_f64(__longlong_as_double((long long)acc[a]), kind));
+      v = as_u64(wave_reduce_f64(as_f64(acc[a]), kind));
     }
     if (lane == 0) wave_part[wave * nslots + a] = v;
   }
-  {
-    uint64_t m = wave_reduce_u64_add(matched);
-    if (lane == 0) {
-      wave_part[wave * nslots + q.num_aggs] = m;
-      wave_part[wave * nslots + q.num_aggs + 1] = scanned;
-    }
+  if (lane == 0) {
+    wave_part[wave * nslots + naggs] = matched;
+    wave_part[wave * nslots + naggs + 1] = scanned;
   }
   __syncthreads();
   if (threadIdx.x < nslots) {
     const int a = threadIdx.x;
+    const int kind = a < naggs ? q.aggs[a].acc : ACC_COUNT;
     uint64_t v = wave_part[a];
-    for (int w = 1; w < kBlock / 64; w++) {
-      uint64_t x = wave_part[w * nslots + a];
-      int kind = a < q.num_aggs ? q.aggs[a].acc : ACC_COUNT;
-      if (kind == ACC_SUM_F64) {
-        v = (uint64_t)__double_as_longlong(__longlong_as_double((long long)v) + __longlong_as_double((long long)x));
-      } else if (kind == ACC_MIN_F64) {
-        v = (uint64_t)__double_as_longlong(fmin(__longlong_as_double((long long)v), __longlong_as_double((long long)x)));
-      } else if (kind == ACC_MAX_F64) {
-        v = (uint64_t)__double_as_longlong(fmax(__longlong_as_double((long long)v), __longlong_as_double((long long)x)));
-      } else {
-        v += x;
-      }
-    }
+    for (int w = 1; w < kWavesPerBlock; w++) v = acc_combine(kind, v, wave_part[w * nslots + a]);
     q.partials[(int64_t)blockIdx.x * nslots + a] = v;
   }
   if (!kGroupBy && hll_words > 0) {
@@ -578,20 +715,9 @@ __global__ void finalize_partials_kernel(const uint64_t *__restrict__ partials, 
   const int kind = kinds[a];
   const bool fp = kind == ACC_SUM_F64 || kind == ACC_MIN_F64 || kind == ACC_MAX_F64;
   uint64_t v = fp ? acc_init(kind) : 0;
-  for (int b = lane; b < nblocks; b += 64) {
-    uint64_t x = partials[(int64_t)b * nslots + a];
-    if (kind == ACC_SUM_F64) {
-      v = (uint64_t)__double_as_longlong(__longlong_as_double((long long)v) + __longlong_as_double((long long)x));
-    } else if (kind == ACC_MIN_F64) {
-      v = (uint64_t)__double_as_longlong(fmin(__longlong_as_double((long long)v), __longlong_as_double((long long)x)));
-    } else if (kind == ACC_MAX_F64) {
-      v = (uint64_t)__double_as_longlong(fmax(__longlong_as_double((long long)v), __longlong_as_double((long long)x)));
-    } else {
-      v += x;
-    }
-  }
+  for (int b = lane; b < nblocks; b += 64) v = acc_combine(kind, v, partials[(int64_t)b * nslots + a]);
   if (fp) {
-    v = (uint64_t)__double_as_longlong(wave_reduce_f64(__longlong_as_double((long long)v), kind));
+    v = as_u64(wave_reduce_f64(as_f64(v), kind));
   } else {
     v = wave_reduce_u64_add(v);
   }
@@ -805,34 +931,30 @@ hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream
   return hipGetLastError();
 }
 template <int NA>
-static void launch_scan_na(const DevQuery &q, int nblocks, size_t lds, bool group_by, hipStream_t s) {
-  if (group_by) {
-    scan_kernel<NA, true><<<nblocks, kBlock, lds, s>>>(q);
-  } else {
-    scan_kernel<NA, false><<<nblocks, kBlock, lds, s>>>(q);
-  }
-}
-
-hipError_t launch_scan(const DevQuery &q, int nblocks, size_t lds_bytes, bool group_by, hipStream_t s) {
+static hipError_t launch_scan_na(const DevQuery &q, int nblocks, size_t lds_bytes, bool group_by, hipStream_t s) {
   if (lds_bytes > 65536) {
     static bool configured = false;  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
     if (!configured) {
-      hipFuncSetAttribute((const void *)scan_kernel<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-      hipFuncSetAttribute((const void *)scan_kernel<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-      hipFuncSetAttribute((const void *)scan_kernel<4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-      hipFuncSetAttribute((const void *)scan_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-      hipFuncSetAttribute((const void *)scan_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-      hipFuncSetAttribute((const void *)scan_kernel<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-      hipFuncSetAttribute((const void *)scan_kernel<4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-      hipFuncSetAttribute((const void *)scan_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipError_t e1 = hipFuncSetAttribute((const void *)scan_kernel<NA, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      hipError_t e2 = hipFuncSetAttribute((const void *)scan_kernel<NA, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+      if (e1 != hipSuccess) return e1;
+      if (e2 != hipSuccess) return e2;
       configured = true;
     }
   }
-  if (q.num_aggs <= 1) launch_scan_na<1>(q, nblocks, lds_bytes, group_by, s);
-  else if (q.num_aggs <= 2) launch_scan_na<2>(q, nblocks, lds_bytes, group_by, s);
-  else if (q.num_aggs <= 4) launch_scan_na<4>(q, nblocks, lds_bytes, group_by, s);
-  else launch_scan_na<8>(q, nblocks, lds_bytes, group_by, s);
+  if (group_by) {
+    scan_kernel<NA, true><<<nblocks, kBlock, lds_bytes, s>>>(q);
+  } else {
+    scan_kernel<NA, false><<<nblocks, kBlock, lds_bytes, s>>>(q);
+  }
   return hipGetLastError();
+}
+
+hipError_t launch_scan(const DevQuery &q, int nblocks, size_t lds_bytes, bool group_by, hipStream_t s) {
+  if (q.num_aggs <= 1) return launch_scan_na<1>(q, nblocks, lds_bytes, group_by, s);
+  if (q.num_aggs <= 2) return launch_scan_na<2>(q, nblocks, lds_bytes, group_by, s);
+  if (q.num_aggs <= 4) return launch_scan_na<4>(q, nblocks, lds_bytes, group_by, s);
+  return launch_scan_na<8>(q, nblocks, lds_bytes, group_by, s);
 }
 hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
                                     uint64_t *out, hipStream_t s) {

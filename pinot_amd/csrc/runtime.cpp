@@ -16,6 +16,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -830,13 +831,12 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
 
   // ---- staging blob: segments, nodes, leaf aux ------------------------------------------------
   Blob blob;
-  const size_t segs_off = blob.reserve(sizeof(DevSeg) * nseg);
   std::vector<DevNode> nodes;
   struct AuxFix {
     size_t node;
     size_t off;
   };
-  std::vector<AuxFix> aux_fix;      // node.aux = dev_base + off
+  std::vector<AuxFix> aux_fix;  // node.aux = dev_base + off
   struct InvLeaf {
     size_t node;
     int seg;
@@ -844,17 +844,17 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     const phip_filter_node *src;
   };
   std::vector<InvLeaf> inv_leaves;
-  int64_t total_tiles = 0;
+  int64_t total_work = 0;
   int64_t total_docs = 0;
-  std::vector<DevSeg> dsegs(nseg);
+  std::vector<DevSeg> dsegs;  // segments with work only
+  dsegs.reserve(nseg);
   for (int s = 0; s < nseg; s++) {
     Segment &sg = *segs[s];
-    DevSeg &ds = dsegs[s];
+    total_docs += sg.num_docs;
+    DevSeg ds;
     memset(&ds, 0, sizeof(ds));
     ds.num_docs = sg.num_docs;
-    ds.tile_begin = (int32_t)total_tiles;
-    total_tiles += ceil_div(sg.num_docs, kTileDocs);
-    total_docs += sg.num_docs;
+    ds.seg_index = s;
     for (int c = 0; c < ncols; c++) {
       ColumnStore &cs = sg.cols[colidx[s][c]];
       DevCol &dc = ds.cols[c];
@@ -876,106 +876,197 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       ds.cols[dq.aggs[a].col_a].hll = h;
     }
     for (int k = 0; k < q->num_group_by; k++) ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
-    // filter program
+    if (sg.num_docs == 0) continue;
+
+    // filter program: validate the preorder ABI tree, then emit postfix with binary AND/OR
     const int nb = q->filter_offsets ? q->filter_offsets[s] : 0;
     const int ne = q->filter_offsets ? q->filter_offsets[s + 1] : 0;
-    ds.node_begin = (int32_t)nodes.size();
+    const size_t node_begin = nodes.size();
+    ds.node_begin = (int32_t)node_begin;
+    int64_t hull_lo = 0, hull_hi = (int64_t)sg.num_docs - 1;  // candidate docs (inclusive)
     if (ne > nb) {
       std::vector<int> next(ne - nb);
       std::string err;
       int after = validate_tree(q->filter_nodes, nb, ne, nb, 0, ncols, next, err);
       if (after < 0) return fail(PHIP_ERR_INVALID, "segment %d filter: %s", s, err.c_str());
       if (after != ne) return fail(PHIP_ERR_INVALID, "segment %d filter: trailing nodes", s);
-      // postfix order for the device (kernels.hip: eval_filter), checking the stack depth
-      std::vector<int> order;
-      {
-        std::vector<std::pair<int, int>> st{{nb, 0}};  // (node, children emitted)
-        while (!st.empty()) {
-          auto &top = st.back();
-          const phip_filter_node &fn = q->filter_nodes[top.first];
-          const int nkids = fn.op == PHIP_NODE_LEAF ? 0 : (fn.op == PHIP_NODE_NOT ? 1 : fn.num_children);
-          if (top.second < nkids) {
-            int c = top.first + 1;
-            for (int k = 0; k < top.second; k++) c = next[c - nb];
-            top.second++;
-            st.push_back({c, 0});
-          } else {
-            order.push_back(top.first);
-            st.pop_back();
-          }
-        }
-        int sp = 0, maxsp = 0;
-        for (int i : order) {
-          const phip_filter_node &fn = q->filter_nodes[i];
-          if (fn.op == PHIP_NODE_LEAF) sp++;
-          else if (fn.op != PHIP_NODE_NOT) sp -= fn.num_children - 1;
-          maxsp = std::max(maxsp, sp);
-        }
-        if (maxsp > kMaxFilterStack) return fail(PHIP_ERR_UNSUPPORTED, "segment %d filter needs stack depth %d", s, maxsp);
-      }
-      for (int i : order) {
-        const phip_filter_node &fn = q->filter_nodes[i];
+      int32_t rc = PHIP_OK;
+      // leaf -> device node
+      auto make_leaf = [&](const phip_filter_node &fn) -> DevNode {
         DevNode dn;
         memset(&dn, 0, sizeof(dn));
-        dn.op = fn.op;
-        dn.num_children = fn.num_children;
+        dn.op = DOP_LEAF;
         dn.leaf_kind = fn.leaf_kind;
         dn.column = fn.column;
         dn.lo = fn.lo;
         dn.hi = fn.hi;
         dn.exclusive = fn.exclusive;
         dn.count = fn.count;
-        dn.next = ds.node_begin + (next[i - nb] - nb);
         dn.lds_off = -1;
+        dn.skip_to = -1;
         const size_t ni = nodes.size();
-        if (fn.op == PHIP_NODE_LEAF) {
-          ColumnStore *cs = (fn.leaf_kind >= PHIP_LEAF_DICT_RANGE && fn.leaf_kind != PHIP_LEAF_DOC_RANGES)
-                                ? &sg.cols[colidx[s][fn.column]]
-                                : nullptr;
-          switch (fn.leaf_kind) {
-            case PHIP_LEAF_DICT_RANGE:
-              if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_INVALID, "dict leaf on raw column");
-              dn.lo = std::max(0, fn.lo);
-              dn.hi = std::min(cs->card, fn.hi);
-              if (dn.hi <= dn.lo) dn.leaf_kind = PHIP_LEAF_MATCH_NONE;
-              else if (dn.lo == 0 && dn.hi == cs->card) dn.leaf_kind = PHIP_LEAF_MATCH_ALL;
-              break;
-            case PHIP_LEAF_DICT_SET: {
-              if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_INVALID, "dict leaf on raw column");
-              std::vector<uint32_t> bits(ceil_div(cs->card, 32) + 1, 0);
-              for (int k = 0; k < fn.count; k++) {
-                int32_t id = fn.ids[k];
-                if (id < 0 || id >= cs->card) return fail(PHIP_ERR_INVALID, "dict id %d out of range", id);
-                bits[id >> 5] |= 1u << (id & 31);
-              }
+        ColumnStore *cs = (fn.leaf_kind >= PHIP_LEAF_DICT_RANGE && fn.leaf_kind != PHIP_LEAF_DOC_RANGES)
+                              ? &sg.cols[colidx[s][fn.column]]
+                              : nullptr;
+        if (cs) dn.bits = cs->bits;
+        switch (fn.leaf_kind) {
+          case PHIP_LEAF_DICT_RANGE:
+            if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "dict leaf on raw column"); break; }
+            dn.lo = std::max(0, fn.lo);
+            dn.hi = std::min(cs->card, fn.hi);
+            if (dn.hi <= dn.lo) dn.leaf_kind = PHIP_LEAF_MATCH_NONE;
+            else if (dn.lo == 0 && dn.hi == cs->card) dn.leaf_kind = PHIP_LEAF_MATCH_ALL;
+            break;
+          case PHIP_LEAF_DICT_SET: {
+            if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "dict leaf on raw column"); break; }
+            std::vector<uint32_t> bits(ceil_div(cs->card, 32) + 1, 0);
+            int32_t n_in = 0, mn = INT32_MAX, mx = -1;
+            for (int k = 0; k < fn.count; k++) {
+              int32_t id = fn.ids[k];
+              if (id < 0 || id >= cs->card) { rc = fail(PHIP_ERR_INVALID, "dict id %d out of range", id); break; }
+              if (!((bits[id >> 5] >> (id & 31)) & 1u)) n_in++;
+              bits[id >> 5] |= 1u << (id & 31);
+              mn = std::min(mn, id);
+              mx = std::max(mx, id);
+            }
+            if (rc) break;
+            // a contiguous id set (or its complement within the dictionary) is a dict-id range
+            const bool contiguous = n_in > 0 && mx - mn + 1 == n_in;
+            if (n_in == 0) {
+              dn.leaf_kind = fn.exclusive ? PHIP_LEAF_MATCH_ALL : PHIP_LEAF_MATCH_NONE;
+            } else if (n_in == cs->card) {
+              dn.leaf_kind = fn.exclusive ? PHIP_LEAF_MATCH_NONE : PHIP_LEAF_MATCH_ALL;
+            } else if (contiguous && !fn.exclusive) {
+              dn.leaf_kind = PHIP_LEAF_DICT_RANGE;
+              dn.lo = mn;
+              dn.hi = mx + 1;
+            } else if (contiguous && fn.exclusive && (mn == 0 || mx == cs->card - 1)) {
+              dn.leaf_kind = PHIP_LEAF_DICT_RANGE;
+              dn.lo = mn == 0 ? mx + 1 : 0;
+              dn.hi = mn == 0 ? cs->card : mn;
+              dn.exclusive = 0;
+            } else if (cs->card <= 64) {
+              dn.small_set = 1;
+              dn.set_mask = (uint64_t)bits[0] | ((uint64_t)bits[1] << 32);
+              if (fn.exclusive) dn.set_mask = ~dn.set_mask;  // ids >= card never occur
+              dn.exclusive = 0;
+            } else {
               aux_fix.push_back({ni, blob.add(bits.data(), bits.size() * 4)});
-              break;
             }
-            case PHIP_LEAF_DOC_RANGES: {
-              int32_t prev = -1;
-              for (int k = 0; k < fn.count; k++) {
-                int32_t a0 = fn.ids[2 * k], a1 = fn.ids[2 * k + 1];
-                if (a0 <= prev || a1 < a0 || a1 >= sg.num_docs)
-                  return fail(PHIP_ERR_INVALID, "doc ranges must be sorted, disjoint and within numDocs");
-                prev = a1;
-              }
-              aux_fix.push_back({ni, blob.add(fn.ids, (size_t)fn.count * 8)});
-              break;
-            }
-            case PHIP_LEAF_INVERTED:
-              if (cs->inv_begin.empty()) return fail(PHIP_ERR_INVALID, "column %s has no inverted index", cs->name.c_str());
-              inv_leaves.push_back({ni, s, colidx[s][fn.column], &fn});
-              break;
-            default: break;
+            break;
           }
+          case PHIP_LEAF_DOC_RANGES: {
+            int32_t prev = -1;
+            for (int k = 0; k < fn.count; k++) {
+              int32_t a0 = fn.ids[2 * k], a1 = fn.ids[2 * k + 1];
+              if (a0 <= prev || a1 < a0 || a1 >= sg.num_docs) {
+                rc = fail(PHIP_ERR_INVALID, "doc ranges must be sorted, disjoint and within numDocs");
+                break;
+              }
+              prev = a1;
+            }
+            if (rc) break;
+            if (fn.count == 0) {
+              dn.leaf_kind = PHIP_LEAF_MATCH_NONE;
+            } else {
+              dn.lo = fn.ids[0];
+              dn.hi = fn.ids[2 * fn.count - 1];
+              aux_fix.push_back({ni, blob.add(fn.ids, (size_t)fn.count * 8)});
+            }
+            break;
+          }
+          case PHIP_LEAF_INVERTED:
+            if (cs->inv_begin.empty()) { rc = fail(PHIP_ERR_INVALID, "column %s has no inverted index", cs->name.c_str()); break; }
+            inv_leaves.push_back({ni, s, colidx[s][fn.column], &fn});
+            break;
+          default: break;
         }
-        nodes.push_back(dn);
+        return dn;
+      };
+      // recursive postfix emission (depth bounded by validate_tree)
+      std::function<void(int)> emit = [&](int idx) {
+        if (rc) return;
+        const phip_filter_node &fn = q->filter_nodes[idx];
+        if (fn.op == PHIP_NODE_LEAF) {
+          DevNode dn = make_leaf(fn);
+          nodes.push_back(dn);
+          return;
+        }
+        if (fn.op == PHIP_NODE_NOT) {
+          emit(idx + 1);
+          DevNode dn;
+          memset(&dn, 0, sizeof(dn));
+          dn.op = DOP_NOT;
+          dn.lds_off = -1;
+          dn.skip_to = -1;
+          nodes.push_back(dn);
+          return;
+        }
+        int c = idx + 1;
+        for (int k = 0; k < fn.num_children && !rc; k++) {
+          const size_t first = nodes.size();
+          emit(c);
+          if (k > 0) {
+            DevNode dn;
+            memset(&dn, 0, sizeof(dn));
+            dn.op = fn.op == PHIP_NODE_AND ? DOP_AND : DOP_OR;
+            dn.lds_off = -1;
+            dn.skip_to = -1;
+            nodes.push_back(dn);
+            // the child's first node is its leftmost leaf: skip the child when the node is decided
+            nodes[first].skip_kind = fn.op == PHIP_NODE_AND ? SKIP_IF_NONE : SKIP_IF_ALL;
+            nodes[first].skip_to = (int32_t)nodes.size();
+          }
+          c = next[c - nb];
+        }
+      };
+      emit(nb);
+      if (rc) return rc;
+      // stack depth and candidate-doc hull (SortedIndexBasedFilterOperator ranges under ANDs)
+      struct Hull {
+        int64_t lo, hi;
+      };
+      std::vector<Hull> hst;
+      int sp = 0, maxsp = 0;
+      const int64_t full_hi = (int64_t)sg.num_docs - 1;
+      for (size_t i = node_begin; i < nodes.size(); i++) {
+        const DevNode &dn = nodes[i];
+        if (dn.op == DOP_LEAF) {
+          sp++;
+          Hull h{0, full_hi};
+          if (dn.leaf_kind == PHIP_LEAF_MATCH_NONE) h = {1, 0};
+          if (dn.leaf_kind == PHIP_LEAF_DOC_RANGES) h = {dn.lo, dn.hi};  // first start .. last end
+          hst.push_back(h);
+        } else if (dn.op == DOP_NOT) {
+          hst.back() = {0, full_hi};
+        } else {
+          sp--;
+          Hull b = hst.back();
+          hst.pop_back();
+          Hull a = hst.back();
+          if (dn.op == DOP_AND) hst.back() = {std::max(a.lo, b.lo), std::min(a.hi, b.hi)};
+          else if (a.lo > a.hi) hst.back() = b;
+          else if (b.lo > b.hi) hst.back() = a;
+          else hst.back() = {std::min(a.lo, b.lo), std::max(a.hi, b.hi)};
+        }
+        maxsp = std::max(maxsp, sp);
       }
+      if (maxsp > kMaxFilterStack) return fail(PHIP_ERR_UNSUPPORTED, "segment %d filter needs stack depth %d", s, maxsp);
+      hull_lo = hst.back().lo;
+      hull_hi = hst.back().hi;
     }
     ds.node_end = (int32_t)nodes.size();
+    if (hull_lo > hull_hi) continue;  // no candidate doc: the segment is pruned (no work)
+    ds.tile0 = (int32_t)(hull_lo / kTileDocs);
+    ds.num_work = (int32_t)(hull_hi / kTileDocs - ds.tile0 + 1);
+    ds.work_begin = (int32_t)total_work;
+    total_work += ds.num_work;
+    dsegs.push_back(ds);
   }
-  if (total_tiles > INT32_MAX / 2) return fail(PHIP_ERR_UNSUPPORTED, "too many tiles in one query");
-  dq.total_tiles = (int32_t)total_tiles;
+  if (total_work > INT32_MAX / 2) return fail(PHIP_ERR_UNSUPPORTED, "too many tiles in one query");
+  dq.total_work = (int32_t)total_work;
+  dq.num_segs = (int32_t)dsegs.size();
+  const size_t segs_off = blob.reserve(sizeof(DevSeg) * std::max<size_t>(dsegs.size(), 1));
 
   // inverted leaves: dense doc words per leaf + roaring container tasks
   std::vector<RoaringTask> tasks;
@@ -1003,7 +1094,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       for (int64_t ci = cs.inv_begin[id]; ci < cs.inv_begin[id + 1]; ci++) {
         const Container &ct = cs.inv_conts[ci];
         RoaringTask t;
-        t.payload = cs.inv_blob + ct.off + (ct.kind == 2 ? 0 : 0);
+        t.payload = cs.inv_blob + ct.off;
         t.out_words = words;
         t.key = ct.key;
         t.kind = ct.kind;
@@ -1016,62 +1107,59 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   const size_t tasks_off = tasks.empty() ? 0 : blob.add(tasks.data(), tasks.size() * sizeof(RoaringTask));
 
   // ---- LDS staging layout per segment (kernels.hip: stage_tile) --------------------------------
-  // Every wave copies, per 2048-doc tile, the fixed-bit words of the filter columns, then of the value
-  // columns, and the dense words of inverted leaves into its LDS stage buffer. Regions are padded by
-  // kStagePad bytes on both sides (window_at reads one word before / after).
-  const int64_t kStageBudget = 36 * 1024;  // bytes per wave and buffer
+  // Every wave copies, per 2048-doc tile, the fixed-bit words of the scanned filter columns and the
+  // dense words of inverted leaves into its LDS stage buffer. Value / group-by columns are NOT staged:
+  // they are read for matched docs only (decoded from LDS when the column is also a filter column).
+  // Regions are padded by kStagePad bytes on both sides (window_at reads one word before / after).
+  const int64_t kStageBudget = 24 * 1024;  // bytes per wave and buffer
   int32_t stage_stride = 0;
-  for (int s = 0; s < nseg; s++) {
-    DevSeg &ds = dsegs[s];
+  for (DevSeg &ds : dsegs) {
     int32_t off = 0;
     ds.num_stage = 0;
-    auto add_col = [&](int c) -> bool {
-      DevCol &dc = ds.cols[c];
-      if (!dc.has_dict || dc.words == nullptr) return false;
-      if (dc.lds_off >= 0) return true;
-      const int32_t bytes = 256 * dc.bits;
-      if (ds.num_stage >= kMaxStage || off + bytes + 2 * kStagePad > kStageBudget) return false;
-      dc.lds_off = off + kStagePad;
-      ds.stage[ds.num_stage++] = {(const uint8_t *)dc.words, bytes, dc.lds_off};
+    ds.num_dma = 0;
+    auto add_region = [&](const uint8_t *base, int32_t bytes) -> int32_t {
+      if (ds.num_stage >= kMaxStage || off + bytes + 2 * kStagePad > kStageBudget) return -1;
+      const int32_t lds_off = off + kStagePad;
+      ds.stage[ds.num_stage++] = {base, bytes, lds_off};
+      ds.num_dma += (int32_t)ceil_div(bytes, 1024);
       off += bytes + 2 * kStagePad;
-      return true;
+      return lds_off;
     };
     for (int i = ds.node_begin; i < ds.node_end; i++) {
       DevNode &dn = nodes[i];
-      if (dn.op != PHIP_NODE_LEAF) continue;
+      if (dn.op != DOP_LEAF) continue;
       if (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || dn.leaf_kind == PHIP_LEAF_DICT_SET) {
-        if (add_col(dn.column)) dn.lds_off = ds.cols[dn.column].lds_off;
+        DevCol &dc = ds.cols[dn.column];
+        if (dc.lds_off < 0) dc.lds_off = add_region((const uint8_t *)dc.words, 256 * dc.bits);
+        dn.lds_off = dc.lds_off;
       } else if (dn.leaf_kind == PHIP_LEAF_INVERTED && dn.aux != nullptr) {
-        if (ds.num_stage < kMaxStage && off + 256 + 2 * kStagePad <= kStageBudget) {
-          dn.lds_off = off + kStagePad;
-          ds.stage[ds.num_stage++] = {(const uint8_t *)dn.aux, 256, dn.lds_off};
-          off += 256 + 2 * kStagePad;
-        }
+        dn.lds_off = add_region((const uint8_t *)dn.aux, 256);
       }
     }
-    for (int a = 0; a < naggs; a++) {
-      if (dq.aggs[a].acc == ACC_COUNT) continue;
-      add_col(dq.aggs[a].col_a);
-      if (dq.aggs[a].expr != PHIP_EXPR_COLUMN) add_col(dq.aggs[a].col_b);
-    }
-    for (int k = 0; k < q->num_group_by; k++) add_col(q->group_by_columns[k]);
     stage_stride = std::max(stage_stride, off);
   }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
   const size_t lds_fixed = (size_t)round_up((int64_t)(group_by ? 0 : nhll * (1 << std::max(log2m, 0)) * 4), 16) +
-                           (size_t)round_up((int64_t)(kBlock / 64) * (naggs + 2) * 8, 16);
-  int nbuf = (lds_fixed + (size_t)(kBlock / 64) * 2 * stage_stride <= 80 * 1024) ? 2 : 1;
-  const size_t lds = lds_fixed + (size_t)(kBlock / 64) * nbuf * stage_stride;
+                           (size_t)round_up((int64_t)kWavesPerBlock * (naggs + 2) * 8, 16);
+  int nbuf = 2;
+  size_t lds = lds_fixed + (size_t)kWavesPerBlock * (kListBytes + nbuf * stage_stride);
+  if (lds > 160 * 1024) {
+    nbuf = 1;
+    lds = lds_fixed + (size_t)kWavesPerBlock * (kListBytes + stage_stride);
+  }
   if (lds > 160 * 1024) return fail(PHIP_ERR_UNSUPPORTED, "query needs %zu bytes of LDS", lds);
   dq.stage_stride = stage_stride;
   dq.nbuf = nbuf;
+  dq.need_docs = group_by ? 1 : 0;
+  for (int a = 0; a < naggs; a++)
+    if (dq.aggs[a].acc != ACC_COUNT) dq.need_docs = 1;
   const size_t nodes_off = blob.reserve(std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
   const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
 
   // device buffers
   const int nslots = naggs + 2;
   const int blocks_per_cu = std::max(1, std::min<int>(8, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
-  int nblocks = (int)std::min<int64_t>(ceil_div(total_tiles, kBlock / 64), (int64_t)dev->num_cus * blocks_per_cu);
+  int nblocks = (int)std::min<int64_t>(ceil_div(total_work, kWavesPerBlock), (int64_t)dev->num_cus * blocks_per_cu);
   nblocks = std::max(nblocks, 1);
   void *dblob;
   int32_t rc = dev->ws.get("blob", blob.data.size() + 64, &dblob);
@@ -1079,8 +1167,8 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   uint8_t *base = (uint8_t *)dblob;
   for (auto &f : aux_fix) nodes[f.node].aux = base + f.off;
   // rewrite nodes (aux pointers now final) and segments
-  memcpy(blob.data.data() + nodes_off, nodes.data(), nodes.size() * sizeof(DevNode));
-  memcpy(blob.data.data() + segs_off, dsegs.data(), sizeof(DevSeg) * nseg);
+  if (!nodes.empty()) memcpy(blob.data.data() + nodes_off, nodes.data(), nodes.size() * sizeof(DevNode));
+  if (!dsegs.empty()) memcpy(blob.data.data() + segs_off, dsegs.data(), sizeof(DevSeg) * dsegs.size());
   dq.segs = (const DevSeg *)(base + segs_off);
   dq.nodes = (const DevNode *)(base + nodes_off);
 
@@ -1119,6 +1207,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   HIP_TRY(hipEventRecord(dev->ev[0], st));
   HIP_TRY(hipMemcpyAsync(dblob, blob.data.data(), blob.data.size(), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)nseg * 8, st));
+  if (filter_words) HIP_TRY(hipMemsetAsync(dq.filter_out, 0, (size_t)filter_nwords * 8, st));
   if (nhll && !group_by) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, (size_t)nhll * (1 << log2m) * 4, st));
   if (inv_words_total) {
     HIP_TRY(hipMemsetAsync(inv_words, 0, inv_words_total * 8, st));
