@@ -124,13 +124,15 @@ def main():
     ops = {q: pm.make_instance_plan(qcs[q], gsegs) for q in queries}
     alg_bytes = {q: algorithmic_bytes(qcs[q], raw_meta) for q in queries}
 
+    from pinot_amd.engine.distributed import allreduce_block
+
     def run_query(q):
         blk = ops[q].next_block()
         if dist is not None:
-            # RCCL all-reduce of the partial aggregates (aggregation queries: exact int64 slots)
-            vals = [v if isinstance(v, int) else 0 for v in blk.results] if hasattr(blk, "results") else [0]
-            t = torch.tensor(vals + [blk.stats.num_docs_scanned], dtype=torch.int64, device="cuda")
-            dist.all_reduce(t)
+            # the exchange step: RCCL all-reduce of the partial blocks (exact int64 / f64 / HLL-max slots)
+            merged = allreduce_block(blk, dist)
+            merged.scan_kernel_ms = blk.scan_kernel_ms
+            return merged
         return blk
 
     for _ in range(args.warmup):
