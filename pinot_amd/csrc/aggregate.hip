@@ -1,0 +1,575 @@
+// aggregate.hip -- projection + aggregation / group-by over the filter kernel's tile masks
+// (K5-K9 of SURVEY.md §2.4), and the small reduction / compaction kernels behind them.
+//
+// Execution model. Waves walk tiles in an XCD-aware order: the global work list is cut into 8
+// contiguous ranges, one per XCD (workgroups b and b+8 share an XCD: MI355X_MICROARCH.md §Workgroup
+// dispatch; placement is used for speed only, never for correctness), and inside its range an XCD's
+// waves stride together, so at any time all of them read the same segment and its dictionaries stay
+// in that XCD's 4 MiB L2. Per tile a wave loads the 64 lane-major mask words (256 B), compacts the
+// matched docs into a per-wave LDS ring (mbcnt ranks) and, 64 at a time, reads the projected columns
+// for exactly those docs (late materialisation, as DataFetcher reads only the block's doc ids,
+// pinot-core/.../common/DataFetcher.java:335-386): fixed-bit dict id from HBM, dictionary gather,
+// expression (TransformOperator subset: a, a+b, a-b, a*b), then
+//   GB_NONE    per-lane accumulators (int64-exact or f64), HLL registers in LDS;
+//   GB_LDS     a per-workgroup group table in LDS (DictionaryBasedGroupKeyGenerator's dense key:
+//              mixed radix over query-global dict ids, column 0 least significant), written to a
+//              per-workgroup slab and reduced in a fixed order by slab_reduce_kernel (bitwise
+//              reproducible, no global atomics);
+//   GB_GLOBAL  one dense table in HBM updated with global atomics (large key spaces).
+#include "dev_common.h"
+
+namespace phip {
+
+// The launch descriptor lives in device memory and is read through the constant address space
+// (scalar loads), so no per-lane copy of it is ever made.
+typedef const PHIP_CAS DevAggQuery cquery_t;
+typedef const PHIP_CAS DevAgg cagg_t;
+
+__device__ __forceinline__ int64_t dict_i64(ccol_t &c, uint32_t id) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return ((const PHIP_GLB int32_t *)c.dict)[id];
+    case PHIP_TYPE_LONG: return ((const PHIP_GLB int64_t *)c.dict)[id];
+    case PHIP_TYPE_FLOAT: return (int64_t)((const PHIP_GLB float *)c.dict)[id];
+    default: return (int64_t)((const PHIP_GLB double *)c.dict)[id];
+  }
+}
+__device__ __forceinline__ double dict_f64(ccol_t &c, uint32_t id) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return (double)((const PHIP_GLB int32_t *)c.dict)[id];
+    case PHIP_TYPE_LONG: return (double)((const PHIP_GLB int64_t *)c.dict)[id];
+    case PHIP_TYPE_FLOAT: return (double)((const PHIP_GLB float *)c.dict)[id];
+    default: return ((const PHIP_GLB double *)c.dict)[id];
+  }
+}
+__device__ __forceinline__ int64_t raw_i64(ccol_t &c, int32_t doc) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return ((const PHIP_GLB int32_t *)c.raw)[doc];
+    case PHIP_TYPE_LONG: return ((const PHIP_GLB int64_t *)c.raw)[doc];
+    case PHIP_TYPE_FLOAT: return (int64_t)((const PHIP_GLB float *)c.raw)[doc];
+    default: return (int64_t)((const PHIP_GLB double *)c.raw)[doc];
+  }
+}
+__device__ __forceinline__ double raw_f64(ccol_t &c, int32_t doc) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return (double)((const PHIP_GLB int32_t *)c.raw)[doc];
+    case PHIP_TYPE_LONG: return (double)((const PHIP_GLB int64_t *)c.raw)[doc];
+    case PHIP_TYPE_FLOAT: return (double)((const PHIP_GLB float *)c.raw)[doc];
+    default: return ((const PHIP_GLB double *)c.raw)[doc];
+  }
+}
+
+__device__ __forceinline__ uint32_t col_dict_id(ccol_t &c, int32_t doc) {
+  return decode_bits(c.words, (uint64_t)(uint32_t)doc * (uint32_t)c.bits, (uint32_t)c.bits);
+}
+__device__ __forceinline__ int64_t col_i64(ccol_t &c, int32_t doc) {
+  if (c.has_dict) return dict_i64(c, col_dict_id(c, doc));
+  return raw_i64(c, doc);
+}
+__device__ __forceinline__ double col_f64(ccol_t &c, int32_t doc) {
+  if (c.has_dict) return dict_f64(c, col_dict_id(c, doc));
+  return raw_f64(c, doc);
+}
+__device__ __forceinline__ int64_t expr_i64(cseg_t &s, cagg_t &a, int32_t doc) {
+  int64_t x = col_i64(s.cols[a.col_a], doc);
+  if (a.expr == PHIP_EXPR_COLUMN) return x;
+  int64_t y = col_i64(s.cols[a.col_b], doc);
+  if (a.expr == PHIP_EXPR_ADD) return x + y;
+  if (a.expr == PHIP_EXPR_SUB) return x - y;
+  return x * y;
+}
+__device__ __forceinline__ double expr_f64(cseg_t &s, cagg_t &a, int32_t doc) {
+  double x = col_f64(s.cols[a.col_a], doc);
+  if (a.expr == PHIP_EXPR_COLUMN) return x;
+  double y = col_f64(s.cols[a.col_b], doc);
+  if (a.expr == PHIP_EXPR_ADD) return x + y;
+  if (a.expr == PHIP_EXPR_SUB) return x - y;
+  return x * y;
+}
+
+// Typed atomics: LDS tables use ds_* atomics, HBM tables global_* atomics (no flat_* forms).
+#define PHIP_RLX __ATOMIC_RELAXED
+#define PHIP_WG __HIP_MEMORY_SCOPE_WORKGROUP
+#define PHIP_AG __HIP_MEMORY_SCOPE_AGENT
+typedef PHIP_LDS uint64_t lds_u64;
+typedef PHIP_LDS uint32_t lds_u32;
+typedef PHIP_GLB uint64_t glb_u64;
+typedef PHIP_GLB uint32_t glb_u32;
+
+// Packed u8 HLL register max in LDS (4 registers per u32 word; no byte max exists in the DS ISA).
+__device__ __forceinline__ void lds_hll_max(lds_u32 *words, uint32_t reg, uint32_t rho) {
+  lds_u32 *w = words + (reg >> 2);
+  const uint32_t sh = (reg & 3) * 8;
+  uint32_t old = *w;
+  while (((old >> sh) & 0xffu) < rho) {
+    const uint32_t want = (old & ~(0xffu << sh)) | (rho << sh);
+    if (__hip_atomic_compare_exchange_strong(w, &old, want, PHIP_RLX, PHIP_RLX, PHIP_WG)) break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-chunk work: 64 lanes = up to 64 matched docs of one segment (inactive lanes carry doc 0, a valid
+// doc, so every load stays in bounds, and contribute the identity)
+// ------------------------------------------------------------------------------------------------
+template <int NA>
+__device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc, bool act,
+                                          uint64_t (&acc)[NA], lds_u32 *hll_lds) {
+#pragma unroll
+  for (int a = 0; a < NA; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    const int kind = ag.acc;
+    if (kind == ACC_COUNT) {
+      acc[a] += act ? 1ull : 0ull;
+    } else if (kind == ACC_SUM_I64) {
+      const int64_t v = expr_i64(seg, ag, doc);
+      acc[a] += act ? (uint64_t)v : 0ull;
+    } else if (kind == ACC_HLL) {
+      ccol_t &c = seg.cols[ag.col_a];
+      const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+      if (act) __hip_atomic_fetch_max(&hll_lds[(ag.hll_slot << q.log2m) + (h >> 8)], h & 0xffu, PHIP_RLX, PHIP_WG);
+    } else {
+      const double v = expr_f64(seg, ag, doc);
+      const double cur = as_f64(acc[a]);
+      double nv;
+      if (kind == ACC_SUM_F64) nv = cur + (act ? v : 0.0);
+      else if (kind == ACC_MIN_F64) nv = fmin(cur, act ? v : __builtin_huge_val());
+      else nv = fmax(cur, act ? v : -__builtin_huge_val());
+      acc[a] = as_u64(nv);
+    }
+  }
+}
+
+// Dense group key of one doc: mixed radix over query-global dict ids, column 0 least significant
+// (DictionaryBasedGroupKeyGenerator.java:314,322,345,442).
+__device__ __forceinline__ int64_t group_key(cquery_t &q, cseg_t &seg, int32_t doc) {
+  int64_t key = 0;
+  for (int k = 0; k < q.num_group_by; k++) {
+    ccol_t &c = seg.cols[q.gb_cols[k]];
+    const uint32_t id = col_dict_id(c, doc);
+    const int32_t gid = c.remap ? ((const PHIP_GLB int32_t *)c.remap)[id] : (int32_t)id;
+    key += (int64_t)gid * q.gb_stride[k];
+  }
+  return key;
+}
+
+// GB_LDS: table rows in LDS (row 0 counts, row 1+a aggregation a), packed HLL registers in LDS.
+__device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_t doc, bool act, lds_u64 *tbl,
+                                                lds_u32 *hll_packed) {
+  const int64_t key = group_key(q, seg, doc);
+  if (!act) return;
+  const int32_t G = (int32_t)q.num_groups;
+  __hip_atomic_fetch_add(&tbl[key], 1ull, PHIP_RLX, PHIP_WG);
+  for (int a = 0; a < kMaxAggs; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    lds_u64 *slot = tbl + (1 + a) * G + key;
+    switch (ag.acc) {
+      case ACC_COUNT: break;  // == row 0
+      case ACC_SUM_I64: __hip_atomic_fetch_add(slot, (uint64_t)expr_i64(seg, ag, doc), PHIP_RLX, PHIP_WG); break;
+      case ACC_SUM_F64:
+        __hip_atomic_fetch_add((PHIP_LDS double *)slot, expr_f64(seg, ag, doc), PHIP_RLX, PHIP_WG);
+        break;
+      case ACC_MIN_F64: __hip_atomic_fetch_min(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_WG); break;
+      case ACC_MAX_F64: __hip_atomic_fetch_max(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_WG); break;
+      case ACC_HLL: {
+        ccol_t &c = seg.cols[ag.col_a];
+        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+        lds_hll_max(hll_packed + ((((int64_t)ag.hll_slot * G + key) << q.log2m) >> 2), h >> 8, h & 0xffu);
+        break;
+      }
+    }
+  }
+}
+
+// GB_GLOBAL: one table in HBM ([1 + naggs][G] u64, row 0 counts), HLL registers [nhll][G][m] u32.
+__device__ __forceinline__ void group_chunk_global(cquery_t &q, cseg_t &seg, int32_t doc, bool act) {
+  const int64_t key = group_key(q, seg, doc);
+  if (!act) return;
+  const int64_t G = q.num_groups;
+  glb_u64 *tbl = (glb_u64 *)q.gb_table;
+  __hip_atomic_fetch_add(&tbl[key], 1ull, PHIP_RLX, PHIP_AG);
+  for (int a = 0; a < kMaxAggs; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    glb_u64 *slot = tbl + (1 + a) * G + key;
+    switch (ag.acc) {
+      case ACC_COUNT: break;
+      case ACC_SUM_I64: __hip_atomic_fetch_add(slot, (uint64_t)expr_i64(seg, ag, doc), PHIP_RLX, PHIP_AG); break;
+      case ACC_SUM_F64:
+        __hip_atomic_fetch_add((PHIP_GLB double *)slot, expr_f64(seg, ag, doc), PHIP_RLX, PHIP_AG);
+        break;
+      case ACC_MIN_F64: __hip_atomic_fetch_min(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_AG); break;
+      case ACC_MAX_F64: __hip_atomic_fetch_max(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_AG); break;
+      case ACC_HLL: {
+        ccol_t &c = seg.cols[ag.col_a];
+        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+        glb_u32 *r = (glb_u32 *)q.gb_hll + (((int64_t)ag.hll_slot * G + key) << q.log2m) + (h >> 8);
+        // registers only grow: a stale read costs one extra atomic, never a result
+        if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
+        break;
+      }
+    }
+  }
+}
+
+template <int NA, int MODE>
+__device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, bool act, uint64_t (&acc)[NA],
+                                         lds_u32 *hll_lds, lds_u64 *tbl, lds_u32 *hll_packed) {
+  if constexpr (MODE == GB_NONE) agg_chunk<NA>(q, seg, doc, act, acc, hll_lds);
+  else if constexpr (MODE == GB_LDS) group_chunk_lds(q, seg, doc, act, tbl, hll_packed);
+  else group_chunk_global(q, seg, doc, act);
+}
+
+// ------------------------------------------------------------------------------------------------
+// the aggregation kernel
+// LDS: [per-wave doc rings] [GB_NONE: HLL registers u32] [GB_LDS: table u64 | packed HLL u32]
+// ------------------------------------------------------------------------------------------------
+template <int NA, int MODE>
+__global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cquery_t &q = *(cquery_t *)qptr;
+  const int lane = lane_id();
+  const int wave = uniform(threadIdx.x >> 6);
+  PHIP_LDS unsigned char *lds = (PHIP_LDS unsigned char *)smem;
+  lds_u32 *ring = (lds_u32 *)lds + wave * kRing;
+  PHIP_LDS unsigned char *rest = lds + kAggWaves * kRing * 4;
+  lds_u32 *hll_lds = (lds_u32 *)rest;
+  lds_u64 *tbl = (lds_u64 *)rest;
+  lds_u32 *hll_packed = (lds_u32 *)(rest + (size_t)q.tbl_words * 8);
+  int hll_words = 0;
+  if (MODE == GB_NONE && q.num_hll > 0) {
+    hll_words = q.num_hll << q.log2m;
+    for (int i = threadIdx.x; i < hll_words; i += kAggBlock) hll_lds[i] = 0;
+  }
+  if (MODE == GB_LDS) {
+    const int G = (int)q.num_groups;
+    for (int i = threadIdx.x; i < q.tbl_words; i += kAggBlock) {
+      const int row = i / G;
+      uint64_t init = 0;
+      if (row > 0 && q.aggs[row - 1].acc == ACC_MIN_F64) init = ~0ull;  // ordered(+inf) < ~0
+      tbl[i] = init;
+    }
+    for (int i = threadIdx.x; i < q.hll_words; i += kAggBlock) hll_packed[i] = 0;
+  }
+  __syncthreads();
+
+  // XCD-aware walk (grid is a multiple of 8 workgroups)
+  const int x = blockIdx.x & 7;
+  const int j = blockIdx.x >> 3;
+  const int gx = gridDim.x >> 3;
+  const int xs = (int)((int64_t)q.total_work * x / 8);
+  const int xe = (int)((int64_t)q.total_work * (x + 1) / 8);
+  const int wx = gx * kAggWaves;
+  const int wid = j * kAggWaves + wave;
+
+  uint64_t acc[NA];
+#pragma unroll
+  for (int a = 0; a < NA; a++) acc[a] = (a < q.num_aggs) ? acc_init(q.aggs[a].acc) : 0;
+
+  cseg_t *segs = (cseg_t *)q.segs;
+  const glb_u32 *mask = (const glb_u32 *)q.mask;
+  int head = 0, tail = 0;  // ring cursors (wave-uniform)
+  int si = 0;
+  int t = xs + wid;
+  uint32_t m_next = 0;
+  if (mask != nullptr && t < xe) m_next = mask[(size_t)t * 64 + lane];
+  for (; t < xe; t += wx) {
+    const uint32_t m_raw = m_next;
+    if (mask != nullptr && t + wx < xe) m_next = mask[(size_t)(t + wx) * 64 + lane];  // prefetch
+    if (segs[si].work_begin + segs[si].num_work <= t) {
+      if (head > tail) {  // leftover (< 64) matched docs of the previous segment
+        const bool act = lane < head - tail;
+        const int32_t doc = act ? (int32_t)ring[(tail + lane) & (kRing - 1)] : 0;
+        do_chunk<NA, MODE>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
+      }
+      head = tail = 0;
+      while (si + 1 < q.num_segs && segs[si + 1].work_begin <= t) si++;
+    }
+    cseg_t &seg = segs[si];
+    const int32_t doc0 = (seg.tile0 + (t - seg.work_begin)) * kTileDocs;
+    const int32_t nvalid = min(kTileDocs, seg.num_docs - doc0);
+    const uint32_t valid = valid_word(nvalid, lane);
+    const uint32_t m = mask != nullptr ? (m_raw & valid) : valid;
+    if (ballot(m != valid) == 0) {
+      // every doc of the tile matched: consecutive chunks, coalesced column reads
+      for (int c = 0; c < nvalid; c += 64) {
+        const bool act = c + lane < nvalid;
+        do_chunk<NA, MODE>(q, seg, act ? doc0 + c + lane : 0, act, acc, hll_lds, tbl, hll_packed);
+      }
+    } else {
+      uint32_t any = wave_or32(m);
+      while (any) {
+        const int bit = 31 - __builtin_clz(any);
+        any &= ~(1u << bit);
+        const bool b = (m >> bit) & 1u;
+        const uint64_t mm = ballot(b);
+        if (b) ring[(head + mbcnt64(mm)) & (kRing - 1)] = (uint32_t)(doc0 + (31 - bit) * 64 + lane);
+        head += __popcll(mm);
+        if (head - tail >= 64) {
+          const int32_t doc = (int32_t)ring[(tail + lane) & (kRing - 1)];
+          tail += 64;
+          do_chunk<NA, MODE>(q, seg, doc, true, acc, hll_lds, tbl, hll_packed);
+        }
+      }
+    }
+  }
+  if (head > tail) {
+    const bool act = lane < head - tail;
+    const int32_t doc = act ? (int32_t)ring[(tail + lane) & (kRing - 1)] : 0;
+    do_chunk<NA, MODE>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
+  }
+
+  // ---- workgroup epilogue --------------------------------------------------------------------
+  if constexpr (MODE == GB_NONE) {
+    __shared__ uint64_t part[kAggWaves][kMaxAggs];
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      if (a >= q.num_aggs) break;
+      const int kind = q.aggs[a].acc;
+      uint64_t v;
+      if (kind == ACC_COUNT || kind == ACC_SUM_I64 || kind == ACC_HLL) v = wave_reduce_u64_add(acc[a]);
+      else v = as_u64(wave_reduce_f64(as_f64(acc[a]), kind));
+      if (lane == 0) part[wave][a] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int a = 0; a < NA; a++) {
+        if (a >= q.num_aggs) break;
+        const int kind = q.aggs[a].acc;
+        uint64_t v = part[0][a];
+        for (int w = 1; w < kAggWaves; w++) v = acc_combine(kind, v, part[w][a]);
+        q.partials[(size_t)blockIdx.x * q.num_aggs + a] = v;
+      }
+    }
+    for (int i = threadIdx.x; i < hll_words; i += kAggBlock)
+      if (hll_lds[i]) __hip_atomic_fetch_max((glb_u32 *)q.hll_regs + i, (uint32_t)hll_lds[i], PHIP_RLX, PHIP_AG);
+  } else if constexpr (MODE == GB_LDS) {
+    __syncthreads();
+    glb_u64 *slab = (glb_u64 *)q.gb_table + (size_t)blockIdx.x * q.tbl_words;
+    for (int i = threadIdx.x; i < q.tbl_words; i += kAggBlock) slab[i] = tbl[i];
+    glb_u32 *hs = (glb_u32 *)q.gb_hll + (size_t)blockIdx.x * q.hll_words;
+    for (int i = threadIdx.x; i < q.hll_words; i += kAggBlock) hs[i] = hll_packed[i];
+  }
+}
+
+// Fixed-order reduction of the per-workgroup group-table slabs into the global layout
+// ([1 + naggs][G] u64, row 0 = counts) and of the packed HLL slabs into [nhll][G][m] u32.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const uint64_t *__restrict__ slab, int32_t nslabs,
+                                                          int32_t tbl_words, int64_t G, const int32_t *__restrict__ kinds,
+                                                          uint64_t *__restrict__ out, const uint32_t *__restrict__ hslab,
+                                                          int32_t hll_words, uint32_t *__restrict__ hout) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < tbl_words) {
+    const int row = (int)(i / G);
+    const int kind = row == 0 ? ACC_COUNT : kinds[row - 1];
+    uint64_t v = slab[i];
+    for (int b = 1; b < nslabs; b++) {
+      const uint64_t w = slab[(size_t)b * tbl_words + i];
+      if (kind == ACC_SUM_F64) v = as_u64(as_f64(v) + as_f64(w));
+      else if (kind == ACC_MIN_F64) v = v < w ? v : w;
+      else if (kind == ACC_MAX_F64) v = v > w ? v : w;
+      else v += w;
+    }
+    out[i] = v;
+  }
+  if (i < hll_words) {
+    uint32_t v = hslab[i];
+    for (int b = 1; b < nslabs; b++) {
+      const uint32_t w = hslab[(size_t)b * hll_words + i];
+      uint32_t r = 0;
+#pragma unroll
+      for (int k = 0; k < 32; k += 8) r |= max((v >> k) & 0xffu, (w >> k) & 0xffu) << k;
+      v = r;
+    }
+    hout[4 * i + 0] = v & 0xffu;
+    hout[4 * i + 1] = (v >> 8) & 0xffu;
+    hout[4 * i + 2] = (v >> 16) & 0xffu;
+    hout[4 * i + 3] = v >> 24;
+  }
+}
+
+// Deterministic reduction of per-block partials -> out[nslots]: one wave per slot, lane-strided over
+// blocks in a fixed order, then a fixed shuffle tree (bitwise reproducible run to run).
+__global__ void finalize_partials_kernel(const uint64_t *__restrict__ partials, int nblocks, int nslots,
+                                         const int32_t *__restrict__ kinds, uint64_t *__restrict__ out) {
+  const int a = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (a >= nslots) return;
+  const int kind = kinds[a];
+  const bool fp = kind == ACC_SUM_F64 || kind == ACC_MIN_F64 || kind == ACC_MAX_F64;
+  uint64_t v = fp ? acc_init(kind) : 0;
+  for (int b = lane; b < nblocks; b += 64) v = acc_combine(kind, v, partials[(int64_t)b * nslots + a]);
+  if (fp) v = as_u64(wave_reduce_f64(as_f64(v), kind));
+  else v = wave_reduce_u64_add(v);
+  if (lane == 0) out[a] = v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// group-by table init / compaction
+// ------------------------------------------------------------------------------------------------
+__global__ void fill_u64_kernel(uint64_t *__restrict__ p, int64_t n, uint64_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+// Per 1024-group chunk: number of non-empty groups.
+__global__ __launch_bounds__(256) void group_count_kernel(const uint64_t *__restrict__ counts, int64_t n,
+                                                          int32_t *__restrict__ chunk_counts) {
+  __shared__ int32_t s;
+  if (threadIdx.x == 0) s = 0;
+  __syncthreads();
+  int64_t base = (int64_t)blockIdx.x * 1024;
+  int c = 0;
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    int64_t gidx = base + i;
+    if (gidx < n && counts[gidx] != 0) c++;
+  }
+  atomicAdd(&s, c);
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_counts[blockIdx.x] = s;
+}
+
+// Single-block exclusive scan of chunk counts; total in offsets[nchunks].
+__global__ void exclusive_scan_kernel(const int32_t *__restrict__ in, int32_t n, int64_t *__restrict__ offsets) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t s = 0;
+  for (int i = 0; i < n; i++) {
+    offsets[i] = s;
+    s += in[i];
+  }
+  offsets[n] = s;
+}
+
+// Ordered compaction: writes group indices of non-empty groups, ascending.
+__global__ __launch_bounds__(256) void group_compact_kernel(const uint64_t *__restrict__ counts, int64_t n,
+                                                            const int64_t *__restrict__ offsets,
+                                                            int64_t *__restrict__ out_keys) {
+  __shared__ int32_t wave_counts[4];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  int64_t base = (int64_t)blockIdx.x * 1024;
+  int64_t out = offsets[blockIdx.x];
+  for (int round = 0; round < 1024 / 256; round++) {
+    int64_t gidx = base + round * 256 + threadIdx.x;
+    bool nz = gidx < n && counts[gidx] != 0;
+    uint64_t b = ballot(nz);
+    if (lane == 0) wave_counts[wave] = __popcll(b);
+    __syncthreads();
+    int32_t before = 0;
+    for (int w = 0; w < wave; w++) before += wave_counts[w];
+    int32_t total = 0;
+    for (int w = 0; w < 4; w++) total += wave_counts[w];
+    if (nz) {
+      int32_t rank = before + __popcll(b & ((1ull << lane) - 1));
+      out_keys[out + rank] = gidx;
+    }
+    out += total;
+    __syncthreads();
+  }
+}
+
+// Gather the aggregates of the compacted groups. table = [1 + naggs][ndense], row 0 = counts.
+__global__ void group_gather_kernel(const int64_t *__restrict__ keys, int64_t ngroups, int64_t ndense,
+                                    int32_t naggs, const int32_t *__restrict__ kinds,
+                                    const uint64_t *__restrict__ table, const uint32_t *__restrict__ hll, int32_t nhll,
+                                    int32_t log2m, double *__restrict__ out_values, int64_t *__restrict__ out_longs,
+                                    uint8_t *__restrict__ out_hll) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ngroups; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t key = keys[i];
+    for (int a = 0; a < naggs; a++) {
+      const int kind = kinds[a];
+      const uint64_t v = table[(int64_t)(1 + a) * ndense + key];
+      double d = 0.0;
+      int64_t l = 0;
+      switch (kind) {
+        case ACC_COUNT: l = (int64_t)table[key]; d = (double)l; break;
+        case ACC_SUM_I64: l = (int64_t)v; d = (double)l; break;
+        case ACC_SUM_F64: d = __longlong_as_double((long long)v); break;
+        case ACC_MIN_F64:
+        case ACC_MAX_F64: d = f64_unordered(v); break;
+        default: break;
+      }
+      out_values[i * naggs + a] = d;
+      out_longs[i * naggs + a] = l;
+    }
+    const int m = 1 << log2m;
+    for (int h = 0; h < nhll; h++) {
+      const uint32_t *src = hll + ((int64_t)h * ndense + key) * m;
+      uint8_t *dst = out_hll + (i * nhll + h) * m;
+      for (int j = 0; j < m; j++) dst[j] = (uint8_t)src[j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-callable launchers (runtime.cpp)
+// ------------------------------------------------------------------------------------------------
+static inline int grid_for(int64_t n, int per_block = 256, int cap = 4096) {
+  int64_t g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+template <int NA, int MODE>
+static hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s) {
+  if (lds > 65536) {
+    static bool configured = false;
+    if (!configured) {
+      hipError_t e = hipFuncSetAttribute((const void *)agg_kernel<NA, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+      if (e != hipSuccess) return e;
+      configured = true;
+    }
+  }
+  agg_kernel<NA, MODE><<<nblocks, kAggBlock, lds, s>>>(q);
+  return hipGetLastError();
+}
+
+// q: host copy (for the variant choice); dq: the same descriptor in device memory.
+hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s) {
+  if (q.mode == GB_LDS) return launch_agg_t<1, GB_LDS>(dq, nblocks, lds, s);
+  if (q.mode == GB_GLOBAL) return launch_agg_t<1, GB_GLOBAL>(dq, nblocks, lds, s);
+  if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE>(dq, nblocks, lds, s);
+  if (q.num_aggs <= 2) return launch_agg_t<2, GB_NONE>(dq, nblocks, lds, s);
+  if (q.num_aggs <= 4) return launch_agg_t<4, GB_NONE>(dq, nblocks, lds, s);
+  return launch_agg_t<8, GB_NONE>(dq, nblocks, lds, s);
+}
+
+hipError_t launch_slab_reduce(const uint64_t *slab, int32_t nslabs, int32_t tbl_words, int64_t G, const int32_t *kinds,
+                              uint64_t *out, const uint32_t *hslab, int32_t hll_words, uint32_t *hout, hipStream_t s) {
+  const int64_t n = std::max<int64_t>(tbl_words, hll_words);
+  slab_reduce_kernel<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(slab, nslabs, tbl_words, G, kinds, out, hslab, hll_words,
+                                                               hout);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
+                                    uint64_t *out, hipStream_t s) {
+  finalize_partials_kernel<<<nslots, 64, 0, s>>>(partials, nblocks, nslots, kinds, out);
+  return hipGetLastError();
+}
+hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  fill_u64_kernel<<<grid_for(n), 256, 0, s>>>(p, n, v);
+  return hipGetLastError();
+}
+hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_counts, int64_t nchunks,
+                              int64_t *offsets, hipStream_t s) {
+  group_count_kernel<<<(unsigned)nchunks, 256, 0, s>>>(counts, n, chunk_counts);
+  exclusive_scan_kernel<<<1, 64, 0, s>>>(chunk_counts, (int32_t)nchunks, offsets);
+  return hipGetLastError();
+}
+hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *offsets, int64_t nchunks,
+                                int64_t *keys, hipStream_t s) {
+  group_compact_kernel<<<(unsigned)nchunks, 256, 0, s>>>(counts, n, offsets, keys);
+  return hipGetLastError();
+}
+hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs,
+                               const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
+                               int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s) {
+  if (ngroups <= 0) return hipSuccess;
+  group_gather_kernel<<<grid_for(ngroups), 256, 0, s>>>(keys, ngroups, ndense, naggs, kinds, table, hll, nhll, log2m,
+                                                       vals, longs, hll_out);
+  return hipGetLastError();
+}
+
+}  // namespace phip

@@ -1,5 +1,5 @@
 // device.h -- structures shared by the host runtime (runtime.cpp) and the gfx950 kernels
-// (kernels.hip). Plain POD, identical layout on host and device.
+// (filter.hip, aggregate.hip, load.hip). Plain POD, identical layout on host and device.
 #pragma once
 #include <stdint.h>
 
@@ -8,15 +8,22 @@ namespace phip {
 constexpr int kMaxQueryColumns = 16;  // distinct columns one query may reference
 constexpr int kMaxAggs = 8;           // aggregation slots per query
 constexpr int kMaxFilterStack = 6;    // postfix evaluation stack depth (host rejects deeper programs)
+constexpr int kMaxGroupBy = 4;
 constexpr int kWave = 64;             // CDNA wavefront
-constexpr int kBlock = 256;           // 4 waves per workgroup
-constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kTileGroups = 32;       // 64-doc groups per wave tile: lane g (< 32) owns group g's bitmap word
+constexpr int kTileGroups = 32;       // 64-doc groups per tile: bit (31-g) of lane l's mask word = doc 64g+l
 constexpr int kTileDocs = kTileGroups * 64;  // 2048 docs per tile
 constexpr int kMaxStage = 12;         // LDS-staged filter sources (scan columns / inverted leaves) per segment
 constexpr int kStagePad = 16;         // guard bytes before and after every staged region
-constexpr int kListBytes = kTileDocs * 2;  // per-wave compacted list of matched doc offsets (u16)
 constexpr int kMaxHllRegs = 1 << 12;  // log2m <= 12 on the GPU path
+
+// filter kernel: 4 waves per workgroup, each wave streams its own contiguous range of tiles
+constexpr int kFilterBlock = 256;
+constexpr int kFilterWaves = kFilterBlock / kWave;
+constexpr int kMaxRing = 8;           // LDS-DMA ring slots per wave
+// aggregation kernel: 8 waves per workgroup
+constexpr int kAggBlock = 512;
+constexpr int kAggWaves = kAggBlock / kWave;
+constexpr int kRing = 128;            // per-wave ring of matched doc ids (u32), flushed 64 at a time
 
 // Accumulator kinds of one aggregation slot.
 enum AccKind : int32_t {
@@ -33,6 +40,13 @@ enum AccKind : int32_t {
 enum DevOp : int32_t { DOP_LEAF = 0, DOP_AND = 1, DOP_OR = 2, DOP_NOT = 3 };
 enum SkipKind : int32_t { SKIP_NONE = 0, SKIP_IF_NONE = 1, SKIP_IF_ALL = 2 };
 
+// Group-by table placement (aggregate kernel).
+enum GroupMode : int32_t {
+  GB_NONE = 0,    // aggregation only: per-lane accumulators -> per-block partials
+  GB_LDS = 1,     // per-workgroup table in LDS -> per-block slab in HBM -> fixed-order reduction
+  GB_GLOBAL = 2,  // one table in HBM, global atomics
+};
+
 // One column as seen by one segment of a query.
 struct DevCol {
   const uint32_t *words;  // fixed-bit dict ids: u32 words holding the BE stream (bit 31 = first bit)
@@ -44,17 +58,17 @@ struct DevCol {
   int32_t card;
   int32_t type;      // PHIP_TYPE_*
   int32_t has_dict;  // 1: dictionary-encoded; 0: raw
-  int32_t lds_off;   // byte offset of this column's tile region in the wave's stage buffer, -1 = not staged
+  int32_t lds_off;   // filter kernel: byte offset of this column's tile region in the stage slot, -1 = not staged
   int32_t pad;
 };
 
-// One source the wave copies into its LDS stage buffer for every tile (LDS-DMA, 1 KiB per
+// One source the filter wave copies into its LDS stage slot for every tile (LDS-DMA, 1 KiB per
 // wave-instruction): a fixed-bit filter column (256*b bytes per 2048-doc tile) or the dense doc words of
 // an inverted leaf (256 bytes per tile).
 struct StageSrc {
   const uint8_t *base;  // tile t starts at base + t * bytes
   int32_t bytes;        // per tile, multiple of 16
-  int32_t lds_off;      // region offset in the stage buffer
+  int32_t lds_off;      // region offset in the stage slot
 };
 
 // One segment with work in this query. Its tiles [tile0, tile0 + num_work) are global work items
@@ -93,9 +107,22 @@ struct DevNode {
                       // INVERTED: u64 doc bitmap words of the segment (materialised)
 };
 
+// Filter kernel launch (K1-K4 of SURVEY.md §2.4).
+struct DevFilter {
+  const DevSeg *segs;
+  const DevNode *nodes;
+  int32_t num_segs;
+  int32_t total_work;
+  int32_t stage_stride;  // bytes of one ring slot (max over segments), multiple of 16
+  int32_t nbuf;          // ring slots per wave (2..kMaxRing): nbuf-1 tiles in flight while one is evaluated
+  uint32_t *mask_out;    // optional: [total_work][64] lane-major tile masks
+  uint64_t *partials;    // [num_blocks][2]: matched docs, entries scanned in filter
+  uint64_t *seg_matched; // [num query segments]
+};
+
 struct DevAgg {
-  int32_t acc;     // AccKind
-  int32_t expr;    // PHIP_EXPR_*
+  int32_t acc;       // AccKind
+  int32_t expr;      // PHIP_EXPR_*
   int32_t col_a;
   int32_t col_b;
   int32_t integral;  // expression evaluated in int64 (both inputs INT/LONG)
@@ -104,31 +131,30 @@ struct DevAgg {
   int32_t pad;
 };
 
-struct DevQuery {
+// Aggregation / group-by kernel launch (K5-K9).
+struct DevAggQuery {
   const DevSeg *segs;
-  const DevNode *nodes;
   int32_t num_segs;
   int32_t total_work;
+  const uint32_t *mask;  // [total_work][64] lane-major tile masks from the filter kernel; null = all docs
   int32_t num_aggs;
   int32_t num_hll;
-  int32_t stage_stride;  // bytes of one stage buffer (max over segments)
-  int32_t nbuf;          // stage buffers per wave (2: the next tile's DMA overlaps this tile)
-  int32_t need_docs;     // 1 if any aggregation / group-by reads per-doc values (else COUNT only)
-  int32_t pad0;
+  int32_t log2m;         // shared by all HLL aggs (host enforces)
+  int32_t mode;          // GroupMode
   DevAgg aggs[kMaxAggs];
   // group-by
   int32_t num_group_by;
-  int32_t gb_cols[4];
-  int64_t gb_stride[4];   // mixed radix, column 0 least significant
-  int64_t num_groups;     // dense key space size (0 = no group-by)
-  uint64_t *gb_table;     // [num_aggs][num_groups] 64-bit accumulators (int64 / f64 bits / ordered min-max)
-  uint64_t *gb_count;     // [num_groups] int64 doc counts
-  uint32_t *gb_hll;       // [num_hll][num_groups][1<<log2m]
-  // aggregation-only partials
-  uint64_t *partials;     // [num_blocks][num_aggs + 2] (slot num_aggs: matched docs, +1: entries scanned)
-  uint32_t *hll_regs;     // [num_hll][1<<log2m] (aggregation-only)
-  uint64_t *seg_matched;  // [num query segments] matched docs per segment
-  uint64_t *filter_out;   // optional: filter bitmap words of segment 0 (phip_filter_bitmap)
+  int32_t gb_cols[kMaxGroupBy];
+  int32_t pad0;
+  int64_t gb_stride[kMaxGroupBy];  // mixed radix, column 0 least significant
+  int64_t num_groups;     // dense key space size
+  int32_t tbl_words;      // GB_LDS: u64 words of one workgroup table = num_groups * (1 + num_aggs)
+  int32_t hll_words;      // GB_LDS: u32 words of one workgroup's packed HLL registers = groups*nhll*m/4
+  uint64_t *gb_table;     // GB_GLOBAL: [1 + num_aggs][num_groups] (row 0 = counts); GB_LDS: [blocks][tbl_words] slab
+  uint32_t *gb_hll;       // GB_GLOBAL: [nhll][num_groups][m] u32; GB_LDS: [blocks][hll_words] packed u8x4 slab
+  // aggregation only
+  uint64_t *partials;     // [num_blocks][num_aggs]
+  uint32_t *hll_regs;     // [nhll][m] u32 (atomicMax from every block)
 };
 
 // One Roaring container of one selected dictionary id, OR-ed into a segment's dense doc words.

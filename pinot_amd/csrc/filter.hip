@@ -1,0 +1,472 @@
+// filter.hip -- the filter kernel (K1-K4 of SURVEY.md §2.4) and the Roaring decode of inverted leaves.
+//
+// Execution model. One wave streams a CONTIGUOUS range of 2048-doc tiles (the global work list is
+// segment-ordered, so a wave changes segment at most a few times and its segment / filter-program
+// metadata stays in the scalar cache). Every scanned column's bytes for a tile (256*b bytes: a
+// 64-doc group is exactly 2b words of the u32 word layout, kernels.hip/runtime.cpp) and every
+// inverted leaf's 256 dense-word bytes arrive in the wave's LDS ring by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB per wave-instruction); nbuf-1 tiles are in flight while one is
+// evaluated, and completion is awaited with a counted vmcnt (the per-slot count of younger
+// vector-memory operations is kept packed in one wave-uniform u64).
+//
+// A tile's doc set is lane-major: lane l owns a 32-bit word whose bit (31-g) is doc 64g + l. Scan
+// leaves decode with lanes = docs of one 64-doc group at a time (one v_alignbit per doc and group),
+// which is SVScanDocIdIterator + PredicateEvaluator.applySV
+// (pinot-core/.../operator/dociditerators/SVScanDocIdIterator.java:75-142) without the doc-id
+// materialisation; AND / OR / NOT (AndDocIdSet / OrDocIdSet / NotDocIdSet) are one VALU op per lane.
+// The tile's 64 lane words (256 B, one coalesced store) go to the aggregation kernel when the query
+// projects anything; COUNT-only queries stop here (FastFilteredCountOperator.java:66-78).
+#include "dev_common.h"
+
+namespace phip {
+
+// ------------------------------------------------------------------------------------------------
+// LDS-DMA staging. The copy is issued through inline asm so that hipcc does not see an LDS write in
+// flight: it would otherwise put s_waitcnt vmcnt(0) in front of the first ds_read of the CURRENT
+// tile and drain the prefetch of the next ones. Completion is awaited by wait_vmcnt(n).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
+// Issue the LDS-DMA copies of one tile's staged regions; returns the number of wave-instructions.
+__device__ __forceinline__ int stage_tile(cseg_t &seg, int32_t tile_in_seg, PHIP_LDS uint8_t *buf) {
+  const int lane = lane_id();
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)buf);
+  const int ns = seg.num_stage;
+  for (int i = 0; i < ns; i++) {
+    const int32_t sbytes = seg.stage[i].bytes;
+    const uint8_t *g = seg.stage[i].base + (int64_t)tile_in_seg * sbytes + lane * 16;
+    const uint32_t l = lbase + (uint32_t)seg.stage[i].lds_off;
+    for (int c = 0; c < sbytes; c += 1024) {
+      if (c + lane * 16 < sbytes) dma16(g + c, l + (uint32_t)c);
+    }
+  }
+  return seg.num_dma;
+}
+
+struct Tile {
+  int32_t doc0;          // first doc of the tile within the segment
+  int32_t valid_docs;    // docs of the tile inside the segment (1..2048)
+  const PHIP_LDS uint8_t *stage;  // the tile's LDS ring slot
+};
+
+// ------------------------------------------------------------------------------------------------
+// filter leaves
+// ------------------------------------------------------------------------------------------------
+// Group loop of one scan leaf: lane l decodes doc g*64 + l from the staged words (2B words per group).
+#define PHIP_GROUP_LOOP(PASS_EXPR)                                             \
+  const int lane = lane_id();                                                  \
+  const int32_t p = lane * B;                                                  \
+  const int32_t q = (p - 1) >> 5;                                              \
+  const uint32_t s = (uint32_t)(32 * (q + 1) - p);                             \
+  const PHIP_LDS uint32_t *wl = w + q;                                         \
+  const int32_t gstride = 2 * B;                                               \
+  uint32_t r = 0;                                                              \
+  _Pragma("unroll 8") for (int g = 0; g < kTileGroups; g++) {                  \
+    const uint32_t win = __builtin_amdgcn_alignbit(wl[0], wl[1], s);           \
+    wl += gstride;                                                             \
+    r = r + r + (uint32_t)(PASS_EXPR);                                         \
+  }                                                                            \
+  return r;
+
+// RangePredicateEvaluator on dict ids: lo <= v < hi  <=>  (win - lo<<k) < (hi-lo)<<k with k = 32-B
+// (the low k bits of the window belong to the next doc and never carry into the comparison).
+__device__ __forceinline__ uint32_t scan_range(const PHIP_LDS uint32_t *w, int B, uint32_t LO, uint32_t SPAN) {
+  PHIP_GROUP_LOOP((win - LO) < SPAN)
+}
+
+// IN / NOT IN / EQ / NEQ on a column with card <= 64: membership in a 64-bit mask (the host
+// complements it for exclusive predicates).
+__device__ __forceinline__ uint32_t scan_small_set(const PHIP_LDS uint32_t *w, int B, uint64_t set) {
+  const uint32_t k = 32 - B;
+  PHIP_GROUP_LOOP(((set >> (win >> k)) & 1ull) != 0)
+}
+
+// IN / NOT IN on a larger dictionary: bitset over dict ids in HBM (L1/L2 resident).
+__device__ __forceinline__ uint32_t scan_big_set(const PHIP_LDS uint32_t *w, int B, const PHIP_GLB uint32_t *set, bool excl) {
+  const uint32_t k = 32 - B;
+  PHIP_GROUP_LOOP(((((set[(win >> k) >> 5] >> ((win >> k) & 31)) & 1u) != 0) != excl))
+}
+
+// bits [lo, hi] (inclusive, 0 <= lo <= hi <= 31) of a u32
+__device__ __forceinline__ uint32_t span32(int lo, int hi) {
+  const uint32_t upto = (hi == 31) ? ~0u : ((1u << (hi + 1)) - 1u);
+  return upto & ~((1u << lo) - 1u);
+}
+
+// Lane-major word of the doc range [s, e] (tile-relative, inclusive, clamped to the tile).
+__device__ __forceinline__ uint32_t range_word(int32_t s, int32_t e, int lane) {
+  const int32_t g_lo = max(0, (s - lane + 63) >> 6);
+  const int32_t g_hi = min(kTileGroups - 1, (e - lane) >= 0 ? (e - lane) >> 6 : -1);
+  if (g_lo > g_hi) return 0u;
+  return span32(31 - g_hi, 31 - g_lo);
+}
+
+// One leaf over the tile; `valid` = lane-major docs of the tile inside the segment.
+__device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__ n, uint32_t valid, const Tile &t,
+                                              uint32_t &scanned) {
+  const int lane = lane_id();
+  const int kind = n->leaf_kind;
+  if (kind == PHIP_LEAF_MATCH_ALL) return valid;
+  if (kind == PHIP_LEAF_MATCH_NONE) return 0;
+  if (kind == PHIP_LEAF_DOC_RANGES) {
+    // SortedIndexBasedFilterOperator: inclusive doc ranges, sorted and disjoint (scalar loads)
+    const PHIP_CAS int32_t *rg = (const PHIP_CAS int32_t *)n->aux;
+    const int32_t cnt = n->count;
+    const int32_t tile_end = t.doc0 + kTileDocs - 1;
+    int a = 0, b = cnt;  // first range that may intersect the tile
+    while (a < b) {
+      int mid = (a + b) >> 1;
+      if (rg[2 * mid + 1] < t.doc0) a = mid + 1; else b = mid;
+    }
+    uint32_t m = 0;
+    for (int i = a; i < cnt; i++) {
+      const int32_t s = rg[2 * i], e = rg[2 * i + 1];
+      if (s > tile_end) break;
+      m |= range_word(max(s, t.doc0) - t.doc0, min(e, tile_end) - t.doc0, lane);
+    }
+    return valid & m;
+  }
+  if (kind == PHIP_LEAF_INVERTED) {
+    // dense u64 doc words (bit d%64 of word d/64), transposed into the lane-major form
+    uint32_t r = 0;
+    if (n->lds_off >= 0) {
+      const PHIP_LDS uint64_t *w = (const PHIP_LDS uint64_t *)(t.stage + n->lds_off);
+#pragma unroll 8
+      for (int g = 0; g < kTileGroups; g++) r = r + r + (uint32_t)((w[g] >> lane) & 1ull);
+    } else {
+      const PHIP_GLB uint64_t *w = (const PHIP_GLB uint64_t *)n->aux + (t.doc0 >> 6);
+#pragma unroll 8
+      for (int g = 0; g < kTileGroups; g++) r = r + r + (uint32_t)((w[g] >> lane) & 1ull);
+    }
+    if (n->exclusive) r = ~r;
+    return valid & r;
+  }
+  // DICT_RANGE / DICT_SET on the bit-packed forward index
+  scanned += (uint32_t)t.valid_docs;
+  const int32_t B = n->bits;
+  if (n->lds_off >= 0) {
+    const PHIP_LDS uint32_t *w = (const PHIP_LDS uint32_t *)(t.stage + n->lds_off);
+    uint32_t r;
+    if (kind == PHIP_LEAF_DICT_RANGE) {
+      const uint32_t LO = (uint32_t)n->lo << (32 - B);
+      const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - B);
+      r = scan_range(w, B, LO, SPAN);
+    } else if (n->small_set) {
+      r = scan_small_set(w, B, n->set_mask);
+    } else {
+      r = scan_big_set(w, B, (const PHIP_GLB uint32_t *)n->aux, n->exclusive != 0);
+    }
+    return r & valid;
+  }
+  // not staged (LDS budget exceeded): decode from HBM
+  ccol_t &c = seg.cols[n->column];
+  const bool is_range = kind == PHIP_LEAF_DICT_RANGE;
+  const PHIP_GLB uint32_t *set = (const PHIP_GLB uint32_t *)n->aux;
+  const uint32_t lo = (uint32_t)n->lo;
+  const uint32_t span = (uint32_t)(n->hi - n->lo);
+  const bool excl = n->exclusive != 0;
+  const int32_t last = t.valid_docs - 1;
+  uint32_t r = 0;
+  for (int g = 0; g < kTileGroups; g++) {
+    const int32_t dit = min(g * 64 + lane, last);
+    const uint32_t v = decode_bits(c.words, (uint64_t)(uint32_t)(t.doc0 + dit) * (uint32_t)B, (uint32_t)B);
+    bool pass;
+    if (is_range) {
+      pass = (v - lo) < span;
+    } else if (n->small_set) {
+      pass = ((n->set_mask >> v) & 1ull) != 0;
+    } else {
+      pass = (((set[v >> 5] >> (v & 31)) & 1u) != 0) != excl;
+    }
+    r = r + r + (uint32_t)pass;
+  }
+  return r & valid;
+}
+
+// Filter program: the segment's tree in postfix order with binary AND/OR (runtime.cpp converts the
+// preorder ABI tree), evaluated once per tile over lane-major words with a small register stack.
+// The first leaf of the j-th (j >= 2) child of an AND / OR carries a skip: when the running value of
+// the node is already all-false (AND) / all-valid (OR) for the tile, the child is not evaluated.
+#define PHIP_PUSH(v)           \
+  do {                         \
+    const uint32_t _v = (v);   \
+    switch (sp) {              \
+      case 0: s0 = _v; break;  \
+      case 1: s1 = _v; break;  \
+      case 2: s2 = _v; break;  \
+      case 3: s3 = _v; break;  \
+      case 4: s4 = _v; break;  \
+      default: s5 = _v; break; \
+    }                          \
+    sp++;                      \
+  } while (0)
+#define PHIP_TOP(dst)             \
+  do {                            \
+    switch (sp - 1) {             \
+      case 0: dst = s0; break;    \
+      case 1: dst = s1; break;    \
+      case 2: dst = s2; break;    \
+      case 3: dst = s3; break;    \
+      case 4: dst = s4; break;    \
+      default: dst = s5; break;   \
+    }                             \
+  } while (0)
+#define PHIP_POP(dst) \
+  do {                \
+    PHIP_TOP(dst);    \
+    sp--;             \
+  } while (0)
+
+__device__ __forceinline__ uint32_t eval_filter(cseg_t &seg, cnode_t *__restrict__ nodes, uint32_t valid,
+                                                const Tile &t, uint32_t &scanned) {
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
+  int sp = 0;
+  int i = seg.node_begin;
+  const int end = seg.node_end;
+  while (i < end) {
+    cnode_t *n = nodes + i;
+    const int op = n->op;
+    if (op == DOP_LEAF) {
+      const int sk = n->skip_kind;
+      if (sk != SKIP_NONE) {
+        uint32_t top;
+        PHIP_TOP(top);
+        const bool decided = (sk == SKIP_IF_NONE) ? (ballot(top != 0) == 0) : (ballot(top != valid) == 0);
+        if (decided) {
+          i = n->skip_to;
+          continue;
+        }
+      }
+      PHIP_PUSH(eval_leaf(seg, n, valid, t, scanned));
+    } else if (op == DOP_NOT) {
+      uint32_t v;
+      PHIP_POP(v);
+      PHIP_PUSH(valid & ~v);
+    } else {
+      uint32_t v, w;
+      PHIP_POP(v);
+      PHIP_POP(w);
+      PHIP_PUSH(op == DOP_AND ? (v & w) : (v | w));
+    }
+    i++;
+  }
+  uint32_t r;
+  PHIP_POP(r);
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// the filter kernel
+// ------------------------------------------------------------------------------------------------
+// Per ring slot, the number of vector-memory instructions issued AFTER that slot's DMA (8 bits per
+// slot, packed; only slots with a tile in flight are counted).
+struct VmLedger {
+  uint64_t cnt = 0;     // byte s = younger ops of slot s
+  uint64_t active = 0;  // byte s = 0xff while slot s holds a tile in flight
+  __device__ __forceinline__ void issued(int k) {  // k more vector-memory instructions were issued
+    cnt += ((uint64_t)(uint32_t)k * 0x0101010101010101ull) & active;
+  }
+  __device__ __forceinline__ void start(int slot) {  // slot's DMA was just issued
+    cnt &= ~(0xffull << (8 * slot));
+    active |= 0xffull << (8 * slot);
+  }
+  __device__ __forceinline__ int younger(int slot) const { return (int)((cnt >> (8 * slot)) & 0xff); }
+  __device__ __forceinline__ void done(int slot) { active &= ~(0xffull << (8 * slot)); }
+};
+
+__global__ __launch_bounds__(kFilterBlock) void filter_kernel(DevFilter q) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  const int wave = uniform(threadIdx.x >> 6);
+  const int64_t waves_total = (int64_t)gridDim.x * kFilterWaves;
+  const int64_t gw = (int64_t)blockIdx.x * kFilterWaves + wave;
+  const int begin = (int)((int64_t)q.total_work * gw / waves_total);
+  const int end = (int)((int64_t)q.total_work * (gw + 1) / waves_total);
+  const int nbuf = q.nbuf;
+  const int stride = q.stage_stride;
+  PHIP_LDS uint8_t *ring = (PHIP_LDS uint8_t *)(smem + (size_t)wave * nbuf * stride);
+
+  cseg_t *segs = (cseg_t *)q.segs;
+  cnode_t *nodes = (cnode_t *)q.nodes;
+  uint32_t lane_matched = 0;  // per-lane popcount, reduced once per segment
+  uint64_t scanned = 0;
+  uint64_t matched_total = 0;
+  VmLedger vm;
+
+  // prefetch cursor: tiles [begin, pf) have their DMA issued
+  int pf = begin;
+  int sn = 0;  // segment of tile pf
+  auto prefetch = [&](int slot) {
+    while (sn + 1 < q.num_segs && segs[sn + 1].work_begin <= pf) sn++;
+    const int k = stage_tile(segs[sn], segs[sn].tile0 + (pf - segs[sn].work_begin), ring + slot * stride);
+    vm.issued(k);
+    vm.start(slot);
+    pf++;
+  };
+  int pslot = 0;
+  for (int i = 0; i < nbuf - 1 && pf < end; i++) {
+    prefetch(pslot);
+    pslot = pslot + 1 == nbuf ? 0 : pslot + 1;
+  }
+
+  int si = -1;  // segment of the current tile
+  int seg_end = -1;
+  int slot = 0;
+  for (int t = begin; t < end; t++) {
+    if (pf < end) {
+      prefetch(pslot);
+      pslot = pslot + 1 == nbuf ? 0 : pslot + 1;
+    }
+    if (t >= seg_end) {  // entering a new segment: flush the previous one's count
+      if (si >= 0) {
+        const uint64_t m = wave_reduce_u64_add(lane_matched);
+        lane_matched = 0;
+        matched_total += m;
+        if (m) {  // m is wave-uniform: one atomic wave-instruction (lane 0)
+          if (lane == 0) atomicAdd((unsigned long long *)&q.seg_matched[segs[si].seg_index], (unsigned long long)m);
+          vm.issued(1);
+        }
+      }
+      si = si < 0 ? 0 : si;
+      while (si + 1 < q.num_segs && segs[si + 1].work_begin <= t) si++;
+      seg_end = segs[si].work_begin + segs[si].num_work;
+    }
+    cseg_t &seg = segs[si];
+    Tile tl;
+    const int32_t tile_in_seg = seg.tile0 + (t - seg.work_begin);
+    tl.doc0 = tile_in_seg * kTileDocs;
+    tl.valid_docs = min(kTileDocs, seg.num_docs - tl.doc0);
+    tl.stage = ring + slot * stride;
+    wait_vmcnt(min(vm.younger(slot), 63));
+    vm.done(slot);
+
+    const uint32_t valid = valid_word(tl.valid_docs, lane);
+    uint32_t scanned_t = 0;
+    const uint32_t mask = seg.node_end > seg.node_begin ? eval_filter(seg, nodes, valid, tl, scanned_t) : valid;
+    scanned += scanned_t;
+    lane_matched += (uint32_t)__popc(mask);
+    if (q.mask_out != nullptr) {
+      ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
+      vm.issued(1);
+    }
+    slot = slot + 1 == nbuf ? 0 : slot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (si >= 0) {
+    const uint64_t m = wave_reduce_u64_add(lane_matched);
+    matched_total += m;
+    if (lane == 0 && m) atomicAdd((unsigned long long *)&q.seg_matched[segs[si].seg_index], (unsigned long long)m);
+  }
+  // per-block partials: matched docs, entries scanned in filter (fixed-order reduction on the host side)
+  __shared__ uint64_t part[kFilterWaves][2];
+  if (lane == 0) {
+    part[wave][0] = matched_total;
+    part[wave][1] = scanned;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint64_t v = 0;
+    for (int w = 0; w < kFilterWaves; w++) v += part[w][threadIdx.x];
+    q.partials[(size_t)blockIdx.x * 2 + threadIdx.x] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Roaring containers of the selected dict ids -> OR into dense u64 doc words
+// (BitmapInvertedIndexReader.getDocIds + ImmutableRoaringBitmap.or, InvertedIndexFilterOperator.java:79-95)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void roaring_or_kernel(const RoaringTask *__restrict__ tasks, int32_t ntasks) {
+  for (int ti = blockIdx.x; ti < ntasks; ti += gridDim.x) {
+    const RoaringTask tk = tasks[ti];
+    uint64_t *out = tk.out_words + (int64_t)tk.key * 1024;  // 65536 docs per container = 1024 words
+    if (tk.kind == 0) {
+      const uint16_t *v = (const uint16_t *)tk.payload;
+      for (int i = threadIdx.x; i < tk.card; i += blockDim.x) {
+        uint32_t x = v[i];
+        atomicOr((unsigned long long *)&out[x >> 6], 1ull << (x & 63));
+      }
+    } else if (tk.kind == 1) {
+      const uint64_t *w = (const uint64_t *)tk.payload;
+      for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        uint64_t x = w[i];
+        if (x) atomicOr((unsigned long long *)&out[i], x);
+      }
+    } else {
+      const uint16_t *r = (const uint16_t *)tk.payload;
+      const int nruns = tk.card;
+      for (int ri = 0; ri < nruns; ri++) {
+        uint32_t s = r[1 + 2 * ri], e = s + r[2 + 2 * ri];  // inclusive
+        uint32_t ws = s >> 6, we = e >> 6;
+        for (uint32_t wi = ws + threadIdx.x; wi <= we; wi += blockDim.x) {
+          int lo = (wi == ws) ? (int)(s & 63) : 0;
+          int hi = (wi == we) ? (int)(e & 63) : 63;
+          uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+          atomicOr((unsigned long long *)&out[wi], m);
+        }
+      }
+    }
+  }
+}
+
+// Lane-major tile masks -> doc-order u64 bitmap words of one segment (phip_filter_bitmap):
+// word (tile*32 + g) bit l = bit (31-g) of lane l's mask word.
+__global__ __launch_bounds__(256) void masks_to_words_kernel(const uint32_t *__restrict__ masks, int32_t tile0,
+                                                             int32_t ntiles, uint64_t *__restrict__ words,
+                                                             int64_t nwords) {
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t t = wave; t < ntiles; t += nw) {
+    const uint32_t m = masks[t * 64 + lane];
+    uint64_t mine = 0;
+    for (int g = 0; g < kTileGroups; g++) {
+      const uint64_t b = ballot((m >> (31 - g)) & 1u);
+      if (lane == g) mine = b;
+    }
+    const int64_t wi = (int64_t)(tile0 + t) * kTileGroups + lane;
+    if (lane < kTileGroups && wi < nwords) words[wi] = mine;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-callable launchers (runtime.cpp)
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream_t s) {
+  if (ntasks <= 0) return hipSuccess;
+  roaring_or_kernel<<<ntasks < 8192 ? ntasks : 8192, 256, 0, s>>>(tasks, ntasks);
+  return hipGetLastError();
+}
+
+hipError_t launch_filter(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s) {
+  if (lds_bytes > 65536) {
+    static bool configured = false;  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
+    if (!configured) {
+      hipError_t e = hipFuncSetAttribute((const void *)filter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+      if (e != hipSuccess) return e;
+      configured = true;
+    }
+  }
+  filter_kernel<<<nblocks, kFilterBlock, lds_bytes, s>>>(q);
+  return hipGetLastError();
+}
+
+hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,
+                                 hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  int blocks = (int)std::min<int64_t>(((int64_t)ntiles + 3) / 4, 4096);
+  masks_to_words_kernel<<<blocks, 256, 0, s>>>(masks, tile0, ntiles, words, nwords);
+  return hipGetLastError();
+}
+
+}  // namespace phip

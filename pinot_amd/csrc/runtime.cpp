@@ -34,7 +34,12 @@ hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32
                                    uint32_t *words, int64_t nwords, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
 hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream_t s);
-hipError_t launch_scan(const DevQuery &q, int nblocks, size_t lds_bytes, bool group_by, hipStream_t s);
+hipError_t launch_filter(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s);
+hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,
+                                 hipStream_t s);
+hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s);
+hipError_t launch_slab_reduce(const uint64_t *slab, int32_t nslabs, int32_t tbl_words, int64_t G, const int32_t *kinds,
+                              uint64_t *out, const uint32_t *hslab, int32_t hll_words, uint32_t *hout, hipStream_t s);
 hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
                                     uint64_t *out, hipStream_t s);
 hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_counts, int64_t nchunks,
@@ -42,9 +47,8 @@ hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_
 hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *offsets, int64_t nchunks,
                                 int64_t *keys, hipStream_t s);
 hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs,
-                               const int32_t *kinds, const uint64_t *table, const uint64_t *counts,
-                               const uint32_t *hll, int32_t nhll, int32_t log2m, double *vals, int64_t *longs,
-                               uint8_t *hll_out, hipStream_t s);
+                               const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
+                               int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
 }  // namespace phip
 
 using namespace phip;
@@ -746,7 +750,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     }
 
   // aggregations
-  DevQuery dq;
+  DevAggQuery dq;
   memset(&dq, 0, sizeof(dq));
   dq.num_segs = nseg;
   dq.num_aggs = naggs;
@@ -1106,21 +1110,26 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   }
   const size_t tasks_off = tasks.empty() ? 0 : blob.add(tasks.data(), tasks.size() * sizeof(RoaringTask));
 
-  // ---- LDS staging layout per segment (kernels.hip: stage_tile) --------------------------------
-  // Every wave copies, per 2048-doc tile, the fixed-bit words of the scanned filter columns and the
-  // dense words of inverted leaves into its LDS stage buffer. Value / group-by columns are NOT staged:
-  // they are read for matched docs only (decoded from LDS when the column is also a filter column).
-  // Regions are padded by kStagePad bytes on both sides (window_at reads one word before / after).
-  const int64_t kStageBudget = 24 * 1024;  // bytes per wave and buffer
+  // ---- filter kernel configuration (filter.hip) -------------------------------------------------
+  // Per 2048-doc tile, the wave's ring slot receives the fixed-bit words of every scanned filter column
+  // (256*b bytes) and the dense words of inverted leaves (256 bytes), each padded by kStagePad bytes on
+  // both sides (window_at reads one word before / after). Value / group-by columns are not staged:
+  // the aggregation kernel reads them for matched docs only.
+  bool has_filter = false;
+  for (const DevSeg &ds : dsegs) has_filter |= ds.node_end > ds.node_begin;
+  bool need_agg = group_by;
+  for (int a = 0; a < naggs; a++) need_agg |= dq.aggs[a].acc != ACC_COUNT;
+  const bool need_mask = has_filter && (need_agg || filter_words != nullptr);
+  const int64_t kSlotBudget = 20 * 1024;  // bytes per ring slot
   int32_t stage_stride = 0;
   for (DevSeg &ds : dsegs) {
     int32_t off = 0;
     ds.num_stage = 0;
     ds.num_dma = 0;
-    auto add_region = [&](const uint8_t *base, int32_t bytes) -> int32_t {
-      if (ds.num_stage >= kMaxStage || off + bytes + 2 * kStagePad > kStageBudget) return -1;
+    auto add_region = [&](const uint8_t *rbase, int32_t bytes) -> int32_t {
+      if (ds.num_stage >= kMaxStage || off + bytes + 2 * kStagePad > kSlotBudget) return -1;
       const int32_t lds_off = off + kStagePad;
-      ds.stage[ds.num_stage++] = {base, bytes, lds_off};
+      ds.stage[ds.num_stage++] = {rbase, bytes, lds_off};
       ds.num_dma += (int32_t)ceil_div(bytes, 1024);
       off += bytes + 2 * kStagePad;
       return lds_off;
@@ -1139,111 +1148,188 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     stage_stride = std::max(stage_stride, off);
   }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
-  const size_t lds_fixed = (size_t)round_up((int64_t)(group_by ? 0 : nhll * (1 << std::max(log2m, 0)) * 4), 16) +
-                           (size_t)round_up((int64_t)kWavesPerBlock * (naggs + 2) * 8, 16);
-  int nbuf = 2;
-  size_t lds = lds_fixed + (size_t)kWavesPerBlock * (kListBytes + nbuf * stage_stride);
-  if (lds > 160 * 1024) {
-    nbuf = 1;
-    lds = lds_fixed + (size_t)kWavesPerBlock * (kListBytes + stage_stride);
+  // ring depth: maximise the bytes in flight per CU, (blocks/CU) x 4 waves x (nbuf-1) slots, under
+  // the 160 KiB LDS; prefer >= 2 workgroups (8 waves) per CU for the VALU work of the leaves
+  int nbuf = 2, fbpc = 1;
+  {
+    int64_t best = -1;
+    for (int nb = 2; nb <= kMaxRing; nb++) {
+      const int64_t per_block = (int64_t)kFilterWaves * nb * stage_stride;
+      const int bpc = (int)std::min<int64_t>(8, (160 * 1024 - 1024) / per_block);
+      if (bpc < 1) break;
+      const int64_t inflight = (int64_t)bpc * kFilterWaves * (nb - 1) * stage_stride * (bpc >= 2 ? 2 : 1);
+      if (inflight > best) {
+        best = inflight;
+        nbuf = nb;
+        fbpc = bpc;
+      }
+    }
+    if (best < 0) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
   }
-  if (lds > 160 * 1024) return fail(PHIP_ERR_UNSUPPORTED, "query needs %zu bytes of LDS", lds);
-  dq.stage_stride = stage_stride;
-  dq.nbuf = nbuf;
-  dq.need_docs = group_by ? 1 : 0;
-  for (int a = 0; a < naggs; a++)
-    if (dq.aggs[a].acc != ACC_COUNT) dq.need_docs = 1;
-  const size_t nodes_off = blob.reserve(std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
-  const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
+  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride;
+  const int filter_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)dev->num_cus * fbpc,
+                                                                        ceil_div(total_work, kFilterWaves)));
 
-  // device buffers
-  const int nslots = naggs + 2;
-  const int blocks_per_cu = std::max(1, std::min<int>(8, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
-  int nblocks = (int)std::min<int64_t>(ceil_div(total_work, kWavesPerBlock), (int64_t)dev->num_cus * blocks_per_cu);
-  nblocks = std::max(nblocks, 1);
+  // ---- aggregation kernel configuration (aggregate.hip) -----------------------------------------
+  dq.log2m = log2m;
+  dq.mode = group_by ? GB_GLOBAL : GB_NONE;
+  const int m_regs = nhll ? (1 << log2m) : 0;
+  size_t agg_lds = (size_t)kAggWaves * kRing * 4;
+  int agg_bpc = 4;
+  if (group_by) {
+    const int64_t tbl_words = (int64_t)(1 + naggs) * dq.num_groups;
+    const int64_t hll_words = (int64_t)nhll * dq.num_groups * m_regs / 4;
+    const int64_t table_bytes = tbl_words * 8 + hll_words * 4;
+    const char *force = getenv("PHIP_GB_MODE");  // measurement override: "lds" / "global"
+    bool use_lds = table_bytes <= 128 * 1024;
+    if (force && !strcmp(force, "global")) use_lds = false;
+    if (force && !strcmp(force, "lds") && table_bytes <= 150 * 1024) use_lds = true;
+    if (use_lds) {
+      dq.mode = GB_LDS;
+      dq.tbl_words = (int32_t)tbl_words;
+      dq.hll_words = (int32_t)hll_words;
+      agg_lds += (size_t)round_up(table_bytes, 16);
+      agg_bpc = std::max(1, std::min(4, (int)((160 * 1024 - 1024) / agg_lds)));
+    }
+  } else if (nhll) {
+    agg_lds += (size_t)nhll * m_regs * 4;
+  }
+  int agg_blocks = (int)std::min<int64_t>((int64_t)dev->num_cus * agg_bpc, ceil_div(total_work, kAggWaves));
+  agg_blocks = (int)round_up(std::max(agg_blocks, 8), 8);  // the XCD walk needs a multiple of 8 workgroups
+
+  const size_t nodes_off = blob.reserve(std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
+  kinds[naggs] = ACC_COUNT;
+  kinds[naggs + 1] = ACC_COUNT;
+  const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
+  const size_t dq_off = blob.reserve(sizeof(DevAggQuery));  // written once every pointer is known
+
   void *dblob;
   int32_t rc = dev->ws.get("blob", blob.data.size() + 64, &dblob);
   if (rc) return rc;
   uint8_t *base = (uint8_t *)dblob;
   for (auto &f : aux_fix) nodes[f.node].aux = base + f.off;
-  // rewrite nodes (aux pointers now final) and segments
   if (!nodes.empty()) memcpy(blob.data.data() + nodes_off, nodes.data(), nodes.size() * sizeof(DevNode));
   if (!dsegs.empty()) memcpy(blob.data.data() + segs_off, dsegs.data(), sizeof(DevSeg) * dsegs.size());
-  dq.segs = (const DevSeg *)(base + segs_off);
-  dq.nodes = (const DevNode *)(base + nodes_off);
+  const DevSeg *dev_segs = (const DevSeg *)(base + segs_off);
+  const int32_t *dev_kinds = (const int32_t *)(base + kinds_off);
 
-  void *partials, *finals, *seg_matched;
-  rc = dev->ws.get("partials", (size_t)nblocks * nslots * 8, &partials);
+  DevFilter fq;
+  memset(&fq, 0, sizeof(fq));
+  fq.segs = dev_segs;
+  fq.nodes = (const DevNode *)(base + nodes_off);
+  fq.num_segs = (int32_t)dsegs.size();
+  fq.total_work = (int32_t)total_work;
+  fq.stage_stride = stage_stride;
+  fq.nbuf = nbuf;
+  dq.segs = dev_segs;
+
+  void *fpart, *finals, *seg_matched, *apart = nullptr, *masks = nullptr;
+  rc = dev->ws.get("filter_partials", (size_t)filter_blocks * 2 * 8, &fpart);
   if (rc) return rc;
   rc = dev->ws.get("finals", 64 * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
   if (rc) return rc;
   rc = dev->ws.get("seg_matched", (size_t)nseg * 8, &seg_matched);
   if (rc) return rc;
-  dq.partials = (uint64_t *)partials;
+  fq.partials = (uint64_t *)fpart;
+  fq.seg_matched = (uint64_t *)seg_matched;
+  uint64_t *fin_agg = (uint64_t *)finals;          // [naggs]
+  uint64_t *fin_filter = (uint64_t *)finals + 32;  // [2]: matched, entries scanned
   dq.hll_regs = (uint32_t *)((uint8_t *)finals + 64 * 8);
-  dq.seg_matched = (uint64_t *)seg_matched;
-  if (filter_words) {
-    void *fo;
-    rc = dev->ws.get("filter_out", (size_t)filter_nwords * 8 + 4096 * 8, &fo);
+  if (need_mask) {
+    rc = dev->ws.get("masks", (size_t)std::max<int64_t>(total_work, 1) * 64 * 4, &masks);
     if (rc) return rc;
-    dq.filter_out = (uint64_t *)fo;
+    fq.mask_out = (uint32_t *)masks;
+    dq.mask = (const uint32_t *)masks;
   }
-  if (group_by) {
-    void *tb, *cnt, *gh = nullptr;
-    rc = dev->ws.get("gb_table", (size_t)std::max(naggs, 1) * dq.num_groups * 8, &tb);
+  if (need_agg && !group_by) {
+    rc = dev->ws.get("agg_partials", (size_t)agg_blocks * std::max(naggs, 1) * 8, &apart);
     if (rc) return rc;
-    rc = dev->ws.get("gb_count", (size_t)dq.num_groups * 8, &cnt);
+    dq.partials = (uint64_t *)apart;
+  }
+  void *gtab = nullptr, *ghll = nullptr, *slab = nullptr, *hslab = nullptr;
+  if (group_by) {
+    rc = dev->ws.get("gb_table", (size_t)(1 + naggs) * dq.num_groups * 8, &gtab);
     if (rc) return rc;
     if (nhll) {
-      rc = dev->ws.get("gb_hll", (size_t)nhll * dq.num_groups * (1 << log2m) * 4, &gh);
+      rc = dev->ws.get("gb_hll", (size_t)nhll * dq.num_groups * m_regs * 4, &ghll);
       if (rc) return rc;
     }
-    dq.gb_table = (uint64_t *)tb;
-    dq.gb_count = (uint64_t *)cnt;
-    dq.gb_hll = (uint32_t *)gh;
+    if (dq.mode == GB_LDS) {
+      rc = dev->ws.get("gb_slab", (size_t)agg_blocks * dq.tbl_words * 8 + 16, &slab);
+      if (rc) return rc;
+      if (nhll) {
+        rc = dev->ws.get("gb_hslab", (size_t)agg_blocks * dq.hll_words * 4 + 16, &hslab);
+        if (rc) return rc;
+      }
+      dq.gb_table = (uint64_t *)slab;
+      dq.gb_hll = (uint32_t *)hslab;
+    } else {
+      dq.gb_table = (uint64_t *)gtab;
+      dq.gb_hll = (uint32_t *)ghll;
+    }
   }
+  void *fo = nullptr;
+  if (filter_words) {
+    rc = dev->ws.get("filter_out", (size_t)filter_nwords * 8 + 4096 * 8, &fo);
+    if (rc) return rc;
+  }
+
+  memcpy(blob.data.data() + dq_off, &dq, sizeof(dq));
 
   // ---- launch ---------------------------------------------------------------------------------
   HIP_TRY(hipEventRecord(dev->ev[0], st));
   HIP_TRY(hipMemcpyAsync(dblob, blob.data.data(), blob.data.size(), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)nseg * 8, st));
-  if (filter_words) HIP_TRY(hipMemsetAsync(dq.filter_out, 0, (size_t)filter_nwords * 8, st));
-  if (nhll && !group_by) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, (size_t)nhll * (1 << log2m) * 4, st));
+  if (filter_words) HIP_TRY(hipMemsetAsync(fo, 0, (size_t)filter_nwords * 8, st));
+  if (nhll && !group_by) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, (size_t)nhll * m_regs * 4, st));
   if (inv_words_total) {
     HIP_TRY(hipMemsetAsync(inv_words, 0, inv_words_total * 8, st));
     HIP_TRY(launch_roaring_or((const RoaringTask *)(base + tasks_off), (int32_t)tasks.size(), st));
   }
-  if (group_by) {
-    HIP_TRY(hipMemsetAsync(dq.gb_count, 0, (size_t)dq.num_groups * 8, st));
+  if (group_by && dq.mode == GB_GLOBAL) {
+    HIP_TRY(hipMemsetAsync(gtab, 0, (size_t)dq.num_groups * 8, st));  // counts
     for (int a = 0; a < naggs; a++) {
       uint64_t init = 0;
       if (dq.aggs[a].acc == ACC_MIN_F64) init = ~0ull;  // ordered(+inf) < ~0: atomicMin from the top
-      if (dq.aggs[a].acc == ACC_MAX_F64) init = 0ull;
-      HIP_TRY(launch_fill_u64(dq.gb_table + (int64_t)a * dq.num_groups, dq.num_groups, init, st));
+      HIP_TRY(launch_fill_u64((uint64_t *)gtab + (int64_t)(1 + a) * dq.num_groups, dq.num_groups, init, st));
     }
-    if (nhll) HIP_TRY(hipMemsetAsync(dq.gb_hll, 0, (size_t)nhll * dq.num_groups * (1 << log2m) * 4, st));
+    if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
   HIP_TRY(hipEventRecord(dev->ev[1], st));
-  HIP_TRY(launch_scan(dq, nblocks, lds, group_by, st));
+  if (has_filter && total_work > 0) HIP_TRY(launch_filter(fq, filter_blocks, filter_lds, st));
+  if (need_agg && total_work > 0) HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
   HIP_TRY(hipEventRecord(dev->ev[2], st));
-  HIP_TRY(launch_finalize_partials((const uint64_t *)partials, nblocks, nslots, (const int32_t *)(base + kinds_off),
-                                   (uint64_t *)finals, st));
+  if (has_filter && total_work > 0)
+    HIP_TRY(launch_finalize_partials((const uint64_t *)fpart, filter_blocks, 2, dev_kinds + naggs, fin_filter, st));
+  if (need_agg && !group_by && total_work > 0)
+    HIP_TRY(launch_finalize_partials((const uint64_t *)apart, agg_blocks, naggs, dev_kinds, fin_agg, st));
+  if (group_by && dq.mode == GB_LDS && total_work > 0)
+    HIP_TRY(launch_slab_reduce((const uint64_t *)slab, agg_blocks, dq.tbl_words, dq.num_groups, dev_kinds,
+                               (uint64_t *)gtab, (const uint32_t *)hslab, nhll ? dq.hll_words : 0, (uint32_t *)ghll, st));
+  if (group_by && dq.mode == GB_LDS && total_work == 0) {
+    HIP_TRY(hipMemsetAsync(gtab, 0, (size_t)dq.num_groups * 8, st));
+  }
+  if (filter_words && need_mask && !dsegs.empty())
+    HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
+                                  filter_nwords, st));
 
   auto impl = std::make_unique<ResultImpl>();
   phip_result &r = impl->pub;
   memset(&r, 0, sizeof(r));
-  std::vector<uint64_t> fin(nslots);
-  std::vector<uint64_t> segm(nseg);
+  std::vector<uint64_t> fin(64, 0);
+  std::vector<uint64_t> segm(nseg, 0);
   std::vector<uint32_t> hll_host;
-  HIP_TRY(hipMemcpyAsync(fin.data(), finals, nslots * 8, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(segm.data(), seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
+  if (total_work > 0) HIP_TRY(hipMemcpyAsync(fin.data(), finals, 64 * 8, hipMemcpyDeviceToHost, st));
+  if (has_filter) HIP_TRY(hipMemcpyAsync(segm.data(), seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
   if (nhll && !group_by) {
     hll_host.resize((size_t)nhll << log2m);
     HIP_TRY(hipMemcpyAsync(hll_host.data(), dq.hll_regs, hll_host.size() * 4, hipMemcpyDeviceToHost, st));
   }
-  if (filter_words)
-    HIP_TRY(hipMemcpyAsync(filter_words, dq.filter_out, (size_t)filter_nwords * 8, hipMemcpyDeviceToHost, st));
+  if (filter_words) HIP_TRY(hipMemcpyAsync(filter_words, fo, (size_t)filter_nwords * 8, hipMemcpyDeviceToHost, st));
 
+  // matched docs: the filter kernel's count, or every doc of every segment with work when unfiltered
+  int64_t docs_in_work = 0;
+  for (const DevSeg &ds : dsegs) docs_in_work += ds.num_docs;
   int64_t ngroups = 1;
   if (group_by) {
     const int64_t nchunks = ceil_div(dq.num_groups, 1024);
@@ -1252,7 +1338,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     if (rc) return rc;
     rc = dev->ws.get("gb_offsets", (size_t)(nchunks + 1) * 8, &offs);
     if (rc) return rc;
-    HIP_TRY(launch_group_count(dq.gb_count, dq.num_groups, (int32_t *)cc, nchunks, (int64_t *)offs, st));
+    HIP_TRY(launch_group_count((const uint64_t *)gtab, dq.num_groups, (int32_t *)cc, nchunks, (int64_t *)offs, st));
     int64_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -1265,17 +1351,16 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     rc = dev->ws.get("gb_out_longs", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ol);
     if (rc) return rc;
     if (nhll) {
-      rc = dev->ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * (1 << log2m), &oh);
+      rc = dev->ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * m_regs, &oh);
       if (rc) return rc;
     }
-    HIP_TRY(launch_group_compact(dq.gb_count, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
-    HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, (const int32_t *)(base + kinds_off),
-                                dq.gb_table, dq.gb_count, dq.gb_hll, nhll, log2m, (double *)ov, (int64_t *)ol,
-                                (uint8_t *)oh, st));
+    HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
+    HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, dev_kinds, (const uint64_t *)gtab,
+                                (const uint32_t *)ghll, nhll, log2m, (double *)ov, (int64_t *)ol, (uint8_t *)oh, st));
     std::vector<int64_t> hkeys(ngroups);
     impl->values.resize(ngroups * naggs);
     impl->longs.resize(ngroups * naggs);
-    impl->hll.resize((size_t)ngroups * nhll * (nhll ? (1 << log2m) : 0));
+    impl->hll.resize((size_t)ngroups * nhll * m_regs);
     if (ngroups) {
       HIP_TRY(hipMemcpyAsync(hkeys.data(), keys, ngroups * 8, hipMemcpyDeviceToHost, st));
       if (naggs) {
@@ -1299,14 +1384,30 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   } else {
     HIP_TRY(hipEventRecord(dev->ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
+  }
+  const int64_t matched = has_filter ? (int64_t)fin[32] : docs_in_work;
+  if (filter_words && !has_filter) {  // no filter program: every doc of the (single) segment matches
+    const int64_t n = dsegs.empty() ? 0 : dsegs[0].num_docs;
+    for (int64_t w = 0; w < filter_nwords; w++) {
+      const int64_t lo = w * 64;
+      filter_words[w] = lo >= n ? 0ull : (n - lo >= 64 ? ~0ull : ((1ull << (n - lo)) - 1ull));
+    }
+  }
+  if (!group_by) {
     impl->values.resize(naggs);
     impl->longs.resize(naggs);
     impl->hll.resize((size_t)nhll << (nhll ? log2m : 0));
     for (int a = 0; a < naggs; a++) {
-      uint64_t v = fin[a];
+      const int kind = dq.aggs[a].acc;
+      uint64_t v = need_agg ? fin[a] : 0;
+      if (!need_agg || total_work == 0) v = kind == ACC_COUNT ? (uint64_t)matched : 0;
+      if (total_work == 0 && (kind == ACC_MIN_F64 || kind == ACC_MAX_F64)) {
+        const double d = kind == ACC_MIN_F64 ? HUGE_VAL : -HUGE_VAL;
+        memcpy(&v, &d, 8);
+      }
       double d = 0.0;
       int64_t l = 0;
-      switch (dq.aggs[a].acc) {
+      switch (kind) {
         case ACC_COUNT:
         case ACC_SUM_I64: l = (int64_t)v; d = (double)l; break;
         default: memcpy(&d, &v, 8);
@@ -1320,12 +1421,16 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   HIP_TRY(hipEventElapsedTime(&t_all, dev->ev[0], dev->ev[3]));
   HIP_TRY(hipEventElapsedTime(&t_scan, dev->ev[1], dev->ev[2]));
 
-  r.num_docs_scanned = (int64_t)fin[naggs];
-  r.num_entries_scanned_in_filter = (int64_t)fin[naggs + 1];
+  r.num_docs_scanned = matched;
+  r.num_entries_scanned_in_filter = has_filter ? (int64_t)fin[33] : 0;
   r.num_entries_scanned_post_filter = r.num_docs_scanned * num_projected;
   r.num_total_docs = total_docs;
   r.num_segments_processed = nseg;
-  for (int s = 0; s < nseg; s++) r.num_segments_matched += segm[s] ? 1 : 0;
+  if (has_filter) {
+    for (int s = 0; s < nseg; s++) r.num_segments_matched += segm[s] ? 1 : 0;
+  } else {
+    for (const DevSeg &ds : dsegs) r.num_segments_matched += ds.num_docs > 0 ? 1 : 0;
+  }
   r.num_aggregations = naggs;
   r.num_groups = group_by ? ngroups : 1;
   r.num_group_by = q->num_group_by;

@@ -37,9 +37,26 @@ hipError_t launch_bswap64(uint64_t *, int64_t, hipStream_t) { return hipSuccess;
 hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }
 hipError_t launch_roaring_or(const RoaringTask *, int32_t, hipStream_t) { return hipSuccess; }
-hipError_t launch_scan(const DevQuery &q, int nblocks, size_t, bool, hipStream_t) {
-  memset(q.partials, 0, (size_t)nblocks * (q.num_aggs + 2) * 8);
-  if (q.num_groups > 0) q.gb_count[0] = 1;  // one non-empty group
+hipError_t launch_filter(const DevFilter &q, int nblocks, size_t, hipStream_t) {
+  memset(q.partials, 0, (size_t)nblocks * 2 * 8);
+  if (q.mask_out) memset(q.mask_out, 0, (size_t)q.total_work * 64 * 4);
+  return hipSuccess;
+}
+hipError_t launch_masks_to_words(const uint32_t *, int32_t, int32_t, uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *, int nblocks, size_t, hipStream_t) {
+  if (q.mode == GB_NONE) memset(q.partials, 0, (size_t)nblocks * q.num_aggs * 8);
+  else if (q.mode == GB_GLOBAL) q.gb_table[0] = 1;  // one non-empty group
+  else {
+    memset(q.gb_table, 0, (size_t)nblocks * q.tbl_words * 8);
+    q.gb_table[0] = 1;
+    if (q.gb_hll) memset(q.gb_hll, 0, (size_t)nblocks * q.hll_words * 4);
+  }
+  return hipSuccess;
+}
+hipError_t launch_slab_reduce(const uint64_t *slab, int32_t, int32_t tbl_words, int64_t, const int32_t *, uint64_t *out,
+                              const uint32_t *, int32_t hll_words, uint32_t *hout, hipStream_t) {
+  memcpy(out, slab, (size_t)tbl_words * 8);
+  if (hll_words) memset(hout, 0, (size_t)hll_words * 16);
   return hipSuccess;
 }
 hipError_t launch_finalize_partials(const uint64_t *, int, int nslots, const int32_t *, uint64_t *out, hipStream_t) {
@@ -53,7 +70,7 @@ hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *cc, in
 hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *, int64_t, int64_t *keys, hipStream_t) {
   int64_t o = 0; for (int64_t i = 0; i < n; i++) if (counts[i]) keys[o++] = i; return hipSuccess;
 }
-hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t naggs, const int32_t *, const uint64_t *, const uint64_t *,
+hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t naggs, const int32_t *, const uint64_t *,
                                const uint32_t *, int32_t nhll, int32_t log2m, double *v, int64_t *l, uint8_t *h, hipStream_t) {
   memset(v, 0, ng * naggs * 8); memset(l, 0, ng * naggs * 8); if (nhll) memset(h, 0, ng * nhll * (1 << log2m)); return hipSuccess;
 }
