@@ -71,6 +71,18 @@ struct StageSrc {
   int32_t lds_off;      // region offset in the stage slot
 };
 
+// A leaf of a conjunctive filter program (fast path): a staged scan of one fixed-bit column.
+constexpr int kMaxConj = 6;
+struct ConjLeaf {
+  int32_t lds_off;  // staged region in the ring slot
+  int32_t bits;
+  int32_t kind;     // 0: dict-id range, 1: dict-id set over card <= 64
+  uint32_t lo;      // range: lo << (32 - bits)
+  uint32_t span;    // range: (hi - lo) << (32 - bits)
+  int32_t pad;
+  uint64_t set_mask;
+};
+
 // One segment with work in this query. Its tiles [tile0, tile0 + num_work) are global work items
 // [work_begin, work_begin + num_work): tiles outside the candidate doc range of a sorted-index leaf
 // under the root AND are never visited (SortedIndexBasedFilterOperator prunes them on the CPU too).
@@ -84,7 +96,9 @@ struct DevSeg {
   int32_t num_stage;
   int32_t seg_index;   // index into the query's segment list (seg_matched)
   int32_t num_dma;     // LDS-DMA wave-instructions per tile (sum of ceil(stage bytes / 1 KiB))
-  int32_t pad;
+  int32_t conj;        // > 0: the program is AND of `conj` staged scan leaves (conj_leaf, most selective
+                       // first); the filter kernel evaluates it without the stack machine
+  ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
 };

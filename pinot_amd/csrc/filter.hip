@@ -267,6 +267,93 @@ __device__ __forceinline__ uint32_t eval_filter(cseg_t &seg, cnode_t *__restrict
 }
 
 // ------------------------------------------------------------------------------------------------
+// conjunctive fast path: AND of staged scan leaves, each a width-specialised group loop (the
+// per-group reads are ds_read2_b32 at compile-time offsets; the range test is v_sub + v_cmp into
+// VCC + v_addc, which shifts the predicate bit into the lane's word in one instruction)
+// ------------------------------------------------------------------------------------------------
+template <int B>
+__device__ __forceinline__ uint32_t conj_range(const PHIP_LDS uint32_t *w, uint32_t LO, uint32_t SPAN) {
+  const int lane = lane_id();
+  const int32_t p = lane * B;
+  const int32_t q = (p - 1) >> 5;
+  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
+  const PHIP_LDS uint32_t *wl = w + q;
+  uint32_t r = 0;
+  // batches of 8 groups: the 8 ds_read2 are issued before the compare block (inline asm is a
+  // scheduling barrier, so the loads are placed explicitly)
+#pragma unroll
+  for (int g0 = 0; g0 < kTileGroups; g0 += 8) {
+    uint32_t x[8], y[8];
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+      x[g] = wl[(g0 + g) * 2 * B];
+      y[g] = wl[(g0 + g) * 2 * B + 1];
+    }
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+      const uint32_t win = __builtin_amdgcn_alignbit(x[g], y[g], s);
+      uint32_t d;
+      asm("v_sub_u32 %[d], %[w], %[lo]\n\t"
+          "v_cmp_gt_u32 vcc, %[sp], %[d]\n\t"
+          "v_addc_co_u32 %[r], vcc, %[r], %[r], vcc"
+          : [r] "+v"(r), [d] "=&v"(d)
+          : [w] "v"(win), [lo] "s"(LO), [sp] "s"(SPAN)
+          : "vcc");
+    }
+  }
+  return r;
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t conj_set(const PHIP_LDS uint32_t *w, uint64_t set) {
+  const int lane = lane_id();
+  const int32_t p = lane * B;
+  const int32_t q = (p - 1) >> 5;
+  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
+  const PHIP_LDS uint32_t *wl = w + q;
+  uint32_t r = 0;
+#pragma unroll
+  for (int g = 0; g < kTileGroups; g++) {
+    const uint32_t win = __builtin_amdgcn_alignbit(wl[g * 2 * B], wl[g * 2 * B + 1], s);
+    r = r + r + (uint32_t)((set >> (win >> (32 - B))) & 1ull);
+  }
+  return r;
+}
+
+#define PHIP_B_CASES(X) \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
+  X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
+
+__device__ __forceinline__ uint32_t conj_leaf_eval(const PHIP_LDS uint32_t *w, int bits, int kind, uint32_t lo,
+                                                uint32_t span, uint64_t set) {
+  if (kind == 0) {
+    switch (bits) {
+#define PHIP_RC(b) case b: return conj_range<b>(w, lo, span);
+      PHIP_B_CASES(PHIP_RC)
+#undef PHIP_RC
+    }
+  } else {
+    switch (bits) {
+#define PHIP_SC(b) case b: return conj_set<b>(w, set);
+      PHIP_B_CASES(PHIP_SC)
+#undef PHIP_SC
+    }
+  }
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_t *slot, uint32_t valid) {
+  uint32_t r = valid;
+  const int k = seg.conj;
+  for (int i = 0; i < k; i++) {
+    if (i > 0 && ballot(r != 0) == 0) break;  // every doc already rejected (AndDocIdSet short-circuit)
+    const PHIP_CAS ConjLeaf &L = seg.conj_leaf[i];
+    r &= conj_leaf_eval((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.kind, L.lo, L.span, L.set_mask);
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
 // the filter kernel
 // ------------------------------------------------------------------------------------------------
 // Per ring slot, the number of vector-memory instructions issued AFTER that slot's DMA (8 bits per
@@ -353,7 +440,13 @@ __global__ __launch_bounds__(kFilterBlock) void filter_kernel(DevFilter q) {
 
     const uint32_t valid = valid_word(tl.valid_docs, lane);
     uint32_t scanned_t = 0;
-    const uint32_t mask = seg.node_end > seg.node_begin ? eval_filter(seg, nodes, valid, tl, scanned_t) : valid;
+    uint32_t mask;
+    if (seg.conj > 0) {
+      mask = eval_conj(seg, tl.stage, valid);
+      scanned_t = (uint32_t)seg.conj * (uint32_t)tl.valid_docs;
+    } else {
+      mask = seg.node_end > seg.node_begin ? eval_filter(seg, nodes, valid, tl, scanned_t) : valid;
+    }
     scanned += scanned_t;
     lane_matched += (uint32_t)__popc(mask);
     if (q.mask_out != nullptr) {

@@ -1120,7 +1120,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   bool need_agg = group_by;
   for (int a = 0; a < naggs; a++) need_agg |= dq.aggs[a].acc != ACC_COUNT;
   const bool need_mask = has_filter && (need_agg || filter_words != nullptr);
-  const int64_t kSlotBudget = 20 * 1024;  // bytes per ring slot
+  const int64_t kSlotBudget = 19 * 1024;  // bytes per ring slot
   int32_t stage_stride = 0;
   for (DevSeg &ds : dsegs) {
     int32_t off = 0;
@@ -1146,25 +1146,62 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       }
     }
     stage_stride = std::max(stage_stride, off);
+    // conjunctive fast path: a program made of AND nodes over staged range / small-set scan leaves
+    ds.conj = 0;
+    std::vector<std::pair<double, ConjLeaf>> conj;
+    bool ok = ds.node_end > ds.node_begin;
+    for (int i = ds.node_begin; i < ds.node_end && ok; i++) {
+      const DevNode &dn = nodes[i];
+      if (dn.op == DOP_AND) continue;
+      if (dn.op != DOP_LEAF || dn.lds_off < 0 ||
+          !(dn.leaf_kind == PHIP_LEAF_DICT_RANGE || (dn.leaf_kind == PHIP_LEAF_DICT_SET && dn.small_set))) {
+        ok = false;
+        break;
+      }
+      const int card = std::max(1, ds.cols[dn.column].card);
+      ConjLeaf L;
+      memset(&L, 0, sizeof(L));
+      L.lds_off = dn.lds_off;
+      L.bits = dn.bits;
+      double sel;
+      if (dn.leaf_kind == PHIP_LEAF_DICT_RANGE) {
+        L.kind = 0;
+        L.lo = (uint32_t)dn.lo << (32 - dn.bits);
+        L.span = (uint32_t)(dn.hi - dn.lo) << (32 - dn.bits);
+        sel = double(dn.hi - dn.lo) / card;
+      } else {
+        L.kind = 1;
+        L.set_mask = dn.set_mask;
+        const uint64_t in_dict = card >= 64 ? ~0ull : ((1ull << card) - 1);
+        sel = double(__builtin_popcountll(dn.set_mask & in_dict)) / card;
+      }
+      conj.push_back({sel, L});
+    }
+    if (ok && !conj.empty() && (int)conj.size() <= kMaxConj) {
+      // most selective leaf first: the short-circuit then skips the others on more tiles (AND is
+      // commutative, so the doc set is unchanged)
+      std::stable_sort(conj.begin(), conj.end(),
+                       [](const std::pair<double, ConjLeaf> &a, const std::pair<double, ConjLeaf> &b) { return a.first < b.first; });
+      ds.conj = (int32_t)conj.size();
+      for (size_t i = 0; i < conj.size(); i++) ds.conj_leaf[i] = conj[i].second;
+    }
   }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
-  // ring depth: maximise the bytes in flight per CU, (blocks/CU) x 4 waves x (nbuf-1) slots, under
-  // the 160 KiB LDS; prefer >= 2 workgroups (8 waves) per CU for the VALU work of the leaves
-  int nbuf = 2, fbpc = 1;
+  // ring depth: prefer 4 workgroups (16 waves) per CU for the VALU/LDS work of the leaves, and give
+  // each wave the deepest ring that then fits the 160 KiB LDS (bytes in flight per CU =
+  // blocks x 4 waves x (nbuf-1) x slot)
+  int nbuf = 0, fbpc = 0;
   {
-    int64_t best = -1;
-    for (int nb = 2; nb <= kMaxRing; nb++) {
-      const int64_t per_block = (int64_t)kFilterWaves * nb * stage_stride;
-      const int bpc = (int)std::min<int64_t>(8, (160 * 1024 - 1024) / per_block);
-      if (bpc < 1) break;
-      const int64_t inflight = (int64_t)bpc * kFilterWaves * (nb - 1) * stage_stride * (bpc >= 2 ? 2 : 1);
-      if (inflight > best) {
-        best = inflight;
-        nbuf = nb;
+    const char *env = getenv("PHIP_FILTER_BPC");  // measurement override
+    const int want = env ? std::max(1, std::min(8, atoi(env))) : 4;
+    for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
+      const int64_t nb = std::min<int64_t>(kMaxRing, (160 * 1024 - 1024) / ((int64_t)bpc * kFilterWaves * stage_stride));
+      if (nb >= 2) {
+        nbuf = (int)nb;
         fbpc = bpc;
       }
     }
-    if (best < 0) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
+    if (nbuf < 2) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
   }
   const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride;
   const int filter_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)dev->num_cus * fbpc,

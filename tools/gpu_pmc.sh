@@ -11,8 +11,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 i=0
 # passes: default groups, or PMC_PASSES="group1;group2;..." (counters of one group space-separated)
 PASSES=${PMC_PASSES:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES;SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA;FETCH_SIZE;GRBM_GUI_ACTIVE GRBM_COUNT"}
-IFS=';' read -ra GROUPS <<< "$PASSES"
-for ctr in "${GROUPS[@]}"; do
+IFS=';' read -ra PGROUPS <<< "$PASSES"
+for ctr in "${PGROUPS[@]}"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc$i -o run -- python3 tools/explore.py "$@" > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i ($ctr) failed rc=$?"; exit 1; }
 done
