@@ -272,10 +272,10 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
   int si = 0;
   int t = xs + wid;
   uint32_t m_next = 0;
-  if (mask != nullptr && t < xe) m_next = mask[(size_t)t * 64 + lane];
+  if (mask != nullptr && t < xe) m_next = __builtin_nontemporal_load(mask + (size_t)t * 64 + lane);
   for (; t < xe; t += wx) {
     const uint32_t m_raw = m_next;
-    if (mask != nullptr && t + wx < xe) m_next = mask[(size_t)(t + wx) * 64 + lane];  // prefetch
+    if (mask != nullptr && t + wx < xe) m_next = __builtin_nontemporal_load(mask + (size_t)(t + wx) * 64 + lane);  // prefetch
     if (segs[si].work_begin + segs[si].num_work <= t) {
       if (head > tail) {  // leftover (< 64) matched docs of the previous segment
         const bool act = lane < head - tail;

@@ -29,8 +29,9 @@ __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirs
 
 // Bits [off, off+bits) of the MSB-first stream held in words (u32, bit 31 first).
 __device__ __forceinline__ uint32_t decode_bits(const uint32_t *words_generic, uint64_t off, uint32_t bits) {
+  // streamed once: non-temporal, so the words do not evict the dictionaries the gathers re-read
   const PHIP_GLB uint32_t *p = (const PHIP_GLB uint32_t *)words_generic + (off >> 5);
-  const uint64_t win = ((uint64_t)p[0] << 32) | (uint64_t)p[1];
+  const uint64_t win = ((uint64_t)__builtin_nontemporal_load(p) << 32) | (uint64_t)__builtin_nontemporal_load(p + 1);
   return (uint32_t)((win << (off & 31)) >> (64 - bits));
 }
 

@@ -31,7 +31,7 @@ __device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds_dst) {
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_dst)
@@ -271,13 +271,10 @@ __device__ __forceinline__ uint32_t eval_filter(cseg_t &seg, cnode_t *__restrict
 // per-group reads are ds_read2_b32 at compile-time offsets; the range test is v_sub + v_cmp into
 // VCC + v_addc, which shifts the predicate bit into the lane's word in one instruction)
 // ------------------------------------------------------------------------------------------------
+// wl / s: the lane's first word and window shift (computed once from the runtime width, so the 31
+// specialisations share them instead of each hoisting its own copy out of the tile loop)
 template <int B>
-__device__ __forceinline__ uint32_t conj_range(const PHIP_LDS uint32_t *w, uint32_t LO, uint32_t SPAN) {
-  const int lane = lane_id();
-  const int32_t p = lane * B;
-  const int32_t q = (p - 1) >> 5;
-  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
-  const PHIP_LDS uint32_t *wl = w + q;
+__device__ __forceinline__ uint32_t conj_range(const PHIP_LDS uint32_t *wl, uint32_t s, uint32_t LO, uint32_t SPAN) {
   uint32_t r = 0;
   // batches of 8 groups: the 8 ds_read2 are issued before the compare block (inline asm is a
   // scheduling barrier, so the loads are placed explicitly)
@@ -305,17 +302,22 @@ __device__ __forceinline__ uint32_t conj_range(const PHIP_LDS uint32_t *w, uint3
 }
 
 template <int B>
-__device__ __forceinline__ uint32_t conj_set(const PHIP_LDS uint32_t *w, uint64_t set) {
-  const int lane = lane_id();
-  const int32_t p = lane * B;
-  const int32_t q = (p - 1) >> 5;
-  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
-  const PHIP_LDS uint32_t *wl = w + q;
+__device__ __forceinline__ uint32_t conj_set(const PHIP_LDS uint32_t *wl, uint32_t s, uint64_t set) {
   uint32_t r = 0;
 #pragma unroll
-  for (int g = 0; g < kTileGroups; g++) {
-    const uint32_t win = __builtin_amdgcn_alignbit(wl[g * 2 * B], wl[g * 2 * B + 1], s);
-    r = r + r + (uint32_t)((set >> (win >> (32 - B))) & 1ull);
+  for (int g0 = 0; g0 < kTileGroups; g0 += 8) {
+    uint32_t x[8], y[8];
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+      x[g] = wl[(g0 + g) * 2 * B];
+      y[g] = wl[(g0 + g) * 2 * B + 1];
+    }
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+      const uint32_t win = __builtin_amdgcn_alignbit(x[g], y[g], s);
+      r = r + r + (uint32_t)((set >> (win >> (32 - B))) & 1ull);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (registers -> resident waves)
   }
   return r;
 }
@@ -326,15 +328,19 @@ __device__ __forceinline__ uint32_t conj_set(const PHIP_LDS uint32_t *w, uint64_
 
 __device__ __forceinline__ uint32_t conj_leaf_eval(const PHIP_LDS uint32_t *w, int bits, int kind, uint32_t lo,
                                                 uint32_t span, uint64_t set) {
+  const int32_t p = lane_id() * bits;
+  const int32_t q = (p - 1) >> 5;
+  const uint32_t s = (uint32_t)(32 * (q + 1) - p);
+  const PHIP_LDS uint32_t *wl = w + q;
   if (kind == 0) {
     switch (bits) {
-#define PHIP_RC(b) case b: return conj_range<b>(w, lo, span);
+#define PHIP_RC(b) case b: return conj_range<b>(wl, s, lo, span);
       PHIP_B_CASES(PHIP_RC)
 #undef PHIP_RC
     }
   } else {
     switch (bits) {
-#define PHIP_SC(b) case b: return conj_set<b>(w, set);
+#define PHIP_SC(b) case b: return conj_set<b>(wl, s, set);
       PHIP_B_CASES(PHIP_SC)
 #undef PHIP_SC
     }
@@ -372,7 +378,8 @@ struct VmLedger {
   __device__ __forceinline__ void done(int slot) { active &= ~(0xffull << (8 * slot)); }
 };
 
-__global__ __launch_bounds__(kFilterBlock) void filter_kernel(DevFilter q) {
+template <bool kConjOnly>
+__global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel(DevFilter q) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);
@@ -441,7 +448,7 @@ __global__ __launch_bounds__(kFilterBlock) void filter_kernel(DevFilter q) {
     const uint32_t valid = valid_word(tl.valid_docs, lane);
     uint32_t scanned_t = 0;
     uint32_t mask;
-    if (seg.conj > 0) {
+    if (kConjOnly || seg.conj > 0) {
       mask = eval_conj(seg, tl.stage, valid);
       scanned_t = (uint32_t)seg.conj * (uint32_t)tl.valid_docs;
     } else {
@@ -541,17 +548,24 @@ hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream
   return hipGetLastError();
 }
 
-hipError_t launch_filter(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s) {
+template <bool C>
+static hipError_t launch_filter_t(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s) {
   if (lds_bytes > 65536) {
     static bool configured = false;  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
     if (!configured) {
-      hipError_t e = hipFuncSetAttribute((const void *)filter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+      hipError_t e = hipFuncSetAttribute((const void *)filter_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
       if (e != hipSuccess) return e;
       configured = true;
     }
   }
-  filter_kernel<<<nblocks, kFilterBlock, lds_bytes, s>>>(q);
+  filter_kernel<C><<<nblocks, kFilterBlock, lds_bytes, s>>>(q);
   return hipGetLastError();
+}
+
+// conj_only: every segment's program takes the conjunctive fast path (the interpreter is compiled
+// out, which frees registers for more resident waves)
+hipError_t launch_filter(const DevFilter &q, bool conj_only, int nblocks, size_t lds_bytes, hipStream_t s) {
+  return conj_only ? launch_filter_t<true>(q, nblocks, lds_bytes, s) : launch_filter_t<false>(q, nblocks, lds_bytes, s);
 }
 
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,

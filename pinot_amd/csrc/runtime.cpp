@@ -34,7 +34,7 @@ hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32
                                    uint32_t *words, int64_t nwords, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
 hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream_t s);
-hipError_t launch_filter(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s);
+hipError_t launch_filter(const DevFilter &q, bool conj_only, int nblocks, size_t lds_bytes, hipStream_t s);
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,
                                  hipStream_t s);
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s);
@@ -1187,13 +1187,15 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     }
   }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
+  bool conj_only = true;
+  for (const DevSeg &ds : dsegs) conj_only &= ds.conj > 0;
   // ring depth: prefer 4 workgroups (16 waves) per CU for the VALU/LDS work of the leaves, and give
   // each wave the deepest ring that then fits the 160 KiB LDS (bytes in flight per CU =
   // blocks x 4 waves x (nbuf-1) x slot)
   int nbuf = 0, fbpc = 0;
   {
     const char *env = getenv("PHIP_FILTER_BPC");  // measurement override
-    const int want = env ? std::max(1, std::min(8, atoi(env))) : 4;
+    const int want = env ? std::max(1, std::min(8, atoi(env))) : (conj_only ? 6 : 4);
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
       const int64_t nb = std::min<int64_t>(kMaxRing, (160 * 1024 - 1024) / ((int64_t)bpc * kFilterWaves * stage_stride));
       if (nb >= 2) {
@@ -1333,7 +1335,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
   HIP_TRY(hipEventRecord(dev->ev[1], st));
-  if (has_filter && total_work > 0) HIP_TRY(launch_filter(fq, filter_blocks, filter_lds, st));
+  if (has_filter && total_work > 0) HIP_TRY(launch_filter(fq, conj_only, filter_blocks, filter_lds, st));
   if (need_agg && total_work > 0) HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
   HIP_TRY(hipEventRecord(dev->ev[2], st));
   if (has_filter && total_work > 0)
