@@ -198,6 +198,16 @@ PHIP_API int32_t phip_segment_unload(uint64_t handle);
 PHIP_API int32_t phip_segment_device_bytes(uint64_t handle, uint64_t *out_bytes);
 
 PHIP_API int32_t phip_query(const phip_query_desc *query, phip_result **out_result);
+
+/* Prepared queries: InstancePlanMakerImplV2.makeInstancePlan returns a Plan that
+ * GlobalPlanImplV0.execute runs (pinot-core/.../plan/GlobalPlanImplV0.java:48-57). phip_plan_create does
+ * every host-side step once (predicate programs per segment, descriptors, launch shapes, device buffers);
+ * phip_plan_execute replays the launch sequence (eagerly; PHIP_GRAPH=1 opts into a captured hipGraph) and
+ * returns a result exactly as phip_query would. A plan keeps its segments' HBM alive: unloading a
+ * segment a plan uses defers the release to phip_plan_destroy. Executions of one plan serialise. */
+PHIP_API int32_t phip_plan_create(const phip_query_desc *query, uint64_t *out_plan);
+PHIP_API int32_t phip_plan_execute(uint64_t plan, phip_result **out_result);
+PHIP_API int32_t phip_plan_destroy(uint64_t plan);
 PHIP_API int32_t phip_result_dictionary(const phip_result *result, int32_t group_by_index,
                                         phip_dictionary_view *out_view);
 PHIP_API void phip_result_free(phip_result *result);

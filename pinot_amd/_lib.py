@@ -25,7 +25,8 @@ EXPR_COLUMN, EXPR_ADD, EXPR_SUB, EXPR_MUL = range(4)
 EXPORTED_SYMBOLS = (
     "phip_init", "phip_shutdown", "phip_device_count", "phip_last_error", "phip_version",
     "phip_segment_load", "phip_segment_unload", "phip_segment_device_bytes", "phip_query",
-    "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap",
+    "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap", "phip_plan_create", "phip_plan_execute",
+    "phip_plan_destroy",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -125,6 +126,12 @@ def load():
     lib.phip_result_free.restype = None
     lib.phip_filter_bitmap.argtypes = [ctypes.POINTER(QueryDesc), ctypes.POINTER(u64), i64]
     lib.phip_filter_bitmap.restype = i32
+    lib.phip_plan_create.argtypes = [ctypes.POINTER(QueryDesc), ctypes.POINTER(u64)]
+    lib.phip_plan_create.restype = i32
+    lib.phip_plan_execute.argtypes = [u64, ctypes.POINTER(ctypes.POINTER(Result))]
+    lib.phip_plan_execute.restype = i32
+    lib.phip_plan_destroy.argtypes = [u64]
+    lib.phip_plan_destroy.restype = i32
     _lib = lib
     return lib
 

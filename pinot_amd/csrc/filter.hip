@@ -267,55 +267,70 @@ __device__ __forceinline__ uint32_t eval_filter(cseg_t &seg, cnode_t *__restrict
 }
 
 // ------------------------------------------------------------------------------------------------
-// conjunctive fast path: AND of staged scan leaves, each a width-specialised group loop (the
-// per-group reads are ds_read2_b32 at compile-time offsets; the range test is v_sub + v_cmp into
-// VCC + v_addc, which shifts the predicate bit into the lane's word in one instruction)
+// conjunctive fast path: AND of staged scan leaves, each a width-specialised loop.
+//
+// P-layout. With P docs per lane-window (P * B <= 32), lane l reads ONE 32-bit window per 64P docs and
+// tests its P consecutive docs from it: bit i (MSB first) of the lane's word is doc
+// 64P*(i/P) + P*l + (i%P) of the tile. That cuts the LDS reads of a leaf from 32 to 32/P per tile
+// (ds_read2_b32 at compile-time offsets); the range test is v_sub + v_cmp into VCC + v_addc, which
+// shifts the predicate bit into the word in one instruction. After the AND of all leaves the word is
+// permuted once into the lane-major tile layout (to_lane_major).
 // ------------------------------------------------------------------------------------------------
-// wl / s: the lane's first word and window shift (computed once from the runtime width, so the 31
-// specialisations share them instead of each hoisting its own copy out of the tile loop)
-template <int B>
+template <int B, int P>
 __device__ __forceinline__ uint32_t conj_range(const PHIP_LDS uint32_t *wl, uint32_t s, uint32_t LO, uint32_t SPAN) {
+  constexpr int NK = kTileGroups / P;  // P-groups (64P docs) per tile
+  constexpr int STRIDE = 2 * P * B;    // words per P-group
+  constexpr int NB = NK < 8 ? NK : 8;  // loads issued ahead of each compare block
   uint32_t r = 0;
-  // batches of 8 groups: the 8 ds_read2 are issued before the compare block (inline asm is a
-  // scheduling barrier, so the loads are placed explicitly)
 #pragma unroll
-  for (int g0 = 0; g0 < kTileGroups; g0 += 8) {
-    uint32_t x[8], y[8];
+  for (int k0 = 0; k0 < NK; k0 += NB) {
+    uint32_t x[NB], y[NB];
 #pragma unroll
-    for (int g = 0; g < 8; g++) {
-      x[g] = wl[(g0 + g) * 2 * B];
-      y[g] = wl[(g0 + g) * 2 * B + 1];
+    for (int k = 0; k < NB; k++) {
+      x[k] = wl[(k0 + k) * STRIDE];
+      y[k] = wl[(k0 + k) * STRIDE + 1];
     }
 #pragma unroll
-    for (int g = 0; g < 8; g++) {
-      const uint32_t win = __builtin_amdgcn_alignbit(x[g], y[g], s);
-      uint32_t d;
-      asm("v_sub_u32 %[d], %[w], %[lo]\n\t"
-          "v_cmp_gt_u32 vcc, %[sp], %[d]\n\t"
-          "v_addc_co_u32 %[r], vcc, %[r], %[r], vcc"
-          : [r] "+v"(r), [d] "=&v"(d)
-          : [w] "v"(win), [lo] "s"(LO), [sp] "s"(SPAN)
-          : "vcc");
+    for (int k = 0; k < NB; k++) {
+      const uint32_t win = __builtin_amdgcn_alignbit(x[k], y[k], s);
+#pragma unroll
+      for (int j = 0; j < P; j++) {
+        const uint32_t f = j == 0 ? win : (win << (j * B));
+        uint32_t d;
+        asm("v_sub_u32 %[d], %[w], %[lo]\n\t"
+            "v_cmp_gt_u32 vcc, %[sp], %[d]\n\t"
+            "v_addc_co_u32 %[r], vcc, %[r], %[r], vcc"
+            : [r] "+v"(r), [d] "=&v"(d)
+            : [w] "v"(f), [lo] "s"(LO), [sp] "s"(SPAN)
+            : "vcc");
+      }
     }
   }
   return r;
 }
 
-template <int B>
+template <int B, int P>
 __device__ __forceinline__ uint32_t conj_set(const PHIP_LDS uint32_t *wl, uint32_t s, uint64_t set) {
+  constexpr int NK = kTileGroups / P;
+  constexpr int STRIDE = 2 * P * B;
+  constexpr int NB = NK < 8 ? NK : 8;
   uint32_t r = 0;
 #pragma unroll
-  for (int g0 = 0; g0 < kTileGroups; g0 += 8) {
-    uint32_t x[8], y[8];
+  for (int k0 = 0; k0 < NK; k0 += NB) {
+    uint32_t x[NB], y[NB];
 #pragma unroll
-    for (int g = 0; g < 8; g++) {
-      x[g] = wl[(g0 + g) * 2 * B];
-      y[g] = wl[(g0 + g) * 2 * B + 1];
+    for (int k = 0; k < NB; k++) {
+      x[k] = wl[(k0 + k) * STRIDE];
+      y[k] = wl[(k0 + k) * STRIDE + 1];
     }
 #pragma unroll
-    for (int g = 0; g < 8; g++) {
-      const uint32_t win = __builtin_amdgcn_alignbit(x[g], y[g], s);
-      r = r + r + (uint32_t)((set >> (win >> (32 - B))) & 1ull);
+    for (int k = 0; k < NB; k++) {
+      const uint32_t win = __builtin_amdgcn_alignbit(x[k], y[k], s);
+#pragma unroll
+      for (int j = 0; j < P; j++) {
+        const uint32_t f = j == 0 ? win : (win << (j * B));
+        r = r + r + (uint32_t)((set >> (f >> (32 - B))) & 1ull);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (registers -> resident waves)
   }
@@ -326,21 +341,30 @@ __device__ __forceinline__ uint32_t conj_set(const PHIP_LDS uint32_t *wl, uint32
   X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
   X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
 
+// The lane's first word and window shift are computed once from the runtime width, so the
+// specialisations share them instead of each hoisting its own copy out of the tile loop.
+template <int P>
 __device__ __forceinline__ uint32_t conj_leaf_eval(const PHIP_LDS uint32_t *w, int bits, int kind, uint32_t lo,
                                                 uint32_t span, uint64_t set) {
-  const int32_t p = lane_id() * bits;
+  const int32_t p = lane_id() * P * bits;
   const int32_t q = (p - 1) >> 5;
   const uint32_t s = (uint32_t)(32 * (q + 1) - p);
   const PHIP_LDS uint32_t *wl = w + q;
   if (kind == 0) {
     switch (bits) {
-#define PHIP_RC(b) case b: return conj_range<b>(wl, s, lo, span);
+#define PHIP_RC(b)                                                     \
+  case b:                                                              \
+    if constexpr (b * P <= 32) return conj_range<b, P>(wl, s, lo, span); \
+    break;
       PHIP_B_CASES(PHIP_RC)
 #undef PHIP_RC
     }
   } else {
     switch (bits) {
-#define PHIP_SC(b) case b: return conj_set<b>(wl, s, set);
+#define PHIP_SC(b)                                                \
+  case b:                                                         \
+    if constexpr (b * P <= 32) return conj_set<b, P>(wl, s, set); \
+    break;
       PHIP_B_CASES(PHIP_SC)
 #undef PHIP_SC
     }
@@ -348,15 +372,48 @@ __device__ __forceinline__ uint32_t conj_leaf_eval(const PHIP_LDS uint32_t *w, i
   return 0;
 }
 
-__device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_t *slot, uint32_t valid) {
-  uint32_t r = valid;
+// P-layout word -> lane-major word (bit 31-g of lane L = doc 64g + L). Group g = kP + c of lane L comes
+// from lane (64/P)c + L/P, bit index kP + (L % P): one ds_bpermute per c, then a mask and a shift.
+template <int P>
+__device__ __forceinline__ uint32_t to_lane_major(uint32_t r) {
+  if constexpr (P == 1) {
+    return r;
+  } else {
+    const int L = lane_id();
+    const int j = L & (P - 1);
+    constexpr uint32_t kBase = P == 2 ? 0xAAAAAAAAu : (P == 4 ? 0x88888888u : 0x80808080u);
+    const uint32_t mj = kBase >> j;  // bits with index = j (mod P), index 0 = bit 31
+    uint32_t out = 0;
+#pragma unroll
+    for (int c = 0; c < P; c++) {
+      const int src = (64 / P) * c + (L / P);
+      const uint32_t t = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)r) & mj;
+      const int d = c - j;
+      out |= d >= 0 ? (t >> d) : (t << (-d));
+    }
+    return out;
+  }
+}
+
+template <int P>
+__device__ __forceinline__ uint32_t eval_conj_p(cseg_t &seg, const PHIP_LDS uint8_t *slot) {
+  uint32_t r = ~0u;
   const int k = seg.conj;
   for (int i = 0; i < k; i++) {
     if (i > 0 && ballot(r != 0) == 0) break;  // every doc already rejected (AndDocIdSet short-circuit)
     const PHIP_CAS ConjLeaf &L = seg.conj_leaf[i];
-    r &= conj_leaf_eval((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.kind, L.lo, L.span, L.set_mask);
+    r &= conj_leaf_eval<P>((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.kind, L.lo, L.span, L.set_mask);
   }
-  return r;
+  return to_lane_major<P>(r);
+}
+
+__device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_t *slot, uint32_t valid) {
+  switch (seg.conj_p) {
+    case 8: return valid & eval_conj_p<8>(seg, slot);
+    case 4: return valid & eval_conj_p<4>(seg, slot);
+    case 2: return valid & eval_conj_p<2>(seg, slot);
+    default: return valid & eval_conj_p<1>(seg, slot);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -383,10 +440,22 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);
-  const int64_t waves_total = (int64_t)gridDim.x * kFilterWaves;
-  const int64_t gw = (int64_t)blockIdx.x * kFilterWaves + wave;
-  const int begin = (int)((int64_t)q.total_work * gw / waves_total);
-  const int end = (int)((int64_t)q.total_work * (gw + 1) / waves_total);
+  int begin, end, step;
+  if (q.xcd_walk) {
+    // XCD sweep (grid is a multiple of 8): the work list is cut into 8 ranges, one per XCD, and an
+    // XCD's waves stride through its range together, so at any time they read neighbouring tiles
+    const int x = blockIdx.x & 7, gx = gridDim.x >> 3;
+    begin = (int)((int64_t)q.total_work * x / 8) + (int)(blockIdx.x >> 3) * kFilterWaves + wave;
+    end = (int)((int64_t)q.total_work * (x + 1) / 8);
+    step = gx * kFilterWaves;
+  } else {
+    // contiguous range per wave
+    const int64_t waves_total = (int64_t)gridDim.x * kFilterWaves;
+    const int64_t gw = (int64_t)blockIdx.x * kFilterWaves + wave;
+    begin = (int)((int64_t)q.total_work * gw / waves_total);
+    end = (int)((int64_t)q.total_work * (gw + 1) / waves_total);
+    step = 1;
+  }
   const int nbuf = q.nbuf;
   const int stride = q.stage_stride;
   PHIP_LDS uint8_t *ring = (PHIP_LDS uint8_t *)(smem + (size_t)wave * nbuf * stride);
@@ -406,7 +475,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     const int k = stage_tile(segs[sn], segs[sn].tile0 + (pf - segs[sn].work_begin), ring + slot * stride);
     vm.issued(k);
     vm.start(slot);
-    pf++;
+    pf += step;
   };
   int pslot = 0;
   for (int i = 0; i < nbuf - 1 && pf < end; i++) {
@@ -417,7 +486,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   int si = -1;  // segment of the current tile
   int seg_end = -1;
   int slot = 0;
-  for (int t = begin; t < end; t++) {
+  for (int t = begin; t < end; t += step) {
     if (pf < end) {
       prefetch(pslot);
       pslot = pslot + 1 == nbuf ? 0 : pslot + 1;

@@ -213,6 +213,10 @@ struct Device {
     int32_t type = 0;
     int32_t width = 0;
     std::vector<uint8_t> values;  // LE typed or fixed-width strings
+    ~Remap() {
+      for (auto *p : dev)
+        if (p) (void)hipFree(p);
+    }
   };
   std::map<std::string, std::shared_ptr<Remap>> remaps;
 };
@@ -246,11 +250,20 @@ struct Segment {
   std::unordered_map<std::string, int> by_name;
   uint64_t device_bytes = 0;
   std::vector<void *> allocations;
+  ~Segment() {
+    (void)hipSetDevice(device);
+    for (void *p : allocations) (void)hipFree(p);
+    for (auto &c : cols)
+      for (auto &kv : c.hll) (void)hipFree(kv.second);
+  }
 };
 
 static std::mutex g_mu;  // guards the registries below
 static std::vector<std::unique_ptr<Device>> g_devices;
-static std::unordered_map<uint64_t, std::unique_ptr<Segment>> g_segments;
+// Segments are shared with the plans that reference them: unloading drops the registry's reference
+// and the HBM is released when the last prepared plan over the segment is destroyed (the role of the
+// Phaser guard in BaseCombineOperator.java:87-92).
+static std::unordered_map<uint64_t, std::shared_ptr<Segment>> g_segments;
 static std::atomic<uint64_t> g_next_handle{1};
 
 static int32_t ensure_devices_locked() {
@@ -711,14 +724,67 @@ int acc_kind_for(const phip_aggregation &a, bool integral) {
 
 }  // namespace
 
-static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uint64_t *filter_words,
-                         int64_t filter_nwords) {
+// A prepared query (InstancePlanMakerImplV2.makeInstancePlan's Plan, executed like
+// GlobalPlanImplV0.execute, pinot-core/.../plan/GlobalPlanImplV0.java:48-57): every host-side step
+// (predicate programs, segment descriptors, launch shapes) is done once; the device-side descriptor
+// blob and every buffer the launches touch are owned by the plan, so an execution is a replay of the
+// same launch sequence (a captured hipGraph from the second execution on).
+struct Plan {
+  Device *dev = nullptr;
+  std::vector<std::shared_ptr<Segment>> segs;  // keeps the segments' HBM alive while the plan exists
+  std::vector<void *> allocs;
+  int32_t alloc(size_t bytes, void **out) {
+    void *p = nullptr;
+    HIP_TRY(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+    allocs.push_back(p);
+    *out = p;
+    return PHIP_OK;
+  }
+  ~Plan() {
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    if (dev) (void)hipSetDevice(dev->ordinal);
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (void *p : allocs) (void)hipFree(p);
+    if (pinned) (void)hipHostFree(pinned);
+  }
+  // configuration
+  DevAggQuery dq;
+  DevFilter fq;
+  std::vector<DevSeg> dsegs;
+  std::vector<RoaringTask> tasks;
+  std::vector<std::shared_ptr<Device::Remap>> gb_dicts;
+  int nseg = 0, naggs = 0, nhll = 0, log2m = 0, m_regs = 0, num_group_by = 0, num_projected = 0;
+  int64_t num_groups_limit = 0, total_work = 0, total_docs = 0, docs_in_work = 0;
+  bool has_filter = false, need_agg = false, need_mask = false, group_by = false, conj_only = false;
+  bool want_bitmap = false;
+  int64_t filter_nwords = 0;
+  int filter_blocks = 1, agg_blocks = 8;
+  size_t filter_lds = 0, agg_lds = 0;
+  // device buffers (plan-owned)
+  uint8_t *base = nullptr;  // descriptor blob
+  size_t tasks_off = 0, dq_off = 0, kinds_off = 0;
+  void *inv_words = nullptr;
+  size_t inv_words_total = 0;
+  void *fpart = nullptr, *finals = nullptr, *seg_matched = nullptr, *apart = nullptr, *masks = nullptr;
+  void *gtab = nullptr, *ghll = nullptr, *slab = nullptr, *hslab = nullptr, *fo = nullptr;
+  // pinned host landing area for the per-execution results: finals[64] | seg_matched[nseg] | hll
+  uint64_t *pinned = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  bool graph_failed = false;
+  int executions = 0;
+  // per-plan timing events (recorded by every eager run and by every replay of the captured graph)
+  hipEvent_t ev[4] = {};
+};
+
+static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
+
   if (!q || q->num_segments <= 0 || q->num_columns < 0 || q->num_columns > kMaxQueryColumns)
     return fail(PHIP_ERR_INVALID, "query: need >=1 segment and <= %d columns", kMaxQueryColumns);
   if (q->num_aggregations < 0 || q->num_aggregations > kMaxAggs)
     return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d aggregations on the GPU path", kMaxAggs);
   if (q->num_group_by < 0 || q->num_group_by > 4) return fail(PHIP_ERR_UNSUPPORTED, "query: at most 4 group-by columns");
-  if (q->num_segments > 1 && filter_words) return fail(PHIP_ERR_INVALID, "filter bitmap: one segment only");
+  if (q->num_segments > 1 && want_bitmap) return fail(PHIP_ERR_INVALID, "filter bitmap: one segment only");
 
   std::vector<Segment *> segs(q->num_segments);
   Device *dev = nullptr;
@@ -728,6 +794,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       auto it = g_segments.find(q->segments[i]);
       if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle %llu", (unsigned long long)q->segments[i]);
       segs[i] = it->second.get();
+      P.segs.push_back(it->second);
       if (i > 0 && segs[i]->device != segs[0]->device)
         return fail(PHIP_ERR_UNSUPPORTED, "segments of one query must reside on one device");
     }
@@ -737,6 +804,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   std::lock_guard<std::mutex> dlock(dev->mu);
   HIP_TRY(hipSetDevice(dev->ordinal));
   hipStream_t st = dev->stream;
+  P.dev = dev;
 
   const int nseg = q->num_segments, ncols = q->num_columns, naggs = q->num_aggregations;
   // resolve columns
@@ -1084,7 +1152,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   }
   void *inv_words = nullptr;
   if (inv_words_total) {
-    int32_t rc = dev->ws.get("inv_words", inv_words_total * 8, &inv_words);
+    int32_t rc = P.alloc(inv_words_total * 8, &inv_words);
     if (rc) return rc;
   }
   for (size_t i = 0; i < inv_leaves.size(); i++) {
@@ -1119,7 +1187,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   for (const DevSeg &ds : dsegs) has_filter |= ds.node_end > ds.node_begin;
   bool need_agg = group_by;
   for (int a = 0; a < naggs; a++) need_agg |= dq.aggs[a].acc != ACC_COUNT;
-  const bool need_mask = has_filter && (need_agg || filter_words != nullptr);
+  const bool need_mask = has_filter && (need_agg || want_bitmap);
   const int64_t kSlotBudget = 19 * 1024;  // bytes per ring slot
   int32_t stage_stride = 0;
   for (DevSeg &ds : dsegs) {
@@ -1183,7 +1251,12 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       std::stable_sort(conj.begin(), conj.end(),
                        [](const std::pair<double, ConjLeaf> &a, const std::pair<double, ConjLeaf> &b) { return a.first < b.first; });
       ds.conj = (int32_t)conj.size();
-      for (size_t i = 0; i < conj.size(); i++) ds.conj_leaf[i] = conj[i].second;
+      ds.conj_p = 8;
+      for (size_t i = 0; i < conj.size(); i++) {
+        ds.conj_leaf[i] = conj[i].second;
+        while (ds.conj_p > 1 && ds.conj_p * conj[i].second.bits > 32) ds.conj_p >>= 1;
+      }
+      if (const char *e = getenv("PHIP_CONJ_P")) ds.conj_p = std::min(ds.conj_p, std::max(1, atoi(e)));  // measurement override
     }
   }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
@@ -1206,8 +1279,11 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     if (nbuf < 2) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
   }
   const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride;
-  const int filter_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)dev->num_cus * fbpc,
-                                                                        ceil_div(total_work, kFilterWaves)));
+  const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "contig"
+  const bool xcd_walk = walk_env ? strcmp(walk_env, "xcd") == 0 : false;  // contig measured faster
+  int filter_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)dev->num_cus * fbpc,
+                                                                  ceil_div(total_work, kFilterWaves)));
+  if (xcd_walk) filter_blocks = (int)round_up(std::max(filter_blocks, 8), 8);
 
   // ---- aggregation kernel configuration (aggregate.hip) -----------------------------------------
   dq.log2m = log2m;
@@ -1243,14 +1319,13 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   const size_t dq_off = blob.reserve(sizeof(DevAggQuery));  // written once every pointer is known
 
   void *dblob;
-  int32_t rc = dev->ws.get("blob", blob.data.size() + 64, &dblob);
+  int32_t rc = P.alloc(blob.data.size() + 64, &dblob);
   if (rc) return rc;
   uint8_t *base = (uint8_t *)dblob;
   for (auto &f : aux_fix) nodes[f.node].aux = base + f.off;
   if (!nodes.empty()) memcpy(blob.data.data() + nodes_off, nodes.data(), nodes.size() * sizeof(DevNode));
   if (!dsegs.empty()) memcpy(blob.data.data() + segs_off, dsegs.data(), sizeof(DevSeg) * dsegs.size());
   const DevSeg *dev_segs = (const DevSeg *)(base + segs_off);
-  const int32_t *dev_kinds = (const int32_t *)(base + kinds_off);
 
   DevFilter fq;
   memset(&fq, 0, sizeof(fq));
@@ -1260,44 +1335,44 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   fq.total_work = (int32_t)total_work;
   fq.stage_stride = stage_stride;
   fq.nbuf = nbuf;
+  fq.xcd_walk = xcd_walk ? 1 : 0;
   dq.segs = dev_segs;
 
   void *fpart, *finals, *seg_matched, *apart = nullptr, *masks = nullptr;
-  rc = dev->ws.get("filter_partials", (size_t)filter_blocks * 2 * 8, &fpart);
+  rc = P.alloc((size_t)filter_blocks * 2 * 8, &fpart);
   if (rc) return rc;
-  rc = dev->ws.get("finals", 64 * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
+  rc = P.alloc(64 * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
   if (rc) return rc;
-  rc = dev->ws.get("seg_matched", (size_t)nseg * 8, &seg_matched);
+  rc = P.alloc((size_t)nseg * 8, &seg_matched);
   if (rc) return rc;
   fq.partials = (uint64_t *)fpart;
   fq.seg_matched = (uint64_t *)seg_matched;
-  uint64_t *fin_agg = (uint64_t *)finals;          // [naggs]
-  uint64_t *fin_filter = (uint64_t *)finals + 32;  // [2]: matched, entries scanned
+  // finals: [0, naggs) aggregation slots, [32, 34) matched docs + entries scanned in filter
   dq.hll_regs = (uint32_t *)((uint8_t *)finals + 64 * 8);
   if (need_mask) {
-    rc = dev->ws.get("masks", (size_t)std::max<int64_t>(total_work, 1) * 64 * 4, &masks);
+    rc = P.alloc((size_t)std::max<int64_t>(total_work, 1) * 64 * 4, &masks);
     if (rc) return rc;
     fq.mask_out = (uint32_t *)masks;
     dq.mask = (const uint32_t *)masks;
   }
   if (need_agg && !group_by) {
-    rc = dev->ws.get("agg_partials", (size_t)agg_blocks * std::max(naggs, 1) * 8, &apart);
+    rc = P.alloc((size_t)agg_blocks * std::max(naggs, 1) * 8, &apart);
     if (rc) return rc;
     dq.partials = (uint64_t *)apart;
   }
   void *gtab = nullptr, *ghll = nullptr, *slab = nullptr, *hslab = nullptr;
   if (group_by) {
-    rc = dev->ws.get("gb_table", (size_t)(1 + naggs) * dq.num_groups * 8, &gtab);
+    rc = P.alloc((size_t)(1 + naggs) * dq.num_groups * 8, &gtab);
     if (rc) return rc;
     if (nhll) {
-      rc = dev->ws.get("gb_hll", (size_t)nhll * dq.num_groups * m_regs * 4, &ghll);
+      rc = P.alloc((size_t)nhll * dq.num_groups * m_regs * 4, &ghll);
       if (rc) return rc;
     }
     if (dq.mode == GB_LDS) {
-      rc = dev->ws.get("gb_slab", (size_t)agg_blocks * dq.tbl_words * 8 + 16, &slab);
+      rc = P.alloc((size_t)agg_blocks * dq.tbl_words * 8 + 16, &slab);
       if (rc) return rc;
       if (nhll) {
-        rc = dev->ws.get("gb_hslab", (size_t)agg_blocks * dq.hll_words * 4 + 16, &hslab);
+        rc = P.alloc((size_t)agg_blocks * dq.hll_words * 4 + 16, &hslab);
         if (rc) return rc;
       }
       dq.gb_table = (uint64_t *)slab;
@@ -1308,16 +1383,93 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     }
   }
   void *fo = nullptr;
-  if (filter_words) {
-    rc = dev->ws.get("filter_out", (size_t)filter_nwords * 8 + 4096 * 8, &fo);
+  if (want_bitmap) {
+    rc = P.alloc((size_t)filter_nwords * 8 + 4096 * 8, &fo);
     if (rc) return rc;
   }
 
   memcpy(blob.data.data() + dq_off, &dq, sizeof(dq));
-
-  // ---- launch ---------------------------------------------------------------------------------
-  HIP_TRY(hipEventRecord(dev->ev[0], st));
+  // the descriptor blob goes up once, synchronously (its host copy dies with this function)
   HIP_TRY(hipMemcpyAsync(dblob, blob.data.data(), blob.data.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+
+  P.dq = dq;
+  P.fq = fq;
+  P.dsegs = dsegs;
+  P.tasks = tasks;
+  P.gb_dicts = gb_dicts;
+  P.nseg = nseg;
+  P.naggs = naggs;
+  P.nhll = nhll;
+  P.log2m = log2m;
+  P.m_regs = m_regs;
+  P.num_group_by = q->num_group_by;
+  P.num_projected = num_projected;
+  P.num_groups_limit = q->num_groups_limit;
+  P.total_work = total_work;
+  P.total_docs = total_docs;
+  P.docs_in_work = 0;
+  for (const DevSeg &ds : dsegs) P.docs_in_work += ds.num_docs;
+  P.has_filter = has_filter;
+  P.need_agg = need_agg;
+  P.need_mask = need_mask;
+  P.group_by = group_by;
+  P.conj_only = conj_only;
+  P.want_bitmap = want_bitmap;
+  P.filter_nwords = filter_nwords;
+  P.filter_blocks = filter_blocks;
+  P.agg_blocks = agg_blocks;
+  P.filter_lds = filter_lds;
+  P.agg_lds = agg_lds;
+  P.base = base;
+  P.tasks_off = tasks_off;
+  P.dq_off = dq_off;
+  P.kinds_off = kinds_off;
+  P.inv_words = inv_words;
+  P.inv_words_total = inv_words_total;
+  P.fpart = fpart;
+  P.finals = finals;
+  P.seg_matched = seg_matched;
+  P.apart = apart;
+  P.masks = masks;
+  P.gtab = gtab;
+  P.ghll = ghll;
+  P.slab = slab;
+  P.hslab = hslab;
+  P.fo = fo;
+  for (auto &e : P.ev) HIP_TRY(hipEventCreate(&e));
+  {
+    void *h = nullptr;
+    const size_t pbytes = (64 + (size_t)nseg) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4;
+    HIP_TRY(hipHostMalloc(&h, pbytes, hipHostMallocDefault));
+    memset(h, 0, pbytes);
+    P.pinned = (uint64_t *)h;
+  }
+  return PHIP_OK;
+}
+
+// The device work of one execution, on `st` (eager, or recorded into a graph by stream capture).
+static int32_t enqueue_plan(Plan &P, hipStream_t st) {
+  DevAggQuery &dq = P.dq;
+  DevFilter &fq = P.fq;
+  const int nseg = P.nseg, naggs = P.naggs, nhll = P.nhll, m_regs = P.m_regs;
+  const bool group_by = P.group_by, has_filter = P.has_filter, need_agg = P.need_agg, need_mask = P.need_mask;
+  const bool conj_only = P.conj_only;
+  const int64_t total_work = P.total_work;
+  uint8_t *base = P.base;
+  const int32_t *dev_kinds = (const int32_t *)(base + P.kinds_off);
+  uint64_t *fin_agg = (uint64_t *)P.finals;
+  uint64_t *fin_filter = (uint64_t *)P.finals + 32;
+  void *seg_matched = P.seg_matched, *inv_words = P.inv_words, *gtab = P.gtab, *ghll = P.ghll;
+  void *fpart = P.fpart, *apart = P.apart, *slab = P.slab, *hslab = P.hslab, *masks = P.masks, *fo = P.fo;
+  const size_t inv_words_total = P.inv_words_total, tasks_off = P.tasks_off, dq_off = P.dq_off;
+  const std::vector<RoaringTask> &tasks = P.tasks;
+  const std::vector<DevSeg> &dsegs = P.dsegs;
+  const int filter_blocks = P.filter_blocks, agg_blocks = P.agg_blocks;
+  const size_t filter_lds = P.filter_lds, agg_lds = P.agg_lds;
+  const int64_t filter_nwords = P.filter_nwords;
+  const bool filter_words = P.want_bitmap;
+  HIP_TRY(hipEventRecord(P.ev[0], st));
   HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)nseg * 8, st));
   if (filter_words) HIP_TRY(hipMemsetAsync(fo, 0, (size_t)filter_nwords * 8, st));
   if (nhll && !group_by) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, (size_t)nhll * m_regs * 4, st));
@@ -1334,10 +1486,10 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     }
     if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
-  HIP_TRY(hipEventRecord(dev->ev[1], st));
+  HIP_TRY(hipEventRecord(P.ev[1], st));
   if (has_filter && total_work > 0) HIP_TRY(launch_filter(fq, conj_only, filter_blocks, filter_lds, st));
   if (need_agg && total_work > 0) HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
-  HIP_TRY(hipEventRecord(dev->ev[2], st));
+  HIP_TRY(hipEventRecord(P.ev[2], st));
   if (has_filter && total_work > 0)
     HIP_TRY(launch_finalize_partials((const uint64_t *)fpart, filter_blocks, 2, dev_kinds + naggs, fin_filter, st));
   if (need_agg && !group_by && total_work > 0)
@@ -1352,23 +1504,71 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
     HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
                                   filter_nwords, st));
 
+  // results land in the plan's pinned buffer: finals[64] | seg_matched[nseg] | hll registers
+  uint64_t *pin = P.pinned;
+  if (total_work > 0) HIP_TRY(hipMemcpyAsync(pin, P.finals, 64 * 8, hipMemcpyDeviceToHost, st));
+  if (has_filter) HIP_TRY(hipMemcpyAsync(pin + 64, seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
+  if (nhll && !group_by)
+    HIP_TRY(hipMemcpyAsync(pin + 64 + nseg, dq.hll_regs, ((size_t)nhll << P.log2m) * 4, hipMemcpyDeviceToHost, st));
+  if (!group_by) HIP_TRY(hipEventRecord(P.ev[3], st));
+  (void)fin_agg;
+  (void)fo;
+  return PHIP_OK;
+}
+
+static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_words) {
+  Device *dev = P.dev;
+  std::lock_guard<std::mutex> dlock(dev->mu);
+  HIP_TRY(hipSetDevice(dev->ordinal));
+  hipStream_t st = dev->stream;
+  // Opt-in (PHIP_GRAPH=1): replay a captured hipGraph from the second execution on. Measured on
+  // MI355X it saves nothing once the plan is prepared (host time per execution is ~50 us either way),
+  // and event records inside a replayed graph did not give trustworthy kernel times, so eager is the
+  // default. Group-by needs a host step mid-way and always runs eager.
+  const bool graphable = !P.group_by && !filter_words && getenv("PHIP_GRAPH") != nullptr;
+  if (graphable && P.executions >= 1 && !P.graph_exec && !P.graph_failed) {
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    int32_t rc = ok ? enqueue_plan(P, st) : PHIP_ERR_HIP;
+    hipError_t e = hipStreamEndCapture(st, &g);
+    if (ok && rc == PHIP_OK && e == hipSuccess && g &&
+        hipGraphInstantiate(&P.graph_exec, g, nullptr, nullptr, 0) == hipSuccess) {
+      (void)hipGraphDestroy(g);
+    } else {
+      if (g) (void)hipGraphDestroy(g);
+      P.graph_exec = nullptr;
+      P.graph_failed = true;
+      (void)hipGetLastError();
+    }
+  }
+  if (P.graph_exec) {
+    HIP_TRY(hipGraphLaunch(P.graph_exec, st));
+  } else {
+    int32_t rc = enqueue_plan(P, st);
+    if (rc) return rc;
+  }
+  P.executions++;
+  DevAggQuery &dq = P.dq;
+  const int nseg = P.nseg, naggs = P.naggs, nhll = P.nhll, log2m = P.log2m, m_regs = P.m_regs;
+  const bool group_by = P.group_by, has_filter = P.has_filter, need_agg = P.need_agg;
+  const int64_t total_work = P.total_work, total_docs = P.total_docs, docs_in_work = P.docs_in_work;
+  const int num_projected = P.num_projected;
+  const int64_t filter_nwords = P.filter_nwords;
+  const int32_t *dev_kinds = (const int32_t *)(P.base + P.kinds_off);
+  void *gtab = P.gtab, *ghll = P.ghll;
+  const std::vector<DevSeg> &dsegs = P.dsegs;
+  const std::vector<std::shared_ptr<Device::Remap>> &gb_dicts = P.gb_dicts;
+  int32_t rc = PHIP_OK;
+  if (filter_words && P.need_mask)
+    HIP_TRY(hipMemcpyAsync(filter_words, P.fo, (size_t)filter_nwords * 8, hipMemcpyDeviceToHost, st));
+
   auto impl = std::make_unique<ResultImpl>();
   phip_result &r = impl->pub;
   memset(&r, 0, sizeof(r));
-  std::vector<uint64_t> fin(64, 0);
-  std::vector<uint64_t> segm(nseg, 0);
-  std::vector<uint32_t> hll_host;
-  if (total_work > 0) HIP_TRY(hipMemcpyAsync(fin.data(), finals, 64 * 8, hipMemcpyDeviceToHost, st));
-  if (has_filter) HIP_TRY(hipMemcpyAsync(segm.data(), seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
-  if (nhll && !group_by) {
-    hll_host.resize((size_t)nhll << log2m);
-    HIP_TRY(hipMemcpyAsync(hll_host.data(), dq.hll_regs, hll_host.size() * 4, hipMemcpyDeviceToHost, st));
-  }
-  if (filter_words) HIP_TRY(hipMemcpyAsync(filter_words, fo, (size_t)filter_nwords * 8, hipMemcpyDeviceToHost, st));
+  const uint64_t *fin = P.pinned;
+  const uint64_t *segm = P.pinned + 64;
+  const uint32_t *hll_host = (const uint32_t *)(P.pinned + 64 + nseg);
 
-  // matched docs: the filter kernel's count, or every doc of every segment with work when unfiltered
-  int64_t docs_in_work = 0;
-  for (const DevSeg &ds : dsegs) docs_in_work += ds.num_docs;
   int64_t ngroups = 1;
   if (group_by) {
     const int64_t nchunks = ceil_div(dq.num_groups, 1024);
@@ -1408,20 +1608,19 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       }
       if (nhll) HIP_TRY(hipMemcpyAsync(impl->hll.data(), oh, impl->hll.size(), hipMemcpyDeviceToHost, st));
     }
-    HIP_TRY(hipEventRecord(dev->ev[3], st));
+    HIP_TRY(hipEventRecord(P.ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
-    impl->keys.resize(ngroups * q->num_group_by);
+    impl->keys.resize(ngroups * P.num_group_by);
     for (int64_t g = 0; g < ngroups; g++) {
       int64_t key = hkeys[g];
-      for (int k = 0; k < q->num_group_by; k++) {
-        impl->keys[g * q->num_group_by + k] = (int32_t)(key % gb_dicts[k]->card);
+      for (int k = 0; k < P.num_group_by; k++) {
+        impl->keys[g * P.num_group_by + k] = (int32_t)(key % gb_dicts[k]->card);
         key /= gb_dicts[k]->card;
       }
     }
     impl->dicts = gb_dicts;
-    if (q->num_groups_limit > 0 && ngroups > q->num_groups_limit) r.num_groups_limit_reached = 1;
+    if (P.num_groups_limit > 0 && ngroups > P.num_groups_limit) r.num_groups_limit_reached = 1;
   } else {
-    HIP_TRY(hipEventRecord(dev->ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
   }
   const int64_t matched = has_filter ? (int64_t)fin[32] : docs_in_work;
@@ -1454,11 +1653,11 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
       impl->values[a] = d;
       impl->longs[a] = l;
     }
-    for (size_t i = 0; i < hll_host.size(); i++) impl->hll[i] = (uint8_t)hll_host[i];
+    if (nhll) for (size_t i = 0; i < ((size_t)nhll << log2m); i++) impl->hll[i] = (uint8_t)hll_host[i];
   }
   float t_all = 0.f, t_scan = 0.f;
-  HIP_TRY(hipEventElapsedTime(&t_all, dev->ev[0], dev->ev[3]));
-  HIP_TRY(hipEventElapsedTime(&t_scan, dev->ev[1], dev->ev[2]));
+  HIP_TRY(hipEventElapsedTime(&t_all, P.ev[0], P.ev[3]));
+  HIP_TRY(hipEventElapsedTime(&t_scan, P.ev[1], P.ev[2]));
 
   r.num_docs_scanned = matched;
   r.num_entries_scanned_in_filter = has_filter ? (int64_t)fin[33] : 0;
@@ -1472,7 +1671,7 @@ static int32_t run_query(const phip_query_desc *q, phip_result **out_result, uin
   }
   r.num_aggregations = naggs;
   r.num_groups = group_by ? ngroups : 1;
-  r.num_group_by = q->num_group_by;
+  r.num_group_by = P.num_group_by;
   r.num_hll = nhll;
   r.values = impl->values.data();
   r.long_values = impl->longs.data();
@@ -1520,25 +1719,17 @@ PHIP_API int32_t phip_init(const int32_t *devices, int32_t num_devices) {
   return PHIP_OK;
 }
 
-static void free_segment(Segment &s) {
-  (void)hipSetDevice(s.device);
-  for (void *p : s.allocations) (void)hipFree(p);
-  for (auto &c : s.cols)
-    for (auto &kv : c.hll) (void)hipFree(kv.second);
-  s.allocations.clear();
-}
+static std::unordered_map<uint64_t, std::unique_ptr<Plan>> g_plans;  // guarded by g_mu
+static std::atomic<uint64_t> g_next_plan{1};
 
 PHIP_API int32_t phip_shutdown(void) {
   std::lock_guard<std::mutex> g(g_mu);
-  for (auto &kv : g_segments) free_segment(*kv.second);
+  g_plans.clear();
   g_segments.clear();
   for (auto &d : g_devices) {
     std::lock_guard<std::mutex> dl(d->mu);
     (void)hipSetDevice(d->ordinal);
     d->ws.release();
-    for (auto &kv : d->remaps)
-      for (auto *p : kv.second->dev)
-        if (p) (void)hipFree(p);
     d->remaps.clear();
     for (auto &e : d->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
@@ -1561,7 +1752,7 @@ PHIP_API int32_t phip_segment_load(const phip_segment_desc *desc, uint64_t *out_
   }
   std::lock_guard<std::mutex> dl(dev->mu);
   HIP_TRY(hipSetDevice(dev->ordinal));
-  auto seg = std::make_unique<Segment>();
+  auto seg = std::make_shared<Segment>();
   seg->device = dev->ordinal;
   seg->num_docs = desc->num_docs;
   seg->name = desc->name ? desc->name : "";
@@ -1577,10 +1768,7 @@ PHIP_API int32_t phip_segment_load(const phip_segment_desc *desc, uint64_t *out_
   hipError_t se = hipStreamSynchronize(dev->stream);
   for (void *p : temps) (void)hipFree(p);
   if (rc == PHIP_OK && se != hipSuccess) rc = fail(PHIP_ERR_HIP, "segment load: %s", hipGetErrorString(se));
-  if (rc != PHIP_OK) {
-    free_segment(*seg);
-    return rc;
-  }
+  if (rc != PHIP_OK) return rc;  // the partial segment frees itself
   seg->handle = g_next_handle++;
   *out_handle = seg->handle;
   std::lock_guard<std::mutex> g(g_mu);
@@ -1589,7 +1777,7 @@ PHIP_API int32_t phip_segment_load(const phip_segment_desc *desc, uint64_t *out_
 }
 
 PHIP_API int32_t phip_segment_unload(uint64_t handle) {
-  std::unique_ptr<Segment> seg;
+  std::shared_ptr<Segment> seg;
   {
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_segments.find(handle);
@@ -1603,17 +1791,10 @@ PHIP_API int32_t phip_segment_unload(uint64_t handle) {
     (void)hipSetDevice(dev->ordinal);
     (void)hipStreamSynchronize(dev->stream);
     for (auto it = dev->remaps.begin(); it != dev->remaps.end();) {
-      if (it->first.find(":" + std::to_string(handle)) != std::string::npos) {
-        for (auto *p : it->second->dev)
-          if (p) (void)hipFree(p);
-        it = dev->remaps.erase(it);
-      } else {
-        ++it;
-      }
+      if (it->first.find(":" + std::to_string(handle)) != std::string::npos) it = dev->remaps.erase(it);
+      else ++it;
     }
-    free_segment(*seg);
-  } else {
-    free_segment(*seg);
+    seg.reset();  // frees the HBM now unless a prepared plan still holds the segment
   }
   return PHIP_OK;
 }
@@ -1629,7 +1810,53 @@ PHIP_API int32_t phip_segment_device_bytes(uint64_t handle, uint64_t *out_bytes)
 PHIP_API int32_t phip_query(const phip_query_desc *query, phip_result **out_result) {
   if (!out_result) return fail(PHIP_ERR_INVALID, "null result pointer");
   *out_result = nullptr;
-  return run_query(query, out_result, nullptr, 0);
+  Plan plan;
+  int32_t rc = prepare_plan(query, false, 0, plan);
+  if (rc) return rc;
+  return execute_plan(plan, out_result, nullptr);
+}
+
+PHIP_API int32_t phip_plan_create(const phip_query_desc *query, uint64_t *out_plan) {
+  if (!out_plan) return fail(PHIP_ERR_INVALID, "null plan pointer");
+  *out_plan = 0;
+  auto plan = std::make_unique<Plan>();
+  int32_t rc = prepare_plan(query, false, 0, *plan);
+  if (rc) return rc;
+  const uint64_t h = g_next_plan++;
+  std::lock_guard<std::mutex> g(g_mu);
+  g_plans[h] = std::move(plan);
+  *out_plan = h;
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_plan_execute(uint64_t plan, phip_result **out_result) {
+  if (!out_result) return fail(PHIP_ERR_INVALID, "null result pointer");
+  *out_result = nullptr;
+  Plan *p;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_plans.find(plan);
+    if (it == g_plans.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown plan handle %llu", (unsigned long long)plan);
+    p = it->second.get();
+  }
+  return execute_plan(*p, out_result, nullptr);
+}
+
+PHIP_API int32_t phip_plan_destroy(uint64_t plan) {
+  std::unique_ptr<Plan> p;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_plans.find(plan);
+    if (it == g_plans.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown plan handle %llu", (unsigned long long)plan);
+    p = std::move(it->second);
+    g_plans.erase(it);
+  }
+  if (p && p->dev) {
+    std::lock_guard<std::mutex> dl(p->dev->mu);  // an execution on another thread finishes first
+    (void)hipSetDevice(p->dev->ordinal);
+    (void)hipStreamSynchronize(p->dev->stream);
+  }
+  return PHIP_OK;
 }
 
 PHIP_API int32_t phip_result_dictionary(const phip_result *result, int32_t k, phip_dictionary_view *out) {
@@ -1662,7 +1889,10 @@ PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *word
     if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle");
     if (num_words < ceil_div(it->second->num_docs, 64)) return fail(PHIP_ERR_INVALID, "words_out too small");
   }
-  rc = run_query(&q, &r, words_out, num_words);
+  Plan plan;
+  rc = prepare_plan(&q, true, num_words, plan);
+  if (rc) return rc;
+  rc = execute_plan(plan, &r, words_out);
   if (r) phip_result_free(r);
   return rc;
 }

@@ -303,14 +303,31 @@ class GpuCombineOperator:
         return out[:nwords]
 
     def run_raw(self):
-        # the descriptor is built once per operator and reused (plan reuse across executions)
-        if getattr(self, "_cached", None) is None:
+        """One execution of the prepared plan (phip_plan_create once per operator, then phip_plan_execute:
+        InstancePlanMakerImplV2's Plan run by GlobalPlanImplV0.execute)."""
+        lib = _lib.load()
+        if getattr(self, "_plan", None) is None:
             keep = []
-            self._cached = (self._desc(keep), keep)
-        q = self._cached[0]
+            q = self._desc(keep)
+            h = ctypes.c_uint64(0)
+            _lib.check(lib.phip_plan_create(ctypes.byref(q), ctypes.byref(h)))
+            self._plan = h.value
+            self._lib = lib
         res = ctypes.POINTER(_lib.Result)()
-        _lib.check(_lib.load().phip_query(ctypes.byref(q), ctypes.byref(res)))
+        _lib.check(lib.phip_plan_execute(self._plan, ctypes.byref(res)))
         return res
+
+    def close(self):
+        """Release the prepared plan (and with it the last references to unloaded segments)."""
+        if getattr(self, "_plan", None):
+            self._lib.phip_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     # -- NonScanBasedAggregationOperator (AggregationPlanNode.java:107-118, isFitForNonScanBasedPlan :165-190)
     _NON_SCAN = ("count", "min", "max", "minmaxrange", "distinctcounthll", "distinctcountrawhll")
@@ -423,6 +440,8 @@ class GpuCombineOperator:
             lib.phip_result_free(res)
 
     def _integral_sums(self):
+        if getattr(self, "_integral_cache", None) is not None:
+            return self._integral_cache
         out = {}
         for i, p in enumerate(self.prims):
             if p[0] != _lib.AGG_SUM:
@@ -433,6 +452,7 @@ class GpuCombineOperator:
                     if c is not None and not s.column_metadata(c).data_type.is_integral:
                         ok = False
             out[i] = ok
+        self._integral_cache = out
         return out
 
 

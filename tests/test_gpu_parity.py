@@ -246,3 +246,84 @@ def test_gpu_empty_result_and_tiny_segment(gpu_lib):
                 _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
     finally:
         seg.destroy()
+
+
+# ---- conjunctive fast path: mixed widths (P-layout windows of 1/2/4/8 docs), wide dictionaries -------
+@pytest.fixture(scope="module")
+def wide_segment(gpu_lib):
+    """600,003 docs; column wN has exactly N bits per value (card in (2^(N-1), 2^N])."""
+    rng = np.random.default_rng(20)
+    n = 600_003
+    c = SegmentCreator("wide")
+    for b in list(range(1, 10)) + [12, 16, 19, 20]:
+        card = min(n, (1 << (b - 1)) + 1 + int(rng.integers(0, 1 << (b - 1))))
+        v = rng.integers(0, card, n)
+        v[:card] = np.arange(card)  # every dictionary value present
+        rng.shuffle(v)
+        c.add_column(f"w{b}", DataType.INT, v * 7 - 3)
+    raw = c.build()
+    for b in list(range(1, 10)) + [12, 16, 19, 20]:
+        assert raw.columns[f"w{b}"].metadata.bits_per_element == b
+    seg = GpuSegment(raw)
+    yield raw, seg
+    seg.destroy()
+
+
+CONJ_CASES = [(1, 2, 3), (3, 4, 6), (4, 5, 7), (2, 9, 12), (3, 19, 5), (8, 8), (16, 2), (20, 1), (6, 7, 8, 9),
+              (1, 2, 3, 4, 5, 6)]
+
+
+@pytest.mark.parametrize("widths", CONJ_CASES, ids=lambda w: "w" + "_".join(map(str, w)))
+def test_gpu_conjunction_mixed_widths(widths, wide_segment):
+    raw, seg = wide_segment
+    rng = np.random.default_rng(sum(widths))
+    preds = []
+    for i, b in enumerate(widths):
+        card = raw.columns[f"w{b}"].metadata.cardinality
+        if b <= 6 and i % 2 == 1:  # a small-set (card <= 64) leaf
+            ids = sorted(set(rng.integers(0, card, 1 + card // 2).tolist()))
+            preds.append(f"w{b} IN ({', '.join(str(x * 7 - 3) for x in ids)})")
+        else:
+            lo = int(rng.integers(0, card))
+            hi = int(rng.integers(lo, card))
+            span = max(1, card // (2 if i == 0 else 1))
+            hi = min(card - 1, max(hi, lo + span // 2))
+            preds.append(f"w{b} BETWEEN {lo * 7 - 3} AND {hi * 7 - 3}")
+    qc = parse(f"SELECT COUNT(*), SUM(w{widths[0]}) FROM t WHERE " + " AND ".join(preds))
+    op = GpuInstancePlanMaker().make_instance_plan(qc, [seg])
+    expect = executor.filter_mask(qc, raw)
+    assert np.array_equal(op.filter_bitmap(), _words_from_mask(expect)), preds
+    blk = op.next_block()
+    oblk, ex = executor.execute(qc, [raw])
+    _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
+
+
+# ---- SSB queries (flattened lineorder, tools/ssbgen.c) vs the oracle: 3 segments, per-segment dicts ---
+SSB_NAMES = ["Q1.1", "Q1.2", "Q1.3", "Q2.1", "Q2.2", "Q2.3", "Q3.1", "Q3.2", "Q3.3", "Q3.4", "Q4.1", "Q4.2", "Q4.3", "C5"]
+
+
+@pytest.fixture(scope="module")
+def ssb_segments(gpu_lib):
+    from tools import ssb
+    cols = ssb.columns_for(SSB_NAMES)
+    raws = ssb.make_segments(1, cols, seed=7, segment_rows=2_000_000)
+    segs = [GpuSegment(r) for r in raws]
+    yield raws, segs
+    for s in segs:
+        s.destroy()
+
+
+@pytest.mark.parametrize("name", SSB_NAMES)
+def test_gpu_ssb_vs_oracle(name, ssb_segments):
+    from tools import ssb
+    raws, segs = ssb_segments
+    qc = parse(ssb.SSB_QUERIES[name])
+    gblk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
+    oblk, exact = executor.execute(qc, raws)
+    assert gblk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+    if not qc.group_by:
+        _assert_intermediates_equal(qc.aggregations, gblk.results, oblk.results, exact)
+    else:
+        assert set(gblk.groups) == set(oblk.groups)
+        for k, v in oblk.groups.items():
+            _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
