@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpinot_hip.so")
+LIB_PATH = os.environ.get("PHIP_LIB") or os.path.join(_HERE, "libpinot_hip.so")  # PHIP_LIB: A/B builds
 
 PHIP_OK = 0
 PHIP_ERR_INVALID = 1

@@ -68,6 +68,10 @@ __device__ __forceinline__ uint64_t wave_reduce_u64_add(uint64_t v) {
   }
   return v;
 }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return __builtin_amdgcn_readfirstlane(v);
+}
 __device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
   return __builtin_amdgcn_readfirstlane(v);

@@ -99,7 +99,8 @@ struct DevSeg {
   int32_t conj;        // > 0: the program is AND of `conj` staged scan leaves (conj_leaf, most selective
                        // first); the filter kernel evaluates it without the stack machine
   int32_t conj_p;      // docs per lane-window of the fast path (1, 2, 4, 8; P * bits <= 32 for every leaf)
-  int32_t pad2;
+  int32_t conj_sparse;  // 1: leaves 2.. are dict-id ranges, so a tile whose first leaf passes few docs
+                        // may test them per passing doc (SVScanDocIdIterator.applyAnd) instead of per doc
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
@@ -132,7 +133,7 @@ struct DevFilter {
   int32_t stage_stride;  // bytes of one ring slot (max over segments), multiple of 16
   int32_t nbuf;          // ring slots per wave (2..kMaxRing): nbuf-1 tiles in flight while one is evaluated
   int32_t xcd_walk;      // 1: XCD-sweep tile order (grid multiple of 8); 0: contiguous range per wave
-  int32_t pad;
+  int32_t min_dma;       // min over segments of LDS-DMA wave-instructions per tile (vmcnt lower bound)
   uint32_t *mask_out;    // optional: [total_work][64] lane-major tile masks
   uint64_t *partials;    // [num_blocks][2]: matched docs, entries scanned in filter
   uint64_t *seg_matched; // [num query segments]

@@ -6,8 +6,8 @@
 // 64-doc group is exactly 2b words of the u32 word layout, kernels.hip/runtime.cpp) and every
 // inverted leaf's 256 dense-word bytes arrive in the wave's LDS ring by LDS-DMA
 // (global_load_lds_dwordx4, 1 KiB per wave-instruction); nbuf-1 tiles are in flight while one is
-// evaluated, and completion is awaited with a counted vmcnt (the per-slot count of younger
-// vector-memory operations is kept packed in one wave-uniform u64).
+// evaluated, and completion is awaited with a counted vmcnt (a lower bound of the vector-memory
+// operations issued after the tile's DMA, kept in SGPRs together with the stage cursor).
 //
 // A tile's doc set is lane-major: lane l owns a 32-bit word whose bit (31-g) is doc 64g + l. Scan
 // leaves decode with lanes = docs of one 64-doc group at a time (one v_alignbit per doc and group),
@@ -25,33 +25,20 @@ namespace phip {
 // flight: it would otherwise put s_waitcnt vmcnt(0) in front of the first ds_read of the CURRENT
 // tile and drain the prefetch of the next ones. Completion is awaited by wait_vmcnt(n).
 // ------------------------------------------------------------------------------------------------
+#ifndef PHIP_DMA_POLICY
+#define PHIP_DMA_POLICY "nt"  // streamed once: non-temporal
+#endif
 __device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds_dst) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "global_load_lds_dwordx4 %1, off " PHIP_DMA_POLICY "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_dst)
       : "memory");
-}
-
-// Issue the LDS-DMA copies of one tile's staged regions; returns the number of wave-instructions.
-__device__ __forceinline__ int stage_tile(cseg_t &seg, int32_t tile_in_seg, PHIP_LDS uint8_t *buf) {
-  const int lane = lane_id();
-  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)buf);
-  const int ns = seg.num_stage;
-  for (int i = 0; i < ns; i++) {
-    const int32_t sbytes = seg.stage[i].bytes;
-    const uint8_t *g = seg.stage[i].base + (int64_t)tile_in_seg * sbytes + lane * 16;
-    const uint32_t l = lbase + (uint32_t)seg.stage[i].lds_off;
-    for (int c = 0; c < sbytes; c += 1024) {
-      if (c + lane * 16 < sbytes) dma16(g + c, l + (uint32_t)c);
-    }
-  }
-  return seg.num_dma;
 }
 
 struct Tile {
@@ -395,14 +382,69 @@ __device__ __forceinline__ uint32_t to_lane_major(uint32_t r) {
   }
 }
 
+// Leaves 2.. of a tile whose first leaf passed at most kSparseMax docs in every lane: each passing doc is
+// tested against the remaining range leaves on its own (one window read per leaf), the way
+// SVScanDocIdIterator.applyAnd (pinot-core/.../dociditerators/SVScanDocIdIterator.java:114-142) scans
+// only the candidate docs of the preceding AND children. Lanes loop over their set bits together.
+constexpr uint32_t kSparseMax = 6;
+
+template <int P>
+__device__ __forceinline__ uint32_t conj_sparse_rest(cseg_t &seg, const PHIP_LDS uint8_t *slot, uint32_t r) {
+  const int k = seg.conj;
+  int32_t off[kMaxConj - 1], bits[kMaxConj - 1];
+  uint32_t lo[kMaxConj - 1], span[kMaxConj - 1];
+#pragma unroll
+  for (int j = 0; j < kMaxConj - 1; j++) {
+    off[j] = 0;
+    bits[j] = 1;
+    lo[j] = 0;
+    span[j] = 0xffffffffu;
+    if (j + 1 < k) {
+      off[j] = seg.conj_leaf[j + 1].lds_off;
+      bits[j] = seg.conj_leaf[j + 1].bits;
+      lo[j] = seg.conj_leaf[j + 1].lo;
+      span[j] = seg.conj_leaf[j + 1].span;
+    }
+  }
+  const int lane = lane_id();
+  uint32_t todo = r;
+  while (ballot(todo != 0)) {
+    if (todo != 0) {
+      const int i = __builtin_clz(todo);
+      const uint32_t bit = 0x80000000u >> i;
+      todo &= ~bit;
+      const int32_t d = 64 * P * (i / P) + P * lane + (i % P);  // tile-relative doc of bit i (P-layout)
+      bool pass = true;
+#pragma unroll
+      for (int j = 0; j < kMaxConj - 1; j++) {
+        if (j + 1 < k) {
+          const uint32_t win = window_at((const PHIP_LDS uint32_t *)(slot + off[j]), d * bits[j]);
+          pass = pass && ((win - lo[j]) < span[j]);
+        }
+      }
+      if (!pass) r &= ~bit;
+    }
+  }
+  return r;
+}
+
 template <int P>
 __device__ __forceinline__ uint32_t eval_conj_p(cseg_t &seg, const PHIP_LDS uint8_t *slot) {
-  uint32_t r = ~0u;
   const int k = seg.conj;
-  for (int i = 0; i < k; i++) {
-    if (i > 0 && ballot(r != 0) == 0) break;  // every doc already rejected (AndDocIdSet short-circuit)
-    const PHIP_CAS ConjLeaf &L = seg.conj_leaf[i];
-    r &= conj_leaf_eval<P>((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.kind, L.lo, L.span, L.set_mask);
+  const PHIP_CAS ConjLeaf &L0 = seg.conj_leaf[0];
+  uint32_t r = conj_leaf_eval<P>((const PHIP_LDS uint32_t *)(slot + L0.lds_off), L0.bits, L0.kind, L0.lo, L0.span,
+                                 L0.set_mask);
+  if (k > 1) {
+    if (seg.conj_sparse && wave_max_u32((uint32_t)__popc(r)) <= kSparseMax) {
+      r = conj_sparse_rest<P>(seg, slot, r);
+    } else {
+      for (int i = 1; i < k; i++) {
+        if (ballot(r != 0) == 0) break;  // every doc already rejected (AndDocIdSet short-circuit)
+        const PHIP_CAS ConjLeaf &L = seg.conj_leaf[i];
+        r &= conj_leaf_eval<P>((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.kind, L.lo, L.span,
+                               L.set_mask);
+      }
+    }
   }
   return to_lane_major<P>(r);
 }
@@ -419,24 +461,66 @@ __device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_
 // ------------------------------------------------------------------------------------------------
 // the filter kernel
 // ------------------------------------------------------------------------------------------------
-// Per ring slot, the number of vector-memory instructions issued AFTER that slot's DMA (8 bits per
-// slot, packed; only slots with a tile in flight are counted).
-struct VmLedger {
-  uint64_t cnt = 0;     // byte s = younger ops of slot s
-  uint64_t active = 0;  // byte s = 0xff while slot s holds a tile in flight
-  __device__ __forceinline__ void issued(int k) {  // k more vector-memory instructions were issued
-    cnt += ((uint64_t)(uint32_t)k * 0x0101010101010101ull) & active;
+// s_waitcnt vmcnt(n) for a wave-uniform n. n > 14 waits for vmcnt(15), which is stricter and so safe.
+// (The count is forced into an SGPR, so this is a scalar branch tree, never a divergent one.)
+#define PHIP_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+__device__ __forceinline__ void wait_vmcnt_lb(int n) {
+  switch (__builtin_amdgcn_readfirstlane(n)) {
+    PHIP_VMW(0) PHIP_VMW(1) PHIP_VMW(2) PHIP_VMW(3) PHIP_VMW(4) PHIP_VMW(5) PHIP_VMW(6) PHIP_VMW(7)
+    PHIP_VMW(8) PHIP_VMW(9) PHIP_VMW(10) PHIP_VMW(11) PHIP_VMW(12) PHIP_VMW(13) PHIP_VMW(14)
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
   }
-  __device__ __forceinline__ void start(int slot) {  // slot's DMA was just issued
-    cnt &= ~(0xffull << (8 * slot));
-    active |= 0xffull << (8 * slot);
-  }
-  __device__ __forceinline__ int younger(int slot) const { return (int)((cnt >> (8 * slot)) & 0xff); }
-  __device__ __forceinline__ void done(int slot) { active &= ~(0xffull << (8 * slot)); }
+}
+#undef PHIP_VMW
+
+// The staged sources of the segment being prefetched, held in SGPRs: loaded once when the prefetch
+// cursor enters a segment, then advanced by one tile per prefetch (no per-tile metadata loads).
+template <int kS>
+struct StageCursor {
+  const uint8_t *ptr[kS];  // bytes of the next tile to prefetch, per source
+  int32_t bytes[kS];       // per tile
+  int32_t lds[kS];         // region offset in the ring slot
+  int32_t n;
 };
+
+template <int kS>
+__device__ __forceinline__ void cursor_load(StageCursor<kS> &c, cseg_t &seg, int32_t tile_in_seg) {
+  c.n = seg.num_stage;
+#pragma unroll
+  for (int i = 0; i < kS; i++) {
+    c.ptr[i] = nullptr;
+    c.bytes[i] = 0;
+    c.lds[i] = 0;
+    if (i < c.n) {
+      c.bytes[i] = seg.stage[i].bytes;
+      c.lds[i] = seg.stage[i].lds_off;
+      c.ptr[i] = seg.stage[i].base + (int64_t)tile_in_seg * c.bytes[i];
+    }
+  }
+}
+
+// LDS-DMA of one tile into the ring slot at LDS address lbase; advances the cursor by `step` tiles.
+template <int kS>
+__device__ __forceinline__ void cursor_issue(StageCursor<kS> &c, uint32_t lbase, int step) {
+  const int lane16 = lane_id() * 16;
+#pragma unroll
+  for (int i = 0; i < kS; i++) {
+    if (i < c.n) {
+      const uint8_t *g = c.ptr[i] + lane16;
+      const uint32_t l = lbase + (uint32_t)c.lds[i];
+      const int32_t nb = c.bytes[i];
+      for (int off = 0; off < nb; off += 1024) {
+        if (off + lane16 < nb) dma16(g + off, l + (uint32_t)off);
+      }
+      c.ptr[i] += (int64_t)nb * step;
+    }
+  }
+}
 
 template <bool kConjOnly>
 __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel(DevFilter q) {
+  constexpr int kS = kConjOnly ? kMaxConj : kMaxStage;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);
@@ -459,47 +543,51 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   const int nbuf = q.nbuf;
   const int stride = q.stage_stride;
   PHIP_LDS uint8_t *ring = (PHIP_LDS uint8_t *)(smem + (size_t)wave * nbuf * stride);
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
 
   cseg_t *segs = (cseg_t *)q.segs;
   cnode_t *nodes = (cnode_t *)q.nodes;
   uint32_t lane_matched = 0;  // per-lane popcount, reduced once per segment
   uint64_t scanned = 0;
   uint64_t matched_total = 0;
-  VmLedger vm;
+  // Completion of a tile's DMA is awaited with a LOWER bound of the vector-memory instructions issued
+  // after it: >= min_dma per later prefetched tile, plus the mask stores of the tiles evaluated since
+  // (atomics only add to the true count). Waiting for fewer outstanding operations is always safe.
+  const int nd = q.min_dma;
+  const int st = q.mask_out != nullptr ? 1 : 0;
 
-  // prefetch cursor: tiles [begin, pf) have their DMA issued
-  int pf = begin;
-  int sn = 0;  // segment of tile pf
-  auto prefetch = [&](int slot) {
-    while (sn + 1 < q.num_segs && segs[sn + 1].work_begin <= pf) sn++;
-    const int k = stage_tile(segs[sn], segs[sn].tile0 + (pf - segs[sn].work_begin), ring + slot * stride);
-    vm.issued(k);
-    vm.start(slot);
-    pf += step;
-  };
-  int pslot = 0;
-  for (int i = 0; i < nbuf - 1 && pf < end; i++) {
-    prefetch(pslot);
-    pslot = pslot + 1 == nbuf ? 0 : pslot + 1;
-  }
+  // prefetch cursor: tiles [begin, pf) have their DMA issued (pfc of them)
+  int pf = begin, pfc = 0, psn = 0, pend = -1, pslot = 0;
+  StageCursor<kS> cur;
+  cur.n = 0;
+#define PHIP_PREFETCH()                                                                         \
+  do {                                                                                          \
+    if (pf >= pend) {                                                                           \
+      while (psn + 1 < q.num_segs && segs[psn].work_begin + segs[psn].num_work <= pf) psn++;    \
+      cseg_t &ps = segs[psn];                                                                   \
+      pend = ps.work_begin + ps.num_work;                                                       \
+      cursor_load<kS>(cur, ps, ps.tile0 + (pf - ps.work_begin));                                \
+    }                                                                                           \
+    cursor_issue<kS>(cur, ring_lds + (uint32_t)(pslot * stride), step);                         \
+    pf += step;                                                                                 \
+    pfc++;                                                                                      \
+    pslot = pslot + 1 == nbuf ? 0 : pslot + 1;                                                  \
+  } while (0)
+  for (int i = 0; i < nbuf - 1 && pf < end; i++) PHIP_PREFETCH();
 
   int si = -1;  // segment of the current tile
   int seg_end = -1;
   int slot = 0;
-  for (int t = begin; t < end; t += step) {
-    if (pf < end) {
-      prefetch(pslot);
-      pslot = pslot + 1 == nbuf ? 0 : pslot + 1;
-    }
+  int k = 0;  // tiles evaluated
+  for (int t = begin; t < end; t += step, k++) {
+    if (pf < end) PHIP_PREFETCH();
     if (t >= seg_end) {  // entering a new segment: flush the previous one's count
       if (si >= 0) {
         const uint64_t m = wave_reduce_u64_add(lane_matched);
         lane_matched = 0;
         matched_total += m;
-        if (m) {  // m is wave-uniform: one atomic wave-instruction (lane 0)
-          if (lane == 0) atomicAdd((unsigned long long *)&q.seg_matched[segs[si].seg_index], (unsigned long long)m);
-          vm.issued(1);
-        }
+        if (m && lane == 0)  // m is wave-uniform: one atomic wave-instruction
+          atomicAdd((unsigned long long *)&q.seg_matched[segs[si].seg_index], (unsigned long long)m);
       }
       si = si < 0 ? 0 : si;
       while (si + 1 < q.num_segs && segs[si + 1].work_begin <= t) si++;
@@ -511,8 +599,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     tl.doc0 = tile_in_seg * kTileDocs;
     tl.valid_docs = min(kTileDocs, seg.num_docs - tl.doc0);
     tl.stage = ring + slot * stride;
-    wait_vmcnt(min(vm.younger(slot), 63));
-    vm.done(slot);
+    wait_vmcnt_lb((pfc - k - 1) * nd + min(k, nbuf - 1) * st);
 
     const uint32_t valid = valid_word(tl.valid_docs, lane);
     uint32_t scanned_t = 0;
@@ -525,12 +612,10 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     }
     scanned += scanned_t;
     lane_matched += (uint32_t)__popc(mask);
-    if (q.mask_out != nullptr) {
-      ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
-      vm.issued(1);
-    }
+    if (st) ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
     slot = slot + 1 == nbuf ? 0 : slot + 1;
   }
+#undef PHIP_PREFETCH
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (si >= 0) {
     const uint64_t m = wave_reduce_u64_add(lane_matched);

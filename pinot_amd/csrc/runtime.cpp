@@ -1251,6 +1251,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       std::stable_sort(conj.begin(), conj.end(),
                        [](const std::pair<double, ConjLeaf> &a, const std::pair<double, ConjLeaf> &b) { return a.first < b.first; });
       ds.conj = (int32_t)conj.size();
+      ds.conj_sparse = 1;
+      for (size_t i = 1; i < conj.size(); i++) ds.conj_sparse &= conj[i].second.kind == 0 ? 1 : 0;
+      if (getenv("PHIP_NO_SPARSE")) ds.conj_sparse = 0;  // measurement override
       ds.conj_p = 8;
       for (size_t i = 0; i < conj.size(); i++) {
         ds.conj_leaf[i] = conj[i].second;
@@ -1336,6 +1339,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   fq.stage_stride = stage_stride;
   fq.nbuf = nbuf;
   fq.xcd_walk = xcd_walk ? 1 : 0;
+  fq.min_dma = 0;
+  for (size_t i = 0; i < dsegs.size(); i++)
+    fq.min_dma = i == 0 ? dsegs[i].num_dma : std::min(fq.min_dma, dsegs[i].num_dma);
   dq.segs = dev_segs;
 
   void *fpart, *finals, *seg_matched, *apart = nullptr, *masks = nullptr;
