@@ -212,6 +212,222 @@ __device__ __forceinline__ void group_chunk_global(cquery_t &q, cseg_t &seg, int
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// dense tiles (aggregation only): kBatch groups of 64 docs at a time in the mask's lane-major order
+// (doc 64g + lane), every load of the batch issued before the first use, so a dense tile costs a few
+// memory round trips instead of one per 64 matched docs. Lanes whose doc did not match load the
+// tile's first doc (always valid) and contribute the identity.
+// ------------------------------------------------------------------------------------------------
+constexpr int kBatch = 4;
+constexpr int kDenseMin = 640;  // matched docs per 2048-doc tile from which the batched walk is used
+
+template <int U>
+__device__ __forceinline__ void batch_docs(int32_t doc, uint32_t act, int32_t safe, int32_t (&d)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; u++) d[u] = ((act >> u) & 1u) ? doc + 64 * u : safe;
+}
+
+// Dict ids of the batch: from the wave's LDS stage (sw != null; td = tile-relative doc of group g0,
+// bit window at td * b, ids of non-matching docs forced to 0) or straight from HBM.
+struct BatchSrc {
+  const PHIP_LDS uint32_t *sw;
+  int32_t td;
+  uint32_t act;
+  const PHIP_LDS unsigned char *dict;  // the segment's dictionary copied into LDS (small ones), or null
+};
+
+template <int U>
+__device__ __forceinline__ void batch_ids(ccol_t &c, const int32_t (&d)[U], const BatchSrc &bs, uint32_t (&id)[U]) {
+  const uint32_t b = (uint32_t)c.bits;
+  if (bs.sw != nullptr) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t v = window_at(bs.sw, (bs.td + 64 * u) * (int32_t)b) >> (32 - b);
+      id[u] = ((bs.act >> u) & 1u) ? v : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) id[u] = decode_bits(c.words, (uint64_t)(uint32_t)d[u] * b, b);
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void batch_i64(ccol_t &c, const int32_t (&d)[U], const BatchSrc &bs, int64_t (&v)[U]) {
+  if (c.has_dict) {
+    uint32_t id[U];
+    batch_ids<U>(c, d, bs, id);
+    if (bs.dict != nullptr) {
+      if (c.type == PHIP_TYPE_INT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_LDS int32_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_LONG) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_LDS int64_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_FLOAT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (int64_t)((const PHIP_LDS float *)bs.dict)[id[u]];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (int64_t)((const PHIP_LDS double *)bs.dict)[id[u]];
+      }
+      return;
+    }
+    switch (c.type) {
+      case PHIP_TYPE_INT:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int32_t *)c.dict)[id[u]];
+        break;
+      case PHIP_TYPE_LONG:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int64_t *)c.dict)[id[u]];
+        break;
+      default:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = dict_i64(c, id[u]);
+        break;
+    }
+  } else {
+    switch (c.type) {
+      case PHIP_TYPE_INT:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int32_t *)c.raw)[d[u]];
+        break;
+      case PHIP_TYPE_LONG:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int64_t *)c.raw)[d[u]];
+        break;
+      default:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = raw_i64(c, d[u]);
+        break;
+    }
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void batch_f64(ccol_t &c, const int32_t (&d)[U], const BatchSrc &bs, double (&v)[U]) {
+  if (c.has_dict) {
+    uint32_t id[U];
+    batch_ids<U>(c, d, bs, id);
+    if (bs.dict != nullptr) {
+      if (c.type == PHIP_TYPE_INT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_LDS int32_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_LONG) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_LDS int64_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_FLOAT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_LDS float *)bs.dict)[id[u]];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_LDS double *)bs.dict)[id[u]];
+      }
+      return;
+    }
+    switch (c.type) {
+      case PHIP_TYPE_INT:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_GLB int32_t *)c.dict)[id[u]];
+        break;
+      case PHIP_TYPE_DOUBLE:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB double *)c.dict)[id[u]];
+        break;
+      default:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = dict_f64(c, id[u]);
+        break;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = raw_f64(c, d[u]);
+  }
+}
+
+// Same arithmetic as expr_i64 / expr_f64, U docs at a time.
+template <int U>
+__device__ __forceinline__ void batch_expr_i64(cseg_t &s, cagg_t &a, const int32_t (&d)[U], const BatchSrc &sa,
+                                               const BatchSrc &sb, int64_t (&x)[U]) {
+  batch_i64<U>(s.cols[a.col_a], d, sa, x);
+  if (a.expr == PHIP_EXPR_COLUMN) return;
+  int64_t y[U];
+  batch_i64<U>(s.cols[a.col_b], d, sb, y);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (a.expr == PHIP_EXPR_ADD) x[u] = x[u] + y[u];
+    else if (a.expr == PHIP_EXPR_SUB) x[u] = x[u] - y[u];
+    else x[u] = x[u] * y[u];
+  }
+}
+template <int U>
+__device__ __forceinline__ void batch_expr_f64(cseg_t &s, cagg_t &a, const int32_t (&d)[U], const BatchSrc &sa,
+                                               const BatchSrc &sb, double (&x)[U]) {
+  batch_f64<U>(s.cols[a.col_a], d, sa, x);
+  if (a.expr == PHIP_EXPR_COLUMN) return;
+  double y[U];
+  batch_f64<U>(s.cols[a.col_b], d, sb, y);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (a.expr == PHIP_EXPR_ADD) x[u] = x[u] + y[u];
+    else if (a.expr == PHIP_EXPR_SUB) x[u] = x[u] - y[u];
+    else x[u] = x[u] * y[u];
+  }
+}
+
+// Groups [g0, g0 + U) of a tile; act bit u = doc 64(g0 + u) + lane matched. Accumulation order per
+// lane is the doc order, as in agg_chunk.
+template <int NA, int U>
+__device__ __forceinline__ void agg_batch(cquery_t &q, cseg_t &seg, int32_t doc, uint32_t act, int32_t safe,
+                                          const PHIP_LDS uint8_t *stg, int32_t td, uint64_t (&acc)[NA],
+                                          lds_u32 *hll_lds) {
+  int32_t d[U];
+  batch_docs<U>(doc, act, safe, d);
+#pragma unroll
+  for (int a = 0; a < NA; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    const int kind = ag.acc;
+    const int ka = q.stage_slot_a[a], kb = q.stage_slot_b[a];
+    const int ja = ka < 0 ? 0 : ka, jb = kb < 0 ? 0 : kb;
+    const BatchSrc sa{ka >= 0 ? (const PHIP_LDS uint32_t *)(stg + q.stage_off[ja]) : nullptr, td, act,
+                      ka >= 0 && q.stage_dict_off[ja] >= 0 ? stg + q.stage_dict_off[ja] : nullptr};
+    const BatchSrc sb{kb >= 0 ? (const PHIP_LDS uint32_t *)(stg + q.stage_off[jb]) : nullptr, td, act,
+                      kb >= 0 && q.stage_dict_off[jb] >= 0 ? stg + q.stage_dict_off[jb] : nullptr};
+    if (kind == ACC_COUNT) {
+      acc[a] += (uint64_t)__popc(act);
+    } else if (kind == ACC_SUM_I64) {
+      int64_t v[U];
+      batch_expr_i64<U>(seg, ag, d, sa, sb, v);
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[a] += ((act >> u) & 1u) ? (uint64_t)v[u] : 0ull;
+    } else if (kind == ACC_HLL) {
+      ccol_t &c = seg.cols[ag.col_a];
+      uint32_t id[U];
+      batch_ids<U>(c, d, sa, id);
+      uint32_t h[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll)[id[u]];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if ((act >> u) & 1u)
+          __hip_atomic_fetch_max(&hll_lds[(ag.hll_slot << q.log2m) + (h[u] >> 8)], h[u] & 0xffu, PHIP_RLX, PHIP_WG);
+    } else {
+      double v[U];
+      batch_expr_f64<U>(seg, ag, d, sa, sb, v);
+      double cur = as_f64(acc[a]);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const bool on = (act >> u) & 1u;
+        if (kind == ACC_SUM_F64) cur = cur + (on ? v[u] : 0.0);
+        else if (kind == ACC_MIN_F64) cur = fmin(cur, on ? v[u] : __builtin_huge_val());
+        else cur = fmax(cur, on ? v[u] : -__builtin_huge_val());
+      }
+      acc[a] = as_u64(cur);
+    }
+  }
+}
+
 template <int NA, int MODE>
 __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, bool act, uint64_t (&acc)[NA],
                                          lds_u32 *hll_lds, lds_u64 *tbl, lds_u32 *hll_packed) {
@@ -232,7 +448,10 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
   const int wave = uniform(threadIdx.x >> 6);
   PHIP_LDS unsigned char *lds = (PHIP_LDS unsigned char *)smem;
   lds_u32 *ring = (lds_u32 *)lds + wave * kRing;
-  PHIP_LDS unsigned char *rest = lds + kAggWaves * kRing * 4;
+  PHIP_LDS unsigned char *stage = lds + kAggWaves * kRing * 4;  // GB_NONE dense-tile staging
+  PHIP_LDS unsigned char *stg = stage + wave * q.stage_bytes;
+  const uint32_t stg_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)stg);
+  PHIP_LDS unsigned char *rest = stage + kAggWaves * q.stage_bytes;
   lds_u32 *hll_lds = (lds_u32 *)rest;
   lds_u64 *tbl = (lds_u64 *)rest;
   lds_u32 *hll_packed = (lds_u32 *)(rest + (size_t)q.tbl_words * 8);
@@ -270,6 +489,7 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
   const glb_u32 *mask = (const glb_u32 *)q.mask;
   int head = 0, tail = 0;  // ring cursors (wave-uniform)
   int si = 0;
+  int dict_si = -1;        // segment whose small dictionaries sit in the wave's stage area
   int t = xs + wid;
   uint32_t m_next = 0;
   if (mask != nullptr && t < xe) m_next = __builtin_nontemporal_load(mask + (size_t)t * 64 + lane);
@@ -290,7 +510,49 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
     const int32_t nvalid = min(kTileDocs, seg.num_docs - doc0);
     const uint32_t valid = valid_word(nvalid, lane);
     const uint32_t m = mask != nullptr ? (m_raw & valid) : valid;
-    if (ballot(m != valid) == 0) {
+    bool dense = ballot(m != valid) == 0;  // every valid doc of the tile matched
+    if constexpr (MODE == GB_NONE) {
+      if (!dense && q.dense_batch) dense = wave_sum_u32((uint32_t)__popc(m)) >= (uint32_t)kDenseMin;
+    }
+    bool batched = false;
+    if constexpr (MODE == GB_NONE) batched = dense && q.dense_batch;
+    if (batched) {
+      // lane-major batches: bit (31 - g) of m = doc 64g + lane (coalesced column reads per group)
+      if (q.num_stage > 0) {
+        if (dict_si != si) {
+          // small dictionaries of the staged columns -> the wave's LDS, once per segment (the wave's
+          // LDS operations execute in order, so the batch's reads see these writes)
+          for (int k = 0; k < q.num_stage; k++) {
+            if (q.stage_dict_off[k] < 0) continue;
+            ccol_t &c = seg.cols[q.stage_col[k]];
+            if (!c.has_dict) continue;
+            const int32_t nw = c.card * ((c.type == PHIP_TYPE_LONG || c.type == PHIP_TYPE_DOUBLE) ? 2 : 1);
+            lds_u32 *dst = (lds_u32 *)(stg + q.stage_dict_off[k]);
+            for (int i = lane; i < nw; i += 64) dst[i] = ((const glb_u32 *)c.dict)[i];
+          }
+          dict_si = si;
+        }
+        // the tile's words of every staged column -> LDS (1 KiB per wave-instruction), one round trip
+        const int32_t tile = doc0 / kTileDocs;
+        for (int k = 0; k < q.num_stage; k++) {
+          ccol_t &c = seg.cols[q.stage_col[k]];
+          if (!c.has_dict) continue;  // raw in this segment: read from HBM (batch_i64 / batch_f64)
+          const int32_t nb = 256 * c.bits;
+          const uint8_t *src = (const uint8_t *)c.words + (size_t)tile * nb + lane * 16;
+          const uint32_t dst = stg_lds + (uint32_t)q.stage_off[k];
+          for (int off = 0; off < nb; off += 1024)
+            if (off + lane * 16 < nb) dma16(src + off, dst + (uint32_t)off);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+#pragma unroll 1
+      for (int g0 = 0; g0 < kTileGroups; g0 += kBatch) {
+        const uint32_t act = __builtin_bitreverse32(m << g0) & ((1u << kBatch) - 1u);
+        if (ballot(act != 0) == 0) continue;
+        agg_batch<NA, kBatch>(q, seg, doc0 + 64 * g0 + lane, act, doc0, stg, 64 * g0 + lane, acc, hll_lds);
+      }
+      if (q.num_stage > 0) __builtin_amdgcn_wave_barrier();  // LDS reads done before the next tile's DMA
+    } else if (dense) {
       // every doc of the tile matched: consecutive chunks, coalesced column reads
       for (int c = 0; c < nvalid; c += 64) {
         const bool act = c + lane < nvalid;

@@ -43,6 +43,27 @@ __device__ __forceinline__ uint32_t window_at(const PHIP_LDS uint32_t *w, int32_
   return __builtin_amdgcn_alignbit(w[q], w[q + 1], s);
 }
 
+// ------------------------------------------------------------------------------------------------
+// LDS-DMA staging. The copy is issued through inline asm so that hipcc does not see an LDS write in
+// flight: it would otherwise put s_waitcnt vmcnt(0) in front of the first ds_read of the CURRENT
+// tile and drain the prefetch of the next ones. Completion is awaited by wait_vmcnt(n).
+// ------------------------------------------------------------------------------------------------
+#ifndef PHIP_DMA_POLICY
+#define PHIP_DMA_POLICY "nt"  // streamed once: non-temporal
+#endif
+__device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off " PHIP_DMA_POLICY "\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
 // Order-preserving map double <-> u64 (for atomicMin/atomicMax on group tables).
 __device__ __forceinline__ uint64_t f64_ordered(double d) {
   uint64_t u = (uint64_t)__double_as_longlong(d);
@@ -70,6 +91,10 @@ __device__ __forceinline__ uint64_t wave_reduce_u64_add(uint64_t v) {
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
   return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ uint32_t wave_or32(uint32_t v) {

@@ -23,7 +23,10 @@ constexpr int kMaxRing = 8;           // LDS-DMA ring slots per wave
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;
-constexpr int kRing = 128;            // per-wave ring of matched doc ids (u32), flushed 64 at a time
+constexpr int kRing = 128;
+constexpr int kMaxAggStage = 4;      // staged aggregation columns
+constexpr int kAggStageBudget = 4096; // LDS bytes per wave for them
+constexpr int kAggLdsDict = 1024;     // dictionaries up to this many bytes are copied next to them            // per-wave ring of matched doc ids (u32), flushed 64 at a time
 
 // Accumulator kinds of one aggregation slot.
 enum AccKind : int32_t {
@@ -164,7 +167,7 @@ struct DevAggQuery {
   // group-by
   int32_t num_group_by;
   int32_t gb_cols[kMaxGroupBy];
-  int32_t pad0;
+  int32_t dense_batch;    // GB_NONE: dense tiles take the batched lane-major walk (small dictionaries)
   int64_t gb_stride[kMaxGroupBy];  // mixed radix, column 0 least significant
   int64_t num_groups;     // dense key space size
   int32_t tbl_words;      // GB_LDS: u64 words of one workgroup table = num_groups * (1 + num_aggs)
@@ -174,6 +177,15 @@ struct DevAggQuery {
   // aggregation only
   uint64_t *partials;     // [num_blocks][num_aggs]
   uint32_t *hll_regs;     // [nhll][m] u32 (atomicMax from every block)
+  // dense-tile staging (GB_NONE, dense_batch): the tile's fixed-bit words of each staged column are
+  // LDS-DMA-ed into the wave's stage region, so the ids of all 2048 docs cost one memory round trip
+  int32_t stage_bytes;    // per wave (0 = no staging)
+  int32_t num_stage;
+  int32_t stage_col[kMaxAggStage];
+  int32_t stage_off[kMaxAggStage];  // region of staged column k in the wave's stage area (kStagePad guards)
+  int32_t stage_dict_off[kMaxAggStage];  // the column's dictionary copied into the stage area, -1 = HBM
+  int32_t stage_slot_a[kMaxAggs];   // staged slot of aggs[a].col_a / col_b, -1 = read from HBM
+  int32_t stage_slot_b[kMaxAggs];
 };
 
 // One Roaring container of one selected dictionary id, OR-ed into a segment's dense doc words.

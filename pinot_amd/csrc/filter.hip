@@ -20,27 +20,6 @@
 
 namespace phip {
 
-// ------------------------------------------------------------------------------------------------
-// LDS-DMA staging. The copy is issued through inline asm so that hipcc does not see an LDS write in
-// flight: it would otherwise put s_waitcnt vmcnt(0) in front of the first ds_read of the CURRENT
-// tile and drain the prefetch of the next ones. Completion is awaited by wait_vmcnt(n).
-// ------------------------------------------------------------------------------------------------
-#ifndef PHIP_DMA_POLICY
-#define PHIP_DMA_POLICY "nt"  // streamed once: non-temporal
-#endif
-__device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off " PHIP_DMA_POLICY "\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_dst)
-      : "memory");
-}
-
 struct Tile {
   int32_t doc0;          // first doc of the tile within the segment
   int32_t valid_docs;    // docs of the tile inside the segment (1..2048)

@@ -327,3 +327,46 @@ def test_gpu_ssb_vs_oracle(name, ssb_segments):
         assert set(gblk.groups) == set(oblk.groups)
         for k, v in oblk.groups.items():
             _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
+
+
+# ---- dense tiles: batched lane-major aggregation walk vs per-64-doc chunks vs the oracle ------------
+DENSE_QUERIES = [
+    "SELECT COUNT(*), SUM(a), SUM(r), SUM(d), MIN(d), MAX(a), MIN(r), DISTINCTCOUNTHLL(a) FROM t",
+    "SELECT COUNT(*), SUM(a), SUM(r), SUM(d), MIN(d), MAX(a), DISTINCTCOUNTHLL(a) FROM t WHERE f < 90",
+    "SELECT SUM(a * d), SUM(a - r), SUM(a + a), MAX(d), COUNT(*) FROM t WHERE f >= 40",
+    "SELECT SUM(a), COUNT(*), MIN(a) FROM t WHERE f < 33",
+    "SELECT SUM(r), MAX(r) FROM t WHERE f BETWEEN 10 AND 99",
+    "SELECT SUM(s), SUM(sl), SUM(sd), MIN(sd), MAX(sl), SUM(s * sd), SUM(sl - s), COUNT(*) FROM t WHERE f < 80",
+    "SELECT SUM(s), SUM(sl * s), MAX(s), DISTINCTCOUNTHLL(s), SUM(a) FROM t",
+]
+
+
+@pytest.mark.parametrize("walk", ["chunks", "batch", "staged", "staged_lds_dict"])
+@pytest.mark.parametrize("q", DENSE_QUERIES)
+def test_gpu_dense_tile_batches(q, walk, monkeypatch, gpu_lib):
+    """Tiles with >= kDenseMin matched docs take agg_batch (aggregate.hip) when PHIP_DENSE_BATCH allows,
+    with the dict-id words LDS-staged unless PHIP_AGG_STAGE=0; every walk must give the oracle's answers
+    (ragged last tile, raw INT, dict INT / DOUBLE, HLL)."""
+    monkeypatch.setenv("PHIP_DENSE_BATCH", "0" if walk == "chunks" else "1")
+    monkeypatch.setenv("PHIP_AGG_STAGE", "1" if walk.startswith("staged") else "0")
+    monkeypatch.setenv("PHIP_AGG_LDS_DICT", "1" if walk == "staged_lds_dict" else "0")
+    rng = np.random.default_rng(31)
+    n = 2048 * 37 + 1234
+    c = SegmentCreator("dense", no_dictionary_columns=["r"])
+    c.add_column("a", DataType.INT, rng.integers(-3000, 5000, n))
+    c.add_column("d", DataType.DOUBLE, np.round(rng.normal(0, 1e4, n), 2))
+    c.add_column("r", DataType.INT, rng.integers(-2 ** 31, 2 ** 31 - 1, n))
+    c.add_column("f", DataType.INT, rng.integers(0, 100, n))
+    c.add_column("s", DataType.INT, rng.integers(-50, 50, n))                  # 400-B dictionary
+    c.add_column("sl", DataType.LONG, rng.integers(0, 60, n) * 10 ** 12)       # 480-B dictionary
+    c.add_column("sd", DataType.DOUBLE, rng.integers(0, 50, n) * 0.37 - 3.5)  # 400-B dictionary
+    raw = c.build()
+    seg = GpuSegment(raw)
+    try:
+        qc = parse(q)
+        blk = GpuInstancePlanMaker().make_instance_plan(qc, [seg]).next_block()
+        oblk, ex = executor.execute(qc, [raw])
+        assert blk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+        _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
+    finally:
+        seg.destroy()
