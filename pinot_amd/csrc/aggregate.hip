@@ -181,37 +181,6 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
   }
 }
 
-// GB_GLOBAL: one table in HBM ([1 + naggs][G] u64, row 0 counts), HLL registers [nhll][G][m] u32.
-__device__ __forceinline__ void group_chunk_global(cquery_t &q, cseg_t &seg, int32_t doc, bool act) {
-  const int64_t key = group_key(q, seg, doc);
-  if (!act) return;
-  const int64_t G = q.num_groups;
-  glb_u64 *tbl = (glb_u64 *)q.gb_table;
-  __hip_atomic_fetch_add(&tbl[key], 1ull, PHIP_RLX, PHIP_AG);
-  for (int a = 0; a < kMaxAggs; a++) {
-    if (a >= q.num_aggs) break;
-    cagg_t &ag = q.aggs[a];
-    glb_u64 *slot = tbl + (1 + a) * G + key;
-    switch (ag.acc) {
-      case ACC_COUNT: break;
-      case ACC_SUM_I64: __hip_atomic_fetch_add(slot, (uint64_t)expr_i64(seg, ag, doc), PHIP_RLX, PHIP_AG); break;
-      case ACC_SUM_F64:
-        __hip_atomic_fetch_add((PHIP_GLB double *)slot, expr_f64(seg, ag, doc), PHIP_RLX, PHIP_AG);
-        break;
-      case ACC_MIN_F64: __hip_atomic_fetch_min(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_AG); break;
-      case ACC_MAX_F64: __hip_atomic_fetch_max(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_AG); break;
-      case ACC_HLL: {
-        ccol_t &c = seg.cols[ag.col_a];
-        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
-        glb_u32 *r = (glb_u32 *)q.gb_hll + (((int64_t)ag.hll_slot * G + key) << q.log2m) + (h >> 8);
-        // registers only grow: a stale read costs one extra atomic, never a result
-        if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
-        break;
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // dense tiles (aggregation only): kBatch groups of 64 docs at a time in the mask's lane-major order
 // (doc 64g + lane), every load of the batch issued before the first use, so a dense tile costs a few
@@ -428,11 +397,87 @@ __device__ __forceinline__ void agg_batch(cquery_t &q, cseg_t &seg, int32_t doc,
   }
 }
 
+// GB_HASH: linear probing from a 64-bit finaliser of the key; a slot is claimed by CAS(empty -> key).
+// Plain loads may see a stale "empty" (the CAS then returns the owner) but never a wrong key, because
+// a slot changes at most once.
+__device__ __forceinline__ uint64_t mix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+__device__ __forceinline__ int64_t hash_slot(cquery_t &q, uint64_t key) {
+  glb_u64 *keys = (glb_u64 *)q.gb_keys;
+  const uint64_t mask = (uint64_t)q.num_groups - 1;
+  uint64_t i = mix64(key) & mask;
+  for (uint64_t p = 0; p <= mask; p++) {
+    const uint64_t k = keys[i];
+    if (k == key) return (int64_t)i;
+    if (k == kHashEmpty) {
+      uint64_t expected = kHashEmpty;
+      if (__hip_atomic_compare_exchange_strong(&keys[i], &expected, key, PHIP_RLX, PHIP_RLX, PHIP_AG) ||
+          expected == key)
+        return (int64_t)i;
+    }
+    i = (i + 1) & mask;
+  }
+  return -1;
+}
+
+// GB_GLOBAL / GB_HASH: one table in HBM ([1 + naggs][G] u64, row 0 counts) at index `slot`.
+__device__ __forceinline__ void group_update_global(cquery_t &q, cseg_t &seg, int32_t doc, int64_t slot) {
+  const int64_t G = q.num_groups;
+  glb_u64 *tbl = (glb_u64 *)q.gb_table;
+  __hip_atomic_fetch_add(&tbl[slot], 1ull, PHIP_RLX, PHIP_AG);
+  for (int a = 0; a < kMaxAggs; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    glb_u64 *p = tbl + (1 + a) * G + slot;
+    switch (ag.acc) {
+      case ACC_COUNT: break;
+      case ACC_SUM_I64: __hip_atomic_fetch_add(p, (uint64_t)expr_i64(seg, ag, doc), PHIP_RLX, PHIP_AG); break;
+      case ACC_SUM_F64:
+        __hip_atomic_fetch_add((PHIP_GLB double *)p, expr_f64(seg, ag, doc), PHIP_RLX, PHIP_AG);
+        break;
+      case ACC_MIN_F64: __hip_atomic_fetch_min(p, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_AG); break;
+      case ACC_MAX_F64: __hip_atomic_fetch_max(p, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_AG); break;
+      case ACC_HLL: {
+        ccol_t &c = seg.cols[ag.col_a];
+        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+        glb_u32 *r = (glb_u32 *)q.gb_hll + (((int64_t)ag.hll_slot * G + slot) << q.log2m) + (h >> 8);
+        if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
+        break;
+      }
+    }
+  }
+}
+
+// GB_GLOBAL: the dense key is the slot (HLL registers [nhll][G][m] u32).
+__device__ __forceinline__ void group_chunk_global(cquery_t &q, cseg_t &seg, int32_t doc, bool act) {
+  const int64_t key = group_key(q, seg, doc);
+  if (!act) return;
+  group_update_global(q, seg, doc, key);
+}
+
+__device__ __forceinline__ void group_chunk_hash(cquery_t &q, cseg_t &seg, int32_t doc, bool act) {
+  const int64_t key = group_key(q, seg, doc);
+  if (!act) return;
+  const int64_t slot = hash_slot(q, (uint64_t)key);
+  if (slot < 0) {
+    __hip_atomic_fetch_or((glb_u32 *)q.hash_overflow, 1u, PHIP_RLX, PHIP_AG);
+    return;
+  }
+  group_update_global(q, seg, doc, slot);
+}
+
 template <int NA, int MODE>
 __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, bool act, uint64_t (&acc)[NA],
                                          lds_u32 *hll_lds, lds_u64 *tbl, lds_u32 *hll_packed) {
   if constexpr (MODE == GB_NONE) agg_chunk<NA>(q, seg, doc, act, acc, hll_lds);
   else if constexpr (MODE == GB_LDS) group_chunk_lds(q, seg, doc, act, tbl, hll_packed);
+  else if constexpr (MODE == GB_HASH) group_chunk_hash(q, seg, doc, act);
   else group_chunk_global(q, seg, doc, act);
 }
 
@@ -762,6 +807,13 @@ __global__ void group_gather_kernel(const int64_t *__restrict__ keys, int64_t ng
   }
 }
 
+// GB_HASH: compacted slot indices -> the mixed-radix keys they hold (after group_gather_kernel used
+// the slots).
+__global__ void hash_keys_kernel(int64_t *__restrict__ slots, int64_t n, const uint64_t *__restrict__ keys) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    slots[i] = (int64_t)keys[slots[i]];
+}
+
 // ------------------------------------------------------------------------------------------------
 // host-callable launchers (runtime.cpp)
 // ------------------------------------------------------------------------------------------------
@@ -790,6 +842,7 @@ static hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hi
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s) {
   if (q.mode == GB_LDS) return launch_agg_t<1, GB_LDS>(dq, nblocks, lds, s);
   if (q.mode == GB_GLOBAL) return launch_agg_t<1, GB_GLOBAL>(dq, nblocks, lds, s);
+  if (q.mode == GB_HASH) return launch_agg_t<1, GB_HASH>(dq, nblocks, lds, s);
   if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE>(dq, nblocks, lds, s);
   if (q.num_aggs <= 2) return launch_agg_t<2, GB_NONE>(dq, nblocks, lds, s);
   if (q.num_aggs <= 4) return launch_agg_t<4, GB_NONE>(dq, nblocks, lds, s);
@@ -831,6 +884,12 @@ hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t nde
   if (ngroups <= 0) return hipSuccess;
   group_gather_kernel<<<grid_for(ngroups), 256, 0, s>>>(keys, ngroups, ndense, naggs, kinds, table, hll, nhll, log2m,
                                                        vals, longs, hll_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hash_keys_kernel<<<grid_for(n), 256, 0, s>>>(slots, n, keys);
   return hipGetLastError();
 }
 

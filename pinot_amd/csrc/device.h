@@ -48,7 +48,10 @@ enum GroupMode : int32_t {
   GB_NONE = 0,    // aggregation only: per-lane accumulators -> per-block partials
   GB_LDS = 1,     // per-workgroup table in LDS -> per-block slab in HBM -> fixed-order reduction
   GB_GLOBAL = 2,  // one table in HBM, global atomics
+  GB_HASH = 3,    // key space too large for a dense table: open-addressing hash in HBM (slot = group),
+                  // IntMapBasedHolder's role (DictionaryBasedGroupKeyGenerator.java:416-495)
 };
+constexpr uint64_t kHashEmpty = ~0ull;  // empty key slot (mixed-radix keys are < 2^62)
 
 // One column as seen by one segment of a query.
 struct DevCol {
@@ -186,6 +189,9 @@ struct DevAggQuery {
   int32_t stage_dict_off[kMaxAggStage];  // the column's dictionary copied into the stage area, -1 = HBM
   int32_t stage_slot_a[kMaxAggs];   // staged slot of aggs[a].col_a / col_b, -1 = read from HBM
   int32_t stage_slot_b[kMaxAggs];
+  // GB_HASH: num_groups = capacity (power of two); gb_table / gb_hll are indexed by slot
+  uint64_t *gb_keys;        // [capacity] mixed-radix key of each slot, kHashEmpty = free
+  uint32_t *hash_overflow;  // set to 1 when a probe sequence found no slot (host reports an error)
 };
 
 // One Roaring container of one selected dictionary id, OR-ed into a segment's dense doc words.

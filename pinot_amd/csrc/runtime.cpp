@@ -38,6 +38,7 @@ hipError_t launch_filter(const DevFilter &q, bool conj_only, int nblocks, size_t
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,
                                  hipStream_t s);
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s);
+hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hipStream_t s);
 hipError_t launch_slab_reduce(const uint64_t *slab, int32_t nslabs, int32_t tbl_words, int64_t G, const int32_t *kinds,
                               uint64_t *out, const uint32_t *hslab, int32_t hll_words, uint32_t *hout, hipStream_t s);
 hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
@@ -985,11 +986,30 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       gb_dicts.push_back(r);
       dq.gb_cols[k] = c;
       dq.gb_stride[k] = stride;
+      if ((double)stride * (double)r->card > (double)((int64_t)1 << 62))
+        return fail(PHIP_ERR_UNSUPPORTED, "group-by key space exceeds 2^62");
       stride *= r->card;
-      if (stride > (int64_t)1 << 26)
-        return fail(PHIP_ERR_UNSUPPORTED, "group-by key space %lld exceeds the dense table limit", (long long)stride);
     }
-    dq.num_groups = stride;
+    // Dense table (ArrayBasedHolder's role) while the key space is small, or not much larger than the
+    // docs that can create groups; above that an open-addressing hash over the keys (IntMapBasedHolder's
+    // role, DictionaryBasedGroupKeyGenerator.java:105-186): capacity = the next power of two >= 2x the
+    // number of groups possible (min of key space and docs), so probe sequences stay short.
+    int64_t docs = 0;
+    for (int s = 0; s < nseg; s++) docs += segs[s]->num_docs;
+    const char *hm = getenv("PHIP_GB_HASH");  // measurement override: "1" forces the hash table
+    const bool force_hash = hm && atoi(hm) != 0;
+    if (force_hash || stride > ((int64_t)1 << 26) || (stride > ((int64_t)1 << 22) && stride > 4 * docs)) {
+      const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(stride, docs));
+      int64_t cap = 1024;
+      while (cap < 2 * bound) cap <<= 1;
+      const int64_t per_slot = 8 + 8 * (1 + (int64_t)naggs);
+      if (cap * per_slot > ((int64_t)24 << 30))
+        return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table of %lld slots exceeds the memory budget", (long long)cap);
+      dq.num_groups = cap;
+      dq.mode = GB_HASH;
+    } else {
+      dq.num_groups = stride;
+    }
   }
 
   // ---- staging blob: segments, nodes, leaf aux ------------------------------------------------
@@ -1381,11 +1401,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
 
   // ---- aggregation kernel configuration (aggregate.hip) -----------------------------------------
   dq.log2m = log2m;
-  dq.mode = group_by ? GB_GLOBAL : GB_NONE;
+  if (dq.mode != GB_HASH) dq.mode = group_by ? GB_GLOBAL : GB_NONE;
   const int m_regs = nhll ? (1 << log2m) : 0;
   size_t agg_lds = (size_t)kAggWaves * kRing * 4 + (size_t)kAggWaves * dq.stage_bytes;
   int agg_bpc = 4;
-  if (group_by) {
+  if (group_by && dq.mode == GB_HASH) {
+    if ((int64_t)nhll * dq.num_groups * m_regs * 4 > ((int64_t)16 << 30))
+      return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL registers of %lld hash slots exceed the memory budget",
+                  (long long)dq.num_groups);
+  } else if (group_by) {
     const int64_t tbl_words = (int64_t)(1 + naggs) * dq.num_groups;
     const int64_t hll_words = (int64_t)nhll * dq.num_groups * m_regs / 4;
     const int64_t table_bytes = tbl_words * 8 + hll_words * 4;
@@ -1464,6 +1488,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     if (nhll) {
       rc = P.alloc((size_t)nhll * dq.num_groups * m_regs * 4, &ghll);
       if (rc) return rc;
+    }
+    if (dq.mode == GB_HASH) {
+      void *hk = nullptr, *ho = nullptr;
+      rc = P.alloc((size_t)dq.num_groups * 8, &hk);
+      if (rc) return rc;
+      rc = P.alloc(16, &ho);
+      if (rc) return rc;
+      dq.gb_keys = (uint64_t *)hk;
+      dq.hash_overflow = (uint32_t *)ho;
     }
     if (dq.mode == GB_LDS) {
       rc = P.alloc((size_t)agg_blocks * dq.tbl_words * 8 + 16, &slab);
@@ -1574,7 +1607,11 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     HIP_TRY(hipMemsetAsync(inv_words, 0, inv_words_total * 8, st));
     HIP_TRY(launch_roaring_or((const RoaringTask *)(base + tasks_off), (int32_t)tasks.size(), st));
   }
-  if (group_by && dq.mode == GB_GLOBAL) {
+  if (group_by && dq.mode == GB_HASH) {
+    HIP_TRY(hipMemsetAsync(dq.gb_keys, 0xff, (size_t)dq.num_groups * 8, st));  // kHashEmpty
+    HIP_TRY(hipMemsetAsync(dq.hash_overflow, 0, 4, st));
+  }
+  if (group_by && (dq.mode == GB_GLOBAL || dq.mode == GB_HASH)) {
     HIP_TRY(hipMemsetAsync(gtab, 0, (size_t)dq.num_groups * 8, st));  // counts
     for (int a = 0; a < naggs; a++) {
       uint64_t init = 0;
@@ -1693,6 +1730,11 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
     HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, dev_kinds, (const uint64_t *)gtab,
                                 (const uint32_t *)ghll, nhll, log2m, (double *)ov, (int64_t *)ol, (uint8_t *)oh, st));
+    uint32_t overflow = 0;
+    if (dq.mode == GB_HASH) {
+      HIP_TRY(launch_hash_keys((int64_t *)keys, ngroups, dq.gb_keys, st));
+      HIP_TRY(hipMemcpyAsync(&overflow, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
+    }
     std::vector<int64_t> hkeys(ngroups);
     impl->values.resize(ngroups * naggs);
     impl->longs.resize(ngroups * naggs);
@@ -1707,6 +1749,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     }
     HIP_TRY(hipEventRecord(P.ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
     impl->keys.resize(ngroups * P.num_group_by);
     for (int64_t g = 0; g < ngroups; g++) {
       int64_t key = hkeys[g];

@@ -370,3 +370,44 @@ def test_gpu_dense_tile_batches(q, walk, monkeypatch, gpu_lib):
         _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
     finally:
         seg.destroy()
+
+
+# ---- high-cardinality group-by: open-addressing hash table in HBM (GB_HASH) -------------------------
+GB_CASES = [c for c in CASES if "group by" in c["query"].lower()]
+
+
+@pytest.mark.parametrize("case", GB_CASES, ids=[f"{c['ref'].split('/')[-1]}|{c['query'][:60]}" for c in GB_CASES])
+def test_gpu_group_by_hash_table_known_answers(case, gsegs, monkeypatch):
+    """PHIP_GB_HASH=1 forces the hash table for small key spaces too: same known answers."""
+    monkeypatch.setenv("PHIP_GB_HASH", "1")
+    test_gpu_known_answers(case, gsegs)
+    test_gpu_intermediates_vs_oracle(case, gsegs)
+
+
+def test_gpu_group_by_high_cardinality(gpu_lib):
+    """Key space 30011 x 20011 x 7 (> 2^26) over 3 segments with different dictionaries -> GB_HASH
+    without any override; every group and intermediate equals the oracle's."""
+    rng = np.random.default_rng(41)
+    raws = []
+    for k in range(3):
+        n = 150_000 + 777 * k
+        c = SegmentCreator(f"hc{k}")
+        c.add_column("a", DataType.INT, rng.integers(0, 30011, n))
+        c.add_column("b", DataType.LONG, rng.integers(0, 20011, n) * 3 - 7)
+        c.add_column("s", DataType.STRING, np.array([f"v{x}" for x in rng.integers(0, 7, n)]))
+        c.add_column("m", DataType.LONG, rng.integers(-10 ** 12, 10 ** 12, n))
+        c.add_column("d", DataType.DOUBLE, np.round(rng.random(n) * 1000, 3))
+        raws.append(c.build())
+    segs = [GpuSegment(r) for r in raws]
+    try:
+        qc = parse("SELECT a, b, s, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTHLL(m) FROM t "
+                   "WHERE a < 25000 GROUP BY a, b, s LIMIT 10000000")
+        gblk = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, segs).next_block()
+        oblk, exact = executor.execute(qc, raws)
+        assert gblk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+        assert set(gblk.groups) == set(oblk.groups)
+        for k, v in oblk.groups.items():
+            _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
+    finally:
+        for s in segs:
+            s.destroy()
