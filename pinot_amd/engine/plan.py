@@ -387,10 +387,12 @@ class GpuCombineOperator:
             na = r.num_aggregations
             ng = r.num_groups
             m = 1 << max([p[4] for p in self.prims if p[0] == _lib.AGG_HLL] + [0])
-            vals = np.ctypeslib.as_array(r.values, shape=(max(ng * na, 1),))[:ng * na].reshape(ng, na).copy() if na else np.zeros((ng, 0))
-            longs = np.ctypeslib.as_array(r.long_values, shape=(max(ng * na, 1),))[:ng * na].reshape(ng, na).copy() if na else np.zeros((ng, 0), np.int64)
+            # (no groups: the library's arrays may be null)
+            vals = np.ctypeslib.as_array(r.values, shape=(ng * na,)).reshape(ng, na).copy() if ng * na else np.zeros((ng, na))
+            longs = (np.ctypeslib.as_array(r.long_values, shape=(ng * na,)).reshape(ng, na).copy() if ng * na
+                     else np.zeros((ng, na), np.int64))
             hll = None
-            if r.num_hll:
+            if r.num_hll and ng:
                 hll = np.ctypeslib.as_array(r.hll_registers, shape=(ng * r.num_hll * m,)).reshape(ng, r.num_hll, m).copy()
             hll_slot = {}
             for i, p in enumerate(self.prims):

@@ -17,6 +17,9 @@ maps), so the C-ABI receives exactly what ``ImmutableSegmentLoader`` would hand 
 * inverted index (card+1) BE u32 absolute offsets + portable Roaring bitmaps
                  (BitmapInvertedIndexWriter.java:35-156)
 """
+import ctypes
+import os
+import subprocess
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -25,6 +28,59 @@ import numpy as np
 from .. import spi
 from ..spi import DataType
 from . import roaring
+
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_INVIDX_SO = os.path.join(_HERE, "libinvidx.so")
+_invidx = None
+
+
+def build_native():
+    """Compile invidx.c (the native inverted-index writer; byte-identical to the Python path)."""
+    src = os.path.join(_HERE, "invidx.c")
+    if not os.path.exists(_INVIDX_SO) or os.path.getmtime(_INVIDX_SO) < os.path.getmtime(src):
+        subprocess.check_call(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-o", _INVIDX_SO, src])
+
+
+def _native():
+    global _invidx
+    if _invidx is None:
+        build_native()
+        L = ctypes.CDLL(_INVIDX_SO)
+        for f in (L.phip_invidx_size, L.phip_invidx_write):
+            f.restype = ctypes.c_int64
+        L.phip_invidx_size.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+        L.phip_invidx_write.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_int64]
+        L.phip_pack_bits.restype = None
+        L.phip_pack_bits.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
+        _invidx = L
+    return _invidx
+
+
+def inverted_index_bytes(ids: np.ndarray, card: int, run_optimize: bool = True, native: bool = True) -> bytes:
+    """Bitmap inverted index of dict ids (BitmapInvertedIndexWriter layout): native writer, or the
+    Python restatement (``native=False``; kept as the reference the native one is tested against)."""
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    if native:
+        L = _native()
+        size = L.phip_invidx_size(ids.ctypes.data, len(ids), card, int(run_optimize))
+        if size < 0:
+            raise ValueError("invalid dict ids for the inverted index")
+        out = np.empty(size, dtype=np.uint8)
+        if L.phip_invidx_write(ids.ctypes.data, len(ids), card, int(run_optimize), out.ctypes.data, size) != size:
+            raise RuntimeError("inverted index writer failed")
+        return out.tobytes()
+    order = np.argsort(ids, kind="stable")
+    bounds = np.searchsorted(ids[order], np.arange(card + 1), side="left")
+    bitmaps = [roaring.serialize(order[bounds[d]:bounds[d + 1]], run_optimize) for d in range(card)]
+    offsets = np.empty(card + 1, dtype=np.int64)
+    pos = (card + 1) * 4
+    for d, bm in enumerate(bitmaps):
+        offsets[d] = pos
+        pos += len(bm)
+    offsets[card] = pos
+    return offsets.astype(">u4").tobytes() + b"".join(bitmaps)
 
 
 @dataclass
@@ -58,12 +114,19 @@ class ImmutableSegment:
         return list(self.columns.keys())
 
 
-def pack_bits(dict_ids: np.ndarray, bits: int) -> bytes:
-    """MSB-first big-endian packing (FixedBitIntReaderWriter.writeInt semantics)."""
+def pack_bits(dict_ids: np.ndarray, bits: int, native: bool = True) -> bytes:
+    """MSB-first big-endian packing (FixedBitIntReaderWriter.writeInt semantics); native writer, or the
+    numpy restatement (``native=False``) it is tested against."""
     ids = np.asarray(dict_ids, dtype=np.uint32)
     n = len(ids)
     if n == 0:
         return b""
+    if native:
+        L = _native()
+        ids32 = np.ascontiguousarray(ids.view(np.int32))
+        out = np.zeros((n * bits + 7) // 8, dtype=np.uint8)
+        L.phip_pack_bits(ids32.ctypes.data, ctypes.c_int64(n), ctypes.c_int32(bits), out.ctypes.data)
+        return out.tobytes()
     be = ids.astype(">u4").view(np.uint8).reshape(n, 4)
     allbits = np.unpackbits(be, axis=1)[:, 32 - bits:]
     packed = np.packbits(allbits.reshape(-1))
@@ -162,15 +225,6 @@ class SegmentCreator:
             fwd = pack_bits(ids, bits)
         inv = None
         if name in self.inverted and not is_sorted:
-            order = np.argsort(ids, kind="stable")
-            bounds = np.searchsorted(ids[order], np.arange(card + 1), side="left")
-            bitmaps = [roaring.serialize(order[bounds[d]:bounds[d + 1]], self.run_optimize) for d in range(card)]
-            offsets = np.empty(card + 1, dtype=np.int64)
-            pos = (card + 1) * 4
-            for d, bm in enumerate(bitmaps):
-                offsets[d] = pos
-                pos += len(bm)
-            offsets[card] = pos
-            inv = offsets.astype(">u4").tobytes() + b"".join(bitmaps)
+            inv = inverted_index_bytes(ids, card, self.run_optimize)
         meta = ColumnMetadata(name, dt, n, card, bits, is_sorted, True, inv is not None, width)
         return ColumnIndexes(meta, fwd, dict_bytes, inv)

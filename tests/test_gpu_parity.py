@@ -411,3 +411,56 @@ def test_gpu_group_by_high_cardinality(gpu_lib):
     finally:
         for s in segs:
             s.destroy()
+
+
+# ---- config C1: BenchmarkQueries-style segments (tools/bq.py), every query of the GPU subset ----------
+@pytest.fixture(scope="module")
+def bq_segments(gpu_lib):
+    from tools import bq
+    raws = bq.make_segments(250_000, num_segments=2, scenario="EXP(0.001)")
+    segs = [GpuSegment(r) for r in raws]
+    yield raws, segs
+    for s in segs:
+        s.destroy()
+
+
+def _check_vs_oracle(qc, raws, segs):
+    gblk = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, segs).next_block()
+    oblk, exact = executor.execute(qc, raws)
+    assert gblk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+    if not qc.group_by:
+        _assert_intermediates_equal(qc.aggregations, gblk.results, oblk.results, exact)
+    else:
+        assert set(gblk.groups) == set(oblk.groups)
+        for k, v in oblk.groups.items():
+            _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
+
+
+@pytest.mark.parametrize("name", sorted(__import__("tools.bq", fromlist=["QUERIES"]).QUERIES))
+def test_gpu_c1_benchmark_queries_vs_oracle(name, bq_segments):
+    from tools import bq
+    raws, segs = bq_segments
+    _check_vs_oracle(parse(bq.QUERIES[name]), raws, segs)
+
+
+# ---- config C4: 5-predicate AND/OR/NOT over inverted indexes, selectivity sweep (tools/c4.py) ---------
+@pytest.fixture(scope="module")
+def c4_segments(gpu_lib):
+    from tools import c4
+    raws = [c4.make_segment(i, num_rows=1_000_003) for i in range(2)]
+    segs = [GpuSegment(r) for r in raws]
+    yield raws, segs
+    for s in segs:
+        s.destroy()
+
+
+@pytest.mark.parametrize("agg", ["COUNT(*)", "SUM(M), COUNT(*), MAX(C5)"])
+@pytest.mark.parametrize("sel", __import__("tools.c4", fromlist=["SELECTIVITIES"]).SELECTIVITIES)
+def test_gpu_c4_inverted_sweep_vs_oracle(sel, agg, c4_segments):
+    from tools import c4
+    raws, segs = c4_segments
+    qc = parse(c4.query(sel, agg))
+    _check_vs_oracle(qc, raws, segs)
+    # bit-exact doc-id set of the first segment through the filter-only entry point
+    op = GpuInstancePlanMaker().make_instance_plan(qc, [segs[0]])
+    assert np.array_equal(op.filter_bitmap(), _words_from_mask(executor.filter_mask(qc, raws[0])))
