@@ -53,6 +53,7 @@ hipError_t launch_masks_to_words(const uint32_t *, int32_t, int32_t, uint64_t *,
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *, int nblocks, size_t, hipStream_t) {
   if (q.mode == GB_NONE) memset(q.partials, 0, (size_t)nblocks * q.num_aggs * 8);
   else if (q.mode == GB_GLOBAL) q.gb_table[0] = 1;  // one non-empty group
+  else if (q.mode == GB_HASH) { q.gb_table[0] = 1; q.gb_keys[0] = 0; }  // slot 0 holds key 0
   else {
     memset(q.gb_table, 0, (size_t)nblocks * q.tbl_words * 8);
     q.gb_table[0] = 1;
@@ -80,5 +81,9 @@ hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t
 hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t naggs, const int32_t *, const uint64_t *,
                                const uint32_t *, int32_t nhll, int32_t log2m, double *v, int64_t *l, uint8_t *h, hipStream_t) {
   memset(v, 0, ng * naggs * 8); memset(l, 0, ng * naggs * 8); if (nhll) memset(h, 0, ng * nhll * (1 << log2m)); return hipSuccess;
+}
+hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hipStream_t) {
+  for (int64_t i = 0; i < n; i++) slots[i] = (int64_t)keys[slots[i]];
+  return hipSuccess;
 }
 }  // namespace phip

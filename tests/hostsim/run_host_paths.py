@@ -47,6 +47,9 @@ for q in ("SELECT g, h, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTH
           "SELECT SUM(r), AVG(d), DISTINCTCOUNTHLL(g) FROM t WHERE h IN (1, 2) OR m > 0",
           "SELECT COUNT(*) FROM t WHERE NOT (h = 1 AND (g = 'k3' OR d < 0.5))"):
     pm.make_instance_plan(parse(q), gs).next_block()
+os.environ["PHIP_GB_HASH"] = "1"  # the hash-table group-by's host path (allocation, key decode)
+pm.make_instance_plan(parse("SELECT g, h, COUNT(*), SUM(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY g, h"), gs).next_block()
+del os.environ["PHIP_GB_HASH"]
 for g in gs:
     g.destroy()
 for s in segs.values():
