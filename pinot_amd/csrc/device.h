@@ -204,4 +204,14 @@ struct RoaringTask {
   int32_t pad;
 };
 
+// The containers of one (inverted leaf, 65536-doc key) pair: roaring_or_kernel decodes them into an
+// 8 KiB LDS bitmap and writes the key's 1024 doc words once.
+struct RoaringGroup {
+  uint64_t *out_words;   // the leaf's dense doc words
+  int32_t task_begin;    // containers [task_begin, task_end) of the RoaringTask array
+  int32_t task_end;
+  int32_t key;
+  int32_t pad;
+};
+
 }  // namespace phip

@@ -619,36 +619,49 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
 // Roaring containers of the selected dict ids -> OR into dense u64 doc words
 // (BitmapInvertedIndexReader.getDocIds + ImmutableRoaringBitmap.or, InvertedIndexFilterOperator.java:79-95)
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void roaring_or_kernel(const RoaringTask *__restrict__ tasks, int32_t ntasks) {
-  for (int ti = blockIdx.x; ti < ntasks; ti += gridDim.x) {
-    const RoaringTask tk = tasks[ti];
-    uint64_t *out = tk.out_words + (int64_t)tk.key * 1024;  // 65536 docs per container = 1024 words
-    if (tk.kind == 0) {
-      const uint16_t *v = (const uint16_t *)tk.payload;
-      for (int i = threadIdx.x; i < tk.card; i += blockDim.x) {
-        uint32_t x = v[i];
-        atomicOr((unsigned long long *)&out[x >> 6], 1ull << (x & 63));
-      }
-    } else if (tk.kind == 1) {
-      const uint64_t *w = (const uint64_t *)tk.payload;
-      for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-        uint64_t x = w[i];
-        if (x) atomicOr((unsigned long long *)&out[i], x);
-      }
-    } else {
-      const uint16_t *r = (const uint16_t *)tk.payload;
-      const int nruns = tk.card;
-      for (int ri = 0; ri < nruns; ri++) {
-        uint32_t s = r[1 + 2 * ri], e = s + r[2 + 2 * ri];  // inclusive
-        uint32_t ws = s >> 6, we = e >> 6;
-        for (uint32_t wi = ws + threadIdx.x; wi <= we; wi += blockDim.x) {
-          int lo = (wi == ws) ? (int)(s & 63) : 0;
-          int hi = (wi == we) ? (int)(e & 63) : 63;
-          uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
-          atomicOr((unsigned long long *)&out[wi], m);
+// One workgroup per (leaf, key) group: every selected container of that 65536-doc range is OR-ed into
+// an LDS bitmap with LDS atomics (array: one bit per value, bitmap: word OR, run: word masks), then the
+// 1024 words go to HBM with plain coalesced stores -- no global atomics, each word written once.
+__global__ __launch_bounds__(256) void roaring_or_kernel(const RoaringTask *__restrict__ tasks,
+                                                         const RoaringGroup *__restrict__ groups, int32_t ngroups) {
+  __shared__ uint64_t bm[1024];
+  typedef PHIP_LDS uint64_t lds64;
+  for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const RoaringGroup g = groups[gi];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) bm[i] = 0;
+    __syncthreads();
+    for (int ti = g.task_begin; ti < g.task_end; ti++) {
+      const RoaringTask tk = tasks[ti];
+      if (tk.kind == 0) {
+        const uint16_t *v = (const uint16_t *)tk.payload;
+        for (int i = threadIdx.x; i < tk.card; i += blockDim.x) {
+          const uint32_t x = v[i];
+          __hip_atomic_fetch_or((lds64 *)&bm[x >> 6], 1ull << (x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      } else if (tk.kind == 1) {
+        const uint64_t *w = (const uint64_t *)tk.payload;
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+          const uint64_t x = w[i];
+          if (x) __hip_atomic_fetch_or((lds64 *)&bm[i], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      } else {
+        const uint16_t *r = (const uint16_t *)tk.payload;
+        for (int ri = 0; ri < tk.card; ri++) {
+          const uint32_t s = r[1 + 2 * ri], e = s + r[2 + 2 * ri];  // inclusive
+          const uint32_t ws = s >> 6, we = e >> 6;
+          for (uint32_t wi = ws + threadIdx.x; wi <= we; wi += blockDim.x) {
+            const int lo = (wi == ws) ? (int)(s & 63) : 0;
+            const int hi = (wi == we) ? (int)(e & 63) : 63;
+            const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+            __hip_atomic_fetch_or((lds64 *)&bm[wi], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
         }
       }
     }
+    __syncthreads();
+    uint64_t *out = g.out_words + (int64_t)g.key * 1024;  // 65536 docs per container = 1024 words
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) out[i] = bm[i];
+    __syncthreads();
   }
 }
 
@@ -675,9 +688,9 @@ __global__ __launch_bounds__(256) void masks_to_words_kernel(const uint32_t *__r
 // ------------------------------------------------------------------------------------------------
 // host-callable launchers (runtime.cpp)
 // ------------------------------------------------------------------------------------------------
-hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream_t s) {
-  if (ntasks <= 0) return hipSuccess;
-  roaring_or_kernel<<<ntasks < 8192 ? ntasks : 8192, 256, 0, s>>>(tasks, ntasks);
+hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *groups, int32_t ngroups, hipStream_t s) {
+  if (ngroups <= 0) return hipSuccess;
+  roaring_or_kernel<<<ngroups < 16384 ? ngroups : 16384, 256, 0, s>>>(tasks, groups, ngroups);
   return hipGetLastError();
 }
 

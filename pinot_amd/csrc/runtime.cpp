@@ -33,7 +33,7 @@ hipError_t launch_bswap64(uint64_t *p, int64_t n, hipStream_t s);
 hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32_t *ids_tmp, int64_t n, int32_t bits,
                                    uint32_t *words, int64_t nwords, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
-hipError_t launch_roaring_or(const RoaringTask *tasks, int32_t ntasks, hipStream_t s);
+hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *groups, int32_t ngroups, hipStream_t s);
 hipError_t launch_filter(const DevFilter &q, bool conj_only, int nblocks, size_t lds_bytes, hipStream_t s);
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,
                                  hipStream_t s);
@@ -764,7 +764,7 @@ struct Plan {
   size_t filter_lds = 0, agg_lds = 0;
   // device buffers (plan-owned)
   uint8_t *base = nullptr;  // descriptor blob
-  size_t tasks_off = 0, dq_off = 0, kinds_off = 0;
+  size_t tasks_off = 0, dq_off = 0, kinds_off = 0, rgroups_off = 0, num_rgroups = 0;
   void *inv_words = nullptr;
   size_t inv_words_total = 0;
   void *fpart = nullptr, *finals = nullptr, *seg_matched = nullptr, *apart = nullptr, *masks = nullptr;
@@ -1266,11 +1266,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     int32_t rc = P.alloc(inv_words_total * 8, &inv_words);
     if (rc) return rc;
   }
+  std::vector<RoaringGroup> rgroups;
   for (size_t i = 0; i < inv_leaves.size(); i++) {
     const InvLeaf &L = inv_leaves[i];
     const ColumnStore &cs = segs[L.seg]->cols[L.col];
     uint64_t *words = (uint64_t *)inv_words + inv_word_off[i];
     nodes[L.node].aux = words;
+    const size_t first = tasks.size();
     for (int k = 0; k < L.src->count; k++) {
       int32_t id = L.src->ids[k];
       if (id < 0 || id >= cs.card) return fail(PHIP_ERR_INVALID, "inverted dict id %d out of range", id);
@@ -1286,8 +1288,25 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         tasks.push_back(t);
       }
     }
+    // group the leaf's containers by key (one LDS-decoding workgroup per key)
+    std::stable_sort(tasks.begin() + first, tasks.end(),
+                     [](const RoaringTask &a, const RoaringTask &b) { return a.key < b.key; });
+    for (size_t t = first; t < tasks.size();) {
+      size_t e = t;
+      while (e < tasks.size() && tasks[e].key == tasks[t].key) e++;
+      if (e > (size_t)INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "too many inverted-index containers");
+      RoaringGroup g;
+      g.out_words = words;
+      g.task_begin = (int32_t)t;
+      g.task_end = (int32_t)e;
+      g.key = tasks[t].key;
+      g.pad = 0;
+      rgroups.push_back(g);
+      t = e;
+    }
   }
   const size_t tasks_off = tasks.empty() ? 0 : blob.add(tasks.data(), tasks.size() * sizeof(RoaringTask));
+  const size_t rgroups_off = rgroups.empty() ? 0 : blob.add(rgroups.data(), rgroups.size() * sizeof(RoaringGroup));
 
   // ---- filter kernel configuration (filter.hip) -------------------------------------------------
   // Per 2048-doc tile, the wave's ring slot receives the fixed-bit words of every scanned filter column
@@ -1553,6 +1572,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.agg_lds = agg_lds;
   P.base = base;
   P.tasks_off = tasks_off;
+  P.rgroups_off = rgroups_off;
+  P.num_rgroups = rgroups.size();
   P.dq_off = dq_off;
   P.kinds_off = kinds_off;
   P.inv_words = inv_words;
@@ -1605,7 +1626,8 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (nhll && !group_by) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, (size_t)nhll * m_regs * 4, st));
   if (inv_words_total) {
     HIP_TRY(hipMemsetAsync(inv_words, 0, inv_words_total * 8, st));
-    HIP_TRY(launch_roaring_or((const RoaringTask *)(base + tasks_off), (int32_t)tasks.size(), st));
+    HIP_TRY(launch_roaring_or((const RoaringTask *)(base + tasks_off), (const RoaringGroup *)(base + P.rgroups_off),
+                              (int32_t)P.num_rgroups, st));
   }
   if (group_by && dq.mode == GB_HASH) {
     HIP_TRY(hipMemsetAsync(dq.gb_keys, 0xff, (size_t)dq.num_groups * 8, st));  // kHashEmpty

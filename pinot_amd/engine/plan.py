@@ -12,6 +12,7 @@
                          with one phip_query call.
 """
 import ctypes
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Union
 
@@ -70,6 +71,9 @@ def _doc_ranges_for(seg: GpuSegment, column: str, ev: predeval.DictPredicateEval
     return np.asarray(ranges, dtype=np.int32).reshape(-1)
 
 
+INVERTED_COST_RATIO = 0.5  # decode bytes allowed per forward-index byte (measured: tools/configs_bench.py C4)
+
+
 def compile_predicate(seg: GpuSegment, pred) -> object:
     column = pred.column
     m = seg.column_metadata(column)
@@ -83,10 +87,20 @@ def compile_predicate(seg: GpuSegment, pred) -> object:
     if m.is_sorted:
         return _Leaf(_lib.LEAF_DOC_RANGES, column, ids=_doc_ranges_for(seg, column, ev))
     if m.has_inverted_index and pred.type != "RANGE":
-        if ev.kind == "range":
-            ids = np.arange(ev.start, ev.end, dtype=np.int32)
-            return _Leaf(_lib.LEAF_INVERTED, column, ids=ids)
-        return _Leaf(_lib.LEAF_INVERTED, column, exclusive=ev.exclusive, ids=np.asarray(ev.ids, dtype=np.int32))
+        # FilterOperatorUtils picks the inverted index for EQ / IN / NOT_EQ / NOT_IN (:118-131). The GPU
+        # planner keeps that choice unless decoding the selected bitmaps would move more bytes than
+        # streaming the forward index (inverted_cost_ratio x forward bytes): a scan leaf of the same
+        # dict ids gives the identical doc set. PINOT_AMD_INVERTED=always restores the reference choice.
+        ids = (np.arange(ev.start, ev.end, dtype=np.int32) if ev.kind == "range"
+               else np.asarray(ev.ids, dtype=np.int32))
+        fwd = (seg.num_docs * m.bits_per_element + 7) // 8
+        inv_ok = os.environ.get("PINOT_AMD_INVERTED", "") == "always"
+        if not inv_ok:
+            inv_ok = seg.inverted_bytes(column, ids) <= INVERTED_COST_RATIO * fwd
+        if inv_ok:
+            if ev.kind == "range":
+                return _Leaf(_lib.LEAF_INVERTED, column, ids=ids)
+            return _Leaf(_lib.LEAF_INVERTED, column, exclusive=ev.exclusive, ids=ids)
     if ev.kind == "range":
         return _Leaf(_lib.LEAF_DICT_RANGE, column, lo=ev.start, hi=ev.end)
     return _Leaf(_lib.LEAF_DICT_SET, column, exclusive=ev.exclusive, ids=np.asarray(ev.ids, dtype=np.int32))

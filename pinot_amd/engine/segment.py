@@ -22,6 +22,7 @@ class GpuSegment:
         self.num_docs = segment.num_docs
         self._dicts = {}
         self._sorted = {}
+        self._inv_offsets = {}
         cols = list(segment.columns.values())
         descs = (_lib.ColumnDesc * max(len(cols), 1))()
         keep = []
@@ -77,6 +78,16 @@ class GpuSegment:
             d = Dictionary(ci.dictionary, m.data_type, m.cardinality, m.string_width)
             self._dicts[column] = d
         return d
+
+    def inverted_bytes(self, column, dict_ids) -> int:
+        """Bytes of the inverted-index bitmaps of `dict_ids` (the bytes an inverted leaf reads)."""
+        if column not in self._inv_offsets:
+            ci = self.segment.columns[column]
+            card = ci.metadata.cardinality
+            self._inv_offsets[column] = np.frombuffer(ci.inverted[:4 * (card + 1)], dtype=">u4").astype(np.int64)
+        offs = self._inv_offsets[column]
+        ids = np.asarray(dict_ids, dtype=np.int64)
+        return int(np.sum(offs[ids + 1] - offs[ids])) if len(ids) else 0
 
     def sorted_doc_range(self, column, dict_id):
         """SortedIndexReaderImpl.getDocIds(dictId) (SortedIndexReaderImpl.java:114-116): inclusive pair."""

@@ -43,7 +43,7 @@ hipError_t launch_bswap32(uint32_t *, int64_t, hipStream_t) { return hipSuccess;
 hipError_t launch_bswap64(uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }
-hipError_t launch_roaring_or(const RoaringTask *, int32_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_roaring_or(const RoaringTask *, const RoaringGroup *, int32_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_filter(const DevFilter &q, bool, int nblocks, size_t, hipStream_t) {
   memset(q.partials, 0, (size_t)nblocks * 2 * 8);
   if (q.mask_out) memset(q.mask_out, 0, (size_t)q.total_work * 64 * 4);

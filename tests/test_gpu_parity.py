@@ -454,10 +454,14 @@ def c4_segments(gpu_lib):
         s.destroy()
 
 
+@pytest.mark.parametrize("policy", ["cost", "always"])
 @pytest.mark.parametrize("agg", ["COUNT(*)", "SUM(M), COUNT(*), MAX(C5)"])
 @pytest.mark.parametrize("sel", __import__("tools.c4", fromlist=["SELECTIVITIES"]).SELECTIVITIES)
-def test_gpu_c4_inverted_sweep_vs_oracle(sel, agg, c4_segments):
+def test_gpu_c4_inverted_sweep_vs_oracle(sel, agg, policy, c4_segments, monkeypatch):
+    """policy 'always' = the reference's leaf choice (every EQ/IN/NOT leaf on the inverted index);
+    'cost' = the GPU planner's (inverted only while its bitmaps are cheaper than the forward scan)."""
     from tools import c4
+    monkeypatch.setenv("PINOT_AMD_INVERTED", "always" if policy == "always" else "")
     raws, segs = c4_segments
     qc = parse(c4.query(sel, agg))
     _check_vs_oracle(qc, raws, segs)
