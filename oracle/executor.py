@@ -284,6 +284,8 @@ def execute(query, segments):
         stats.num_segments_processed += 1
         stats.num_segments_matched += int(len(docs) > 0)
         per_seg.append((os_, docs))
+    if not query.group_by and any(ag.filter is not None for ag in query.aggregations):
+        return _execute_filtered(query, segments)
     if not query.group_by:
         results, exact = None, None
         for os_, docs in per_seg:
@@ -318,6 +320,49 @@ def execute(query, segments):
                 groups[k] = vals
                 exact_groups[k] = exs
     return GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats), exact_groups
+
+
+def _execute_filtered(query, segments):
+    """FilteredAggregationOperator (pinot-core/.../operator/query/FilteredAggregationOperator.java:67-113):
+    aggregations grouped by their FILTER (unfiltered ones under the main filter), each group evaluated
+    over main AND its filter; numDocsScanned / post-filter entries summed over the groups
+    (AggregationFunctionUtils.buildFilteredAggregationInfos builds the groups)."""
+    from pinot_amd.engine.results import AggregationResultsBlock, ExecutionStatistics, merge_intermediate
+    from pinot_amd.query.context import columns_of
+    infos = {}
+    for i, ag in enumerate(query.aggregations):
+        infos.setdefault(ag.filter, []).append(i)
+    stats = ExecutionStatistics()
+    results = [None] * len(query.aggregations)
+    exact = [None] * len(query.aggregations)
+    first = True
+    for seg in segments:
+        os_ = OracleSegment(seg)
+        base = eval_filter(os_, query.filter)
+        scanned = 0
+        for flt, idxs in infos.items():
+            mask = base if flt is None else (base & eval_filter(os_, flt))
+            docs = np.nonzero(mask)[0]
+            proj = set()
+            for i in idxs:
+                if query.aggregations[i].argument is not None:
+                    proj.update(columns_of(query.aggregations[i].argument))
+            scanned += len(docs)
+            stats.num_entries_scanned_post_filter += len(docs) * len(proj)
+            for i in idxs:
+                ag = query.aggregations[i]
+                v, ex = _agg_segment(os_, ag, docs)
+                if first:
+                    results[i], exact[i] = v, ex
+                else:
+                    results[i] = merge_intermediate(ag.function, results[i], v)
+                    exact[i] = exact[i] + ex if exact[i] is not None and ex is not None else None
+        first = False
+        stats.num_docs_scanned += scanned
+        stats.num_total_docs += seg.num_docs
+        stats.num_segments_processed += 1
+        stats.num_segments_matched += int(scanned > 0)
+    return AggregationResultsBlock(query.aggregations, results, stats), exact
 
 
 def filter_mask(query, segment):

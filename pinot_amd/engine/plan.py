@@ -484,13 +484,69 @@ def _dictionary_values(dv):
     return [x.item() for x in arr]
 
 
+class GpuFilteredAggregationOperator:
+    """FilteredAggregationOperator (pinot-core/.../operator/query/FilteredAggregationOperator.java:67-113)
+    over all segments: the aggregations are grouped by their FILTER clause (unfiltered ones under the
+    main filter), as AggregationFunctionUtils.buildFilteredAggregationInfos does, and every group runs as
+    one GPU combine operator over main AND its filter. Results return in query order; numDocsScanned
+    and the entries scanned are summed over the groups, like the reference operator's statistics."""
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
+        if query.group_by:
+            raise UnsupportedOnGpu("FILTER clause with GROUP BY (FilteredGroupByOperator)")
+        self.query = query
+        self.segments = list(segments)
+        groups = {}
+        for i, ag in enumerate(query.aggregations):
+            groups.setdefault(ag.filter, []).append(i)
+        self.parts = []
+        for flt, idxs in groups.items():
+            if flt is None:
+                f = query.filter
+            elif query.filter is None:
+                f = flt
+            else:
+                f = FilterContext.AND(query.filter, flt)
+            sub = QueryContext(query.table, [], [query.aggregations[i].unfiltered() for i in idxs], f, [],
+                               limit=query.limit, options=dict(query.options))
+            self.parts.append((idxs, GpuCombineOperator(sub, self.segments, num_groups_limit)))
+
+    def next_block(self):
+        results = [None] * len(self.query.aggregations)
+        stats = ExecutionStatistics()
+        scan_ms = device_ms = 0.0
+        for idxs, op in self.parts:
+            blk = op.next_block()
+            for j, i in enumerate(idxs):
+                results[i] = blk.results[j]
+            s = blk.stats
+            stats.num_docs_scanned += s.num_docs_scanned
+            stats.num_entries_scanned_in_filter += s.num_entries_scanned_in_filter
+            stats.num_entries_scanned_post_filter += s.num_entries_scanned_post_filter
+            stats.num_total_docs = s.num_total_docs
+            stats.num_segments_processed = s.num_segments_processed
+            stats.num_segments_matched = max(stats.num_segments_matched, s.num_segments_matched)
+            scan_ms += getattr(blk, "scan_kernel_ms", 0.0) or 0.0
+            device_ms += getattr(blk, "device_ms", 0.0) or 0.0
+        blk = AggregationResultsBlock(self.query.aggregations, results, stats)
+        blk.scan_kernel_ms = scan_ms
+        blk.device_ms = device_ms
+        return blk
+
+    def close(self):
+        for _, op in self.parts:
+            op.close()
+
+
 class GpuInstancePlanMaker:
     """``pinot.server.query.executor.plan.maker.class`` plug-in."""
 
     def __init__(self, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT):
         self.num_groups_limit = num_groups_limit
 
-    def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]) -> GpuCombineOperator:
+    def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]):
         if isinstance(query, str):
             query = parse(query)
+        if any(ag.filter is not None for ag in query.aggregations):
+            return GpuFilteredAggregationOperator(query, segments, self.num_groups_limit)
         return GpuCombineOperator(query, segments, self.num_groups_limit)

@@ -13,7 +13,7 @@ from typing import List
 
 import numpy as np
 
-from ..query.context import Function, Identifier, Literal, QueryContext, SUPPORTED_AGGREGATIONS
+from ..query.context import FilterClause, Function, Identifier, Literal, QueryContext, SUPPORTED_AGGREGATIONS
 from ..spi import DEFAULT_HYPERLOGLOG_LOG2M
 from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock, merge_intermediate
 
@@ -68,8 +68,11 @@ class ResultTable:
 
 
 def _agg_index(query: QueryContext, expr):
+    flt = None
+    if isinstance(expr, FilterClause):
+        expr, flt = expr.function, expr.filter
     for i, a in enumerate(query.aggregations):
-        if isinstance(expr, Function) and expr.name == a.function:
+        if isinstance(expr, Function) and expr.name == a.function and a.filter == flt:
             if a.function == "count" or (expr.args and expr.args[0] == a.argument):
                 return i
     return None

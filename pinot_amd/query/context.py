@@ -38,12 +38,25 @@ class Function:
         return f"{self.name}({','.join(str(a) for a in self.args)})"
 
 
-Expression = Union[Identifier, Literal, Function]
+@dataclass(frozen=True)
+class FilterClause:
+    """`agg(...) FILTER(WHERE ...)`: an aggregation with its own filter (QueryContext's
+    filtered-aggregation pairs, pinot-core/.../query/request/context/QueryContext.java)."""
+    function: "Function"
+    filter: "FilterContext"
+
+    def __str__(self):
+        return f"{self.function} FILTER(WHERE {self.filter})"
+
+
+Expression = Union[Identifier, Literal, Function, FilterClause]
 
 
 def columns_of(expr) -> List[str]:
     if isinstance(expr, Identifier):
         return [expr.name]
+    if isinstance(expr, FilterClause):
+        return columns_of(expr.function)
     if isinstance(expr, Function):
         out = []
         for a in expr.args:
@@ -127,13 +140,16 @@ class AggregationInfo:
     function: str           # canonical lower-case name, e.g. "sum"
     argument: Optional[Expression]  # None for COUNT(*)
     log2m: int = 8
+    filter: Optional["FilterContext"] = None  # FILTER(WHERE ...) of a filtered aggregation
 
     @property
     def result_column_name(self) -> str:
         """AggregationFunction.getResultColumnName(): lower-case function name + argument."""
-        if self.function == "count":
-            return "count(*)"
-        return f"{self.function}({self.argument})"
+        base = "count(*)" if self.function == "count" else f"{self.function}({self.argument})"
+        return base if self.filter is None else f"{base} FILTER(WHERE {self.filter})"
+
+    def unfiltered(self) -> "AggregationInfo":
+        return AggregationInfo(self.function, self.argument, self.log2m)
 
 
 @dataclass

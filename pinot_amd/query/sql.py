@@ -10,7 +10,7 @@ expressions. The reference optimizer's flattening of nested AND/OR
 """
 import re
 
-from .context import (AggregationInfo, FilterContext, Function, Identifier, Literal, OrderByExpression,
+from .context import (AggregationInfo, FilterClause, FilterContext, Function, Identifier, Literal, OrderByExpression,
                       Predicate, PredicateType, QueryContext, SUPPORTED_AGGREGATIONS, UNBOUNDED)
 
 _TOKEN = re.compile(r"""\s*(?:
@@ -280,6 +280,16 @@ class _Parser:
 
     def _select_item(self):
         e = self.expr()
+        if self.peek()[0] == "ident" and str(self.peek()[1]).lower() == "filter":
+            # agg(...) FILTER(WHERE ...) (CalciteSqlParser's FILTER clause -> filtered aggregation)
+            if not (isinstance(e, Function) and e.name in SUPPORTED_AGGREGATIONS):
+                raise SqlError("FILTER applies to an aggregation")
+            self.next()
+            self.expect("op", "(")
+            self.expect("kw", "where")
+            f = self.bool_or()
+            self.expect("op", ")")
+            e = FilterClause(e, f)
         alias = None
         if self.accept("kw", "as"):
             alias = self.next()[1]
@@ -297,7 +307,10 @@ class _Parser:
         return OrderByExpression(e, asc)
 
 
-def _collect_aggs(expr, out):
+def _collect_aggs(expr, out, flt=None):
+    if isinstance(expr, FilterClause):
+        _collect_aggs(expr.function, out, expr.filter)
+        return
     if isinstance(expr, Function):
         if expr.name in SUPPORTED_AGGREGATIONS:
             arg = None
@@ -310,7 +323,7 @@ def _collect_aggs(expr, out):
             log2m = 8
             if expr.name in ("distinctcounthll", "distinctcountrawhll") and len(expr.args) > 1:
                 log2m = int(expr.args[1].value)
-            info = AggregationInfo(expr.name, arg, log2m)
+            info = AggregationInfo(expr.name, arg, log2m, flt)
             if info not in out:
                 out.append(info)
             return
@@ -333,6 +346,8 @@ def parse(sql: str) -> QueryContext:
         _collect_aggs(e, aggs)
         resolved_order.append(OrderByExpression(e, ob.ascending))
     for e, _ in select:
+        if isinstance(e, FilterClause):
+            continue
         if not isinstance(e, Function) or e.name not in SUPPORTED_AGGREGATIONS:
             if group_by and e not in group_by:
                 raise SqlError(f"select expression {e} is neither an aggregation nor a group-by expression")

@@ -24,6 +24,12 @@ SCENARIOS = {"EXP(0.001)": 0.001, "EXP(0.5)": 0.5, "EXP(0.999)": 0.999}
 # BenchmarkQueries' query constants that fall inside the GPU subset (same text; MyTable)
 QUERIES = {
     "SUM_QUERY": "SELECT SUM(RAW_INT_COL) FROM MyTable",
+    "FILTERED_QUERY": "SELECT SUM(INT_COL) FILTER(WHERE INT_COL > 123 AND INT_COL < 599999),"
+                      "MAX(INT_COL) FILTER(WHERE INT_COL > 123 AND INT_COL < 599999) "
+                      "FROM MyTable WHERE NO_INDEX_INT_COL > 5 AND NO_INDEX_INT_COL < 1499999",
+    "FILTERED_MIXED": "SELECT COUNT(*), SUM(RAW_INT_COL) FILTER(WHERE LOW_CARDINALITY_STRING_COL IN ('value1', 'value7')), "
+                      "MIN(NO_INDEX_INT_COL) FILTER(WHERE INT_COL BETWEEN 10 AND 20), "
+                      "COUNT(*) FILTER(WHERE INT_COL BETWEEN 10 AND 20) FROM MyTable WHERE NO_INDEX_INT_COL >= 3 OR INT_COL < 50",
     "RAW_COLUMN_SUMMARY_STATS": "SELECT MIN(RAW_INT_COL), MAX(RAW_INT_COL), COUNT(*) FROM MyTable",
     "FILTERED_SCAN_SUM": "SELECT SUM(INT_COL), MAX(INT_COL) FROM MyTable "
                          "WHERE NO_INDEX_INT_COL > 5 AND NO_INDEX_INT_COL < 1499999",
