@@ -79,6 +79,7 @@ struct StageSrc {
 
 // A leaf of a conjunctive filter program (fast path): a staged scan of one fixed-bit column.
 constexpr int kMaxConj = 6;
+constexpr int kConjSparseMax = 6;     // default per-lane bound of the sparse conjunction walk
 struct ConjLeaf {
   int32_t lds_off;  // staged region in the ring slot
   int32_t bits;
@@ -105,8 +106,9 @@ struct DevSeg {
   int32_t conj;        // > 0: the program is AND of `conj` staged scan leaves (conj_leaf, most selective
                        // first); the filter kernel evaluates it without the stack machine
   int32_t conj_p;      // docs per lane-window of the fast path (1, 2, 4, 8; P * bits <= 32 for every leaf)
-  int32_t conj_sparse;  // 1: leaves 2.. are dict-id ranges, so a tile whose first leaf passes few docs
-                        // may test them per passing doc (SVScanDocIdIterator.applyAnd) instead of per doc
+  int32_t conj_sparse;  // > 0: leaves 2.. are dict-id ranges, so a tile whose first leaf passes at most
+                        // this many docs per lane tests them per passing doc (SVScanDocIdIterator.applyAnd)
+                        // instead of per doc
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];

@@ -361,11 +361,10 @@ __device__ __forceinline__ uint32_t to_lane_major(uint32_t r) {
   }
 }
 
-// Leaves 2.. of a tile whose first leaf passed at most kSparseMax docs in every lane: each passing doc is
+// Leaves 2.. of a tile whose first leaf passed at most seg.conj_sparse docs in every lane: each passing doc is
 // tested against the remaining range leaves on its own (one window read per leaf), the way
 // SVScanDocIdIterator.applyAnd (pinot-core/.../dociditerators/SVScanDocIdIterator.java:114-142) scans
 // only the candidate docs of the preceding AND children. Lanes loop over their set bits together.
-constexpr uint32_t kSparseMax = 6;
 
 template <int P>
 __device__ __forceinline__ uint32_t conj_sparse_rest(cseg_t &seg, const PHIP_LDS uint8_t *slot, uint32_t r) {
@@ -414,7 +413,7 @@ __device__ __forceinline__ uint32_t eval_conj_p(cseg_t &seg, const PHIP_LDS uint
   uint32_t r = conj_leaf_eval<P>((const PHIP_LDS uint32_t *)(slot + L0.lds_off), L0.bits, L0.kind, L0.lo, L0.span,
                                  L0.set_mask);
   if (k > 1) {
-    if (seg.conj_sparse && wave_max_u32((uint32_t)__popc(r)) <= kSparseMax) {
+    if (seg.conj_sparse && wave_max_u32((uint32_t)__popc(r)) <= (uint32_t)seg.conj_sparse) {
       r = conj_sparse_rest<P>(seg, slot, r);
     } else {
       for (int i = 1; i < k; i++) {

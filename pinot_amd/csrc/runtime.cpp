@@ -1384,6 +1384,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       ds.conj_sparse = 1;
       for (size_t i = 1; i < conj.size(); i++) ds.conj_sparse &= conj[i].second.kind == 0 ? 1 : 0;
       if (getenv("PHIP_NO_SPARSE")) ds.conj_sparse = 0;  // measurement override
+      // the value is the per-lane passing-doc bound under which the sparse walk is taken
+      if (ds.conj_sparse) {
+        const char *sm = getenv("PHIP_SPARSE_MAX");  // measurement override
+        ds.conj_sparse = sm ? std::max(1, std::min(32, atoi(sm))) : kConjSparseMax;
+      }
       ds.conj_p = 8;
       for (size_t i = 0; i < conj.size(); i++) {
         ds.conj_leaf[i] = conj[i].second;
