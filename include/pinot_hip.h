@@ -104,6 +104,17 @@ typedef struct phip_segment_desc {
 #define PHIP_LEAF_DICT_SET 3   /* scan forward index: dictId in ids (xor exclusive) */
 #define PHIP_LEAF_DOC_RANGES 4 /* ids = count x (startDoc, endDoc) inclusive, sorted, disjoint */
 #define PHIP_LEAF_INVERTED 5   /* OR of inverted-index bitmaps of ids (xor exclusive) */
+/* Raw (no-dictionary) columns, value-based (RawValueBasedPredicateEvaluator, ScanBasedFilterOperator.java:58-66).
+ * ids points at `count` int32 words holding a phip_raw_range (RAW_RANGE) or count/2 int64 values -- doubles for
+ * FLOAT/DOUBLE columns -- (RAW_SET, xor exclusive). */
+#define PHIP_LEAF_RAW_RANGE 6
+#define PHIP_LEAF_RAW_SET 7
+
+typedef struct phip_raw_range {
+  int64_t lo_int, hi_int; /* INT/LONG columns: lo_int <= v <= hi_int */
+  double lo_real, hi_real; /* FLOAT/DOUBLE columns, with the inclusive flags below */
+  int32_t lo_inclusive, hi_inclusive;
+} phip_raw_range;
 
 typedef struct phip_filter_node {
   int32_t op;           /* PHIP_NODE_* */

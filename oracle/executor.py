@@ -112,8 +112,11 @@ def _read_raw_chunk(buf, dtype, n):
 
 # ----------------------------------------------------------------------------------- filter
 def _literal(m, lit):
+    """Literal converted to the column type (the reference parses predicate values per data type)."""
     if int(m.data_type) == 4:
         return str(lit)
+    if int(m.data_type) == 2:
+        return np.float32(float(lit))  # FLOAT: Float.parseFloat, compared in float32
     return lit
 
 

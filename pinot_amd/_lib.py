@@ -18,7 +18,16 @@ PHIP_ERR_NO_DEVICE = 5
 
 FWD_FIXED_BIT, FWD_SORTED, FWD_RAW_CHUNK = 0, 1, 2
 NODE_LEAF, NODE_AND, NODE_OR, NODE_NOT = 0, 1, 2, 3
-LEAF_MATCH_ALL, LEAF_MATCH_NONE, LEAF_DICT_RANGE, LEAF_DICT_SET, LEAF_DOC_RANGES, LEAF_INVERTED = range(6)
+LEAF_MATCH_ALL, LEAF_MATCH_NONE, LEAF_DICT_RANGE, LEAF_DICT_SET, LEAF_DOC_RANGES, LEAF_INVERTED, LEAF_RAW_RANGE, \
+    LEAF_RAW_SET = range(8)
+
+
+class RawRange(ctypes.Structure):
+    """phip_raw_range (include/pinot_hip.h)."""
+    _fields_ = [("lo_int", ctypes.c_int64), ("hi_int", ctypes.c_int64), ("lo_real", ctypes.c_double),
+                ("hi_real", ctypes.c_double), ("lo_inclusive", ctypes.c_int32), ("hi_inclusive", ctypes.c_int32)]
+
+
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_HLL = range(5)
 EXPR_COLUMN, EXPR_ADD, EXPR_SUB, EXPR_MUL = range(4)
 

@@ -129,7 +129,8 @@ struct DevNode {
   int32_t pad;
   uint64_t set_mask;
   const void *aux;    // DICT_SET: u32 bitset over dict ids; DOC_RANGES: int32 pairs;
-                      // INVERTED: u64 doc bitmap words of the segment (materialised)
+                      // INVERTED: u64 doc bitmap words of the segment (materialised);
+                      // RAW_RANGE: phip_raw_range; RAW_SET: `count` int64 / double values
 };
 
 // Filter kernel launch (K1-K4 of SURVEY.md §2.4).

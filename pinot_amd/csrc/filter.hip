@@ -79,6 +79,13 @@ __device__ __forceinline__ uint32_t range_word(int32_t s, int32_t e, int lane) {
 }
 
 // One leaf over the tile; `valid` = lane-major docs of the tile inside the segment.
+__device__ __forceinline__ int64_t raw_int_at(ccol_t &c, int32_t doc) {
+  return c.type == PHIP_TYPE_LONG ? ((const PHIP_GLB int64_t *)c.raw)[doc] : (int64_t)((const PHIP_GLB int32_t *)c.raw)[doc];
+}
+__device__ __forceinline__ double raw_real_at(ccol_t &c, int32_t doc) {
+  return c.type == PHIP_TYPE_DOUBLE ? ((const PHIP_GLB double *)c.raw)[doc] : (double)((const PHIP_GLB float *)c.raw)[doc];
+}
+
 __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__ n, uint32_t valid, const Tile &t,
                                               uint32_t &scanned) {
   const int lane = lane_id();
@@ -117,6 +124,46 @@ __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__
     }
     if (n->exclusive) r = ~r;
     return valid & r;
+  }
+  if (kind == PHIP_LEAF_RAW_RANGE || kind == PHIP_LEAF_RAW_SET) {
+    // value-based scan of a raw column (RawValueBasedPredicateEvaluator): one coalesced load per 64 docs
+    scanned += (uint32_t)t.valid_docs;
+    ccol_t &c = seg.cols[n->column];
+    const int32_t last = t.valid_docs - 1;
+    const bool real = c.type == PHIP_TYPE_FLOAT || c.type == PHIP_TYPE_DOUBLE;
+    const PHIP_CAS phip_raw_range &rr = *(const PHIP_CAS phip_raw_range *)n->aux;
+    const PHIP_GLB int64_t *set_i = (const PHIP_GLB int64_t *)n->aux;
+    const PHIP_GLB double *set_f = (const PHIP_GLB double *)n->aux;
+    const int64_t lo_i = rr.lo_int, hi_i = rr.hi_int;
+    const double lo_f = rr.lo_real, hi_f = rr.hi_real;
+    const bool lo_in = rr.lo_inclusive != 0, hi_in = rr.hi_inclusive != 0;
+    const bool excl = n->exclusive != 0;
+    uint32_t r = 0;
+    for (int g = 0; g < kTileGroups; g++) {
+      const int32_t doc = t.doc0 + min(g * 64 + lane, last);
+      bool pass;
+      if (!real) {
+        const int64_t v = raw_int_at(c, doc);
+        if (kind == PHIP_LEAF_RAW_RANGE) {
+          pass = v >= lo_i && v <= hi_i;
+        } else {
+          pass = false;
+          for (int k = 0; k < n->count; k++) pass = pass || set_i[k] == v;
+          pass = pass != excl;
+        }
+      } else {
+        const double v = raw_real_at(c, doc);
+        if (kind == PHIP_LEAF_RAW_RANGE) {
+          pass = (lo_in ? v >= lo_f : v > lo_f) && (hi_in ? v <= hi_f : v < hi_f);
+        } else {
+          pass = false;
+          for (int k = 0; k < n->count; k++) pass = pass || set_f[k] == v;
+          pass = pass != excl;
+        }
+      }
+      r = r + r + (uint32_t)pass;
+    }
+    return r & valid;
   }
   // DICT_RANGE / DICT_SET on the bit-packed forward index
   scanned += (uint32_t)t.valid_docs;

@@ -531,7 +531,7 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
   int after;
   switch (n.op) {
     case PHIP_NODE_LEAF:
-      if (n.leaf_kind < PHIP_LEAF_MATCH_ALL || n.leaf_kind > PHIP_LEAF_INVERTED) {
+      if (n.leaf_kind < PHIP_LEAF_MATCH_ALL || n.leaf_kind > PHIP_LEAF_RAW_SET) {
         err = "bad leaf kind";
         return -1;
       }
@@ -540,7 +540,17 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
         err = "leaf column out of range";
         return -1;
       }
-      if ((n.leaf_kind == PHIP_LEAF_DICT_SET || n.leaf_kind == PHIP_LEAF_INVERTED || n.leaf_kind == PHIP_LEAF_DOC_RANGES) &&
+      if (n.leaf_kind == PHIP_LEAF_RAW_RANGE &&
+          (n.ids == nullptr || n.count * 4 != (int32_t)sizeof(phip_raw_range))) {
+        err = "raw range leaf needs a phip_raw_range";
+        return -1;
+      }
+      if (n.leaf_kind == PHIP_LEAF_RAW_SET && (n.count % 2 != 0 || n.count > 2 * 1024)) {
+        err = "raw set leaf: count must be 2 x (values <= 1024)";
+        return -1;
+      }
+      if ((n.leaf_kind == PHIP_LEAF_DICT_SET || n.leaf_kind == PHIP_LEAF_INVERTED || n.leaf_kind == PHIP_LEAF_DOC_RANGES ||
+           n.leaf_kind == PHIP_LEAF_RAW_SET) &&
           n.count > 0 && n.ids == nullptr) {
         err = "leaf ids missing";
         return -1;
@@ -1158,6 +1168,19 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             }
             break;
           }
+          case PHIP_LEAF_RAW_RANGE:
+          case PHIP_LEAF_RAW_SET:
+            if (cs->fwd_kind != PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "raw leaf on dictionary column"); break; }
+            if (cs->type == PHIP_TYPE_STRING) { rc = fail(PHIP_ERR_UNSUPPORTED, "raw STRING predicate"); break; }
+            if (fn.leaf_kind == PHIP_LEAF_RAW_SET) {
+              dn.count = fn.count / 2;  // values
+              if (dn.count == 0) {
+                dn.leaf_kind = fn.exclusive ? PHIP_LEAF_MATCH_ALL : PHIP_LEAF_MATCH_NONE;
+                break;
+              }
+            }
+            aux_fix.push_back({ni, blob.add(fn.ids, (size_t)fn.count * 4)});
+            break;
           case PHIP_LEAF_INVERTED:
             if (cs->inv_begin.empty()) { rc = fail(PHIP_ERR_INVALID, "column %s has no inverted index", cs->name.c_str()); break; }
             inv_leaves.push_back({ni, s, colidx[s][fn.column], &fn});

@@ -12,6 +12,7 @@
                          with one phip_query call.
 """
 import ctypes
+import math
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Union
@@ -20,8 +21,8 @@ import numpy as np
 
 from .. import _lib
 from ..query import predicate as predeval
-from ..query.context import (AggregationInfo, FilterContext, Function, Identifier, Literal, QueryContext,
-                             columns_of)
+from ..query.context import (UNBOUNDED, AggregationInfo, FilterContext, Function, Identifier, Literal,
+                             QueryContext, columns_of)
 from ..query.sql import parse
 from ..spi import DEFAULT_NUM_GROUPS_LIMIT, DataType
 from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock
@@ -71,6 +72,61 @@ def _doc_ranges_for(seg: GpuSegment, column: str, ev: predeval.DictPredicateEval
     return np.asarray(ranges, dtype=np.int32).reshape(-1)
 
 
+def _raw_predicate(column, dt: DataType, pred):
+    """Value-based leaf on a raw column (RawValueBasedPredicateEvaluatorFactory + ScanBasedFilterOperator):
+    literals converted to the column type first (FLOAT literals rounded to float32, as Float.parseFloat);
+    integral ranges folded to closed integer intervals."""
+    if dt == DataType.STRING:
+        raise UnsupportedOnGpu(f"predicate on raw STRING column {column}")
+    real = dt in (DataType.FLOAT, DataType.DOUBLE)
+
+    def conv(v):
+        x = float(v)
+        return float(np.float32(x)) if dt == DataType.FLOAT else x
+
+    if pred.type == "RANGE":
+        rr = _lib.RawRange()
+        rr.lo_int, rr.hi_int = -(1 << 63), (1 << 63) - 1
+        rr.lo_real, rr.hi_real = -math.inf, math.inf
+        rr.lo_inclusive = rr.hi_inclusive = 1
+        if pred.lower != UNBOUNDED:
+            x = conv(pred.lower)
+            if real:
+                rr.lo_real, rr.lo_inclusive = x, int(pred.lower_inclusive)
+            else:
+                v = pred.lower
+                lo = (math.ceil(x) if pred.lower_inclusive else math.floor(x) + 1) if not isinstance(v, int) else \
+                    (v if pred.lower_inclusive else v + 1)
+                rr.lo_int = max(lo, -(1 << 63))
+        if pred.upper != UNBOUNDED:
+            x = conv(pred.upper)
+            if real:
+                rr.hi_real, rr.hi_inclusive = x, int(pred.upper_inclusive)
+            else:
+                v = pred.upper
+                hi = (math.floor(x) if pred.upper_inclusive else math.ceil(x) - 1) if not isinstance(v, int) else \
+                    (v if pred.upper_inclusive else v - 1)
+                rr.hi_int = min(hi, (1 << 63) - 1)
+        if not real and rr.lo_int > rr.hi_int:
+            return _FALSE
+        words = np.frombuffer(bytes(rr), dtype=np.int32).copy()
+        return _Leaf(_lib.LEAF_RAW_RANGE, column, ids=words)
+    exclusive = pred.type in ("NOT_EQ", "NOT_IN")
+    vals = []
+    for v in pred.values:
+        x = conv(v)
+        if real:
+            vals.append(x)
+        elif float(x).is_integer():
+            vals.append(int(v) if isinstance(v, int) else int(x))
+    if len(vals) > 1024:
+        raise UnsupportedOnGpu("raw IN list longer than 1024 values")
+    if not vals:
+        return _TRUE if exclusive else _FALSE
+    arr = np.asarray(vals, dtype=np.float64 if real else np.int64)
+    return _Leaf(_lib.LEAF_RAW_SET, column, exclusive=exclusive, ids=arr.view(np.int32).copy())
+
+
 INVERTED_COST_RATIO = 0.5  # decode bytes allowed per forward-index byte (measured: tools/configs_bench.py C4)
 
 
@@ -78,7 +134,7 @@ def compile_predicate(seg: GpuSegment, pred) -> object:
     column = pred.column
     m = seg.column_metadata(column)
     if not m.has_dictionary:
-        raise UnsupportedOnGpu(f"predicate on raw (no-dictionary) column {column}")
+        return _raw_predicate(column, m.data_type, pred)
     ev = predeval.evaluate(pred, seg.dictionary(column))
     if ev.always_false:
         return _FALSE
@@ -120,7 +176,7 @@ def compile_filter(seg: GpuSegment, fc: Optional[FilterContext]):
             return _FALSE
         if _is_const(c, _FALSE):
             return _TRUE
-        if isinstance(c, _Leaf) and c.kind in (_lib.LEAF_DICT_SET, _lib.LEAF_INVERTED):
+        if isinstance(c, _Leaf) and c.kind in (_lib.LEAF_DICT_SET, _lib.LEAF_INVERTED, _lib.LEAF_RAW_SET):
             return _Leaf(c.kind, c.column, c.lo, c.hi, not c.exclusive, c.ids)
         return _Node(_lib.NODE_NOT, [c])
     kids = [compile_filter(seg, c) for c in fc.children]
@@ -133,7 +189,8 @@ def compile_filter(seg: GpuSegment, fc: Optional[FilterContext]):
         if len(kids) == 1:
             return kids[0]
         # evaluation order (FilterOperatorUtils :205-252): sorted < bitmap < scan
-        prio = {_lib.LEAF_DOC_RANGES: 0, _lib.LEAF_INVERTED: 1, _lib.LEAF_DICT_RANGE: 3, _lib.LEAF_DICT_SET: 3}
+        prio = {_lib.LEAF_DOC_RANGES: 0, _lib.LEAF_INVERTED: 1, _lib.LEAF_DICT_RANGE: 3, _lib.LEAF_DICT_SET: 3,
+                _lib.LEAF_RAW_RANGE: 3, _lib.LEAF_RAW_SET: 3}
         kids.sort(key=lambda k: prio.get(k.kind, 2) if isinstance(k, _Leaf) else (4 if k.op == _lib.NODE_AND else 5))
         return _Node(_lib.NODE_AND, kids)
     if fc.type == "OR":
@@ -159,7 +216,7 @@ def _flatten(tree, col_index, out, keep):
         if tree.ids is not None:
             ids = np.ascontiguousarray(tree.ids, dtype=np.int32)
             keep.append(ids)
-            n.count = len(ids) // 2 if tree.kind == _lib.LEAF_DOC_RANGES else len(ids)
+            n.count = len(ids) // 2 if tree.kind == _lib.LEAF_DOC_RANGES else len(ids)  # RAW_*: int32 words
             n.ids = ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
         out.append(n)
         return

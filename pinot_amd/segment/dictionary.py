@@ -34,6 +34,8 @@ class Dictionary:
         if self.data_type.is_integral:
             f = float(value)
             return int(value) if f == int(f) else f
+        if self.data_type == DataType.FLOAT:
+            return float(np.float32(float(value)))  # FloatDictionary: Float.parseFloat of the literal
         return float(value)
 
     def insertion_index_of(self, value) -> int:

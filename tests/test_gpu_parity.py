@@ -468,3 +468,35 @@ def test_gpu_c4_inverted_sweep_vs_oracle(sel, agg, policy, c4_segments, monkeypa
     # bit-exact doc-id set of the first segment through the filter-only entry point
     op = GpuInstancePlanMaker().make_instance_plan(qc, [segs[0]])
     assert np.array_equal(op.filter_bitmap(), _words_from_mask(executor.filter_mask(qc, raws[0])))
+
+
+# ---- raw (no-dictionary) columns in filters: value-based scan leaves (RAW_RANGE / RAW_SET) ----------
+RAW_FILTERS = [
+    "ri BETWEEN -1000 AND 250000", "ri > 5.5 AND ri <= 100000", "ri IN (3, 7, 11, -5, 2.5)", "ri NOT IN (3, 7)",
+    "rl >= 1099511627776 OR rl < -5", "rl = 42", "rf > 0.1 AND rf < 0.7", "rf = 0.25", "rf IN (0.1, 0.5)",
+    "rd >= 0.5", "rd < 0.25 OR NOT (ri BETWEEN 0 AND 1000000 AND rd > 0.9)", "d IN (1, 2) AND rd <> 0.5",
+]
+
+
+@pytest.mark.parametrize("flt", RAW_FILTERS)
+def test_gpu_raw_column_filters(flt, gpu_lib):
+    rng = np.random.default_rng(77)
+    n = 2048 * 13 + 77
+    c = SegmentCreator("rawf", no_dictionary_columns=["ri", "rl", "rf", "rd"])
+    c.add_column("ri", DataType.INT, rng.integers(-2000, 2_000_000, n))
+    c.add_column("rl", DataType.LONG, np.where(rng.random(n) < 0.01, 42, rng.integers(-2 ** 41, 2 ** 41, n)))
+    c.add_column("rf", DataType.FLOAT, np.round(rng.random(n), 2).astype(np.float32))
+    c.add_column("rd", DataType.DOUBLE, np.round(rng.random(n), 3))
+    c.add_column("d", DataType.INT, rng.integers(0, 5, n))
+    raw = c.build()
+    seg = GpuSegment(raw)
+    try:
+        qc = parse("SELECT COUNT(*), SUM(ri), MAX(rd) FROM t WHERE " + flt)
+        blk = GpuInstancePlanMaker().make_instance_plan(qc, [seg]).next_block()
+        oblk, ex = executor.execute(qc, [raw])
+        assert blk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+        _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
+        words = GpuInstancePlanMaker().make_instance_plan(qc, [seg]).filter_bitmap()
+        assert np.array_equal(words, _words_from_mask(executor.filter_mask(qc, raw)))
+    finally:
+        seg.destroy()

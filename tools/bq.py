@@ -33,6 +33,8 @@ QUERIES = {
     "RAW_COLUMN_SUMMARY_STATS": "SELECT MIN(RAW_INT_COL), MAX(RAW_INT_COL), COUNT(*) FROM MyTable",
     "FILTERED_SCAN_SUM": "SELECT SUM(INT_COL), MAX(INT_COL) FROM MyTable "
                          "WHERE NO_INDEX_INT_COL > 5 AND NO_INDEX_INT_COL < 1499999",
+    "FILTERING_SCAN_QUERY": "SELECT SUM(RAW_INT_COL) FROM MyTable WHERE RAW_INT_COL BETWEEN 1 AND 10",
+    "FILTERING_BITMAP_SCAN_COUNT": "SELECT COUNT(*) FROM MyTable WHERE INT_COL = 1 AND RAW_INT_COL IN (0, 1, 2)",
     "COUNT_RANGE_SCAN": "SELECT COUNT(*) FROM MyTable WHERE NO_INDEX_INT_COL BETWEEN 10 AND 2000",
     "COUNT_OVER_BITMAP_INDEX_IN": "SELECT COUNT(*) FROM MyTable WHERE INT_COL IN (0, 1, 2, 3, 4, 5, 7, 9, 10)",
     "COUNT_OVER_BITMAP_INDEX_EQUALS": "SELECT COUNT(*) FROM MyTable WHERE LOW_CARDINALITY_STRING_COL = 'value1'",
