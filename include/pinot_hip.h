@@ -60,7 +60,8 @@
 /* ---- forward index encodings -------------------------------------------------------------- */
 #define PHIP_FWD_FIXED_BIT 0 /* FixedBitSVForwardIndexWriter: ceil(N*b/8) BE bytes, MSB first */
 #define PHIP_FWD_SORTED 1    /* SortedIndexReaderImpl: card x (start,end) BE int32, inclusive */
-#define PHIP_FWD_RAW_CHUNK 2 /* BaseChunkForwardIndexWriter v2/v3, PASS_THROUGH fixed-width */
+#define PHIP_FWD_RAW_CHUNK 2 /* BaseChunkForwardIndexWriter v2/v3 fixed-width chunks: PASS_THROUGH, or SNAPPY / LZ4 /
+                              * LZ4_LENGTH_PREFIXED decoded on the GPU at load (ZSTANDARD / GZIP -> UNSUPPORTED) */
 
 typedef struct phip_column_desc {
   const char *name;

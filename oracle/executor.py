@@ -98,15 +98,27 @@ class OracleSegment:
 
 
 def _read_raw_chunk(buf, dtype, n):
+    """FixedByteChunkSVForwardIndexReader over PASS_THROUGH or compressed chunks: chunk k spans
+    [offset_k, offset_{k+1}) (the last one runs to the end of the buffer) and decodes to
+    docs_k x entry bytes (BaseChunkForwardIndexReader.java:60-111,204-232)."""
     h = np.frombuffer(buf, dtype=">i4", count=7)
     version, num_chunks, per_chunk, entry, total, comp, data_hdr = [int(x) for x in h]
-    assert comp == 0 and total == n
+    assert total == n and comp in (0, 1, 3, 4), (total, comp)
     osz = 4 if version == 2 else 8
     offs = np.frombuffer(buf, dtype=">i4" if osz == 4 else ">i8", count=num_chunks, offset=data_hdr)
+    raw = np.frombuffer(buf, dtype=np.uint8)
     parts = []
     for k in range(num_chunks):
         docs = min(per_chunk, n - k * per_chunk)
-        parts.append(np.frombuffer(buf, dtype=_BE[dtype], count=docs, offset=int(offs[k])))
+        if comp == 0:
+            parts.append(np.frombuffer(buf, dtype=_BE[dtype], count=docs, offset=int(offs[k])))
+            continue
+        end = int(offs[k + 1]) if k + 1 < num_chunks else len(buf)
+        src = np.ascontiguousarray(raw[int(offs[k]):end])
+        dst = np.empty(max(docs * entry, 1), dtype=np.uint8)
+        got = _oracle_lib().oracle_chunk_decode(comp, src.ctypes.data, len(src), dst.ctypes.data, docs * entry)
+        assert got == docs * entry, f"chunk {k}: decoded {got} bytes, expected {docs * entry}"
+        parts.append(dst[:docs * entry].view(_BE[dtype]))
     return np.concatenate(parts).astype(_NATIVE[dtype]) if parts else np.zeros(0, _NATIVE[dtype])
 
 

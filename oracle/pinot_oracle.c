@@ -242,3 +242,118 @@ double oracle_block_sum_f64(const double *vals, int64_t n, int32_t block) {
   }
   return holder;
 }
+
+/* --------------------------------------------------------------------------------------------
+ * Compressed raw chunks (ChunkCompressionType SNAPPY=1, LZ4=3, LZ4_LENGTH_PREFIXED=4;
+ * pinot-segment-spi/.../compression/ChunkCompressionType.java:22). Pinot hands each chunk to a
+ * third-party codec: lz4-java 1.8.0 (LZ4Decompressor.java: safeDecompressor().decompress over the
+ * LZ4 *block* format; LZ4WithLengthDecompressor.java: LZ4DecompressorWithLength = 4-byte
+ * little-endian original length, then the block) and snappy-java 1.1.10.7 (SnappyDecompressor.java:
+ * Snappy.uncompress over the raw snappy format). Restated from the published format specs
+ * (lz4 "Block format description", snappy "format_description.txt"). Return the decoded length,
+ * or -1 on malformed input / overflow of `cap`.
+ * ------------------------------------------------------------------------------------------ */
+int64_t oracle_lz4_block_decode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  while (ip < n) {
+    uint32_t tok = src[ip++];
+    int64_t lit = tok >> 4;
+    if (lit == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (ip + lit > n || op + lit > cap) return -1;
+    for (int64_t i = 0; i < lit; i++) dst[op + i] = src[ip + i];
+    ip += lit;
+    op += lit;
+    if (ip == n) break; /* the last sequence carries literals only */
+    if (ip + 2 > n) return -1;
+    int64_t off = (int64_t)src[ip] | ((int64_t)src[ip + 1] << 8);
+    ip += 2;
+    if (off == 0 || off > op) return -1;
+    int64_t ml = tok & 15;
+    if (ml == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        ml += b;
+      } while (b == 255);
+    }
+    ml += 4;
+    if (op + ml > cap) return -1;
+    for (int64_t i = 0; i < ml; i++) dst[op + i] = dst[op + i - off]; /* overlapping copy repeats */
+    op += ml;
+  }
+  return op;
+}
+
+int64_t oracle_snappy_decode(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  uint64_t ulen = 0;
+  for (int shift = 0;; shift += 7) {
+    if (ip >= n || shift > 28) return -1;
+    uint32_t b = src[ip++];
+    ulen |= (uint64_t)(b & 0x7f) << shift;
+    if (!(b & 0x80)) break;
+  }
+  if ((int64_t)ulen > cap) return -1;
+  while (ip < n) {
+    uint32_t tag = src[ip++];
+    int64_t len, off;
+    if ((tag & 3) == 0) {
+      len = (tag >> 2) + 1;
+      if (len > 60) {
+        int nb = (int)len - 60;
+        if (ip + nb > n) return -1;
+        len = 0;
+        for (int k = 0; k < nb; k++) len |= (int64_t)src[ip + k] << (8 * k);
+        len += 1;
+        ip += nb;
+      }
+      if (ip + len > n || op + len > (int64_t)ulen) return -1;
+      for (int64_t i = 0; i < len; i++) dst[op + i] = src[ip + i];
+      ip += len;
+      op += len;
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (ip + 1 > n) return -1;
+      len = 4 + ((tag >> 2) & 7);
+      off = ((int64_t)(tag >> 5) << 8) | src[ip];
+      ip += 1;
+    } else if ((tag & 3) == 2) {
+      if (ip + 2 > n) return -1;
+      len = (tag >> 2) + 1;
+      off = (int64_t)src[ip] | ((int64_t)src[ip + 1] << 8);
+      ip += 2;
+    } else {
+      if (ip + 4 > n) return -1;
+      len = (tag >> 2) + 1;
+      off = (int64_t)le32(src + ip);
+      ip += 4;
+    }
+    if (off == 0 || off > op || op + len > (int64_t)ulen) return -1;
+    for (int64_t i = 0; i < len; i++) dst[op + i] = dst[op + i - off];
+    op += len;
+  }
+  return op == (int64_t)ulen ? op : -1;
+}
+
+/* One chunk of a compressed fixed-byte forward index -> its decoded bytes
+ * (BaseChunkForwardIndexReader.decompressChunk, BaseChunkForwardIndexReader.java:204-232). */
+int64_t oracle_chunk_decode(int32_t codec, const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
+  if (codec == 1) return oracle_snappy_decode(src, n, dst, cap);
+  if (codec == 3) return oracle_lz4_block_decode(src, n, dst, cap);
+  if (codec == 4) {
+    if (n < 4) return -1;
+    int64_t want = (int64_t)le32(src);
+    int64_t got = oracle_lz4_block_decode(src + 4, n - 4, dst, cap);
+    return got == want ? got : -1;
+  }
+  return -1;
+}

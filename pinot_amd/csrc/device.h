@@ -197,6 +197,15 @@ struct DevAggQuery {
   uint32_t *hash_overflow;  // set to 1 when a probe sequence found no slot (host reports an error)
 };
 
+// One compressed chunk of a raw fixed-byte forward index (BaseChunkForwardIndexReader.java:204-232):
+// `csize` bytes at blob + src decode to `usize` BE bytes, stored byte-swapped at out + dst.
+struct RawChunk {
+  uint64_t src;
+  uint64_t dst;
+  uint32_t csize;
+  uint32_t usize;
+};
+
 // One Roaring container of one selected dictionary id, OR-ed into a segment's dense doc words.
 struct RoaringTask {
   const uint8_t *payload;

@@ -66,3 +66,196 @@ hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32
 }
 
 }  // namespace phip
+
+namespace phip {
+
+// ---- compressed raw chunks (ChunkCompressionType SNAPPY=1, LZ4=3, LZ4_LENGTH_PREFIXED=4) ----------------
+// Decoded ONCE at pin time into the resident raw layout (HBM holds the decoded values; every query then
+// reads them like a PASS_THROUGH column). One single-wave workgroup per chunk: the compressed bytes are
+// staged into LDS with dword loads, the sequence stream is parsed wave-uniformly (bytes broadcast from
+// LDS, readfirstlane keeps the parse state in SGPRs), literal and match bytes are copied by the 64 lanes
+// in parallel into an LDS output buffer, and the chunk is stored with the BE->LE swap fused into
+// coalesced 4/8-byte stores. An LZ4 / snappy match copy with offset < length repeats a period of `off`
+// bytes, so byte j of the copy reads out[op - off + j % off]: every source byte is already written,
+// and the copy needs no rounds. Malformed input (bad offsets, overruns, a decoded length other than
+// docs x entry) sets *err = chunk + 1 and that chunk is not stored; the host fails the load.
+// Formats: lz4 block format (lz4-java LZ4SafeDecompressor, LZ4Decompressor.java), lz4-java
+// LZ4DecompressorWithLength (4-byte LE length + block, LZ4WithLengthDecompressor.java), snappy raw
+// format (snappy-java Snappy.uncompress, SnappyDecompressor.java).
+__device__ __forceinline__ uint32_t lds_byte(const uint8_t *p, int i) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)p[i]);
+}
+
+template <int kCodec>
+__device__ __forceinline__ int decode_chunk(const uint8_t *__restrict__ in, int n, uint8_t *__restrict__ out, int cap,
+                                            int lane) {
+  int ip = 0, op = 0;
+  if (kCodec == 1) {  // snappy: varint32 uncompressed length, then tagged elements
+    uint32_t ulen = 0;
+    for (int shift = 0;; shift += 7) {
+      if (ip >= n || shift > 28) return -1;
+      uint32_t b = lds_byte(in, ip++);
+      ulen |= (b & 0x7fu) << shift;
+      if (!(b & 0x80u)) break;
+    }
+    if (ulen != (uint32_t)cap) return -1;
+    while (ip < n) {
+      uint32_t tag = lds_byte(in, ip++);
+      uint32_t len, off;
+      if ((tag & 3u) == 0) {
+        len = (tag >> 2) + 1;
+        if (len > 60) {
+          int nb = (int)len - 60;
+          if (ip + nb > n) return -1;
+          len = 0;
+          for (int k = 0; k < nb; k++) len |= lds_byte(in, ip + k) << (8 * k);
+          len += 1;
+          ip += nb;
+          if (len == 0) return -1;  // 2^32 wrapped
+        }
+        if (len > (uint32_t)(n - ip) || len > (uint32_t)(cap - op)) return -1;
+        for (int i = lane; i < (int)len; i += 64) out[op + i] = in[ip + i];
+        ip += (int)len;
+        op += (int)len;
+        continue;
+      }
+      if ((tag & 3u) == 1) {
+        if (ip + 1 > n) return -1;
+        len = 4 + ((tag >> 2) & 7u);
+        off = ((tag >> 5) << 8) | lds_byte(in, ip);
+        ip += 1;
+      } else if ((tag & 3u) == 2) {
+        if (ip + 2 > n) return -1;
+        len = (tag >> 2) + 1;
+        off = lds_byte(in, ip) | (lds_byte(in, ip + 1) << 8);
+        ip += 2;
+      } else {
+        if (ip + 4 > n) return -1;
+        len = (tag >> 2) + 1;
+        off = lds_byte(in, ip) | (lds_byte(in, ip + 1) << 8) | (lds_byte(in, ip + 2) << 16) | (lds_byte(in, ip + 3) << 24);
+        ip += 4;
+      }
+      if (off == 0 || off > (uint32_t)op || len > (uint32_t)(cap - op)) return -1;
+      __syncthreads();  // earlier literal/match bytes from every lane are visible
+      for (int i = lane; i < (int)len; i += 64) {
+        int j = off >= len ? i : (int)((uint32_t)i % off);
+        out[op + i] = out[op - (int)off + j];
+      }
+      op += (int)len;
+    }
+    return op;
+  }
+  // LZ4 block format
+  while (ip < n) {
+    uint32_t tok = lds_byte(in, ip++);
+    int lit = (int)(tok >> 4);
+    if (lit == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = lds_byte(in, ip++);
+        lit += (int)b;
+      } while (b == 255 && lit < (1 << 30));
+    }
+    if (lit > n - ip || lit > cap - op) return -1;
+    for (int i = lane; i < lit; i += 64) out[op + i] = in[ip + i];
+    ip += lit;
+    op += lit;
+    if (ip == n) break;  // last sequence: literals only
+    if (ip + 2 > n) return -1;
+    int off = (int)(lds_byte(in, ip) | (lds_byte(in, ip + 1) << 8));
+    ip += 2;
+    if (off == 0 || off > op) return -1;
+    int ml = (int)(tok & 15u);
+    if (ml == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = lds_byte(in, ip++);
+        ml += (int)b;
+      } while (b == 255 && ml < (1 << 30));
+    }
+    ml += 4;
+    if (ml > cap - op) return -1;
+    __syncthreads();
+    for (int i = lane; i < ml; i += 64) {
+      int j = off >= ml ? i : (int)((uint32_t)i % (uint32_t)off);
+      out[op + i] = out[op - off + j];
+    }
+    op += ml;
+  }
+  return op;
+}
+
+template <int kCodec, int kEntry>
+__global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restrict__ blob,
+                                                          const RawChunk *__restrict__ chunks, int32_t nchunks,
+                                                          int32_t out_cap, uint8_t *__restrict__ out,
+                                                          int32_t *__restrict__ err) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  uint8_t *lout = lds;
+  uint8_t *lin = lds + out_cap;
+  const int lane = threadIdx.x;
+  for (int32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint64_t src = chunks[c].src, dst = chunks[c].dst;
+    const int csize = (int)chunks[c].csize, usize = (int)chunks[c].usize;
+    const int head = (int)(src & 3u);
+    const uint32_t *sw = (const uint32_t *)(blob + (src - head));
+    const int nw = (head + csize + 3) >> 2;
+    for (int i = lane; i < nw; i += 64) ((uint32_t *)lin)[i] = sw[i];
+    __syncthreads();
+    const uint8_t *in = lin + head;
+    int n = csize, got;
+    if (kCodec == 4) {
+      int want = n < 4 ? -2 : (int)(lds_byte(in, 0) | (lds_byte(in, 1) << 8) | (lds_byte(in, 2) << 16) | (lds_byte(in, 3) << 24));
+      got = n < 4 ? -1 : decode_chunk<3>(in + 4, n - 4, lout, usize, lane);
+      if (got != want) got = -1;
+    } else {
+      got = decode_chunk<kCodec>(in, n, lout, usize, lane);
+    }
+    __syncthreads();
+    if (got != usize) {
+      if (lane == 0) atomicMax(err, c + 1);
+    } else if (kEntry == 8) {
+      uint64_t *o = (uint64_t *)(out + dst);
+      const uint32_t *w = (const uint32_t *)lout;
+      for (int i = lane; i < usize / 8; i += 64)
+        o[i] = ((uint64_t)__builtin_bswap32(w[2 * i]) << 32) | __builtin_bswap32(w[2 * i + 1]);
+    } else {
+      uint32_t *o = (uint32_t *)(out + dst);
+      const uint32_t *w = (const uint32_t *)lout;
+      for (int i = lane; i < usize / 4; i += 64) o[i] = __builtin_bswap32(w[i]);
+    }
+    __syncthreads();  // LDS reused by the next chunk
+  }
+}
+
+template <int kCodec>
+static hipError_t launch_chunk_decode_codec(int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
+                                            int32_t out_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s) {
+  const int grid = nchunks < (1 << 20) ? nchunks : (1 << 20);
+  if (lds > 65536) {  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
+    hipError_t e = hipFuncSetAttribute(entry == 8 ? (const void *)chunk_decode_kernel<kCodec, 8>
+                                                  : (const void *)chunk_decode_kernel<kCodec, 4>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+    if (e != hipSuccess) return e;
+  }
+  if (entry == 8)
+    chunk_decode_kernel<kCodec, 8><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, out, err);
+  else
+    chunk_decode_kernel<kCodec, 4><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, out, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
+                               int32_t out_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+  switch (codec) {
+    case 1: return launch_chunk_decode_codec<1>(entry, blob, chunks, nchunks, out_cap, lds, out, err, s);
+    case 3: return launch_chunk_decode_codec<3>(entry, blob, chunks, nchunks, out_cap, lds, out, err, s);
+    case 4: return launch_chunk_decode_codec<4>(entry, blob, chunks, nchunks, out_cap, lds, out, err, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace phip

@@ -30,6 +30,8 @@
 namespace phip {
 hipError_t launch_bswap32(uint32_t *p, int64_t n, hipStream_t s);
 hipError_t launch_bswap64(uint64_t *p, int64_t n, hipStream_t s);
+hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
+                               int32_t out_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s);
 hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32_t *ids_tmp, int64_t n, int32_t bits,
                                    uint32_t *words, int64_t nwords, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
@@ -461,26 +463,74 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
     int32_t version = (int32_t)be32(h), num_chunks = (int32_t)be32(h + 4), per_chunk = (int32_t)be32(h + 8);
     int32_t entry = (int32_t)be32(h + 12), total = (int32_t)be32(h + 16), comp = (int32_t)be32(h + 20);
     int32_t data_hdr = (int32_t)be32(h + 24);
-    if (comp != 0) return fail(PHIP_ERR_UNSUPPORTED, "column %s: compressed chunks (type %d) are not on the GPU path", c.name, comp);
+    // ChunkCompressionType (ChunkCompressionType.java:22): PASS_THROUGH 0, SNAPPY 1, LZ4 3, LZ4_LENGTH_PREFIXED 4
+    // are decoded on the GPU; ZSTANDARD 2 and GZIP 5 (entropy-coded) stay on the Java path.
+    if (comp != 0 && comp != 1 && comp != 3 && comp != 4)
+      return fail(PHIP_ERR_UNSUPPORTED, "column %s: chunk compression type %d (ZSTANDARD/GZIP) is not on the GPU path",
+                  c.name, comp);
     if (entry != type_width(c.data_type) || total != n || per_chunk <= 0 ||
         num_chunks != ceil_div(n, per_chunk) || (version < 2 || version > 3))
       return fail(PHIP_ERR_INVALID, "column %s: bad chunk header", c.name);
     const int osz = version == 2 ? 4 : 8;
-    if ((uint64_t)data_hdr + (uint64_t)num_chunks * osz > c.forward_bytes)
+    const uint64_t hdr_end = (uint64_t)data_hdr + (uint64_t)num_chunks * osz;
+    if (data_hdr < 28 || hdr_end > c.forward_bytes)
       return fail(PHIP_ERR_INVALID, "column %s: chunk offsets truncated", c.name);
     void *p;
     int32_t rc = dev_alloc(seg, (uint64_t)std::max<int64_t>(n, 1) * entry + 16, &p);
     if (rc) return rc;
     cs.raw = p;
-    for (int32_t k = 0; k < num_chunks; k++) {
-      uint64_t off = osz == 4 ? be32(h + data_hdr + 4 * k) : be64(h + data_hdr + 8 * k);
-      int64_t docs = std::min<int64_t>(per_chunk, n - (int64_t)k * per_chunk);
-      if (off + (uint64_t)docs * entry > c.forward_bytes) return fail(PHIP_ERR_INVALID, "column %s: chunk %d overflow", c.name, k);
-      HIP_TRY(hipMemcpyAsync((uint8_t *)p + (int64_t)k * per_chunk * entry, h + off, docs * entry,
-                             hipMemcpyHostToDevice, st));
+    auto chunk_off = [&](int32_t k) -> uint64_t { return osz == 4 ? be32(h + data_hdr + 4 * k) : be64(h + data_hdr + 8 * k); };
+    if (comp == 0) {
+      for (int32_t k = 0; k < num_chunks; k++) {
+        uint64_t off = chunk_off(k);
+        int64_t docs = std::min<int64_t>(per_chunk, n - (int64_t)k * per_chunk);
+        if (off + (uint64_t)docs * entry > c.forward_bytes) return fail(PHIP_ERR_INVALID, "column %s: chunk %d overflow", c.name, k);
+        HIP_TRY(hipMemcpyAsync((uint8_t *)p + (int64_t)k * per_chunk * entry, h + off, docs * entry,
+                               hipMemcpyHostToDevice, st));
+      }
+      if (entry == 4) HIP_TRY(launch_bswap32((uint32_t *)p, n, st));
+      else HIP_TRY(launch_bswap64((uint64_t *)p, n, st));
+    } else if (num_chunks > 0) {
+      // chunk k spans [offset_k, offset_{k+1}), the last one to the end of the buffer
+      // (BaseChunkForwardIndexReader.decompressChunk, BaseChunkForwardIndexReader.java:204-232)
+      std::vector<RawChunk> chunks(num_chunks);
+      const uint64_t first = chunk_off(0);
+      uint32_t max_c = 0, max_u = 0;
+      for (int32_t k = 0; k < num_chunks; k++) {
+        const uint64_t off = chunk_off(k), end = k + 1 < num_chunks ? chunk_off(k + 1) : c.forward_bytes;
+        if (off < hdr_end || end < off || end > c.forward_bytes || end - off > (1u << 30))
+          return fail(PHIP_ERR_INVALID, "column %s: chunk %d offsets out of order", c.name, k);
+        const int64_t docs = std::min<int64_t>(per_chunk, n - (int64_t)k * per_chunk);
+        chunks[k].src = off - first;
+        chunks[k].dst = (uint64_t)k * per_chunk * entry;
+        chunks[k].csize = (uint32_t)(end - off);
+        chunks[k].usize = (uint32_t)(docs * entry);
+        max_c = std::max(max_c, chunks[k].csize);
+        max_u = std::max(max_u, chunks[k].usize);
+      }
+      const uint32_t out_cap = (uint32_t)round_up(max_u, 16);
+      const size_t lds = out_cap + round_up(max_c + 8, 16);
+      if (lds > 163840 - 1024)
+        return fail(PHIP_ERR_UNSUPPORTED, "column %s: chunks of %u -> %u bytes exceed the 159 KiB LDS decode window",
+                    c.name, max_c, max_u);
+      const uint64_t blob_bytes = c.forward_bytes - first;
+      void *blob, *table, *err;
+      HIP_TRY(hipMalloc(&blob, blob_bytes + 16));
+      temps.push_back(blob);
+      HIP_TRY(hipMalloc(&table, sizeof(RawChunk) * num_chunks));
+      temps.push_back(table);
+      HIP_TRY(hipMalloc(&err, 4));
+      temps.push_back(err);
+      HIP_TRY(hipMemsetAsync(err, 0, 4, st));
+      HIP_TRY(hipMemcpyAsync(blob, h + first, blob_bytes, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(table, chunks.data(), sizeof(RawChunk) * num_chunks, hipMemcpyHostToDevice, st));
+      HIP_TRY(launch_chunk_decode(comp, entry, (const uint8_t *)blob, (const RawChunk *)table, num_chunks,
+                                  (int32_t)out_cap, lds, (uint8_t *)p, (int32_t *)err, st));
+      int32_t bad = 0;
+      HIP_TRY(hipMemcpyAsync(&bad, err, 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      if (bad) return fail(PHIP_ERR_INVALID, "column %s: malformed compressed chunk %d (type %d)", c.name, bad - 1, comp);
     }
-    if (entry == 4) HIP_TRY(launch_bswap32((uint32_t *)p, n, st));
-    else HIP_TRY(launch_bswap64((uint64_t *)p, n, st));
   }
   seg.by_name[cs.name] = (int)seg.cols.size();
   seg.cols.push_back(std::move(cs));
@@ -1642,7 +1692,6 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   void *seg_matched = P.seg_matched, *inv_words = P.inv_words, *gtab = P.gtab, *ghll = P.ghll;
   void *fpart = P.fpart, *apart = P.apart, *slab = P.slab, *hslab = P.hslab, *masks = P.masks, *fo = P.fo;
   const size_t inv_words_total = P.inv_words_total, tasks_off = P.tasks_off, dq_off = P.dq_off;
-  const std::vector<RoaringTask> &tasks = P.tasks;
   const std::vector<DevSeg> &dsegs = P.dsegs;
   const int filter_blocks = P.filter_blocks, agg_blocks = P.agg_blocks;
   const size_t filter_lds = P.filter_lds, agg_lds = P.agg_lds;

@@ -155,30 +155,65 @@ def _sorted_unique(values: np.ndarray, dt: DataType):
     return uniq, ids.astype(np.int32)
 
 
-def _chunk_forward(values: np.ndarray, dt: DataType, docs_per_chunk: int = 1000, version: int = 3) -> bytes:
-    """Fixed-byte chunk forward index, PASS_THROUGH (compression type 0)."""
+# ChunkCompressionType (pinot-segment-spi/.../compression/ChunkCompressionType.java:22)
+CHUNK_COMPRESSION = {"PASS_THROUGH": 0, "SNAPPY": 1, "ZSTANDARD": 2, "LZ4": 3, "LZ4_LENGTH_PREFIXED": 4, "GZIP": 5}
+
+
+def _compress_chunk(chunk: bytes, codec: int) -> bytes:
+    """One chunk through the codec Pinot's writer uses (BaseChunkForwardIndexWriter.writeChunk,
+    BaseChunkForwardIndexWriter.java:175-200). The reference binds lz4-java / snappy-java; here the
+    same published block formats come from Arrow's bundled liblz4 / libsnappy ("lz4_raw" = LZ4 block
+    format without a frame). LZ4_LENGTH_PREFIXED prepends the 4-byte little-endian original length
+    (lz4-java LZ4CompressorWithLength)."""
+    import pyarrow as pa
+    if codec == 0:
+        return chunk
+    if codec == 1:
+        return pa.compress(chunk, codec="snappy", asbytes=True)
+    if codec in (3, 4):
+        body = pa.compress(chunk, codec="lz4_raw", asbytes=True)
+        return (len(chunk).to_bytes(4, "little") + body) if codec == 4 else body
+    if codec == 2:
+        return pa.compress(chunk, codec="zstd", asbytes=True)
+    raise NotImplementedError(f"chunk compression {codec}")
+
+
+def _chunk_forward(values: np.ndarray, dt: DataType, docs_per_chunk: int = 1000, version: int = 3,
+                   compression: str = "PASS_THROUGH") -> bytes:
+    """Fixed-byte chunk forward index (BaseChunkForwardIndexWriter.java:40-60,130-200): 7-int header,
+    chunk offsets (int for v2, long for v3), then each chunk through its codec; offsets are absolute."""
+    codec = CHUNK_COMPRESSION[compression]
     n = len(values)
     entry = np.dtype(dt.numpy_be).itemsize
     num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
     off_size = 4 if version == 2 else 8
     header_size = 7 * 4 + num_chunks * off_size
-    header = np.array([version, num_chunks, docs_per_chunk, entry, n, 0, 7 * 4], dtype=">i4").tobytes()
+    header = np.array([version, num_chunks, docs_per_chunk, entry, n, codec, 7 * 4], dtype=">i4").tobytes()
     data = np.asarray(values, dtype=dt.numpy_be).tobytes()
-    offsets = []
+    offsets, chunks = [], []
     pos = header_size
     for c in range(num_chunks):
+        lo = c * docs_per_chunk * entry
+        body = _compress_chunk(data[lo:lo + min(docs_per_chunk, n - c * docs_per_chunk) * entry], codec)
         offsets.append(pos)
-        pos += min(docs_per_chunk, n - c * docs_per_chunk) * entry
+        chunks.append(body)
+        pos += len(body)
     offs = np.asarray(offsets, dtype=">i4" if version == 2 else ">i8").tobytes()
-    return header + offs + data
+    return header + offs + b"".join(chunks)
 
 
 class SegmentCreator:
     """Builds an ImmutableSegment from column arrays (``SegmentIndexCreationDriverImpl`` role)."""
 
     def __init__(self, name: str, inverted_index_columns: Sequence[str] = (),
-                 no_dictionary_columns: Sequence[str] = (), run_optimize_bitmaps: bool = True):
+                 no_dictionary_columns: Sequence[str] = (), run_optimize_bitmaps: bool = True,
+                 raw_compression=None, docs_per_chunk: int = 1000, raw_version: int = 3):
+        """raw_compression: column -> ChunkCompressionType name for no-dictionary columns
+        (PASS_THROUGH when absent, the METRIC default of ForwardIndexType.java:144-150)."""
         self.name = name
+        self.compression = dict(raw_compression or {})
+        self.docs_per_chunk = docs_per_chunk
+        self.raw_version = raw_version
         self.inverted = set(inverted_index_columns)
         self.raw = set(no_dictionary_columns)
         self.run_optimize = run_optimize_bitmaps
@@ -208,7 +243,8 @@ class SegmentCreator:
             if dt == DataType.STRING:
                 raise NotImplementedError("raw STRING forward index is out of scope")
             meta = ColumnMetadata(name, dt, n, 0, 0, False, False, False)
-            return ColumnIndexes(meta, _chunk_forward(vals, dt))
+            return ColumnIndexes(meta, _chunk_forward(vals, dt, self.docs_per_chunk, self.raw_version,
+                                                      self.compression.get(name, "PASS_THROUGH")))
         uniq, ids = _sorted_unique(vals, dt)
         card = len(uniq)
         dict_bytes, width = _encode_dictionary(uniq, dt)
