@@ -308,14 +308,23 @@ __device__ __forceinline__ uint32_t conj_range(const PHIP_LDS uint32_t *wl, uint
       const uint32_t win = __builtin_amdgcn_alignbit(x[k], y[k], s);
 #pragma unroll
       for (int j = 0; j < P; j++) {
-        const uint32_t f = j == 0 ? win : (win << (j * B));
+        // field j moved to the top and offset by -LO in one v_lshl_add_u32 (3 VALU per doc, not 4)
         uint32_t d;
-        asm("v_sub_u32 %[d], %[w], %[lo]\n\t"
-            "v_cmp_gt_u32 vcc, %[sp], %[d]\n\t"
-            "v_addc_co_u32 %[r], vcc, %[r], %[r], vcc"
-            : [r] "+v"(r), [d] "=&v"(d)
-            : [w] "v"(f), [lo] "s"(LO), [sp] "s"(SPAN)
-            : "vcc");
+        if (j == 0) {
+          asm("v_sub_u32 %[d], %[w], %[lo]\n\t"
+              "v_cmp_gt_u32 vcc, %[sp], %[d]\n\t"
+              "v_addc_co_u32 %[r], vcc, %[r], %[r], vcc"
+              : [r] "+v"(r), [d] "=&v"(d)
+              : [w] "v"(win), [lo] "s"(LO), [sp] "s"(SPAN)
+              : "vcc");
+        } else {
+          asm("v_lshl_add_u32 %[d], %[w], %[sh], %[nlo]\n\t"
+              "v_cmp_gt_u32 vcc, %[sp], %[d]\n\t"
+              "v_addc_co_u32 %[r], vcc, %[r], %[r], vcc"
+              : [r] "+v"(r), [d] "=&v"(d)
+              : [w] "v"(win), [sh] "i"(j * B), [nlo] "s"(0u - LO), [sp] "s"(SPAN)
+              : "vcc");
+        }
       }
     }
   }
