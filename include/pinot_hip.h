@@ -161,6 +161,19 @@ typedef struct phip_query_desc {
   const phip_aggregation *aggregations;
   const int32_t *group_by_columns; /* indices into columns */
   int64_t num_groups_limit;        /* InstancePlanMakerImplV2 numGroupsLimit (default 100,000) */
+  /* Server-level trim of a group-by with ORDER BY on one aggregation (IndexedTable.finish ->
+   * TableResizer.getTopRecords, GroupByUtils.java:96-140): when trim_size > 0 and more groups than trim_size
+   * exist, only the top trim_size groups by aggregations[order_by_aggregation] (Double.compare order,
+   * descending when order_by_desc) are returned; ties at the boundary keep the lowest group key.
+   * order_by_aggregation = -1 disables it. */
+  int32_t order_by_aggregation;
+  int32_t order_by_desc;
+  int64_t trim_size;               /* max(5 * limit, minServerGroupTrimSize) (GroupByUtils.java:55-58) */
+  /* ORDER BY on group-by columns instead (takes precedence when > 0): entry j = k + 1 (ASC) or -(k + 1)
+   * (DESC) for group-by column k; the query-global dictionaries are value-sorted, so id order is value order. */
+  int32_t num_order_by_keys;
+  int32_t reserved0;
+  const int32_t *order_by_keys;
 } phip_query_desc;
 
 /* ---- results ------------------------------------------------------------------------------
@@ -188,6 +201,8 @@ typedef struct phip_result {
   const int32_t *group_keys;
   double scan_kernel_ms; /* device time of the fused filter/aggregate kernel(s) */
   double device_ms;      /* device time of the whole query on the stream */
+  int32_t num_groups_trimmed; /* 1 when the group set was trimmed to phip_query_desc.trim_size */
+  int32_t reserved;
 } phip_result;
 
 typedef struct phip_dictionary_view {

@@ -74,7 +74,10 @@ class QueryDesc(ctypes.Structure):
                 ("filter_offsets", ctypes.POINTER(ctypes.c_int32)), ("filter_nodes", ctypes.POINTER(FilterNode)),
                 ("num_aggregations", ctypes.c_int32), ("num_group_by", ctypes.c_int32),
                 ("aggregations", ctypes.POINTER(Aggregation)), ("group_by_columns", ctypes.POINTER(ctypes.c_int32)),
-                ("num_groups_limit", ctypes.c_int64)]
+                ("num_groups_limit", ctypes.c_int64),
+                ("order_by_aggregation", ctypes.c_int32), ("order_by_desc", ctypes.c_int32),
+                ("trim_size", ctypes.c_int64), ("num_order_by_keys", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("order_by_keys", ctypes.POINTER(ctypes.c_int32))]
 
 
 class Result(ctypes.Structure):
@@ -85,7 +88,8 @@ class Result(ctypes.Structure):
                 ("num_groups", ctypes.c_int64), ("num_group_by", ctypes.c_int32), ("num_hll", ctypes.c_int32),
                 ("values", ctypes.POINTER(ctypes.c_double)), ("long_values", ctypes.POINTER(ctypes.c_int64)),
                 ("hll_registers", ctypes.POINTER(ctypes.c_uint8)), ("group_keys", ctypes.POINTER(ctypes.c_int32)),
-                ("scan_kernel_ms", ctypes.c_double), ("device_ms", ctypes.c_double)]
+                ("scan_kernel_ms", ctypes.c_double), ("device_ms", ctypes.c_double),
+                ("num_groups_trimmed", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class DictionaryView(ctypes.Structure):

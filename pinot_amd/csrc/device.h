@@ -197,6 +197,16 @@ struct DevAggQuery {
   uint32_t *hash_overflow;  // set to 1 when a probe sequence found no slot (host reports an error)
 };
 
+// ORDER BY on group-by columns for the device trim (trim.hip)
+constexpr int kMaxOrderKeys = 8;
+struct KeyOrder {
+  int32_t num_group_by;
+  int32_t num_keys;
+  int32_t gb[kMaxOrderKeys];    // group-by index of ORDER BY expression j
+  int32_t desc[kMaxOrderKeys];
+  int64_t card[kMaxOrderKeys];  // query-global cardinality of group-by column k
+};
+
 // One compressed chunk of a raw fixed-byte forward index (BaseChunkForwardIndexReader.java:204-232):
 // `csize` bytes at blob + src decode to `usize` BE bytes, stored byte-swapped at out + dst.
 struct RawChunk {

@@ -30,6 +30,12 @@
 namespace phip {
 hipError_t launch_bswap32(uint32_t *p, int64_t n, hipStream_t s);
 hipError_t launch_bswap64(uint64_t *p, int64_t n, hipStream_t s);
+hipError_t launch_trim_order(const double *vals, const int64_t *keys, const KeyOrder *ko, int64_t n, int32_t naggs,
+                             int32_t agg, int32_t desc, void *scratch, size_t *scratch_bytes, const int32_t **order_out,
+                             hipStream_t s);
+hipError_t launch_trim_gather(const int32_t *order, int64_t k, int32_t naggs, int64_t hll_bytes, const int64_t *keys,
+                              const double *vals, const int64_t *longs, const uint8_t *hll, int64_t *keys_out,
+                              double *vals_out, int64_t *longs_out, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
                                int32_t out_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s);
 hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32_t *ids_tmp, int64_t n, int32_t bits,
@@ -817,6 +823,10 @@ struct Plan {
   std::vector<std::shared_ptr<Device::Remap>> gb_dicts;
   int nseg = 0, naggs = 0, nhll = 0, log2m = 0, m_regs = 0, num_group_by = 0, num_projected = 0;
   int64_t num_groups_limit = 0, total_work = 0, total_docs = 0, docs_in_work = 0;
+  int32_t order_agg = -1, order_desc = 0;  // server-level trim (phip_query_desc.order_by_aggregation)
+  int32_t order_nkeys = 0;                 // > 0: ORDER BY group-by columns (order_keys)
+  int32_t order_keys[kMaxOrderKeys] = {};
+  int64_t trim_size = 0;
   bool has_filter = false, need_agg = false, need_mask = false, group_by = false, conj_only = false;
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
@@ -1633,6 +1643,25 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.num_group_by = q->num_group_by;
   P.num_projected = num_projected;
   P.num_groups_limit = q->num_groups_limit;
+  if (q->trim_size > 0 && q->num_order_by_keys > 0) {
+    if (q->num_order_by_keys > kMaxOrderKeys || q->num_group_by > kMaxOrderKeys || !q->order_by_keys)
+      return fail(PHIP_ERR_UNSUPPORTED, "device trim: at most %d ORDER BY / group-by columns", kMaxOrderKeys);
+    for (int j = 0; j < q->num_order_by_keys; j++) {
+      const int32_t e = q->order_by_keys[j], k = (e > 0 ? e : -e) - 1;
+      if (e == 0 || k >= q->num_group_by) return fail(PHIP_ERR_INVALID, "order_by_keys[%d] = %d out of range", j, e);
+      P.order_keys[j] = e;
+    }
+    P.order_nkeys = q->num_order_by_keys;
+    P.trim_size = q->trim_size;
+  } else if (q->trim_size > 0 && q->order_by_aggregation >= 0) {
+    if (q->order_by_aggregation >= q->num_aggregations)
+      return fail(PHIP_ERR_INVALID, "order_by_aggregation %d out of range", q->order_by_aggregation);
+    const int32_t f = q->aggregations[q->order_by_aggregation].function;
+    if (f == PHIP_AGG_HLL) return fail(PHIP_ERR_UNSUPPORTED, "device trim by a DISTINCTCOUNTHLL intermediate");
+    P.order_agg = q->order_by_aggregation;
+    P.order_desc = q->order_by_desc ? 1 : 0;
+    P.trim_size = q->trim_size;
+  }
   P.total_work = total_work;
   P.total_docs = total_docs;
   P.docs_in_work = 0;
@@ -1833,6 +1862,41 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     if (dq.mode == GB_HASH) {
       HIP_TRY(launch_hash_keys((int64_t *)keys, ngroups, dq.gb_keys, st));
       HIP_TRY(hipMemcpyAsync(&overflow, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
+    }
+    if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0)) {
+      // ORDER BY <aggregation> with more groups than trimSize: keep the top trimSize on the device
+      // (IndexedTable.finish -> TableResizer.getTopRecords), so only those records cross PCIe.
+      size_t sbytes = 0;
+      const int32_t *order = nullptr;
+      KeyOrder ko{};
+      ko.num_group_by = P.num_group_by;
+      ko.num_keys = P.order_nkeys;
+      for (int k = 0; k < P.num_group_by; k++) ko.card[k] = gb_dicts[k]->card;
+      for (int j = 0; j < P.order_nkeys; j++) {
+        ko.gb[j] = (P.order_keys[j] > 0 ? P.order_keys[j] : -P.order_keys[j]) - 1;
+        ko.desc[j] = P.order_keys[j] < 0;
+      }
+      const KeyOrder *kop = P.order_nkeys > 0 ? &ko : nullptr;
+      HIP_TRY(launch_trim_order(nullptr, nullptr, kop, ngroups, naggs, P.order_agg, P.order_desc, nullptr, &sbytes,
+                                &order, st));
+      void *scratch, *k2, *v2, *l2, *h2 = nullptr;
+      const int64_t k = P.trim_size;
+      if ((rc = dev->ws.get("trim_scratch", sbytes, &scratch))) return rc;
+      if ((rc = dev->ws.get("trim_keys", (size_t)k * 8, &k2))) return rc;
+      if ((rc = dev->ws.get("trim_vals", (size_t)k * std::max(naggs, 1) * 8, &v2))) return rc;
+      if ((rc = dev->ws.get("trim_longs", (size_t)k * std::max(naggs, 1) * 8, &l2))) return rc;
+      if (nhll && (rc = dev->ws.get("trim_hll", (size_t)k * nhll * m_regs, &h2))) return rc;
+      HIP_TRY(launch_trim_order((const double *)ov, (const int64_t *)keys, kop, ngroups, naggs, P.order_agg,
+                                P.order_desc, scratch, &sbytes, &order, st));
+      HIP_TRY(launch_trim_gather(order, k, naggs, nhll ? (int64_t)nhll * m_regs : 0, (const int64_t *)keys,
+                                 (const double *)ov, (const int64_t *)ol, (const uint8_t *)oh, (int64_t *)k2,
+                                 (double *)v2, (int64_t *)l2, (uint8_t *)h2, st));
+      keys = k2;
+      ov = v2;
+      ol = l2;
+      oh = h2;
+      ngroups = k;
+      r.num_groups_trimmed = 1;
     }
     std::vector<int64_t> hkeys(ngroups);
     impl->values.resize(ngroups * naggs);

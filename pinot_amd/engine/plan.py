@@ -359,7 +359,43 @@ class GpuCombineOperator:
         q.num_group_by = len(self.query.group_by)
         q.group_by_columns = gb
         q.num_groups_limit = self.num_groups_limit
+        q.order_by_aggregation, q.order_by_desc, q.trim_size, okeys = self._trim_spec()
+        if okeys:
+            arr = (ctypes.c_int32 * len(okeys))(*okeys)
+            keep.append(arr)
+            q.num_order_by_keys = len(okeys)
+            q.order_by_keys = arr
         return q
+
+    def _trim_spec(self):
+        """Server-level trim of GroupByUtils.createIndexedTableForCombineOperator (GroupByUtils.java:96-140):
+        with ORDER BY the combine keeps trimSize = getTableCapacity(limit, minServerGroupTrimSize)
+        = max(5 * limit, 5000) records (:55-58; default minServerGroupTrimSize 5000,
+        InstancePlanMakerImplV2.java:92), ordered by the ORDER BY. The device trims when the ORDER BY is a
+        single SUM/MIN/MAX/COUNT aggregation or only group-by columns; otherwise every group is returned (the broker's ORDER BY +
+        LIMIT gives the same final rows)."""
+        from .reduce import _agg_index
+        q = self.query
+        none = (-1, 0, 0, [])
+        if not q.group_by or not q.order_by:
+            return none
+        min_trim = int(q.options.get("minServerGroupTrimSize", 5000))
+        if min_trim <= 0:  # trim disabled (GroupByUtils.java:108)
+            return none
+        trim = min(max(5 * int(q.limit), min_trim), 2 ** 31 - 1)
+        gb = [str(e) for e in q.group_by]
+        if all(str(ob.expression) in gb for ob in q.order_by) and len(q.order_by) <= 8 and len(gb) <= 8:
+            keys = [(gb.index(str(ob.expression)) + 1) * (1 if ob.ascending else -1) for ob in q.order_by]
+            return -1, 0, trim, keys
+        if len(q.order_by) != 1:
+            return none
+        i = _agg_index(q, q.order_by[0].expression)
+        if i is None:
+            return none
+        f, s = self.mapping[i]
+        if f not in ("sum", "min", "max", "count") or q.aggregations[i].filter is not None:
+            return none
+        return int(s), int(not q.order_by[0].ascending), trim, []
 
     def filter_bitmap(self) -> np.ndarray:
         """BaseFilterOperator.getTrues for a single segment, as 64-doc bitmap words."""
@@ -506,6 +542,7 @@ class GpuCombineOperator:
                     groups[key] = intermediates(g)
                 blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
                                           bool(r.num_groups_limit_reached))
+                blk.num_groups_trimmed = bool(r.num_groups_trimmed)
             blk.device_ms = r.device_ms
             blk.scan_kernel_ms = r.scan_kernel_ms
             return blk
