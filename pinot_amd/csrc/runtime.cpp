@@ -2184,6 +2184,8 @@ PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *word
   phip_query_desc q = *query;
   q.num_aggregations = 0;
   q.num_group_by = 0;
+  q.trim_size = 0;  // filter only: no groups to trim
+  q.num_order_by_keys = 0;
   phip_result *r = nullptr;
   int32_t rc;
   {

@@ -41,6 +41,14 @@ const char *hipGetErrorString(hipError_t) { return "stub"; }
 namespace phip {
 hipError_t launch_bswap32(uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_bswap64(uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_trim_order(const double *, const int64_t *, const KeyOrder *, int64_t n, int32_t, int32_t, int32_t, void *scratch,
+                             size_t *bytes, const int32_t **order, hipStream_t) {
+  if (!scratch) *bytes = (size_t)n * 24 + 256;
+  else *order = (const int32_t *)((uint8_t *)scratch + (size_t)n * 16);
+  return hipSuccess;
+}
+hipError_t launch_trim_gather(const int32_t *, int64_t, int32_t, int64_t, const int64_t *, const double *, const int64_t *,
+                              const uint8_t *, int64_t *, double *, int64_t *, uint8_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_chunk_decode(int, int, const uint8_t *, const RawChunk *, int32_t, int32_t, size_t, uint8_t *, int32_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }
