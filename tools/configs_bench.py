@@ -88,6 +88,17 @@ def time_gpu(qc, gsegs, reps, warmup):
     op = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, gsegs)
     wall, kern, dev = [], [], []
     ngroups = None
+    if not hasattr(op, "run_raw"):  # FILTER(WHERE) aggregations: several prepared plans per block
+        for i in range(warmup + reps):
+            t0 = time.perf_counter()
+            blk = op.next_block()
+            t1 = time.perf_counter()
+            if i >= warmup:
+                wall.append((t1 - t0) * 1e3)
+                kern.append(blk.scan_kernel_ms)
+                dev.append(blk.device_ms)
+        op.close()
+        return float(np.median(wall)), float(np.median(kern)), float(np.median(dev)), blk.stats.num_docs_scanned, None
     for i in range(warmup + reps):
         t0 = time.perf_counter()
         res = op.run_raw()
