@@ -78,6 +78,13 @@ __device__ __forceinline__ uint32_t range_word(int32_t s, int32_t e, int lane) {
   return span32(31 - g_hi, 31 - g_lo);
 }
 
+// P-layout leaf evaluation and its transpose to lane-major (the conjunctive fast path, below)
+template <int P>
+__device__ __forceinline__ uint32_t conj_leaf_eval(const PHIP_LDS uint32_t *w, int bits, int kind, uint32_t lo,
+                                                uint32_t span, uint64_t set);
+template <int P>
+__device__ __forceinline__ uint32_t to_lane_major(uint32_t r);
+
 // One leaf over the tile; `valid` = lane-major docs of the tile inside the segment.
 __device__ __forceinline__ int64_t raw_int_at(ccol_t &c, int32_t doc) {
   return c.type == PHIP_TYPE_LONG ? ((const PHIP_GLB int64_t *)c.raw)[doc] : (int64_t)((const PHIP_GLB int32_t *)c.raw)[doc];
@@ -171,7 +178,15 @@ __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__
   if (n->lds_off >= 0) {
     const PHIP_LDS uint32_t *w = (const PHIP_LDS uint32_t *)(t.stage + n->lds_off);
     uint32_t r;
-    if (kind == PHIP_LEAF_DICT_RANGE) {
+    if ((kind == PHIP_LEAF_DICT_RANGE || n->small_set) && B <= 16) {
+      // narrow columns: P docs per lane-window (1/P of the LDS reads), then one transpose to lane-major
+      const uint32_t LO = (uint32_t)n->lo << (32 - B);
+      const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - B);
+      const int k = kind == PHIP_LEAF_DICT_RANGE ? 0 : 1;
+      if (B <= 4) r = to_lane_major<8>(conj_leaf_eval<8>(w, B, k, LO, SPAN, n->set_mask));
+      else if (B <= 8) r = to_lane_major<4>(conj_leaf_eval<4>(w, B, k, LO, SPAN, n->set_mask));
+      else r = to_lane_major<2>(conj_leaf_eval<2>(w, B, k, LO, SPAN, n->set_mask));
+    } else if (kind == PHIP_LEAF_DICT_RANGE) {
       const uint32_t LO = (uint32_t)n->lo << (32 - B);
       const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - B);
       r = scan_range(w, B, LO, SPAN);
