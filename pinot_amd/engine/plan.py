@@ -377,7 +377,7 @@ class GpuCombineOperator:
         from .reduce import _agg_index
         q = self.query
         none = (-1, 0, 0, [])
-        if not q.group_by or not q.order_by:
+        if not q.group_by or not q.order_by or not getattr(self, "device_trim", True):
             return none
         min_trim = int(q.options.get("minServerGroupTrimSize", 5000))
         if min_trim <= 0:  # trim disabled (GroupByUtils.java:108)
@@ -635,12 +635,17 @@ class GpuFilteredAggregationOperator:
 class GpuInstancePlanMaker:
     """``pinot.server.query.executor.plan.maker.class`` plug-in."""
 
-    def __init__(self, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT):
+    def __init__(self, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT, device_trim: bool = True):
+        """device_trim=False: return every group (a rank of a multi-GPU server, whose partial groups must
+        meet in ``distributed.allreduce_block`` BEFORE the server-level trim, ``reduce.trim_groups``)."""
         self.num_groups_limit = num_groups_limit
+        self.device_trim = device_trim
 
     def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]):
         if isinstance(query, str):
             query = parse(query)
         if any(ag.filter is not None for ag in query.aggregations):
             return GpuFilteredAggregationOperator(query, segments, self.num_groups_limit)
-        return GpuCombineOperator(query, segments, self.num_groups_limit)
+        op = GpuCombineOperator(query, segments, self.num_groups_limit)
+        op.device_trim = self.device_trim
+        return op

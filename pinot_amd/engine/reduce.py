@@ -138,6 +138,38 @@ def reduce_blocks(query: QueryContext, blocks) -> ResultTable:
     return ResultTable(names, rows, stats, limit_reached)
 
 
+def trim_size(query: QueryContext) -> int:
+    """GroupByUtils.getTableCapacity(limit, minServerGroupTrimSize) (GroupByUtils.java:55-58,96-140); 0 = no trim."""
+    min_trim = int(query.options.get("minServerGroupTrimSize", 5000))
+    if not query.group_by or not query.order_by or min_trim <= 0:
+        return 0
+    return min(max(5 * int(query.limit), min_trim), 2 ** 31 - 1)
+
+
+def trim_groups(query: QueryContext, block):
+    """Server-level trim on the host (IndexedTable.finish -> TableResizer.getTopRecords): the merged
+    group-by block of a multi-GPU server keeps its top trimSize groups by the full ORDER BY. Ties at the
+    boundary keep the smallest keys (the reference's choice is heap-order dependent)."""
+    k = trim_size(query)
+    if not k or len(block.groups) <= k:
+        return block
+    gb_index = {str(e): i for i, e in enumerate(query.group_by)}
+    recs = [(key, [final_result(a.function, x) for a, x in zip(query.aggregations, v)]) for key, v in block.groups.items()]
+    recs.sort(key=lambda r: r[0])
+
+    def value_of(expr, rec):
+        if str(expr) in gb_index:
+            return rec[0][gb_index[str(expr)]]
+        return rec[1][_agg_index(query, expr)]
+
+    for ob in reversed(query.order_by):
+        recs.sort(key=lambda r: value_of(ob.expression, r), reverse=not ob.ascending)
+    keep = {r[0] for r in recs[:k]}
+    block.groups = {key: v for key, v in block.groups.items() if key in keep}
+    block.num_groups_trimmed = True
+    return block
+
+
 def broker_response(plan_maker, query, segments) -> ResultTable:
     """BaseQueriesTest.getBrokerResponse: server over ``segments``, reduced as OFFLINE + REALTIME."""
     from ..query.sql import parse

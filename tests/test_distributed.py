@@ -17,6 +17,8 @@ QUERIES = [
     "SELECT g, h, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTHLL(g) FROM t WHERE m > 0 "
     "GROUP BY g, h ORDER BY g, h LIMIT 100000",
     "SELECT g, COUNT(*) FROM t WHERE h = 5 GROUP BY g ORDER BY g LIMIT 100000",
+    # server-level trim AFTER the cross-GPU merge (reduce.trim_groups; minServerGroupTrimSize = 20 below)
+    "SELECT g, h, SUM(m), COUNT(*) FROM t GROUP BY g, h ORDER BY SUM(m) DESC LIMIT 4",
 ]
 REL = 1e-9
 
@@ -58,11 +60,15 @@ def _worker(rank, world, port, q, errs):
         from pinot_amd.engine.distributed import allreduce_block
         from pinot_amd.query.sql import parse
         segs = _segments()
+        from pinot_amd.engine.reduce import trim_groups
         qc = parse(q)
+        qc.options["minServerGroupTrimSize"] = 20
         mine = [s for i, s in enumerate(segs) if i % world == rank]
         part, _ = executor.execute(qc, mine)
-        merged = allreduce_block(part, dist)
-        whole, _ = executor.execute(qc, segs)
+        merged = trim_groups(qc, allreduce_block(part, dist))
+        whole = trim_groups(qc, executor.execute(qc, segs)[0])
+        if "DESC LIMIT 4" in q:
+            assert len(whole.groups) == 20 and getattr(merged, "num_groups_trimmed", False)
         assert merged.stats.num_docs_scanned == whole.stats.num_docs_scanned
         assert merged.stats.num_total_docs == whole.stats.num_total_docs
         if qc.group_by:
