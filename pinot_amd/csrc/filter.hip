@@ -121,9 +121,11 @@ __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__
     // dense u64 doc words (bit d%64 of word d/64), transposed into the lane-major form
     uint32_t r = 0;
     if (n->lds_off >= 0) {
-      const PHIP_LDS uint64_t *w = (const PHIP_LDS uint64_t *)(t.stage + n->lds_off);
+      // lane L takes bit L % 32 of the u32 half (L / 32) of word g: one 32-bit LDS read, v_bfe + v_lshl_or
+      const PHIP_LDS uint32_t *w = (const PHIP_LDS uint32_t *)(t.stage + n->lds_off) + (lane >> 5);
+      const uint32_t sh = (uint32_t)(lane & 31);
 #pragma unroll 8
-      for (int g = 0; g < kTileGroups; g++) r = r + r + (uint32_t)((w[g] >> lane) & 1ull);
+      for (int g = 0; g < kTileGroups; g++) r = (r << 1) | __builtin_amdgcn_ubfe(w[2 * g], sh, 1u);
     } else {
       const PHIP_GLB uint64_t *w = (const PHIP_GLB uint64_t *)n->aux + (t.doc0 >> 6);
 #pragma unroll 8
