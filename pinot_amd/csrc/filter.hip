@@ -64,6 +64,14 @@ __device__ __forceinline__ uint32_t scan_big_set(const PHIP_LDS uint32_t *w, int
   PHIP_GROUP_LOOP(((((set[(win >> k) >> 5] >> ((win >> k) & 31)) & 1u) != 0) != excl))
 }
 
+// IN / NOT IN on a dictionary of <= 2048 ids: the bitset is spread over the wave (lane l holds word l) and
+// each doc fetches its word with ds_bpermute instead of a per-doc global gather.
+__device__ __forceinline__ uint32_t scan_lane_set(const PHIP_LDS uint32_t *w, int B, uint32_t myw, bool excl) {
+  const uint32_t k = 32 - B;
+  PHIP_GROUP_LOOP(((((uint32_t)__builtin_amdgcn_ds_bpermute((int)(((win >> k) >> 5) << 2), (int)myw) >>
+                     ((win >> k) & 31)) & 1u) != 0) != excl)
+}
+
 // bits [lo, hi] (inclusive, 0 <= lo <= hi <= 31) of a u32
 __device__ __forceinline__ uint32_t span32(int lo, int hi) {
   const uint32_t upto = (hi == 31) ? ~0u : ((1u << (hi + 1)) - 1u);
@@ -194,6 +202,10 @@ __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__
       r = scan_range(w, B, LO, SPAN);
     } else if (n->small_set) {
       r = scan_small_set(w, B, n->set_mask);
+    } else if (n->count > 0 && n->count <= 64) {
+      const PHIP_GLB uint32_t *set = (const PHIP_GLB uint32_t *)n->aux;
+      const uint32_t myw = lane < n->count ? set[lane] : 0u;
+      r = scan_lane_set(w, B, myw, n->exclusive != 0);
     } else {
       r = scan_big_set(w, B, (const PHIP_GLB uint32_t *)n->aux, n->exclusive != 0);
     }

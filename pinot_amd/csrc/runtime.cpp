@@ -1204,6 +1204,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
               if (fn.exclusive) dn.set_mask = ~dn.set_mask;  // ids >= card never occur
               dn.exclusive = 0;
             } else {
+              dn.count = (int32_t)bits.size();  // bitset words (filter.hip: <= 64 words ride in one VGPR per lane)
               aux_fix.push_back({ni, blob.add(bits.data(), bits.size() * 4)});
             }
             break;
