@@ -431,6 +431,10 @@ def _check_vs_oracle(qc, raws, segs):
     if not qc.group_by:
         _assert_intermediates_equal(qc.aggregations, gblk.results, oblk.results, exact)
     else:
+        if getattr(gblk, "num_groups_trimmed", False):
+            # server-level trim (IndexedTable.finish): the oracle's full group set, trimmed the same way
+            from pinot_amd.engine.reduce import trim_groups
+            oblk = trim_groups(qc, oblk)
         assert set(gblk.groups) == set(oblk.groups)
         for k, v in oblk.groups.items():
             _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
