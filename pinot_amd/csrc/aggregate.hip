@@ -705,11 +705,26 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const uint64_t *__rest
 
 // Deterministic reduction of per-block partials -> out[nslots]: one wave per slot, lane-strided over
 // blocks in a fixed order, then a fixed shuffle tree (bitwise reproducible run to run).
+__device__ __forceinline__ void finalize_slot(const uint64_t *__restrict__ partials, int nblocks, int nslots,
+                                              const int32_t *__restrict__ kinds, uint64_t *__restrict__ out, int a);
+
 __global__ void finalize_partials_kernel(const uint64_t *__restrict__ partials, int nblocks, int nslots,
                                          const int32_t *__restrict__ kinds, uint64_t *__restrict__ out) {
-  const int a = blockIdx.x;
+  if ((int)blockIdx.x < nslots) finalize_slot(partials, nblocks, nslots, kinds, out, blockIdx.x);
+}
+
+// Both partial sets of a filtered aggregation in one launch (blocks [0, na) -> set a, the rest -> set b).
+__global__ void finalize_partials2_kernel(const uint64_t *__restrict__ pa, int nba, int na, const int32_t *__restrict__ ka,
+                                          uint64_t *__restrict__ oa, const uint64_t *__restrict__ pb, int nbb, int nb,
+                                          const int32_t *__restrict__ kb, uint64_t *__restrict__ ob) {
+  const int i = blockIdx.x;
+  if (i < na) finalize_slot(pa, nba, na, ka, oa, i);
+  else if (i < na + nb) finalize_slot(pb, nbb, nb, kb, ob, i - na);
+}
+
+__device__ __forceinline__ void finalize_slot(const uint64_t *__restrict__ partials, int nblocks, int nslots,
+                                              const int32_t *__restrict__ kinds, uint64_t *__restrict__ out, int a) {
   const int lane = threadIdx.x;
-  if (a >= nslots) return;
   const int kind = kinds[a];
   const bool fp = kind == ACC_SUM_F64 || kind == ACC_MIN_F64 || kind == ACC_MAX_F64;
   uint64_t v = fp ? acc_init(kind) : 0;
@@ -873,6 +888,11 @@ hipError_t launch_slab_reduce(const uint64_t *slab, int32_t nslabs, int32_t tbl_
 hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
                                     uint64_t *out, hipStream_t s) {
   finalize_partials_kernel<<<nslots, 64, 0, s>>>(partials, nblocks, nslots, kinds, out);
+  return hipGetLastError();
+}
+hipError_t launch_finalize_partials2(const uint64_t *pa, int nba, int na, const int32_t *ka, uint64_t *oa,
+                                     const uint64_t *pb, int nbb, int nb, const int32_t *kb, uint64_t *ob, hipStream_t s) {
+  finalize_partials2_kernel<<<na + nb, 64, 0, s>>>(pa, nba, na, ka, oa, pb, nbb, nb, kb, ob);
   return hipGetLastError();
 }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s) {

@@ -49,6 +49,8 @@ hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, 
 hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hipStream_t s);
 hipError_t launch_slab_reduce(const uint64_t *slab, int32_t nslabs, int32_t tbl_words, int64_t G, const int32_t *kinds,
                               uint64_t *out, const uint32_t *hslab, int32_t hll_words, uint32_t *hout, hipStream_t s);
+hipError_t launch_finalize_partials2(const uint64_t *pa, int nba, int na, const int32_t *ka, uint64_t *oa,
+                                     const uint64_t *pb, int nbb, int nb, const int32_t *kb, uint64_t *ob, hipStream_t s);
 hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
                                     uint64_t *out, hipStream_t s);
 hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_counts, int64_t nchunks,
@@ -1570,14 +1572,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   void *fpart, *finals, *seg_matched, *apart = nullptr, *masks = nullptr;
   rc = P.alloc((size_t)filter_blocks * 2 * 8, &fpart);
   if (rc) return rc;
-  rc = P.alloc(64 * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
+  // finals[64] | seg_matched[nseg] | hll registers: the same layout as the pinned landing area, so one
+  // D2H copy brings every per-execution result back
+  rc = P.alloc((64 + (size_t)nseg) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
   if (rc) return rc;
-  rc = P.alloc((size_t)nseg * 8, &seg_matched);
-  if (rc) return rc;
+  seg_matched = (uint64_t *)finals + 64;
   fq.partials = (uint64_t *)fpart;
   fq.seg_matched = (uint64_t *)seg_matched;
   // finals: [0, naggs) aggregation slots, [32, 34) matched docs + entries scanned in filter
-  dq.hll_regs = (uint32_t *)((uint8_t *)finals + 64 * 8);
+  dq.hll_regs = (uint32_t *)((uint64_t *)finals + 64 + nseg);
   if (need_mask) {
     rc = P.alloc((size_t)std::max<int64_t>(total_work, 1) * 64 * 4, &masks);
     if (rc) return rc;
@@ -1753,10 +1756,15 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (has_filter && total_work > 0) HIP_TRY(launch_filter(fq, conj_only, filter_blocks, filter_lds, st));
   if (need_agg && total_work > 0) HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
   HIP_TRY(hipEventRecord(P.ev[2], st));
-  if (has_filter && total_work > 0)
-    HIP_TRY(launch_finalize_partials((const uint64_t *)fpart, filter_blocks, 2, dev_kinds + naggs, fin_filter, st));
-  if (need_agg && !group_by && total_work > 0)
-    HIP_TRY(launch_finalize_partials((const uint64_t *)apart, agg_blocks, naggs, dev_kinds, fin_agg, st));
+  if (has_filter && need_agg && !group_by && total_work > 0 && naggs > 0) {
+    HIP_TRY(launch_finalize_partials2((const uint64_t *)apart, agg_blocks, naggs, dev_kinds, fin_agg,
+                                      (const uint64_t *)fpart, filter_blocks, 2, dev_kinds + naggs, fin_filter, st));
+  } else {
+    if (has_filter && total_work > 0)
+      HIP_TRY(launch_finalize_partials((const uint64_t *)fpart, filter_blocks, 2, dev_kinds + naggs, fin_filter, st));
+    if (need_agg && !group_by && total_work > 0)
+      HIP_TRY(launch_finalize_partials((const uint64_t *)apart, agg_blocks, naggs, dev_kinds, fin_agg, st));
+  }
   if (group_by && dq.mode == GB_LDS && total_work > 0)
     HIP_TRY(launch_slab_reduce((const uint64_t *)slab, agg_blocks, dq.tbl_words, dq.num_groups, dev_kinds,
                                (uint64_t *)gtab, (const uint32_t *)hslab, nhll ? dq.hll_words : 0, (uint32_t *)ghll, st));
@@ -1769,10 +1777,13 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
 
   // results land in the plan's pinned buffer: finals[64] | seg_matched[nseg] | hll registers
   uint64_t *pin = P.pinned;
-  if (total_work > 0) HIP_TRY(hipMemcpyAsync(pin, P.finals, 64 * 8, hipMemcpyDeviceToHost, st));
-  if (has_filter) HIP_TRY(hipMemcpyAsync(pin + 64, seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
-  if (nhll && !group_by)
-    HIP_TRY(hipMemcpyAsync(pin + 64 + nseg, dq.hll_regs, ((size_t)nhll << P.log2m) * 4, hipMemcpyDeviceToHost, st));
+  const size_t hll_bytes = nhll && !group_by ? ((size_t)nhll << P.log2m) * 4 : 0;
+  if (total_work > 0) {
+    HIP_TRY(hipMemcpyAsync(pin, P.finals, (64 + (size_t)nseg) * 8 + hll_bytes, hipMemcpyDeviceToHost, st));
+  } else {
+    if (has_filter) HIP_TRY(hipMemcpyAsync(pin + 64, seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
+    if (hll_bytes) HIP_TRY(hipMemcpyAsync(pin + 64 + nseg, dq.hll_regs, hll_bytes, hipMemcpyDeviceToHost, st));
+  }
   if (!group_by) HIP_TRY(hipEventRecord(P.ev[3], st));
   (void)fin_agg;
   (void)fo;
