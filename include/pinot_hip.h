@@ -203,6 +203,10 @@ typedef struct phip_result {
   double device_ms;      /* device time of the whole query on the stream */
   int32_t num_groups_trimmed; /* 1 when the group set was trimmed to phip_query_desc.trim_size */
   int32_t reserved;
+  /* long_exact[a] = 1 when long_values[g*num_aggregations + a] holds the exact integer result (COUNT, and SUM
+   * over INT/LONG inputs whose bound sum |value| stays below 2^62); 0 when the SUM accumulated in double like
+   * SumAggregationFunction (a possible int64 overflow) -- values[] is then the only result. */
+  const int32_t *long_exact;
 } phip_result;
 
 typedef struct phip_dictionary_view {

@@ -224,8 +224,21 @@ def _exact_values(os_, e, docs):
             a, b = _exact_values(os_, e.args[0], docs), _exact_values(os_, e.args[1], docs)
             if a is None or b is None:
                 return None
+            if a.dtype != object and b.dtype != object and _maxabs(a) * _maxabs(b) + _maxabs(a) + _maxabs(b) >= 2 ** 62:
+                a, b = a.astype(object), b.astype(object)  # Python ints: exact beyond int64
             return {"times": a * b, "minus": a - b, "plus": a + b}[e.name]
     return None
+
+
+def _maxabs(a):
+    return max(abs(int(a.min())), abs(int(a.max()))) if len(a) else 0
+
+
+def _exact_sum(ex):
+    """Exact integer sum (never wraps: int64 only while the bound stays below 2^62)."""
+    if ex.dtype != object and _maxabs(ex) * len(ex) < 2 ** 62:
+        return int(ex.sum(dtype=np.int64))
+    return int(sum(int(x) for x in ex.tolist()))
 
 
 def _hll_registers(os_, col, docs, log2m):
@@ -262,7 +275,7 @@ def _agg_segment(os_, ag, docs):
     if f == "sum":
         s = _oracle_lib().oracle_block_sum_f64(np.ascontiguousarray(vals).ctypes.data, len(vals), MAX_DOC_PER_CALL)
         ex = _exact_values(os_, ag.argument, docs)
-        return s, (int(ex.sum(dtype=np.int64)) if ex is not None else None)
+        return s, (_exact_sum(ex) if ex is not None else None)
     if f == "min":
         return (float(vals.min()) if len(vals) else float("inf")), None
     if f == "max":
@@ -276,8 +289,124 @@ def _agg_segment(os_, ag, docs):
     raise NotImplementedError(f)
 
 
-def execute(query, segments):
-    """Server-side execution over ImmutableSegments -> (results block, exact_sums)."""
+def _group_segment(os_, query, docs, num_groups_limit):
+    """One segment's GroupByOperator: first-seen group ids in doc order, capped at numGroupsLimit
+    (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:1023-1048); per-doc holder updates in
+    doc order (DoubleGroupByResultHolder.java:94-98, SumAggregationFunction.aggregateGroupBySV :160-180);
+    HLL registers of the distinct matched values per group. Returns ({key: intermediates}, {key: exact sums},
+    limit reached)."""
+    codes = np.zeros(len(docs), dtype=np.int64)
+    uniq_vals = []
+    stride = 1
+    for e in query.group_by:
+        u, inv = np.unique(os_.values(e.name)[docs], return_inverse=True)
+        uniq_vals.append(u)
+        codes += inv.astype(np.int64) * stride
+        stride *= max(len(u), 1)
+    ukeys, first, inv = np.unique(codes, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")           # groups in first-seen (doc) order
+    rank = np.empty(len(order), dtype=np.int64)
+    rank[order] = np.arange(len(order))
+    reached = num_groups_limit is not None and len(order) >= num_groups_limit
+    gid = rank[inv]                                     # first-seen group id of every matched doc
+    if num_groups_limit is not None and len(order) > num_groups_limit:
+        keep = gid < num_groups_limit                   # later new keys: INVALID_ID, doc dropped
+        docs, gid = docs[keep], gid[keep]
+    ng = min(len(order), num_groups_limit) if num_groups_limit is not None else len(order)
+    key_codes = ukeys[order[:ng]]
+    keys = []
+    for code in key_codes.tolist():
+        k = []
+        for u in uniq_vals:
+            k.append(u[code % len(u)].item() if hasattr(u[code % len(u)], "item") else u[code % len(u)])
+            code //= len(u)
+        keys.append(tuple(k))
+    per_agg, per_exact = [], []
+    for ag in query.aggregations:
+        f = ag.function
+        ex = None
+        if f == "count":
+            v = np.bincount(gid, minlength=ng).tolist()
+        elif f in ("distinctcounthll", "distinctcountrawhll"):
+            v = _hll_group_registers(os_, ag.argument.name, docs, gid, ng, ag.log2m)
+        else:
+            vals = _expr_values(os_, ag.argument, docs).astype(np.float64)
+            if f in ("sum", "avg"):
+                acc = np.zeros(ng)
+                np.add.at(acc, gid, vals)               # sequential, doc order within a group
+                sums = acc.tolist()
+                if f == "sum":
+                    e = _exact_values(os_, ag.argument, docs)
+                    if e is not None:
+                        if e.dtype != object and _maxabs(e) * len(e) < 2 ** 62:
+                            ea = np.zeros(ng, dtype=np.int64)
+                            np.add.at(ea, gid, e)
+                            ex = [int(x) for x in ea.tolist()]
+                        else:
+                            ex = [0] * ng
+                            for g_, x in zip(gid.tolist(), e.tolist()):
+                                ex[g_] += int(x)
+                    v = sums
+                else:
+                    v = list(zip(sums, np.bincount(gid, minlength=ng).tolist()))
+            elif f in ("min", "max", "minmaxrange"):
+                mn = np.full(ng, np.inf)
+                mx = np.full(ng, -np.inf)
+                np.minimum.at(mn, gid, vals)
+                np.maximum.at(mx, gid, vals)
+                v = mn.tolist() if f == "min" else (mx.tolist() if f == "max" else list(zip(mn.tolist(), mx.tolist())))
+            else:
+                raise NotImplementedError(f)
+        per_agg.append(v)
+        per_exact.append(ex)
+    groups, exact = {}, {}
+    for g, k in enumerate(keys):
+        groups[k] = [per_agg[a][g] for a in range(len(query.aggregations))]
+        exact[k] = [per_exact[a][g] if per_exact[a] is not None else None for a in range(len(query.aggregations))]
+    return groups, exact, reached
+
+
+def _hll_group_registers(os_, col, docs, gid, ng, log2m):
+    """Registers per group: every distinct matched dictionary value offered once (order-free max)."""
+    L = _oracle_lib()
+    ids = os_.dict_ids(col)[docs]
+    uid, uinv = np.unique(ids, return_inverse=True)
+    reg_of = np.empty(len(uid), dtype=np.int64)
+    rho_of = np.empty(len(uid), dtype=np.uint8)
+    d = os_.dictionary(col)
+    t = int(os_.meta(col).data_type)
+    one = np.zeros(1 << log2m, dtype=np.uint8)
+    for j, i in enumerate(uid.tolist()):
+        one[:] = 0
+        v = d[i]
+        if t == 4:
+            b = v.encode("utf-8")
+            arr = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
+            x = L.oracle_murmur_hash_bytes(arr.ctypes.data, len(b), -1)
+        elif t in (0, 1):
+            x = L.oracle_murmur_hash_long(int(v))
+        elif t == 2:
+            x = L.oracle_murmur_hash_long(int(np.float32(v).view(np.int32)))
+        else:
+            x = L.oracle_murmur_hash_long(int(np.float64(v).view(np.int64)))
+        L.oracle_hll_offer_hashed(one.ctypes.data, log2m, x)
+        r = int(np.nonzero(one)[0][0])
+        reg_of[j], rho_of[j] = r, one[r]
+    regs = np.zeros((ng, 1 << log2m), dtype=np.uint8)
+    np.maximum.at(regs, (gid, reg_of[uinv]), rho_of[uinv])
+    return [regs[g] for g in range(ng)]
+
+
+DEFAULT_NUM_GROUPS_LIMIT = 100_000  # InstancePlanMakerImplV2.java:78
+
+
+def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
+    """Server-side execution over ImmutableSegments -> (results block, exact_sums).
+
+    Group-by keeps, per segment, the first ``num_groups_limit`` distinct keys in doc order and drops the
+    docs of later new keys (IntGroupIdMap.getGroupId returns INVALID_ID once the map holds
+    groupIdUpperBound keys, DictionaryBasedGroupKeyGenerator.java:153-174,1023-1048); the block is flagged
+    when a segment's group count reaches the limit (GroupByOperator.java:116)."""
     from pinot_amd.engine.results import (AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock,
                                           merge_intermediate)
     from pinot_amd.query.context import columns_of
@@ -314,19 +443,14 @@ def execute(query, segments):
                 exact = [(a + b) if a is not None and b is not None else None for a, b in zip(exact, exs)]
         return AggregationResultsBlock(query.aggregations, results, stats), exact
     groups, exact_groups = {}, {}
+    limit_reached = False
     for os_, docs in per_seg:
         if len(docs) == 0:
             continue
-        keycols = [os_.values(e.name)[docs] for e in query.group_by]
-        keys = list(zip(*[k.tolist() for k in keycols]))
-        order = {}
-        for i, k in enumerate(keys):
-            order.setdefault(k, []).append(i)
-        for k, idx in order.items():
-            gdocs = docs[np.asarray(idx, dtype=np.int64)]
-            r = [_agg_segment(os_, ag, gdocs) for ag in query.aggregations]
-            vals = [x[0] for x in r]
-            exs = [x[1] for x in r]
+        seg_groups, seg_exact, reached = _group_segment(os_, query, docs, num_groups_limit)
+        limit_reached |= reached
+        for k, vals in seg_groups.items():
+            exs = seg_exact[k]
             if k in groups:
                 groups[k] = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(query.aggregations, groups[k], vals)]
                 exact_groups[k] = [(a + b) if a is not None and b is not None else None
@@ -334,7 +458,7 @@ def execute(query, segments):
             else:
                 groups[k] = vals
                 exact_groups[k] = exs
-    return GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats), exact_groups
+    return GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats, limit_reached), exact_groups
 
 
 def _execute_filtered(query, segments):

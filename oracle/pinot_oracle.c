@@ -219,6 +219,7 @@ int64_t oracle_hll_cardinality(const uint8_t *regs, int log2m) {
   }
   double estimate = alpha_mm * (1.0 / sum);
   if (estimate <= (5.0 / 2.0) * m) {
+    if (zeros == 0) return INT64_MAX; /* m * log(m / 0.0) = +Infinity; Math.round(+Infinity) = Long.MAX_VALUE */
     return (int64_t)floor(m * log((double)m / zeros) + 0.5); /* Math.round */
   }
   return (int64_t)floor(estimate + 0.5);

@@ -89,7 +89,8 @@ class Result(ctypes.Structure):
                 ("values", ctypes.POINTER(ctypes.c_double)), ("long_values", ctypes.POINTER(ctypes.c_int64)),
                 ("hll_registers", ctypes.POINTER(ctypes.c_uint8)), ("group_keys", ctypes.POINTER(ctypes.c_int32)),
                 ("scan_kernel_ms", ctypes.c_double), ("device_ms", ctypes.c_double),
-                ("num_groups_trimmed", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("num_groups_trimmed", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("long_exact", ctypes.POINTER(ctypes.c_int32))]
 
 
 class DictionaryView(ctypes.Structure):

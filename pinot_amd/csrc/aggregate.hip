@@ -462,12 +462,17 @@ __device__ __forceinline__ void group_chunk_global(cquery_t &q, cseg_t &seg, int
 }
 
 __device__ __forceinline__ void group_chunk_hash(cquery_t &q, cseg_t &seg, int32_t doc, bool act) {
-  const int64_t key = group_key(q, seg, doc);
+  int64_t key = group_key(q, seg, doc);
   if (!act) return;
+  if (q.seg_keys) key = key * q.seg_key_mult + seg.seg_index;  // numGroupsLimit pass (limit.hip)
   const int64_t slot = hash_slot(q, (uint64_t)key);
   if (slot < 0) {
     __hip_atomic_fetch_or((glb_u32 *)q.hash_overflow, 1u, PHIP_RLX, PHIP_AG);
     return;
+  }
+  if (q.seg_keys) {
+    glb_u32 *fd = (glb_u32 *)q.first_doc + slot;
+    if (*fd > (uint32_t)doc) __hip_atomic_fetch_min(fd, (uint32_t)doc, PHIP_RLX, PHIP_AG);
   }
   group_update_global(q, seg, doc, slot);
 }

@@ -195,6 +195,11 @@ struct DevAggQuery {
   // GB_HASH: num_groups = capacity (power of two); gb_table / gb_hll are indexed by slot
   uint64_t *gb_keys;        // [capacity] mixed-radix key of each slot, kHashEmpty = free
   uint32_t *hash_overflow;  // set to 1 when a probe sequence found no slot (host reports an error)
+  // numGroupsLimit pass (limit.hip): GB_HASH over composite keys key * seg_key_mult + segment index, and
+  // the first matched doc of every slot (atomicMin) -- the reference's per-segment first-seen order
+  int32_t seg_keys;
+  int32_t seg_key_mult;
+  uint32_t *first_doc;
 };
 
 // ORDER BY on group-by columns for the device trim (trim.hip)

@@ -731,7 +731,7 @@ __global__ __launch_bounds__(256) void roaring_or_kernel(const RoaringTask *__re
       } else {
         const uint16_t *r = (const uint16_t *)tk.payload;
         for (int ri = 0; ri < tk.card; ri++) {
-          const uint32_t s = r[1 + 2 * ri], e = s + r[2 + 2 * ri];  // inclusive
+          const uint32_t s = r[1 + 2 * ri], e = min(s + r[2 + 2 * ri], 65535u);  // inclusive (load validates)
           const uint32_t ws = s >> 6, we = e >> 6;
           for (uint32_t wi = ws + threadIdx.x; wi <= we; wi += blockDim.x) {
             const int lo = (wi == ws) ? (int)(s & 63) : 0;

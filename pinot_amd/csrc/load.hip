@@ -65,6 +65,33 @@ hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32
   return hipGetLastError();
 }
 
+// Value range of a raw INT / LONG column (LE, resident), for the plan-time int64 overflow bound of
+// integer SUMs (SumAggregationFunction adds in double and never wraps, :76-101). out = {min, max},
+// preset to {INT64_MAX, INT64_MIN} by the caller.
+__global__ void minmax_i64_kernel(const void *__restrict__ raw, int32_t type, int64_t n, int64_t *__restrict__ out) {
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = type == PHIP_TYPE_LONG ? ((const int64_t *)raw)[i] : (int64_t)((const int32_t *)raw)[i];
+    lo = v < lo ? v : lo;
+    hi = v > hi ? v : hi;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin((long long *)&out[0], (long long)lo);
+    atomicMax((long long *)&out[1], (long long)hi);
+  }
+}
+
+hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  minmax_i64_kernel<<<grid_for(n, 256, 1024), 256, 0, s>>>(raw, type, n, out);
+  return hipGetLastError();
+}
+
 }  // namespace phip
 
 namespace phip {

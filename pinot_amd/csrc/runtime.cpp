@@ -60,6 +60,20 @@ hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t
 hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs,
                                const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
                                int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
+hipError_t launch_limit_prepare(const int64_t *slots, int64_t n, const uint64_t *hkeys, const uint32_t *first_doc,
+                                int32_t nseg, uint64_t *sortkey, int32_t *idx, int32_t *seg_counts, hipStream_t s);
+hipError_t launch_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *k_in, uint64_t *k_out, const void *v_in,
+                             void *v_out, bool wide, int64_t n, int end_bit, hipStream_t s);
+hipError_t launch_limit_select(const uint64_t *sk_sorted, const int32_t *idx_sorted, int64_t n, const int64_t *seg_start,
+                               int64_t limit, const int64_t *slots, const uint64_t *hkeys, int32_t nseg, uint64_t *key2,
+                               int64_t *slot2, hipStream_t s);
+hipError_t launch_limit_runs(void *temp, size_t *scan_bytes, const uint64_t *k, int64_t n, int32_t *head, int32_t *run,
+                             hipStream_t s);
+hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t n, const int32_t *head, const int32_t *run,
+                               int64_t cap, int32_t naggs, const int32_t *kinds, const uint64_t *table,
+                               const uint32_t *hll, int32_t nhll, int32_t log2m, int64_t *keys_out, double *vals,
+                               int64_t *longs, uint8_t *hll_out, hipStream_t s);
+hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s);
 }  // namespace phip
 
 using namespace phip;
@@ -246,6 +260,8 @@ struct ColumnStore {
   std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
   std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
   std::map<int, uint32_t *> hll;      // per log2m
+  bool has_range = false;             // INT / LONG: value range (plan-time overflow bound of integer sums)
+  int64_t vmin = 0, vmax = 0;
   // inverted index
   uint8_t *inv_blob = nullptr;
   std::vector<int64_t> inv_begin;  // card+1 into inv_conts
@@ -371,8 +387,14 @@ static int32_t parse_inverted(const phip_column_desc &c, ColumnStore &cs, Segmen
         psize = 8192;
       }
       if (pos + psize > blen) return fail(PHIP_ERR_INVALID, "column %s: bitmap %d payload overflow", c.name, d);
-      if ((int64_t)ct.key * 65536 >= (int64_t)seg.num_docs + 65536)
+      // a container's first doc must lie inside the segment (its 1024 decoded words land in the leaf's
+      // round_up(numDocs, 65536) / 64 words), and a run may not pass the container's 65536 docs
+      if ((int64_t)ct.key * 65536 >= (int64_t)seg.num_docs)
         return fail(PHIP_ERR_INVALID, "column %s: bitmap %d key beyond numDocs", c.name, d);
+      if (is_run)
+        for (int32_t ri = 0; ri < ct.card; ri++)
+          if ((uint32_t)le16(bm + pos + 2 + 4 * ri) + le16(bm + pos + 4 + 4 * ri) > 65535u)
+            return fail(PHIP_ERR_INVALID, "column %s: bitmap %d run container past 65535", c.name, d);
       ct.off = off_bytes + o0 + pos - off_bytes;  // relative to blob start (after offsets)
       cs.inv_conts.push_back(ct);
       pos += psize;
@@ -407,6 +429,12 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
       return fail(PHIP_ERR_INVALID, "column %s: dictionary size %llu != card %d x width %d", c.name,
                   (unsigned long long)c.dictionary_bytes, c.cardinality, w);
     cs.host_dict.assign(c.dictionary, c.dictionary + c.dictionary_bytes);
+    if (c.data_type == PHIP_TYPE_INT || c.data_type == PHIP_TYPE_LONG) {  // sorted: first and last entries
+      const size_t last = (size_t)(c.cardinality - 1) * w;
+      cs.vmin = w == 4 ? (int64_t)(int32_t)be32(c.dictionary) : (int64_t)be64(c.dictionary);
+      cs.vmax = w == 4 ? (int64_t)(int32_t)be32(c.dictionary + last) : (int64_t)be64(c.dictionary + last);
+      cs.has_range = true;
+    }
     if (c.data_type != PHIP_TYPE_STRING) {
       void *p;
       int32_t rc = dev_alloc(seg, c.dictionary_bytes, &p);
@@ -539,6 +567,19 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
       HIP_TRY(hipStreamSynchronize(st));
       if (bad) return fail(PHIP_ERR_INVALID, "column %s: malformed compressed chunk %d (type %d)", c.name, bad - 1, comp);
     }
+    if (c.data_type == PHIP_TYPE_INT || c.data_type == PHIP_TYPE_LONG) {
+      int64_t mm[2] = {INT64_MAX, INT64_MIN};
+      void *dmm;
+      HIP_TRY(hipMalloc(&dmm, 16));
+      temps.push_back(dmm);
+      HIP_TRY(hipMemcpyAsync(dmm, mm, 16, hipMemcpyHostToDevice, st));
+      HIP_TRY(launch_minmax_i64(cs.raw, c.data_type, n, (int64_t *)dmm, st));
+      HIP_TRY(hipMemcpyAsync(mm, dmm, 16, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      cs.vmin = n > 0 ? mm[0] : 0;
+      cs.vmax = n > 0 ? mm[1] : 0;
+      cs.has_range = true;
+    }
   }
   seg.by_name[cs.name] = (int)seg.cols.size();
   seg.cols.push_back(std::move(cs));
@@ -571,6 +612,7 @@ struct ResultImpl {
   std::vector<int64_t> longs;
   std::vector<uint8_t> hll;
   std::vector<int32_t> keys;
+  std::vector<int32_t> exact;
   std::vector<std::shared_ptr<Device::Remap>> dicts;
 };
 
@@ -929,6 +971,26 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
           if (cb.type == PHIP_TYPE_STRING) return fail(PHIP_ERR_INVALID, "numeric expression over STRING column");
         }
       }
+    }
+    if (integral && ag.function == PHIP_AGG_SUM) {
+      // int64 accumulation is exact only while no partial can leave int64: bound sum |expr| over every doc
+      // from the columns' value ranges. Past 2^62 the SUM takes the reference's own double accumulation
+      // (SumAggregationFunction.java:76-101; MultiplicationTransformFunction computes 1.0*a*b in double),
+      // which cannot wrap.
+      long double bound = 0;
+      for (int s = 0; s < nseg && integral; s++) {
+        const ColumnStore &ca = segs[s]->cols[colidx[s][ag.column_a]];
+        auto mag = [](const ColumnStore &c) -> long double {
+          return c.has_range ? std::max(fabsl((long double)c.vmin), fabsl((long double)c.vmax)) : 1e30L;
+        };
+        long double e = mag(ca);
+        if (ag.expr != PHIP_EXPR_COLUMN) {
+          const long double b = mag(segs[s]->cols[colidx[s][ag.column_b]]);
+          e = ag.expr == PHIP_EXPR_MUL ? e * b : e + b;
+        }
+        bound += e * (long double)segs[s]->num_docs;
+      }
+      if (bound >= (long double)((int64_t)1 << 62)) integral = false;
     }
     d.integral = integral;
     d.acc = acc_kind_for(ag, integral);
@@ -1790,6 +1852,128 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   return PHIP_OK;
 }
 
+// numGroupsLimit (limit.hip header): the normal pass found ngroups >= limit query-wide, so some segment may
+// have dropped keys. Re-aggregate per (segment, key) with first-seen docs, keep each segment's first `limit`
+// keys and merge them by key. On return keys / vals / longs / hll and *ngroups describe the kept groups.
+static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched, void **keys, void **ov, void **ol,
+                           void **oh, int64_t *ngroups, int32_t *limit_reached) {
+  const int32_t S = P.nseg, naggs = P.naggs, nhll = P.nhll, m_regs = P.m_regs;
+  const int64_t limit = P.num_groups_limit;
+  int64_t space = 1;
+  for (auto &d : P.gb_dicts) space *= d->card;
+  if ((double)space * (double)S >= (double)((int64_t)1 << 62))
+    return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: key space x %d segments exceeds 2^62", S);
+  const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(matched, (int64_t)std::min<double>(
+                                                                           (double)*ngroups * S, 9e18)));
+  int64_t cap = 1024;
+  while (cap < 2 * bound) cap <<= 1;
+  if (cap * (8 + 4 + 8 * (1 + (int64_t)naggs)) > ((int64_t)24 << 30) ||
+      (int64_t)nhll * cap * m_regs * 4 > ((int64_t)16 << 30) || cap > INT32_MAX)
+    return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: %lld (segment, key) slots exceed the memory budget",
+                (long long)cap);
+  int32_t rc;
+  void *hk, *tab, *fd, *hll = nullptr, *ovf, *ddq;
+  if ((rc = dev->ws.get("lim_hkeys", (size_t)cap * 8, &hk))) return rc;
+  if ((rc = dev->ws.get("lim_table", (size_t)cap * 8 * (1 + naggs), &tab))) return rc;
+  if ((rc = dev->ws.get("lim_first", (size_t)cap * 4, &fd))) return rc;
+  if (nhll && (rc = dev->ws.get("lim_hll", (size_t)nhll * cap * m_regs * 4, &hll))) return rc;
+  if ((rc = dev->ws.get("lim_ovf", 16, &ovf))) return rc;
+  if ((rc = dev->ws.get("lim_dq", sizeof(DevAggQuery), &ddq))) return rc;
+  DevAggQuery dq = P.dq;
+  dq.mode = GB_HASH;
+  dq.num_groups = cap;
+  dq.seg_keys = 1;
+  dq.seg_key_mult = S;
+  dq.gb_keys = (uint64_t *)hk;
+  dq.gb_table = (uint64_t *)tab;
+  dq.gb_hll = (uint32_t *)hll;
+  dq.hash_overflow = (uint32_t *)ovf;
+  dq.first_doc = (uint32_t *)fd;
+  dq.tbl_words = 0;
+  dq.hll_words = 0;
+  HIP_TRY(hipMemsetAsync(hk, 0xff, (size_t)cap * 8, st));
+  HIP_TRY(hipMemsetAsync(fd, 0xff, (size_t)cap * 4, st));
+  HIP_TRY(hipMemsetAsync(ovf, 0, 4, st));
+  HIP_TRY(hipMemsetAsync(tab, 0, (size_t)cap * 8, st));
+  for (int a = 0; a < naggs; a++)
+    HIP_TRY(launch_fill_u64((uint64_t *)tab + (int64_t)(1 + a) * cap, cap, dq.aggs[a].acc == ACC_MIN_F64 ? ~0ull : 0ull, st));
+  if (nhll) HIP_TRY(hipMemsetAsync(hll, 0, (size_t)nhll * cap * m_regs * 4, st));
+  HIP_TRY(hipMemcpyAsync(ddq, &dq, sizeof(dq), hipMemcpyHostToDevice, st));
+  if (P.total_work > 0)
+    HIP_TRY(launch_agg(dq, (const DevAggQuery *)ddq, P.agg_blocks, (size_t)kAggWaves * kRing * 4, st));
+  // compact the occupied slots
+  const int64_t nchunks = ceil_div(cap, 1024);
+  void *cc, *offs, *slots;
+  if ((rc = dev->ws.get("lim_cc", (size_t)nchunks * 4, &cc))) return rc;
+  if ((rc = dev->ws.get("lim_offs", (size_t)(nchunks + 1) * 8, &offs))) return rc;
+  HIP_TRY(launch_group_count((const uint64_t *)tab, cap, (int32_t *)cc, nchunks, (int64_t *)offs, st));
+  int64_t n = 0;
+  uint32_t overflow = 0;
+  HIP_TRY(hipMemcpyAsync(&n, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&overflow, ovf, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: hash table overflow (%lld slots)", (long long)cap);
+  if ((rc = dev->ws.get("lim_slots", (size_t)std::max<int64_t>(n, 1) * 8, &slots))) return rc;
+  HIP_TRY(launch_group_compact((const uint64_t *)tab, cap, (const int64_t *)offs, nchunks, (int64_t *)slots, st));
+  // (segment, first doc) order -> ranks -> kept entries
+  size_t sort1 = 0, sort2 = 0, scanb = 0;
+  HIP_TRY(launch_sort_pairs(nullptr, &sort1, nullptr, nullptr, nullptr, nullptr, false, n, 64, st));
+  HIP_TRY(launch_sort_pairs(nullptr, &sort2, nullptr, nullptr, nullptr, nullptr, true, n, 64, st));
+  HIP_TRY(launch_limit_runs(nullptr, &scanb, nullptr, n, nullptr, nullptr, st));
+  const size_t n8 = (size_t)std::max<int64_t>(n, 1) * 8;
+  void *sk0, *sk1, *ix0, *ix1, *k2a, *k2b, *s2a, *s2b, *segc, *segs_start, *tmp, *head, *run;
+  if ((rc = dev->ws.get("lim_sk0", n8, &sk0)) || (rc = dev->ws.get("lim_sk1", n8, &sk1)) ||
+      (rc = dev->ws.get("lim_ix0", n8, &ix0)) || (rc = dev->ws.get("lim_ix1", n8, &ix1)) ||
+      (rc = dev->ws.get("lim_k2a", n8, &k2a)) || (rc = dev->ws.get("lim_k2b", n8, &k2b)) ||
+      (rc = dev->ws.get("lim_s2a", n8, &s2a)) || (rc = dev->ws.get("lim_s2b", n8, &s2b)) ||
+      (rc = dev->ws.get("lim_segc", (size_t)S * 4, &segc)) || (rc = dev->ws.get("lim_segs", (size_t)S * 8, &segs_start)) ||
+      (rc = dev->ws.get("lim_tmp", std::max(std::max(sort1, sort2), scanb) + 256, &tmp)) ||
+      (rc = dev->ws.get("lim_head", n8, &head)) || (rc = dev->ws.get("lim_run", n8, &run)))
+    return rc;
+  HIP_TRY(hipMemsetAsync(segc, 0, (size_t)S * 4, st));
+  HIP_TRY(launch_limit_prepare((const int64_t *)slots, n, (const uint64_t *)hk, (const uint32_t *)fd, S,
+                               (uint64_t *)sk0, (int32_t *)ix0, (int32_t *)segc, st));
+  std::vector<int32_t> seg_counts(S);
+  HIP_TRY(hipMemcpyAsync(seg_counts.data(), segc, (size_t)S * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  std::vector<int64_t> seg_start(S);
+  int64_t kept = 0, acc = 0;
+  *limit_reached = 0;
+  for (int s = 0; s < S; s++) {
+    seg_start[s] = acc;
+    acc += seg_counts[s];
+    kept += std::min<int64_t>(seg_counts[s], limit);
+    if (seg_counts[s] >= limit) *limit_reached = 1;  // GroupByOperator.java:116: numGroups >= numGroupsLimit
+  }
+  HIP_TRY(hipMemcpyAsync(segs_start, seg_start.data(), (size_t)S * 8, hipMemcpyHostToDevice, st));
+  const int end1 = 32 + std::max(1, num_bits_per_value(S - 1));
+  HIP_TRY(launch_sort_pairs(tmp, &sort1, (const uint64_t *)sk0, (uint64_t *)sk1, ix0, ix1, false, n, end1, st));
+  HIP_TRY(launch_limit_select((const uint64_t *)sk1, (const int32_t *)ix1, n, (const int64_t *)segs_start, limit,
+                              (const int64_t *)slots, (const uint64_t *)hk, S, (uint64_t *)k2a, (int64_t *)s2a, st));
+  HIP_TRY(launch_sort_pairs(tmp, &sort2, (const uint64_t *)k2a, (uint64_t *)k2b, s2a, s2b, true, n, 64, st));
+  HIP_TRY(launch_limit_runs(tmp, &scanb, (const uint64_t *)k2b, kept, (int32_t *)head, (int32_t *)run, st));
+  int32_t runs = 0;
+  if (kept > 0) HIP_TRY(hipMemcpyAsync(&runs, (int32_t *)run + kept - 1, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  void *k_out, *v_out, *l_out, *h_out = nullptr;
+  const size_t r1 = (size_t)std::max(runs, 1);
+  if ((rc = dev->ws.get("lim_keys_out", r1 * 8, &k_out)) ||
+      (rc = dev->ws.get("lim_vals_out", r1 * std::max(naggs, 1) * 8, &v_out)) ||
+      (rc = dev->ws.get("lim_longs_out", r1 * std::max(naggs, 1) * 8, &l_out)) ||
+      (nhll && (rc = dev->ws.get("lim_hll_out", r1 * nhll * m_regs, &h_out))))
+    return rc;
+  HIP_TRY(launch_limit_reduce((const uint64_t *)k2b, (const int64_t *)s2b, kept, (const int32_t *)head,
+                              (const int32_t *)run, cap, naggs, (const int32_t *)(P.base + P.kinds_off),
+                              (const uint64_t *)tab, (const uint32_t *)hll, nhll, P.log2m, (int64_t *)k_out,
+                              (double *)v_out, (int64_t *)l_out, (uint8_t *)h_out, st));
+  *keys = k_out;
+  *ov = v_out;
+  *ol = l_out;
+  *oh = h_out;
+  *ngroups = runs;
+  return PHIP_OK;
+}
+
 static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_words) {
   Device *dev = P.dev;
   std::lock_guard<std::mutex> dlock(dev->mu);
@@ -1875,6 +2059,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       HIP_TRY(launch_hash_keys((int64_t *)keys, ngroups, dq.gb_keys, st));
       HIP_TRY(hipMemcpyAsync(&overflow, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
     }
+    if (P.num_groups_limit > 0 && ngroups >= P.num_groups_limit) {
+      // some segment may have reached numGroupsLimit: the first-seen pass decides which keys it kept
+      HIP_TRY(hipStreamSynchronize(st));
+      if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
+      const int64_t matched_docs = has_filter ? (int64_t)fin[32] : docs_in_work;
+      rc = group_limit(P, dev, st, matched_docs, &keys, &ov, &ol, &oh, &ngroups, &r.num_groups_limit_reached);
+      if (rc) return rc;
+    }
     if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0)) {
       // ORDER BY <aggregation> with more groups than trimSize: keep the top trimSize on the device
       // (IndexedTable.finish -> TableResizer.getTopRecords), so only those records cross PCIe.
@@ -1933,8 +2125,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         key /= gb_dicts[k]->card;
       }
     }
-    impl->dicts = gb_dicts;
-    if (P.num_groups_limit > 0 && ngroups > P.num_groups_limit) r.num_groups_limit_reached = 1;
+    impl->dicts = gb_dicts;  // (num_groups_limit_reached was set by group_limit, before any trim)
   } else {
     HIP_TRY(hipStreamSynchronize(st));
   }
@@ -1992,6 +2183,9 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   r.long_values = impl->longs.data();
   r.hll_registers = impl->hll.data();
   r.group_keys = impl->keys.data();
+  impl->exact.resize(std::max(naggs, 1), 0);
+  for (int a = 0; a < naggs; a++) impl->exact[a] = (dq.aggs[a].acc == ACC_COUNT || dq.aggs[a].acc == ACC_SUM_I64) ? 1 : 0;
+  r.long_exact = impl->exact.data();
   r.scan_kernel_ms = t_scan;
   r.device_ms = t_all;
   if (out_result) {

@@ -505,14 +505,15 @@ class GpuCombineOperator:
             for i, p in enumerate(self.prims):
                 if p[0] == _lib.AGG_HLL:
                     hll_slot[i] = len(hll_slot)
-            integral = self._integral_sums()
+            # long_exact[a]: the library kept an exact int64 sum (else it summed in double: int64 overflow bound)
+            exact = [bool(r.long_exact[i]) for i in range(na)] if na else []
 
             def prim_value(g, i):
                 f = self.prims[i][0]
                 if f == _lib.AGG_COUNT:
                     return int(longs[g, i])
                 if f == _lib.AGG_SUM:
-                    return int(longs[g, i]) if integral[i] else float(vals[g, i])
+                    return int(longs[g, i]) if exact[i] else float(vals[g, i])
                 if f in (_lib.AGG_MIN, _lib.AGG_MAX):
                     return float(vals[g, i])
                 return hll[g, hll_slot[i]].copy()
@@ -548,22 +549,6 @@ class GpuCombineOperator:
             return blk
         finally:
             lib.phip_result_free(res)
-
-    def _integral_sums(self):
-        if getattr(self, "_integral_cache", None) is not None:
-            return self._integral_cache
-        out = {}
-        for i, p in enumerate(self.prims):
-            if p[0] != _lib.AGG_SUM:
-                continue
-            ok = True
-            for s in self.segments:
-                for c in (p[2], p[3]):
-                    if c is not None and not s.column_metadata(c).data_type.is_integral:
-                        ok = False
-            out[i] = ok
-        self._integral_cache = out
-        return out
 
 
 def _dictionary_values(dv):

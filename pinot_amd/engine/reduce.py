@@ -37,6 +37,8 @@ def hll_cardinality(regs: np.ndarray) -> int:
         zeros += r == 0
     est = alpha_mm * (1.0 / s)
     if est <= 2.5 * m:
+        if zeros == 0:  # linearCounting(m, 0) = m * log(m / 0.0) = +Infinity; Math.round(+Infinity) = Long.MAX_VALUE
+            return 2 ** 63 - 1
         return int(math.floor(m * math.log(m / zeros) + 0.5))
     return int(math.floor(est + 0.5))
 

@@ -101,4 +101,17 @@ hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hip
   for (int64_t i = 0; i < n; i++) slots[i] = (int64_t)keys[slots[i]];
   return hipSuccess;
 }
+hipError_t launch_minmax_i64(const void *, int32_t, int64_t, int64_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_limit_prepare(const int64_t *, int64_t, const uint64_t *, const uint32_t *, int32_t, uint64_t *,
+                                int32_t *, int32_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_sort_pairs(void *, size_t *temp_bytes, const uint64_t *, uint64_t *, const void *, void *, bool,
+                             int64_t, int, hipStream_t) { *temp_bytes = 256; return hipSuccess; }
+hipError_t launch_limit_select(const uint64_t *, const int32_t *, int64_t, const int64_t *, int64_t, const int64_t *,
+                               const uint64_t *, int32_t, uint64_t *, int64_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_limit_runs(void *, size_t *scan_bytes, const uint64_t *, int64_t, int32_t *, int32_t *, hipStream_t) {
+  *scan_bytes = 256; return hipSuccess;
+}
+hipError_t launch_limit_reduce(const uint64_t *, const int64_t *, int64_t, const int32_t *, const int32_t *, int64_t,
+                               int32_t, const int32_t *, const uint64_t *, const uint32_t *, int32_t, int32_t, int64_t *,
+                               double *, int64_t *, uint8_t *, hipStream_t) { return hipSuccess; }
 }  // namespace phip

@@ -43,10 +43,16 @@ def _assert_intermediates_equal(aggs, gpu_vals, ora_vals, ora_exact):
         elif f == "count":
             assert g == o
         elif f == "sum":
-            if ex is not None:
-                assert isinstance(g, int) and g == ex, (g, ex)  # exact int64
+            if ex is not None and isinstance(g, int):
+                assert g == ex, (g, ex)  # exact int64
                 if abs(ex) < 2 ** 53:
                     assert float(g) == o
+            elif ex is not None:
+                # integer inputs whose |sum| bound passed 2^62: the library summed in double, as
+                # SumAggregationFunction does -- within REL of both the exact sum and the reference's fold
+                assert isinstance(g, float), g
+                assert abs(g - ex) <= REL * max(abs(ex), 1.0), (g, ex)
+                assert g == o or abs(g - o) <= REL * max(abs(g), abs(o)), (g, o)
             else:
                 assert g == o or abs(g - o) <= REL * max(abs(g), abs(o))
         elif f in ("min", "max"):
@@ -384,9 +390,12 @@ def test_gpu_group_by_hash_table_known_answers(case, gsegs, monkeypatch):
     test_gpu_intermediates_vs_oracle(case, gsegs)
 
 
-def test_gpu_group_by_high_cardinality(gpu_lib):
+@pytest.mark.parametrize("limit", [None, 10 ** 9], ids=["default_limit", "no_limit"])
+def test_gpu_group_by_high_cardinality(gpu_lib, limit):
     """Key space 30011 x 20011 x 7 (> 2^26) over 3 segments with different dictionaries -> GB_HASH
-    without any override; every group and intermediate equals the oracle's."""
+    without any override; every group and intermediate equals the oracle's. With the default
+    numGroupsLimit (100,000) every segment holds more distinct keys than the limit: the first-seen
+    100,000 per segment are kept (limit.hip), as the oracle's IntGroupIdMap restatement does."""
     rng = np.random.default_rng(41)
     raws = []
     for k in range(3):
@@ -402,9 +411,11 @@ def test_gpu_group_by_high_cardinality(gpu_lib):
     try:
         qc = parse("SELECT a, b, s, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTHLL(m) FROM t "
                    "WHERE a < 25000 GROUP BY a, b, s LIMIT 10000000")
-        gblk = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, segs).next_block()
-        oblk, exact = executor.execute(qc, raws)
+        kw = {} if limit is None else {"num_groups_limit": limit}
+        gblk = GpuInstancePlanMaker(**kw).make_instance_plan(qc, segs).next_block()
+        oblk, exact = executor.execute(qc, raws, **kw)
         assert gblk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+        assert gblk.num_groups_limit_reached == oblk.num_groups_limit_reached == (limit is None)
         assert set(gblk.groups) == set(oblk.groups)
         for k, v in oblk.groups.items():
             _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
@@ -425,7 +436,8 @@ def bq_segments(gpu_lib):
 
 
 def _check_vs_oracle(qc, raws, segs):
-    gblk = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, segs).next_block()
+    """Default numGroupsLimit on both sides (first-seen keys per segment past 100,000)."""
+    gblk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
     oblk, exact = executor.execute(qc, raws)
     assert gblk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
     if not qc.group_by:
@@ -435,6 +447,7 @@ def _check_vs_oracle(qc, raws, segs):
             # server-level trim (IndexedTable.finish): the oracle's full group set, trimmed the same way
             from pinot_amd.engine.reduce import trim_groups
             oblk = trim_groups(qc, oblk)
+        assert gblk.num_groups_limit_reached == oblk.num_groups_limit_reached
         assert set(gblk.groups) == set(oblk.groups)
         for k, v in oblk.groups.items():
             _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])

@@ -73,7 +73,7 @@ def test_gpu_device_trim(gpu_lib, sql, exact_set):
     try:
         qc = parse(sql)
         blk = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, segs).next_block()
-        oblk, _ = executor.execute(qc, raws)
+        oblk, _ = executor.execute(qc, raws, num_groups_limit=10 ** 9)
         trim = max(5 * qc.limit, 5000)
         assert len(oblk.groups) > trim
         assert blk.num_groups_trimmed and len(blk.groups) == trim
@@ -122,7 +122,7 @@ def test_gpu_device_trim_by_group_keys(gpu_lib, sql):
     try:
         qc = parse(sql)
         blk = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, segs).next_block()
-        oblk, _ = executor.execute(qc, raws)
+        oblk, _ = executor.execute(qc, raws, num_groups_limit=10 ** 9)
         trim = max(5 * qc.limit, 5000)
         assert len(oblk.groups) > trim
         assert blk.num_groups_trimmed and len(blk.groups) == trim
