@@ -145,6 +145,8 @@ def test_gpu_default_limit_over_100k_groups(sql, mode, many_groups, monkeypatch)
         oblk = trim_groups(qc, oblk)
     _check(qc, gblk, oblk, exact)
     got, want = reduce_blocks(qc, [gblk]).rows, reduce_blocks(qc, [oblk]).rows
+    if not qc.order_by:  # no ORDER BY: the broker's LIMIT rows come in table order; compare as sets
+        got, want = sorted(got), sorted(want)
     assert fixtures.rows_match(got, want)
 
 
@@ -178,7 +180,7 @@ def test_gpu_sum_beyond_int64(gpu_lib):
         gblk = _gpu().make_instance_plan(qc, [seg]).next_block()
         oblk, exact = executor.execute(qc, [raw])
         _check(qc, gblk, oblk, exact)
-        assert all(isinstance(v[1], float) and isinstance(v[2], float) and isinstance(v[3], int)
+        assert all(isinstance(v[0], float) and isinstance(v[1], float) and isinstance(v[2], int)
                    for v in gblk.groups.values())
     finally:
         seg.destroy()
