@@ -61,7 +61,8 @@
 #define PHIP_FWD_FIXED_BIT 0 /* FixedBitSVForwardIndexWriter: ceil(N*b/8) BE bytes, MSB first */
 #define PHIP_FWD_SORTED 1    /* SortedIndexReaderImpl: card x (start,end) BE int32, inclusive */
 #define PHIP_FWD_RAW_CHUNK 2 /* BaseChunkForwardIndexWriter v2/v3 fixed-width chunks: PASS_THROUGH, or SNAPPY / LZ4 /
-                              * LZ4_LENGTH_PREFIXED decoded on the GPU at load (ZSTANDARD / GZIP -> UNSUPPORTED) */
+                              * LZ4_LENGTH_PREFIXED decoded on the GPU at load (ZSTANDARD / GZIP -> UNSUPPORTED);
+                              * v1 (4-int header, SNAPPY chunks: BaseChunkForwardIndexReader.java:86-95) as well */
 
 typedef struct phip_column_desc {
   const char *name;

@@ -101,10 +101,13 @@ def _read_raw_chunk(buf, dtype, n):
     """FixedByteChunkSVForwardIndexReader over PASS_THROUGH or compressed chunks: chunk k spans
     [offset_k, offset_{k+1}) (the last one runs to the end of the buffer) and decodes to
     docs_k x entry bytes (BaseChunkForwardIndexReader.java:60-111,204-232)."""
-    h = np.frombuffer(buf, dtype=">i4", count=7)
-    version, num_chunks, per_chunk, entry, total, comp, data_hdr = [int(x) for x in h]
+    version, num_chunks, per_chunk, entry = [int(x) for x in np.frombuffer(buf, dtype=">i4", count=4)]
+    if version > 1:
+        total, comp, data_hdr = [int(x) for x in np.frombuffer(buf, dtype=">i4", count=3, offset=16)]
+    else:  # v1: 4-int header, SNAPPY chunks, offsets from byte 16 (BaseChunkForwardIndexReader.java:86-95)
+        total, comp, data_hdr = n, 1, 16
     assert total == n and comp in (0, 1, 3, 4), (total, comp)
-    osz = 4 if version == 2 else 8
+    osz = 4 if version <= 2 else 8
     offs = np.frombuffer(buf, dtype=">i4" if osz == 4 else ">i8", count=num_chunks, offset=data_hdr)
     raw = np.frombuffer(buf, dtype=np.uint8)
     parts = []

@@ -495,21 +495,26 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
     // raw fixed-width chunk forward index (BaseChunkForwardIndexWriter.java:40-160)
     if (c.data_type == PHIP_TYPE_STRING) return fail(PHIP_ERR_UNSUPPORTED, "raw STRING columns are not on the GPU path");
     const uint8_t *h = c.forward;
-    if (c.forward_bytes < 28) return fail(PHIP_ERR_INVALID, "column %s: chunk header truncated", c.name);
+    if (c.forward_bytes < 16) return fail(PHIP_ERR_INVALID, "column %s: chunk header truncated", c.name);
     int32_t version = (int32_t)be32(h), num_chunks = (int32_t)be32(h + 4), per_chunk = (int32_t)be32(h + 8);
-    int32_t entry = (int32_t)be32(h + 12), total = (int32_t)be32(h + 16), comp = (int32_t)be32(h + 20);
-    int32_t data_hdr = (int32_t)be32(h + 24);
+    int32_t entry = (int32_t)be32(h + 12), total = (int32_t)n, comp = 1, data_hdr = 16;
+    if (version > 1) {  // v2+: total docs, compression type, data header start (BaseChunkForwardIndexReader.java:61-111)
+      if (c.forward_bytes < 28) return fail(PHIP_ERR_INVALID, "column %s: chunk header truncated", c.name);
+      total = (int32_t)be32(h + 16);
+      comp = (int32_t)be32(h + 20);
+      data_hdr = (int32_t)be32(h + 24);
+    }  // v1: 4-int header, SNAPPY chunks, int offsets from byte 16
     // ChunkCompressionType (ChunkCompressionType.java:22): PASS_THROUGH 0, SNAPPY 1, LZ4 3, LZ4_LENGTH_PREFIXED 4
     // are decoded on the GPU; ZSTANDARD 2 and GZIP 5 (entropy-coded) stay on the Java path.
     if (comp != 0 && comp != 1 && comp != 3 && comp != 4)
       return fail(PHIP_ERR_UNSUPPORTED, "column %s: chunk compression type %d (ZSTANDARD/GZIP) is not on the GPU path",
                   c.name, comp);
     if (entry != type_width(c.data_type) || total != n || per_chunk <= 0 ||
-        num_chunks != ceil_div(n, per_chunk) || (version < 2 || version > 3))
+        num_chunks != ceil_div(n, per_chunk) || (version < 1 || version > 3))
       return fail(PHIP_ERR_INVALID, "column %s: bad chunk header", c.name);
-    const int osz = version == 2 ? 4 : 8;
+    const int osz = version <= 2 ? 4 : 8;
     const uint64_t hdr_end = (uint64_t)data_hdr + (uint64_t)num_chunks * osz;
-    if (data_hdr < 28 || hdr_end > c.forward_bytes)
+    if (data_hdr < (version > 1 ? 28 : 16) || hdr_end > c.forward_bytes)
       return fail(PHIP_ERR_INVALID, "column %s: chunk offsets truncated", c.name);
     void *p;
     int32_t rc = dev_alloc(seg, (uint64_t)std::max<int64_t>(n, 1) * entry + 16, &p);
