@@ -208,6 +208,15 @@ typedef struct phip_result {
    * over INT/LONG inputs whose bound sum |value| stays below 2^62); 0 when the SUM accumulated in double like
    * SumAggregationFunction (a possible int64 overflow) -- values[] is then the only result. */
   const int32_t *long_exact;
+  /* Per-kernel device time and algorithmic bytes (the roofline numerators):
+   * filter_bytes = per work tile, the fixed-bit words of every scanned column (256*b bytes), the dense words of
+   * every inverted leaf (256) and the raw values of raw leaves -- what the filter launch must stream;
+   * agg_bytes = per segment, matched docs x (b/8 per projected dictionary column, value width per raw one) plus
+   * min(card, matched) dictionary entries per gathered column. Intermediates (tile masks, tables) excluded. */
+  double filter_kernel_ms;
+  double agg_kernel_ms;
+  int64_t filter_bytes;
+  int64_t agg_bytes;
 } phip_result;
 
 typedef struct phip_dictionary_view {

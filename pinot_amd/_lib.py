@@ -90,7 +90,9 @@ class Result(ctypes.Structure):
                 ("hll_registers", ctypes.POINTER(ctypes.c_uint8)), ("group_keys", ctypes.POINTER(ctypes.c_int32)),
                 ("scan_kernel_ms", ctypes.c_double), ("device_ms", ctypes.c_double),
                 ("num_groups_trimmed", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("long_exact", ctypes.POINTER(ctypes.c_int32))]
+                ("long_exact", ctypes.POINTER(ctypes.c_int32)),
+                ("filter_kernel_ms", ctypes.c_double), ("agg_kernel_ms", ctypes.c_double),
+                ("filter_bytes", ctypes.c_int64), ("agg_bytes", ctypes.c_int64)]
 
 
 class DictionaryView(ctypes.Structure):

@@ -854,12 +854,10 @@ static inline int grid_for(int64_t n, int per_block = 256, int cap = 4096) {
 template <int NA, int MODE, bool D = false>
 static hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s) {
   if (lds > 65536) {
-    static bool configured = false;
-    if (!configured) {
-      hipError_t e = hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
-      if (e != hipSuccess) return e;
-      configured = true;
-    }
+    // once per instantiation (a magic static: thread-safe under concurrent queries)
+    static const hipError_t configured =
+        hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+    if (configured != hipSuccess) return configured;
   }
   agg_kernel<NA, MODE, D><<<nblocks, kAggBlock, lds, s>>>(q);
   return hipGetLastError();

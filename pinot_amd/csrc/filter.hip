@@ -781,12 +781,10 @@ hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *group
 template <bool C>
 static hipError_t launch_filter_t(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s) {
   if (lds_bytes > 65536) {
-    static bool configured = false;  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
-    if (!configured) {
-      hipError_t e = hipFuncSetAttribute((const void *)filter_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
-      if (e != hipSuccess) return e;
-      configured = true;
-    }
+    // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup); once, thread-safe (magic static)
+    static const hipError_t configured =
+        hipFuncSetAttribute((const void *)filter_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+    if (configured != hipSuccess) return configured;
   }
   filter_kernel<C><<<nblocks, kFilterBlock, lds_bytes, s>>>(q);
   return hipGetLastError();

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -224,13 +225,26 @@ struct Workspace {
   }
 };
 
+// One execution lane: a HIP stream and the scratch buffers of the queries that run on it. Queries on
+// different lanes run concurrently (the server's worker threads, BaseCombineOperator.java:87-92 /
+// ResourceManager.java:59-60); a lane is taken for the length of one execution.
+struct Lane {
+  hipStream_t stream = nullptr;
+  Workspace ws;
+};
+
 struct Device {
   int ordinal = 0;
   int num_cus = 256;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // setup stream: segment load, plan preparation (under mu)
   hipEvent_t ev[4] = {};
-  std::mutex mu;
+  std::mutex mu;                 // guards setup work and the remap cache
   Workspace ws;
+  std::mutex lane_mu;
+  std::condition_variable lane_cv;
+  std::vector<std::unique_ptr<Lane>> lanes;
+  std::vector<Lane *> free_lanes;
+  int max_lanes = 8;
   // query-global dictionary remaps for group-by (key: column + segment handles)
   struct Remap {
     std::vector<int32_t *> dev;  // per segment (nullptr = identity)
@@ -293,6 +307,8 @@ static std::vector<std::unique_ptr<Device>> g_devices;
 static std::unordered_map<uint64_t, std::shared_ptr<Segment>> g_segments;
 static std::atomic<uint64_t> g_next_handle{1};
 
+static void init_lanes(Device *d);
+
 static int32_t ensure_devices_locked() {
   if (!g_devices.empty()) return PHIP_OK;
   int n = 0;
@@ -305,6 +321,7 @@ static int32_t ensure_devices_locked() {
   HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, cur));
   HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
+  init_lanes(d.get());
   g_devices.push_back(std::move(d));
   return PHIP_OK;
 }
@@ -313,6 +330,43 @@ static Device *find_device(int ordinal) {
   for (auto &d : g_devices)
     if (d->ordinal == ordinal) return d.get();
   return nullptr;
+}
+
+// A free lane of the device, created on demand up to max_lanes (PHIP_STREAMS), else wait for one.
+static int32_t acquire_lane(Device *dev, Lane **out) {
+  std::unique_lock<std::mutex> lk(dev->lane_mu);
+  while (dev->free_lanes.empty() && (int)dev->lanes.size() >= dev->max_lanes) dev->lane_cv.wait(lk);
+  if (dev->free_lanes.empty()) {
+    auto l = std::make_unique<Lane>();
+    HIP_TRY(hipSetDevice(dev->ordinal));
+    HIP_TRY(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
+    dev->free_lanes.push_back(l.get());
+    dev->lanes.push_back(std::move(l));
+  }
+  *out = dev->free_lanes.back();
+  dev->free_lanes.pop_back();
+  return PHIP_OK;
+}
+
+static void release_lane(Device *dev, Lane *l) {
+  {
+    std::lock_guard<std::mutex> lk(dev->lane_mu);
+    dev->free_lanes.push_back(l);
+  }
+  dev->lane_cv.notify_one();
+}
+
+struct LaneGuard {
+  Device *dev;
+  Lane *lane = nullptr;
+  ~LaneGuard() {
+    if (lane) release_lane(dev, lane);
+  }
+};
+
+static void init_lanes(Device *d) {
+  const char *e = getenv("PHIP_STREAMS");  // execution lanes per device (default 8)
+  if (e) d->max_lanes = std::max(1, std::min(64, atoi(e)));
 }
 
 // ================================================================================================
@@ -876,6 +930,12 @@ struct Plan {
   int32_t order_nkeys = 0;                 // > 0: ORDER BY group-by columns (order_keys)
   int32_t order_keys[kMaxOrderKeys] = {};
   int64_t trim_size = 0;
+  int64_t filter_bytes = 0;  // algorithmic bytes of one filter launch (phip_result.filter_bytes)
+  std::vector<int64_t> seg_docs;  // num_docs per query segment
+  struct ProjCol {
+    std::vector<int32_t> bits, card, width;  // per query segment: fixed-bit width (0 = raw), dictionary
+  };                                         // entries, bytes per value / dictionary entry
+  std::vector<ProjCol> proj;
   bool has_filter = false, need_agg = false, need_mask = false, group_by = false, conj_only = false;
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
@@ -893,8 +953,11 @@ struct Plan {
   hipGraphExec_t graph_exec = nullptr;
   bool graph_failed = false;
   int executions = 0;
-  // per-plan timing events (recorded by every eager run and by every replay of the captured graph)
-  hipEvent_t ev[4] = {};
+  // per-plan timing events (recorded by every eager run and by every replay of the captured graph):
+  // 0 start, 1 before the filter kernel, 4 between filter and aggregation, 2 after the aggregation, 3 end
+  hipEvent_t ev[5] = {};
+  std::mutex exec_mu;  // executions of one plan serialise (its buffers are reused)
+  hipStream_t graph_stream = nullptr;  // the lane stream the graph was captured on
 };
 
 static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
@@ -1551,6 +1614,38 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
   }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
+  for (const DevSeg &ds : dsegs) {
+    int64_t per_tile = 0;
+    std::vector<int> seen;
+    for (int i = ds.node_begin; i < ds.node_end; i++) {
+      const DevNode &dn = nodes[i];
+      if (dn.op != DOP_LEAF) continue;
+      if (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || dn.leaf_kind == PHIP_LEAF_DICT_SET) {
+        if (std::find(seen.begin(), seen.end(), dn.column) == seen.end()) {
+          seen.push_back(dn.column);
+          per_tile += 256ll * ds.cols[dn.column].bits;
+        }
+      } else if (dn.leaf_kind == PHIP_LEAF_INVERTED) {
+        per_tile += 256;
+      } else if (dn.leaf_kind == PHIP_LEAF_RAW_RANGE || dn.leaf_kind == PHIP_LEAF_RAW_SET) {
+        per_tile += (int64_t)kTileDocs * type_width(ds.cols[dn.column].type);
+      }
+    }
+    P.filter_bytes += per_tile * ds.num_work;
+  }
+  for (int c = 0; c < ncols; c++) {
+    if (!projected[c]) continue;
+    Plan::ProjCol pc;
+    for (int s = 0; s < nseg; s++) {
+      const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
+      const bool raw = cs.fwd_kind == PHIP_FWD_RAW_CHUNK;
+      pc.bits.push_back(raw ? 0 : cs.bits);
+      pc.card.push_back(raw ? 0 : cs.card);
+      pc.width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));  // STRING: remap / HLL entry
+    }
+    P.proj.push_back(pc);
+  }
+  for (int s = 0; s < nseg; s++) P.seg_docs.push_back(segs[s]->num_docs);
   bool conj_only = true;
   for (const DevSeg &ds : dsegs) conj_only &= ds.conj > 0;
   // ring depth: prefer 4 workgroups (16 waves) per CU for the VALU/LDS work of the leaves, and give
@@ -1821,6 +1916,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   }
   HIP_TRY(hipEventRecord(P.ev[1], st));
   if (has_filter && total_work > 0) HIP_TRY(launch_filter(fq, conj_only, filter_blocks, filter_lds, st));
+  HIP_TRY(hipEventRecord(P.ev[4], st));
   if (need_agg && total_work > 0) HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
   HIP_TRY(hipEventRecord(P.ev[2], st));
   if (has_filter && need_agg && !group_by && total_work > 0 && naggs > 0) {
@@ -1860,7 +1956,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
 // numGroupsLimit (limit.hip header): the normal pass found ngroups >= limit query-wide, so some segment may
 // have dropped keys. Re-aggregate per (segment, key) with first-seen docs, keep each segment's first `limit`
 // keys and merge them by key. On return keys / vals / longs / hll and *ngroups describe the kept groups.
-static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched, void **keys, void **ov, void **ol,
+static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t matched, void **keys, void **ov, void **ol,
                            void **oh, int64_t *ngroups, int32_t *limit_reached) {
   const int32_t S = P.nseg, naggs = P.naggs, nhll = P.nhll, m_regs = P.m_regs;
   const int64_t limit = P.num_groups_limit;
@@ -1878,12 +1974,12 @@ static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched
                 (long long)cap);
   int32_t rc;
   void *hk, *tab, *fd, *hll = nullptr, *ovf, *ddq;
-  if ((rc = dev->ws.get("lim_hkeys", (size_t)cap * 8, &hk))) return rc;
-  if ((rc = dev->ws.get("lim_table", (size_t)cap * 8 * (1 + naggs), &tab))) return rc;
-  if ((rc = dev->ws.get("lim_first", (size_t)cap * 4, &fd))) return rc;
-  if (nhll && (rc = dev->ws.get("lim_hll", (size_t)nhll * cap * m_regs * 4, &hll))) return rc;
-  if ((rc = dev->ws.get("lim_ovf", 16, &ovf))) return rc;
-  if ((rc = dev->ws.get("lim_dq", sizeof(DevAggQuery), &ddq))) return rc;
+  if ((rc = ws.get("lim_hkeys", (size_t)cap * 8, &hk))) return rc;
+  if ((rc = ws.get("lim_table", (size_t)cap * 8 * (1 + naggs), &tab))) return rc;
+  if ((rc = ws.get("lim_first", (size_t)cap * 4, &fd))) return rc;
+  if (nhll && (rc = ws.get("lim_hll", (size_t)nhll * cap * m_regs * 4, &hll))) return rc;
+  if ((rc = ws.get("lim_ovf", 16, &ovf))) return rc;
+  if ((rc = ws.get("lim_dq", sizeof(DevAggQuery), &ddq))) return rc;
   DevAggQuery dq = P.dq;
   dq.mode = GB_HASH;
   dq.num_groups = cap;
@@ -1909,8 +2005,8 @@ static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched
   // compact the occupied slots
   const int64_t nchunks = ceil_div(cap, 1024);
   void *cc, *offs, *slots;
-  if ((rc = dev->ws.get("lim_cc", (size_t)nchunks * 4, &cc))) return rc;
-  if ((rc = dev->ws.get("lim_offs", (size_t)(nchunks + 1) * 8, &offs))) return rc;
+  if ((rc = ws.get("lim_cc", (size_t)nchunks * 4, &cc))) return rc;
+  if ((rc = ws.get("lim_offs", (size_t)(nchunks + 1) * 8, &offs))) return rc;
   HIP_TRY(launch_group_count((const uint64_t *)tab, cap, (int32_t *)cc, nchunks, (int64_t *)offs, st));
   int64_t n = 0;
   uint32_t overflow = 0;
@@ -1918,7 +2014,7 @@ static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched
   HIP_TRY(hipMemcpyAsync(&overflow, ovf, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: hash table overflow (%lld slots)", (long long)cap);
-  if ((rc = dev->ws.get("lim_slots", (size_t)std::max<int64_t>(n, 1) * 8, &slots))) return rc;
+  if ((rc = ws.get("lim_slots", (size_t)std::max<int64_t>(n, 1) * 8, &slots))) return rc;
   HIP_TRY(launch_group_compact((const uint64_t *)tab, cap, (const int64_t *)offs, nchunks, (int64_t *)slots, st));
   // (segment, first doc) order -> ranks -> kept entries
   size_t sort1 = 0, sort2 = 0, scanb = 0;
@@ -1927,13 +2023,13 @@ static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched
   HIP_TRY(launch_limit_runs(nullptr, &scanb, nullptr, n, nullptr, nullptr, st));
   const size_t n8 = (size_t)std::max<int64_t>(n, 1) * 8;
   void *sk0, *sk1, *ix0, *ix1, *k2a, *k2b, *s2a, *s2b, *segc, *segs_start, *tmp, *head, *run;
-  if ((rc = dev->ws.get("lim_sk0", n8, &sk0)) || (rc = dev->ws.get("lim_sk1", n8, &sk1)) ||
-      (rc = dev->ws.get("lim_ix0", n8, &ix0)) || (rc = dev->ws.get("lim_ix1", n8, &ix1)) ||
-      (rc = dev->ws.get("lim_k2a", n8, &k2a)) || (rc = dev->ws.get("lim_k2b", n8, &k2b)) ||
-      (rc = dev->ws.get("lim_s2a", n8, &s2a)) || (rc = dev->ws.get("lim_s2b", n8, &s2b)) ||
-      (rc = dev->ws.get("lim_segc", (size_t)S * 4, &segc)) || (rc = dev->ws.get("lim_segs", (size_t)S * 8, &segs_start)) ||
-      (rc = dev->ws.get("lim_tmp", std::max(std::max(sort1, sort2), scanb) + 256, &tmp)) ||
-      (rc = dev->ws.get("lim_head", n8, &head)) || (rc = dev->ws.get("lim_run", n8, &run)))
+  if ((rc = ws.get("lim_sk0", n8, &sk0)) || (rc = ws.get("lim_sk1", n8, &sk1)) ||
+      (rc = ws.get("lim_ix0", n8, &ix0)) || (rc = ws.get("lim_ix1", n8, &ix1)) ||
+      (rc = ws.get("lim_k2a", n8, &k2a)) || (rc = ws.get("lim_k2b", n8, &k2b)) ||
+      (rc = ws.get("lim_s2a", n8, &s2a)) || (rc = ws.get("lim_s2b", n8, &s2b)) ||
+      (rc = ws.get("lim_segc", (size_t)S * 4, &segc)) || (rc = ws.get("lim_segs", (size_t)S * 8, &segs_start)) ||
+      (rc = ws.get("lim_tmp", std::max(std::max(sort1, sort2), scanb) + 256, &tmp)) ||
+      (rc = ws.get("lim_head", n8, &head)) || (rc = ws.get("lim_run", n8, &run)))
     return rc;
   HIP_TRY(hipMemsetAsync(segc, 0, (size_t)S * 4, st));
   HIP_TRY(launch_limit_prepare((const int64_t *)slots, n, (const uint64_t *)hk, (const uint32_t *)fd, S,
@@ -1962,10 +2058,10 @@ static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched
   HIP_TRY(hipStreamSynchronize(st));
   void *k_out, *v_out, *l_out, *h_out = nullptr;
   const size_t r1 = (size_t)std::max(runs, 1);
-  if ((rc = dev->ws.get("lim_keys_out", r1 * 8, &k_out)) ||
-      (rc = dev->ws.get("lim_vals_out", r1 * std::max(naggs, 1) * 8, &v_out)) ||
-      (rc = dev->ws.get("lim_longs_out", r1 * std::max(naggs, 1) * 8, &l_out)) ||
-      (nhll && (rc = dev->ws.get("lim_hll_out", r1 * nhll * m_regs, &h_out))))
+  if ((rc = ws.get("lim_keys_out", r1 * 8, &k_out)) ||
+      (rc = ws.get("lim_vals_out", r1 * std::max(naggs, 1) * 8, &v_out)) ||
+      (rc = ws.get("lim_longs_out", r1 * std::max(naggs, 1) * 8, &l_out)) ||
+      (nhll && (rc = ws.get("lim_hll_out", r1 * nhll * m_regs, &h_out))))
     return rc;
   HIP_TRY(launch_limit_reduce((const uint64_t *)k2b, (const int64_t *)s2b, kept, (const int32_t *)head,
                               (const int32_t *)run, cap, naggs, (const int32_t *)(P.base + P.kinds_off),
@@ -1981,9 +2077,15 @@ static int32_t group_limit(Plan &P, Device *dev, hipStream_t st, int64_t matched
 
 static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_words) {
   Device *dev = P.dev;
-  std::lock_guard<std::mutex> dlock(dev->mu);
+  std::lock_guard<std::mutex> xlock(P.exec_mu);
   HIP_TRY(hipSetDevice(dev->ordinal));
-  hipStream_t st = dev->stream;
+  LaneGuard lg{dev};
+  {
+    int32_t lrc = acquire_lane(dev, &lg.lane);
+    if (lrc) return lrc;
+  }
+  hipStream_t st = lg.lane->stream;
+  Workspace &ws = lg.lane->ws;
   // Opt-in (PHIP_GRAPH=1): replay a captured hipGraph from the second execution on. Measured on
   // MI355X it saves nothing once the plan is prepared (host time per execution is ~50 us either way),
   // and event records inside a replayed graph did not give trustworthy kernel times, so eager is the
@@ -2036,24 +2138,24 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   if (group_by) {
     const int64_t nchunks = ceil_div(dq.num_groups, 1024);
     void *cc, *offs, *keys;
-    rc = dev->ws.get("gb_chunk_counts", (size_t)nchunks * 4, &cc);
+    rc = ws.get("gb_chunk_counts", (size_t)nchunks * 4, &cc);
     if (rc) return rc;
-    rc = dev->ws.get("gb_offsets", (size_t)(nchunks + 1) * 8, &offs);
+    rc = ws.get("gb_offsets", (size_t)(nchunks + 1) * 8, &offs);
     if (rc) return rc;
     HIP_TRY(launch_group_count((const uint64_t *)gtab, dq.num_groups, (int32_t *)cc, nchunks, (int64_t *)offs, st));
     int64_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     ngroups = total;
-    rc = dev->ws.get("gb_keys", (size_t)std::max<int64_t>(ngroups, 1) * 8, &keys);
+    rc = ws.get("gb_keys", (size_t)std::max<int64_t>(ngroups, 1) * 8, &keys);
     if (rc) return rc;
     void *ov, *ol, *oh = nullptr;
-    rc = dev->ws.get("gb_out_vals", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ov);
+    rc = ws.get("gb_out_vals", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ov);
     if (rc) return rc;
-    rc = dev->ws.get("gb_out_longs", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ol);
+    rc = ws.get("gb_out_longs", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ol);
     if (rc) return rc;
     if (nhll) {
-      rc = dev->ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * m_regs, &oh);
+      rc = ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * m_regs, &oh);
       if (rc) return rc;
     }
     HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
@@ -2069,7 +2171,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       HIP_TRY(hipStreamSynchronize(st));
       if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
       const int64_t matched_docs = has_filter ? (int64_t)fin[32] : docs_in_work;
-      rc = group_limit(P, dev, st, matched_docs, &keys, &ov, &ol, &oh, &ngroups, &r.num_groups_limit_reached);
+      rc = group_limit(P, ws, st, matched_docs, &keys, &ov, &ol, &oh, &ngroups, &r.num_groups_limit_reached);
       if (rc) return rc;
     }
     if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0)) {
@@ -2090,11 +2192,11 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
                                 &order, st));
       void *scratch, *k2, *v2, *l2, *h2 = nullptr;
       const int64_t k = P.trim_size;
-      if ((rc = dev->ws.get("trim_scratch", sbytes, &scratch))) return rc;
-      if ((rc = dev->ws.get("trim_keys", (size_t)k * 8, &k2))) return rc;
-      if ((rc = dev->ws.get("trim_vals", (size_t)k * std::max(naggs, 1) * 8, &v2))) return rc;
-      if ((rc = dev->ws.get("trim_longs", (size_t)k * std::max(naggs, 1) * 8, &l2))) return rc;
-      if (nhll && (rc = dev->ws.get("trim_hll", (size_t)k * nhll * m_regs, &h2))) return rc;
+      if ((rc = ws.get("trim_scratch", sbytes, &scratch))) return rc;
+      if ((rc = ws.get("trim_keys", (size_t)k * 8, &k2))) return rc;
+      if ((rc = ws.get("trim_vals", (size_t)k * std::max(naggs, 1) * 8, &v2))) return rc;
+      if ((rc = ws.get("trim_longs", (size_t)k * std::max(naggs, 1) * 8, &l2))) return rc;
+      if (nhll && (rc = ws.get("trim_hll", (size_t)k * nhll * m_regs, &h2))) return rc;
       HIP_TRY(launch_trim_order((const double *)ov, (const int64_t *)keys, kop, ngroups, naggs, P.order_agg,
                                 P.order_desc, scratch, &sbytes, &order, st));
       HIP_TRY(launch_trim_gather(order, k, naggs, nhll ? (int64_t)nhll * m_regs : 0, (const int64_t *)keys,
@@ -2166,9 +2268,25 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     }
     if (nhll) for (size_t i = 0; i < ((size_t)nhll << log2m); i++) impl->hll[i] = (uint8_t)hll_host[i];
   }
-  float t_all = 0.f, t_scan = 0.f;
+  float t_all = 0.f, t_scan = 0.f, t_filter = 0.f, t_agg = 0.f;
   HIP_TRY(hipEventElapsedTime(&t_all, P.ev[0], P.ev[3]));
   HIP_TRY(hipEventElapsedTime(&t_scan, P.ev[1], P.ev[2]));
+  HIP_TRY(hipEventElapsedTime(&t_filter, P.ev[1], P.ev[4]));
+  HIP_TRY(hipEventElapsedTime(&t_agg, P.ev[4], P.ev[2]));
+  r.filter_kernel_ms = has_filter ? t_filter : 0.0;
+  r.agg_kernel_ms = need_agg ? t_agg : 0.0;
+  r.filter_bytes = has_filter ? P.filter_bytes : 0;
+  if (need_agg) {
+    int64_t ab = 0;
+    for (int s = 0; s < nseg; s++) {
+      const int64_t m = has_filter ? (int64_t)segm[s] : P.seg_docs[s];
+      for (const Plan::ProjCol &pc : P.proj) {
+        ab += pc.bits[s] ? ceil_div(m * pc.bits[s], 8) : m * pc.width[s];
+        if (pc.bits[s]) ab += std::min<int64_t>(pc.card[s], m) * pc.width[s];
+      }
+    }
+    r.agg_bytes = ab;
+  }
 
   r.num_docs_scanned = matched;
   r.num_entries_scanned_in_filter = has_filter ? (int64_t)fin[33] : 0;
@@ -2228,6 +2346,7 @@ PHIP_API int32_t phip_init(const int32_t *devices, int32_t num_devices) {
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, d->ordinal));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
+    init_lanes(d.get());
     g_devices.push_back(std::move(d));
   }
   return PHIP_OK;
@@ -2247,6 +2366,13 @@ PHIP_API int32_t phip_shutdown(void) {
     d->remaps.clear();
     for (auto &e : d->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
+    for (auto &l : d->lanes) {
+      (void)hipStreamSynchronize(l->stream);
+      l->ws.release();
+      (void)hipStreamDestroy(l->stream);
+    }
+    d->lanes.clear();
+    d->free_lanes.clear();
   }
   g_devices.clear();
   return PHIP_OK;
@@ -2366,9 +2492,8 @@ PHIP_API int32_t phip_plan_destroy(uint64_t plan) {
     g_plans.erase(it);
   }
   if (p && p->dev) {
-    std::lock_guard<std::mutex> dl(p->dev->mu);  // an execution on another thread finishes first
+    std::lock_guard<std::mutex> xl(p->exec_mu);  // an execution on another thread finishes first
     (void)hipSetDevice(p->dev->ordinal);
-    (void)hipStreamSynchronize(p->dev->stream);
   }
   return PHIP_OK;
 }

@@ -546,6 +546,8 @@ class GpuCombineOperator:
                 blk.num_groups_trimmed = bool(r.num_groups_trimmed)
             blk.device_ms = r.device_ms
             blk.scan_kernel_ms = r.scan_kernel_ms
+            blk.filter_kernel_ms, blk.agg_kernel_ms = r.filter_kernel_ms, r.agg_kernel_ms
+            blk.filter_bytes, blk.agg_bytes = int(r.filter_bytes), int(r.agg_bytes)
             return blk
         finally:
             lib.phip_result_free(res)
