@@ -1,15 +1,26 @@
 """Headline benchmark: SSB SF100 flattened lineorder, Q1.1-Q1.3 (scan filter + SUM), per GPU.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; N>1 is launched by
-torch.distributed.run with one rank per GPU. A step = Q1.1 + Q1.2 + Q1.3, each one phip_query over
-every segment resident on the rank (SF100 = 100 segments x 6M rows per GPU, weak scaling: rank r owns
-segments [100r, 100r+100) of an SF(100N) table). Partial aggregates of each query are merged across
-ranks with an RCCL all-reduce (the CombineOperator replacement's exchange step). value = rows
-scanned per second over the whole job (3 x 600M x N rows per step / max-over-ranks step time).
+torch.distributed.run with one rank per GPU. A step = Q1.1 + Q1.2 + Q1.3, each one query over every
+segment resident on the rank (SF100 = 100 segments x 6M rows per GPU, weak scaling: rank r owns segments
+[100r, 100r+100) of an SF(100N) table). Partial aggregates of each query are merged across ranks with an
+RCCL all-reduce (the CombineOperator replacement's exchange step). value = rows scanned per second over the
+whole job (3 x 600M x N rows per step / max-over-ranks wall time of the K timed steps).
 
-Also reported: p50 latency per query, the fused scan kernel's HBM roofline fraction (algorithmic
-bytes per SURVEY.md §8(d) / scan-kernel time from HIP events recorded by libpinot_hip on the stream
-the kernel runs on), and the CPU oracle timed on a bounded sample of the same workload.
+Layout: rows sorted by LO_ORDERDATE, so D_YEAR / D_YEARMONTHNUM / D_WEEKNUMINYEAR carry
+sorted forward indexes and their predicates are doc ranges (SortedIndexBasedFilterOperator), exactly as
+Pinot's CPU path would use them. The same queries over the unsorted layout (every row scanned: the
+scan-bound case) are measured in the same run and reported under "unsorted_layout".
+
+Roofline (per kernel, from the library's own HIP events on the stream the kernels run on): achieved =
+the kernel's algorithmic bytes per launch (phip_result.filter_bytes / agg_bytes, SURVEY.md §8d, computed by
+libpinot_hip from the tiles it must stream and the docs it must project) / its mean launch time; the
+dominant kernel (largest time share) is the headline `roofline`. `traffic` = HBM bytes per launch of that
+kernel from this round's rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes
+(profiles/<round>_traffic.json, tools/traffic.py), or null.
+
+cpu_baseline: oracle/cpu_scan.c, an OpenMP C restatement of Pinot's CPU server path ("restatement, not
+Pinot": no JVM here), over the SAME segments and queries, OMP_NUM_THREADS workers (16 on the GPU box).
 """
 import argparse
 import json
@@ -23,51 +34,97 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ROUND = "r02"
 
 
-def algorithmic_bytes(qc, segments):
-    """sum over referenced columns of ceil(N*b/8) + value-lookup dictionaries card*w."""
-    from pinot_amd.query.context import columns_of
-    filt = qc.filter.columns() if qc.filter else []
-    vals = []
-    for a in qc.aggregations:
-        if a.argument is not None:
-            vals += columns_of(a.argument)
-    for e in qc.group_by:
-        vals += columns_of(e)
-    total = 0
-    for seg in segments:
-        for c in set(filt) | set(vals):
-            m = seg.columns[c].metadata
-            total += (seg.num_docs * m.bits_per_element + 7) // 8
-        for c in set(vals):
-            m = seg.columns[c].metadata
-            if c not in [e.name for e in qc.group_by]:
-                total += m.cardinality * 4
-    return total
+def load_layout(ssb, sf, world, rank, cols, seed, layout, keep_host):
+    from pinot_amd.engine.segment import GpuSegment
+    seg_per_gpu = (sf * ssb.ROWS_PER_SF) // ssb.SEGMENT_ROWS
+    my_segs = list(range(rank * seg_per_gpu, (rank + 1) * seg_per_gpu))
+    gsegs, raws = [], []
+    for i in range(0, len(my_segs), 10):  # generate + load in chunks to bound host memory
+        for r in ssb.make_segments(sf * world, cols, seed=seed, segments=my_segs[i:i + 10], layout=layout):
+            gsegs.append(GpuSegment(r))
+            if keep_host:
+                raws.append(r)
+            else:
+                for ci in r.columns.values():  # free host copies of the (large) index bytes
+                    ci.forward = b""
+    return gsegs, raws
 
 
-def cpu_baseline(queries, sf, seed, target_s=15.0):
-    """The oracle ('port', scalar C + numpy, 1 thread) on a bounded sample of the same segments."""
-    from oracle import executor
-    from pinot_amd.query.sql import parse
-    from tools import ssb
-    cols = ssb.columns_for(queries)
-    qcs = [parse(ssb.SSB_QUERIES[q]) for q in queries]
-    rows = 0
-    t_total = 0.0
-    nseg = 0
-    while t_total < target_s and nseg < 48:
-        seg = ssb.make_segments(sf, cols, seed=seed, segments=[nseg])[0]
-        t0 = time.perf_counter()
-        for qc in qcs:
-            executor.execute(qc, [seg])
-            rows += seg.num_docs
-        t_total += time.perf_counter() - t0
-        nseg += 1
-    return {"value": rows / t_total / 1e9, "unit": "G rows/s", "cores": 1, "kind": "port",
-            "sample": f"{'+'.join(queries)} over {nseg} x 6M-row SF{sf} segments ({rows} rows scanned, "
-                      f"{t_total:.1f} s, oracle/executor.py single thread)"}
+def run_layout(args, dist, queries, qcs, gsegs, torch):
+    """Warm-up, then exactly args.steps timed steps bracketed by barrier + synchronize on both sides."""
+    from pinot_amd.engine.distributed import allreduce_block
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    pm = GpuInstancePlanMaker()
+    ops = {q: pm.make_instance_plan(qcs[q], gsegs) for q in queries}
+
+    def run_query(q):
+        blk = ops[q].next_block()
+        if dist is not None:  # the exchange step: RCCL all-reduce of the partial blocks
+            merged = allreduce_block(blk, dist)
+            for k in ("filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes", "scan_kernel_ms"):
+                setattr(merged, k, getattr(blk, k, 0))
+            return merged
+        return blk
+
+    for _ in range(args.warmup):
+        for q in queries:
+            run_query(q)
+    lat = {q: [] for q in queries}
+    kstats = {q: [] for q in queries}
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        for q in queries:
+            ts = time.perf_counter()
+            blk = run_query(q)
+            lat[q].append((time.perf_counter() - ts) * 1e3)
+            kstats[q].append((blk.filter_kernel_ms, blk.agg_kernel_ms, blk.filter_bytes, blk.agg_bytes))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    for op in ops.values():
+        op.close()
+    return elapsed, lat, kstats
+
+
+def roofline(kstats, queries, traffic, layout):
+    """Per-kernel achieved bandwidth on algorithmic bytes; headline = the kernel with the most time."""
+    kernels = {}
+    for name, ti, bi in (("filter_kernel", 0, 2), ("agg_kernel", 1, 3)):
+        ms = [s[ti] for q in queries for s in kstats[q]]
+        by = [s[bi] for q in queries for s in kstats[q]]
+        launches = sum(1 for x in ms if x > 0)
+        if not launches:
+            continue
+        mean_ms = sum(ms) / launches
+        mean_b = sum(by) / launches
+        ach = mean_b / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
+        tr = ((traffic or {}).get(layout) or {}).get(name)
+        kernels[name] = {"ms_per_launch": round(mean_ms, 4), "alg_bytes_per_launch": int(mean_b),
+                         "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic_per_launch": tr,
+                         "traffic_frac": (round(tr / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
+                         "time_share": None, "per_query_ms": {q: round(float(np.mean([s[ti] for s in kstats[q]])), 4)
+                                                              for q in queries}}
+    tot = sum(k["ms_per_launch"] for k in kernels.values()) or 1.0
+    for k in kernels.values():
+        k["time_share"] = round(k["ms_per_launch"] / tot, 3)
+    dom = max(kernels, key=lambda k: kernels[k]["ms_per_launch"])
+    d = kernels[dom]
+    return {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": d["frac"], "traffic": d["traffic_per_launch"], "kernels": kernels,
+            "bytes": "algorithmic bytes per launch (phip_result.filter_bytes / agg_bytes, SURVEY.md §8d) / mean "
+                     "launch time from HIP events on the library's stream; traffic = PMC HBM bytes per launch"}
 
 
 def main():
@@ -77,9 +134,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sf", type=int, default=100, help="scale factor per GPU (SF100 = 600M rows)")
     ap.add_argument("--queries", default="Q1.1,Q1.2,Q1.3")
+    ap.add_argument("--layout", default="both", choices=["sorted", "unsorted", "both"],
+                    help="headline = sorted (SURVEY.md §8d C2); both also measures the unsorted layout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
-                    help="HBM bytes per scan launch from a rocprofv3 --pmc pass (see profiles/)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", f"{ROUND}_traffic.json"),
+                    help="HBM bytes per launch per kernel and layout from rocprofv3 --pmc passes (tools/traffic.py)")
     ap.add_argument("--seed", type=int, default=42)
     args = ap.parse_args()
 
@@ -97,86 +156,55 @@ def main():
     dev = (ctypes.c_int32 * 1)(local_rank if world > 1 else 0)
     _lib.check(_lib.load().phip_init(dev, 1))
 
-    from pinot_amd.engine.plan import GpuInstancePlanMaker
-    from pinot_amd.engine.segment import GpuSegment
     from pinot_amd.query.sql import parse
     from tools import ssb
 
     queries = args.queries.split(",")
     cols = ssb.columns_for(queries)
-    seg_per_gpu = (args.sf * ssb.ROWS_PER_SF) // ssb.SEGMENT_ROWS
-    my_segs = list(range(rank * seg_per_gpu, (rank + 1) * seg_per_gpu))
-    t0 = time.time()
-    gsegs, raw_meta = [], []
-    chunk = 10
-    for i in range(0, len(my_segs), chunk):  # generate + load in chunks to bound host memory
-        raws = ssb.make_segments(args.sf * world, cols, seed=args.seed, segments=my_segs[i:i + chunk])
-        for r in raws:
-            gsegs.append(GpuSegment(r))
-            raw_meta.append(r)
-            for ci in r.columns.values():  # free host copies of the (large) index bytes
-                ci.forward = b""
-    load_s = time.time() - t0
-    rows_per_rank = sum(s.num_docs for s in gsegs)
-
-    pm = GpuInstancePlanMaker()
     qcs = {q: parse(ssb.SSB_QUERIES[q]) for q in queries}
-    ops = {q: pm.make_instance_plan(qcs[q], gsegs) for q in queries}
-    alg_bytes = {q: algorithmic_bytes(qcs[q], raw_meta) for q in queries}
-
-    from pinot_amd.engine.distributed import allreduce_block
-
-    def run_query(q):
-        blk = ops[q].next_block()
-        if dist is not None:
-            # the exchange step: RCCL all-reduce of the partial blocks (exact int64 / f64 / HLL-max slots)
-            merged = allreduce_block(blk, dist)
-            merged.scan_kernel_ms = blk.scan_kernel_ms
-            return merged
-        return blk
-
-    for _ in range(args.warmup):
-        for q in queries:
-            run_query(q)
-    lat = {q: [] for q in queries}
-    kern = {q: [] for q in queries}
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        for q in queries:
-            ts = time.perf_counter()
-            blk = run_query(q)
-            lat[q].append((time.perf_counter() - ts) * 1e3)
-            kern[q].append(blk.scan_kernel_ms)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    if rank != 0:
-        dist.destroy_process_group()
-        return
-    total_rows = rows_per_rank * world * len(queries) * args.steps
-    value = total_rows / elapsed / 1e9
-    ms_per_step = elapsed * 1e3 / args.steps
-    kern_ms = sum(np.mean(kern[q]) for q in queries)
-    bytes_per_step = sum(alg_bytes[q] for q in queries)
-    achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("queries") == queries and tj.get("sf") == args.sf:
-                traffic = tj.get("hbm_bytes_per_step")
+                traffic = tj.get("per_launch")
         except Exception:
             traffic = None
+    layouts = ["sorted", "unsorted"] if args.layout == "both" else [args.layout]
+    want_cpu = not args.no_cpu_baseline and rank == 0 and world == 1
+    results = {}
+    for li, layout in enumerate(layouts):
+        t0 = time.time()
+        gsegs, raws = load_layout(ssb, args.sf, world, rank, cols, args.seed, layout, keep_host=want_cpu and li == 0)
+        load_s = time.time() - t0
+        rows_per_rank = sum(s.num_docs for s in gsegs)
+        elapsed, lat, kstats = run_layout(args, dist, queries, qcs, gsegs, torch)
+        for s in gsegs:
+            s.destroy()
+        res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(gsegs),
+               "lat": lat, "roofline": roofline(kstats, queries, traffic, layout)}
+        if want_cpu and li == 0:
+            from oracle import cpu_baseline
+            v, threads, reps, el, _ = cpu_baseline.time_queries([qcs[q] for q in queries], raws, min_seconds=10.0)
+            res["cpu"] = {"value": round(v / 1e9, 4), "unit": "G rows/s", "cores": threads, "kind": "port",
+                          "sample": f"restatement, not Pinot: oracle/cpu_scan.c (OpenMP C restatement of the CPU "
+                                    f"server path, {threads} threads; host nproc = {os.cpu_count()}) running "
+                                    f"{'+'.join(queries)} over the same {len(raws)} x {ssb.SEGMENT_ROWS}-row "
+                                    f"SF{args.sf} {layout} segments, {reps} reps in {el:.1f} s"}
+            del raws
+        results[layout] = res
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    head = results[layouts[0]]
+
+    def summary(r):
+        total_rows = r["rows_per_rank"] * world * len(queries) * args.steps
+        return total_rows / r["elapsed"] / 1e9, r["elapsed"] * 1e3 / args.steps
+
+    value, ms_per_step = summary(head)
     out = {
         "metric": "rows scanned/s (G) + p50 query latency, SSB flattened SF100, Q1.1-Q1.3",
         "value": round(value, 3),
@@ -190,23 +218,23 @@ def main():
         "vs_baseline": None,
         "dtype": "u32 dict ids / int64 sums",
         "data": "synthetic SSB-shaped (tools/ssbgen.c, seeded), Pinot segment encodings",
-        "config": {"workload": f"SSB SF{args.sf} flattened lineorder per GPU, {len(gsegs)} segments x "
+        "config": {"workload": f"SSB SF{args.sf} flattened lineorder per GPU, {head['nseg']} segments x "
                                f"{ssb.SEGMENT_ROWS} rows, queries {'+'.join(queries)}",
-                   "rows_per_gpu": rows_per_rank, "parallelism": f"segment-sharded x{world}, RCCL all-reduce"},
-        "p50_latency_ms": {q: round(float(np.median(lat[q])), 3) for q in queries},
-        "scan_kernel_ms": {q: round(float(np.mean(kern[q])), 3) for q in queries},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_step": bytes_per_step,
-                     "kernels": "filter_kernel + agg_kernel per query (HIP events around both, on the library's stream)",
-                     "kernel_ms_per_step": round(kern_ms, 4)},
-        "load_s": round(load_s, 1),
+                   "layout": f"{layouts[0]}" + (" by LO_ORDERDATE (SURVEY.md §8d C2)" if layouts[0] == "sorted" else ""),
+                   "rows_per_gpu": head["rows_per_rank"], "parallelism": f"segment-sharded x{world}, RCCL all-reduce"},
+        "p50_latency_ms": {q: round(float(np.median(head["lat"][q])), 3) for q in queries},
+        "roofline": head["roofline"],
+        "load_s": round(head["load_s"], 1),
     }
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(queries, args.sf * world, args.seed)
+    if "cpu" in head:
+        out["cpu_baseline"] = head["cpu"]
+    if len(layouts) > 1:
+        r = results[layouts[1]]
+        v2, ms2 = summary(r)
+        out["unsorted_layout"] = {"value": round(v2, 3), "unit": "G rows/s", "ms_per_step": round(ms2, 3),
+                                  "p50_latency_ms": {q: round(float(np.median(r["lat"][q])), 3) for q in queries},
+                                  "roofline": r["roofline"]}
     print(json.dumps(out), flush=True)
-    for s in gsegs:
-        s.destroy()
     if dist is not None:
         dist.destroy_process_group()
 

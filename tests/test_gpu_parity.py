@@ -308,11 +308,15 @@ def test_gpu_conjunction_mixed_widths(widths, wide_segment):
 SSB_NAMES = ["Q1.1", "Q1.2", "Q1.3", "Q2.1", "Q2.2", "Q2.3", "Q3.1", "Q3.2", "Q3.3", "Q3.4", "Q4.1", "Q4.2", "Q4.3", "C5"]
 
 
-@pytest.fixture(scope="module")
-def ssb_segments(gpu_lib):
+@pytest.fixture(scope="module", params=["unsorted", "sorted"])
+def ssb_segments(gpu_lib, request):
+    """SF1 in 3 segments; 'sorted' = rows ordered by LO_ORDERDATE, so the date columns
+    carry sorted forward indexes and their predicates become SortedIndexBasedFilterOperator doc ranges."""
     from tools import ssb
     cols = ssb.columns_for(SSB_NAMES)
-    raws = ssb.make_segments(1, cols, seed=7, segment_rows=2_000_000)
+    raws = ssb.make_segments(1, cols, seed=7, segment_rows=2_000_000, layout=request.param)
+    if request.param == "sorted":
+        assert all(r.columns["D_YEAR"].metadata.is_sorted for r in raws)
     segs = [GpuSegment(r) for r in raws]
     yield raws, segs
     for s in segs:

@@ -1,9 +1,9 @@
 #!/bin/bash
-# One GPU call: parity tests, smoke, bench, rocprof kernel trace, FETCH/WRITE PMC passes for the
-# traffic figure. Stops at the first failure / timeout (never retries).
-# usage: tools/gpu_round.sh <tag> [bench args...]
+# One GPU call: parity tests, smoke, bench (both SSB layouts + CPU baseline), rocprof kernel trace, PMC passes
+# (FETCH_SIZE / WRITE_SIZE per layout for the traffic figure, one SQ pass for VALU / LDS / stall counters).
+# Stops at the first failure / timeout (never retries). usage: tools/gpu_round.sh <tag> [bench args...]
 set -u
-TAG=${1:-r01}; shift || true
+TAG=${1:-r02}; shift || true
 mkdir -p gpurun_out
 : > gpurun_out/steps.log
 step() {  # name, timeout, command...
@@ -15,14 +15,21 @@ step() {  # name, timeout, command...
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; tail -30 "gpurun_out/$name.log"; exit $rc; fi
 }
 if [ -z "${SKIP_TESTS:-}" ]; then
-  step pytest_gpu 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread
   step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
 fi
-step bench 400 python -u bench.py --steps 10 --warmup 3 "$@"
+step bench 600 python -u bench.py --steps 10 --warmup 3 "$@"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 -u bench.py --no-cpu-baseline --steps 10 --warmup 3 "$@"
-step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_$TAG -o run -- python3 -u bench.py --no-cpu-baseline --steps 10 --warmup 3 "$@"
-step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_$TAG -o run -- python3 -u bench.py --no-cpu-baseline --steps 10 --warmup 3 "$@"
-python3 tools/traffic.py gpurun_out/pmcf_$TAG gpurun_out/pmcw_$TAG --steps 10 --warmup 3 --queries Q1.1,Q1.2,Q1.3 --sf 100 -o gpurun_out/traffic_$TAG.json
+B="--no-cpu-baseline --steps 10 --warmup 3 $*"
+step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 -u bench.py $B
+for L in sorted unsorted; do
+  step pmcf_$L 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
+  step pmcw_$L 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
+done
+step pmcsq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmcsq_$TAG -o run -- python3 -u bench.py $B --layout unsorted
+python3 tools/traffic.py --layout sorted gpurun_out/pmcf_${TAG}_sorted gpurun_out/pmcw_${TAG}_sorted \
+  --layout unsorted gpurun_out/pmcf_${TAG}_unsorted gpurun_out/pmcw_${TAG}_unsorted \
+  --queries Q1.1,Q1.2,Q1.3 --sf 100 -o gpurun_out/traffic_$TAG.json
+python3 tools/pmc_summary.py gpurun_out/pmcsq_$TAG > gpurun_out/pmcsq_$TAG.txt 2>&1 || true
 cat gpurun_out/steps.log
 tail -2 gpurun_out/bench.log

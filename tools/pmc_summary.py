@@ -1,4 +1,5 @@
-"""Summarise rocprofv3 --pmc CSVs of tools/gpu_pmc.sh: per kernel name, counters averaged per dispatch.
+"""Summarise rocprofv3 --pmc CSVs (tools/gpu_round.sh, tools/gpu_pmc.sh): per kernel name, counters averaged per
+dispatch (VALU / LDS / stall counters of the query kernels).
 
   python tools/pmc_summary.py gpurun_out/pmc_<tag> [kernel-substring]
 """
@@ -11,10 +12,10 @@ from collections import defaultdict
 
 def main():
     root = sys.argv[1]
-    pat = sys.argv[2] if len(sys.argv) > 2 else "scan_kernel"
+    pat = sys.argv[2] if len(sys.argv) > 2 else "phip::"
     vals = defaultdict(lambda: defaultdict(list))
     meta = {}
-    for f in sorted(glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         per_dispatch = defaultdict(float)
         names = {}
         with open(f) as fh:

@@ -88,10 +88,10 @@ def lib():
         L.ssbgen_column_type.argtypes = [ctypes.c_int32]
         L.ssbgen_column_type.restype = ctypes.c_int32
         L.ssbgen_column.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                    ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
-                                    ctypes.POINTER(ctypes.c_int32)]
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
         L.ssbgen_column.restype = ctypes.c_int32
         _lib = L
     return _lib
@@ -120,25 +120,29 @@ def columns_for(queries):
     return cols
 
 
-def _gen_column(seed, first_row, nrows, sf, cid, name):
+LAYOUTS = {"unsorted": 0, "sorted": 1}  # sorted: rows ordered by LO_ORDERDATE
+
+
+def _gen_column(seed, first_row, nrows, sf, cid, name, layout="unsorted"):
     L = lib()
     fwd = np.empty((nrows * 31 + 7) // 8 + 16, dtype=np.uint8)
     dict_cap = 11_000_000 * 4
     dbuf = np.empty(dict_cap, dtype=np.uint8)
-    card, bits, width = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    card, bits, width, srt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
     flen, dlen = ctypes.c_int64(), ctypes.c_int64()
-    rc = L.ssbgen_column(seed, first_row, nrows, sf, cid, fwd.ctypes.data, len(fwd), dbuf.ctypes.data, dict_cap,
-                         ctypes.byref(card), ctypes.byref(bits), ctypes.byref(flen), ctypes.byref(dlen),
-                         ctypes.byref(width))
+    rc = L.ssbgen_column(seed, first_row, nrows, sf, cid, LAYOUTS[layout], fwd.ctypes.data, len(fwd),
+                         dbuf.ctypes.data, dict_cap, ctypes.byref(card), ctypes.byref(bits), ctypes.byref(flen),
+                         ctypes.byref(dlen), ctypes.byref(width), ctypes.byref(srt))
     if rc != 0:
         raise RuntimeError(f"ssbgen_column({name}) failed: {rc}")
     dt = DataType.STRING if L.ssbgen_column_type(cid) == 4 else DataType.INT
-    meta = ColumnMetadata(name, dt, nrows, card.value, bits.value, False, True, False, width.value)
+    meta = ColumnMetadata(name, dt, nrows, card.value, bits.value, bool(srt.value), True, False, width.value)
     return name, ColumnIndexes(meta, fwd[:flen.value].tobytes(), dbuf[:dlen.value].tobytes(), None)
 
 
-def make_segments(sf, columns, seed=42, segment_rows=SEGMENT_ROWS, segments=None, workers=None):
-    """Segments [0, nseg) of an SF-`sf` flattened lineorder; `segments` selects a subset (indexes)."""
+def make_segments(sf, columns, seed=42, segment_rows=SEGMENT_ROWS, segments=None, workers=None, layout="unsorted"):
+    """Segments [0, nseg) of an SF-`sf` flattened lineorder; `segments` selects a subset (indexes);
+    layout "sorted" orders the rows by LO_ORDERDATE (date columns then carry sorted forward indexes)."""
     total = sf * ROWS_PER_SF
     nseg = (total + segment_rows - 1) // segment_rows
     which = list(range(nseg)) if segments is None else list(segments)
@@ -151,7 +155,7 @@ def make_segments(sf, columns, seed=42, segment_rows=SEGMENT_ROWS, segments=None
             tasks.append((s, first, n, c))
     workers = workers or min(16, os.cpu_count() or 4)
     with ThreadPoolExecutor(workers) as ex:
-        res = list(ex.map(lambda t: (t[0], _gen_column(seed, t[1], t[2], sf, ids[t[3]], t[3])), tasks))
+        res = list(ex.map(lambda t: (t[0], _gen_column(seed, t[1], t[2], sf, ids[t[3]], t[3], layout)), tasks))
     out = {}
     for s in which:
         first = s * segment_rows

@@ -10,7 +10,8 @@
  * counter-based pseudo-random stream per (seed, row, attribute), so any row range regenerates
  * identically:
  *   orderdate uniform over 1992-01-01 .. 1998-08-02 -> D_YEAR, D_YEARMONTHNUM, D_YEARMONTH,
- *             D_WEEKNUMINYEAR, LO_ORDERDATE (yyyymmdd)
+ *             D_WEEKNUMINYEAR, LO_ORDERDATE (yyyymmdd); layout 1 instead sorts the
+ *             table by orderdate: row r of R gets day floor(r * 2406 / R)
  *   LO_QUANTITY 1..50, LO_DISCOUNT 0..10, LO_TAX 0..8
  *   LO_PARTKEY 1..200000*floor(1+log2 SF), LO_CUSTKEY 1..30000*SF, LO_SUPPKEY 1..2000*SF
  *   p_retailprice(pk) = 90000 + (pk/10 mod 20001) + 100*(pk mod 1000)   (cents, TPC-H formula)
@@ -174,11 +175,15 @@ static void domains(void) {
 typedef struct {
   int32_t sf;
   int64_t nparts, ncust, nsupp;
+  int64_t total_rows;  /* sorted layout: orderdate of row r = day floor(r * NDAYS / total_rows) */
+  int32_t sorted;
 } Scale;
 
 static Scale scale_of(int32_t sf) {
   Scale s;
   s.sf = sf;
+  s.total_rows = 6000000LL * sf;
+  s.sorted = 0;
   s.nparts = 200000LL * (int64_t)floor(1.0 + log2((double)sf));
   s.ncust = 30000LL * sf;
   s.nsupp = 2000LL * sf;
@@ -189,7 +194,7 @@ static inline int64_t retail(int64_t pk) { return 90000 + ((pk / 10) % 20001) + 
 
 /* domain index of column c for row r (numeric: value - domain_min; strings: natural index) */
 static inline int64_t row_value(int c, uint64_t seed, uint64_t r, const Scale *s) {
-  int day = (int)(H(seed, r, 1) % NDAYS);
+  int day = s->sorted ? (int)((int64_t)r * NDAYS / s->total_rows) : (int)(H(seed, r, 1) % NDAYS);
   switch (c) {
     case C_LO_ORDERDATE: return g_datekey[day];
     case C_D_YEAR: return g_year[day];
@@ -291,14 +296,19 @@ static int bits_for(int32_t max_value) {
 }
 
 /* Generate column c of rows [first_row, first_row + nrows). Buffers: fwd >= ceil(nrows*31/8)+8,
- * dict >= domain size * width. Returns 0 on success. */
-int32_t ssbgen_column(uint64_t seed, int64_t first_row, int32_t nrows, int32_t sf, int32_t c, uint8_t *fwd,
-                      int64_t fwd_cap, uint8_t *dict, int64_t dict_cap, int32_t *out_card, int32_t *out_bits,
-                      int64_t *out_fwd_len, int64_t *out_dict_len, int32_t *out_width) {
+ * dict >= domain size * width. layout 1 = rows sorted by LO_ORDERDATE: a column whose
+ * dict ids are then non-decreasing over the segment is written as Pinot writes sorted columns -- card x
+ * (startDocId, endDocId) BE int32 (SortedIndexReaderImpl.java:114-116) -- and *out_sorted = 1.
+ * Returns 0 on success. */
+int32_t ssbgen_column(uint64_t seed, int64_t first_row, int32_t nrows, int32_t sf, int32_t c, int32_t layout,
+                      uint8_t *fwd, int64_t fwd_cap, uint8_t *dict, int64_t dict_cap, int32_t *out_card,
+                      int32_t *out_bits, int64_t *out_fwd_len, int64_t *out_dict_len, int32_t *out_width,
+                      int32_t *out_sorted) {
   if (c < 0 || c >= C_NUM_COLUMNS || nrows <= 0 || sf <= 0) return 1;
   calendar();
   domains();
   Scale s = scale_of(sf);
+  s.sorted = layout == 1;
   const StrDomain *sd = str_domain(c);
   int64_t lo = 0, hi = 0;
   if (sd) {
@@ -354,6 +364,48 @@ int32_t ssbgen_column(uint64_t seed, int64_t first_row, int32_t nrows, int32_t s
       }
       d++;
     }
+  }
+  int sorted = 1;
+  for (int32_t i = 1; i < nrows && sorted; i++) sorted = idx[i] >= idx[i - 1];
+  *out_sorted = sorted && layout == 1;
+  if (*out_sorted) {
+    /* sorted forward index: per dict id its inclusive doc range (every dictionary value is present) */
+    if ((int64_t)card * 8 > fwd_cap) {
+      free(present);
+      free(idx);
+      free(prefix);
+      return 3;
+    }
+    int32_t id = -1;
+    for (int32_t i = 0; i <= nrows; i++) {
+      int32_t cur = -1;
+      if (i < nrows) {
+        int64_t k = idx[i];
+        cur = prefix[k >> 6] + __builtin_popcountll(present[k >> 6] & ((1ull << (k & 63)) - 1));
+      }
+      if (cur != id) {
+        if (id >= 0) {  /* end of id's range at doc i-1 */
+          uint32_t e = (uint32_t)(i - 1);
+          uint8_t *p = fwd + 8 * (int64_t)id + 4;
+          p[0] = (uint8_t)(e >> 24); p[1] = (uint8_t)(e >> 16); p[2] = (uint8_t)(e >> 8); p[3] = (uint8_t)e;
+        }
+        if (cur >= 0) {
+          uint32_t b = (uint32_t)i;
+          uint8_t *p = fwd + 8 * (int64_t)cur;
+          p[0] = (uint8_t)(b >> 24); p[1] = (uint8_t)(b >> 16); p[2] = (uint8_t)(b >> 8); p[3] = (uint8_t)b;
+        }
+        id = cur;
+      }
+    }
+    free(present);
+    free(idx);
+    free(prefix);
+    *out_card = card;
+    *out_bits = bits;
+    *out_fwd_len = (int64_t)card * 8;
+    *out_dict_len = (int64_t)card * width;
+    *out_width = sd ? width : 0;
+    return 0;
   }
   /* forward index: MSB-first big-endian bit packing of the dict ids */
   const int64_t nbytes = ((int64_t)nrows * bits + 7) / 8;
