@@ -48,8 +48,9 @@ def load_layout(ssb, sf, world, rank, cols, seed, layout, keep_host):
             if keep_host:
                 raws.append(r)
             else:
-                for ci in r.columns.values():  # free host copies of the (large) index bytes
-                    ci.forward = b""
+                for ci in r.columns.values():  # free host copies of the (large) fixed-bit index bytes; the plan
+                    if not ci.metadata.is_sorted:  # reads sorted columns' doc ranges on the host (tiny)
+                        ci.forward = b""
     return gsegs, raws
 
 

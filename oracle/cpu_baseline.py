@@ -130,7 +130,7 @@ class Prepared:
         return total, m.value
 
 
-def time_queries(qcs, segments, threads=None, min_seconds=2.0, max_reps=50):
+def time_queries(qcs, segments, threads=None, min_seconds=2.0, max_reps=100000):
     """Runs every query over all segments with `threads` workers, repeated until min_seconds have passed;
     returns (rows scanned per second, threads, reps, results). Rows = sum of numTotalDocs per query run."""
     threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1

@@ -1,0 +1,332 @@
+// agg_common.h -- projection / expression / accumulation helpers shared by the aggregation kernel
+// (aggregate.hip) and the fused filter+aggregation path of the filter kernel (filter.hip).
+#pragma once
+#include "dev_common.h"
+
+namespace phip {
+
+// The launch descriptor lives in device memory and is read through the constant address space
+// (scalar loads), so no per-lane copy of it is ever made.
+typedef const PHIP_CAS DevAggQuery cquery_t;
+typedef const PHIP_CAS DevAgg cagg_t;
+
+__device__ __forceinline__ int64_t dict_i64(ccol_t &c, uint32_t id) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return ((const PHIP_GLB int32_t *)c.dict)[id];
+    case PHIP_TYPE_LONG: return ((const PHIP_GLB int64_t *)c.dict)[id];
+    case PHIP_TYPE_FLOAT: return (int64_t)((const PHIP_GLB float *)c.dict)[id];
+    default: return (int64_t)((const PHIP_GLB double *)c.dict)[id];
+  }
+}
+__device__ __forceinline__ double dict_f64(ccol_t &c, uint32_t id) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return (double)((const PHIP_GLB int32_t *)c.dict)[id];
+    case PHIP_TYPE_LONG: return (double)((const PHIP_GLB int64_t *)c.dict)[id];
+    case PHIP_TYPE_FLOAT: return (double)((const PHIP_GLB float *)c.dict)[id];
+    default: return ((const PHIP_GLB double *)c.dict)[id];
+  }
+}
+__device__ __forceinline__ int64_t raw_i64(ccol_t &c, int32_t doc) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return ((const PHIP_GLB int32_t *)c.raw)[doc];
+    case PHIP_TYPE_LONG: return ((const PHIP_GLB int64_t *)c.raw)[doc];
+    case PHIP_TYPE_FLOAT: return (int64_t)((const PHIP_GLB float *)c.raw)[doc];
+    default: return (int64_t)((const PHIP_GLB double *)c.raw)[doc];
+  }
+}
+__device__ __forceinline__ double raw_f64(ccol_t &c, int32_t doc) {
+  switch (c.type) {
+    case PHIP_TYPE_INT: return (double)((const PHIP_GLB int32_t *)c.raw)[doc];
+    case PHIP_TYPE_LONG: return (double)((const PHIP_GLB int64_t *)c.raw)[doc];
+    case PHIP_TYPE_FLOAT: return (double)((const PHIP_GLB float *)c.raw)[doc];
+    default: return ((const PHIP_GLB double *)c.raw)[doc];
+  }
+}
+
+__device__ __forceinline__ uint32_t col_dict_id(ccol_t &c, int32_t doc) {
+  return decode_bits(c.words, (uint64_t)(uint32_t)doc * (uint32_t)c.bits, (uint32_t)c.bits);
+}
+__device__ __forceinline__ int64_t col_i64(ccol_t &c, int32_t doc) {
+  if (c.has_dict) return dict_i64(c, col_dict_id(c, doc));
+  return raw_i64(c, doc);
+}
+__device__ __forceinline__ double col_f64(ccol_t &c, int32_t doc) {
+  if (c.has_dict) return dict_f64(c, col_dict_id(c, doc));
+  return raw_f64(c, doc);
+}
+__device__ __forceinline__ int64_t expr_i64(cseg_t &s, cagg_t &a, int32_t doc) {
+  int64_t x = col_i64(s.cols[a.col_a], doc);
+  if (a.expr == PHIP_EXPR_COLUMN) return x;
+  int64_t y = col_i64(s.cols[a.col_b], doc);
+  if (a.expr == PHIP_EXPR_ADD) return x + y;
+  if (a.expr == PHIP_EXPR_SUB) return x - y;
+  return x * y;
+}
+__device__ __forceinline__ double expr_f64(cseg_t &s, cagg_t &a, int32_t doc) {
+  double x = col_f64(s.cols[a.col_a], doc);
+  if (a.expr == PHIP_EXPR_COLUMN) return x;
+  double y = col_f64(s.cols[a.col_b], doc);
+  if (a.expr == PHIP_EXPR_ADD) return x + y;
+  if (a.expr == PHIP_EXPR_SUB) return x - y;
+  return x * y;
+}
+
+// Typed atomics: LDS tables use ds_* atomics, HBM tables global_* atomics (no flat_* forms).
+#define PHIP_RLX __ATOMIC_RELAXED
+#define PHIP_WG __HIP_MEMORY_SCOPE_WORKGROUP
+#define PHIP_AG __HIP_MEMORY_SCOPE_AGENT
+typedef PHIP_LDS uint64_t lds_u64;
+typedef PHIP_LDS uint32_t lds_u32;
+typedef PHIP_GLB uint64_t glb_u64;
+typedef PHIP_GLB uint32_t glb_u32;
+
+// Packed u8 HLL register max in LDS (4 registers per u32 word; no byte max exists in the DS ISA).
+__device__ __forceinline__ void lds_hll_max(lds_u32 *words, uint32_t reg, uint32_t rho) {
+  lds_u32 *w = words + (reg >> 2);
+  const uint32_t sh = (reg & 3) * 8;
+  uint32_t old = *w;
+  while (((old >> sh) & 0xffu) < rho) {
+    const uint32_t want = (old & ~(0xffu << sh)) | (rho << sh);
+    if (__hip_atomic_compare_exchange_strong(w, &old, want, PHIP_RLX, PHIP_RLX, PHIP_WG)) break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-chunk work: 64 lanes = up to 64 matched docs of one segment (inactive lanes carry doc 0, a valid
+// doc, so every load stays in bounds, and contribute the identity)
+// ------------------------------------------------------------------------------------------------
+template <int NA>
+__device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc, bool act,
+                                          uint64_t (&acc)[NA], lds_u32 *hll_lds) {
+#pragma unroll
+  for (int a = 0; a < NA; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    const int kind = ag.acc;
+    if (kind == ACC_COUNT) {
+      acc[a] += act ? 1ull : 0ull;
+    } else if (kind == ACC_SUM_I64) {
+      const int64_t v = expr_i64(seg, ag, doc);
+      acc[a] += act ? (uint64_t)v : 0ull;
+    } else if (kind == ACC_HLL) {
+      ccol_t &c = seg.cols[ag.col_a];
+      const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+      if (act) __hip_atomic_fetch_max(&hll_lds[(ag.hll_slot << q.log2m) + (h >> 8)], h & 0xffu, PHIP_RLX, PHIP_WG);
+    } else {
+      const double v = expr_f64(seg, ag, doc);
+      const double cur = as_f64(acc[a]);
+      double nv;
+      if (kind == ACC_SUM_F64) nv = cur + (act ? v : 0.0);
+      else if (kind == ACC_MIN_F64) nv = fmin(cur, act ? v : __builtin_huge_val());
+      else nv = fmax(cur, act ? v : -__builtin_huge_val());
+      acc[a] = as_u64(nv);
+    }
+  }
+}
+
+// Dense group key of one doc: mixed radix over query-global dict ids, column 0 least significant
+// (DictionaryBasedGroupKeyGenerator.java:314,322,345,442).
+__device__ __forceinline__ int64_t group_key(cquery_t &q, cseg_t &seg, int32_t doc) {
+  int64_t key = 0;
+  for (int k = 0; k < q.num_group_by; k++) {
+    ccol_t &c = seg.cols[q.gb_cols[k]];
+    const uint32_t id = col_dict_id(c, doc);
+    const int32_t gid = c.remap ? ((const PHIP_GLB int32_t *)c.remap)[id] : (int32_t)id;
+    key += (int64_t)gid * q.gb_stride[k];
+  }
+  return key;
+}
+
+// GB_LDS: table rows in LDS (row 0 counts, row 1+a aggregation a), packed HLL registers in LDS.
+__device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_t doc, bool act, lds_u64 *tbl,
+                                                lds_u32 *hll_packed) {
+  const int64_t key = group_key(q, seg, doc);
+  if (!act) return;
+  const int32_t G = (int32_t)q.num_groups;
+  __hip_atomic_fetch_add(&tbl[key], 1ull, PHIP_RLX, PHIP_WG);
+  for (int a = 0; a < kMaxAggs; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    lds_u64 *slot = tbl + (1 + a) * G + key;
+    switch (ag.acc) {
+      case ACC_COUNT: break;  // == row 0
+      case ACC_SUM_I64: __hip_atomic_fetch_add(slot, (uint64_t)expr_i64(seg, ag, doc), PHIP_RLX, PHIP_WG); break;
+      case ACC_SUM_F64:
+        __hip_atomic_fetch_add((PHIP_LDS double *)slot, expr_f64(seg, ag, doc), PHIP_RLX, PHIP_WG);
+        break;
+      case ACC_MIN_F64: __hip_atomic_fetch_min(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_WG); break;
+      case ACC_MAX_F64: __hip_atomic_fetch_max(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_WG); break;
+      case ACC_HLL: {
+        ccol_t &c = seg.cols[ag.col_a];
+        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+        lds_hll_max(hll_packed + ((((int64_t)ag.hll_slot * G + key) << q.log2m) >> 2), h >> 8, h & 0xffu);
+        break;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dense tiles (aggregation only): kBatch groups of 64 docs at a time in the mask's lane-major order
+// (doc 64g + lane), every load of the batch issued before the first use, so a dense tile costs a few
+// memory round trips instead of one per 64 matched docs. Lanes whose doc did not match load the
+// tile's first doc (always valid) and contribute the identity.
+// ------------------------------------------------------------------------------------------------
+constexpr int kBatch = 4;
+constexpr int kDenseMin = 640;  // matched docs per 2048-doc tile from which the batched walk is used
+
+template <int U>
+__device__ __forceinline__ void batch_docs(int32_t doc, uint32_t act, int32_t safe, int32_t (&d)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; u++) d[u] = ((act >> u) & 1u) ? doc + 64 * u : safe;
+}
+
+// Dict ids of the batch: from the wave's LDS stage (sw != null; td = tile-relative doc of group g0,
+// bit window at td * b, ids of non-matching docs forced to 0) or straight from HBM.
+struct BatchSrc {
+  const PHIP_LDS uint32_t *sw;
+  int32_t td;
+  uint32_t act;
+  const PHIP_LDS unsigned char *dict;  // the segment's dictionary copied into LDS (small ones), or null
+};
+
+template <int U>
+__device__ __forceinline__ void batch_ids(ccol_t &c, const int32_t (&d)[U], const BatchSrc &bs, uint32_t (&id)[U]) {
+  const uint32_t b = (uint32_t)c.bits;
+  if (bs.sw != nullptr) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t v = window_at(bs.sw, (bs.td + 64 * u) * (int32_t)b) >> (32 - b);
+      id[u] = ((bs.act >> u) & 1u) ? v : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) id[u] = decode_bits(c.words, (uint64_t)(uint32_t)d[u] * b, b);
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void batch_i64(ccol_t &c, const int32_t (&d)[U], const BatchSrc &bs, int64_t (&v)[U]) {
+  if (c.has_dict) {
+    uint32_t id[U];
+    batch_ids<U>(c, d, bs, id);
+    if (bs.dict != nullptr) {
+      if (c.type == PHIP_TYPE_INT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_LDS int32_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_LONG) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_LDS int64_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_FLOAT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (int64_t)((const PHIP_LDS float *)bs.dict)[id[u]];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (int64_t)((const PHIP_LDS double *)bs.dict)[id[u]];
+      }
+      return;
+    }
+    switch (c.type) {
+      case PHIP_TYPE_INT:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int32_t *)c.dict)[id[u]];
+        break;
+      case PHIP_TYPE_LONG:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int64_t *)c.dict)[id[u]];
+        break;
+      default:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = dict_i64(c, id[u]);
+        break;
+    }
+  } else {
+    switch (c.type) {
+      case PHIP_TYPE_INT:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int32_t *)c.raw)[d[u]];
+        break;
+      case PHIP_TYPE_LONG:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int64_t *)c.raw)[d[u]];
+        break;
+      default:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = raw_i64(c, d[u]);
+        break;
+    }
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void batch_f64(ccol_t &c, const int32_t (&d)[U], const BatchSrc &bs, double (&v)[U]) {
+  if (c.has_dict) {
+    uint32_t id[U];
+    batch_ids<U>(c, d, bs, id);
+    if (bs.dict != nullptr) {
+      if (c.type == PHIP_TYPE_INT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_LDS int32_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_LONG) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_LDS int64_t *)bs.dict)[id[u]];
+      } else if (c.type == PHIP_TYPE_FLOAT) {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_LDS float *)bs.dict)[id[u]];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_LDS double *)bs.dict)[id[u]];
+      }
+      return;
+    }
+    switch (c.type) {
+      case PHIP_TYPE_INT:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_GLB int32_t *)c.dict)[id[u]];
+        break;
+      case PHIP_TYPE_DOUBLE:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB double *)c.dict)[id[u]];
+        break;
+      default:
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = dict_f64(c, id[u]);
+        break;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = raw_f64(c, d[u]);
+  }
+}
+
+// Same arithmetic as expr_i64 / expr_f64, U docs at a time.
+template <int U>
+__device__ __forceinline__ void batch_expr_i64(cseg_t &s, cagg_t &a, const int32_t (&d)[U], const BatchSrc &sa,
+                                               const BatchSrc &sb, int64_t (&x)[U]) {
+  batch_i64<U>(s.cols[a.col_a], d, sa, x);
+  if (a.expr == PHIP_EXPR_COLUMN) return;
+  int64_t y[U];
+  batch_i64<U>(s.cols[a.col_b], d, sb, y);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (a.expr == PHIP_EXPR_ADD) x[u] = x[u] + y[u];
+    else if (a.expr == PHIP_EXPR_SUB) x[u] = x[u] - y[u];
+    else x[u] = x[u] * y[u];
+  }
+}
+template <int U>
+__device__ __forceinline__ void batch_expr_f64(cseg_t &s, cagg_t &a, const int32_t (&d)[U], const BatchSrc &sa,
+                                               const BatchSrc &sb, double (&x)[U]) {
+  batch_f64<U>(s.cols[a.col_a], d, sa, x);
+  if (a.expr == PHIP_EXPR_COLUMN) return;
+  double y[U];
+  batch_f64<U>(s.cols[a.col_b], d, sb, y);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (a.expr == PHIP_EXPR_ADD) x[u] = x[u] + y[u];
+    else if (a.expr == PHIP_EXPR_SUB) x[u] = x[u] - y[u];
+    else x[u] = x[u] * y[u];
+  }
+}
+
+}  // namespace phip

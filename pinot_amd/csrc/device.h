@@ -109,6 +109,12 @@ struct DevSeg {
   int32_t conj_sparse;  // > 0: leaves 2.. are dict-id ranges, so a tile whose first leaf passes at most
                         // this many docs per lane tests them per passing doc (SVScanDocIdIterator.applyAnd)
                         // instead of per doc
+  int32_t conj_path;    // 1: the segment's program takes the conjunctive path (conj >= 0 scan leaves, plus the
+                        // optional doc range below); 0: the postfix interpreter
+  int32_t conj_range;   // 1: AND with the doc range [conj_lo, conj_hi] (single-range sorted-index leaves,
+  int32_t conj_lo;      // SortedIndexBasedFilterOperator; tiles outside it are pruned on the host, so only the
+  int32_t conj_hi;      // boundary tiles are masked)
+  int32_t pad_conj;
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
@@ -146,6 +152,10 @@ struct DevFilter {
   uint32_t *mask_out;    // optional: [total_work][64] lane-major tile masks
   uint64_t *partials;    // [num_blocks][2]: matched docs, entries scanned in filter
   uint64_t *seg_matched; // [num query segments]
+  // fused aggregation (conjunctive programs, no group-by / HLL): the filter kernel projects and aggregates
+  // each tile's matched docs itself, reading staged columns from the tile's ring slot (DevCol.lds_off)
+  const struct DevAggQuery *agg;  // device copy of the aggregation descriptor, null = not fused
+  uint64_t *agg_partials;         // [num_blocks][num_aggs]
 };
 
 struct DevAgg {

@@ -16,7 +16,7 @@
 // materialisation; AND / OR / NOT (AndDocIdSet / OrDocIdSet / NotDocIdSet) are one VALU op per lane.
 // The tile's 64 lane words (256 B, one coalesced store) go to the aggregation kernel when the query
 // projects anything; COUNT-only queries stop here (FastFilteredCountOperator.java:66-78).
-#include "dev_common.h"
+#include "agg_common.h"
 
 namespace phip {
 
@@ -522,6 +522,62 @@ __device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_
 }
 
 // ------------------------------------------------------------------------------------------------
+// fused projection + aggregation (conjunctive programs without group-by / HLL). The tile's matched docs
+// are aggregated right after the mask is known: kBatch consecutive 64-doc groups at a time (groups with
+// no match anywhere in the wave are skipped), dict ids of columns staged in the tile's ring slot (filter
+// columns, and value columns the host chose to stream) read from LDS, the others decoded from HBM; then
+// the dictionary gathers and the expression, into per-lane accumulators in doc order -- the agg_batch
+// walk of aggregate.hip without the mask round trip, the re-read of the filter columns and a second launch.
+// ------------------------------------------------------------------------------------------------
+template <int NA>
+__device__ __forceinline__ void fused_tile(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
+                                           uint64_t (&acc)[NA]) {
+  const uint32_t gm = wave_or32(mask);
+  if (gm == 0) return;
+  const int lane = lane_id();
+#pragma unroll 1
+  for (int g0 = 0; g0 < kTileGroups; g0 += kBatch) {
+    if (((gm << g0) >> (32 - kBatch)) == 0) continue;  // no lane matched in groups [g0, g0 + kBatch)
+    const uint32_t act = __builtin_bitreverse32(mask << g0) & ((1u << kBatch) - 1u);
+    int32_t d[kBatch];
+    batch_docs<kBatch>(t.doc0 + 64 * g0 + lane, act, t.doc0, d);
+    const int32_t td = 64 * g0 + lane;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      if (a >= aq.num_aggs) break;
+      cagg_t &ag = aq.aggs[a];
+      const int kind = ag.acc;
+      if (kind == ACC_COUNT) {
+        acc[a] += (uint64_t)__popc(act);
+        continue;
+      }
+      ccol_t &ca = seg.cols[ag.col_a];
+      ccol_t &cb = seg.cols[ag.expr != PHIP_EXPR_COLUMN ? ag.col_b : ag.col_a];
+      const BatchSrc sa{ca.lds_off >= 0 ? (const PHIP_LDS uint32_t *)(t.stage + ca.lds_off) : nullptr, td, act, nullptr};
+      const BatchSrc sb{cb.lds_off >= 0 ? (const PHIP_LDS uint32_t *)(t.stage + cb.lds_off) : nullptr, td, act, nullptr};
+      if (kind == ACC_SUM_I64) {
+        int64_t v[kBatch];
+        batch_expr_i64<kBatch>(seg, ag, d, sa, sb, v);
+#pragma unroll
+        for (int u = 0; u < kBatch; u++) acc[a] += ((act >> u) & 1u) ? (uint64_t)v[u] : 0ull;
+      } else {
+        double v[kBatch];
+        batch_expr_f64<kBatch>(seg, ag, d, sa, sb, v);
+        double cur = as_f64(acc[a]);
+#pragma unroll
+        for (int u = 0; u < kBatch; u++) {
+          const bool on = (act >> u) & 1u;
+          if (kind == ACC_SUM_F64) cur = cur + (on ? v[u] : 0.0);
+          else if (kind == ACC_MIN_F64) cur = fmin(cur, on ? v[u] : __builtin_huge_val());
+          else cur = fmax(cur, on ? v[u] : -__builtin_huge_val());
+        }
+        acc[a] = as_u64(cur);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // the filter kernel
 // ------------------------------------------------------------------------------------------------
 // s_waitcnt vmcnt(n) for a wave-uniform n. n > 14 waits for vmcnt(15), which is stricter and so safe.
@@ -581,9 +637,9 @@ __device__ __forceinline__ void cursor_issue(StageCursor<kS> &c, uint32_t lbase,
   }
 }
 
-template <bool kConjOnly>
+template <bool kConjOnly, int NA>
 __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel(DevFilter q) {
-  constexpr int kS = kConjOnly ? kMaxConj : kMaxStage;
+  constexpr int kS = kConjOnly ? (NA > 0 ? kMaxConj + kMaxAggStage : kMaxConj) : kMaxStage;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);
@@ -618,6 +674,12 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   // (atomics only add to the true count). Waiting for fewer outstanding operations is always safe.
   const int nd = q.min_dma;
   const int st = q.mask_out != nullptr ? 1 : 0;
+  uint64_t acc[NA > 0 ? NA : 1];
+  if constexpr (NA > 0) {
+    cquery_t &aq = *(cquery_t *)q.agg;
+#pragma unroll
+    for (int a = 0; a < NA; a++) acc[a] = a < aq.num_aggs ? acc_init(aq.aggs[a].acc) : 0;
+  }
 
   // prefetch cursor: tiles [begin, pf) have their DMA issued (pfc of them)
   int pf = begin, pfc = 0, psn = 0, pend = -1, pslot = 0;
@@ -667,8 +729,12 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     const uint32_t valid = valid_word(tl.valid_docs, lane);
     uint32_t scanned_t = 0;
     uint32_t mask;
-    if (kConjOnly || seg.conj > 0) {
-      mask = eval_conj(seg, tl.stage, valid);
+    if (kConjOnly || seg.conj_path) {
+      mask = seg.conj > 0 ? eval_conj(seg, tl.stage, valid) : valid;
+      if (seg.conj_range && (seg.conj_lo > tl.doc0 || seg.conj_hi < tl.doc0 + kTileDocs - 1)) {
+        const int32_t lo = max(seg.conj_lo - tl.doc0, 0), hi = min(seg.conj_hi - tl.doc0, kTileDocs - 1);
+        mask &= lo <= hi ? range_word(lo, hi, lane) : 0u;
+      }
       scanned_t = (uint32_t)seg.conj * (uint32_t)tl.valid_docs;
     } else {
       mask = seg.node_end > seg.node_begin ? eval_filter(seg, nodes, valid, tl, scanned_t) : valid;
@@ -676,6 +742,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     scanned += scanned_t;
     lane_matched += (uint32_t)__popc(mask);
     if (st) ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
+    if constexpr (NA > 0) fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, acc);
     slot = slot + 1 == nbuf ? 0 : slot + 1;
   }
 #undef PHIP_PREFETCH
@@ -696,6 +763,30 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     uint64_t v = 0;
     for (int w = 0; w < kFilterWaves; w++) v += part[w][threadIdx.x];
     q.partials[(size_t)blockIdx.x * 2 + threadIdx.x] = v;
+  }
+  if constexpr (NA > 0) {  // fused aggregation: per-block partials, reduced in a fixed order by finalize
+    cquery_t &aq = *(cquery_t *)q.agg;
+    __shared__ uint64_t apart[kFilterWaves][NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      if (a >= aq.num_aggs) break;
+      const int kind = aq.aggs[a].acc;
+      uint64_t v;
+      if (kind == ACC_COUNT || kind == ACC_SUM_I64) v = wave_reduce_u64_add(acc[a]);
+      else v = as_u64(wave_reduce_f64(as_f64(acc[a]), kind));
+      if (lane == 0) apart[wave][a] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int a = 0; a < NA; a++) {
+        if (a >= aq.num_aggs) break;
+        const int kind = aq.aggs[a].acc;
+        uint64_t v = apart[0][a];
+        for (int w = 1; w < kFilterWaves; w++) v = acc_combine(kind, v, apart[w][a]);
+        q.agg_partials[(size_t)blockIdx.x * aq.num_aggs + a] = v;
+      }
+    }
   }
 }
 
@@ -778,22 +869,28 @@ hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *group
   return hipGetLastError();
 }
 
-template <bool C>
+template <bool C, int NA>
 static hipError_t launch_filter_t(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s) {
   if (lds_bytes > 65536) {
     // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup); once, thread-safe (magic static)
-    static const hipError_t configured =
-        hipFuncSetAttribute((const void *)filter_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+    static const hipError_t configured = hipFuncSetAttribute((const void *)filter_kernel<C, NA>,
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
     if (configured != hipSuccess) return configured;
   }
-  filter_kernel<C><<<nblocks, kFilterBlock, lds_bytes, s>>>(q);
+  filter_kernel<C, NA><<<nblocks, kFilterBlock, lds_bytes, s>>>(q);
   return hipGetLastError();
 }
 
 // conj_only: every segment's program takes the conjunctive fast path (the interpreter is compiled
-// out, which frees registers for more resident waves)
-hipError_t launch_filter(const DevFilter &q, bool conj_only, int nblocks, size_t lds_bytes, hipStream_t s) {
-  return conj_only ? launch_filter_t<true>(q, nblocks, lds_bytes, s) : launch_filter_t<false>(q, nblocks, lds_bytes, s);
+// out, which frees registers for more resident waves); fused_naggs > 0: the aggregation runs inside
+// (q.agg set, conj_only required)
+hipError_t launch_filter(const DevFilter &q, bool conj_only, int fused_naggs, int nblocks, size_t lds_bytes,
+                         hipStream_t s) {
+  if (!conj_only) return launch_filter_t<false, 0>(q, nblocks, lds_bytes, s);
+  if (fused_naggs <= 0) return launch_filter_t<true, 0>(q, nblocks, lds_bytes, s);
+  if (fused_naggs <= 1) return launch_filter_t<true, 1>(q, nblocks, lds_bytes, s);
+  if (fused_naggs <= 2) return launch_filter_t<true, 2>(q, nblocks, lds_bytes, s);
+  return launch_filter_t<true, 4>(q, nblocks, lds_bytes, s);
 }
 
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,

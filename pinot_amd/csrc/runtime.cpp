@@ -43,7 +43,8 @@ hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32
                                    uint32_t *words, int64_t nwords, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
 hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *groups, int32_t ngroups, hipStream_t s);
-hipError_t launch_filter(const DevFilter &q, bool conj_only, int nblocks, size_t lds_bytes, hipStream_t s);
+hipError_t launch_filter(const DevFilter &q, bool conj_only, int fused_naggs, int nblocks, size_t lds_bytes,
+                         hipStream_t s);
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,
                                  hipStream_t s);
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s);
@@ -54,6 +55,9 @@ hipError_t launch_finalize_partials2(const uint64_t *pa, int nba, int na, const 
                                      const uint64_t *pb, int nbb, int nb, const int32_t *kb, uint64_t *ob, hipStream_t s);
 hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int nslots, const int32_t *kinds,
                                     uint64_t *out, hipStream_t s);
+hipError_t launch_finalize_all(const uint64_t *pa, int nba, int na, const int32_t *ka, const uint64_t *pf, int nbf,
+                               const int32_t *kf, uint64_t *segm, int nseg, uint32_t *hll, int hll_words, uint64_t *out,
+                               hipStream_t s);
 hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_counts, int64_t nchunks,
                               int64_t *offsets, hipStream_t s);
 hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *offsets, int64_t nchunks,
@@ -937,6 +941,7 @@ struct Plan {
   };                                         // entries, bytes per value / dictionary entry
   std::vector<ProjCol> proj;
   bool has_filter = false, need_agg = false, need_mask = false, group_by = false, conj_only = false;
+  int fused_naggs = 0;  // > 0: the filter kernel aggregates (fused_tile), no aggregation launch
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
   int filter_blocks = 1, agg_blocks = 8;
@@ -950,6 +955,7 @@ struct Plan {
   void *gtab = nullptr, *ghll = nullptr, *slab = nullptr, *hslab = nullptr, *fo = nullptr;
   // pinned host landing area for the per-execution results: finals[64] | seg_matched[nseg] | hll
   uint64_t *pinned = nullptr;
+  uint64_t *pinned_dev = nullptr;  // the same memory as the device addresses it
   hipGraphExec_t graph_exec = nullptr;
   bool graph_failed = false;
   int executions = 0;
@@ -958,6 +964,7 @@ struct Plan {
   hipEvent_t ev[5] = {};
   std::mutex exec_mu;  // executions of one plan serialise (its buffers are reused)
   hipStream_t graph_stream = nullptr;  // the lane stream the graph was captured on
+  bool clean = false;  // device seg_matched / HLL registers are zero (finalize_all reset them last time)
 };
 
 static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
@@ -1533,9 +1540,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   for (const DevSeg &ds : dsegs) has_filter |= ds.node_end > ds.node_begin;
   bool need_agg = group_by;
   for (int a = 0; a < naggs; a++) need_agg |= dq.aggs[a].acc != ACC_COUNT;
-  const bool need_mask = has_filter && (need_agg || want_bitmap);
+  bool need_mask = has_filter && (need_agg || want_bitmap);
   const int64_t kSlotBudget = 19 * 1024;  // bytes per ring slot
   int32_t stage_stride = 0;
+  std::vector<double> seg_est(dsegs.size(), 1.0);
+  std::vector<int32_t> seg_off(dsegs.size(), 0);
   for (DevSeg &ds : dsegs) {
     int32_t off = 0;
     ds.num_stage = 0;
@@ -1560,13 +1569,28 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       }
     }
     stage_stride = std::max(stage_stride, off);
-    // conjunctive fast path: a program made of AND nodes over staged range / small-set scan leaves
+    // conjunctive fast path: a program made of AND nodes over staged range / small-set scan leaves and
+    // single-range sorted-index leaves (doc ranges intersected; the tiles outside are already pruned), or
+    // no program at all (every doc of the segment)
     ds.conj = 0;
+    ds.conj_path = 0;
+    ds.conj_range = 0;
+    ds.conj_lo = 0;
+    ds.conj_hi = ds.num_docs - 1;
     std::vector<std::pair<double, ConjLeaf>> conj;
-    bool ok = ds.node_end > ds.node_begin;
+    bool ok = true;
+    double est = 1.0;  // estimated selectivity of the program (product of the leaves')
     for (int i = ds.node_begin; i < ds.node_end && ok; i++) {
       const DevNode &dn = nodes[i];
       if (dn.op == DOP_AND) continue;
+      if (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_MATCH_ALL) continue;
+      if (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_DOC_RANGES && dn.count == 1) {
+        ds.conj_range = 1;
+        ds.conj_lo = std::max(ds.conj_lo, dn.lo);
+        ds.conj_hi = std::min(ds.conj_hi, dn.hi);
+        est *= double(std::max(0, dn.hi - dn.lo + 1)) / std::max(1, ds.num_docs);
+        continue;
+      }
       if (dn.op != DOP_LEAF || dn.lds_off < 0 ||
           !(dn.leaf_kind == PHIP_LEAF_DICT_RANGE || (dn.leaf_kind == PHIP_LEAF_DICT_SET && dn.small_set))) {
         ok = false;
@@ -1589,9 +1613,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         const uint64_t in_dict = card >= 64 ? ~0ull : ((1ull << card) - 1);
         sel = double(__builtin_popcountll(dn.set_mask & in_dict)) / card;
       }
+      est *= sel;
       conj.push_back({sel, L});
     }
-    if (ok && !conj.empty() && (int)conj.size() <= kMaxConj) {
+    if (ds.conj_range && ds.conj_lo > ds.conj_hi) ok = false;  // (empty: the host pruned the segment already)
+    if (ok && (int)conj.size() <= kMaxConj) {
+      ds.conj_path = 1;
+      seg_est[&ds - dsegs.data()] = est;
       // most selective leaf first: the short-circuit then skips the others on more tiles (AND is
       // commutative, so the doc set is unchanged)
       std::stable_sort(conj.begin(), conj.end(),
@@ -1611,6 +1639,50 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         while (ds.conj_p > 1 && ds.conj_p * conj[i].second.bits > 32) ds.conj_p >>= 1;
       }
       if (const char *e = getenv("PHIP_CONJ_P")) ds.conj_p = std::min(ds.conj_p, std::max(1, atoi(e)));  // measurement override
+    }
+    seg_off[&ds - dsegs.data()] = off;
+  }
+  // Fused aggregation (filter.hip fused_tile): every segment on the conjunctive path, aggregation only
+  // (no group-by, no HLL), at most 4 slots, a filter to fuse into. Value columns are then streamed with
+  // the tile (one more LDS-DMA region) when the expected matches per 128-byte line of the column reach
+  // kStreamValueMin -- a dense gather would touch every line anyway -- else gathered for matched docs.
+  bool conj_all = true;
+  for (const DevSeg &ds : dsegs) conj_all &= ds.conj_path != 0;
+  bool any_filter_prog = false;
+  for (const DevSeg &ds : dsegs) any_filter_prog |= ds.node_end > ds.node_begin;
+  int fused_naggs = 0;
+  {
+    const char *fe = getenv("PHIP_FUSE");  // measurement override: "0" keeps the separate aggregation kernel
+    bool fuse = conj_all && any_filter_prog && !group_by && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
+                !(fe && atoi(fe) == 0);
+    bool any_value = false;
+    for (int a = 0; a < naggs; a++) any_value |= dq.aggs[a].acc != ACC_COUNT;
+    if (fuse && any_value) {
+      fused_naggs = naggs;
+      const char *sv = getenv("PHIP_STREAM_VALUES");  // measurement override: "0" never, "1" always
+      const double kStreamValueMin = 0.5;
+      for (size_t i = 0; i < dsegs.size(); i++) {
+        DevSeg &ds = dsegs[i];
+        int32_t off = seg_off[i];
+        for (int a = 0; a < naggs; a++) {
+          const DevAgg &ag = dq.aggs[a];
+          if (ag.acc == ACC_COUNT) continue;
+          for (int c : {ag.col_a, ag.expr != PHIP_EXPR_COLUMN ? ag.col_b : -1}) {
+            if (c < 0) continue;
+            DevCol &dc = ds.cols[c];
+            if (!dc.has_dict || dc.lds_off >= 0) continue;
+            const bool dense = seg_est[i] * (1024.0 / std::max(1, dc.bits)) >= kStreamValueMin;
+            if (!(sv ? atoi(sv) != 0 : dense)) continue;
+            const int32_t bytes = 256 * dc.bits;
+            if (ds.num_stage >= kMaxConj + kMaxAggStage || off + bytes + 2 * kStagePad > kSlotBudget) continue;
+            dc.lds_off = off + kStagePad;
+            ds.stage[ds.num_stage++] = {(const uint8_t *)dc.words, bytes, dc.lds_off};
+            ds.num_dma += (int32_t)ceil_div(bytes, 1024);
+            off += bytes + 2 * kStagePad;
+          }
+        }
+        stage_stride = std::max(stage_stride, off);
+      }
     }
   }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
@@ -1646,8 +1718,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     P.proj.push_back(pc);
   }
   for (int s = 0; s < nseg; s++) P.seg_docs.push_back(segs[s]->num_docs);
-  bool conj_only = true;
-  for (const DevSeg &ds : dsegs) conj_only &= ds.conj > 0;
+  const bool conj_only = conj_all;
+  if (fused_naggs > 0) need_mask = false;  // the filter kernel aggregates its own tiles
   // ring depth: prefer 4 workgroups (16 waves) per CU for the VALU/LDS work of the leaves, and give
   // each wave the deepest ring that then fits the 160 KiB LDS (bytes in flight per CU =
   // blocks x 4 waves x (nbuf-1) x slot)
@@ -1750,9 +1822,14 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     dq.mask = (const uint32_t *)masks;
   }
   if (need_agg && !group_by) {
-    rc = P.alloc((size_t)agg_blocks * std::max(naggs, 1) * 8, &apart);
+    const int pblocks = fused_naggs > 0 ? filter_blocks : agg_blocks;
+    rc = P.alloc((size_t)pblocks * std::max(naggs, 1) * 8, &apart);
     if (rc) return rc;
     dq.partials = (uint64_t *)apart;
+    if (fused_naggs > 0) {
+      fq.agg_partials = (uint64_t *)apart;
+      fq.agg = (const DevAggQuery *)(base + dq_off);
+    }
   }
   void *gtab = nullptr, *ghll = nullptr, *slab = nullptr, *hslab = nullptr;
   if (group_by) {
@@ -1837,6 +1914,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.need_mask = need_mask;
   P.group_by = group_by;
   P.conj_only = conj_only;
+  P.fused_naggs = fused_naggs;
   P.want_bitmap = want_bitmap;
   P.filter_nwords = filter_nwords;
   P.filter_blocks = filter_blocks;
@@ -1865,9 +1943,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   {
     void *h = nullptr;
     const size_t pbytes = (64 + (size_t)nseg) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4;
-    HIP_TRY(hipHostMalloc(&h, pbytes, hipHostMallocDefault));
+    // device-visible (mapped) pinned memory: finalize_all_kernel writes the results straight into it
+    HIP_TRY(hipHostMalloc(&h, pbytes, hipHostMallocMapped));
     memset(h, 0, pbytes);
     P.pinned = (uint64_t *)h;
+    void *dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
+    P.pinned_dev = (uint64_t *)dp;
   }
   return PHIP_OK;
 }
@@ -1893,9 +1975,15 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   const int64_t filter_nwords = P.filter_nwords;
   const bool filter_words = P.want_bitmap;
   HIP_TRY(hipEventRecord(P.ev[0], st));
-  HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)nseg * 8, st));
+  // seg_matched and the HLL registers are zero between executions (finalize_all resets them); after a
+  // failed execution they are cleared here
+  const size_t hll_words = nhll && !group_by ? ((size_t)nhll << P.log2m) : 0;
+  if (!P.clean) {
+    HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)nseg * 8, st));
+    if (hll_words) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, hll_words * 4, st));
+  }
+  P.clean = false;
   if (filter_words) HIP_TRY(hipMemsetAsync(fo, 0, (size_t)filter_nwords * 8, st));
-  if (nhll && !group_by) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, (size_t)nhll * m_regs * 4, st));
   if (inv_words_total) {
     HIP_TRY(hipMemsetAsync(inv_words, 0, inv_words_total * 8, st));
     HIP_TRY(launch_roaring_or((const RoaringTask *)(base + tasks_off), (const RoaringGroup *)(base + P.rgroups_off),
@@ -1915,19 +2003,13 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
   HIP_TRY(hipEventRecord(P.ev[1], st));
-  if (has_filter && total_work > 0) HIP_TRY(launch_filter(fq, conj_only, filter_blocks, filter_lds, st));
+  const bool fused = P.fused_naggs > 0;
+  if (has_filter && total_work > 0)
+    HIP_TRY(launch_filter(fq, conj_only, P.fused_naggs, filter_blocks, filter_lds, st));
   HIP_TRY(hipEventRecord(P.ev[4], st));
-  if (need_agg && total_work > 0) HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
+  if (need_agg && total_work > 0 && !fused)
+    HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
   HIP_TRY(hipEventRecord(P.ev[2], st));
-  if (has_filter && need_agg && !group_by && total_work > 0 && naggs > 0) {
-    HIP_TRY(launch_finalize_partials2((const uint64_t *)apart, agg_blocks, naggs, dev_kinds, fin_agg,
-                                      (const uint64_t *)fpart, filter_blocks, 2, dev_kinds + naggs, fin_filter, st));
-  } else {
-    if (has_filter && total_work > 0)
-      HIP_TRY(launch_finalize_partials((const uint64_t *)fpart, filter_blocks, 2, dev_kinds + naggs, fin_filter, st));
-    if (need_agg && !group_by && total_work > 0)
-      HIP_TRY(launch_finalize_partials((const uint64_t *)apart, agg_blocks, naggs, dev_kinds, fin_agg, st));
-  }
   if (group_by && dq.mode == GB_LDS && total_work > 0)
     HIP_TRY(launch_slab_reduce((const uint64_t *)slab, agg_blocks, dq.tbl_words, dq.num_groups, dev_kinds,
                                (uint64_t *)gtab, (const uint32_t *)hslab, nhll ? dq.hll_words : 0, (uint32_t *)ghll, st));
@@ -1937,18 +2019,17 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (filter_words && need_mask && !dsegs.empty())
     HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
                                   filter_nwords, st));
-
-  // results land in the plan's pinned buffer: finals[64] | seg_matched[nseg] | hll registers
-  uint64_t *pin = P.pinned;
-  const size_t hll_bytes = nhll && !group_by ? ((size_t)nhll << P.log2m) * 4 : 0;
+  // every result lands in the plan's pinned buffer, written by the device: finals[64] | seg_matched[nseg] | HLL
   if (total_work > 0) {
-    HIP_TRY(hipMemcpyAsync(pin, P.finals, (64 + (size_t)nseg) * 8 + hll_bytes, hipMemcpyDeviceToHost, st));
-  } else {
-    if (has_filter) HIP_TRY(hipMemcpyAsync(pin + 64, seg_matched, nseg * 8, hipMemcpyDeviceToHost, st));
-    if (hll_bytes) HIP_TRY(hipMemcpyAsync(pin + 64 + nseg, dq.hll_regs, hll_bytes, hipMemcpyDeviceToHost, st));
+    const bool aggs_here = need_agg && !group_by && naggs > 0;
+    HIP_TRY(launch_finalize_all(aggs_here ? (const uint64_t *)apart : nullptr, fused ? filter_blocks : agg_blocks,
+                                aggs_here ? naggs : 0, dev_kinds, has_filter ? (const uint64_t *)fpart : nullptr,
+                                filter_blocks, dev_kinds + naggs, (uint64_t *)seg_matched, nseg, dq.hll_regs,
+                                (int)hll_words, P.pinned_dev, st));
   }
   if (!group_by) HIP_TRY(hipEventRecord(P.ev[3], st));
   (void)fin_agg;
+  (void)fin_filter;
   (void)fo;
   return PHIP_OK;
 }
@@ -2113,6 +2194,9 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     if (rc) return rc;
   }
   P.executions++;
+  if (P.total_work == 0) {  // no kernel ran: nothing matched, no registers set
+    memset(P.pinned + 64, 0, (size_t)P.nseg * 8 + (P.nhll && !P.group_by ? ((size_t)P.nhll << P.log2m) * 4 : 0));
+  }
   DevAggQuery &dq = P.dq;
   const int nseg = P.nseg, naggs = P.naggs, nhll = P.nhll, log2m = P.log2m, m_regs = P.m_regs;
   const bool group_by = P.group_by, has_filter = P.has_filter, need_agg = P.need_agg;
@@ -2287,6 +2371,12 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     }
     r.agg_bytes = ab;
   }
+  if (P.fused_naggs > 0) {  // one kernel filtered and aggregated: it owns both times and both byte counts
+    r.filter_kernel_ms = t_filter + t_agg;
+    r.agg_kernel_ms = 0.0;
+    r.filter_bytes += r.agg_bytes;
+    r.agg_bytes = 0;
+  }
 
   r.num_docs_scanned = matched;
   r.num_entries_scanned_in_filter = has_filter ? (int64_t)fin[33] : 0;
@@ -2311,6 +2401,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   r.long_exact = impl->exact.data();
   r.scan_kernel_ms = t_scan;
   r.device_ms = t_all;
+  P.clean = true;
   if (out_result) {
     *out_result = &impl.release()->pub;
   }

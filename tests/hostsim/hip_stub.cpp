@@ -23,6 +23,7 @@ hipError_t hipMalloc(void **p, size_t n) { *p = calloc(1, n ? n : 1); return hip
 hipError_t hipFree(void *p) { free(p); return hipSuccess; }
 hipError_t hipHostMalloc(void **p, size_t n, unsigned) { *p = calloc(1, n ? n : 1); return hipSuccess; }
 hipError_t hipHostFree(void *p) { free(p); return hipSuccess; }
+hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned) { *d = h; return hipSuccess; }
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t) { memmove(d, s, n); return hipSuccess; }
 hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) { memmove(d, s, n); return hipSuccess; }
 hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t) { memset(d, v, n); return hipSuccess; }
@@ -53,8 +54,9 @@ hipError_t launch_chunk_decode(int, int, const uint8_t *, const RawChunk *, int3
 hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }
 hipError_t launch_roaring_or(const RoaringTask *, const RoaringGroup *, int32_t, hipStream_t) { return hipSuccess; }
-hipError_t launch_filter(const DevFilter &q, bool, int nblocks, size_t, hipStream_t) {
+hipError_t launch_filter(const DevFilter &q, bool, int fused_naggs, int nblocks, size_t, hipStream_t) {
   memset(q.partials, 0, (size_t)nblocks * 2 * 8);
+  if (fused_naggs > 0) memset(q.agg_partials, 0, (size_t)nblocks * fused_naggs * 8);
   if (q.mask_out) memset(q.mask_out, 0, (size_t)q.total_work * 64 * 4);
   return hipSuccess;
 }
@@ -80,6 +82,18 @@ hipError_t launch_finalize_partials2(const uint64_t *, int, int na, const int32_
                                      int nb, const int32_t *, uint64_t *ob, hipStream_t) {
   for (int i = 0; i < na; i++) oa[i] = 0;
   for (int i = 0; i < nb; i++) ob[i] = 0;
+  return hipSuccess;
+}
+hipError_t launch_finalize_all(const uint64_t *, int, int na, const int32_t *, const uint64_t *, int, const int32_t *,
+                               uint64_t *segm, int nseg, uint32_t *hll, int hll_words, uint64_t *out, hipStream_t) {
+  memset(out, 0, 64 * 8);
+  memcpy(out + 64, segm, (size_t)nseg * 8);
+  memset(segm, 0, (size_t)nseg * 8);
+  if (hll_words) {
+    memcpy(out + 64 + nseg, hll, (size_t)hll_words * 4);
+    memset(hll, 0, (size_t)hll_words * 4);
+  }
+  (void)na;
   return hipSuccess;
 }
 hipError_t launch_finalize_partials(const uint64_t *, int, int nslots, const int32_t *, uint64_t *out, hipStream_t) {
