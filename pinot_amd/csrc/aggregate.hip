@@ -20,20 +20,19 @@
 
 namespace phip {
 
-// Groups [g0, g0 + U) of a tile; act bit u = doc 64(g0 + u) + lane matched. Accumulation order per
-// lane is the doc order, as in agg_chunk.
+// U docs per lane (d[u], act bit u = doc d[u] matched; inactive entries hold a valid doc and contribute the
+// identity): every load of the U docs is issued before the first use. staged: dict ids of the stage slots
+// come from the wave's LDS stage at tile-relative doc td + 64u (the dense-tile walk); otherwise from HBM.
 template <int NA, int U>
-__device__ __forceinline__ void agg_batch(cquery_t &q, cseg_t &seg, int32_t doc, uint32_t act, int32_t safe,
-                                          const PHIP_LDS uint8_t *stg, int32_t td, uint64_t (&acc)[NA],
-                                          lds_u32 *hll_lds) {
-  int32_t d[U];
-  batch_docs<U>(doc, act, safe, d);
+__device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t (&d)[U], uint32_t act,
+                                         const PHIP_LDS uint8_t *stg, int32_t td, bool staged, uint64_t (&acc)[NA],
+                                         lds_u32 *hll_lds) {
 #pragma unroll
   for (int a = 0; a < NA; a++) {
     if (a >= q.num_aggs) break;
     cagg_t &ag = q.aggs[a];
     const int kind = ag.acc;
-    const int ka = q.stage_slot_a[a], kb = q.stage_slot_b[a];
+    const int ka = staged ? q.stage_slot_a[a] : -1, kb = staged ? q.stage_slot_b[a] : -1;
     const int ja = ka < 0 ? 0 : ka, jb = kb < 0 ? 0 : kb;
     const BatchSrc sa{ka >= 0 ? (const PHIP_LDS uint32_t *)(stg + q.stage_off[ja]) : nullptr, td, act,
                       ka >= 0 && q.stage_dict_off[ja] >= 0 ? stg + q.stage_dict_off[ja] : nullptr};
@@ -71,6 +70,37 @@ __device__ __forceinline__ void agg_batch(cquery_t &q, cseg_t &seg, int32_t doc,
       acc[a] = as_u64(cur);
     }
   }
+}
+
+// Groups [g0, g0 + U) of a tile; act bit u = doc 64(g0 + u) + lane matched. Accumulation order per
+// lane is the doc order, as in agg_chunk.
+template <int NA, int U>
+__device__ __forceinline__ void agg_batch(cquery_t &q, cseg_t &seg, int32_t doc, uint32_t act, int32_t safe,
+                                          const PHIP_LDS uint8_t *stg, int32_t td, uint64_t (&acc)[NA],
+                                          lds_u32 *hll_lds) {
+  int32_t d[U];
+  batch_docs<U>(doc, act, safe, d);
+  agg_docs<NA, U>(q, seg, d, act, stg, td, true, acc, hll_lds);
+}
+
+// Up to kBatch chunks of 64 ring entries at once (GB_NONE): chunk u holds ring[tail + 64u + lane] while
+// 64u + lane < n, so its loads are in flight together -- one gather round trip per 256 matched docs, not
+// per 64. Per lane the docs stay in ring (= doc) order.
+constexpr int kRing = kRingAgg;  // agg_ring_batch runs in GB_NONE only
+
+template <int NA>
+__device__ __forceinline__ void agg_ring_batch(cquery_t &q, cseg_t &seg, const lds_u32 *ring, int tail, int n,
+                                               uint64_t (&acc)[NA], lds_u32 *hll_lds, int32_t safe) {
+  const int lane = lane_id();
+  int32_t d[kBatch];
+  uint32_t act = 0;
+#pragma unroll
+  for (int u = 0; u < kBatch; u++) {
+    const bool on = 64 * u + lane < n;
+    d[u] = on ? (int32_t)ring[(tail + 64 * u + lane) & (kRing - 1)] : safe;
+    act |= on ? (1u << u) : 0u;
+  }
+  agg_docs<NA, kBatch>(q, seg, d, act, nullptr, 0, false, acc, hll_lds);
 }
 
 // GB_HASH: linear probing from a 64-bit finaliser of the key; a slot is claimed by CAS(empty -> key).
@@ -176,8 +206,9 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);
   PHIP_LDS unsigned char *lds = (PHIP_LDS unsigned char *)smem;
-  lds_u32 *ring = (lds_u32 *)lds + wave * kRing;
-  PHIP_LDS unsigned char *stage = lds + kAggWaves * kRing * 4;  // GB_NONE dense-tile staging
+  constexpr int R = ring_entries(MODE);
+  lds_u32 *ring = (lds_u32 *)lds + wave * R;
+  PHIP_LDS unsigned char *stage = lds + kAggWaves * R * 4;  // GB_NONE dense-tile staging
   PHIP_LDS unsigned char *stg = stage + wave * q.stage_bytes;
   const uint32_t stg_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)stg);
   PHIP_LDS unsigned char *rest = stage + kAggWaves * q.stage_bytes;
@@ -226,9 +257,11 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
     const uint32_t m_raw = m_next;
     if (mask != nullptr && t + wx < xe) m_next = __builtin_nontemporal_load(mask + (size_t)(t + wx) * 64 + lane);  // prefetch
     if (segs[si].work_begin + segs[si].num_work <= t) {
-      if (head > tail) {  // leftover (< 64) matched docs of the previous segment
+      if constexpr (MODE == GB_NONE) {
+        if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
+      } else if (head > tail) {  // leftover (< 64) matched docs of the previous segment
         const bool act = lane < head - tail;
-        const int32_t doc = act ? (int32_t)ring[(tail + lane) & (kRing - 1)] : 0;
+        const int32_t doc = act ? (int32_t)ring[(tail + lane) & (R - 1)] : 0;
         do_chunk<NA, MODE>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
       }
       head = tail = 0;
@@ -298,19 +331,26 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
         any &= ~(1u << bit);
         const bool b = (m >> bit) & 1u;
         const uint64_t mm = ballot(b);
-        if (b) ring[(head + mbcnt64(mm)) & (kRing - 1)] = (uint32_t)(doc0 + (31 - bit) * 64 + lane);
+        if (b) ring[(head + mbcnt64(mm)) & (R - 1)] = (uint32_t)(doc0 + (31 - bit) * 64 + lane);
         head += __popcll(mm);
-        if (head - tail >= 64) {
-          const int32_t doc = (int32_t)ring[(tail + lane) & (kRing - 1)];
+        if constexpr (MODE == GB_NONE) {
+          if (head - tail >= 64 * kBatch) {
+            agg_ring_batch<NA>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0);
+            tail += 64 * kBatch;
+          }
+        } else if (head - tail >= 64) {
+          const int32_t doc = (int32_t)ring[(tail + lane) & (R - 1)];
           tail += 64;
           do_chunk<NA, MODE>(q, seg, doc, true, acc, hll_lds, tbl, hll_packed);
         }
       }
     }
   }
-  if (head > tail) {
+  if constexpr (MODE == GB_NONE) {
+    if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
+  } else if (head > tail) {
     const bool act = lane < head - tail;
-    const int32_t doc = act ? (int32_t)ring[(tail + lane) & (kRing - 1)] : 0;
+    const int32_t doc = act ? (int32_t)ring[(tail + lane) & (R - 1)] : 0;
     do_chunk<NA, MODE>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
   }
 

@@ -23,10 +23,14 @@ constexpr int kMaxRing = 8;           // LDS-DMA ring slots per wave
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;
-constexpr int kRing = 128;
+// per-wave ring of matched doc ids (u32): GB_NONE batches up to 4 chunks (+ one group), the group-by walks
+// take one chunk at a time (their LDS goes to the table)
+constexpr int kRingAgg = 512;
+constexpr int kRingGroup = 128;
+constexpr int ring_entries(int mode) { return mode == 0 ? kRingAgg : kRingGroup; }
 constexpr int kMaxAggStage = 4;      // staged aggregation columns
 constexpr int kAggStageBudget = 4096; // LDS bytes per wave for them
-constexpr int kAggLdsDict = 1024;     // dictionaries up to this many bytes are copied next to them            // per-wave ring of matched doc ids (u32), flushed 64 at a time
+constexpr int kAggLdsDict = 1024;     // dictionaries up to this many bytes are copied next to them
 
 // Accumulator kinds of one aggregation slot.
 enum AccKind : int32_t {

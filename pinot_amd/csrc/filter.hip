@@ -522,59 +522,142 @@ __device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_
 }
 
 // ------------------------------------------------------------------------------------------------
-// fused projection + aggregation (conjunctive programs without group-by / HLL). The tile's matched docs
-// are aggregated right after the mask is known: kBatch consecutive 64-doc groups at a time (groups with
-// no match anywhere in the wave are skipped), dict ids of columns staged in the tile's ring slot (filter
-// columns, and value columns the host chose to stream) read from LDS, the others decoded from HBM; then
-// the dictionary gathers and the expression, into per-lane accumulators in doc order -- the agg_batch
-// walk of aggregate.hip without the mask round trip, the re-read of the filter columns and a second launch.
+// fused projection + aggregation (conjunctive programs without group-by / HLL). After a tile's mask is
+// known its matched docs are compacted into a per-wave LDS ring (mbcnt ranks, as the aggregation kernel
+// does) and projected 64 at a time, so a sparse tile costs one gather round trip instead of one per
+// group; the chunk is flushed at the end of the tile because columns staged in the tile's ring slot
+// (the filter columns, and value columns the host chose to stream) are read from LDS by tile-relative
+// doc. Dictionaries of <= 64 entries live one entry per lane (loaded when the wave enters a segment) and
+// are read with ds_bpermute; larger ones are gathered from HBM. Per-lane accumulators take their docs
+// in doc order, as agg_chunk does -- the aggregation kernel's walk without the mask round trip, the
+// re-read of the filter columns and a second launch.
 // ------------------------------------------------------------------------------------------------
-template <int NA>
-__device__ __forceinline__ void fused_tile(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
-                                           uint64_t (&acc)[NA]) {
-  const uint32_t gm = wave_or32(mask);
-  if (gm == 0) return;
+constexpr int kFusedRing = 128;  // u16 tile-relative doc ids per wave (a partial chunk + one group)
+
+// The lane's share of a small dictionary: entry `lane` (64-bit image of the value), or 0.
+struct SmallDict {
+  uint32_t lo, hi;
+  bool on;
+};
+
+__device__ __forceinline__ SmallDict load_small_dict(ccol_t &c) {
+  SmallDict d{0u, 0u, false};
+  if (!c.has_dict || c.card > 64 || c.type == PHIP_TYPE_STRING) return d;
+  d.on = true;
   const int lane = lane_id();
-#pragma unroll 1
-  for (int g0 = 0; g0 < kTileGroups; g0 += kBatch) {
-    if (((gm << g0) >> (32 - kBatch)) == 0) continue;  // no lane matched in groups [g0, g0 + kBatch)
-    const uint32_t act = __builtin_bitreverse32(mask << g0) & ((1u << kBatch) - 1u);
-    int32_t d[kBatch];
-    batch_docs<kBatch>(t.doc0 + 64 * g0 + lane, act, t.doc0, d);
-    const int32_t td = 64 * g0 + lane;
-#pragma unroll
-    for (int a = 0; a < NA; a++) {
-      if (a >= aq.num_aggs) break;
-      cagg_t &ag = aq.aggs[a];
-      const int kind = ag.acc;
-      if (kind == ACC_COUNT) {
-        acc[a] += (uint64_t)__popc(act);
-        continue;
-      }
-      ccol_t &ca = seg.cols[ag.col_a];
-      ccol_t &cb = seg.cols[ag.expr != PHIP_EXPR_COLUMN ? ag.col_b : ag.col_a];
-      const BatchSrc sa{ca.lds_off >= 0 ? (const PHIP_LDS uint32_t *)(t.stage + ca.lds_off) : nullptr, td, act, nullptr};
-      const BatchSrc sb{cb.lds_off >= 0 ? (const PHIP_LDS uint32_t *)(t.stage + cb.lds_off) : nullptr, td, act, nullptr};
-      if (kind == ACC_SUM_I64) {
-        int64_t v[kBatch];
-        batch_expr_i64<kBatch>(seg, ag, d, sa, sb, v);
-#pragma unroll
-        for (int u = 0; u < kBatch; u++) acc[a] += ((act >> u) & 1u) ? (uint64_t)v[u] : 0ull;
-      } else {
-        double v[kBatch];
-        batch_expr_f64<kBatch>(seg, ag, d, sa, sb, v);
-        double cur = as_f64(acc[a]);
-#pragma unroll
-        for (int u = 0; u < kBatch; u++) {
-          const bool on = (act >> u) & 1u;
-          if (kind == ACC_SUM_F64) cur = cur + (on ? v[u] : 0.0);
-          else if (kind == ACC_MIN_F64) cur = fmin(cur, on ? v[u] : __builtin_huge_val());
-          else cur = fmax(cur, on ? v[u] : -__builtin_huge_val());
-        }
-        acc[a] = as_u64(cur);
+  if (lane < c.card) {
+    if (c.type == PHIP_TYPE_INT || c.type == PHIP_TYPE_FLOAT) {
+      d.lo = ((const PHIP_GLB uint32_t *)c.dict)[lane];
+    } else {
+      const uint64_t v = ((const PHIP_GLB uint64_t *)c.dict)[lane];
+      d.lo = (uint32_t)v;
+      d.hi = (uint32_t)(v >> 32);
+    }
+  }
+  return d;
+}
+
+// dict id of tile-relative doc td: from the staged words (LDS) or the forward index in HBM
+__device__ __forceinline__ uint32_t fused_id(ccol_t &c, const Tile &t, int32_t td) {
+  const uint32_t b = (uint32_t)c.bits;
+  if (c.lds_off >= 0) return window_at((const PHIP_LDS uint32_t *)(t.stage + c.lds_off), td * (int32_t)b) >> (32 - b);
+  return decode_bits(c.words, (uint64_t)(uint32_t)(t.doc0 + td) * b, b);
+}
+
+__device__ __forceinline__ double fused_f64(ccol_t &c, const SmallDict &sd, const Tile &t, int32_t td) {
+  if (!c.has_dict) return raw_f64(c, t.doc0 + td);
+  const uint32_t id = fused_id(c, t, td);
+  if (sd.on) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.lo);
+    switch (c.type) {
+      case PHIP_TYPE_INT: return (double)(int32_t)lo;
+      case PHIP_TYPE_FLOAT: return (double)__uint_as_float(lo);
+      default: {
+        const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.hi) << 32) | lo;
+        return c.type == PHIP_TYPE_LONG ? (double)(int64_t)v : __longlong_as_double((long long)v);
       }
     }
   }
+  return dict_f64(c, id);
+}
+
+__device__ __forceinline__ int64_t fused_i64(ccol_t &c, const SmallDict &sd, const Tile &t, int32_t td) {
+  if (!c.has_dict) return raw_i64(c, t.doc0 + td);
+  const uint32_t id = fused_id(c, t, td);
+  if (sd.on) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.lo);
+    if (c.type == PHIP_TYPE_INT) return (int64_t)(int32_t)lo;
+    const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.hi) << 32) | lo;
+    return (int64_t)v;  // (integral sums only see INT / LONG columns)
+  }
+  return dict_i64(c, id);
+}
+
+// one chunk of up to 64 matched docs of the current tile (lane: tile-relative doc td, active flag)
+template <int NA>
+__device__ __forceinline__ void fused_chunk(cquery_t &aq, cseg_t &seg, const Tile &t, int32_t td, bool act,
+                                            const SmallDict (&sda)[NA], const SmallDict (&sdb)[NA],
+                                            uint64_t (&acc)[NA]) {
+#pragma unroll
+  for (int a = 0; a < NA; a++) {
+    if (a >= aq.num_aggs) break;
+    cagg_t &ag = aq.aggs[a];
+    const int kind = ag.acc;
+    if (kind == ACC_COUNT) {
+      acc[a] += act ? 1ull : 0ull;
+      continue;
+    }
+    ccol_t &ca = seg.cols[ag.col_a];
+    if (kind == ACC_SUM_I64) {
+      int64_t x = fused_i64(ca, sda[a], t, td);
+      if (ag.expr != PHIP_EXPR_COLUMN) {
+        const int64_t y = fused_i64(seg.cols[ag.col_b], sdb[a], t, td);
+        x = ag.expr == PHIP_EXPR_ADD ? x + y : (ag.expr == PHIP_EXPR_SUB ? x - y : x * y);
+      }
+      acc[a] += act ? (uint64_t)x : 0ull;
+    } else {
+      double x = fused_f64(ca, sda[a], t, td);
+      if (ag.expr != PHIP_EXPR_COLUMN) {
+        const double y = fused_f64(seg.cols[ag.col_b], sdb[a], t, td);
+        x = ag.expr == PHIP_EXPR_ADD ? x + y : (ag.expr == PHIP_EXPR_SUB ? x - y : x * y);
+      }
+      const double cur = as_f64(acc[a]);
+      double nv;
+      if (kind == ACC_SUM_F64) nv = cur + (act ? x : 0.0);
+      else if (kind == ACC_MIN_F64) nv = fmin(cur, act ? x : __builtin_huge_val());
+      else nv = fmax(cur, act ? x : -__builtin_huge_val());
+      acc[a] = as_u64(nv);
+    }
+  }
+}
+
+template <int NA>
+__device__ __forceinline__ void fused_tile(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
+                                           PHIP_LDS uint16_t *ring, const SmallDict (&sda)[NA],
+                                           const SmallDict (&sdb)[NA], uint64_t (&acc)[NA]) {
+  uint32_t any = wave_or32(mask);
+  if (any == 0) return;
+  const int lane = lane_id();
+  int head = 0, tail = 0;  // wave-uniform ring cursors
+  while (any) {
+    const int bit = 31 - __builtin_clz(any);
+    any &= ~(1u << bit);
+    const bool b = (mask >> bit) & 1u;
+    const uint64_t mm = ballot(b);
+    if (b) ring[(head + mbcnt64(mm)) & (kFusedRing - 1)] = (uint16_t)((31 - bit) * 64 + lane);
+    head += __popcll(mm);
+    if (head - tail >= 64) {
+      const int32_t td = ring[(tail + lane) & (kFusedRing - 1)];
+      tail += 64;
+      fused_chunk<NA>(aq, seg, t, td, true, sda, sdb, acc);
+    }
+  }
+  if (head > tail) {
+    const bool act = lane < head - tail;
+    const int32_t td = act ? (int32_t)ring[(tail + lane) & (kFusedRing - 1)] : 0;
+    fused_chunk<NA>(aq, seg, t, td, act, sda, sdb, acc);
+  }
+  __builtin_amdgcn_wave_barrier();  // ring reads done before the next tile's writes
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -662,6 +745,9 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   const int nbuf = q.nbuf;
   const int stride = q.stage_stride;
   PHIP_LDS uint8_t *ring = (PHIP_LDS uint8_t *)(smem + (size_t)wave * nbuf * stride);
+  // fused aggregation: the wave's matched-doc ring sits after every wave's DMA ring
+  PHIP_LDS uint16_t *docring =
+      (PHIP_LDS uint16_t *)(smem + (size_t)kFilterWaves * nbuf * stride) + (NA > 0 ? wave * kFusedRing : 0);
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
 
   cseg_t *segs = (cseg_t *)q.segs;
@@ -674,11 +760,16 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   // (atomics only add to the true count). Waiting for fewer outstanding operations is always safe.
   const int nd = q.min_dma;
   const int st = q.mask_out != nullptr ? 1 : 0;
-  uint64_t acc[NA > 0 ? NA : 1];
+  constexpr int NAX = NA > 0 ? NA : 1;
+  uint64_t acc[NAX];
+  SmallDict sda[NAX], sdb[NAX];
   if constexpr (NA > 0) {
     cquery_t &aq = *(cquery_t *)q.agg;
 #pragma unroll
-    for (int a = 0; a < NA; a++) acc[a] = a < aq.num_aggs ? acc_init(aq.aggs[a].acc) : 0;
+    for (int a = 0; a < NA; a++) {
+      acc[a] = a < aq.num_aggs ? acc_init(aq.aggs[a].acc) : 0;
+      sda[a] = sdb[a] = SmallDict{0u, 0u, false};
+    }
   }
 
   // prefetch cursor: tiles [begin, pf) have their DMA issued (pfc of them)
@@ -717,6 +808,15 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
       si = si < 0 ? 0 : si;
       while (si + 1 < q.num_segs && segs[si + 1].work_begin <= t) si++;
       seg_end = segs[si].work_begin + segs[si].num_work;
+      if constexpr (NA > 0) {  // the segment's small dictionaries, one entry per lane
+        cquery_t &aq = *(cquery_t *)q.agg;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+          if (a >= aq.num_aggs || aq.aggs[a].acc == ACC_COUNT) continue;
+          sda[a] = load_small_dict(segs[si].cols[aq.aggs[a].col_a]);
+          if (aq.aggs[a].expr != PHIP_EXPR_COLUMN) sdb[a] = load_small_dict(segs[si].cols[aq.aggs[a].col_b]);
+        }
+      }
     }
     cseg_t &seg = segs[si];
     Tile tl;
@@ -742,7 +842,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     scanned += scanned_t;
     lane_matched += (uint32_t)__popc(mask);
     if (st) ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
-    if constexpr (NA > 0) fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, acc);
+    if constexpr (NA > 0) fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, docring, sda, sdb, acc);
     slot = slot + 1 == nbuf ? 0 : slot + 1;
   }
 #undef PHIP_PREFETCH

@@ -1652,9 +1652,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   for (const DevSeg &ds : dsegs) any_filter_prog |= ds.node_end > ds.node_begin;
   int fused_naggs = 0;
   {
-    const char *fe = getenv("PHIP_FUSE");  // measurement override: "0" keeps the separate aggregation kernel
+    // Fusion saves a launch, the mask round trip and the filter columns' re-read, but a streaming filter
+    // wave that stops for a tile's projection gathers leaves its LDS-DMA ring idle. Measured on SSB SF100
+    // (tools/ab_env.sh, profiles/r02_*): fused wins while the query has at most a few thousand work tiles
+    // (Q1.2 / Q1.3 over the sorted layout: 0.112 -> 0.081 / 0.066 -> 0.057 ms p50) and loses beyond
+    // (Q1.1 sorted, 44K tiles: 0.207 -> 0.270 ms; unsorted, 293K tiles: 1.6 -> 2.4 ms per step).
+    const char *fe = getenv("PHIP_FUSE");  // measurement override: "0" never, "1" always, unset = by size
+    const int64_t kFuseMaxTiles = 8192;
     bool fuse = conj_all && any_filter_prog && !group_by && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
-                !(fe && atoi(fe) == 0);
+                (fe ? atoi(fe) != 0 : total_work <= kFuseMaxTiles);
     bool any_value = false;
     for (int a = 0; a < naggs; a++) any_value |= dq.aggs[a].acc != ACC_COUNT;
     if (fuse && any_value) {
@@ -1727,8 +1733,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   {
     const char *env = getenv("PHIP_FILTER_BPC");  // measurement override
     const int want = env ? std::max(1, std::min(8, atoi(env))) : (conj_only ? 6 : 4);
+    const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * 128 * 2 : 0;  // filter.hip kFusedRing u16
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
-      const int64_t nb = std::min<int64_t>(kMaxRing, (160 * 1024 - 1024) / ((int64_t)bpc * kFilterWaves * stage_stride));
+      const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024 - 1024) / bpc - fring) / ((int64_t)kFilterWaves * stage_stride));
       if (nb >= 2) {
         nbuf = (int)nb;
         fbpc = bpc;
@@ -1736,7 +1743,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
     if (nbuf < 2) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
   }
-  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride;
+  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_naggs > 0 ? (size_t)kFilterWaves * 128 * 2 : 0);
   const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "contig"
   const bool xcd_walk = walk_env ? strcmp(walk_env, "xcd") == 0 : false;  // contig measured faster
   int filter_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)dev->num_cus * fbpc,
@@ -1747,7 +1754,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   dq.log2m = log2m;
   if (dq.mode != GB_HASH) dq.mode = group_by ? GB_GLOBAL : GB_NONE;
   const int m_regs = nhll ? (1 << log2m) : 0;
-  size_t agg_lds = (size_t)kAggWaves * kRing * 4 + (size_t)kAggWaves * dq.stage_bytes;
+  size_t agg_lds = (size_t)kAggWaves * ring_entries(dq.mode) * 4 + (size_t)kAggWaves * dq.stage_bytes;
   int agg_bpc = 4;
   if (group_by && dq.mode == GB_HASH) {
     if ((int64_t)nhll * dq.num_groups * m_regs * 4 > ((int64_t)16 << 30))
@@ -2082,7 +2089,7 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   if (nhll) HIP_TRY(hipMemsetAsync(hll, 0, (size_t)nhll * cap * m_regs * 4, st));
   HIP_TRY(hipMemcpyAsync(ddq, &dq, sizeof(dq), hipMemcpyHostToDevice, st));
   if (P.total_work > 0)
-    HIP_TRY(launch_agg(dq, (const DevAggQuery *)ddq, P.agg_blocks, (size_t)kAggWaves * kRing * 4, st));
+    HIP_TRY(launch_agg(dq, (const DevAggQuery *)ddq, P.agg_blocks, (size_t)kAggWaves * kRingGroup * 4, st));
   // compact the occupied slots
   const int64_t nchunks = ceil_div(cap, 1024);
   void *cc, *offs, *slots;
