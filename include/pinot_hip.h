@@ -256,4 +256,59 @@ PHIP_API void phip_result_free(phip_result *result);
 /* Filter only, one segment: words_out receives ceil(num_docs/64) bitmap words. */
 PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *words_out, int64_t num_words);
 
+/* ---- multi-GPU servers: one process per GPU, partial group tables merged on the device ----------------
+ * The reference's combine merges per-segment group-by results by VALUE on one JVM
+ * (GroupByCombineOperator.java:138-147 upserting into an IndexedTable). A server spread over several GPUs
+ * instead keys every group-by column by a NODE-GLOBAL dictionary: the sorted union of
+ * the column's dictionary values over every segment on every GPU, registered once per column after load.
+ * Plans created afterwards key that column by ids in it on every GPU, so each GPU's dense partial table has
+ * the same shape and key order and the GPUs merge them element-wise with RCCL all-reduce on the device
+ * buffers -- no host round trip of group records.
+ *
+ * phip_global_dictionary: values as phip_dictionary_view lays them out (LE typed array, or
+ * cardinality x string_width '\0'-padded bytes), ascending, distinct. Registering a column again replaces
+ * it for plans created later; cardinality = -1 removes the registration. Columns are keyed by the name the
+ * query descriptors use (one table per server process). A segment value missing from it fails plan creation
+ * with PHIP_ERR_INVALID. */
+PHIP_API int32_t phip_global_dictionary(int32_t device, const char *column, int32_t data_type, int32_t cardinality,
+                                        int32_t string_width, const void *values);
+
+/* Row kinds of a partial table; the reduce operator of each row follows from its kind. */
+#define PHIP_ROW_COUNT 0   /* int64 doc count per group (row 0; unused rows of COUNT aggregations hold 0): SUM */
+#define PHIP_ROW_SUM_I64 1 /* exact int64 sum: SUM (int64) */
+#define PHIP_ROW_SUM_F64 2 /* double sum (bits): SUM (float64) */
+#define PHIP_ROW_MIN 3     /* order-preserving u64 image of a double (f64_ordered): MIN as unsigned */
+#define PHIP_ROW_MAX 4     /* same image: MAX as unsigned */
+#define PHIP_ROW_HLL 5     /* row unused (0); the registers are in phip_partial.hll: MAX (int32) */
+#define PHIP_PARTIAL_MAX_ROWS 9
+
+typedef struct phip_partial {
+  int64_t num_groups;   /* dense key space G = product of the group-by columns' (global) cardinalities */
+  int32_t num_rows;     /* 1 + num_aggregations */
+  int32_t num_hll;
+  int32_t log2m;
+  int32_t device;
+  uint64_t *table;      /* DEVICE memory owned by the plan: [num_rows][G] u64, row 0 = doc count per group */
+  uint32_t *hll;        /* DEVICE memory: [num_hll][G][1 << log2m] u32 registers, or NULL */
+  /* row_kinds[r] for r < num_rows. A caller merging GPUs whose plans disagree on SUM_I64 vs SUM_F64 for a
+   * row (the int64-overflow bound is per GPU) converts its int64 row to doubles in place and sets the kind to
+   * PHIP_ROW_SUM_F64 before phip_plan_finish. */
+  int32_t row_kinds[PHIP_PARTIAL_MAX_ROWS];
+  int32_t global_keys;  /* 1 when every group-by column is keyed by a registered global dictionary (else the
+                         * key order is this GPU's own and the table must not be merged element-wise) */
+  /* This GPU's execution statistics (phip_result order: docs scanned, entries scanned in filter, entries
+   * scanned post filter, total docs, segments processed, segments matched); summed over GPUs by the caller. */
+  int64_t stats[6];
+} phip_partial;
+
+/* Runs a dense group-by plan up to its partial table and returns it (the kernels have completed). Returns
+ * PHIP_ERR_UNSUPPORTED, with nothing to merge, for hash-table key spaces and when the GPU's distinct groups
+ * reach numGroupsLimit (the per-segment first-seen limit needs the record path: phip_plan_execute). Until
+ * phip_plan_finish the table belongs to the caller: it may all-reduce it in place (on any stream, synchronised
+ * before phip_plan_finish). No other execution of the same plan may start in between. */
+PHIP_API int32_t phip_plan_execute_partial(uint64_t plan, phip_partial *out_partial);
+/* Compacts the (merged) partial table into a result exactly as phip_plan_execute would -- present groups,
+ * the server-level trim (trim_size), statistics taken from merged->stats. */
+PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phip_result **out_result);
+
 #endif /* PINOT_HIP_H_ */

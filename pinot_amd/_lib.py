@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "phip_init", "phip_shutdown", "phip_device_count", "phip_last_error", "phip_version",
     "phip_segment_load", "phip_segment_unload", "phip_segment_device_bytes", "phip_query",
     "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap", "phip_plan_create", "phip_plan_execute",
-    "phip_plan_destroy",
+    "phip_plan_destroy", "phip_global_dictionary", "phip_plan_execute_partial", "phip_plan_finish",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -100,6 +100,19 @@ class DictionaryView(ctypes.Structure):
                 ("reserved", ctypes.c_int32), ("values", ctypes.c_void_p)]
 
 
+ROW_COUNT, ROW_SUM_I64, ROW_SUM_F64, ROW_MIN, ROW_MAX, ROW_HLL = range(6)
+PARTIAL_MAX_ROWS = 9
+
+
+class Partial(ctypes.Structure):
+    """phip_partial: a GPU's dense partial group table (device pointers), merged by the caller."""
+    _fields_ = [("num_groups", ctypes.c_int64), ("num_rows", ctypes.c_int32), ("num_hll", ctypes.c_int32),
+                ("log2m", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("table", ctypes.c_void_p), ("hll", ctypes.c_void_p),
+                ("row_kinds", ctypes.c_int32 * PARTIAL_MAX_ROWS), ("global_keys", ctypes.c_int32),
+                ("stats", ctypes.c_int64 * 6)]
+
+
 class PhipError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"pinot_hip error {code}: {msg}")
@@ -116,6 +129,13 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (same soname), so importing torch
+    # first makes the library bind to that copy. Loaded the other way round, the process would hold two
+    # runtimes and torch (RCCL merges, engine/distributed.py) would find no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     i32, u64, i64 = ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64
     lib.phip_init.argtypes = [ctypes.POINTER(i32), i32]
@@ -148,6 +168,12 @@ def load():
     lib.phip_plan_execute.restype = i32
     lib.phip_plan_destroy.argtypes = [u64]
     lib.phip_plan_destroy.restype = i32
+    lib.phip_global_dictionary.argtypes = [i32, ctypes.c_char_p, i32, i32, i32, ctypes.c_void_p]
+    lib.phip_global_dictionary.restype = i32
+    lib.phip_plan_execute_partial.argtypes = [u64, ctypes.POINTER(Partial)]
+    lib.phip_plan_execute_partial.restype = i32
+    lib.phip_plan_finish.argtypes = [u64, ctypes.POINTER(Partial), ctypes.POINTER(ctypes.POINTER(Result))]
+    lib.phip_plan_finish.restype = i32
     _lib = lib
     return lib
 

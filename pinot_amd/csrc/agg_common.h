@@ -173,7 +173,6 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
 // tile's first doc (always valid) and contribute the identity.
 // ------------------------------------------------------------------------------------------------
 constexpr int kBatch = 4;
-constexpr int kDenseMin = 640;  // matched docs per 2048-doc tile from which the batched walk is used
 
 template <int U>
 __device__ __forceinline__ void batch_docs(int32_t doc, uint32_t act, int32_t safe, int32_t (&d)[U]) {

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
     const uint32_t m = mask != nullptr ? (m_raw & valid) : valid;
     bool dense = ballot(m != valid) == 0;  // every valid doc of the tile matched
     if constexpr (MODE == GB_NONE && kDense) {
-      if (!dense) dense = wave_sum_u32((uint32_t)__popc(m)) >= (uint32_t)kDenseMin;
+      if (!dense) dense = wave_sum_u32((uint32_t)__popc(m)) >= (uint32_t)q.dense_min;
     }
     bool batched = false;
     if constexpr (MODE == GB_NONE && kDense) batched = dense;

@@ -7,6 +7,7 @@ namespace phip {
 
 constexpr int kMaxQueryColumns = 16;  // distinct columns one query may reference
 constexpr int kMaxAggs = 8;           // aggregation slots per query
+constexpr int kDenseMin = 640;        // default DevAggQuery::dense_min
 constexpr int kMaxFilterStack = 6;    // postfix evaluation stack depth (host rejects deeper programs)
 constexpr int kMaxGroupBy = 4;
 constexpr int kWave = 64;             // CDNA wavefront
@@ -214,6 +215,8 @@ struct DevAggQuery {
   int32_t seg_keys;
   int32_t seg_key_mult;
   uint32_t *first_doc;
+  int32_t dense_min;  // GB_NONE + dense_batch: matched docs per 2048-doc tile from which the batched walk is used
+  int32_t pad_dense;
 };
 
 // ORDER BY on group-by columns for the device trim (trim.hip)

@@ -255,6 +255,7 @@ struct Device {
     int32_t card = 0;
     int32_t type = 0;
     int32_t width = 0;
+    bool global = false;          // the column's registered node-global dictionary
     std::vector<uint8_t> values;  // LE typed or fixed-width strings
     ~Remap() {
       for (auto *p : dev)
@@ -262,6 +263,14 @@ struct Device {
     }
   };
   std::map<std::string, std::shared_ptr<Remap>> remaps;
+  // node-global dictionaries registered by phip_global_dictionary, per column
+  struct GlobalDict {
+    int32_t type = 0, card = 0, width = 0;
+    uint64_t gen = 0;
+    std::vector<uint8_t> values;  // LE typed or card x width padded strings
+  };
+  std::map<std::string, GlobalDict> globals;
+  uint64_t global_gen = 0;
 };
 
 struct Container {
@@ -748,10 +757,58 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
 
 std::string dict_key(const ColumnStore &c) { return std::string((const char *)c.host_dict.data(), c.host_dict.size()); }
 
-// Query-global dictionary of one group-by column across the query's segments.
+// Total order of dictionary values as the reference sorts them: numbers by value (FLOAT / DOUBLE in
+// Float.compare / Double.compare order: -0.0 < 0.0, NaN last), strings as '\0'-padded bytes (memcmp order ==
+// String.compareTo for ASCII / BMP UTF-8).
+static int compare_value(int32_t type, const uint8_t *a, const uint8_t *b, int width) {
+  auto ord = [](uint64_t u, int bits) {  // order-preserving unsigned image of an IEEE value
+    const uint64_t sign = 1ull << (bits - 1);
+    return (u & sign) ? ~u & (bits == 64 ? ~0ull : 0xffffffffull) : u | sign;
+  };
+  switch (type) {
+    case PHIP_TYPE_INT: {
+      int32_t x, y;
+      memcpy(&x, a, 4);
+      memcpy(&y, b, 4);
+      return x < y ? -1 : x > y;
+    }
+    case PHIP_TYPE_LONG: {
+      int64_t x, y;
+      memcpy(&x, a, 8);
+      memcpy(&y, b, 8);
+      return x < y ? -1 : x > y;
+    }
+    case PHIP_TYPE_FLOAT: {
+      uint32_t x, y;
+      memcpy(&x, a, 4);
+      memcpy(&y, b, 4);
+      const uint64_t ox = ord(x, 32), oy = ord(y, 32);
+      return ox < oy ? -1 : ox > oy;
+    }
+    case PHIP_TYPE_DOUBLE: {
+      uint64_t x, y;
+      memcpy(&x, a, 8);
+      memcpy(&y, b, 8);
+      const uint64_t ox = ord(x, 64), oy = ord(y, 64);
+      return ox < oy ? -1 : ox > oy;
+    }
+    default: {
+      const int c = memcmp(a, b, width);
+      return c < 0 ? -1 : c > 0;
+    }
+  }
+}
+
+// Query-global dictionary of one group-by column across the query's segments: the
+// node-global dictionary registered for the column (phip_global_dictionary, multi-GPU servers), else the
+// sorted union of the segments' dictionaries. Per segment a dict-id -> global-id map in HBM (nullptr when
+// the segment's dictionary IS the global one).
 int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
                     const std::string &name, std::shared_ptr<Device::Remap> &out) {
+  auto git = dev.globals.find(name);
+  const Device::GlobalDict *gd = git == dev.globals.end() ? nullptr : &git->second;
   std::string key = name;
+  if (gd) key += "@g" + std::to_string(gd->gen);
   for (auto *s : segs) key += ":" + std::to_string(s->handle);
   auto it = dev.remaps.find(key);
   if (it != dev.remaps.end()) {
@@ -760,95 +817,88 @@ int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::
   }
   auto r = std::make_shared<Device::Remap>();
   const ColumnStore &c0 = segs[0]->cols[colidx[0]];
-  r->type = c0.type;
-  bool identical = true;
-  int width = c0.type == PHIP_TYPE_STRING ? c0.string_width : type_width(c0.type);
+  const int32_t type = c0.type;
+  r->type = type;
+  r->global = gd != nullptr;
+  int width = type == PHIP_TYPE_STRING ? c0.string_width : type_width(type);
   for (size_t i = 0; i < segs.size(); i++) {
     const ColumnStore &c = segs[i]->cols[colidx[i]];
     if (c.fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s", name.c_str());
-    if (c.type != c0.type) return fail(PHIP_ERR_INVALID, "column %s has different types across segments", name.c_str());
-    if (c.host_dict != c0.host_dict) identical = false;
-    if (c.type == PHIP_TYPE_STRING) width = std::max(width, c.string_width);
+    if (c.type != type) return fail(PHIP_ERR_INVALID, "column %s has different types across segments", name.c_str());
+    if (type == PHIP_TYPE_STRING) width = std::max(width, c.string_width);
   }
-  r->width = c0.type == PHIP_TYPE_STRING ? width : 0;
-  auto to_le = [&](const ColumnStore &c, int32_t id, std::vector<uint8_t> &dst) {
-    if (c.type == PHIP_TYPE_STRING) {
-      size_t o = dst.size();
-      dst.resize(o + width, 0);
-      memcpy(dst.data() + o, c.host_dict.data() + (size_t)id * c.string_width, c.string_width);
-    } else {
-      int w = type_width(c.type);
-      const uint8_t *p = c.host_dict.data() + (size_t)id * w;
-      for (int b = w - 1; b >= 0; b--) dst.push_back(p[b]);
+  if (gd && gd->type != type)
+    return fail(PHIP_ERR_INVALID, "global dictionary of column %s has type %d, the segments %d", name.c_str(), gd->type, type);
+  if (gd && type == PHIP_TYPE_STRING) width = std::max(width, gd->width);
+  const int ew = width;  // bytes per value in the comparable LE / padded form
+  r->width = type == PHIP_TYPE_STRING ? width : 0;
+  auto seg_values = [&](const ColumnStore &c) {
+    std::vector<uint8_t> v((size_t)c.card * ew, 0);
+    for (int32_t id = 0; id < c.card; id++) {
+      uint8_t *d = v.data() + (size_t)id * ew;
+      if (type == PHIP_TYPE_STRING) {
+        memcpy(d, c.host_dict.data() + (size_t)id * c.string_width, c.string_width);
+      } else {
+        const uint8_t *p = c.host_dict.data() + (size_t)id * ew;
+        for (int b = 0; b < ew; b++) d[b] = p[ew - 1 - b];  // BE -> LE
+      }
     }
+    return v;
   };
-  r->dev.assign(segs.size(), nullptr);
-  if (identical) {
-    r->card = c0.card;
-    for (int32_t id = 0; id < c0.card; id++) to_le(c0, id, r->values);
+  std::vector<uint8_t> gvals;
+  int64_t n = 0;
+  if (gd) {
+    n = gd->card;
+    const int gw = type == PHIP_TYPE_STRING ? gd->width : ew;
+    gvals.assign((size_t)n * ew, 0);
+    for (int64_t i = 0; i < n; i++) memcpy(gvals.data() + i * ew, gd->values.data() + i * gw, std::min(gw, ew));
   } else {
-    // merge: collect (value bytes in comparable form) and sort
-    // comparable form: strings as padded bytes (memcmp order == Java compareTo for '\0'-padded
-    // ASCII/BMP UTF-8), numbers via typed compare
-    struct V {
-      std::vector<uint8_t> le;
-    };
-    std::vector<std::vector<uint8_t>> all;
+    std::vector<uint8_t> all;
     for (size_t i = 0; i < segs.size(); i++) {
-      const ColumnStore &c = segs[i]->cols[colidx[i]];
-      for (int32_t id = 0; id < c.card; id++) {
-        std::vector<uint8_t> v;
-        to_le(c, id, v);
-        all.push_back(std::move(v));
-      }
+      std::vector<uint8_t> v = seg_values(segs[i]->cols[colidx[i]]);
+      all.insert(all.end(), v.begin(), v.end());
     }
-    auto less = [&](const std::vector<uint8_t> &a, const std::vector<uint8_t> &b) {
-      switch (c0.type) {
-        case PHIP_TYPE_INT: {
-          int32_t x, y;
-          memcpy(&x, a.data(), 4);
-          memcpy(&y, b.data(), 4);
-          return x < y;
-        }
-        case PHIP_TYPE_LONG: {
-          int64_t x, y;
-          memcpy(&x, a.data(), 8);
-          memcpy(&y, b.data(), 8);
-          return x < y;
-        }
-        case PHIP_TYPE_FLOAT: {
-          float x, y;
-          memcpy(&x, a.data(), 4);
-          memcpy(&y, b.data(), 4);
-          return x < y;
-        }
-        case PHIP_TYPE_DOUBLE: {
-          double x, y;
-          memcpy(&x, a.data(), 8);
-          memcpy(&y, b.data(), 8);
-          return x < y;
-        }
-        default: return memcmp(a.data(), b.data(), a.size()) < 0;
-      }
-    };
-    std::sort(all.begin(), all.end(), less);
-    all.erase(std::unique(all.begin(), all.end()), all.end());
-    r->card = (int32_t)all.size();
-    for (auto &v : all) r->values.insert(r->values.end(), v.begin(), v.end());
-    for (size_t i = 0; i < segs.size(); i++) {
-      const ColumnStore &c = segs[i]->cols[colidx[i]];
-      std::vector<int32_t> m(c.card);
-      for (int32_t id = 0; id < c.card; id++) {
-        std::vector<uint8_t> v;
-        to_le(c, id, v);
-        m[id] = (int32_t)(std::lower_bound(all.begin(), all.end(), v, less) - all.begin());
-      }
-      void *p;
-      HIP_TRY(hipMalloc(&p, std::max<size_t>(m.size(), 1) * 4));
-      HIP_TRY(hipMemcpy(p, m.data(), m.size() * 4, hipMemcpyHostToDevice));
-      r->dev[i] = (int32_t *)p;
+    const int64_t total = (int64_t)(all.size() / std::max(ew, 1));
+    std::vector<int64_t> order(total);
+    for (int64_t i = 0; i < total; i++) order[i] = i;
+    const uint8_t *A = all.data();
+    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+      return compare_value(type, A + x * ew, A + y * ew, ew) < 0;
+    });
+    for (int64_t k = 0; k < total; k++) {
+      const uint8_t *v = A + order[k] * ew;
+      if (n > 0 && compare_value(type, gvals.data() + (n - 1) * ew, v, ew) == 0) continue;
+      gvals.insert(gvals.end(), v, v + ew);
+      n++;
     }
   }
+  if (n > INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "column %s: dictionary of %lld values", name.c_str(), (long long)n);
+  r->card = (int32_t)n;
+  r->dev.assign(segs.size(), nullptr);
+  for (size_t i = 0; i < segs.size(); i++) {
+    const ColumnStore &c = segs[i]->cols[colidx[i]];
+    std::vector<uint8_t> v = seg_values(c);
+    if (v == gvals) continue;  // identity map
+    std::vector<int32_t> m(c.card);
+    for (int32_t id = 0; id < c.card; id++) {
+      const uint8_t *x = v.data() + (size_t)id * ew;
+      int64_t lo = 0, hi = n;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (compare_value(type, gvals.data() + mid * ew, x, ew) < 0) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo == n || compare_value(type, gvals.data() + lo * ew, x, ew) != 0)
+        return fail(PHIP_ERR_INVALID, "column %s: a value of segment %s is missing from the global dictionary",
+                    name.c_str(), segs[i]->name.c_str());
+      m[id] = (int32_t)lo;
+    }
+    void *p;
+    HIP_TRY(hipMalloc(&p, std::max<size_t>(m.size(), 1) * 4));
+    r->dev[i] = (int32_t *)p;  // owned by r from here (freed by ~Remap on any later failure)
+    HIP_TRY(hipMemcpy(p, m.data(), m.size() * 4, hipMemcpyHostToDevice));
+  }
+  r->values = std::move(gvals);
   dev.remaps[key] = r;
   out = r;
   return PHIP_OK;
@@ -965,6 +1015,7 @@ struct Plan {
   std::mutex exec_mu;  // executions of one plan serialise (its buffers are reused)
   hipStream_t graph_stream = nullptr;  // the lane stream the graph was captured on
   bool clean = false;  // device seg_matched / HLL registers are zero (finalize_all reset them last time)
+  bool partial_pending = false;  // phip_plan_execute_partial handed the table out; phip_plan_finish is next
 };
 
 static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
@@ -1102,6 +1153,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     dq.dense_batch = max_dict <= (512 << 10) ? 1 : 0;
     const char *db = getenv("PHIP_DENSE_BATCH");  // measurement override: "0" / "1"
     if (db) dq.dense_batch = atoi(db) != 0;
+    dq.dense_min = kDenseMin;
+    const char *dm = getenv("PHIP_DENSE_MIN");  // measurement override
+    if (dm) dq.dense_min = std::max(1, atoi(dm));
     // Stage the fixed-bit words of the gathered dictionary columns of a dense tile in LDS (one region
     // per distinct column, sized for its widest segment), when they fit kAggStageBudget per wave.
     for (int a = 0; a < kMaxAggs; a++) dq.stage_slot_a[a] = dq.stage_slot_b[a] = -1;
@@ -2021,7 +2075,12 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     HIP_TRY(launch_slab_reduce((const uint64_t *)slab, agg_blocks, dq.tbl_words, dq.num_groups, dev_kinds,
                                (uint64_t *)gtab, (const uint32_t *)hslab, nhll ? dq.hll_words : 0, (uint32_t *)ghll, st));
   if (group_by && dq.mode == GB_LDS && total_work == 0) {
+    // nothing to reduce: the table holds every row's identity (a partial table is merged row by row)
     HIP_TRY(hipMemsetAsync(gtab, 0, (size_t)dq.num_groups * 8, st));
+    for (int a = 0; a < naggs; a++)
+      HIP_TRY(launch_fill_u64((uint64_t *)gtab + (int64_t)(1 + a) * dq.num_groups, dq.num_groups,
+                              dq.aggs[a].acc == ACC_MIN_F64 ? ~0ull : 0ull, st));
+    if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
   if (filter_words && need_mask && !dsegs.empty())
     HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
@@ -2163,9 +2222,33 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   return PHIP_OK;
 }
 
-static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_words) {
+// EXEC_FULL: one execution end to end (phip_plan_execute). EXEC_PARTIAL: the kernels up to the dense
+// group table, handed to the caller (phip_plan_execute_partial). EXEC_FINISH: compaction / trim / copy-out
+// of the caller-merged table (phip_plan_finish).
+enum { EXEC_FULL = 0, EXEC_PARTIAL = 1, EXEC_FINISH = 2 };
+static_assert(ACC_COUNT == PHIP_ROW_COUNT && ACC_SUM_I64 == PHIP_ROW_SUM_I64 && ACC_SUM_F64 == PHIP_ROW_SUM_F64 &&
+                  ACC_MIN_F64 == PHIP_ROW_MIN && ACC_MAX_F64 == PHIP_ROW_MAX && ACC_HLL == PHIP_ROW_HLL,
+              "partial row kinds are the accumulator kinds");
+static_assert(kMaxAggs + 1 <= PHIP_PARTIAL_MAX_ROWS, "phip_partial.row_kinds holds every row");
+
+static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_words, int mode = EXEC_FULL,
+                            phip_partial *part = nullptr, const phip_partial *merged = nullptr) {
   Device *dev = P.dev;
   std::lock_guard<std::mutex> xlock(P.exec_mu);
+  if (mode != EXEC_FULL && (!P.group_by || P.dq.mode == GB_HASH))
+    return fail(PHIP_ERR_UNSUPPORTED, "partial tables: dense group-by plans only (this plan: %s)",
+                P.group_by ? "hash-table key space" : "no group-by");
+  if (mode == EXEC_FINISH) {
+    if (!P.partial_pending) return fail(PHIP_ERR_INVALID, "phip_plan_finish without a pending phip_plan_execute_partial");
+    if (merged->num_groups != P.dq.num_groups || merged->num_rows != 1 + P.naggs || merged->table != (uint64_t *)P.gtab)
+      return fail(PHIP_ERR_INVALID, "phip_plan_finish: partial does not belong to this plan");
+    for (int a = 0; a < P.naggs; a++) {
+      const int k = merged->row_kinds[1 + a], own = P.dq.aggs[a].acc;
+      if (k != own && !(own == ACC_SUM_I64 && k == ACC_SUM_F64))
+        return fail(PHIP_ERR_INVALID, "phip_plan_finish: row %d kind %d (plan: %d)", 1 + a, k, own);
+    }
+  }
+  if (mode == EXEC_PARTIAL) P.partial_pending = false;
   HIP_TRY(hipSetDevice(dev->ordinal));
   LaneGuard lg{dev};
   {
@@ -2196,13 +2279,15 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   }
   if (P.graph_exec) {
     HIP_TRY(hipGraphLaunch(P.graph_exec, st));
-  } else {
+  } else if (mode != EXEC_FINISH) {
     int32_t rc = enqueue_plan(P, st);
     if (rc) return rc;
   }
-  P.executions++;
-  if (P.total_work == 0) {  // no kernel ran: nothing matched, no registers set
-    memset(P.pinned + 64, 0, (size_t)P.nseg * 8 + (P.nhll && !P.group_by ? ((size_t)P.nhll << P.log2m) * 4 : 0));
+  if (mode != EXEC_FINISH) {
+    P.executions++;
+    if (P.total_work == 0) {  // no kernel ran: nothing matched, no registers set
+      memset(P.pinned + 64, 0, (size_t)P.nseg * 8 + (P.nhll && !P.group_by ? ((size_t)P.nhll << P.log2m) * 4 : 0));
+    }
   }
   DevAggQuery &dq = P.dq;
   const int nseg = P.nseg, naggs = P.naggs, nhll = P.nhll, log2m = P.log2m, m_regs = P.m_regs;
@@ -2225,6 +2310,36 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   const uint64_t *segm = P.pinned + 64;
   const uint32_t *hll_host = (const uint32_t *)(P.pinned + 64 + nseg);
 
+  // this GPU's statistics (valid once the stream has synchronised)
+  auto local_stats = [&](int64_t st6[6]) {
+    const int64_t m = has_filter ? (int64_t)fin[32] : docs_in_work;
+    st6[0] = m;
+    st6[1] = has_filter ? (int64_t)fin[33] : 0;
+    st6[2] = m * num_projected;
+    st6[3] = total_docs;
+    st6[4] = nseg;
+    st6[5] = 0;
+    if (has_filter) {
+      for (int s = 0; s < nseg; s++) st6[5] += segm[s] ? 1 : 0;
+    } else {
+      for (const DevSeg &ds : dsegs) st6[5] += ds.num_docs > 0 ? 1 : 0;
+    }
+  };
+  // row kinds of the gather: the plan's, or the caller's after a merge that turned int64 sums into doubles
+  const int32_t *gather_kinds = dev_kinds;
+  std::vector<int32_t> kinds_host(std::max(naggs, 1));
+  for (int a = 0; a < naggs; a++) kinds_host[a] = mode == EXEC_FINISH ? merged->row_kinds[1 + a] : dq.aggs[a].acc;
+  if (mode == EXEC_FINISH) {
+    bool differs = false;
+    for (int a = 0; a < naggs; a++) differs |= kinds_host[a] != dq.aggs[a].acc;
+    if (differs) {
+      void *kb;
+      if ((rc = ws.get("finish_kinds", (size_t)naggs * 4, &kb))) return rc;
+      HIP_TRY(hipMemcpyAsync(kb, kinds_host.data(), (size_t)naggs * 4, hipMemcpyHostToDevice, st));
+      gather_kinds = (const int32_t *)kb;
+    }
+  }
+
   int64_t ngroups = 1;
   if (group_by) {
     const int64_t nchunks = ceil_div(dq.num_groups, 1024);
@@ -2238,6 +2353,28 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     HIP_TRY(hipMemcpyAsync(&total, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     ngroups = total;
+    if (mode == EXEC_PARTIAL) {
+      // per-segment numGroupsLimit needs the first-seen record pass of phip_plan_execute
+      if (P.num_groups_limit > 0 && ngroups >= P.num_groups_limit)
+        return fail(PHIP_ERR_UNSUPPORTED, "partial table: %lld groups reach numGroupsLimit %lld", (long long)ngroups,
+                    (long long)P.num_groups_limit);
+      memset(part, 0, sizeof(*part));
+      part->num_groups = dq.num_groups;
+      part->num_rows = 1 + naggs;
+      part->num_hll = nhll;
+      part->log2m = nhll ? log2m : 0;
+      part->device = dev->ordinal;
+      part->table = (uint64_t *)gtab;
+      part->hll = nhll ? (uint32_t *)ghll : nullptr;
+      part->row_kinds[0] = PHIP_ROW_COUNT;
+      for (int a = 0; a < naggs; a++) part->row_kinds[1 + a] = dq.aggs[a].acc;  // ACC_* == PHIP_ROW_*
+      local_stats(part->stats);
+      part->global_keys = 1;
+      for (const auto &d : gb_dicts) part->global_keys &= d->global ? 1 : 0;
+      P.partial_pending = true;
+      P.clean = true;
+      return PHIP_OK;
+    }
     rc = ws.get("gb_keys", (size_t)std::max<int64_t>(ngroups, 1) * 8, &keys);
     if (rc) return rc;
     void *ov, *ol, *oh = nullptr;
@@ -2250,14 +2387,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       if (rc) return rc;
     }
     HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
-    HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, dev_kinds, (const uint64_t *)gtab,
+    HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, gather_kinds, (const uint64_t *)gtab,
                                 (const uint32_t *)ghll, nhll, log2m, (double *)ov, (int64_t *)ol, (uint8_t *)oh, st));
     uint32_t overflow = 0;
     if (dq.mode == GB_HASH) {
       HIP_TRY(launch_hash_keys((int64_t *)keys, ngroups, dq.gb_keys, st));
       HIP_TRY(hipMemcpyAsync(&overflow, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
     }
-    if (P.num_groups_limit > 0 && ngroups >= P.num_groups_limit) {
+    if (mode == EXEC_FULL && P.num_groups_limit > 0 && ngroups >= P.num_groups_limit) {
       // some segment may have reached numGroupsLimit: the first-seen pass decides which keys it kept
       HIP_TRY(hipStreamSynchronize(st));
       if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
@@ -2385,15 +2522,16 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     r.agg_bytes = 0;
   }
 
-  r.num_docs_scanned = matched;
-  r.num_entries_scanned_in_filter = has_filter ? (int64_t)fin[33] : 0;
-  r.num_entries_scanned_post_filter = r.num_docs_scanned * num_projected;
-  r.num_total_docs = total_docs;
-  r.num_segments_processed = nseg;
-  if (has_filter) {
-    for (int s = 0; s < nseg; s++) r.num_segments_matched += segm[s] ? 1 : 0;
-  } else {
-    for (const DevSeg &ds : dsegs) r.num_segments_matched += ds.num_docs > 0 ? 1 : 0;
+  {
+    int64_t st6[6];
+    if (mode == EXEC_FINISH) memcpy(st6, merged->stats, sizeof(st6));
+    else local_stats(st6);
+    r.num_docs_scanned = st6[0];
+    r.num_entries_scanned_in_filter = st6[1];
+    r.num_entries_scanned_post_filter = st6[2];
+    r.num_total_docs = st6[3];
+    r.num_segments_processed = (int32_t)st6[4];
+    r.num_segments_matched = (int32_t)st6[5];
   }
   r.num_aggregations = naggs;
   r.num_groups = group_by ? ngroups : 1;
@@ -2404,11 +2542,12 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   r.hll_registers = impl->hll.data();
   r.group_keys = impl->keys.data();
   impl->exact.resize(std::max(naggs, 1), 0);
-  for (int a = 0; a < naggs; a++) impl->exact[a] = (dq.aggs[a].acc == ACC_COUNT || dq.aggs[a].acc == ACC_SUM_I64) ? 1 : 0;
+  for (int a = 0; a < naggs; a++) impl->exact[a] = (kinds_host[a] == ACC_COUNT || kinds_host[a] == ACC_SUM_I64) ? 1 : 0;
   r.long_exact = impl->exact.data();
   r.scan_kernel_ms = t_scan;
   r.device_ms = t_all;
   P.clean = true;
+  P.partial_pending = false;
   if (out_result) {
     *out_result = &impl.release()->pub;
   }
@@ -2578,6 +2717,71 @@ PHIP_API int32_t phip_plan_execute(uint64_t plan, phip_result **out_result) {
     p = it->second.get();
   }
   return execute_plan(*p, out_result, nullptr);
+}
+
+static int32_t find_plan(uint64_t plan, Plan **out) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_plans.find(plan);
+  if (it == g_plans.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown plan handle %llu", (unsigned long long)plan);
+  *out = it->second.get();
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_plan_execute_partial(uint64_t plan, phip_partial *out_partial) {
+  if (!out_partial) return fail(PHIP_ERR_INVALID, "null partial pointer");
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  return execute_plan(*p, nullptr, nullptr, EXEC_PARTIAL, out_partial, nullptr);
+}
+
+PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phip_result **out_result) {
+  if (!merged || !out_result) return fail(PHIP_ERR_INVALID, "null argument");
+  *out_result = nullptr;
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  return execute_plan(*p, out_result, nullptr, EXEC_FINISH, nullptr, merged);
+}
+
+PHIP_API int32_t phip_global_dictionary(int32_t device, const char *column, int32_t data_type, int32_t cardinality,
+                                        int32_t string_width, const void *values) {
+  if (!column || cardinality < -1 || (cardinality > 0 && !values))
+    return fail(PHIP_ERR_INVALID, "global dictionary: bad arguments");
+  if (cardinality == -1) {  // remove the registration
+    std::lock_guard<std::mutex> g(g_mu);
+    for (auto &d : g_devices) {
+      if (device >= 0 && d->ordinal != device) continue;
+      std::lock_guard<std::mutex> dl(d->mu);
+      d->globals.erase(column);
+    }
+    return PHIP_OK;
+  }
+  if (data_type < PHIP_TYPE_INT || data_type > PHIP_TYPE_STRING)
+    return fail(PHIP_ERR_INVALID, "global dictionary: bad data type %d", data_type);
+  if (data_type == PHIP_TYPE_STRING && string_width <= 0)
+    return fail(PHIP_ERR_INVALID, "global dictionary: string width must be > 0");
+  const int w = data_type == PHIP_TYPE_STRING ? string_width : type_width(data_type);
+  const uint8_t *v = (const uint8_t *)values;
+  for (int32_t i = 1; i < cardinality; i++)
+    if (compare_value(data_type, v + (size_t)(i - 1) * w, v + (size_t)i * w, w) >= 0)
+      return fail(PHIP_ERR_INVALID, "global dictionary of %s: values not ascending / distinct at %d", column, i);
+  Device *dev;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    int32_t rc = ensure_devices_locked();
+    if (rc) return rc;
+    dev = device >= 0 ? find_device(device) : g_devices[0].get();
+    if (!dev) return fail(PHIP_ERR_NO_DEVICE, "device %d not initialised (call phip_init)", device);
+  }
+  std::lock_guard<std::mutex> dl(dev->mu);
+  Device::GlobalDict &gd = dev->globals[column];
+  gd.type = data_type;
+  gd.card = cardinality;
+  gd.width = data_type == PHIP_TYPE_STRING ? string_width : 0;
+  gd.gen = ++dev->global_gen;
+  gd.values.assign(v, v + (size_t)cardinality * w);
+  return PHIP_OK;
 }
 
 PHIP_API int32_t phip_plan_destroy(uint64_t plan) {

@@ -409,7 +409,7 @@ class GpuCombineOperator:
                                                   len(out)))
         return out[:nwords]
 
-    def run_raw(self):
+    def run_raw(self, prepare_only=False):
         """One execution of the prepared plan (phip_plan_create once per operator, then phip_plan_execute:
         InstancePlanMakerImplV2's Plan run by GlobalPlanImplV0.execute)."""
         lib = _lib.load()
@@ -420,6 +420,8 @@ class GpuCombineOperator:
             _lib.check(lib.phip_plan_create(ctypes.byref(q), ctypes.byref(h)))
             self._plan = h.value
             self._lib = lib
+        if prepare_only:
+            return None
         res = ctypes.POINTER(_lib.Result)()
         _lib.check(lib.phip_plan_execute(self._plan, ctypes.byref(res)))
         return res
@@ -484,8 +486,33 @@ class GpuCombineOperator:
     def next_block(self):
         if self._non_scan_fit():
             return self._non_scan_block()
+        return self._block_from_result(self.run_raw())
+
+    # -- multi-GPU servers (include/pinot_hip.h "multi-GPU servers"; engine/distributed.py) -------------
+    def execute_partial(self):
+        """Runs the plan up to this GPU's dense partial group table (phip_plan_execute_partial). Returns the
+        _lib.Partial (device pointers), or None when the plan cannot hand one out (hash-table key space,
+        numGroupsLimit reached on this GPU) -- the caller then merges records instead."""
+        if not self.query.group_by:
+            return None
         lib = _lib.load()
-        res = self.run_raw()
+        self.run_raw(prepare_only=True)
+        part = _lib.Partial()
+        rc = lib.phip_plan_execute_partial(self._plan, ctypes.byref(part))
+        if rc == _lib.PHIP_ERR_UNSUPPORTED:
+            return None
+        _lib.check(rc)
+        return part
+
+    def finish(self, merged):
+        """Result block of the (merged) partial table: compaction, server-level trim, statistics of `merged`."""
+        lib = _lib.load()
+        res = ctypes.POINTER(_lib.Result)()
+        _lib.check(lib.phip_plan_finish(self._plan, ctypes.byref(merged), ctypes.byref(res)))
+        return self._block_from_result(res)
+
+    def _block_from_result(self, res):
+        lib = _lib.load()
         try:
             r = res.contents
             stats = ExecutionStatistics(r.num_docs_scanned, r.num_entries_scanned_in_filter,

@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PAIRS = [("phip_column_desc", _lib.ColumnDesc), ("phip_segment_desc", _lib.SegmentDesc),
          ("phip_raw_range", _lib.RawRange), ("phip_filter_node", _lib.FilterNode),
          ("phip_aggregation", _lib.Aggregation), ("phip_query_desc", _lib.QueryDesc),
-         ("phip_result", _lib.Result), ("phip_dictionary_view", _lib.DictionaryView)]
+         ("phip_result", _lib.Result), ("phip_dictionary_view", _lib.DictionaryView),
+         ("phip_partial", _lib.Partial)]
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
@@ -39,3 +40,22 @@ def test_ctypes_layout_matches_header(tmp_path):
         assert got[(cname, "size")] == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def _declared_symbols():
+    import re
+    with open(os.path.join(ROOT, "include", "pinot_hip.h")) as f:
+        text = f.read()
+    return set(re.findall(r"PHIP_API\s+[\w\s\*]+?\b(phip_\w+)\s*\(", text))
+
+
+def test_library_exports_every_declared_symbol():
+    """The built libpinot_hip.so loads on a GPU-less host and exports every entry point the header declares
+    (dlsym only -- no compute call without a GPU); the ctypes mirror binds exactly that set."""
+    declared = _declared_symbols()
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libpinot_hip.so not built (python -c 'import __graft_entry__ as g; g.build()')")
+    so = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in sorted(declared) if not hasattr(so, s)]
+    assert not missing, missing

@@ -120,3 +120,140 @@ def test_allreduce_block_single_process_is_identity():
     qc = parse(QUERIES[0])
     blk, _ = executor.execute(qc, _segments()[:1])
     assert allreduce_block(blk) is blk
+
+
+# ---- device-resident merge: node-global dictionaries + dense partial tables (engine/distributed.py) --------
+# CPU restatement of the library's partial-table encoding (pinot_amd/csrc/dev_common.h f64_ordered; row layout
+# of include/pinot_hip.h phip_partial), used to feed the product's all-reduce with oracle partials.
+def _ordered(d):
+    u = int(np.array([d], "<f8").view(np.uint64)[0])
+    return (~u & (2 ** 64 - 1)) if u >> 63 else u | (1 << 63)
+
+
+def _unordered(u):
+    u &= 2 ** 64 - 1
+    v = (u & ((1 << 63) - 1)) if u >> 63 else (~u & (2 ** 64 - 1))
+    return float(np.array([v], np.uint64).view("<f8")[0])
+
+
+def _s64(u):
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+PARTIAL_Q = ("SELECT g, h, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTHLL(h) FROM t WHERE m > -500000000 "
+             "GROUP BY g, h ORDER BY g, h LIMIT 100000")
+
+
+def _partial_worker(rank, world, port, f64_rank, errs):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import executor
+        from pinot_amd import _lib
+        from pinot_amd.engine.distributed import allreduce_partial_table, global_dictionary
+        from pinot_amd.query.sql import parse
+        segs = _segments()
+        mine = [s for i, s in enumerate(segs) if i % world == rank]
+        qc = parse(PARTIAL_Q)
+        gd = {}
+        for col in ("g", "h"):
+            dt, vals = global_dictionary(mine, col, dist)
+            whole_vals = sorted({v.item() if hasattr(v, "item") else v
+                                 for s in segs for v in executor.OracleSegment(s).dictionary(col)})
+            if col == "g":
+                got = [bytes(r).rstrip(b"\0").decode() for r in vals]
+            else:
+                got = [int(x) for x in vals]
+            assert got == whole_vals, (col, got[:5], whole_vals[:5])
+            gd[col] = got
+        cg, ch = len(gd["g"]), len(gd["h"])
+        G = cg * ch
+        ig = {v: i for i, v in enumerate(gd["g"])}
+        ih = {v: i for i, v in enumerate(gd["h"])}
+        part, _ = executor.execute(qc, mine)
+        m = 1 << qc.aggregations[5].log2m
+        kinds = [_lib.ROW_COUNT, _lib.ROW_COUNT, _lib.ROW_SUM_I64, _lib.ROW_SUM_F64, _lib.ROW_MIN, _lib.ROW_MAX,
+                 _lib.ROW_HLL]
+        if rank == f64_rank:
+            kinds[2] = _lib.ROW_SUM_F64  # this GPU's overflow bound chose double for SUM(m)
+        table = np.zeros((7, G), np.int64)
+        table[4, :] = _s64(2 ** 64 - 1)  # MIN identity (atomicMin from the top)
+        hll = np.zeros((G, m), np.int32)
+        for (g, h), v in part.groups.items():
+            k = ig[g] + cg * ih[h]  # mixed radix, column 0 least significant
+            table[0, k] = v[0]
+            if kinds[2] == _lib.ROW_SUM_F64:
+                table[2, k] = np.array([float(v[1])], "<f8").view(np.int64)[0]
+            else:
+                table[2, k] = v[1]
+            table[3, k] = np.array([v[2]], "<f8").view(np.int64)[0]
+            table[4, k] = _s64(_ordered(v[3]))
+            table[5, k] = _s64(_ordered(float(v[4])))
+            hll[k] = np.asarray(v[5], np.int32)
+        s = part.stats
+        stats = [s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
+                 s.num_total_docs, s.num_segments_processed, s.num_segments_matched]
+        t, th = torch.from_numpy(table), torch.from_numpy(hll.reshape(-1))
+        kinds2, stats2 = allreduce_partial_table(t, th, kinds, stats, dist)
+        whole, _ = executor.execute(qc, segs)
+        assert stats2[0] == whole.stats.num_docs_scanned and stats2[3] == whole.stats.num_total_docs
+        want_f64 = f64_rank is not None
+        assert kinds2[2] == (_lib.ROW_SUM_F64 if want_f64 else _lib.ROW_SUM_I64), kinds2
+        table, hll = t.numpy(), th.numpy().reshape(G, m)
+        present = {int(k) for k in np.nonzero(table[0])[0]}
+        assert len(present) == len(whole.groups)
+        for (g, h), v in whole.groups.items():
+            k = ig[g] + cg * ih[h]
+            assert k in present
+            assert table[0, k] == v[0]
+            s_m = float(table[2:3, k].view("<f8")[0]) if want_f64 else int(table[2, k])
+            assert _close(s_m, v[1] if not want_f64 else float(v[1])), (s_m, v[1])
+            assert _close(float(table[3:4, k].view("<f8")[0]), v[2])
+            assert _unordered(int(table[4, k])) == v[3]
+            assert _unordered(int(table[5, k])) == float(v[4])
+            assert np.array_equal(hll[k].astype(np.uint8), np.asarray(v[5]))
+    except Exception as e:  # surfaced to the parent
+        import traceback
+        errs.put(f"rank {rank}: {type(e).__name__}: {e}\n{traceback.format_exc()}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("f64_rank", [None, 1], ids=["int64", "mixed-sum-kinds"])
+def test_allreduce_partial_table_world2_gloo(f64_rank):
+    """The product's device-table merge (allreduce_partial_table) over the library's row encodings: counts,
+    exact and double sums, MIN / MAX on the order-preserving u64 image, HLL registers, statistics, and the
+    per-GPU int64/double disagreement of a SUM row; keys in node-global dictionaries (global_dictionary)."""
+    ctx = mp.get_context("spawn")
+    errs = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_partial_worker, args=(r, 2, port, f64_rank, errs)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not errs.empty():
+        msgs.append(errs.get())
+    assert not msgs, msgs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_float_order_keys_round_trip():
+    """Node-global FLOAT / DOUBLE dictionaries sort in Double.compare order (-0.0 < 0.0, NaN last)."""
+    from pinot_amd.engine.distributed import _order_keys, _values_of_keys
+    from pinot_amd.spi import DataType
+    for dt, code in ((DataType.DOUBLE, "<f8"), (DataType.FLOAT, "<f4")):
+        v = np.array([3.5, -0.0, 0.0, -2.25, np.inf, -np.inf, np.nan, 1e-30], code)
+        k = _order_keys(v, dt)
+        order = np.argsort(k, kind="stable")
+        got = _values_of_keys(k[order], dt)
+        want = np.array([-np.inf, -2.25, -0.0, 0.0, 1e-30, 3.5, np.inf, np.nan], code)
+        assert np.array_equal(got.view(np.uint64 if code == "<f8" else np.uint32),
+                              want.view(np.uint64 if code == "<f8" else np.uint32))
