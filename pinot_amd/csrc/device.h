@@ -154,6 +154,8 @@ struct DevFilter {
   int32_t nbuf;          // ring slots per wave (2..kMaxRing): nbuf-1 tiles in flight while one is evaluated
   int32_t xcd_walk;      // 1: XCD-sweep tile order (grid multiple of 8); 0: contiguous range per wave
   int32_t min_dma;       // min over segments of LDS-DMA wave-instructions per tile (vmcnt lower bound)
+  int32_t probe;         // measurement only (PHIP_FILTER_PROBE): 1 = stream the tiles, skip the evaluation
+  int32_t pad_probe;
   uint32_t *mask_out;    // optional: [total_work][64] lane-major tile masks
   uint64_t *partials;    // [num_blocks][2]: matched docs, entries scanned in filter
   uint64_t *seg_matched; // [num query segments]

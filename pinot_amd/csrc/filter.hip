@@ -829,7 +829,9 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     const uint32_t valid = valid_word(tl.valid_docs, lane);
     uint32_t scanned_t = 0;
     uint32_t mask;
-    if (kConjOnly || seg.conj_path) {
+    if (q.probe) {
+      mask = valid;
+    } else if (kConjOnly || seg.conj_path) {
       mask = seg.conj > 0 ? eval_conj(seg, tl.stage, valid) : valid;
       if (seg.conj_range && (seg.conj_lo > tl.doc0 || seg.conj_hi < tl.doc0 + kTileDocs - 1)) {
         const int32_t lo = max(seg.conj_lo - tl.doc0, 0), hi = min(seg.conj_hi - tl.doc0, kTileDocs - 1);

@@ -1859,6 +1859,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   fq.stage_stride = stage_stride;
   fq.nbuf = nbuf;
   fq.xcd_walk = xcd_walk ? 1 : 0;
+  {
+    const char *pe = getenv("PHIP_FILTER_PROBE");
+    fq.probe = pe ? atoi(pe) : 0;
+  }
   fq.min_dma = 0;
   for (size_t i = 0; i < dsegs.size(); i++)
     fq.min_dma = i == 0 ? dsegs[i].num_dma : std::min(fq.min_dma, dsegs[i].num_dma);
