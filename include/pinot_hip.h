@@ -175,7 +175,26 @@ typedef struct phip_query_desc {
   int32_t num_order_by_keys;
   int32_t reserved0;
   const int32_t *order_by_keys;
+  /* Any other ORDER BY (TableResizer, pinot-core/.../data/table/TableResizer.java:90-125,410-450): a list of
+   * terms, each a group-by column or an aggregation's final result, mixed freely (takes precedence over both
+   * fields above when > 0). The device sorts the groups by the whole list (stable; ties keep the lowest group key)
+   * and keeps trim_size of them. */
+  int32_t num_order_terms;
+  int32_t reserved1;
+  const struct phip_order_term *order_terms;
 } phip_query_desc;
+
+#define PHIP_ORDER_GROUP_KEY 0 /* group-by column `a` (GroupByExpressionExtractor) */
+#define PHIP_ORDER_VALUE 1     /* aggregations[a] as double: SUM / MIN / MAX / COUNT (AggregationFunctionExtractor) */
+#define PHIP_ORDER_AVG 2       /* aggregations[a] (SUM) / aggregations[b] (COUNT); -inf when the count is 0 */
+#define PHIP_ORDER_RANGE 3     /* aggregations[b] (MAX) - aggregations[a] (MIN): MINMAXRANGE */
+
+typedef struct phip_order_term {
+  int32_t kind; /* PHIP_ORDER_* */
+  int32_t a;
+  int32_t b;
+  int32_t desc; /* 1 = DESC */
+} phip_order_term;
 
 /* ---- results ------------------------------------------------------------------------------
  * Library-owned, valid until phip_result_free. For an aggregation-only query num_groups = 1.

@@ -200,6 +200,8 @@ def _expr_values(os_, e, docs):
         if e.name == "cast":
             v = _expr_values(os_, e.args[0], docs)
             return v.astype(np.float64) if str(e.args[1].value).upper() in ("DOUBLE", "FLOAT") else v
+        if e.name == "case":
+            return _case_values(os_, e, docs, lambda x: _expr_values(os_, x, docs).astype(np.float64), np.float64)
         a = _expr_values(os_, e.args[0], docs).astype(np.float64)
         b = _expr_values(os_, e.args[1], docs).astype(np.float64)
         if e.name == "times":
@@ -213,9 +215,24 @@ def _expr_values(os_, e, docs):
     raise NotImplementedError(str(e))
 
 
+def _case_values(os_, e, docs, branch, dtype):
+    """CaseTransformFunction: per doc, the THEN of the first WHEN that holds, else the ELSE
+    (args = when1, then1, ..., else; conditions evaluated on values like any filter)."""
+    out = np.array(branch(e.args[-1]), dtype=dtype)
+    decided = np.zeros(len(docs), dtype=bool)
+    for k in range(0, len(e.args) - 1, 2):
+        cond = eval_filter(os_, e.args[k])[docs] & ~decided
+        v = np.asarray(branch(e.args[k + 1]), dtype=dtype)
+        out[cond] = v[cond]
+        decided |= cond
+    return out
+
+
 def _exact_values(os_, e, docs):
     """Exact integer value of an INT/LONG-only expression, or None."""
-    from pinot_amd.query.context import Function, Identifier
+    from pinot_amd.query.context import Function, Identifier, Literal
+    if isinstance(e, Literal):
+        return np.full(len(docs), e.value, dtype=np.int64) if isinstance(e.value, int) else None
     if isinstance(e, Identifier):
         if int(os_.meta(e.name).data_type) in (0, 1):
             return os_.values(e.name)[docs].astype(object if False else np.int64)
@@ -223,6 +240,13 @@ def _exact_values(os_, e, docs):
     if isinstance(e, Function):
         if e.name == "cast":
             return _exact_values(os_, e.args[0], docs)
+        if e.name == "case":
+            branches = [_exact_values(os_, x, docs) for x in e.args[1::2] + e.args[-1:]]
+            if any(b is None for b in branches):
+                return None
+            dt = object if any(b.dtype == object for b in branches) else np.int64
+            vals = {id(x): b for x, b in zip(e.args[1::2] + e.args[-1:], branches)}
+            return _case_values(os_, e, docs, lambda x: vals[id(x)], dt)
         if e.name in ("times", "minus", "plus") and len(e.args) == 2:
             a, b = _exact_values(os_, e.args[0], docs), _exact_values(os_, e.args[1], docs)
             if a is None or b is None:
@@ -326,40 +350,7 @@ def _group_segment(os_, query, docs, num_groups_limit):
         keys.append(tuple(k))
     per_agg, per_exact = [], []
     for ag in query.aggregations:
-        f = ag.function
-        ex = None
-        if f == "count":
-            v = np.bincount(gid, minlength=ng).tolist()
-        elif f in ("distinctcounthll", "distinctcountrawhll"):
-            v = _hll_group_registers(os_, ag.argument.name, docs, gid, ng, ag.log2m)
-        else:
-            vals = _expr_values(os_, ag.argument, docs).astype(np.float64)
-            if f in ("sum", "avg"):
-                acc = np.zeros(ng)
-                np.add.at(acc, gid, vals)               # sequential, doc order within a group
-                sums = acc.tolist()
-                if f == "sum":
-                    e = _exact_values(os_, ag.argument, docs)
-                    if e is not None:
-                        if e.dtype != object and _maxabs(e) * len(e) < 2 ** 62:
-                            ea = np.zeros(ng, dtype=np.int64)
-                            np.add.at(ea, gid, e)
-                            ex = [int(x) for x in ea.tolist()]
-                        else:
-                            ex = [0] * ng
-                            for g_, x in zip(gid.tolist(), e.tolist()):
-                                ex[g_] += int(x)
-                    v = sums
-                else:
-                    v = list(zip(sums, np.bincount(gid, minlength=ng).tolist()))
-            elif f in ("min", "max", "minmaxrange"):
-                mn = np.full(ng, np.inf)
-                mx = np.full(ng, -np.inf)
-                np.minimum.at(mn, gid, vals)
-                np.maximum.at(mx, gid, vals)
-                v = mn.tolist() if f == "min" else (mx.tolist() if f == "max" else list(zip(mn.tolist(), mx.tolist())))
-            else:
-                raise NotImplementedError(f)
+        v, ex = _group_aggregate(os_, ag, docs, gid, ng)
         per_agg.append(v)
         per_exact.append(ex)
     groups, exact = {}, {}
@@ -367,6 +358,48 @@ def _group_segment(os_, query, docs, num_groups_limit):
         groups[k] = [per_agg[a][g] for a in range(len(query.aggregations))]
         exact[k] = [per_exact[a][g] if per_exact[a] is not None else None for a in range(len(query.aggregations))]
     return groups, exact, reached
+
+
+def _group_aggregate(os_, ag, docs, gid, ng):
+    """One aggregation of one segment's group-by: per-doc holder updates in doc order
+    (DoubleGroupByResultHolder.java:94-98, SumAggregationFunction.aggregateGroupBySV :160-180) into ``ng``
+    groups; docs carry their group id in ``gid``. Groups no doc reached keep the holder defaults
+    (0 / 0.0 / +inf / -inf / empty registers). Returns (per-group intermediates, per-group exact sums or None)."""
+    f = ag.function
+    ex = None
+    if f == "count":
+        v = np.bincount(gid, minlength=ng).tolist()
+    elif f in ("distinctcounthll", "distinctcountrawhll"):
+        v = _hll_group_registers(os_, ag.argument.name, docs, gid, ng, ag.log2m)
+    else:
+        vals = _expr_values(os_, ag.argument, docs).astype(np.float64)
+        if f in ("sum", "avg"):
+            acc = np.zeros(ng)
+            np.add.at(acc, gid, vals)               # sequential, doc order within a group
+            sums = acc.tolist()
+            if f == "sum":
+                e = _exact_values(os_, ag.argument, docs)
+                if e is not None:
+                    if e.dtype != object and _maxabs(e) * len(e) < 2 ** 62:
+                        ea = np.zeros(ng, dtype=np.int64)
+                        np.add.at(ea, gid, e)
+                        ex = [int(x) for x in ea.tolist()]
+                    else:
+                        ex = [0] * ng
+                        for g_, x in zip(gid.tolist(), e.tolist()):
+                            ex[g_] += int(x)
+                v = sums
+            else:
+                v = list(zip(sums, np.bincount(gid, minlength=ng).tolist()))
+        elif f in ("min", "max", "minmaxrange"):
+            mn = np.full(ng, np.inf)
+            mx = np.full(ng, -np.inf)
+            np.minimum.at(mn, gid, vals)
+            np.maximum.at(mx, gid, vals)
+            v = mn.tolist() if f == "min" else (mx.tolist() if f == "max" else list(zip(mn.tolist(), mx.tolist())))
+        else:
+            raise NotImplementedError(f)
+    return v, ex
 
 
 def _hll_group_registers(os_, col, docs, gid, ng, log2m):
@@ -431,7 +464,9 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
         stats.num_segments_processed += 1
         stats.num_segments_matched += int(len(docs) > 0)
         per_seg.append((os_, docs))
-    if not query.group_by and any(ag.filter is not None for ag in query.aggregations):
+    if any(ag.filter is not None for ag in query.aggregations):
+        if query.group_by:
+            return _execute_filtered_group_by(query, segments, num_groups_limit)
         return _execute_filtered(query, segments)
     if not query.group_by:
         results, exact = None, None
@@ -505,6 +540,107 @@ def _execute_filtered(query, segments):
         stats.num_segments_processed += 1
         stats.num_segments_matched += int(scanned > 0)
     return AggregationResultsBlock(query.aggregations, results, stats), exact
+
+
+def _filter_infos(query):
+    """AggregationFunctionUtils.buildFilteredAggregationInfos (:312-400): one info per distinct FILTER
+    (first-appearance order here; the reference's is HashMap order, which only matters for numGroupsLimit), then
+    the main-filter info with the non-filtered functions -- added for a group-by even when it has none, so the
+    groups of the main filter are all generated, unless ``filteredAggregationsSkipEmptyGroups``."""
+    infos = {}
+    main = []
+    for i, ag in enumerate(query.aggregations):
+        if ag.filter is None:
+            main.append(i)
+        else:
+            infos.setdefault(ag.filter, []).append(i)
+    out = list(infos.items())
+    skip = str(query.options.get("filteredAggregationsSkipEmptyGroups", "false")).lower() == "true"
+    if main or (query.group_by and not skip):
+        out.append((None, main))
+    return out
+
+
+def _execute_filtered_group_by(query, segments, num_groups_limit):
+    """FilteredGroupByOperator.getNextBlock (pinot-core/.../operator/query/FilteredGroupByOperator.java:110-176):
+    the infos share ONE group key generator, so a group's id is first-seen over info 0's docs, then info 1's, ...
+    (numGroupsLimit counts the union); holders of functions whose filter never reached a group keep their
+    defaults (ensureCapacity); numDocsScanned / post-filter entries are summed over the infos, each info
+    projecting the group-by columns plus its functions' arguments."""
+    from pinot_amd.engine.results import ExecutionStatistics, GroupByResultsBlock, merge_intermediate
+    from pinot_amd.query.context import columns_of
+    infos = _filter_infos(query)
+    stats = ExecutionStatistics()
+    groups, exact_groups = {}, {}
+    limit_reached = False
+    na = len(query.aggregations)
+    gb_cols = set()
+    for e in query.group_by:
+        gb_cols.update(columns_of(e))
+    for seg in segments:
+        os_ = OracleSegment(seg)
+        base = eval_filter(os_, query.filter)
+        parts = []
+        scanned = 0
+        for flt, idxs in infos:
+            mask = base if flt is None else (base & eval_filter(os_, flt))
+            docs = np.nonzero(mask)[0]
+            proj = set(gb_cols)
+            for i in idxs:
+                if query.aggregations[i].argument is not None:
+                    proj.update(columns_of(query.aggregations[i].argument))
+            scanned += len(docs)
+            stats.num_entries_scanned_post_filter += len(docs) * len(proj)
+            parts.append((docs, idxs))
+        stats.num_docs_scanned += scanned
+        stats.num_total_docs += seg.num_docs
+        stats.num_segments_processed += 1
+        stats.num_segments_matched += int(scanned > 0)
+        if scanned == 0:
+            continue
+        alldocs = np.concatenate([d for d, _ in parts])
+        codes = np.zeros(len(alldocs), dtype=np.int64)
+        uniq_vals = []
+        stride = 1
+        for e in query.group_by:
+            u, inv = np.unique(os_.values(e.name)[alldocs], return_inverse=True)
+            uniq_vals.append(u)
+            codes += inv.astype(np.int64) * stride
+            stride *= max(len(u), 1)
+        ukeys, first, inv = np.unique(codes, return_index=True, return_inverse=True)
+        order = np.argsort(first, kind="stable")       # first seen over info 0, info 1, ...
+        rank = np.empty(len(order), dtype=np.int64)
+        rank[order] = np.arange(len(order))
+        limit_reached |= num_groups_limit is not None and len(order) >= num_groups_limit
+        ng = min(len(order), num_groups_limit) if num_groups_limit is not None else len(order)
+        gid_all = rank[inv]
+        keys = []
+        for code in ukeys[order[:ng]].tolist():
+            k = []
+            for u in uniq_vals:
+                k.append(u[code % len(u)].item() if hasattr(u[code % len(u)], "item") else u[code % len(u)])
+                code //= len(u)
+            keys.append(tuple(k))
+        per_agg = [None] * na
+        per_exact = [None] * na
+        off = 0
+        for docs, idxs in parts:
+            gid = gid_all[off:off + len(docs)]
+            off += len(docs)
+            keep = gid < ng                             # INVALID_ID past the limit: doc dropped
+            for i in idxs:
+                per_agg[i], per_exact[i] = _group_aggregate(os_, query.aggregations[i], docs[keep], gid[keep], ng)
+        for g, k in enumerate(keys):
+            vals = [per_agg[a][g] for a in range(na)]
+            exs = [per_exact[a][g] if per_exact[a] is not None else None for a in range(na)]
+            if k in groups:
+                groups[k] = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(query.aggregations, groups[k], vals)]
+                exact_groups[k] = [(a + b) if a is not None and b is not None else None
+                                   for a, b in zip(exact_groups[k], exs)]
+            else:
+                groups[k] = vals
+                exact_groups[k] = exs
+    return GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats, limit_reached), exact_groups
 
 
 def filter_mask(query, segment):

@@ -68,6 +68,13 @@ class Aggregation(ctypes.Structure):
                 ("column_b", ctypes.c_int32), ("log2m", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class OrderTerm(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("a", ctypes.c_int32), ("b", ctypes.c_int32), ("desc", ctypes.c_int32)]
+
+
+ORDER_GROUP_KEY, ORDER_VALUE, ORDER_AVG, ORDER_RANGE = 0, 1, 2, 3
+
+
 class QueryDesc(ctypes.Structure):
     _fields_ = [("num_columns", ctypes.c_int32), ("num_segments", ctypes.c_int32),
                 ("columns", ctypes.POINTER(ctypes.c_char_p)), ("segments", ctypes.POINTER(ctypes.c_uint64)),
@@ -77,7 +84,9 @@ class QueryDesc(ctypes.Structure):
                 ("num_groups_limit", ctypes.c_int64),
                 ("order_by_aggregation", ctypes.c_int32), ("order_by_desc", ctypes.c_int32),
                 ("trim_size", ctypes.c_int64), ("num_order_by_keys", ctypes.c_int32), ("reserved0", ctypes.c_int32),
-                ("order_by_keys", ctypes.POINTER(ctypes.c_int32))]
+                ("order_by_keys", ctypes.POINTER(ctypes.c_int32)),
+                ("num_order_terms", ctypes.c_int32), ("reserved1", ctypes.c_int32),
+                ("order_terms", ctypes.POINTER(OrderTerm))]
 
 
 class Result(ctypes.Structure):

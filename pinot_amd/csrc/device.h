@@ -231,6 +231,20 @@ struct KeyOrder {
   int64_t card[kMaxOrderKeys];  // query-global cardinality of group-by column k
 };
 
+// General ORDER BY for the device trim (trim.hip, launch_trim_order_terms): up to kMaxOrderKeys terms, each a
+// group-by column or the final result of an aggregation (TableResizer's GroupByExpressionExtractor /
+// AggregationFunctionExtractor), sorted least significant term first with stable radix passes.
+enum OrderTermKind : int32_t { TERM_GROUP_KEY = 0, TERM_VALUE = 1, TERM_AVG = 2, TERM_RANGE = 3 };
+struct OrderTerms {
+  int32_t num_group_by;
+  int32_t num_terms;
+  int64_t card[kMaxOrderKeys];   // query-global cardinality of group-by column k
+  int32_t kind[kMaxOrderKeys];   // OrderTermKind
+  int32_t a[kMaxOrderKeys];      // group-by index (GROUP_KEY), value slot (VALUE), SUM / MIN slot (AVG / RANGE)
+  int32_t b[kMaxOrderKeys];      // COUNT slot (AVG), MAX slot (RANGE)
+  int32_t desc[kMaxOrderKeys];
+};
+
 // One compressed chunk of a raw fixed-byte forward index (BaseChunkForwardIndexReader.java:204-232):
 // `csize` bytes at blob + src decode to `usize` BE bytes, stored byte-swapped at out + dst.
 struct RawChunk {

@@ -34,6 +34,9 @@ hipError_t launch_bswap64(uint64_t *p, int64_t n, hipStream_t s);
 hipError_t launch_trim_order(const double *vals, const int64_t *keys, const KeyOrder *ko, int64_t n, int32_t naggs,
                              int32_t agg, int32_t desc, void *scratch, size_t *scratch_bytes, const int32_t **order_out,
                              hipStream_t s);
+hipError_t launch_trim_order_terms(const double *vals, const int64_t *keys, const OrderTerms *ot, int64_t n,
+                                   int32_t naggs, void *scratch, size_t *scratch_bytes, const int32_t **order_out,
+                                   hipStream_t s);
 hipError_t launch_trim_gather(const int32_t *order, int64_t k, int32_t naggs, int64_t hll_bytes, const int64_t *keys,
                               const double *vals, const int64_t *longs, const uint8_t *hll, int64_t *keys_out,
                               double *vals_out, int64_t *longs_out, uint8_t *hll_out, hipStream_t s);
@@ -983,6 +986,7 @@ struct Plan {
   int32_t order_agg = -1, order_desc = 0;  // server-level trim (phip_query_desc.order_by_aggregation)
   int32_t order_nkeys = 0;                 // > 0: ORDER BY group-by columns (order_keys)
   int32_t order_keys[kMaxOrderKeys] = {};
+  OrderTerms order_terms{};                // num_terms > 0: general ORDER BY (phip_query_desc.order_terms)
   int64_t trim_size = 0;
   int64_t filter_bytes = 0;  // algorithmic bytes of one filter launch (phip_result.filter_bytes)
   std::vector<int64_t> seg_docs;  // num_docs per query segment
@@ -1951,7 +1955,38 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.num_group_by = q->num_group_by;
   P.num_projected = num_projected;
   P.num_groups_limit = q->num_groups_limit;
-  if (q->trim_size > 0 && q->num_order_by_keys > 0) {
+  if (q->trim_size > 0 && q->num_order_terms > 0) {
+    if (q->num_order_terms > kMaxOrderKeys || q->num_group_by > kMaxOrderKeys || !q->order_terms)
+      return fail(PHIP_ERR_UNSUPPORTED, "device trim: at most %d ORDER BY terms / group-by columns", kMaxOrderKeys);
+    OrderTerms &ot = P.order_terms;
+    ot.num_group_by = q->num_group_by;
+    ot.num_terms = q->num_order_terms;
+    for (int j = 0; j < q->num_order_terms; j++) {
+      const phip_order_term &t = q->order_terms[j];
+      auto agg_ok = [&](int32_t i, bool count) {
+        if (i < 0 || i >= q->num_aggregations) return false;
+        const int32_t f = q->aggregations[i].function;
+        return count ? f == PHIP_AGG_COUNT : f != PHIP_AGG_HLL;
+      };
+      bool ok;
+      switch (t.kind) {
+        case PHIP_ORDER_GROUP_KEY: ok = t.a >= 0 && t.a < q->num_group_by; break;
+        case PHIP_ORDER_VALUE: ok = agg_ok(t.a, false); break;
+        case PHIP_ORDER_AVG: ok = agg_ok(t.a, false) && q->aggregations[t.a].function == PHIP_AGG_SUM && agg_ok(t.b, true); break;
+        case PHIP_ORDER_RANGE:
+          ok = agg_ok(t.a, false) && agg_ok(t.b, false) && q->aggregations[t.a].function == PHIP_AGG_MIN &&
+               q->aggregations[t.b].function == PHIP_AGG_MAX;
+          break;
+        default: ok = false;
+      }
+      if (!ok) return fail(PHIP_ERR_INVALID, "order_terms[%d] (kind %d, a %d, b %d) invalid", j, t.kind, t.a, t.b);
+      ot.kind[j] = t.kind;
+      ot.a[j] = t.a;
+      ot.b[j] = t.b;
+      ot.desc[j] = t.desc ? 1 : 0;
+    }
+    P.trim_size = q->trim_size;
+  } else if (q->trim_size > 0 && q->num_order_by_keys > 0) {
     if (q->num_order_by_keys > kMaxOrderKeys || q->num_group_by > kMaxOrderKeys || !q->order_by_keys)
       return fail(PHIP_ERR_UNSUPPORTED, "device trim: at most %d ORDER BY / group-by columns", kMaxOrderKeys);
     for (int j = 0; j < q->num_order_by_keys; j++) {
@@ -2406,7 +2441,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       rc = group_limit(P, ws, st, matched_docs, &keys, &ov, &ol, &oh, &ngroups, &r.num_groups_limit_reached);
       if (rc) return rc;
     }
-    if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0)) {
+    if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0 || P.order_terms.num_terms > 0)) {
       // ORDER BY <aggregation> with more groups than trimSize: keep the top trimSize on the device
       // (IndexedTable.finish -> TableResizer.getTopRecords), so only those records cross PCIe.
       size_t sbytes = 0;
@@ -2420,8 +2455,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         ko.desc[j] = P.order_keys[j] < 0;
       }
       const KeyOrder *kop = P.order_nkeys > 0 ? &ko : nullptr;
-      HIP_TRY(launch_trim_order(nullptr, nullptr, kop, ngroups, naggs, P.order_agg, P.order_desc, nullptr, &sbytes,
-                                &order, st));
+      OrderTerms ot = P.order_terms;
+      for (int k = 0; k < P.num_group_by; k++) ot.card[k] = gb_dicts[k]->card;
+      const bool terms = ot.num_terms > 0;
+      if (terms)
+        HIP_TRY(launch_trim_order_terms(nullptr, nullptr, &ot, ngroups, naggs, nullptr, &sbytes, &order, st));
+      else
+        HIP_TRY(launch_trim_order(nullptr, nullptr, kop, ngroups, naggs, P.order_agg, P.order_desc, nullptr, &sbytes,
+                                  &order, st));
       void *scratch, *k2, *v2, *l2, *h2 = nullptr;
       const int64_t k = P.trim_size;
       if ((rc = ws.get("trim_scratch", sbytes, &scratch))) return rc;
@@ -2429,8 +2470,12 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       if ((rc = ws.get("trim_vals", (size_t)k * std::max(naggs, 1) * 8, &v2))) return rc;
       if ((rc = ws.get("trim_longs", (size_t)k * std::max(naggs, 1) * 8, &l2))) return rc;
       if (nhll && (rc = ws.get("trim_hll", (size_t)k * nhll * m_regs, &h2))) return rc;
-      HIP_TRY(launch_trim_order((const double *)ov, (const int64_t *)keys, kop, ngroups, naggs, P.order_agg,
-                                P.order_desc, scratch, &sbytes, &order, st));
+      if (terms)
+        HIP_TRY(launch_trim_order_terms((const double *)ov, (const int64_t *)keys, &ot, ngroups, naggs, scratch, &sbytes,
+                                        &order, st));
+      else
+        HIP_TRY(launch_trim_order((const double *)ov, (const int64_t *)keys, kop, ngroups, naggs, P.order_agg,
+                                  P.order_desc, scratch, &sbytes, &order, st));
       HIP_TRY(launch_trim_gather(order, k, naggs, nhll ? (int64_t)nhll * m_regs : 0, (const int64_t *)keys,
                                  (const double *)ov, (const int64_t *)ol, (const uint8_t *)oh, (int64_t *)k2,
                                  (double *)v2, (int64_t *)l2, (uint8_t *)h2, st));

@@ -59,6 +59,44 @@ __global__ void key_order_kernel(const int64_t *__restrict__ keys, int64_t n, Ke
   }
 }
 
+// One radix pass of the general ORDER BY: the 64-bit order-preserving key of term j for every group, in the
+// order the previous (less significant) pass left them (perm == nullptr: group order).
+__device__ __forceinline__ uint64_t double_order(double d) {
+  const uint64_t u = (uint64_t)__double_as_longlong(d);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);  // Double.compare order: -0.0 < 0.0, NaN last
+}
+
+__global__ void term_keys_kernel(const double *__restrict__ vals, const int64_t *__restrict__ keys, int64_t n,
+                                 int32_t naggs, OrderTerms ot, int32_t j, const int32_t *__restrict__ perm,
+                                 uint64_t *__restrict__ ukeys, int32_t *__restrict__ idx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = perm ? perm[i] : i;
+    uint64_t u;
+    if (ot.kind[j] == TERM_GROUP_KEY) {
+      int64_t key = keys[g], id = 0;
+      for (int k = 0; k <= ot.a[j]; k++) {
+        id = key % ot.card[k];
+        key /= ot.card[k];
+      }
+      u = (uint64_t)(ot.desc[j] ? ot.card[ot.a[j]] - 1 - id : id);
+    } else {
+      const double *v = vals + g * naggs;
+      double d;
+      if (ot.kind[j] == TERM_VALUE) {
+        d = v[ot.a[j]];
+      } else if (ot.kind[j] == TERM_AVG) {  // AvgAggregationFunction.extractFinalResult: -inf without docs
+        d = v[ot.b[j]] != 0.0 ? v[ot.a[j]] / v[ot.b[j]] : -__builtin_huge_val();
+      } else {                               // MinMaxRangeAggregationFunction.extractFinalResult: max - min
+        d = v[ot.b[j]] - v[ot.a[j]];
+      }
+      u = double_order(d);
+      if (ot.desc[j]) u = ~u;
+    }
+    ukeys[i] = u;
+    idx[i] = (int32_t)g;
+  }
+}
+
 static inline int trim_grid(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -90,6 +128,44 @@ hipError_t launch_trim_order(const double *vals, const int64_t *keys, const KeyO
   e = hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, k0, k1, i0, i1, (int)n, 0, 64, s);
   *order_out = i1;
   return e;
+}
+
+static inline int key_bits(int64_t card) {
+  int b = 1;
+  while (b < 64 && ((int64_t)1 << b) < card) b++;
+  return b;
+}
+
+// General ORDER BY: one stable radix pass per term, least significant term first (LSD over terms), so ties
+// on every term keep the lowest group index. Same scratch layout as launch_trim_order.
+hipError_t launch_trim_order_terms(const double *vals, const int64_t *keys, const OrderTerms *ot, int64_t n,
+                                   int32_t naggs, void *scratch, size_t *scratch_bytes, const int32_t **order_out,
+                                   hipStream_t s) {
+  size_t sort_bytes = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                                    (const int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0, 64, s);
+  if (e != hipSuccess) return e;
+  const size_t keys_bytes = ((size_t)n * 16 + 255) & ~(size_t)255, idx_bytes = ((size_t)n * 8 + 255) & ~(size_t)255;
+  if (scratch == nullptr) {
+    *scratch_bytes = keys_bytes + idx_bytes + sort_bytes;
+    return hipSuccess;
+  }
+  uint64_t *k0 = (uint64_t *)scratch, *k1 = k0 + n;
+  int32_t *i0 = (int32_t *)((uint8_t *)scratch + keys_bytes), *i1 = i0 + n;
+  void *tmp = (uint8_t *)scratch + keys_bytes + idx_bytes;
+  const int32_t *perm = nullptr;
+  for (int j = ot->num_terms - 1; j >= 0; j--) {
+    term_keys_kernel<<<trim_grid(n), 256, 0, s>>>(vals, keys, n, naggs, *ot, j, perm, k0, i0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int end_bit = ot->kind[j] == TERM_GROUP_KEY ? key_bits(ot->card[ot->a[j]]) : 64;
+    size_t tb = sort_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, i0, i1, (int)n, 0, end_bit, s);
+    if (e != hipSuccess) return e;
+    perm = i1;  // the next pass reads i1 and writes k0 / i0: no overlap
+  }
+  *order_out = i1;
+  return hipSuccess;
 }
 
 hipError_t launch_trim_gather(const int32_t *order, int64_t k, int32_t naggs, int64_t hll_bytes, const int64_t *keys,

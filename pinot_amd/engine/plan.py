@@ -359,24 +359,32 @@ class GpuCombineOperator:
         q.num_group_by = len(self.query.group_by)
         q.group_by_columns = gb
         q.num_groups_limit = self.num_groups_limit
-        q.order_by_aggregation, q.order_by_desc, q.trim_size, okeys = self._trim_spec()
+        q.order_by_aggregation, q.order_by_desc, q.trim_size, okeys, terms = self._trim_spec()
         if okeys:
             arr = (ctypes.c_int32 * len(okeys))(*okeys)
             keep.append(arr)
             q.num_order_by_keys = len(okeys)
             q.order_by_keys = arr
+        if terms:
+            arr = (_lib.OrderTerm * len(terms))(*[_lib.OrderTerm(*t) for t in terms])
+            keep.append(arr)
+            q.num_order_terms = len(terms)
+            q.order_terms = arr
         return q
 
     def _trim_spec(self):
         """Server-level trim of GroupByUtils.createIndexedTableForCombineOperator (GroupByUtils.java:96-140):
         with ORDER BY the combine keeps trimSize = getTableCapacity(limit, minServerGroupTrimSize)
         = max(5 * limit, 5000) records (:55-58; default minServerGroupTrimSize 5000,
-        InstancePlanMakerImplV2.java:92), ordered by the ORDER BY. The device trims when the ORDER BY is a
-        single SUM/MIN/MAX/COUNT aggregation or only group-by columns; otherwise every group is returned (the broker's ORDER BY +
-        LIMIT gives the same final rows)."""
+        InstancePlanMakerImplV2.java:92), ordered by the ORDER BY (TableResizer's extractors:
+        group-by values, or aggregations' final results). Returns (order_by_aggregation, desc, trimSize,
+        group-key order, general terms): a single SUM/MIN/MAX/COUNT or only group-by columns use the one-pass
+        device orders, any other mix of group-by columns and SUM/MIN/MAX/COUNT/AVG/MINMAXRANGE goes as
+        PHIP_ORDER_* terms; an ORDER BY outside that (HLL, post-aggregation expressions) returns every group
+        (the broker's ORDER BY + LIMIT gives the same final rows)."""
         from .reduce import _agg_index
         q = self.query
-        none = (-1, 0, 0, [])
+        none = (-1, 0, 0, [], [])
         if not q.group_by or not q.order_by or not getattr(self, "device_trim", True):
             return none
         min_trim = int(q.options.get("minServerGroupTrimSize", 5000))
@@ -384,18 +392,32 @@ class GpuCombineOperator:
             return none
         trim = min(max(5 * int(q.limit), min_trim), 2 ** 31 - 1)
         gb = [str(e) for e in q.group_by]
-        if all(str(ob.expression) in gb for ob in q.order_by) and len(q.order_by) <= 8 and len(gb) <= 8:
+        if len(q.order_by) > 8 or len(gb) > 8:
+            return none
+        if all(str(ob.expression) in gb for ob in q.order_by):
             keys = [(gb.index(str(ob.expression)) + 1) * (1 if ob.ascending else -1) for ob in q.order_by]
-            return -1, 0, trim, keys
-        if len(q.order_by) != 1:
-            return none
-        i = _agg_index(q, q.order_by[0].expression)
-        if i is None:
-            return none
-        f, s = self.mapping[i]
-        if f not in ("sum", "min", "max", "count") or q.aggregations[i].filter is not None:
-            return none
-        return int(s), int(not q.order_by[0].ascending), trim, []
+            return -1, 0, trim, keys, []
+        terms = []
+        for ob in q.order_by:
+            desc = int(not ob.ascending)
+            if str(ob.expression) in gb:
+                terms.append((_lib.ORDER_GROUP_KEY, gb.index(str(ob.expression)), 0, desc))
+                continue
+            i = _agg_index(q, ob.expression)
+            if i is None or q.aggregations[i].filter is not None:
+                return none
+            f, sl = self.mapping[i]
+            if f in ("sum", "min", "max", "count"):
+                terms.append((_lib.ORDER_VALUE, int(sl), 0, desc))
+            elif f == "avg":
+                terms.append((_lib.ORDER_AVG, int(sl[0]), int(sl[1]), desc))
+            elif f == "minmaxrange":
+                terms.append((_lib.ORDER_RANGE, int(sl[0]), int(sl[1]), desc))
+            else:
+                return none
+        if len(terms) == 1 and terms[0][0] == _lib.ORDER_VALUE:
+            return terms[0][1], terms[0][3], trim, [], []
+        return -1, 0, trim, [], terms
 
     def filter_bitmap(self) -> np.ndarray:
         """BaseFilterOperator.getTrues for a single segment, as 64-doc bitmap words."""
@@ -646,6 +668,258 @@ class GpuFilteredAggregationOperator:
             op.close()
 
 
+_HOLDER_DEFAULTS = {"count": 0, "min": float("inf"), "max": float("-inf"), "avg": (0.0, 0),
+                    "minmaxrange": (float("inf"), float("-inf"))}
+
+
+def _holder_default(ag, sample):
+    """The value GroupByResultHolder.ensureCapacity leaves in a group no doc of the function's filter reached
+    (DoubleGroupByResultHolder: the function's default -- 0.0 for SUM, +/-inf for MIN/MAX; count 0; an empty
+    HLL). ``sample`` is another group's intermediate of the same function, to keep its type (exact int sums)."""
+    f = ag.function
+    if f == "sum":
+        return 0 if isinstance(sample, int) else 0.0
+    if f in ("distinctcounthll", "distinctcountrawhll"):
+        return np.zeros(1 << ag.log2m, dtype=np.uint8)
+    return _HOLDER_DEFAULTS[f]
+
+
+class GpuFilteredGroupByOperator:
+    """FilteredGroupByOperator (pinot-core/.../operator/query/FilteredGroupByOperator.java:110-176) over all
+    segments. The infos of AggregationFunctionUtils.buildFilteredAggregationInfos (:312-400) -- one per distinct
+    FILTER (main AND filter), then the main filter with the non-filtered functions, which a group-by always gets
+    so every group of the main filter exists (unless ``filteredAggregationsSkipEmptyGroups``) -- each run as one
+    GPU group-by over all segments (no device trim: the trim belongs after the merge). The reference shares one
+    group key generator across the infos; here the per-info group tables are merged by key, functions whose
+    filter never reached a group keep their holder default, and the server-level trim
+    (GroupByUtils / IndexedTable) runs on the merged block. numDocsScanned / post-filter entries are summed over
+    the infos (each projects the group-by columns + its functions' arguments).
+
+    numGroupsLimit: the reference's shared generator numbers groups first-seen over info 0's docs, then
+    info 1's, ... in its HashMap order of the filters, so which groups survive a reached limit is not defined
+    by the query; when any info reaches the limit the operator raises UnsupportedOnGpu (PHIP_ERR_UNSUPPORTED:
+    the Java plan maker keeps its own CPU operator)."""
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
+        self.query = query
+        self.segments = list(segments)
+        self.num_groups_limit = num_groups_limit
+        main, infos = [], {}
+        for i, ag in enumerate(query.aggregations):
+            if ag.filter is None:
+                main.append(i)
+            else:
+                infos.setdefault(ag.filter, []).append(i)
+        order = list(infos.items())
+        skip = str(query.options.get("filteredAggregationsSkipEmptyGroups", "false")).lower() == "true"
+        if main or not skip:
+            order.append((None, main))
+        self.parts = []
+        for flt, idxs in order:
+            if flt is None:
+                f = query.filter
+            elif query.filter is None:
+                f = flt
+            else:
+                f = FilterContext.AND(query.filter, flt)
+            # an info without functions still generates its groups: a COUNT rides along and is dropped
+            aggs = [query.aggregations[i].unfiltered() for i in idxs] or [AggregationInfo("count", None)]
+            sub = QueryContext(query.table, [], aggs, f, list(query.group_by), limit=query.limit,
+                               options=dict(query.options))
+            op = GpuCombineOperator(sub, self.segments, num_groups_limit)
+            op.device_trim = False
+            self.parts.append((idxs, op))
+
+    def next_block(self):
+        from .reduce import trim_groups
+        na = len(self.query.aggregations)
+        stats = ExecutionStatistics()
+        per_part = []
+        keys = {}
+        device_ms = 0.0
+        for idxs, op in self.parts:
+            blk = op.next_block()
+            if blk.num_groups_limit_reached:
+                raise UnsupportedOnGpu("numGroupsLimit reached by a FILTER + GROUP BY query (group numbering follows "
+                                       "the reference's filter HashMap order)")
+            per_part.append((idxs, blk.groups))
+            for k in blk.groups:
+                keys.setdefault(k, None)
+            s = blk.stats
+            stats.num_docs_scanned += s.num_docs_scanned
+            stats.num_entries_scanned_in_filter += s.num_entries_scanned_in_filter
+            stats.num_entries_scanned_post_filter += s.num_entries_scanned_post_filter
+            stats.num_total_docs = s.num_total_docs
+            stats.num_segments_processed = s.num_segments_processed
+            stats.num_segments_matched = max(stats.num_segments_matched, s.num_segments_matched)
+            device_ms += getattr(blk, "device_ms", 0.0) or 0.0
+        groups = {k: [None] * na for k in keys}
+        for idxs, pg in per_part:
+            for j, i in enumerate(idxs):
+                ag = self.query.aggregations[i]
+                sample = next(iter(pg.values()))[j] if pg else None
+                dflt = _holder_default(ag, sample)
+                for k, vals in groups.items():
+                    v = pg.get(k)
+                    vals[i] = v[j] if v is not None else (dflt.copy() if isinstance(dflt, np.ndarray) else dflt)
+        blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats, False)
+        blk.num_groups_trimmed = False
+        blk = trim_groups(self.query, blk)
+        blk.device_ms = device_ms
+        return blk
+
+    def close(self):
+        for _, op in self.parts:
+            op.close()
+
+
+def _is_case(e):
+    return isinstance(_strip_cast(e), Function) and _strip_cast(e).name == "case"
+
+
+def _and(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    return FilterContext.AND(a, b)
+
+
+class GpuCaseAggregationOperator:
+    """Aggregations over ``CASE WHEN c1 THEN e1 [WHEN c2 THEN e2 ...] ELSE e END`` (the CASE-based sums of
+    SURVEY.md §8f f1; CaseTransformFunction picks, per doc, the THEN of the first WHEN that holds, else the ELSE).
+
+    The GPU never materialises the CASE column: branch k holds exactly the docs of
+    ``c_k AND NOT (c_1 OR ... OR c_{k-1})`` (ELSE: ``NOT (c_1 OR ... OR c_n)``), so the aggregation splits into
+    filtered aggregations of the branch values -- ``agg(e_k) FILTER(WHERE branch_k)`` for an expression,
+    ``COUNT(*) FILTER(WHERE branch_k)`` for a literal -- which run through the filtered operators (one GPU pass
+    per distinct filter) and are folded back per group: SUM = sum of branch sums + literal x branch count,
+    MIN / MAX over the branch results (a literal counts when its branch has docs), AVG = that sum over
+    COUNT(*), COUNT(CASE ...) = COUNT(*). The reference's statistics are those of ONE pass per original filter
+    (an unfiltered CASE query is a plain AggregationOperator / GroupByOperator): hidden ``COUNT(*)`` per
+    original filter give numDocsScanned and, times the columns that filter's functions project (CASE
+    conditions included), numEntriesScannedPostFilter."""
+
+    _FOLDABLE = ("sum", "min", "max", "avg", "minmaxrange", "count")
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
+        self.query = query
+        inner = []
+
+        def slot(fn, arg, flt, log2m=8):
+            a = AggregationInfo(fn, arg, log2m, flt)
+            if a not in inner:
+                inner.append(a)
+            return inner.index(a)
+
+        self.plan = []
+        for ag in query.aggregations:
+            if ag.argument is None or not _is_case(ag.argument):
+                self.plan.append(("pass", slot(ag.function, ag.argument, ag.filter, ag.log2m)))
+                continue
+            if ag.function not in self._FOLDABLE:
+                raise UnsupportedOnGpu(f"{ag.function} over CASE")
+            if ag.function == "count":
+                self.plan.append(("pass", slot("count", None, ag.filter)))
+                continue
+            case = _strip_cast(ag.argument)
+            conds, vals = list(case.args[0:-1:2]), list(case.args[1:-1:2]) + [case.args[-1]]
+            branches = []
+            for k, v in enumerate(vals):
+                prior = None
+                if k:
+                    prior = FilterContext.NOT(conds[0] if k == 1 else FilterContext.OR(*conds[:k]))
+                cond = conds[k] if k < len(conds) else None
+                bflt = _and(ag.filter, _and(cond, prior))
+                v = _strip_cast(v)
+                if isinstance(v, Literal):
+                    if isinstance(v.value, str):
+                        raise UnsupportedOnGpu("string literal in a CASE under an aggregation")
+                    branches.append(("lit", v.value, slot("count", None, bflt)))
+                else:
+                    fn = "sum" if ag.function == "avg" else ag.function
+                    branches.append(("expr", fn, slot(fn, v, bflt)))
+            total = slot("count", None, ag.filter) if ag.function == "avg" else None
+            self.plan.append(("case", ag.function, branches, total))
+        # statistics: one pass per original filter (FilteredAggregationOperator / FilteredGroupByOperator infos)
+        self.stats_slots = []
+        gb_cols = set()
+        for e in query.group_by:
+            gb_cols.update(columns_of(e))
+        per_filter = {}
+        for ag in query.aggregations:
+            cols = per_filter.setdefault(ag.filter, set(gb_cols))
+            if ag.argument is not None:
+                cols.update(columns_of(ag.argument))
+        if query.group_by and None not in per_filter and \
+                str(query.options.get("filteredAggregationsSkipEmptyGroups", "false")).lower() != "true":
+            per_filter[None] = set(gb_cols)
+        for flt, cols in per_filter.items():
+            self.stats_slots.append((slot("count", None, flt), len(cols)))
+        inner_options = dict(query.options)
+        if all(ag.filter is None for ag in query.aggregations):
+            inner_options.pop("filteredAggregationsSkipEmptyGroups", None)  # the CASE query's groups = main filter's
+        self.inner_query = QueryContext(query.table, [], inner, query.filter, list(query.group_by), [],
+                                        limit=query.limit, options=inner_options)
+        if query.group_by:
+            self.inner = GpuFilteredGroupByOperator(self.inner_query, segments, num_groups_limit)
+        else:
+            self.inner = GpuFilteredAggregationOperator(self.inner_query, segments, num_groups_limit)
+
+    def _fold(self, vals):
+        out = []
+        for p in self.plan:
+            if p[0] == "pass":
+                out.append(vals[p[1]])
+                continue
+            _, fn, branches, total = p
+            if fn in ("sum", "avg"):
+                acc = 0
+                for kind, x, s in branches:
+                    acc = acc + (x * vals[s] if kind == "lit" else vals[s])
+                if not all(isinstance(x, int) for kind, x, s in branches if kind == "lit") or \
+                        not all(isinstance(vals[s], int) for kind, x, s in branches if kind == "expr"):
+                    acc = float(acc)
+                out.append(acc if fn == "sum" else (acc, int(vals[total])))
+                continue
+            lo, hi = float("inf"), float("-inf")
+            for kind, x, s in branches:
+                if kind == "lit":
+                    if vals[s] > 0:
+                        lo, hi = min(lo, float(x)), max(hi, float(x))
+                elif fn == "minmaxrange":
+                    lo, hi = min(lo, vals[s][0]), max(hi, vals[s][1])
+                else:
+                    lo, hi = min(lo, vals[s]), max(hi, vals[s])
+            out.append(lo if fn == "min" else hi if fn == "max" else (lo, hi))
+        return out
+
+    def _stats(self, stats, counts):
+        stats.num_docs_scanned = sum(int(c) for c, _ in counts)
+        stats.num_entries_scanned_post_filter = sum(int(c) * ncols for c, ncols in counts)
+        return stats
+
+    def next_block(self):
+        from .reduce import trim_groups
+        blk = self.inner.next_block()
+        if not self.query.group_by:
+            counts = [(blk.results[s], n) for s, n in self.stats_slots]
+            out = AggregationResultsBlock(self.query.aggregations, self._fold(blk.results), self._stats(blk.stats, counts))
+            out.device_ms = getattr(blk, "device_ms", 0.0)
+            return out
+        counts = [(sum(v[s] for v in blk.groups.values()), n) for s, n in self.stats_slots]
+        groups = {k: self._fold(v) for k, v in blk.groups.items()}
+        out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups,
+                                  self._stats(blk.stats, counts), blk.num_groups_limit_reached)
+        out.num_groups_trimmed = False
+        out = trim_groups(self.query, out)
+        out.device_ms = getattr(blk, "device_ms", 0.0)
+        return out
+
+    def close(self):
+        self.inner.close()
+
+
 class GpuInstancePlanMaker:
     """``pinot.server.query.executor.plan.maker.class`` plug-in."""
 
@@ -658,7 +932,11 @@ class GpuInstancePlanMaker:
     def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]):
         if isinstance(query, str):
             query = parse(query)
+        if any(ag.argument is not None and _is_case(ag.argument) for ag in query.aggregations):
+            return GpuCaseAggregationOperator(query, segments, self.num_groups_limit)
         if any(ag.filter is not None for ag in query.aggregations):
+            if query.group_by:
+                return GpuFilteredGroupByOperator(query, segments, self.num_groups_limit)
             return GpuFilteredAggregationOperator(query, segments, self.num_groups_limit)
         op = GpuCombineOperator(query, segments, self.num_groups_limit)
         op.device_trim = self.device_trim

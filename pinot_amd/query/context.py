@@ -55,6 +55,8 @@ Expression = Union[Identifier, Literal, Function, FilterClause]
 def columns_of(expr) -> List[str]:
     if isinstance(expr, Identifier):
         return [expr.name]
+    if isinstance(expr, FilterContext):  # a CASE condition
+        return expr.columns()
     if isinstance(expr, FilterClause):
         return columns_of(expr.function)
     if isinstance(expr, Function):

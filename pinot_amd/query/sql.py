@@ -21,7 +21,7 @@ _TOKEN = re.compile(r"""\s*(?:
 )""", re.VERBOSE)
 
 _KEYWORDS = {"select", "from", "where", "group", "by", "order", "limit", "and", "or", "not", "between",
-             "in", "asc", "desc", "as", "cast", "option"}
+             "in", "asc", "desc", "as", "cast", "option", "case", "when", "then", "else", "end"}
 
 
 class SqlError(ValueError):
@@ -122,6 +122,22 @@ class _Parser:
         if t[0] == "str":
             self.next()
             return Literal(t[1])
+        if t[0] == "kw" and t[1] == "case":
+            # CASE WHEN c1 THEN e1 [WHEN c2 THEN e2 ...] ELSE e END -> case(c1, e1, c2, e2, ..., e)
+            # (CalciteSqlParser's CASE -> the "case" transform function, CaseTransformFunction)
+            self.next()
+            args = []
+            while self.accept("kw", "when"):
+                args.append(self.bool_or())
+                self.expect("kw", "then")
+                args.append(self.expr())
+            if not args:
+                raise SqlError("CASE needs WHEN")
+            if not self.accept("kw", "else"):
+                raise SqlError("CASE without ELSE (a null default) is outside the subset")
+            args.append(self.expr())
+            self.expect("kw", "end")
+            return Function("case", tuple(args))
         if t[0] == "kw" and t[1] == "cast":
             self.next()
             self.expect("op", "(")
@@ -331,7 +347,20 @@ def _collect_aggs(expr, out, flt=None):
             _collect_aggs(a, out)
 
 
+_SET = re.compile(r"\s*SET\s+([A-Za-z_][A-Za-z0-9_.]*)\s*=\s*('(?:[^']|'')*'|[^;]*?)\s*;", re.IGNORECASE)
+
+
 def parse(sql: str) -> QueryContext:
+    """SQL -> QueryContext; leading ``SET key = value;`` statements become query options (as the broker's
+    CalciteSqlParser.compileToPinotQuery collects them)."""
+    options = {}
+    while True:
+        m = _SET.match(sql)
+        if not m:
+            break
+        v = m.group(2)
+        options[m.group(1)] = v[1:-1].replace("''", "'") if v.startswith("'") else v
+        sql = sql[m.end():]
     table, select, filt, group_by, order_by, limit = _Parser(sql).query()
     aggs = []
     for e, _ in select:
@@ -353,4 +382,4 @@ def parse(sql: str) -> QueryContext:
                 raise SqlError(f"select expression {e} is neither an aggregation nor a group-by expression")
     if not aggs and not group_by:
         raise SqlError("selection / distinct queries are out of scope for the hot path")
-    return QueryContext(table, select, aggs, filt, group_by, resolved_order, limit)
+    return QueryContext(table, select, aggs, filt, group_by, resolved_order, limit, options)

@@ -109,6 +109,7 @@ class ImmutableSegment:
     name: str
     num_docs: int
     columns: Dict[str, ColumnIndexes] = field(default_factory=dict)
+    star_trees: list = field(default_factory=list)  # startree.StarTree per StarTreeIndexConfig
 
     def column_names(self) -> List[str]:
         return list(self.columns.keys())
@@ -207,7 +208,8 @@ class SegmentCreator:
 
     def __init__(self, name: str, inverted_index_columns: Sequence[str] = (),
                  no_dictionary_columns: Sequence[str] = (), run_optimize_bitmaps: bool = True,
-                 raw_compression=None, docs_per_chunk: int = 1000, raw_version: int = 3):
+                 raw_compression=None, docs_per_chunk: int = 1000, raw_version: int = 3,
+                 star_tree_configs: Sequence = ()):
         """raw_compression: column -> ChunkCompressionType name for no-dictionary columns
         (PASS_THROUGH when absent, the METRIC default of ForwardIndexType.java:144-150)."""
         self.name = name
@@ -217,7 +219,9 @@ class SegmentCreator:
         self.inverted = set(inverted_index_columns)
         self.raw = set(no_dictionary_columns)
         self.run_optimize = run_optimize_bitmaps
+        self.star_tree_configs = list(star_tree_configs)
         self._cols = []
+        self._ids = {}
 
     def add_column(self, name: str, data_type: DataType, values):
         if data_type == DataType.STRING:
@@ -236,6 +240,16 @@ class SegmentCreator:
             if len(vals) != n:
                 raise ValueError(f"column {name}: {len(vals)} values, expected {n}")
             seg.columns[name] = self._build_column(name, dt, vals, n)
+        if self.star_tree_configs:
+            from .startree import build_star_tree
+            raw = {name: vals for name, _, vals in self._cols}
+            for i, cfg in enumerate(self.star_tree_configs):
+                dims = list(cfg.dimensions_split_order)
+                for d in dims:
+                    if d not in self._ids:
+                        raise ValueError(f"star-tree dimension {d} must be a dictionary-encoded column")
+                seg.star_trees.append(build_star_tree(cfg, [self._ids[d] for d in dims], [seg.columns[d] for d in dims],
+                                                      raw, f"{self.name}.startree{i}"))
         return seg
 
     def _build_column(self, name, dt, vals, n) -> ColumnIndexes:
@@ -246,6 +260,7 @@ class SegmentCreator:
             return ColumnIndexes(meta, _chunk_forward(vals, dt, self.docs_per_chunk, self.raw_version,
                                                       self.compression.get(name, "PASS_THROUGH")))
         uniq, ids = _sorted_unique(vals, dt)
+        self._ids[name] = ids
         card = len(uniq)
         dict_bytes, width = _encode_dictionary(uniq, dt)
         is_sorted = bool(n == 0 or np.all(np.diff(ids) >= 0))

@@ -1,0 +1,268 @@
+"""Star-tree index: builder and the host-side tree.
+
+Restates the reference's single-tree builder
+(pinot-segment-local/.../startree/v2/builder/BaseSingleTreeBuilder.java:300-460, OnHeapSingleTreeBuilder.java:60-159):
+
+* segment records (dimension dict ids in ``dimensionsSplitOrder``, metric values) are sorted by the dimensions
+  and records with equal dimensions aggregated (``sortAndAggregateSegmentRecords``);
+* ``constructStarTree``: a node whose range holds more than ``maxLeafRecords`` records is split on the next
+  dimension into one child per value (the records are sorted, so every child is a contiguous range) plus, when it
+  has more than one child and the dimension is not in ``skipStarNodeCreationForDimensions``, a star child whose
+  records -- appended at the end -- are the node's records with that dimension replaced by STAR, re-sorted by the
+  remaining dimensions and aggregated (``generateRecordsForStarNode``);
+* ``createAggregatedDocs``: every node gets an aggregated document (one appended record with every deeper
+  dimension STAR; a one-record leaf reuses its record; a node with a star child reuses the star child's).
+
+STAR is stored as dictionary id 0 in the star-tree forward index (StarTreeV2Constants.STAR_IN_FORWARD_INDEX = 0),
+and ALL (-1) names the star child. Metric columns are named like AggregationFunctionColumnPair.toColumnName
+(``sum__col``, ``count__*``, ``min__col``, ``max__col``) and hold the aggregated values the ValueAggregators
+produce (SUM / MIN / MAX as DOUBLE, COUNT as LONG). The star-tree documents form an ordinary
+ImmutableSegment (dimension columns share the parent segment's dictionaries), so the GPU loads and scans them with
+the same kernels as any segment.
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from ..spi import DataType
+
+STAR_IN_FORWARD_INDEX = 0  # StarTreeV2Constants.java:39
+ALL = -1                   # StarTreeNode.ALL
+DEFAULT_MAX_LEAF_RECORDS = 10_000  # StarTreeV2BuilderConfig.DEFAULT_MAX_LEAF_RECORDS
+
+_PAIR_FUNCS = ("sum", "count", "min", "max")
+
+
+@dataclass(frozen=True)
+class StarTreeIndexConfig:
+    """StarTreeIndexConfig (pinot-spi/.../config/table/StarTreeIndexConfig.java): split order, star-node
+    skips, function-column pairs (``"SUM__col"``, ``"COUNT__*"``, ...; case-insensitive function) and
+    maxLeafRecords."""
+    dimensions_split_order: Sequence[str]
+    function_column_pairs: Sequence[str]
+    skip_star_node_creation: Sequence[str] = ()
+    max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS
+
+    def pairs(self):
+        out = []
+        for p in self.function_column_pairs:
+            f, _, c = p.partition("__")
+            f = f.lower()
+            if f not in _PAIR_FUNCS:
+                raise ValueError(f"star-tree function {f} is outside the GPU subset (SUM/COUNT/MIN/MAX)")
+            if f == "count":
+                c = "*"
+            if (f, c) not in out:
+                out.append((f, c))
+        return out
+
+
+@dataclass
+class TreeNode:
+    dimension_id: int = -1
+    dimension_value: int = ALL
+    start_doc: int = 0
+    end_doc: int = 0
+    aggregated_doc: int = -1
+    child_dimension_id: int = -1
+    children: Optional[Dict[int, "TreeNode"]] = None  # dimension value (ALL for the star child) -> node
+
+    @property
+    def is_leaf(self):
+        return self.children is None
+
+
+def pair_column(f, c):
+    """AggregationFunctionColumnPair.toColumnName."""
+    return f"{f}__{c}"
+
+
+@dataclass
+class StarTree:
+    config: StarTreeIndexConfig
+    dimensions: List[str]
+    root: TreeNode
+    num_nodes: int
+    docs: object              # ImmutableSegment of the star-tree documents
+    pairs: List[tuple] = field(default_factory=list)
+
+    def pair_columns(self):
+        return [pair_column(f, c) for f, c in self.pairs]
+
+
+class _Records:
+    """Growable record store (dimension ids + aggregated metric values)."""
+
+    def __init__(self, k, metric_dtypes, cap=1024):
+        self.k = k
+        self.n = 0
+        self.dims = np.zeros((cap, k), dtype=np.int32)
+        self.mets = [np.zeros(cap, dtype=dt) for dt in metric_dtypes]
+
+    def append(self, dims, mets):
+        m = len(dims)
+        if self.n + m > len(self.dims):
+            cap = max(2 * len(self.dims), self.n + m)
+            nd = np.zeros((cap, self.k), dtype=np.int32)
+            nd[:self.n] = self.dims[:self.n]
+            self.dims = nd
+            for i, a in enumerate(self.mets):
+                na = np.zeros(cap, dtype=a.dtype)
+                na[:self.n] = a[:self.n]
+                self.mets[i] = na
+        self.dims[self.n:self.n + m] = dims
+        for a, v in zip(self.mets, mets):
+            a[self.n:self.n + m] = v
+        self.n += m
+
+
+def _aggregate_runs(dims, mets, funcs):
+    """Sorted records -> one record per run of equal dimensions, metrics merged in record order
+    (ValueAggregator.applyAggregatedValue: SUM/COUNT add, MIN/MAX compare)."""
+    n = len(dims)
+    if n == 0:
+        return dims, mets
+    change = np.ones(n, dtype=bool)
+    change[1:] = np.any(dims[1:] != dims[:-1], axis=1)
+    starts = np.flatnonzero(change)
+    out = []
+    for f, v in zip(funcs, mets):
+        if f in ("sum", "count"):
+            out.append(np.add.reduceat(v, starts))
+        elif f == "min":
+            out.append(np.minimum.reduceat(v, starts))
+        else:
+            out.append(np.maximum.reduceat(v, starts))
+    return dims[starts], out
+
+
+class _Builder:
+    def __init__(self, config, dims_ids, metric_values):
+        self.cfg = config
+        self.dimensions = list(config.dimensions_split_order)
+        self.k = len(self.dimensions)
+        self.pairs = config.pairs()
+        self.funcs = [f for f, _ in self.pairs]
+        self.skip = {self.dimensions.index(d) for d in config.skip_star_node_creation}
+        self.max_leaf = int(config.max_leaf_records)
+        n = len(dims_ids[0]) if dims_ids else 0
+        D = np.stack([np.asarray(a, dtype=np.int32) for a in dims_ids], axis=1) if self.k else np.zeros((n, 0), np.int32)
+        M = []
+        for f, c in self.pairs:
+            if f == "count":
+                M.append(np.ones(n, dtype=np.int64))     # CountValueAggregator: 1 per raw record
+            else:
+                M.append(np.asarray(metric_values[c], dtype=np.float64))  # Sum/Min/Max: doubleValue()
+        # sortAndAggregateSegmentRecords: sort by the dimensions in split order, merge equal ones
+        order = np.lexsort(D.T[::-1]) if self.k else np.arange(n)
+        dims, mets = _aggregate_runs(D[order], [m[order] for m in M], self.funcs)
+        self.rec = _Records(self.k, [m.dtype for m in M], cap=max(2 * len(dims), 16))
+        self.rec.append(dims, mets)
+        self.num_nodes = 1
+        self.root = TreeNode(start_doc=0, end_doc=self.rec.n)
+
+    def build(self):
+        if self.rec.n:
+            self._construct(self.root, 0, self.rec.n)
+            self._aggregated_docs(self.root)
+        return self.root
+
+    def _construct(self, node, start, end):
+        child_dim = node.dimension_id + 1
+        if child_dim == self.k:
+            return
+        node.child_dimension_id = child_dim
+        vals = self.rec.dims[start:end, child_dim]
+        change = np.flatnonzero(vals[1:] != vals[:-1]) + 1
+        bounds = np.concatenate(([0], change, [end - start]))
+        children = {}
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            self.num_nodes += 1
+            children[int(vals[a])] = TreeNode(child_dim, int(vals[a]), start + int(a), start + int(b))
+        node.children = children
+        if child_dim not in self.skip and len(children) > 1:
+            children[ALL] = self._star_node(start, end, child_dim)
+        for child in list(children.values()):
+            if child.end_doc - child.start_doc > self.max_leaf:
+                self._construct(child, child.start_doc, child.end_doc)
+
+    def _star_node(self, start, end, dim):
+        """constructStarNode / generateRecordsForStarNode: stable sort by the dimensions after ``dim``."""
+        self.num_nodes += 1
+        dims = self.rec.dims[start:end].copy()
+        mets = [m[start:end].copy() for m in self.rec.mets]
+        dims[:, dim] = STAR_IN_FORWARD_INDEX
+        after = dims[:, dim + 1:]
+        order = np.lexsort(after.T[::-1]) if after.shape[1] else np.arange(len(dims))
+        d2, m2 = _aggregate_runs(dims[order], [m[order] for m in mets], self.funcs)
+        node = TreeNode(dim, ALL, self.rec.n, self.rec.n + len(d2))
+        self.rec.append(d2, m2)
+        return node
+
+    def _merge_range(self, start, end):
+        dims = self.rec.dims[start].copy()
+        mets = []
+        for f, m in zip(self.funcs, self.rec.mets):
+            seg = m[start:end]
+            mets.append(seg.sum() if f in ("sum", "count") else (seg.min() if f == "min" else seg.max()))
+        return dims, mets
+
+    def _append_aggregated(self, node, dims, mets):
+        dims = dims.copy()
+        dims[node.dimension_id + 1:] = STAR_IN_FORWARD_INDEX
+        node.aggregated_doc = self.rec.n
+        self.rec.append(dims[None, :], [np.asarray([v]) for v in mets])
+
+    def _aggregated_docs(self, node):
+        """createAggregatedDocs (BaseSingleTreeBuilder.java:414-455); returns the node's aggregated record."""
+        if node.children is None:
+            if node.start_doc == node.end_doc - 1:
+                node.aggregated_doc = node.start_doc
+                return self.rec.dims[node.start_doc].copy(), [m[node.start_doc] for m in self.rec.mets]
+            dims, mets = self._merge_range(node.start_doc, node.end_doc)
+            self._append_aggregated(node, dims, mets)
+            return dims, mets
+        if ALL in node.children:
+            out = None
+            for v, child in node.children.items():
+                r = self._aggregated_docs(child)
+                if v == ALL:
+                    out = r
+                    node.aggregated_doc = child.aggregated_doc
+            return out
+        acc_d, acc_m = None, None
+        for child in node.children.values():
+            d, m = self._aggregated_docs(child)
+            if acc_d is None:
+                acc_d, acc_m = d.copy(), list(m)
+            else:
+                acc_m = [(a + b) if f in ("sum", "count") else (min(a, b) if f == "min" else max(a, b))
+                         for f, a, b in zip(self.funcs, acc_m, m)]
+        self._append_aggregated(node, acc_d, acc_m)
+        return acc_d, acc_m
+
+
+def build_star_tree(config: StarTreeIndexConfig, dims_ids: Sequence[np.ndarray], dim_columns, metric_values,
+                    name: str) -> StarTree:
+    """Builds one star-tree over a segment: ``dims_ids`` = the dict ids of every split-order dimension,
+    ``dim_columns`` = their ColumnIndexes (dictionaries and metadata are shared with the star-tree docs),
+    ``metric_values`` = column -> raw values for the SUM / MIN / MAX pairs."""
+    from .creator import ColumnIndexes, ColumnMetadata, ImmutableSegment, _chunk_forward, pack_bits
+    b = _Builder(config, dims_ids, metric_values)
+    root = b.build()
+    n = b.rec.n
+    seg = ImmutableSegment(name, n)
+    for j, dim in enumerate(b.dimensions):
+        src = dim_columns[j]
+        m = src.metadata
+        ids = b.rec.dims[:n, j]
+        meta = ColumnMetadata(dim, m.data_type, n, m.cardinality, m.bits_per_element, False, True, False,
+                              m.string_width)
+        seg.columns[dim] = ColumnIndexes(meta, pack_bits(ids, m.bits_per_element), src.dictionary, None)
+    for (f, c), vals in zip(b.pairs, b.rec.mets):
+        dt = DataType.LONG if f == "count" else DataType.DOUBLE
+        col = pair_column(f, c)
+        meta = ColumnMetadata(col, dt, n, 0, 0, False, False, False)
+        seg.columns[col] = ColumnIndexes(meta, _chunk_forward(vals[:n], dt))
+    return StarTree(config, b.dimensions, root, b.num_nodes, seg, b.pairs)

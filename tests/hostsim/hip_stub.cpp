@@ -48,6 +48,17 @@ hipError_t launch_trim_order(const double *, const int64_t *, const KeyOrder *, 
   else *order = (const int32_t *)((uint8_t *)scratch + (size_t)n * 16);
   return hipSuccess;
 }
+hipError_t launch_trim_order_terms(const double *, const int64_t *, const OrderTerms *, int64_t n, int32_t,
+                                   void *scratch, size_t *scratch_bytes, const int32_t **order_out, hipStream_t) {
+  if (!scratch) {
+    *scratch_bytes = (size_t)n * 4 + 64;
+    return hipSuccess;
+  }
+  int32_t *o = (int32_t *)scratch;
+  for (int64_t i = 0; i < n; i++) o[i] = (int32_t)i;
+  *order_out = o;
+  return hipSuccess;
+}
 hipError_t launch_trim_gather(const int32_t *, int64_t, int32_t, int64_t, const int64_t *, const double *, const int64_t *,
                               const uint8_t *, int64_t *, double *, int64_t *, uint8_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_chunk_decode(int, int, const uint8_t *, const RawChunk *, int32_t, int32_t, size_t, uint8_t *, int32_t *, hipStream_t) { return hipSuccess; }

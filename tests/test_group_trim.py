@@ -28,21 +28,31 @@ def _spec(sql, **options):
 
 
 def test_trim_spec_rules():
-    (agg, desc, trim, _k), op = _spec("SELECT k, SUM(m) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 10")
+    from pinot_amd import _lib
+    (agg, desc, trim, _k, _t), op = _spec("SELECT k, SUM(m) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 10")
     assert agg >= 0 and (desc, trim) == (1, 5000)
-    (agg, desc, trim, keys), _ = _spec("SELECT a, b, SUM(m) FROM t GROUP BY a, b ORDER BY b, a DESC LIMIT 10")
+    (agg, desc, trim, keys, _t), _ = _spec("SELECT a, b, SUM(m) FROM t GROUP BY a, b ORDER BY b, a DESC LIMIT 10")
     assert (agg, trim, keys) == (-1, 5000, [2, -1])
-    (agg, desc, trim, _k), _ = _spec("SELECT k, COUNT(*) FROM t GROUP BY k ORDER BY COUNT(*) LIMIT 2000")
+    (agg, desc, trim, _k, _t), _ = _spec("SELECT k, COUNT(*) FROM t GROUP BY k ORDER BY COUNT(*) LIMIT 2000")
     assert (agg >= 0, desc, trim) == (True, 0, 10000)
-    (agg, desc, trim, _k), _ = _spec("SELECT k, MAX(m) FROM t GROUP BY k ORDER BY MAX(m) DESC LIMIT 10",
-                                 minServerGroupTrimSize=100)
+    (agg, desc, trim, _k, _t), _ = _spec("SELECT k, MAX(m) FROM t GROUP BY k ORDER BY MAX(m) DESC LIMIT 10",
+                                         minServerGroupTrimSize=100)
     assert trim == 100
-    # no trim: disabled, aggregation + key ORDER BY, AVG, no ORDER BY
+    # mixed ORDER BY: general terms (TableResizer extractors), least significant last
+    (agg, _d, trim, keys, terms), op = _spec("SELECT k, SUM(m), AVG(m) FROM t GROUP BY k ORDER BY SUM(m), k DESC, "
+                                             "AVG(m) DESC LIMIT 10")
+    s_sum = op.mapping[0][1]
+    s_avg = op.mapping[1][1]
+    assert (agg, trim, keys) == (-1, 5000, [])
+    assert terms == [(_lib.ORDER_VALUE, s_sum, 0, 0), (_lib.ORDER_GROUP_KEY, 0, 0, 1),
+                     (_lib.ORDER_AVG, s_avg[0], s_avg[1], 1)]
+    (_a, _d, _t, _k, terms), op = _spec("SELECT k, MINMAXRANGE(m) FROM t GROUP BY k ORDER BY MINMAXRANGE(m) LIMIT 10")
+    assert terms == [(_lib.ORDER_RANGE, op.mapping[0][1][0], op.mapping[0][1][1], 0)]
+    # no trim: disabled, HLL, no ORDER BY
     for sql, opts in (("SELECT k, SUM(m) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 10", {"minServerGroupTrimSize": 0}),
-                      ("SELECT k, SUM(m) FROM t GROUP BY k ORDER BY SUM(m), k LIMIT 10", {}),
-                      ("SELECT k, AVG(m) FROM t GROUP BY k ORDER BY AVG(m) LIMIT 10", {}),
+                      ("SELECT k, DISTINCTCOUNTHLL(m) FROM t GROUP BY k ORDER BY DISTINCTCOUNTHLL(m), k LIMIT 10", {}),
                       ("SELECT k, SUM(m) FROM t GROUP BY k LIMIT 10", {})):
-        assert _spec(sql, **opts)[0] == (-1, 0, 0, []), sql
+        assert _spec(sql, **opts)[0] == (-1, 0, 0, [], []), sql
 
 
 def _segments(n_segs=2, n=200_003, card=60_000, seed=4):
@@ -101,6 +111,55 @@ def test_gpu_device_trim(gpu_lib, sql, exact_set):
             assert got == want
         else:
             assert [r[1:] for r in got] == [r[1:] for r in want]
+    finally:
+        for s in segs:
+            s.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sql", [
+    "SELECT k, COUNT(*), SUM(m) FROM t GROUP BY k ORDER BY COUNT(*) DESC, k LIMIT 10",
+    "SELECT k, k2, AVG(m) FROM t WHERE q < 45 GROUP BY k, k2 ORDER BY AVG(m) DESC, k2 LIMIT 100",  # hash table
+    "SELECT q, k, SUM(m), MIN(m) FROM t GROUP BY q, k ORDER BY q DESC, SUM(m) LIMIT 1200",
+    "SELECT k, MINMAXRANGE(m), MAX(m) FROM t GROUP BY k ORDER BY MINMAXRANGE(m), MAX(m) DESC, k LIMIT 10",
+])
+def test_gpu_device_trim_mixed_order(gpu_lib, sql):
+    """Mixed ORDER BY (GroupByUtils.java:108,161 -> TableResizer over group values and final results): the kept
+    groups are exactly the first trimSize of the untrimmed oracle's groups by the whole ORDER BY (a total order
+    here), each with the oracle's values, and the broker's rows match."""
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    from pinot_amd.engine.reduce import final_result, _agg_index
+    from pinot_amd.engine.segment import GpuSegment
+    raws = _segments()
+    segs = [GpuSegment(r) for r in raws]
+    try:
+        qc = parse(sql)
+        op = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, segs)
+        assert op._trim_spec()[4], "expected the general ORDER BY terms"
+        blk = op.next_block()
+        oblk, _ = executor.execute(qc, raws, num_groups_limit=10 ** 9)
+        trim = max(5 * qc.limit, 5000)
+        assert len(oblk.groups) > trim
+        assert blk.num_groups_trimmed and len(blk.groups) == trim
+        gb = [str(e) for e in qc.group_by]
+
+        def val(k, v, e):
+            if str(e) in gb:
+                return k[gb.index(str(e))]
+            i = _agg_index(qc, e)
+            return final_result(qc.aggregations[i].function, v[i])
+
+        recs = sorted(oblk.groups.items())
+        for ob in reversed(qc.order_by):
+            recs.sort(key=lambda kv: val(kv[0], kv[1], ob.expression), reverse=not ob.ascending)
+        assert set(blk.groups) == {k for k, _ in recs[:trim]}
+        for k, v in blk.groups.items():
+            for g, o in zip(v, oblk.groups[k]):
+                if isinstance(o, tuple):
+                    assert all(x == y or abs(x - y) <= 1e-9 * max(abs(x), abs(y)) for x, y in zip(g, o))
+                else:
+                    assert g == o or abs(g - o) <= 1e-9 * max(abs(g), abs(o))
+        assert reduce_blocks(qc, [blk]).rows == reduce_blocks(qc, [oblk]).rows
     finally:
         for s in segs:
             s.destroy()
