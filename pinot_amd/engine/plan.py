@@ -296,7 +296,10 @@ def plan_aggregations(aggs: Sequence[AggregationInfo]):
 class GpuCombineOperator:
     """One operator over all segments of the query (the all-segment GPU variant of SURVEY.md §8b)."""
 
-    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int,
+                 segment_filters=None):
+        """segment_filters: optional per-segment (FilterContext or None, inclusive doc ranges or None) replacing
+        query.filter -- the star-tree path's matched documents AND remaining predicates."""
         self.query = query
         self.segments = list(segments)
         self.num_groups_limit = num_groups_limit
@@ -304,7 +307,19 @@ class GpuCombineOperator:
             if not isinstance(e, Identifier):
                 raise UnsupportedOnGpu(f"group-by expression {e}")
         self.prims, self.mapping = plan_aggregations(query.aggregations)
-        self.trees = [compile_filter(s, query.filter) for s in self.segments]
+        if segment_filters is None:
+            self.trees = [compile_filter(s, query.filter) for s in self.segments]
+        else:
+            self.trees = []
+            for s, (flt, ranges) in zip(self.segments, segment_filters):
+                t = compile_filter(s, flt)
+                if ranges is not None:
+                    if len(ranges) == 0 or _is_const(t, _FALSE):
+                        t = _FALSE
+                    else:
+                        leaf = _Leaf(_lib.LEAF_DOC_RANGES, None, ids=np.asarray(ranges, dtype=np.int32))
+                        t = leaf if _is_const(t, _TRUE) else _Node(_lib.NODE_AND, [leaf, t])
+                self.trees.append(t)
         cols = []
         for t in self.trees:
             _leaf_columns(t, cols)
@@ -932,6 +947,11 @@ class GpuInstancePlanMaker:
     def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]):
         if isinstance(query, str):
             query = parse(query)
+        from .startree import GpuStarTreeOperator
+        st = GpuStarTreeOperator.plan(query, segments, self.num_groups_limit)
+        if st is not None:
+            st.inner.device_trim = self.device_trim
+            return st
         if any(ag.argument is not None and _is_case(ag.argument) for ag in query.aggregations):
             return GpuCaseAggregationOperator(query, segments, self.num_groups_limit)
         if any(ag.filter is not None for ag in query.aggregations):

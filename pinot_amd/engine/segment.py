@@ -62,6 +62,10 @@ class GpuSegment:
         _lib.check(lib.phip_segment_load(ctypes.byref(sd), ctypes.byref(handle)))
         self.handle = handle.value
         del keep
+        # star-tree indexes load with their segment (ImmutableSegmentLoader -> StarTreeIndexReader): the star-tree
+        # documents are resident like any segment's columns
+        self.star_trees = list(getattr(segment, "star_trees", []) or [])
+        self.star_segments = [GpuSegment(t.docs, device) for t in self.star_trees]
 
     # ---- host-side readers (DataSource equivalents) -----------------------------------------
     def column_metadata(self, column):
@@ -103,6 +107,9 @@ class GpuSegment:
         return out.value
 
     def destroy(self):
+        for s in getattr(self, "star_segments", []):
+            s.destroy()
+        self.star_segments = []
         if self.handle:
             _lib.check(_lib.load().phip_segment_unload(self.handle))
             self.handle = 0

@@ -1,0 +1,136 @@
+"""Star-tree index on the host: the builder's tree invariants and the traversal +
+remaining predicates, checked the way the reference's BaseStarTreeV2Test does it -- a query answered from the
+star-tree documents equals the same query over the raw segment (exact here: integer-valued metrics).
+
+Builder: BaseSingleTreeBuilder.java:300-460; traversal: StarTreeFilterOperator.java:212-364."""
+import numpy as np
+import pytest
+
+from oracle import executor
+from pinot_amd.engine import startree as st
+from pinot_amd.query.context import AggregationInfo, Identifier
+from pinot_amd.query.sql import parse
+from pinot_amd.segment.creator import SegmentCreator
+from pinot_amd.segment.startree import ALL, STAR_IN_FORWARD_INDEX, StarTreeIndexConfig
+from pinot_amd.spi import DataType
+
+PAIRS = ["SUM__m", "COUNT__*", "MIN__m", "MAX__m", "SUM__m2"]
+
+
+def make_segment(seed=3, n=40_000, max_leaf=50, skip=(), name="st"):
+    rng = np.random.default_rng(seed)
+    cfg = StarTreeIndexConfig(["d1", "d2", "d3", "d4"], PAIRS, skip_star_node_creation=skip, max_leaf_records=max_leaf)
+    c = SegmentCreator(name, star_tree_configs=[cfg])
+    c.add_column("d1", DataType.INT, rng.integers(0, 4, n))
+    c.add_column("d2", DataType.STRING, [f"v{x:02d}" for x in rng.integers(0, 12, n)])
+    c.add_column("d3", DataType.INT, rng.integers(0, 60, n) * 3)
+    c.add_column("d4", DataType.LONG, rng.integers(0, 300, n))
+    c.add_column("m", DataType.LONG, rng.integers(-1000, 1000, n))
+    c.add_column("m2", DataType.INT, rng.integers(0, 50, n))
+    return c.build()
+
+
+QUERIES = [
+    "SELECT SUM(m), COUNT(*) FROM t",
+    "SELECT SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE d1 = 2",
+    "SELECT SUM(m), MAX(m) FROM t WHERE d2 IN ('v01', 'v07', 'v11') AND d3 BETWEEN 30 AND 120",
+    "SELECT d1, SUM(m), COUNT(*) FROM t GROUP BY d1",
+    "SELECT d2, d4, SUM(m2), MIN(m) FROM t WHERE d1 <> 3 GROUP BY d2, d4",
+    "SELECT COUNT(*) FROM t WHERE d4 < 17 OR d4 > 280",
+    "SELECT d3, SUM(m) FROM t WHERE NOT d2 = 'v03' AND d4 >= 5 GROUP BY d3",
+    "SELECT SUM(m), COUNT(*) FROM t WHERE d1 IN (0, 1, 2, 3)",            # always true: dropped
+    "SELECT SUM(m), COUNT(*) FROM t WHERE d4 <> 7 AND d2 <> 'v02'",       # all children match: star nodes
+    "SELECT SUM(m) FROM t WHERE d3 = 1",                                 # always false: no star-tree
+    "SELECT d1, d2, d3, d4, COUNT(*) FROM t WHERE d2 = 'v05' GROUP BY d1, d2, d3, d4",
+]
+
+
+def _star_answer(qc, seg):
+    """Answer qc from the star-tree documents: traversal -> doc ranges AND remaining predicates, then the
+    oracle aggregates the pre-aggregated columns (SUM(sum__c), SUM(count__*), MIN(min__c), MAX(max__c))."""
+    view = st.HostSegmentView(seg)
+    pmap = st.predicate_map(view, qc.filter)
+    if pmap is None:
+        return None, 0
+    tree = seg.star_trees[0]
+    res = st.traverse(tree, view, pmap, [e.name for e in qc.group_by])
+    os_ = executor.OracleSegment(tree.docs)
+    mask = np.zeros(tree.docs.num_docs, dtype=bool)
+    if res is not None:
+        ranges, rem = res
+        for a, b in ranges.reshape(-1, 2):
+            mask[a:b + 1] = True
+        rf = st._remaining_filter(pmap, rem)
+        if rf is not None:
+            mask &= executor.eval_filter(os_, rf)
+    docs = np.nonzero(mask)[0]
+    inner = []
+    for ag in qc.aggregations:
+        f, c = st._pair_of(ag)
+        inner.append(AggregationInfo("sum" if f == "count" else f, Identifier(f"{f}__{c}")))
+    if not qc.group_by:
+        return [executor._agg_segment(os_, a, docs)[0] for a in inner], len(docs)
+    iq = parse("SELECT COUNT(*) FROM t")
+    iq.group_by = list(qc.group_by)
+    iq.aggregations = inner
+    groups, _, _ = executor._group_segment(os_, iq, docs, None) if len(docs) else ({}, {}, False)
+    return groups, len(docs)
+
+
+def _tree_invariants(tree):
+    docs = tree.docs
+    n = docs.num_docs
+    seen = 0
+    stack = [tree.root]
+    while stack:
+        node = stack.pop()
+        seen += 1
+        assert 0 <= node.aggregated_doc < n
+        assert node.start_doc < node.end_doc <= n
+        if node.children:
+            kids = [c for v, c in node.children.items() if v != ALL]
+            if ALL in node.children:
+                assert len(kids) > 1
+            for v, c in node.children.items():
+                assert c.dimension_id == node.dimension_id + 1 and c.dimension_value == v
+                stack.append(c)
+    assert seen == tree.num_nodes
+
+
+@pytest.mark.parametrize("max_leaf,skip", [(50, ()), (10 ** 9, ()), (1, ("d2",)), (500, ("d1", "d3"))])
+def test_star_tree_equals_scan(max_leaf, skip):
+    seg = make_segment(max_leaf=max_leaf, skip=skip)
+    tree = seg.star_trees[0]
+    _tree_invariants(tree)
+    # the root's aggregated document holds the totals
+    os_ = executor.OracleSegment(tree.docs)
+    base = executor.OracleSegment(seg)
+    r = tree.root.aggregated_doc
+    assert os_.values("count__*")[r] == seg.num_docs
+    assert os_.values("sum__m")[r] == base.values("m").sum()
+    for sql in QUERIES:
+        qc = parse(sql)
+        want, _ = executor.execute(qc, [seg], num_groups_limit=None)
+        got, ndocs = _star_answer(qc, seg)
+        if got is None:
+            assert "d3 = 1" in sql  # StarTreeUtils: an always-false predicate keeps the scan path
+            continue
+        assert ndocs <= tree.docs.num_docs
+        if not qc.group_by:
+            assert [float(x) for x in got] == [float(x) for x in want.results], sql
+        else:
+            assert set(got) == set(want.groups), sql
+            for k, v in want.groups.items():
+                assert [float(x) for x in got[k]] == [float(x) for x in v], (sql, k)
+
+
+def test_star_tree_fit_rules():
+    seg = make_segment(n=5000)
+    view = st.HostSegmentView(seg)
+    assert st.predicate_map(view, parse("SELECT COUNT(*) FROM t WHERE d1 = 1 OR d2 = 'v01'").filter) is None
+    assert st.predicate_map(view, parse("SELECT COUNT(*) FROM t WHERE NOT (d1 = 1 AND d3 = 3)").filter) is None
+    pm = st.predicate_map(view, parse("SELECT COUNT(*) FROM t WHERE m > 3").filter)
+    assert not set(pm) <= set(seg.star_trees[0].dimensions)  # isFitForStarTree: predicate column not a dimension
+    assert st.predicate_map(view, parse("SELECT COUNT(*) FROM t WHERE d1 >= 0").filter) == {}  # always true
+    assert st._pair_of(parse("SELECT AVG(m) FROM t").aggregations[0]) is None
+    assert st._pair_of(parse("SELECT SUM(m) FILTER(WHERE d1 = 1) FROM t").aggregations[0]) is None
