@@ -106,7 +106,7 @@ def _read_raw_chunk(buf, dtype, n):
         total, comp, data_hdr = [int(x) for x in np.frombuffer(buf, dtype=">i4", count=3, offset=16)]
     else:  # v1: 4-int header, SNAPPY chunks, offsets from byte 16 (BaseChunkForwardIndexReader.java:86-95)
         total, comp, data_hdr = n, 1, 16
-    assert total == n and comp in (0, 1, 3, 4), (total, comp)
+    assert total == n and comp in (0, 1, 2, 3, 4, 5), (total, comp)
     osz = 4 if version <= 2 else 8
     offs = np.frombuffer(buf, dtype=">i4" if osz == 4 else ">i8", count=num_chunks, offset=data_hdr)
     raw = np.frombuffer(buf, dtype=np.uint8)
@@ -118,6 +118,21 @@ def _read_raw_chunk(buf, dtype, n):
             continue
         end = int(offs[k + 1]) if k + 1 < num_chunks else len(buf)
         src = np.ascontiguousarray(raw[int(offs[k]):end])
+        if comp in (2, 5):
+            # ZSTANDARD / GZIP: the libraries the reference binds decode them (zstd-jni = libzstd, here Arrow's;
+            # java.util.zip.Inflater = zlib) -- ZstandardDecompressor.java / GzipDecompressor.java:40-52
+            body = src.tobytes()
+            if comp == 5:
+                import zlib
+                want = int.from_bytes(body[-4:], "big")
+                out = zlib.decompress(body[:-4])
+                assert len(out) == want, f"chunk {k}: GZIP length {len(out)} != {want}"
+            else:
+                import pyarrow as pa
+                out = pa.Codec("zstd").decompress(body, decompressed_size=docs * entry, asbytes=True)
+            assert len(out) == docs * entry, f"chunk {k}: decoded {len(out)} bytes, expected {docs * entry}"
+            parts.append(np.frombuffer(out, dtype=_BE[dtype]))
+            continue
         dst = np.empty(max(docs * entry, 1), dtype=np.uint8)
         got = _oracle_lib().oracle_chunk_decode(comp, src.ctypes.data, len(src), dst.ctypes.data, docs * entry)
         assert got == docs * entry, f"chunk {k}: decoded {got} bytes, expected {docs * entry}"

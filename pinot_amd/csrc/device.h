@@ -13,7 +13,7 @@ constexpr int kMaxGroupBy = 4;
 constexpr int kWave = 64;             // CDNA wavefront
 constexpr int kTileGroups = 32;       // 64-doc groups per tile: bit (31-g) of lane l's mask word = doc 64g+l
 constexpr int kTileDocs = kTileGroups * 64;  // 2048 docs per tile
-constexpr int kMaxStage = 12;         // LDS-staged filter sources (scan columns / inverted leaves) per segment
+constexpr int kMaxStage = 8;          // LDS-staged filter sources (scan columns / inverted leaves) per segment (SGPR budget of the cursor)
 constexpr int kStagePad = 16;         // guard bytes before and after every staged region
 constexpr int kMaxHllRegs = 1 << 12;  // log2m <= 12 on the GPU path
 
@@ -119,7 +119,8 @@ struct DevSeg {
   int32_t conj_range;   // 1: AND with the doc range [conj_lo, conj_hi] (single-range sorted-index leaves,
   int32_t conj_lo;      // SortedIndexBasedFilterOperator; tiles outside it are pruned on the host, so only the
   int32_t conj_hi;      // boundary tiles are masked)
-  int32_t pad_conj;
+  int32_t contig;       // 1: general program evaluated in the contiguous layout (filter.hip eval_filter_contig);
+                        // every leaf staged or tile-free (MATCH_*, DOC_RANGES)
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];

@@ -308,6 +308,218 @@ __device__ __forceinline__ uint32_t eval_filter(cseg_t &seg, cnode_t *__restrict
   return r;
 }
 
+#define PHIP_B_CASES(X) \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
+  X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
+
+// ------------------------------------------------------------------------------------------------
+// Contiguous layout for general programs (seg.contig). Lane L owns docs 32L .. 32L+31 of the tile, doc
+// 32L + j at bit 31 - j. In this layout an inverted leaf's dense doc words ARE the lane words (u32 half L
+// of the tile's 32 u64 words, bit-reversed: one LDS read), a scan leaf's 32 docs are exactly B consecutive
+// words of the staged forward index (read once into registers, fields cut at compile-time offsets), and
+// AND / OR / NOT stay one VALU op. Boolean algebra does not care about the bit order, so the program runs
+// entirely in this layout; only a mask that leaves the kernel is permuted to lane-major once
+// (contig_to_lane_major). The lane-major evaluator above transposes every inverted leaf and decodes every
+// scan leaf 64 docs at a time -- the instruction count that bounded config C4.
+// ------------------------------------------------------------------------------------------------
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t contig_valid(int32_t valid_docs, int lane) {
+  const int32_t n = valid_docs - 32 * lane;
+  return n >= 32 ? ~0u : (n <= 0 ? 0u : (~0u << (32 - n)));
+}
+
+// lane-major (bit 31-g of lane l = doc 64g + l) from contiguous: lane 32h + g first takes the word of
+// contiguous lane 2g + h (its bit 31-i = doc 64g + 32h + i), then each 32-lane half transposes its 32x32 bit
+// matrix (Hacker's Delight transpose32 with rows = lanes, 5 butterfly stages over ds_bpermute).
+__device__ __forceinline__ uint32_t contig_to_lane_major(uint32_t c) {
+  const int lane = lane_id();
+  uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(((2 * (lane & 31)) | (lane >> 5)) << 2, (int)c);
+  uint32_t m = 0x0000FFFFu;
+#pragma unroll
+  for (int j = 16; j != 0; j >>= 1, m ^= m << j) {
+    const uint32_t p = (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ j) << 2, (int)a);
+    if (lane & j) {
+      a ^= ((p ^ (a >> j)) & m) << j;
+    } else {
+      a ^= (a ^ (p >> j)) & m;
+    }
+  }
+  return a;
+}
+
+// One scan leaf over the lane's 32 docs: the B staged words of those docs in registers, field j cut from
+// words (jB)/32, (jB)/32 + 1 at a compile-time shift. KIND 0: dict-id range (v_sub / v_cmp / v_addc, as in
+// conj_range); 1: set of a <= 64-entry dictionary (64-bit mask); 2: set of a <= 2048-entry dictionary spread
+// over the wave (ds_bpermute per doc).
+// docs [J0, J0 + NJ) of the lane: their words (fields at compile-time offsets) in registers, then the test
+template <int B, int KIND, int J0, int NJ>
+__device__ __forceinline__ uint32_t contig_docs(const PHIP_LDS uint32_t *wl, uint32_t r, uint32_t LO, uint32_t SPAN,
+                                                uint64_t set, uint32_t myw, bool excl) {
+  constexpr int W0 = (J0 * B) >> 5;                    // first word of the docs
+  constexpr int W1 = ((J0 + NJ) * B - 1) >> 5;         // last word
+  constexpr int NW = W1 - W0 + 1;
+  uint32_t x[NW + 1];
+  if constexpr (W0 == 0 && NW == B && B % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < B / 4; q++) {
+      const u32x4_t v = ((const PHIP_LDS u32x4_t *)wl)[q];
+      x[4 * q] = v[0];
+      x[4 * q + 1] = v[1];
+      x[4 * q + 2] = v[2];
+      x[4 * q + 3] = v[3];
+    }
+  } else if constexpr (W0 == 0 && NW == B && B % 2 == 0) {
+#pragma unroll
+    for (int q = 0; q < B / 2; q++) {
+      const u32x2_t v = ((const PHIP_LDS u32x2_t *)wl)[q];
+      x[2 * q] = v[0];
+      x[2 * q + 1] = v[1];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NW; q++) x[q] = wl[W0 + q];
+  }
+  x[NW] = 0u;  // only ever supplies the bits below a field
+#pragma unroll
+  for (int j = J0; j < J0 + NJ; j++) {
+    const int o = (j * B) & 31, k = ((j * B) >> 5) - W0;
+    const uint32_t win = o == 0 ? x[k] : __builtin_amdgcn_alignbit(x[k], x[k + 1], 32 - o);
+    if constexpr (KIND == 0) {
+      uint32_t d;
+      asm("v_sub_u32 %[d], %[w], %[lo]\n\t"
+          "v_cmp_gt_u32 vcc, %[sp], %[d]\n\t"
+          "v_addc_co_u32 %[r], vcc, %[r], %[r], vcc"
+          : [r] "+v"(r), [d] "=&v"(d)
+          : [w] "v"(win), [lo] "s"(LO), [sp] "s"(SPAN)
+          : "vcc");
+    } else if constexpr (KIND == 1) {
+      r = r + r + (uint32_t)((set >> (win >> (32 - B))) & 1ull);
+    } else {
+      const uint32_t id = win >> (32 - B);
+      const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((id >> 5) << 2), (int)myw);
+      r = r + r + (((word >> (id & 31)) & 1u) ^ (excl ? 1u : 0u));
+    }
+  }
+  return r;
+}
+
+// One scan leaf over the lane's 32 docs: the B staged words of those docs (words 32L*B/32 .. of the tile)
+// read into registers -- all at once up to 16 bits, in two halves of 16 docs above (VGPR budget) -- and
+// every field cut at a compile-time shift. KIND 0: dict-id range (v_sub / v_cmp / v_addc, as in
+// conj_range); 1: set of a <= 64-entry dictionary (64-bit mask); 2: set of a <= 2048-entry dictionary spread
+// over the wave (ds_bpermute per doc).
+template <int B, int KIND>
+__device__ __forceinline__ uint32_t contig_scan(const PHIP_LDS uint32_t *w, uint32_t LO, uint32_t SPAN, uint64_t set,
+                                                uint32_t myw, bool excl) {
+  const PHIP_LDS uint32_t *wl = w + lane_id() * B;
+  if constexpr (B <= 16) {
+    return contig_docs<B, KIND, 0, 32>(wl, 0u, LO, SPAN, set, myw, excl);
+  } else {
+    const uint32_t r = contig_docs<B, KIND, 0, 16>(wl, 0u, LO, SPAN, set, myw, excl);
+    return contig_docs<B, KIND, 16, 16>(wl, r, LO, SPAN, set, myw, excl);
+  }
+}
+
+// The width / kind dispatch as a real call: its 93 unrolled bodies would otherwise be inlined into the
+// filter kernel and push it past the VGPR / SGPR budget (spills on every tile).
+__device__ __noinline__ uint32_t contig_scan_any(const PHIP_LDS uint32_t *w, int B, int k, uint32_t LO, uint32_t SPAN,
+                                                 uint64_t set, uint32_t myw, bool excl) {
+  switch (B) {
+#define PHIP_CC(b)                                                                  \
+  case b:                                                                           \
+    return k == 0 ? contig_scan<b, 0>(w, LO, SPAN, set, myw, excl)                  \
+                  : (k == 1 ? contig_scan<b, 1>(w, LO, SPAN, set, myw, excl)       \
+                            : contig_scan<b, 2>(w, LO, SPAN, set, myw, excl));
+    PHIP_B_CASES(PHIP_CC)
+#undef PHIP_CC
+  }
+  return 0u;
+}
+
+__device__ __forceinline__ uint32_t eval_leaf_contig(cseg_t &seg, cnode_t *__restrict__ n, uint32_t valid,
+                                                     const Tile &t, uint32_t &scanned) {
+  const int lane = lane_id();
+  const int kind = n->leaf_kind;
+  if (kind == PHIP_LEAF_MATCH_ALL) return valid;
+  if (kind == PHIP_LEAF_MATCH_NONE) return 0;
+  if (kind == PHIP_LEAF_DOC_RANGES) {
+    const PHIP_CAS int32_t *rg = (const PHIP_CAS int32_t *)n->aux;
+    const int32_t cnt = n->count;
+    const int32_t tile_end = t.doc0 + kTileDocs - 1;
+    int a = 0, b = cnt;
+    while (a < b) {
+      int mid = (a + b) >> 1;
+      if (rg[2 * mid + 1] < t.doc0) a = mid + 1; else b = mid;
+    }
+    const int32_t l0 = 32 * lane, l1 = l0 + 31;  // the lane's tile-relative docs
+    uint32_t m = 0;
+    for (int i = a; i < cnt; i++) {
+      const int32_t s = rg[2 * i], e = rg[2 * i + 1];
+      if (s > tile_end) break;
+      const int32_t lo = max(max(s, t.doc0) - t.doc0, l0), hi = min(min(e, tile_end) - t.doc0, l1);
+      if (lo <= hi) m |= span32(31 - (hi - l0), 31 - (lo - l0));
+    }
+    return valid & m;
+  }
+  if (kind == PHIP_LEAF_INVERTED) {  // staged (the host only picks this layout then)
+    const uint32_t w = ((const PHIP_LDS uint32_t *)(t.stage + n->lds_off))[lane];
+    uint32_t r = __builtin_bitreverse32(w);  // bit j of the u32 half = doc 32L + j
+    if (n->exclusive) r = ~r;
+    return valid & r;
+  }
+  // DICT_RANGE / DICT_SET staged scan leaves
+  scanned += (uint32_t)t.valid_docs;
+  const int32_t B = n->bits;
+  const PHIP_LDS uint32_t *w = (const PHIP_LDS uint32_t *)(t.stage + n->lds_off);
+  const uint32_t LO = (uint32_t)n->lo << (32 - B);
+  const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - B);
+  const int k = kind == PHIP_LEAF_DICT_RANGE ? 0 : (n->small_set ? 1 : 2);
+  const uint32_t myw = (k == 2 && lane < n->count) ? ((const PHIP_GLB uint32_t *)n->aux)[lane] : 0u;
+  return contig_scan_any(w, B, k, LO, SPAN, n->set_mask, myw, n->exclusive != 0) & valid;
+}
+
+// The operand stack is a shift register (s0 = top): a push / pop is a handful of v_mov, not a scalar branch
+// tree on the stack pointer -- the interpreter's SALU / branch count per tile is what bounds this path.
+__device__ __forceinline__ uint32_t eval_filter_contig(cseg_t &seg, cnode_t *__restrict__ nodes, uint32_t valid,
+                                                       const Tile &t, uint32_t &scanned) {
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
+  int i = seg.node_begin;
+  const int end = seg.node_end;
+  while (i < end) {
+    cnode_t *n = nodes + i;
+    const int op = n->op;
+    if (op == DOP_LEAF) {
+      const int sk = n->skip_kind;
+      if (sk != SKIP_NONE) {
+        const bool decided = (sk == SKIP_IF_NONE) ? (ballot(s0 != 0) == 0) : (ballot(s0 != valid) == 0);
+        if (decided) {
+          i = n->skip_to;
+          continue;
+        }
+      }
+      const uint32_t v = eval_leaf_contig(seg, n, valid, t, scanned);
+      s5 = s4;
+      s4 = s3;
+      s3 = s2;
+      s2 = s1;
+      s1 = s0;
+      s0 = v;
+    } else if (op == DOP_NOT) {
+      s0 = valid & ~s0;
+    } else {
+      s0 = op == DOP_AND ? (s0 & s1) : (s0 | s1);
+      s1 = s2;
+      s2 = s3;
+      s3 = s4;
+      s4 = s5;
+    }
+    i++;
+  }
+  return s0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // conjunctive fast path: AND of staged scan leaves, each a width-specialised loop.
 //
@@ -388,9 +600,6 @@ __device__ __forceinline__ uint32_t conj_set(const PHIP_LDS uint32_t *wl, uint32
   return r;
 }
 
-#define PHIP_B_CASES(X) \
-  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
-  X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
 
 // The lane's first word and window shift are computed once from the runtime width, so the
 // specialisations share them instead of each hoisting its own copy out of the tile loop.
@@ -838,6 +1047,9 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
         mask &= lo <= hi ? range_word(lo, hi, lane) : 0u;
       }
       scanned_t = (uint32_t)seg.conj * (uint32_t)tl.valid_docs;
+    } else if (seg.contig) {
+      mask = eval_filter_contig(seg, nodes, contig_valid(tl.valid_docs, lane), tl, scanned_t);
+      if (st) mask = contig_to_lane_major(mask);  // (popcounts do not care about the layout)
     } else {
       mask = seg.node_end > seg.node_begin ? eval_filter(seg, nodes, valid, tl, scanned_t) : valid;
     }

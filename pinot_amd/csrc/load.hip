@@ -1,4 +1,5 @@
 // load.hip -- one-time layout transforms at segment load (phip_segment_load, runtime.cpp).
+#include "codec.h"
 #include "dev_common.h"
 
 namespace phip {
@@ -214,14 +215,31 @@ __device__ __forceinline__ int decode_chunk(const uint8_t *__restrict__ in, int 
   return op;
 }
 
+// Entropy-coded chunks (ZSTANDARD = 2, GZIP = 5; codec.h): the serial decode runs on lane 0 over the LDS copy of
+// the chunk into the LDS output (workspace and the zstd literal buffer in LDS too); the wave then stores the
+// chunk with the same fused BE->LE swap.
+template <int kCodec>
+__device__ __forceinline__ int decode_entropy(const uint8_t *in, int n, uint8_t *out, int usize, uint8_t *ws,
+                                              uint8_t *lits, int lane) {
+  __shared__ int32_t got_s;
+  if (lane == 0) {
+    got_s = kCodec == 5 ? codec::pinot_gzip_chunk(in, n, out, usize, ws)
+                        : codec::zstd_decompress(in, n, out, usize, lits, usize, ws);
+  }
+  __syncthreads();
+  return got_s;
+}
+
 template <int kCodec, int kEntry>
 __global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restrict__ blob,
                                                           const RawChunk *__restrict__ chunks, int32_t nchunks,
-                                                          int32_t out_cap, uint8_t *__restrict__ out,
+                                                          int32_t out_cap, int32_t in_cap, uint8_t *__restrict__ out,
                                                           int32_t *__restrict__ err) {
   extern __shared__ __align__(16) uint8_t lds[];
   uint8_t *lout = lds;
   uint8_t *lin = lds + out_cap;
+  uint8_t *lws = lin + in_cap;                                            // codec workspace (GZIP / ZSTANDARD)
+  uint8_t *llits = lws + (kCodec == 2 ? ((codec::kZstdWs + 15) & ~15) : 0);  // zstd literals (out_cap bytes)
   const int lane = threadIdx.x;
   for (int32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const uint64_t src = chunks[c].src, dst = chunks[c].dst;
@@ -233,7 +251,9 @@ __global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restr
     __syncthreads();
     const uint8_t *in = lin + head;
     int n = csize, got;
-    if (kCodec == 4) {
+    if (kCodec == 2 || kCodec == 5) {
+      got = decode_entropy<kCodec>(in, n, lout, usize, lws, llits, lane);
+    } else if (kCodec == 4) {
       int want = n < 4 ? -2 : (int)(lds_byte(in, 0) | (lds_byte(in, 1) << 8) | (lds_byte(in, 2) << 16) | (lds_byte(in, 3) << 24));
       got = n < 4 ? -1 : decode_chunk<3>(in + 4, n - 4, lout, usize, lane);
       if (got != want) got = -1;
@@ -259,7 +279,8 @@ __global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restr
 
 template <int kCodec>
 static hipError_t launch_chunk_decode_codec(int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
-                                            int32_t out_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s) {
+                                            int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err,
+                                            hipStream_t s) {
   const int grid = nchunks < (1 << 20) ? nchunks : (1 << 20);
   if (lds > 65536) {  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
     hipError_t e = hipFuncSetAttribute(entry == 8 ? (const void *)chunk_decode_kernel<kCodec, 8>
@@ -268,19 +289,28 @@ static hipError_t launch_chunk_decode_codec(int entry, const uint8_t *blob, cons
     if (e != hipSuccess) return e;
   }
   if (entry == 8)
-    chunk_decode_kernel<kCodec, 8><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, out, err);
+    chunk_decode_kernel<kCodec, 8><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, in_cap, out, err);
   else
-    chunk_decode_kernel<kCodec, 4><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, out, err);
+    chunk_decode_kernel<kCodec, 4><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, in_cap, out, err);
   return hipGetLastError();
 }
 
+// LDS bytes of the codec's workspace beyond the output and input windows
+size_t chunk_decode_extra_lds(int codec, int32_t out_cap) {
+  if (codec == 5) return (size_t)((codec::kInflateWs + 15) & ~15);
+  if (codec == 2) return (size_t)((codec::kZstdWs + 15) & ~15) + (size_t)out_cap;
+  return 0;
+}
+
 hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
-                               int32_t out_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s) {
+                               int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
   switch (codec) {
-    case 1: return launch_chunk_decode_codec<1>(entry, blob, chunks, nchunks, out_cap, lds, out, err, s);
-    case 3: return launch_chunk_decode_codec<3>(entry, blob, chunks, nchunks, out_cap, lds, out, err, s);
-    case 4: return launch_chunk_decode_codec<4>(entry, blob, chunks, nchunks, out_cap, lds, out, err, s);
+    case 1: return launch_chunk_decode_codec<1>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
+    case 2: return launch_chunk_decode_codec<2>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
+    case 3: return launch_chunk_decode_codec<3>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
+    case 4: return launch_chunk_decode_codec<4>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
+    case 5: return launch_chunk_decode_codec<5>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
     default: return hipErrorInvalidValue;
   }
 }

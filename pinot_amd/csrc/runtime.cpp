@@ -41,7 +41,8 @@ hipError_t launch_trim_gather(const int32_t *order, int64_t k, int32_t naggs, in
                               const double *vals, const int64_t *longs, const uint8_t *hll, int64_t *keys_out,
                               double *vals_out, int64_t *longs_out, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
-                               int32_t out_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s);
+                               int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s);
+size_t chunk_decode_extra_lds(int codec, int32_t out_cap);
 hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32_t *ids_tmp, int64_t n, int32_t bits,
                                    uint32_t *words, int64_t nwords, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
@@ -574,11 +575,10 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
       comp = (int32_t)be32(h + 20);
       data_hdr = (int32_t)be32(h + 24);
     }  // v1: 4-int header, SNAPPY chunks, int offsets from byte 16
-    // ChunkCompressionType (ChunkCompressionType.java:22): PASS_THROUGH 0, SNAPPY 1, LZ4 3, LZ4_LENGTH_PREFIXED 4
-    // are decoded on the GPU; ZSTANDARD 2 and GZIP 5 (entropy-coded) stay on the Java path.
-    if (comp != 0 && comp != 1 && comp != 3 && comp != 4)
-      return fail(PHIP_ERR_UNSUPPORTED, "column %s: chunk compression type %d (ZSTANDARD/GZIP) is not on the GPU path",
-                  c.name, comp);
+    // ChunkCompressionType (ChunkCompressionType.java:22): PASS_THROUGH 0, SNAPPY 1, ZSTANDARD 2, LZ4 3,
+    // LZ4_LENGTH_PREFIXED 4, GZIP 5 -- all decoded on the GPU at load (load.hip, codec.h)
+    if (comp < 0 || comp > 5)
+      return fail(PHIP_ERR_INVALID, "column %s: unknown chunk compression type %d", c.name, comp);
     if (entry != type_width(c.data_type) || total != n || per_chunk <= 0 ||
         num_chunks != ceil_div(n, per_chunk) || (version < 1 || version > 3))
       return fail(PHIP_ERR_INVALID, "column %s: bad chunk header", c.name);
@@ -620,7 +620,8 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
         max_u = std::max(max_u, chunks[k].usize);
       }
       const uint32_t out_cap = (uint32_t)round_up(max_u, 16);
-      const size_t lds = out_cap + round_up(max_c + 8, 16);
+      const uint32_t in_cap = (uint32_t)round_up(max_c + 8, 16);
+      const size_t lds = out_cap + in_cap + chunk_decode_extra_lds(comp, (int32_t)out_cap);
       if (lds > 163840 - 1024)
         return fail(PHIP_ERR_UNSUPPORTED, "column %s: chunks of %u -> %u bytes exceed the 159 KiB LDS decode window",
                     c.name, max_c, max_u);
@@ -636,7 +637,7 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
       HIP_TRY(hipMemcpyAsync(blob, h + first, blob_bytes, hipMemcpyHostToDevice, st));
       HIP_TRY(hipMemcpyAsync(table, chunks.data(), sizeof(RawChunk) * num_chunks, hipMemcpyHostToDevice, st));
       HIP_TRY(launch_chunk_decode(comp, entry, (const uint8_t *)blob, (const RawChunk *)table, num_chunks,
-                                  (int32_t)out_cap, lds, (uint8_t *)p, (int32_t *)err, st));
+                                  (int32_t)out_cap, (int32_t)in_cap, lds, (uint8_t *)p, (int32_t *)err, st));
       int32_t bad = 0;
       HIP_TRY(hipMemcpyAsync(&bad, err, 4, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
@@ -1697,6 +1698,29 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         while (ds.conj_p > 1 && ds.conj_p * conj[i].second.bits > 32) ds.conj_p >>= 1;
       }
       if (const char *e = getenv("PHIP_CONJ_P")) ds.conj_p = std::min(ds.conj_p, std::max(1, atoi(e)));  // measurement override
+    }
+    // general programs whose leaves are all staged (or need no tile data) run in the contiguous layout
+    // (filter.hip eval_filter_contig): inverted leaves become one LDS read, scan leaves one register block
+    ds.contig = 0;
+    if (!ds.conj_path && ds.node_end > ds.node_begin) {
+      bool c = true;
+      for (int i = ds.node_begin; i < ds.node_end && c; i++) {
+        const DevNode &dn = nodes[i];
+        if (dn.op != DOP_LEAF) continue;
+        switch (dn.leaf_kind) {
+          case PHIP_LEAF_MATCH_ALL:
+          case PHIP_LEAF_MATCH_NONE:
+          case PHIP_LEAF_DOC_RANGES: break;
+          case PHIP_LEAF_INVERTED: c = dn.lds_off >= 0; break;
+          case PHIP_LEAF_DICT_RANGE: c = dn.lds_off >= 0 && dn.bits >= 1 && dn.bits <= 31; break;
+          case PHIP_LEAF_DICT_SET:
+            c = dn.lds_off >= 0 && dn.bits >= 1 && dn.bits <= 31 && (dn.small_set || (dn.count > 0 && dn.count <= 64));
+            break;
+          default: c = false;
+        }
+      }
+      const char *ce = getenv("PHIP_CONTIG");  // measurement override: "0" keeps the lane-major interpreter
+      ds.contig = c && !(ce && ce[0] == '0') ? 1 : 0;
     }
     seg_off[&ds - dsegs.data()] = off;
   }

@@ -162,10 +162,10 @@ CHUNK_COMPRESSION = {"PASS_THROUGH": 0, "SNAPPY": 1, "ZSTANDARD": 2, "LZ4": 3, "
 
 def _compress_chunk(chunk: bytes, codec: int) -> bytes:
     """One chunk through the codec Pinot's writer uses (BaseChunkForwardIndexWriter.writeChunk,
-    BaseChunkForwardIndexWriter.java:175-200). The reference binds lz4-java / snappy-java; here the
-    same published block formats come from Arrow's bundled liblz4 / libsnappy ("lz4_raw" = LZ4 block
-    format without a frame). LZ4_LENGTH_PREFIXED prepends the 4-byte little-endian original length
-    (lz4-java LZ4CompressorWithLength)."""
+    BaseChunkForwardIndexWriter.java:175-200). The reference binds lz4-java / snappy-java / zstd-jni /
+    java.util.zip; here the same published formats come from Arrow's bundled liblz4 / libsnappy / libzstd
+    ("lz4_raw" = LZ4 block format without a frame) and Python's zlib (the library java.util.zip wraps).
+    LZ4_LENGTH_PREFIXED prepends the 4-byte little-endian original length (lz4-java LZ4CompressorWithLength)."""
     import pyarrow as pa
     if codec == 0:
         return chunk
@@ -174,8 +174,11 @@ def _compress_chunk(chunk: bytes, codec: int) -> bytes:
     if codec in (3, 4):
         body = pa.compress(chunk, codec="lz4_raw", asbytes=True)
         return (len(chunk).to_bytes(4, "little") + body) if codec == 4 else body
-    if codec == 2:
-        return pa.compress(chunk, codec="zstd", asbytes=True)
+    if codec == 2:  # zstd-jni Zstd.compress: one frame at the default level 3 (ZstandardCompressor.java)
+        return pa.Codec("zstd", compression_level=3).compress(chunk, asbytes=True)
+    if codec == 5:  # GzipCompressor.java:38-46: java.util.zip.Deflater (zlib, default level) + 4-byte BE length
+        import zlib
+        return zlib.compress(chunk) + len(chunk).to_bytes(4, "big")
     raise NotImplementedError(f"chunk compression {codec}")
 
 

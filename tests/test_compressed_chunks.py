@@ -21,6 +21,7 @@ from pinot_amd.segment.creator import CHUNK_COMPRESSION, SegmentCreator, _compre
 from pinot_amd.spi import DataType
 
 CODECS = ("SNAPPY", "LZ4", "LZ4_LENGTH_PREFIXED")
+ENTROPY = ("ZSTANDARD", "GZIP")  # decoded by pinot_amd/csrc/codec.h (tests/test_codec.py pins it on the host)
 
 
 def _payloads():
@@ -98,7 +99,7 @@ def _segment(n, codec, seed=3, docs_per_chunk=1000, version=3):
     return c.build(), c._cols
 
 
-@pytest.mark.parametrize("codec", CODECS + ("PASS_THROUGH",))
+@pytest.mark.parametrize("codec", CODECS + ENTROPY + ("PASS_THROUGH",))
 @pytest.mark.parametrize("docs_per_chunk,version", [(1000, 3), (7, 2), (4096, 3)])
 def test_oracle_reads_compressed_segment(codec, docs_per_chunk, version):
     n = 10_007
@@ -123,7 +124,7 @@ QUERIES = (
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("codec", CODECS)
+@pytest.mark.parametrize("codec", CODECS + ENTROPY)
 def test_gpu_compressed_raw_columns(gpu_lib, codec):
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     from pinot_amd.engine.segment import GpuSegment
@@ -193,7 +194,14 @@ def test_gpu_rejects_malformed_and_unsupported_chunks(gpu_lib):
     seg.columns["M"].forward = bytes(fwd)
     with pytest.raises(_lib.PhipError, match="malformed compressed chunk"):
         GpuSegment(seg)
-    z = SegmentCreator("zstd", no_dictionary_columns=["M"], raw_compression={"M": "ZSTANDARD"})
-    z.add_column("M", DataType.LONG, rng.integers(0, 3, n))
-    with pytest.raises(_lib.PhipError, match="not on the GPU path"):
-        GpuSegment(z.build())
+    for codec in ENTROPY:  # a flipped byte in the last chunk: libzstd / zlib would throw, so the load fails
+        z = SegmentCreator(codec, no_dictionary_columns=["M"], raw_compression={"M": codec})
+        z.add_column("M", DataType.LONG, rng.integers(0, 3, n))
+        zs = z.build()
+        f = bytearray(zs.columns["M"].forward)
+        nchunks = int.from_bytes(f[4:8], "big")
+        last = int.from_bytes(f[28 + 8 * (nchunks - 1):28 + 8 * nchunks], "big")  # v3: long offsets
+        f[last] ^= 0x5A  # the last chunk's zstd magic / zlib CMF byte
+        zs.columns["M"].forward = bytes(f)
+        with pytest.raises(_lib.PhipError, match="malformed compressed chunk"):
+            GpuSegment(zs)
