@@ -83,7 +83,10 @@ struct StageSrc {
 };
 
 // A leaf of a conjunctive filter program (fast path): a staged scan of one fixed-bit column.
-constexpr int kMaxConj = 6;
+#ifndef PHIP_MAX_CONJ
+#define PHIP_MAX_CONJ 6  // (A/B builds override it)
+#endif
+constexpr int kMaxConj = PHIP_MAX_CONJ;
 constexpr int kConjSparseMax = 6;     // default per-lane bound of the sparse conjunction walk
 struct ConjLeaf {
   int32_t lds_off;  // staged region in the ring slot
