@@ -1239,6 +1239,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
 
   // group-by key space
   const bool group_by = q->num_group_by > 0;
+  int64_t gb_key_space = 0;
+  bool gb_force_hash = false;
   std::vector<std::shared_ptr<Device::Remap>> gb_dicts;
   std::vector<std::vector<int32_t *>> gb_remap_dev;  // [k][seg]
   if (group_by) {
@@ -1266,6 +1268,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     for (int s = 0; s < nseg; s++) docs += segs[s]->num_docs;
     const char *hm = getenv("PHIP_GB_HASH");  // measurement override: "1" forces the hash table
     const bool force_hash = hm && atoi(hm) != 0;
+    gb_key_space = stride;
+    gb_force_hash = force_hash;
     if (force_hash || stride > ((int64_t)1 << 26) || (stride > ((int64_t)1 << 22) && stride > 4 * docs)) {
       const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(stride, docs));
       int64_t cap = 1024;
@@ -1530,6 +1534,24 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   }
   if (total_work > INT32_MAX / 2) return fail(PHIP_ERR_UNSUPPORTED, "too many tiles in one query");
   dq.total_work = (int32_t)total_work;
+  if (group_by && gb_key_space > ((int64_t)1 << 22)) {
+    // Re-size a large group table from the docs of the work tiles (sorted-index pruning already cut them):
+    // only those docs can create groups, and the table is cleared and compacted on every execution
+    // (BenchmarkQueries STARTREE_FILTER_QUERY: one candidate tile, yet 2 x 10M hash slots before).
+    const int64_t work_docs = std::max<int64_t>(1, total_work * (int64_t)kTileDocs);
+    if (gb_force_hash || gb_key_space > ((int64_t)1 << 26) || gb_key_space > 4 * work_docs) {
+      const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(gb_key_space, work_docs));
+      int64_t cap = 1024;
+      while (cap < 2 * bound) cap <<= 1;
+      if (dq.mode != GB_HASH || cap < dq.num_groups) {
+        const int64_t per_slot = 8 + 8 * (1 + (int64_t)naggs);
+        if (cap * per_slot > ((int64_t)24 << 30))
+          return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table of %lld slots exceeds the memory budget", (long long)cap);
+        dq.num_groups = cap;
+        dq.mode = GB_HASH;
+      }
+    }
+  }
   dq.num_segs = (int32_t)dsegs.size();
   const size_t segs_off = blob.reserve(sizeof(DevSeg) * std::max<size_t>(dsegs.size(), 1));
 

@@ -630,17 +630,11 @@ def _dictionary_values(dv):
 
 
 def _run_parts(parts):
-    """Runs the per-info operators of a filtered query concurrently: each takes its own execution lane (HIP stream
-    + workspace) in the library, and ctypes releases the GIL for the call, so the infos' launches overlap instead
-    of queueing one behind another (the reference runs its infos one after another on one thread; the results
-    are the same). Returns the blocks in info order."""
-    if len(parts) <= 1:
-        return [op.next_block() for _, op in parts]
-    from concurrent.futures import ThreadPoolExecutor
-    for _, op in parts:  # plan preparation takes the device mutex: do it up front, in order
-        op.run_raw(prepare_only=True) if hasattr(op, "run_raw") else None
-    with ThreadPoolExecutor(max_workers=min(len(parts), 8)) as ex:
-        return list(ex.map(lambda p: p[1].next_block(), parts))
+    """The per-info operators of a filtered query, in info order (FilteredAggregationOperator runs its infos one
+    after another too). Running them on concurrent execution lanes from a thread pool was measured slower on C1
+    FILTERED_MIXED (0.48 -> 0.56 ms p50, profiles/r02c_configs_c1.jsonl): each info's device work is ~50 us and the
+    host side of an execution does not overlap under the GIL."""
+    return [op.next_block() for _, op in parts]
 
 
 class GpuFilteredAggregationOperator:

@@ -140,6 +140,29 @@ def _matching_dict_ids(seg, composites):
     return set(np.flatnonzero(acc).tolist())
 
 
+class _Bulk:
+    """All non-star children of one node, when each is a one-record leaf (see traverse)."""
+
+    def __init__(self, parent):
+        self.dimension_id = parent.child_dimension_id
+        self.start, self.end = parent.start_doc, parent.end_doc  # the non-star children tile the node's range
+
+
+def _bulk_leaves(node):
+    """Cached per node: every non-star child is a leaf holding exactly one record (then the children's
+    records are the contiguous range of the node's original records)."""
+    flag = getattr(node, "_bulk", None)
+    if flag is None:
+        kids = [c for v, c in node.children.items() if v != ALL]
+        flag = len(kids) > 64 and all(c.is_leaf and c.end_doc - c.start_doc == 1 for c in kids)
+        if flag:
+            lo = min(c.start_doc for c in kids)
+            hi = max(c.end_doc for c in kids)
+            flag = hi - lo == len(kids)
+        node._bulk = flag
+    return flag
+
+
 def traverse(tree, seg, pmap, group_by_columns):
     """StarTreeFilterOperator.traverseStarTree (BFS). Returns (inclusive doc ranges as a flat int32 array,
     remaining predicate columns) or None when a predicate column has no matching dictionary id."""
@@ -164,6 +187,10 @@ def traverse(tree, seg, pmap, group_by_columns):
                 global_remaining = set(remaining_pred)
             matching = None
             current_dim = dim_id
+        if isinstance(node, _Bulk):
+            starts.append(node.start)
+            ends.append(node.end)
+            continue
         if not remaining_pred and not remaining_gb:
             starts.append(node.aggregated_doc)
             ends.append(node.aggregated_doc + 1)
@@ -176,7 +203,6 @@ def traverse(tree, seg, pmap, group_by_columns):
         star = None
         if (global_remaining is None or child_dim not in global_remaining) and child_dim not in remaining_gb:
             star = node.children.get(ALL)
-        children = sorted(node.children.items())  # serialized order: by dimension value, ALL (-1) first
         if child_dim in remaining_pred:
             if matching is None:
                 matching = _matching_dict_ids(seg, pmap[child_dim])
@@ -184,6 +210,7 @@ def traverse(tree, seg, pmap, group_by_columns):
                     return None
             nchildren = len(node.children)
             if len(matching) * USE_SCAN_TO_TRAVERSE_NODES_THRESHOLD > nchildren:
+                children = sorted(node.children.items())  # serialized order: by dimension value, ALL (-1) first
                 if star is not None and len(matching) >= nchildren - 1:
                     hits = [c for v, c in children if v in matching]
                     if len(hits) == nchildren - 1:
@@ -207,8 +234,13 @@ def traverse(tree, seg, pmap, group_by_columns):
             if star is not None:
                 queue.append(star)
                 found_leaf |= star.is_leaf
+            elif _bulk_leaves(node):
+                # every non-star child is a one-record leaf: they tile the node's record range, and each would
+                # add its own record (as its range or as its aggregated doc) -- one range, not one node per value
+                queue.append(_Bulk(node))
+                found_leaf = True
             else:
-                for v, c in children:
+                for v, c in sorted(node.children.items()):
                     if v != ALL:
                         queue.append(c)
                         found_leaf |= c.is_leaf

@@ -181,6 +181,8 @@ class _Builder:
             self.num_nodes += 1
             children[int(vals[a])] = TreeNode(child_dim, int(vals[a]), start + int(a), start + int(b))
         node.children = children
+        # one-record leaves tiling the node's range (the traversal then takes them as one range)
+        node._bulk = len(children) > 64 and bool(np.all(np.diff(bounds) == 1))
         if child_dim not in self.skip and len(children) > 1:
             children[ALL] = self._star_node(start, end, child_dim)
         for child in list(children.values()):

@@ -5,8 +5,9 @@ Schema and table config follow pinot-perf/src/main/java/org/apache/pinot/perf/Be
 (dictionary, no index), RAW_INT_COL (no dictionary: PASS_THROUGH raw chunks), LOW_CARDINALITY_STRING_COL
 ("value" + i % 10, inverted index). Values come from Distribution EXP(lambda) over java.util.Random(42)
 (tools/bqgen.c restates both). RAW_STRING_COL / NO_INDEX_STRING_COL (random UUIDs) and TSTMP_COL are
-not generated: no query of the GPU subset reads them. The star-tree and range indexes of the reference
-table config are not built (star-tree is out of scope; the range index is an
+not generated: no query of the GPU subset reads them. The reference table's star-tree (split order SORTED_COL,
+INT_COL; SUM__RAW_INT_COL; maxLeafRecords Integer.MAX_VALUE, :99-104) is built with ``star_tree=True`` (the
+STARTREE_* queries then take the star-tree path, as in the reference benchmark); the range index is not (an
 alternative to the scan leaf with identical results).
 """
 import ctypes
@@ -100,14 +101,18 @@ def generate(num_rows: int, num_segments: int, scenario: str = "EXP(0.001)", see
     return out
 
 
-def make_segments(num_rows: int, num_segments: int = 1, scenario: str = "EXP(0.001)", seed: int = 42):
+def make_segments(num_rows: int, num_segments: int = 1, scenario: str = "EXP(0.001)", seed: int = 42,
+                  star_tree: bool = False):
     from pinot_amd.segment.creator import SegmentCreator
+    from pinot_amd.segment.startree import StarTreeIndexConfig
     from pinot_amd.spi import DataType
+    st = [StarTreeIndexConfig(["SORTED_COL", "INT_COL"], ["SUM__RAW_INT_COL"], max_leaf_records=2 ** 31 - 1)] \
+        if star_tree else []
     low = np.array([f"value{i}" for i in range(10)])
     segs = []
     for k, cols in enumerate(generate(num_rows, num_segments, scenario, seed)):
         c = SegmentCreator(f"testSegment{k}", inverted_index_columns=["INT_COL", "LOW_CARDINALITY_STRING_COL"],
-                           no_dictionary_columns=["RAW_INT_COL"])
+                           no_dictionary_columns=["RAW_INT_COL"], star_tree_configs=st)
         c.add_column("SORTED_COL", DataType.INT, num_rows - np.arange(num_rows, dtype=np.int64))
         c.add_column("INT_COL", DataType.INT, cols["INT_COL"])
         c.add_column("NO_INDEX_INT_COL", DataType.INT, cols["NO_INDEX_INT_COL"])

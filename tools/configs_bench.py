@@ -82,23 +82,27 @@ def alg_bytes(qc, raws):
 
 
 def time_gpu(qc, gsegs, reps, warmup):
+    """p50 wall (ms), and per-kernel device time + library-reported algorithmic bytes (phip_result filter_* /
+    agg_*; SURVEY.md §8d restated per launch, as bench.py reports them)."""
     from pinot_amd import _lib
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     lib = _lib.load()
     op = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, gsegs)
-    wall, kern, dev = [], [], []
+    wall, kern, dev, fk, ak = [], [], [], [], []
+    fb = ab = 0
     ngroups = None
-    if not hasattr(op, "run_raw"):  # FILTER(WHERE) aggregations: several prepared plans per block
+    if not hasattr(op, "run_raw"):  # FILTER / CASE / star-tree operators: several plans per block
         for i in range(warmup + reps):
             t0 = time.perf_counter()
             blk = op.next_block()
             t1 = time.perf_counter()
             if i >= warmup:
                 wall.append((t1 - t0) * 1e3)
-                kern.append(blk.scan_kernel_ms)
-                dev.append(blk.device_ms)
+                kern.append(getattr(blk, "scan_kernel_ms", 0.0) or 0.0)
+                dev.append(getattr(blk, "device_ms", 0.0) or 0.0)
         op.close()
-        return float(np.median(wall)), float(np.median(kern)), float(np.median(dev)), blk.stats.num_docs_scanned, None
+        return (float(np.median(wall)), float(np.median(kern)), float(np.median(dev)), blk.stats.num_docs_scanned,
+                None, None)
     for i in range(warmup + reps):
         t0 = time.perf_counter()
         res = op.run_raw()
@@ -108,11 +112,19 @@ def time_gpu(qc, gsegs, reps, warmup):
             wall.append((t1 - t0) * 1e3)
             kern.append(r.scan_kernel_ms)
             dev.append(r.device_ms)
+            fk.append(r.filter_kernel_ms)
+            ak.append(r.agg_kernel_ms)
+        fb, ab = int(r.filter_bytes), int(r.agg_bytes)
         ngroups = r.num_groups
         docs = r.num_docs_scanned
         lib.phip_result_free(res)
     op.close()
-    return float(np.median(wall)), float(np.median(kern)), float(np.median(dev)), docs, ngroups
+    per = {}
+    for name, ms, b in (("filter_kernel", float(np.mean(fk)), fb), ("agg_kernel", float(np.mean(ak)), ab)):
+        if ms > 0:
+            per[name] = {"ms": round(ms, 4), "alg_bytes": b, "GBps": round(b / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    return float(np.median(wall)), float(np.median(kern)), float(np.median(dev)), docs, ngroups, per
 
 
 def time_cpu(qc, raws, budget_s=10.0):
@@ -131,13 +143,16 @@ def time_cpu(qc, raws, budget_s=10.0):
 
 def emit(cfg, name, qc, raws_meta, gsegs, args, cpu_raws=None, note=None):
     total_docs = sum(s.num_docs for s in gsegs)
-    wall, kern, dev, docs, ng = time_gpu(qc, gsegs, args.reps, args.warmup)
+    wall, kern, dev, docs, ng, per = time_gpu(qc, gsegs, args.reps, args.warmup)
     b = alg_bytes(qc, raws_meta)
+    # roofline: the dominant kernel's own algorithmic bytes over its time (never above 1 by construction of the
+    # per-launch bytes); the whole-query figure is kept as query_alg_bytes for reference
+    dom = max(per, key=lambda k: per[k]["ms"]) if per else None
     out = {"config": cfg, "query": name, "rows": total_docs, "p50_ms": round(wall, 4), "kernel_ms": round(kern, 4),
            "device_ms": round(dev, 4), "G_rows_per_s": round(total_docs / (wall * 1e-3) / 1e9, 2),
            "docs_matched": int(docs), "groups": int(ng) if qc.group_by else None,
-           "alg_bytes": int(b), "alg_GBps": round(b / (kern * 1e-3) / 1e9, 1) if kern > 0 else None,
-           "hbm_frac": round(b / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kern > 0 else None}
+           "query_alg_bytes": int(b), "kernels": per, "dominant_kernel": dom,
+           "hbm_frac": per[dom]["frac"] if dom else None}
     if cpu_raws is not None and not args.no_cpu:
         v, ms = time_cpu(qc, cpu_raws)
         out["cpu_oracle"] = {"G_rows_per_s": round(v, 4), "ms_per_query": round(ms, 1), "cores": 1,
@@ -156,7 +171,7 @@ def run_c1(args):
     from pinot_amd.engine.segment import GpuSegment
     from pinot_amd.query.sql import parse
     from tools import bq
-    raws = bq.make_segments(args.c1_rows, 1, args.c1_scenario)
+    raws = bq.make_segments(args.c1_rows, 1, args.c1_scenario, star_tree=True)  # the reference table config
     gsegs = [GpuSegment(r) for r in raws]
     for name, sql in bq.QUERIES.items():
         qc = parse(sql)
