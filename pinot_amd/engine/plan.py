@@ -596,14 +596,14 @@ class GpuCombineOperator:
             else:
                 nk = r.num_group_by
                 keys = np.ctypeslib.as_array(r.group_keys, shape=(max(ng * nk, 1),))[:ng * nk].reshape(ng, nk) if ng else np.zeros((0, nk), np.int32)
-                dicts = []
+                cols = []  # per group-by column: the values of the groups' keys (only the ids that occur)
                 for k in range(nk):
                     dv = _lib.DictionaryView()
                     _lib.check(lib.phip_result_dictionary(res, k, ctypes.byref(dv)))
-                    dicts.append(_dictionary_values(dv))
+                    cols.append(_dictionary_lookup(dv, keys[:, k]) if ng else [])
                 groups = {}
                 for g in range(ng):
-                    key = tuple(dicts[k][keys[g, k]] for k in range(nk))
+                    key = tuple(cols[k][g] for k in range(nk))
                     groups[key] = intermediates(g)
                 blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
                                           bool(r.num_groups_limit_reached))
@@ -617,16 +617,19 @@ class GpuCombineOperator:
             lib.phip_result_free(res)
 
 
-def _dictionary_values(dv):
+def _dictionary_lookup(dv, ids):
+    """Values of the dictionary entries `ids` (a result's group keys), without converting the whole dictionary."""
+    ids = np.asarray(ids, dtype=np.int64)
     card = dv.cardinality
     t = DataType(dv.data_type)
     if t == DataType.STRING:
         w = dv.string_width
-        raw = ctypes.string_at(dv.values, card * w)
-        return [raw[i * w:(i + 1) * w].rstrip(b"\0").decode("utf-8") for i in range(card)]
+        raw = np.ctypeslib.as_array(ctypes.cast(dv.values, ctypes.POINTER(ctypes.c_uint8)), shape=(card * w,))
+        rows = raw.reshape(card, w)[ids]
+        return [bytes(r).rstrip(b"\0").decode("utf-8") for r in rows]
     dt = {DataType.INT: np.int32, DataType.LONG: np.int64, DataType.FLOAT: np.float32, DataType.DOUBLE: np.float64}[t]
     arr = np.ctypeslib.as_array(ctypes.cast(dv.values, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(card,))
-    return [x.item() for x in arr]
+    return arr[ids].tolist()
 
 
 def _run_parts(parts):

@@ -88,6 +88,8 @@ def time_gpu(qc, gsegs, reps, warmup):
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     lib = _lib.load()
     op = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, gsegs)
+    if hasattr(op, "inner") and hasattr(op.inner, "run_raw"):
+        op = op.inner  # star-tree: the traversal is plan-time; time the prepared plan over the star-tree docs
     wall, kern, dev, fk, ak = [], [], [], [], []
     fb = ab = 0
     ngroups = None
@@ -100,9 +102,18 @@ def time_gpu(qc, gsegs, reps, warmup):
                 wall.append((t1 - t0) * 1e3)
                 kern.append(getattr(blk, "scan_kernel_ms", 0.0) or 0.0)
                 dev.append(getattr(blk, "device_ms", 0.0) or 0.0)
+                fk.append(getattr(blk, "filter_kernel_ms", 0.0) or 0.0)
+                ak.append(getattr(blk, "agg_kernel_ms", 0.0) or 0.0)
+        fb, ab = int(getattr(blk, "filter_bytes", 0) or 0), int(getattr(blk, "agg_bytes", 0) or 0)
         op.close()
+        ng = len(blk.groups) if hasattr(blk, "groups") else None
+        per = {}
+        for name, ms, b in (("filter_kernel", float(np.mean(fk)), fb), ("agg_kernel", float(np.mean(ak)), ab)):
+            if ms > 0:
+                per[name] = {"ms": round(ms, 4), "alg_bytes": b, "GBps": round(b / (ms * 1e-3) / 1e9, 1),
+                             "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         return (float(np.median(wall)), float(np.median(kern)), float(np.median(dev)), blk.stats.num_docs_scanned,
-                None, None)
+                ng, per)
     for i in range(warmup + reps):
         t0 = time.perf_counter()
         res = op.run_raw()
@@ -150,7 +161,8 @@ def emit(cfg, name, qc, raws_meta, gsegs, args, cpu_raws=None, note=None):
     dom = max(per, key=lambda k: per[k]["ms"]) if per else None
     out = {"config": cfg, "query": name, "rows": total_docs, "p50_ms": round(wall, 4), "kernel_ms": round(kern, 4),
            "device_ms": round(dev, 4), "G_rows_per_s": round(total_docs / (wall * 1e-3) / 1e9, 2),
-           "docs_matched": int(docs), "groups": int(ng) if qc.group_by else None,
+           "docs_matched": int(docs), "groups": int(ng) if qc.group_by and ng is not None else None,
+           "star_tree": bool(getattr(gsegs[0], "star_trees", None)) and name.startswith("STARTREE"),
            "query_alg_bytes": int(b), "kernels": per, "dominant_kernel": dom,
            "hbm_frac": per[dom]["frac"] if dom else None}
     if cpu_raws is not None and not args.no_cpu:
