@@ -147,7 +147,7 @@ typedef struct phip_aggregation {
   int32_t column_a; /* index into phip_query_desc.columns */
   int32_t column_b;
   int32_t log2m; /* HLL */
-  int32_t reserved;
+  int32_t program; /* filter program whose docs this aggregation reads (0 unless num_filter_programs > 1) */
 } phip_aggregation;
 
 typedef struct phip_query_desc {
@@ -155,7 +155,8 @@ typedef struct phip_query_desc {
   int32_t num_segments;
   const char *const *columns; /* column names; nodes/aggregations refer to them by index */
   const uint64_t *segments;   /* handles from phip_segment_load */
-  const int32_t *filter_offsets;          /* [num_segments+1] into filter_nodes; empty = match all */
+  const int32_t *filter_offsets;          /* [num_filter_programs * num_segments + 1] into filter_nodes: program p
+                                           * of segment s = [p * num_segments + s, + 1); empty = match all */
   const phip_filter_node *filter_nodes;
   int32_t num_aggregations;
   int32_t num_group_by;
@@ -180,7 +181,13 @@ typedef struct phip_query_desc {
    * fields above when > 0). The device sorts the groups by the whole list (stable; ties keep the lowest group key)
    * and keeps trim_size of them. */
   int32_t num_order_terms;
-  int32_t reserved1;
+  /* Filtered aggregations in one pass (FilteredAggregationOperator.java:67-113, one program per
+   * AggregationFunctionUtils.buildFilteredAggregationInfos info): when > 1, filter_offsets holds that many
+   * programs per segment, one filter launch evaluates all of them into one tile mask each, and one aggregation
+   * launch aggregates every function over its own program's docs (phip_aggregation.program). Statistics sum over
+   * the programs (numDocsScanned, entries scanned; a segment matched when any program matched). Aggregation only
+   * (no group-by), at most 8 programs. 0 or 1 = one program. */
+  int32_t num_filter_programs;
   const struct phip_order_term *order_terms;
 } phip_query_desc;
 

@@ -65,7 +65,7 @@ class FilterNode(ctypes.Structure):
 
 class Aggregation(ctypes.Structure):
     _fields_ = [("function", ctypes.c_int32), ("expr", ctypes.c_int32), ("column_a", ctypes.c_int32),
-                ("column_b", ctypes.c_int32), ("log2m", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("column_b", ctypes.c_int32), ("log2m", ctypes.c_int32), ("program", ctypes.c_int32)]
 
 
 class OrderTerm(ctypes.Structure):
@@ -85,7 +85,7 @@ class QueryDesc(ctypes.Structure):
                 ("order_by_aggregation", ctypes.c_int32), ("order_by_desc", ctypes.c_int32),
                 ("trim_size", ctypes.c_int64), ("num_order_by_keys", ctypes.c_int32), ("reserved0", ctypes.c_int32),
                 ("order_by_keys", ctypes.POINTER(ctypes.c_int32)),
-                ("num_order_terms", ctypes.c_int32), ("reserved1", ctypes.c_int32),
+                ("num_order_terms", ctypes.c_int32), ("num_filter_programs", ctypes.c_int32),
                 ("order_terms", ctypes.POINTER(OrderTerm))]
 
 

@@ -102,6 +102,7 @@ __device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc,
   for (int a = 0; a < NA; a++) {
     if (a >= q.num_aggs) break;
     cagg_t &ag = q.aggs[a];
+    if (ag.program != seg.program) continue;  // another filter program's function (wave-uniform)
     const int kind = ag.acc;
     if (kind == ACC_COUNT) {
       acc[a] += act ? 1ull : 0ull;

@@ -31,6 +31,7 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
   for (int a = 0; a < NA; a++) {
     if (a >= q.num_aggs) break;
     cagg_t &ag = q.aggs[a];
+    if (ag.program != seg.program) continue;  // another filter program's function (wave-uniform)
     const int kind = ag.acc;
     const int ka = staged ? q.stage_slot_a[a] : -1, kb = staged ? q.stage_slot_b[a] : -1;
     const int ja = ka < 0 ? 0 : ka, jb = kb < 0 ? 0 : kb;

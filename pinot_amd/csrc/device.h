@@ -7,6 +7,7 @@ namespace phip {
 
 constexpr int kMaxQueryColumns = 16;  // distinct columns one query may reference
 constexpr int kMaxAggs = 8;           // aggregation slots per query
+constexpr int kMaxPrograms = 8;       // filter programs per query (filtered aggregations in one pass)
 constexpr int kDenseMin = 640;        // default DevAggQuery::dense_min
 constexpr int kMaxFilterStack = 6;    // postfix evaluation stack depth (host rejects deeper programs)
 constexpr int kMaxGroupBy = 4;
@@ -109,7 +110,7 @@ struct DevSeg {
   int32_t node_begin;  // filter nodes [node_begin, node_end); empty = match all
   int32_t node_end;
   int32_t num_stage;
-  int32_t seg_index;   // index into the query's segment list (seg_matched)
+  int32_t seg_index;   // slot of seg_matched: program * num query segments + index into the query's segment list
   int32_t num_dma;     // LDS-DMA wave-instructions per tile (sum of ceil(stage bytes / 1 KiB))
   int32_t conj;        // > 0: the program is AND of `conj` staged scan leaves (conj_leaf, most selective
                        // first); the filter kernel evaluates it without the stack machine
@@ -124,6 +125,9 @@ struct DevSeg {
   int32_t conj_hi;      // boundary tiles are masked)
   int32_t contig;       // 1: general program evaluated in the contiguous layout (filter.hip eval_filter_contig);
                         // every leaf staged or tile-free (MATCH_*, DOC_RANGES)
+  int32_t program;      // filter program of this entry: a plan with k programs (filtered aggregations) holds one
+                        // entry per (segment, program), adjacent per segment; the aggregation kernel applies only
+                        // the functions of that program (DevAgg.program) to its docs
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
@@ -177,7 +181,7 @@ struct DevAgg {
   int32_t integral;  // expression evaluated in int64 (both inputs INT/LONG)
   int32_t hll_slot;  // ACC_HLL: index among HLL aggs
   int32_t log2m;
-  int32_t pad;
+  int32_t program;   // filter program whose docs it aggregates (DevSeg.program; multi-program plans)
 };
 
 // Aggregation / group-by kernel launch (K5-K9).

@@ -983,6 +983,9 @@ struct Plan {
   std::vector<RoaringTask> tasks;
   std::vector<std::shared_ptr<Device::Remap>> gb_dicts;
   int nseg = 0, naggs = 0, nhll = 0, log2m = 0, m_regs = 0, num_group_by = 0, num_projected = 0;
+  int nprog = 1;   // filter programs (phip_query_desc.num_filter_programs)
+  int nmatch = 0;  // seg_matched slots = nprog * nseg
+  std::vector<int64_t> slot_docs;  // per seg_matched slot: the docs of that (program, segment) entry, 0 = pruned
   int64_t num_groups_limit = 0, total_work = 0, total_docs = 0, docs_in_work = 0;
   int32_t order_agg = -1, order_desc = 0;  // server-level trim (phip_query_desc.order_by_aggregation)
   int32_t order_nkeys = 0;                 // > 0: ORDER BY group-by columns (order_keys)
@@ -993,7 +996,9 @@ struct Plan {
   std::vector<int64_t> seg_docs;  // num_docs per query segment
   struct ProjCol {
     std::vector<int32_t> bits, card, width;  // per query segment: fixed-bit width (0 = raw), dictionary
-  };                                         // entries, bytes per value / dictionary entry
+                                             // entries, bytes per value / dictionary entry
+    uint32_t progs = 1;                      // bit p: filter program p projects the column
+  };
   std::vector<ProjCol> proj;
   bool has_filter = false, need_agg = false, need_mask = false, group_by = false, conj_only = false;
   int fused_naggs = 0;  // > 0: the filter kernel aggregates (fused_tile), no aggregation launch
@@ -1008,7 +1013,7 @@ struct Plan {
   size_t inv_words_total = 0;
   void *fpart = nullptr, *finals = nullptr, *seg_matched = nullptr, *apart = nullptr, *masks = nullptr;
   void *gtab = nullptr, *ghll = nullptr, *slab = nullptr, *hslab = nullptr, *fo = nullptr;
-  // pinned host landing area for the per-execution results: finals[64] | seg_matched[nseg] | hll
+  // pinned host landing area for the per-execution results: finals[64] | seg_matched[nmatch] | hll
   uint64_t *pinned = nullptr;
   uint64_t *pinned_dev = nullptr;  // the same memory as the device addresses it
   hipGraphExec_t graph_exec = nullptr;
@@ -1031,6 +1036,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d aggregations on the GPU path", kMaxAggs);
   if (q->num_group_by < 0 || q->num_group_by > 4) return fail(PHIP_ERR_UNSUPPORTED, "query: at most 4 group-by columns");
   if (q->num_segments > 1 && want_bitmap) return fail(PHIP_ERR_INVALID, "filter bitmap: one segment only");
+  const int nprog = std::max(1, q->num_filter_programs);
+  if (nprog > kMaxPrograms) return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d filter programs", kMaxPrograms);
+  if (nprog > 1 && (q->num_group_by > 0 || want_bitmap))
+    return fail(PHIP_ERR_UNSUPPORTED, "several filter programs: aggregation-only queries");
 
   std::vector<Segment *> segs(q->num_segments);
   Device *dev = nullptr;
@@ -1071,20 +1080,26 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   int nhll = 0, log2m = 0;
   std::vector<int32_t> kinds(naggs + 2, ACC_COUNT);
   std::vector<bool> projected(ncols, false);
+  std::vector<uint32_t> proj_progs(ncols, 0);  // column -> bit p: program p projects it
   for (int a = 0; a < naggs; a++) {
     const phip_aggregation &ag = q->aggregations[a];
     DevAgg &d = dq.aggs[a];
     d.expr = ag.expr;
     d.col_a = ag.column_a;
     d.col_b = ag.column_b;
+    if (ag.program < 0 || ag.program >= nprog)
+      return fail(PHIP_ERR_INVALID, "aggregation %d: program %d outside [0, %d)", a, ag.program, nprog);
+    d.program = ag.program;
     if (ag.function < PHIP_AGG_COUNT || ag.function > PHIP_AGG_HLL) return fail(PHIP_ERR_INVALID, "bad aggregation function");
     if (ag.function != PHIP_AGG_COUNT) {
       if (ag.column_a < 0 || ag.column_a >= ncols) return fail(PHIP_ERR_INVALID, "aggregation column out of range");
       projected[ag.column_a] = true;
+      proj_progs[ag.column_a] |= 1u << ag.program;
       if (ag.expr != PHIP_EXPR_COLUMN) {
         if (ag.function == PHIP_AGG_HLL) return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over expressions");
         if (ag.column_b < 0 || ag.column_b >= ncols) return fail(PHIP_ERR_INVALID, "aggregation column out of range");
         projected[ag.column_b] = true;
+        proj_progs[ag.column_b] |= 1u << ag.program;
       }
     }
     bool integral = true;
@@ -1233,6 +1248,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     int c = q->group_by_columns[k];
     if (c < 0 || c >= ncols) return fail(PHIP_ERR_INVALID, "group-by column out of range");
     projected[c] = true;
+    proj_progs[c] |= 1u;
   }
   int num_projected = 0;
   for (bool p : projected) num_projected += p ? 1 : 0;
@@ -1301,13 +1317,14 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   std::vector<InvLeaf> inv_leaves;
   int64_t total_work = 0;
   int64_t total_docs = 0;
-  std::vector<DevSeg> dsegs;  // segments with work only
-  dsegs.reserve(nseg);
+  std::vector<DevSeg> dsegs;  // (segment, program) entries with work only, segment-major
+  dsegs.reserve((size_t)nseg * nprog);
   for (int s = 0; s < nseg; s++) {
     Segment &sg = *segs[s];
     total_docs += sg.num_docs;
-    DevSeg ds;
-    memset(&ds, 0, sizeof(ds));
+    DevSeg seg_ds;
+    memset(&seg_ds, 0, sizeof(seg_ds));
+    DevSeg &ds = seg_ds;
     ds.num_docs = sg.num_docs;
     ds.seg_index = s;
     for (int c = 0; c < ncols; c++) {
@@ -1332,10 +1349,14 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
     for (int k = 0; k < q->num_group_by; k++) ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
     if (sg.num_docs == 0) continue;
-
+   // one entry per filter program (adjacent, so the programs of a segment read its columns back to back)
+   for (int prog = 0; prog < nprog; prog++) {
+    DevSeg ds = seg_ds;
+    ds.program = prog;
+    ds.seg_index = prog * nseg + s;
     // filter program: validate the preorder ABI tree, then emit postfix with binary AND/OR
-    const int nb = q->filter_offsets ? q->filter_offsets[s] : 0;
-    const int ne = q->filter_offsets ? q->filter_offsets[s + 1] : 0;
+    const int nb = q->filter_offsets ? q->filter_offsets[prog * nseg + s] : 0;
+    const int ne = q->filter_offsets ? q->filter_offsets[prog * nseg + s + 1] : 0;
     const size_t node_begin = nodes.size();
     ds.node_begin = (int32_t)node_begin;
     int64_t hull_lo = 0, hull_hi = (int64_t)sg.num_docs - 1;  // candidate docs (inclusive)
@@ -1531,6 +1552,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     ds.work_begin = (int32_t)total_work;
     total_work += ds.num_work;
     dsegs.push_back(ds);
+   }
   }
   if (total_work > INT32_MAX / 2) return fail(PHIP_ERR_UNSUPPORTED, "too many tiles in one query");
   dq.total_work = (int32_t)total_work;
@@ -1619,7 +1641,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // the aggregation kernel reads them for matched docs only.
   bool has_filter = false;
   for (const DevSeg &ds : dsegs) has_filter |= ds.node_end > ds.node_begin;
-  bool need_agg = group_by;
+  bool need_agg = group_by || nprog > 1;  // several programs: every COUNT is per program, in the aggregation walk
   for (int a = 0; a < naggs; a++) need_agg |= dq.aggs[a].acc != ACC_COUNT;
   bool need_mask = has_filter && (need_agg || want_bitmap);
   const int64_t kSlotBudget = 19 * 1024;  // bytes per ring slot
@@ -1763,7 +1785,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // (Q1.1 sorted, 44K tiles: 0.207 -> 0.270 ms; unsorted, 293K tiles: 1.6 -> 2.4 ms per step).
     const char *fe = getenv("PHIP_FUSE");  // measurement override: "0" never, "1" always, unset = by size
     const int64_t kFuseMaxTiles = 8192;
-    bool fuse = conj_all && any_filter_prog && !group_by && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
+    bool fuse = conj_all && any_filter_prog && !group_by && nprog == 1 && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
                 (fe ? atoi(fe) != 0 : total_work <= kFuseMaxTiles);
     bool any_value = false;
     for (int a = 0; a < naggs; a++) any_value |= dq.aggs[a].acc != ACC_COUNT;
@@ -1818,6 +1840,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   for (int c = 0; c < ncols; c++) {
     if (!projected[c]) continue;
     Plan::ProjCol pc;
+    pc.progs = proj_progs[c];
     for (int s = 0; s < nseg; s++) {
       const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
       const bool raw = cs.fwd_kind == PHIP_FWD_RAW_CHUNK;
@@ -1921,15 +1944,16 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   void *fpart, *finals, *seg_matched, *apart = nullptr, *masks = nullptr;
   rc = P.alloc((size_t)filter_blocks * 2 * 8, &fpart);
   if (rc) return rc;
-  // finals[64] | seg_matched[nseg] | hll registers: the same layout as the pinned landing area, so one
+  // finals[64] | seg_matched[nmatch] | hll registers: the same layout as the pinned landing area, so one
   // D2H copy brings every per-execution result back
-  rc = P.alloc((64 + (size_t)nseg) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
+  const int nmatch = nprog * nseg;
+  rc = P.alloc((64 + (size_t)nmatch) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4, &finals);
   if (rc) return rc;
   seg_matched = (uint64_t *)finals + 64;
   fq.partials = (uint64_t *)fpart;
   fq.seg_matched = (uint64_t *)seg_matched;
   // finals: [0, naggs) aggregation slots, [32, 34) matched docs + entries scanned in filter
-  dq.hll_regs = (uint32_t *)((uint64_t *)finals + 64 + nseg);
+  dq.hll_regs = (uint32_t *)((uint64_t *)finals + 64 + nmatch);
   if (need_mask) {
     rc = P.alloc((size_t)std::max<int64_t>(total_work, 1) * 64 * 4, &masks);
     if (rc) return rc;
@@ -1994,6 +2018,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.tasks = tasks;
   P.gb_dicts = gb_dicts;
   P.nseg = nseg;
+  P.nprog = nprog;
+  P.nmatch = nmatch;
   P.naggs = naggs;
   P.nhll = nhll;
   P.log2m = log2m;
@@ -2055,6 +2081,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.total_docs = total_docs;
   P.docs_in_work = 0;
   for (const DevSeg &ds : dsegs) P.docs_in_work += ds.num_docs;
+  P.slot_docs.assign(nmatch, 0);
+  for (const DevSeg &ds : dsegs) P.slot_docs[ds.seg_index] = ds.num_docs;
   P.has_filter = has_filter;
   P.need_agg = need_agg;
   P.need_mask = need_mask;
@@ -2088,7 +2116,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   for (auto &e : P.ev) HIP_TRY(hipEventCreate(&e));
   {
     void *h = nullptr;
-    const size_t pbytes = (64 + (size_t)nseg) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4;
+    const size_t pbytes = (64 + (size_t)nmatch) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4;
     // device-visible (mapped) pinned memory: finalize_all_kernel writes the results straight into it
     HIP_TRY(hipHostMalloc(&h, pbytes, hipHostMallocMapped));
     memset(h, 0, pbytes);
@@ -2104,7 +2132,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
 static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   DevAggQuery &dq = P.dq;
   DevFilter &fq = P.fq;
-  const int nseg = P.nseg, naggs = P.naggs, nhll = P.nhll, m_regs = P.m_regs;
+  const int naggs = P.naggs, nhll = P.nhll, m_regs = P.m_regs;
   const bool group_by = P.group_by, has_filter = P.has_filter, need_agg = P.need_agg, need_mask = P.need_mask;
   const bool conj_only = P.conj_only;
   const int64_t total_work = P.total_work;
@@ -2125,7 +2153,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   // failed execution they are cleared here
   const size_t hll_words = nhll && !group_by ? ((size_t)nhll << P.log2m) : 0;
   if (!P.clean) {
-    HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)nseg * 8, st));
+    HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)P.nmatch * 8, st));
     if (hll_words) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, hll_words * 4, st));
   }
   P.clean = false;
@@ -2170,12 +2198,12 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (filter_words && need_mask && !dsegs.empty())
     HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
                                   filter_nwords, st));
-  // every result lands in the plan's pinned buffer, written by the device: finals[64] | seg_matched[nseg] | HLL
+  // every result lands in the plan's pinned buffer, written by the device: finals[64] | seg_matched[nmatch] | HLL
   if (total_work > 0) {
     const bool aggs_here = need_agg && !group_by && naggs > 0;
     HIP_TRY(launch_finalize_all(aggs_here ? (const uint64_t *)apart : nullptr, fused ? filter_blocks : agg_blocks,
                                 aggs_here ? naggs : 0, dev_kinds, has_filter ? (const uint64_t *)fpart : nullptr,
-                                filter_blocks, dev_kinds + naggs, (uint64_t *)seg_matched, nseg, dq.hll_regs,
+                                filter_blocks, dev_kinds + naggs, (uint64_t *)seg_matched, P.nmatch, dq.hll_regs,
                                 (int)hll_words, P.pinned_dev, st));
   }
   if (!group_by) HIP_TRY(hipEventRecord(P.ev[3], st));
@@ -2371,7 +2399,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   if (mode != EXEC_FINISH) {
     P.executions++;
     if (P.total_work == 0) {  // no kernel ran: nothing matched, no registers set
-      memset(P.pinned + 64, 0, (size_t)P.nseg * 8 + (P.nhll && !P.group_by ? ((size_t)P.nhll << P.log2m) * 4 : 0));
+      memset(P.pinned + 64, 0, (size_t)P.nmatch * 8 + (P.nhll && !P.group_by ? ((size_t)P.nhll << P.log2m) * 4 : 0));
     }
   }
   DevAggQuery &dq = P.dq;
@@ -2393,21 +2421,39 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   memset(&r, 0, sizeof(r));
   const uint64_t *fin = P.pinned;
   const uint64_t *segm = P.pinned + 64;
-  const uint32_t *hll_host = (const uint32_t *)(P.pinned + 64 + nseg);
+  const uint32_t *hll_host = (const uint32_t *)(P.pinned + 64 + P.nmatch);
 
   // this GPU's statistics (valid once the stream has synchronised)
   auto local_stats = [&](int64_t st6[6]) {
     const int64_t m = has_filter ? (int64_t)fin[32] : docs_in_work;
-    st6[0] = m;
+    st6[0] = m;  // several programs: summed over them (FilteredAggregationOperator adds its infos' statistics)
     st6[1] = has_filter ? (int64_t)fin[33] : 0;
     st6[2] = m * num_projected;
     st6[3] = total_docs;
     st6[4] = nseg;
     st6[5] = 0;
-    if (has_filter) {
-      for (int s = 0; s < nseg; s++) st6[5] += segm[s] ? 1 : 0;
-    } else {
-      for (const DevSeg &ds : dsegs) st6[5] += ds.num_docs > 0 ? 1 : 0;
+    if (P.nprog > 1) {  // entries post filter per program: its matched docs x the columns its functions project
+      st6[2] = 0;
+      for (int p = 0; p < P.nprog; p++) {
+        int64_t mp = 0;
+        for (int s = 0; s < nseg; s++) mp += has_filter ? (int64_t)segm[p * nseg + s] : P.slot_docs[p * nseg + s];
+        int np = 0;
+        for (const Plan::ProjCol &pc : P.proj) np += (pc.progs >> p) & 1u;
+        st6[2] += mp * np;
+      }
+    }
+    if (has_filter) {  // a segment matched when any of its programs did
+      for (int s = 0; s < nseg; s++) {
+        bool any = false;
+        for (int p = 0; p < P.nprog; p++) any |= segm[p * nseg + s] != 0;
+        st6[5] += any ? 1 : 0;
+      }
+    } else {  // no program filters: every entry's docs match
+      for (int s = 0; s < nseg; s++) {
+        bool any = false;
+        for (int p = 0; p < P.nprog; p++) any |= P.slot_docs[p * nseg + s] != 0;
+        st6[5] += any ? 1 : 0;
+      }
     }
   };
   // row kinds of the gather: the plan's, or the caller's after a merge that turned int64 sums into doubles
@@ -2602,10 +2648,13 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   if (need_agg) {
     int64_t ab = 0;
     for (int s = 0; s < nseg; s++) {
-      const int64_t m = has_filter ? (int64_t)segm[s] : P.seg_docs[s];
-      for (const Plan::ProjCol &pc : P.proj) {
-        ab += pc.bits[s] ? ceil_div(m * pc.bits[s], 8) : m * pc.width[s];
-        if (pc.bits[s]) ab += std::min<int64_t>(pc.card[s], m) * pc.width[s];
+      for (int p = 0; p < P.nprog; p++) {
+        const int64_t m = has_filter ? (int64_t)segm[p * nseg + s] : P.slot_docs[p * nseg + s];
+        for (const Plan::ProjCol &pc : P.proj) {
+          if (!((pc.progs >> p) & 1u)) continue;
+          ab += pc.bits[s] ? ceil_div(m * pc.bits[s], 8) : m * pc.width[s];
+          if (pc.bits[s]) ab += std::min<int64_t>(pc.card[s], m) * pc.width[s];
+        }
       }
     }
     r.agg_bytes = ab;

@@ -257,17 +257,22 @@ def _gpu_expr(e):
     raise UnsupportedOnGpu(f"aggregation argument {e} is outside the GPU expression subset")
 
 
-def plan_aggregations(aggs: Sequence[AggregationInfo]):
-    """Query aggregations -> GPU primitives (deduplicated) + per-function slot mapping."""
-    prims = []  # (function, expr, col_a, col_b, log2m)
+def plan_aggregations(aggs: Sequence[AggregationInfo], programs: Optional[Sequence[int]] = None):
+    """Query aggregations -> GPU primitives (deduplicated) + per-function slot mapping. ``programs``: per
+    aggregation, the filter program it reads (several programs in one pass); primitives of different programs
+    never merge."""
+    prims = []  # (function, expr, col_a, col_b, log2m, program)
     mapping = []
 
-    def slot(p):
-        if p not in prims:
-            prims.append(p)
-        return prims.index(p)
+    for j, ag in enumerate(aggs):
+        prog = programs[j] if programs is not None else 0
 
-    for ag in aggs:
+        def slot(p):
+            p = p + (prog,)
+            if p not in prims:
+                prims.append(p)
+            return prims.index(p)
+
         f = ag.function
         if f == "count":
             mapping.append(("count", slot((_lib.AGG_COUNT, 0, None, None, 0))))
@@ -297,17 +302,24 @@ class GpuCombineOperator:
     """One operator over all segments of the query (the all-segment GPU variant of SURVEY.md §8b)."""
 
     def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int,
-                 segment_filters=None):
+                 segment_filters=None, programs=None):
         """segment_filters: optional per-segment (FilterContext or None, inclusive doc ranges or None) replacing
-        query.filter -- the star-tree path's matched documents AND remaining predicates."""
+        query.filter -- the star-tree path's matched documents AND remaining predicates.
+        programs: optional (filters, agg_programs) -- k filters (None = every doc) evaluated in one pass, and per
+        query aggregation the index of the filter whose docs it aggregates (phip_query_desc.num_filter_programs;
+        query.filter is then unused)."""
         self.query = query
         self.segments = list(segments)
         self.num_groups_limit = num_groups_limit
         for e in query.group_by:
             if not isinstance(e, Identifier):
                 raise UnsupportedOnGpu(f"group-by expression {e}")
-        self.prims, self.mapping = plan_aggregations(query.aggregations)
-        if segment_filters is None:
+        self.num_programs = len(programs[0]) if programs is not None else 1
+        self.prims, self.mapping = plan_aggregations(query.aggregations, programs[1] if programs is not None else None)
+        if programs is not None:
+            # program-major, as filter_offsets lays them out: program p of segment s at p * nseg + s
+            self.trees = [compile_filter(s, f) for f in programs[0] for s in self.segments]
+        elif segment_filters is None:
             self.trees = [compile_filter(s, query.filter) for s in self.segments]
         else:
             self.trees = []
@@ -359,13 +371,15 @@ class GpuCombineOperator:
         arr = (_lib.FilterNode * max(len(nodes), 1))(*nodes)
         keep.append(arr)
         q.filter_nodes = arr
+        q.num_filter_programs = self.num_programs
         aggs = (_lib.Aggregation * max(len(self.prims), 1))()
-        for i, (f, expr, ca, cb, log2m) in enumerate(self.prims):
+        for i, (f, expr, ca, cb, log2m, prog) in enumerate(self.prims):
             aggs[i].function = f
             aggs[i].expr = expr
             aggs[i].column_a = col_index[ca] if ca is not None else -1
             aggs[i].column_b = col_index[cb] if cb is not None else -1
             aggs[i].log2m = log2m
+            aggs[i].program = prog
         keep.append(aggs)
         q.num_aggregations = len(self.prims)
         q.aggregations = aggs
@@ -643,9 +657,16 @@ def _run_parts(parts):
 class GpuFilteredAggregationOperator:
     """FilteredAggregationOperator (pinot-core/.../operator/query/FilteredAggregationOperator.java:67-113)
     over all segments: the aggregations are grouped by their FILTER clause (unfiltered ones under the
-    main filter), as AggregationFunctionUtils.buildFilteredAggregationInfos does, and every group runs as
-    one GPU combine operator over main AND its filter. Results return in query order; numDocsScanned
-    and the entries scanned are summed over the groups, like the reference operator's statistics."""
+    main filter), as AggregationFunctionUtils.buildFilteredAggregationInfos does, and every group's filter --
+    main AND its FILTER -- becomes one filter program of a single GPU plan: one filter launch evaluates all
+    programs into one tile mask each and one aggregation launch applies every function to its own program's
+    docs (phip_query_desc.num_filter_programs). Results return in query order; numDocsScanned and the entries
+    scanned are summed over the programs, like the reference operator's statistics. More than
+    kMaxPrograms (8) groups, or more than 8 primitive slots, run as one plan per group."""
+
+    _MAX_PROGRAMS = 8  # device.h kMaxPrograms
+    _MAX_SLOTS = 8     # device.h kMaxAggs
+    _TIMES = ("device_ms", "scan_kernel_ms", "filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes")
 
     def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
         if query.group_by:
@@ -655,19 +676,37 @@ class GpuFilteredAggregationOperator:
         groups = {}
         for i, ag in enumerate(query.aggregations):
             groups.setdefault(ag.filter, []).append(i)
-        self.parts = []
-        for flt, idxs in groups.items():
+        filters = []
+        for flt in groups:
             if flt is None:
-                f = query.filter
+                filters.append(query.filter)
             elif query.filter is None:
-                f = flt
+                filters.append(flt)
             else:
-                f = FilterContext.AND(query.filter, flt)
+                filters.append(FilterContext.AND(query.filter, flt))
+        self.one_pass = None
+        self.parts = []
+        if 1 < len(filters) <= self._MAX_PROGRAMS:
+            order = list(groups)
+            sub = QueryContext(query.table, [], [ag.unfiltered() for ag in query.aggregations], None, [],
+                               limit=query.limit, options=dict(query.options))
+            op = GpuCombineOperator(sub, self.segments, num_groups_limit,
+                                    programs=(filters, [order.index(ag.filter) for ag in query.aggregations]))
+            if len(op.prims) <= self._MAX_SLOTS:
+                self.one_pass = op
+                return
+        for f, idxs in zip(filters, groups.values()):
             sub = QueryContext(query.table, [], [query.aggregations[i].unfiltered() for i in idxs], f, [],
                                limit=query.limit, options=dict(query.options))
             self.parts.append((idxs, GpuCombineOperator(sub, self.segments, num_groups_limit)))
 
     def next_block(self):
+        if self.one_pass is not None:
+            blk = self.one_pass.next_block()
+            out = AggregationResultsBlock(self.query.aggregations, blk.results, blk.stats)
+            for k in self._TIMES:
+                setattr(out, k, getattr(blk, k, 0))
+            return out
         results = [None] * len(self.query.aggregations)
         stats = ExecutionStatistics()
         scan_ms = device_ms = 0.0
@@ -689,6 +728,8 @@ class GpuFilteredAggregationOperator:
         return blk
 
     def close(self):
+        if self.one_pass is not None:
+            self.one_pass.close()
         for _, op in self.parts:
             op.close()
 
