@@ -709,7 +709,7 @@ class GpuFilteredAggregationOperator:
             return out
         results = [None] * len(self.query.aggregations)
         stats = ExecutionStatistics()
-        scan_ms = device_ms = 0.0
+        times = dict.fromkeys(self._TIMES, 0)
         for (idxs, op), blk in zip(self.parts, _run_parts(self.parts)):
             for j, i in enumerate(idxs):
                 results[i] = blk.results[j]
@@ -720,11 +720,11 @@ class GpuFilteredAggregationOperator:
             stats.num_total_docs = s.num_total_docs
             stats.num_segments_processed = s.num_segments_processed
             stats.num_segments_matched = max(stats.num_segments_matched, s.num_segments_matched)
-            scan_ms += getattr(blk, "scan_kernel_ms", 0.0) or 0.0
-            device_ms += getattr(blk, "device_ms", 0.0) or 0.0
+            for k in self._TIMES:
+                times[k] += getattr(blk, k, 0) or 0
         blk = AggregationResultsBlock(self.query.aggregations, results, stats)
-        blk.scan_kernel_ms = scan_ms
-        blk.device_ms = device_ms
+        for k, v in times.items():
+            setattr(blk, k, v)
         return blk
 
     def close(self):
