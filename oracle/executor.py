@@ -100,8 +100,12 @@ class OracleSegment:
 def _read_raw_chunk(buf, dtype, n):
     """FixedByteChunkSVForwardIndexReader over PASS_THROUGH or compressed chunks: chunk k spans
     [offset_k, offset_{k+1}) (the last one runs to the end of the buffer) and decodes to
-    docs_k x entry bytes (BaseChunkForwardIndexReader.java:60-111,204-232)."""
+    docs_k x entry bytes (BaseChunkForwardIndexReader.java:60-111,204-232). Version 4 is
+    FixedBytePower2ChunkSVForwardIndexReader (ForwardIndexReaderFactory.java:113-117): the same layout with a
+    power-of-two chunk, doc d in chunk d >> log2(per_chunk) (:40-42,98-100)."""
     version, num_chunks, per_chunk, entry = [int(x) for x in np.frombuffer(buf, dtype=">i4", count=4)]
+    assert 1 <= version <= 5, version
+    assert version != 4 or (per_chunk > 0 and per_chunk & (per_chunk - 1) == 0), per_chunk
     if version > 1:
         total, comp, data_hdr = [int(x) for x in np.frombuffer(buf, dtype=">i4", count=3, offset=16)]
     else:  # v1: 4-int header, SNAPPY chunks, offsets from byte 16 (BaseChunkForwardIndexReader.java:86-95)

@@ -580,8 +580,11 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
     if (comp < 0 || comp > 5)
       return fail(PHIP_ERR_INVALID, "column %s: unknown chunk compression type %d", c.name, comp);
     if (entry != type_width(c.data_type) || total != n || per_chunk <= 0 ||
-        num_chunks != ceil_div(n, per_chunk) || (version < 1 || version > 3))
+        num_chunks != ceil_div(n, per_chunk) || (version < 1 || version > 5))
       return fail(PHIP_ERR_INVALID, "column %s: bad chunk header", c.name);
+    // v4 = FixedBytePower2ChunkSVForwardIndexReader (ForwardIndexReaderFactory.java:113-117): chunk = doc >> shift
+    if (version == 4 && (per_chunk & (per_chunk - 1)) != 0)
+      return fail(PHIP_ERR_INVALID, "column %s: v4 chunk of %d docs is not a power of two", c.name, per_chunk);
     const int osz = version <= 2 ? 4 : 8;
     const uint64_t hdr_end = (uint64_t)data_hdr + (uint64_t)num_chunks * osz;
     if (data_hdr < (version > 1 ? 28 : 16) || hdr_end > c.forward_bytes)

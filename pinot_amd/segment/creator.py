@@ -185,7 +185,14 @@ def _compress_chunk(chunk: bytes, codec: int) -> bytes:
 def _chunk_forward(values: np.ndarray, dt: DataType, docs_per_chunk: int = 1000, version: int = 3,
                    compression: str = "PASS_THROUGH") -> bytes:
     """Fixed-byte chunk forward index (BaseChunkForwardIndexWriter.java:40-60,130-200): 7-int header,
-    chunk offsets (int for v2, long for v3), then each chunk through its codec; offsets are absolute."""
+    chunk offsets (int for v2, long from v3), then each chunk through its codec; offsets are absolute.
+    Versions 4 / 5 (fixed-width only, BaseChunkForwardIndexWriter.java:91) round docs per chunk up to a power of
+    two (FixedByteChunkForwardIndexWriter.normalizeDocsPerChunk :93-98), which the v4 reader
+    (FixedBytePower2ChunkSVForwardIndexReader) turns into a shift."""
+    if version not in (2, 3, 4, 5):
+        raise ValueError(f"illegal chunk writer version {version} for fixed-byte values")
+    if version >= 4 and docs_per_chunk & (docs_per_chunk - 1):
+        docs_per_chunk = 1 << (docs_per_chunk - 1).bit_length()
     codec = CHUNK_COMPRESSION[compression]
     n = len(values)
     entry = np.dtype(dt.numpy_be).itemsize

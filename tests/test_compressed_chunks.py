@@ -100,7 +100,7 @@ def _segment(n, codec, seed=3, docs_per_chunk=1000, version=3):
 
 
 @pytest.mark.parametrize("codec", CODECS + ENTROPY + ("PASS_THROUGH",))
-@pytest.mark.parametrize("docs_per_chunk,version", [(1000, 3), (7, 2), (4096, 3)])
+@pytest.mark.parametrize("docs_per_chunk,version", [(1000, 3), (7, 2), (4096, 3), (1000, 4), (100, 5)])
 def test_oracle_reads_compressed_segment(codec, docs_per_chunk, version):
     n = 10_007
     seg, cols = _segment(n, codec, docs_per_chunk=docs_per_chunk, version=version)
@@ -112,6 +112,17 @@ def test_oracle_reads_compressed_segment(codec, docs_per_chunk, version):
         got = oseg.values(name)
         want = np.asarray(vals, dtype=dt.numpy).astype(got.dtype)
         assert np.array_equal(got, want), (codec, name)
+
+
+def test_v4_chunks_are_power_of_two():
+    """FixedByteChunkForwardIndexWriter.normalizeDocsPerChunk (:93-98): v4 / v5 round the chunk up to a power of
+    two, and the v4 header is what FixedBytePower2ChunkSVForwardIndexReader reads (ForwardIndexReaderFactory:113-117)."""
+    for ver, want in ((3, 1000), (4, 1024), (5, 1024)):
+        seg, _ = _segment(5000, "LZ4", docs_per_chunk=1000, version=ver)
+        hdr = np.frombuffer(seg.columns["L"].forward[:28], dtype=">i4")
+        assert hdr[0] == ver and hdr[2] == want and hdr[1] == -(-5000 // want)
+    with pytest.raises(ValueError):
+        _segment(100, "LZ4", version=6)
 
 
 # ------------------------------------------------------------------------------------------ GPU
@@ -132,7 +143,7 @@ def test_gpu_compressed_raw_columns(gpu_lib, codec):
     from tests.test_gpu_parity import _assert_intermediates_equal
     segs, gsegs = [], []
     try:
-        for seed, dpc, ver in ((3, 1000, 3), (4, 7, 2), (5, 4096, 3)):
+        for seed, dpc, ver in ((3, 1000, 3), (4, 7, 2), (5, 4096, 3), (6, 1000, 4), (7, 300, 5)):
             s, _ = _segment(123_457 if dpc != 7 else 20_001, codec, seed=seed, docs_per_chunk=dpc, version=ver)
             segs.append(s)
             gsegs.append(GpuSegment(s))
