@@ -1108,28 +1108,40 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
 // Roaring containers of the selected dict ids -> OR into dense u64 doc words
 // (BitmapInvertedIndexReader.getDocIds + ImmutableRoaringBitmap.or, InvertedIndexFilterOperator.java:79-95)
 // ------------------------------------------------------------------------------------------------
-// One workgroup per (leaf, key) group: every selected container of that 65536-doc range is OR-ed into
-// an LDS bitmap with LDS atomics (array: one bit per value, bitmap: word OR, run: word masks), then the
-// 1024 words go to HBM with plain coalesced stores -- no global atomics, each word written once.
-__global__ __launch_bounds__(256) void roaring_or_kernel(const RoaringTask *__restrict__ tasks,
-                                                         const RoaringGroup *__restrict__ groups, int32_t ngroups) {
+// One workgroup per (leaf, key) group, one wave per container: every selected container of that 65536-doc
+// range is OR-ed into an LDS bitmap with LDS atomics (array: one bit per value, bitmap: word OR, run: word
+// masks), then the 1024 words go to HBM with plain coalesced stores -- no global atomics, each word written
+// once. A key with at least kRoaringWaves containers (an IN over many values: mostly small arrays) gives each
+// wave its own containers round robin, so that many container loads are in flight instead of one; a key with
+// fewer takes them one at a time with the whole workgroup. Every key of a leaf has a group (keys without
+// containers store zeros), so the dense words need no clearing pass.
+constexpr int kRoaringWaves = 8;
+__global__ __launch_bounds__(kRoaringWaves * 64) void roaring_or_kernel(const RoaringTask *__restrict__ tasks,
+                                                                        const RoaringGroup *__restrict__ groups,
+                                                                        int32_t ngroups) {
   __shared__ uint64_t bm[1024];
   typedef PHIP_LDS uint64_t lds64;
+  const int lane = lane_id();
+  const int wave = (int)(threadIdx.x >> 6);
   for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const RoaringGroup g = groups[gi];
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) bm[i] = 0;
     __syncthreads();
-    for (int ti = g.task_begin; ti < g.task_end; ti++) {
+    const bool per_wave = g.task_end - g.task_begin >= kRoaringWaves;  // uniform over the workgroup
+    const int tstep = per_wave ? kRoaringWaves : 1;
+    const int lid = per_wave ? lane : (int)threadIdx.x;
+    const int lstep = per_wave ? 64 : (int)blockDim.x;
+    for (int ti = g.task_begin + (per_wave ? wave : 0); ti < g.task_end; ti += tstep) {
       const RoaringTask tk = tasks[ti];
       if (tk.kind == 0) {
         const uint16_t *v = (const uint16_t *)tk.payload;
-        for (int i = threadIdx.x; i < tk.card; i += blockDim.x) {
+        for (int i = lid; i < tk.card; i += lstep) {
           const uint32_t x = v[i];
           __hip_atomic_fetch_or((lds64 *)&bm[x >> 6], 1ull << (x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       } else if (tk.kind == 1) {
         const uint64_t *w = (const uint64_t *)tk.payload;
-        for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        for (int i = lid; i < 1024; i += lstep) {
           const uint64_t x = w[i];
           if (x) __hip_atomic_fetch_or((lds64 *)&bm[i], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -1138,7 +1150,7 @@ __global__ __launch_bounds__(256) void roaring_or_kernel(const RoaringTask *__re
         for (int ri = 0; ri < tk.card; ri++) {
           const uint32_t s = r[1 + 2 * ri], e = min(s + r[2 + 2 * ri], 65535u);  // inclusive (load validates)
           const uint32_t ws = s >> 6, we = e >> 6;
-          for (uint32_t wi = ws + threadIdx.x; wi <= we; wi += blockDim.x) {
+          for (uint32_t wi = ws + lid; wi <= we; wi += lstep) {
             const int lo = (wi == ws) ? (int)(s & 63) : 0;
             const int hi = (wi == we) ? (int)(e & 63) : 63;
             const uint64_t m = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
@@ -1179,7 +1191,7 @@ __global__ __launch_bounds__(256) void masks_to_words_kernel(const uint32_t *__r
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *groups, int32_t ngroups, hipStream_t s) {
   if (ngroups <= 0) return hipSuccess;
-  roaring_or_kernel<<<ngroups < 16384 ? ngroups : 16384, 256, 0, s>>>(tasks, groups, ngroups);
+  roaring_or_kernel<<<ngroups < 16384 ? ngroups : 16384, kRoaringWaves * 64, 0, s>>>(tasks, groups, ngroups);
   return hipGetLastError();
 }
 

@@ -1583,10 +1583,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // inverted leaves: dense doc words per leaf + roaring container tasks
   std::vector<RoaringTask> tasks;
   size_t inv_words_total = 0;
-  std::vector<size_t> inv_word_off(inv_leaves.size());
+  std::vector<size_t> inv_word_off(inv_leaves.size()), inv_word_nw(inv_leaves.size());
   for (size_t i = 0; i < inv_leaves.size(); i++) {
     const Segment &sg = *segs[inv_leaves[i].seg];
-    size_t nw = (size_t)std::max(round_up(sg.num_docs, 65536), round_up(sg.num_docs, kTileDocs)) / 64;
+    size_t nw = (size_t)std::max(round_up(sg.num_docs, 65536), round_up(sg.num_docs, kTileDocs)) / 64;  // whole keys
+    inv_word_nw[i] = nw;
     inv_word_off[i] = inv_words_total;
     inv_words_total += nw;
   }
@@ -1617,22 +1618,26 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         tasks.push_back(t);
       }
     }
-    // group the leaf's containers by key (one LDS-decoding workgroup per key)
+    // group the leaf's containers by key (one LDS-decoding workgroup per key); every key of the leaf's words
+    // gets a group -- one without containers stores zeros -- so the words need no clearing pass
     std::stable_sort(tasks.begin() + first, tasks.end(),
                      [](const RoaringTask &a, const RoaringTask &b) { return a.key < b.key; });
-    for (size_t t = first; t < tasks.size();) {
+    if (tasks.size() > (size_t)INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "too many inverted-index containers");
+    const int32_t nkeys = (int32_t)(inv_word_nw[i] / 1024);
+    size_t t = first;
+    for (int32_t key = 0; key < nkeys; key++) {
       size_t e = t;
-      while (e < tasks.size() && tasks[e].key == tasks[t].key) e++;
-      if (e > (size_t)INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "too many inverted-index containers");
+      while (e < tasks.size() && tasks[e].key == key) e++;
       RoaringGroup g;
       g.out_words = words;
       g.task_begin = (int32_t)t;
       g.task_end = (int32_t)e;
-      g.key = tasks[t].key;
+      g.key = key;
       g.pad = 0;
       rgroups.push_back(g);
       t = e;
     }
+    if (t != tasks.size()) return fail(PHIP_ERR_INVALID, "inverted-index container key beyond the segment's docs");
   }
   const size_t tasks_off = tasks.empty() ? 0 : blob.add(tasks.data(), tasks.size() * sizeof(RoaringTask));
   const size_t rgroups_off = rgroups.empty() ? 0 : blob.add(rgroups.data(), rgroups.size() * sizeof(RoaringGroup));
@@ -2143,7 +2148,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   const int32_t *dev_kinds = (const int32_t *)(base + P.kinds_off);
   uint64_t *fin_agg = (uint64_t *)P.finals;
   uint64_t *fin_filter = (uint64_t *)P.finals + 32;
-  void *seg_matched = P.seg_matched, *inv_words = P.inv_words, *gtab = P.gtab, *ghll = P.ghll;
+  void *seg_matched = P.seg_matched, *gtab = P.gtab, *ghll = P.ghll;
   void *fpart = P.fpart, *apart = P.apart, *slab = P.slab, *hslab = P.hslab, *masks = P.masks, *fo = P.fo;
   const size_t inv_words_total = P.inv_words_total, tasks_off = P.tasks_off, dq_off = P.dq_off;
   const std::vector<DevSeg> &dsegs = P.dsegs;
@@ -2161,8 +2166,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   }
   P.clean = false;
   if (filter_words) HIP_TRY(hipMemsetAsync(fo, 0, (size_t)filter_nwords * 8, st));
-  if (inv_words_total) {
-    HIP_TRY(hipMemsetAsync(inv_words, 0, inv_words_total * 8, st));
+  if (inv_words_total) {  // (every key of every leaf is written: no clearing pass)
     HIP_TRY(launch_roaring_or((const RoaringTask *)(base + tasks_off), (const RoaringGroup *)(base + P.rgroups_off),
                               (int32_t)P.num_rgroups, st));
   }

@@ -87,7 +87,9 @@ def time_gpu(qc, gsegs, reps, warmup):
     from pinot_amd import _lib
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     lib = _lib.load()
-    op = GpuInstancePlanMaker(num_groups_limit=10 ** 9).make_instance_plan(qc, gsegs)
+    # the reference's default numGroupsLimit (100,000, InstancePlanMakerImplV2.java): a query with more groups
+    # takes the limit pass (limit.hip), as the reference's per-segment generators stop at the limit
+    op = GpuInstancePlanMaker().make_instance_plan(qc, gsegs)
     if hasattr(op, "inner") and hasattr(op.inner, "run_raw"):
         op = op.inner  # star-tree: the traversal is plan-time; time the prepared plan over the star-tree docs
     wall, kern, dev, fk, ak = [], [], [], [], []
