@@ -28,32 +28,27 @@ static inline int lim_grid(int64_t n) {
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
 }
 
-// (segment, first doc) sort key of every compacted (segment, key) slot; per-segment entry counts. The counts
-// are wave-aggregated -- one atomic per distinct segment among a wave's 64 entries -- since with few segments
-// every entry would otherwise hit the same counter (10M serialised atomics on one address took 113 ms).
+// (segment, first doc) sort key of every compacted (segment, key) slot
 __global__ void limit_prepare_kernel(const int64_t *__restrict__ slots, int64_t n, const uint64_t *__restrict__ hkeys,
                                      const uint32_t *__restrict__ first_doc, int32_t nseg, uint64_t *__restrict__ sortkey,
-                                     int32_t *__restrict__ idx, int32_t *__restrict__ seg_counts) {
-  const int lane = lane_id();
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {  // wave-uniform trip count
-    const int64_t i = base + threadIdx.x;
-    const bool valid = i < n;
-    uint64_t seg = 0;
-    if (valid) {
-      const int64_t slot = slots[i];
-      seg = hkeys[slot] % (uint64_t)nseg;
-      sortkey[i] = (seg << 32) | (uint64_t)first_doc[slot];
-      idx[i] = (int32_t)i;
-    }
-    uint64_t rem = ballot(valid);
-    while (rem) {
-      const int leader = __builtin_ctzll(rem);
-      const uint64_t s0 = (uint64_t)__shfl((long long)seg, leader);
-      const uint64_t same = ballot(valid && seg == s0);
-      if (lane == leader) atomicAdd(&seg_counts[s0], (int32_t)__popcll(same));
-      rem &= ~same;
-    }
+                                     int32_t *__restrict__ idx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t slot = slots[i];
+    const uint64_t seg = hkeys[slot] % (uint64_t)nseg;
+    sortkey[i] = (seg << 32) | (uint64_t)first_doc[slot];
+    idx[i] = (int32_t)i;
+  }
+}
+
+// Per-segment extent of the (segment, first doc) order, from its run boundaries: first[s] / last[s] = the
+// first / last position of segment s (-1 when it has no entry). No atomics -- counting with one counter per
+// segment serialises every entry of a query with few segments on one address (113 ms for 10M entries).
+__global__ void limit_bounds_kernel(const uint64_t *__restrict__ sk_sorted, int64_t n, int64_t *__restrict__ first,
+                                    int64_t *__restrict__ last) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t seg = sk_sorted[j] >> 32;
+    if (j == 0 || (sk_sorted[j - 1] >> 32) != seg) first[seg] = j;
+    if (j == n - 1 || (sk_sorted[j + 1] >> 32) != seg) last[seg] = j;
   }
 }
 
@@ -136,9 +131,15 @@ __global__ void limit_reduce_kernel(const uint64_t *__restrict__ k, const int64_
 
 // ---- host-callable pieces (runtime.cpp: group_limit) ---------------------------------------------------
 hipError_t launch_limit_prepare(const int64_t *slots, int64_t n, const uint64_t *hkeys, const uint32_t *first_doc,
-                                int32_t nseg, uint64_t *sortkey, int32_t *idx, int32_t *seg_counts, hipStream_t s) {
+                                int32_t nseg, uint64_t *sortkey, int32_t *idx, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  limit_prepare_kernel<<<lim_grid(n), 256, 0, s>>>(slots, n, hkeys, first_doc, nseg, sortkey, idx, seg_counts);
+  limit_prepare_kernel<<<lim_grid(n), 256, 0, s>>>(slots, n, hkeys, first_doc, nseg, sortkey, idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_limit_bounds(const uint64_t *sk_sorted, int64_t n, int64_t *first, int64_t *last, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  limit_bounds_kernel<<<lim_grid(n), 256, 0, s>>>(sk_sorted, n, first, last);
   return hipGetLastError();
 }
 

@@ -70,7 +70,8 @@ hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t nde
                                const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
                                int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_limit_prepare(const int64_t *slots, int64_t n, const uint64_t *hkeys, const uint32_t *first_doc,
-                                int32_t nseg, uint64_t *sortkey, int32_t *idx, int32_t *seg_counts, hipStream_t s);
+                                int32_t nseg, uint64_t *sortkey, int32_t *idx, hipStream_t s);
+hipError_t launch_limit_bounds(const uint64_t *sk_sorted, int64_t n, int64_t *first, int64_t *last, hipStream_t s);
 hipError_t launch_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *k_in, uint64_t *k_out, const void *v_in,
                              void *v_out, bool wide, int64_t n, int end_bit, hipStream_t s);
 hipError_t launch_limit_select(const uint64_t *sk_sorted, const int32_t *idx_sorted, int64_t n, const int64_t *seg_start,
@@ -1029,6 +1030,9 @@ struct Plan {
   hipStream_t graph_stream = nullptr;  // the lane stream the graph was captured on
   bool clean = false;  // device seg_matched / HLL registers are zero (finalize_all reset them last time)
   bool partial_pending = false;  // phip_plan_execute_partial handed the table out; phip_plan_finish is next
+  // one segment, hash table, key space >= numGroupsLimit: the normal pass records every slot's first matched doc
+  // (aggregate.hip seg_keys with one segment: the key is unchanged), so the limit pass starts from its table
+  uint32_t *first_doc = nullptr;
 };
 
 static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
@@ -1891,6 +1895,14 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   const int m_regs = nhll ? (1 << log2m) : 0;
   size_t agg_lds = (size_t)kAggWaves * ring_entries(dq.mode) * 4 + (size_t)kAggWaves * dq.stage_bytes;
   int agg_bpc = 4;
+  void *first_doc = nullptr;
+  if (group_by && dq.mode == GB_HASH && nseg == 1 && gb_key_space >= q->num_groups_limit && q->num_groups_limit > 0) {
+    int32_t rc0 = P.alloc((size_t)dq.num_groups * 4, &first_doc);
+    if (rc0) return rc0;
+    dq.seg_keys = 1;
+    dq.seg_key_mult = 1;
+    dq.first_doc = (uint32_t *)first_doc;
+  }
   if (group_by && dq.mode == GB_HASH) {
     if ((int64_t)nhll * dq.num_groups * m_regs * 4 > ((int64_t)16 << 30))
       return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL registers of %lld hash slots exceed the memory budget",
@@ -2121,6 +2133,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.slab = slab;
   P.hslab = hslab;
   P.fo = fo;
+  P.first_doc = (uint32_t *)first_doc;
   for (auto &e : P.ev) HIP_TRY(hipEventCreate(&e));
   {
     void *h = nullptr;
@@ -2173,6 +2186,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (group_by && dq.mode == GB_HASH) {
     HIP_TRY(hipMemsetAsync(dq.gb_keys, 0xff, (size_t)dq.num_groups * 8, st));  // kHashEmpty
     HIP_TRY(hipMemsetAsync(dq.hash_overflow, 0, 4, st));
+    if (P.first_doc) HIP_TRY(hipMemsetAsync(P.first_doc, 0xff, (size_t)dq.num_groups * 4, st));
   }
   if (group_by && (dq.mode == GB_GLOBAL || dq.mode == GB_HASH)) {
     HIP_TRY(hipMemsetAsync(gtab, 0, (size_t)dq.num_groups * 8, st));  // counts
@@ -2241,6 +2255,15 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
                 (long long)cap);
   int32_t rc;
   void *hk, *tab, *fd, *hll = nullptr, *ovf, *ddq;
+  if (P.first_doc && P.dq.mode == GB_HASH && S == 1) {
+    // the normal pass already holds every (key, first doc) of the one segment: no second aggregation
+    cap = P.dq.num_groups;
+    hk = P.dq.gb_keys;
+    tab = P.gtab;
+    fd = P.first_doc;
+    hll = P.ghll;
+    ovf = P.dq.hash_overflow;
+  } else {
   if ((rc = ws.get("lim_hkeys", (size_t)cap * 8, &hk))) return rc;
   if ((rc = ws.get("lim_table", (size_t)cap * 8 * (1 + naggs), &tab))) return rc;
   if ((rc = ws.get("lim_first", (size_t)cap * 4, &fd))) return rc;
@@ -2269,6 +2292,7 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   HIP_TRY(hipMemcpyAsync(ddq, &dq, sizeof(dq), hipMemcpyHostToDevice, st));
   if (P.total_work > 0)
     HIP_TRY(launch_agg(dq, (const DevAggQuery *)ddq, P.agg_blocks, (size_t)kAggWaves * kRingGroup * 4, st));
+  }
   // compact the occupied slots
   const int64_t nchunks = ceil_div(cap, 1024);
   void *cc, *offs, *slots;
@@ -2294,28 +2318,31 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
       (rc = ws.get("lim_ix0", n8, &ix0)) || (rc = ws.get("lim_ix1", n8, &ix1)) ||
       (rc = ws.get("lim_k2a", n8, &k2a)) || (rc = ws.get("lim_k2b", n8, &k2b)) ||
       (rc = ws.get("lim_s2a", n8, &s2a)) || (rc = ws.get("lim_s2b", n8, &s2b)) ||
-      (rc = ws.get("lim_segc", (size_t)S * 4, &segc)) || (rc = ws.get("lim_segs", (size_t)S * 8, &segs_start)) ||
+      (rc = ws.get("lim_segc", (size_t)S * 16, &segc)) || (rc = ws.get("lim_segs", (size_t)S * 8, &segs_start)) ||
       (rc = ws.get("lim_tmp", std::max(std::max(sort1, sort2), scanb) + 256, &tmp)) ||
       (rc = ws.get("lim_head", n8, &head)) || (rc = ws.get("lim_run", n8, &run)))
     return rc;
-  HIP_TRY(hipMemsetAsync(segc, 0, (size_t)S * 4, st));
+  // sort by (segment, first doc), then every segment's extent from its run boundaries
   HIP_TRY(launch_limit_prepare((const int64_t *)slots, n, (const uint64_t *)hk, (const uint32_t *)fd, S,
-                               (uint64_t *)sk0, (int32_t *)ix0, (int32_t *)segc, st));
-  std::vector<int32_t> seg_counts(S);
-  HIP_TRY(hipMemcpyAsync(seg_counts.data(), segc, (size_t)S * 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  std::vector<int64_t> seg_start(S);
-  int64_t kept = 0, acc = 0;
-  *limit_reached = 0;
-  for (int s = 0; s < S; s++) {
-    seg_start[s] = acc;
-    acc += seg_counts[s];
-    kept += std::min<int64_t>(seg_counts[s], limit);
-    if (seg_counts[s] >= limit) *limit_reached = 1;  // GroupByOperator.java:116: numGroups >= numGroupsLimit
-  }
-  HIP_TRY(hipMemcpyAsync(segs_start, seg_start.data(), (size_t)S * 8, hipMemcpyHostToDevice, st));
+                               (uint64_t *)sk0, (int32_t *)ix0, st));
   const int end1 = 32 + std::max(1, num_bits_per_value(S - 1));
   HIP_TRY(launch_sort_pairs(tmp, &sort1, (const uint64_t *)sk0, (uint64_t *)sk1, ix0, ix1, false, n, end1, st));
+  int64_t *seg_first = (int64_t *)segc, *seg_last = (int64_t *)segc + S;
+  HIP_TRY(hipMemsetAsync(segc, 0xff, (size_t)S * 16, st));
+  HIP_TRY(launch_limit_bounds((const uint64_t *)sk1, n, seg_first, seg_last, st));
+  std::vector<int64_t> bounds(2 * (size_t)S);
+  HIP_TRY(hipMemcpyAsync(bounds.data(), segc, (size_t)S * 16, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  std::vector<int64_t> seg_start(S);
+  int64_t kept = 0;
+  *limit_reached = 0;
+  for (int s = 0; s < S; s++) {
+    const int64_t cnt = bounds[s] < 0 ? 0 : bounds[S + s] - bounds[s] + 1;
+    seg_start[s] = bounds[s] < 0 ? 0 : bounds[s];
+    kept += std::min<int64_t>(cnt, limit);
+    if (cnt >= limit) *limit_reached = 1;  // GroupByOperator.java:116: numGroups >= numGroupsLimit
+  }
+  HIP_TRY(hipMemcpyAsync(segs_start, seg_start.data(), (size_t)S * 8, hipMemcpyHostToDevice, st));
   HIP_TRY(launch_limit_select((const uint64_t *)sk1, (const int32_t *)ix1, n, (const int64_t *)segs_start, limit,
                               (const int64_t *)slots, (const uint64_t *)hk, S, (uint64_t *)k2a, (int64_t *)s2a, st));
   HIP_TRY(launch_sort_pairs(tmp, &sort2, (const uint64_t *)k2a, (uint64_t *)k2b, s2a, s2b, true, n, 64, st));

@@ -129,7 +129,8 @@ hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hip
 }
 hipError_t launch_minmax_i64(const void *, int32_t, int64_t, int64_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_limit_prepare(const int64_t *, int64_t, const uint64_t *, const uint32_t *, int32_t, uint64_t *,
-                                int32_t *, int32_t *, hipStream_t) { return hipSuccess; }
+                                int32_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_limit_bounds(const uint64_t *, int64_t, int64_t *, int64_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_sort_pairs(void *, size_t *temp_bytes, const uint64_t *, uint64_t *, const void *, void *, bool,
                              int64_t, int, hipStream_t) { *temp_bytes = 256; return hipSuccess; }
 hipError_t launch_limit_select(const uint64_t *, const int32_t *, int64_t, const int64_t *, int64_t, const int64_t *,

@@ -132,11 +132,14 @@ LIMIT_QUERIES = [
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nseg", [3, 1])
 @pytest.mark.parametrize("mode", ["auto", "hash"])
 @pytest.mark.parametrize("sql", LIMIT_QUERIES)
-def test_gpu_default_limit_over_100k_groups(sql, mode, many_groups, monkeypatch):
+def test_gpu_default_limit_over_100k_groups(sql, mode, nseg, many_groups, monkeypatch):
+    """nseg 1 + hash: the normal pass records first-seen docs and the limit pass starts from its table."""
     monkeypatch.setenv("PHIP_GB_HASH", "1" if mode == "hash" else "0")
     raws, segs = many_groups
+    raws, segs = raws[:nseg], segs[:nseg]
     qc = parse(sql)
     gblk = _gpu().make_instance_plan(qc, segs).next_block()
     oblk, exact = executor.execute(qc, raws)
