@@ -145,7 +145,7 @@ struct DevNode {
   int32_t lds_off;    // staged region of the leaf's column / inverted words, -1 = not staged
   int32_t bits;       // scan leaves: bits per value of the column
   int32_t small_set;  // DICT_SET with card <= 64: membership in set_mask
-  int32_t pad;
+  int32_t aux_stride; // INVERTED: u64 words per 2048-doc tile in aux (32 x the entry's inverted leaves, interleaved)
   uint64_t set_mask;
   const void *aux;    // DICT_SET: u32 bitset over dict ids; DOC_RANGES: int32 pairs;
                       // INVERTED: u64 doc bitmap words of the segment (materialised);
@@ -279,7 +279,7 @@ struct RoaringGroup {
   int32_t task_begin;    // containers [task_begin, task_end) of the RoaringTask array
   int32_t task_end;
   int32_t key;
-  int32_t pad;
+  int32_t tile_words;    // u64 words per 2048-doc tile of the output (the entry's leaves interleaved per tile)
 };
 
 }  // namespace phip

@@ -135,7 +135,7 @@ __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__
 #pragma unroll 8
       for (int g = 0; g < kTileGroups; g++) r = (r << 1) | __builtin_amdgcn_ubfe(w[2 * g], sh, 1u);
     } else {
-      const PHIP_GLB uint64_t *w = (const PHIP_GLB uint64_t *)n->aux + (t.doc0 >> 6);
+      const PHIP_GLB uint64_t *w = (const PHIP_GLB uint64_t *)n->aux + (int64_t)(t.doc0 >> 11) * n->aux_stride;
 #pragma unroll 8
       for (int g = 0; g < kTileGroups; g++) r = r + r + (uint32_t)((w[g] >> lane) & 1ull);
     }
@@ -1160,8 +1160,9 @@ __global__ __launch_bounds__(kRoaringWaves * 64) void roaring_or_kernel(const Ro
       }
     }
     __syncthreads();
-    uint64_t *out = g.out_words + (int64_t)g.key * 1024;  // 65536 docs per container = 1024 words
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) out[i] = bm[i];
+    // 65536 docs per container = 1024 words = 32 tiles of 32 words, each tile's at tile * tile_words
+    uint64_t *out = g.out_words + (int64_t)g.key * 32 * g.tile_words;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) out[(i >> 5) * g.tile_words + (i & 31)] = bm[i];
     __syncthreads();
   }
 }

@@ -1320,8 +1320,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     int seg;
     int col;
     const phip_filter_node *src;
+    int entry;  // (segment, program) entry whose program holds the leaf
+    int slot;   // index among that entry's inverted leaves
   };
   std::vector<InvLeaf> inv_leaves;
+  int num_entries = 0;  // (segment, program) entries, pruned ones included
   int64_t total_work = 0;
   int64_t total_docs = 0;
   std::vector<DevSeg> dsegs;  // (segment, program) entries with work only, segment-major
@@ -1474,7 +1477,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             break;
           case PHIP_LEAF_INVERTED:
             if (cs->inv_begin.empty()) { rc = fail(PHIP_ERR_INVALID, "column %s has no inverted index", cs->name.c_str()); break; }
-            inv_leaves.push_back({ni, s, colidx[s][fn.column], &fn});
+            {
+              int slot = 0;
+              for (const InvLeaf &o : inv_leaves) slot += o.entry == num_entries ? 1 : 0;
+              inv_leaves.push_back({ni, s, colidx[s][fn.column], &fn, num_entries, slot});
+            }
             break;
           default: break;
         }
@@ -1553,6 +1560,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       hull_hi = hst.back().hi;
     }
     ds.node_end = (int32_t)nodes.size();
+    num_entries++;
     if (hull_lo > hull_hi) continue;  // no candidate doc: the segment is pruned (no work)
     ds.tile0 = (int32_t)(hull_lo / kTileDocs);
     ds.num_work = (int32_t)(hull_hi / kTileDocs - ds.tile0 + 1);
@@ -1584,17 +1592,30 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   dq.num_segs = (int32_t)dsegs.size();
   const size_t segs_off = blob.reserve(sizeof(DevSeg) * std::max<size_t>(dsegs.size(), 1));
 
-  // inverted leaves: dense doc words per leaf + roaring container tasks
+  // inverted leaves: dense doc words per leaf + roaring container tasks. The L inverted leaves of one
+  // (segment, program) entry are interleaved per 2048-doc tile -- tile t holds leaf 0's 32 words, then leaf
+  // 1's, ... -- so the filter kernel stages all of them with one L x 256-byte LDS-DMA region per tile instead of
+  // L quarter-filled 256-byte ones.
   std::vector<RoaringTask> tasks;
   size_t inv_words_total = 0;
   std::vector<size_t> inv_word_off(inv_leaves.size()), inv_word_nw(inv_leaves.size());
+  std::vector<int> entry_leaves(num_entries, 0);
+  std::vector<size_t> entry_off(num_entries, 0);
+  for (const InvLeaf &L : inv_leaves) entry_leaves[L.entry]++;
   for (size_t i = 0; i < inv_leaves.size(); i++) {
-    const Segment &sg = *segs[inv_leaves[i].seg];
+    const InvLeaf &L = inv_leaves[i];
+    const Segment &sg = *segs[L.seg];
     size_t nw = (size_t)std::max(round_up(sg.num_docs, 65536), round_up(sg.num_docs, kTileDocs)) / 64;  // whole keys
     inv_word_nw[i] = nw;
-    inv_word_off[i] = inv_words_total;
-    inv_words_total += nw;
+    if (L.slot == 0) {
+      entry_off[L.entry] = inv_words_total;
+      inv_words_total += nw * entry_leaves[L.entry];
+    }
+    inv_word_off[i] = entry_off[L.entry] + 32 * (size_t)L.slot;
   }
+  std::vector<int32_t> node_inv_stride(nodes.size(), 0);   // u64 words per tile of an inverted leaf's aux
+  std::vector<int32_t> node_inv_slot(nodes.size(), 0);
+  std::vector<int32_t> node_inv_leaves(nodes.size(), 0);
   void *inv_words = nullptr;
   if (inv_words_total) {
     int32_t rc = P.alloc(inv_words_total * 8, &inv_words);
@@ -1605,7 +1626,12 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const InvLeaf &L = inv_leaves[i];
     const ColumnStore &cs = segs[L.seg]->cols[L.col];
     uint64_t *words = (uint64_t *)inv_words + inv_word_off[i];
+    const int32_t tile_words = 32 * entry_leaves[L.entry];
     nodes[L.node].aux = words;
+    nodes[L.node].aux_stride = tile_words;
+    node_inv_stride[L.node] = tile_words;
+    node_inv_slot[L.node] = L.slot;
+    node_inv_leaves[L.node] = entry_leaves[L.entry];
     const size_t first = tasks.size();
     for (int k = 0; k < L.src->count; k++) {
       int32_t id = L.src->ids[k];
@@ -1637,7 +1663,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       g.task_begin = (int32_t)t;
       g.task_end = (int32_t)e;
       g.key = key;
-      g.pad = 0;
+      g.tile_words = tile_words;
       rgroups.push_back(g);
       t = e;
     }
@@ -1672,6 +1698,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       off += bytes + 2 * kStagePad;
       return lds_off;
     };
+    int32_t inv_region = -2;  // -2: not added yet, -1: did not fit
     for (int i = ds.node_begin; i < ds.node_end; i++) {
       DevNode &dn = nodes[i];
       if (dn.op != DOP_LEAF) continue;
@@ -1680,7 +1707,12 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         if (dc.lds_off < 0) dc.lds_off = add_region((const uint8_t *)dc.words, 256 * dc.bits);
         dn.lds_off = dc.lds_off;
       } else if (dn.leaf_kind == PHIP_LEAF_INVERTED && dn.aux != nullptr) {
-        dn.lds_off = add_region((const uint8_t *)dn.aux, 256);
+        // the entry's interleaved inverted words: one region of L x 256 bytes per tile, leaf j at 256 j
+        if (inv_region == -2) {
+          const uint64_t *entry_base = (const uint64_t *)dn.aux - 32 * node_inv_slot[i];
+          inv_region = add_region((const uint8_t *)entry_base, 256 * node_inv_leaves[i]);
+        }
+        dn.lds_off = inv_region < 0 ? -1 : inv_region + 256 * node_inv_slot[i];
       }
     }
     stage_stride = std::max(stage_stride, off);
