@@ -2270,7 +2270,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
 // have dropped keys. Re-aggregate per (segment, key) with first-seen docs, keep each segment's first `limit`
 // keys and merge them by key. On return keys / vals / longs / hll and *ngroups describe the kept groups.
 static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t matched, void **keys, void **ov, void **ol,
-                           void **oh, int64_t *ngroups, int32_t *limit_reached) {
+                           void **oh, int64_t *ngroups, int32_t *limit_reached, const int64_t *normal_offs) {
   const int32_t S = P.nseg, naggs = P.naggs, nhll = P.nhll, m_regs = P.m_regs;
   const int64_t limit = P.num_groups_limit;
   int64_t space = 1;
@@ -2287,7 +2287,8 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
                 (long long)cap);
   int32_t rc;
   void *hk, *tab, *fd, *hll = nullptr, *ovf, *ddq;
-  if (P.first_doc && P.dq.mode == GB_HASH && S == 1) {
+  const bool reuse = P.first_doc && P.dq.mode == GB_HASH && S == 1;
+  if (reuse) {
     // the normal pass already holds every (key, first doc) of the one segment: no second aggregation
     cap = P.dq.num_groups;
     hk = P.dq.gb_keys;
@@ -2325,15 +2326,20 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   if (P.total_work > 0)
     HIP_TRY(launch_agg(dq, (const DevAggQuery *)ddq, P.agg_blocks, (size_t)kAggWaves * kRingGroup * 4, st));
   }
-  // compact the occupied slots
+  // compact the occupied slots (reusing the normal pass's table: its counts are already known)
   const int64_t nchunks = ceil_div(cap, 1024);
   void *cc, *offs, *slots;
-  if ((rc = ws.get("lim_cc", (size_t)nchunks * 4, &cc))) return rc;
-  if ((rc = ws.get("lim_offs", (size_t)(nchunks + 1) * 8, &offs))) return rc;
-  HIP_TRY(launch_group_count((const uint64_t *)tab, cap, (int32_t *)cc, nchunks, (int64_t *)offs, st));
   int64_t n = 0;
   uint32_t overflow = 0;
-  HIP_TRY(hipMemcpyAsync(&n, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
+  if (reuse && normal_offs) {
+    offs = (void *)normal_offs;
+    n = *ngroups;
+  } else {
+    if ((rc = ws.get("lim_cc", (size_t)nchunks * 4, &cc))) return rc;
+    if ((rc = ws.get("lim_offs", (size_t)(nchunks + 1) * 8, &offs))) return rc;
+    HIP_TRY(launch_group_count((const uint64_t *)tab, cap, (int32_t *)cc, nchunks, (int64_t *)offs, st));
+    HIP_TRY(hipMemcpyAsync(&n, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipMemcpyAsync(&overflow, ovf, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: hash table overflow (%lld slots)", (long long)cap);
@@ -2377,7 +2383,8 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   HIP_TRY(hipMemcpyAsync(segs_start, seg_start.data(), (size_t)S * 8, hipMemcpyHostToDevice, st));
   HIP_TRY(launch_limit_select((const uint64_t *)sk1, (const int32_t *)ix1, n, (const int64_t *)segs_start, limit,
                               (const int64_t *)slots, (const uint64_t *)hk, S, (uint64_t *)k2a, (int64_t *)s2a, st));
-  HIP_TRY(launch_sort_pairs(tmp, &sort2, (const uint64_t *)k2a, (uint64_t *)k2b, s2a, s2b, true, n, 64, st));
+  // one segment: the kept entries are exactly the first `kept` positions (the rest sort last anyway)
+  HIP_TRY(launch_sort_pairs(tmp, &sort2, (const uint64_t *)k2a, (uint64_t *)k2b, s2a, s2b, true, S == 1 ? kept : n, 64, st));
   HIP_TRY(launch_limit_runs(tmp, &scanb, (const uint64_t *)k2b, kept, (int32_t *)head, (int32_t *)run, st));
   int32_t runs = 0;
   if (kept > 0) HIP_TRY(hipMemcpyAsync(&runs, (int32_t *)run + kept - 1, 4, hipMemcpyDeviceToHost, st));
@@ -2572,31 +2579,34 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       P.clean = true;
       return PHIP_OK;
     }
-    rc = ws.get("gb_keys", (size_t)std::max<int64_t>(ngroups, 1) * 8, &keys);
-    if (rc) return rc;
-    void *ov, *ol, *oh = nullptr;
-    rc = ws.get("gb_out_vals", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ov);
-    if (rc) return rc;
-    rc = ws.get("gb_out_longs", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ol);
-    if (rc) return rc;
-    if (nhll) {
-      rc = ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * m_regs, &oh);
-      if (rc) return rc;
-    }
-    HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
-    HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, gather_kinds, (const uint64_t *)gtab,
-                                (const uint32_t *)ghll, nhll, log2m, (double *)ov, (int64_t *)ol, (uint8_t *)oh, st));
+    void *ov = nullptr, *ol = nullptr, *oh = nullptr;
     uint32_t overflow = 0;
-    if (dq.mode == GB_HASH) {
-      HIP_TRY(launch_hash_keys((int64_t *)keys, ngroups, dq.gb_keys, st));
-      HIP_TRY(hipMemcpyAsync(&overflow, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
+    // some segment may have reached numGroupsLimit: the first-seen pass decides which keys it kept (and the
+    // normal pass's compaction would be thrown away)
+    const bool limit_pass = mode == EXEC_FULL && P.num_groups_limit > 0 && ngroups >= P.num_groups_limit;
+    if (!limit_pass) {
+      rc = ws.get("gb_keys", (size_t)std::max<int64_t>(ngroups, 1) * 8, &keys);
+      if (rc) return rc;
+      rc = ws.get("gb_out_vals", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ov);
+      if (rc) return rc;
+      rc = ws.get("gb_out_longs", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ol);
+      if (rc) return rc;
+      if (nhll) {
+        rc = ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * m_regs, &oh);
+        if (rc) return rc;
+      }
+      HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
+      HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, gather_kinds, (const uint64_t *)gtab,
+                                  (const uint32_t *)ghll, nhll, log2m, (double *)ov, (int64_t *)ol, (uint8_t *)oh, st));
+      if (dq.mode == GB_HASH) HIP_TRY(launch_hash_keys((int64_t *)keys, ngroups, dq.gb_keys, st));
     }
-    if (mode == EXEC_FULL && P.num_groups_limit > 0 && ngroups >= P.num_groups_limit) {
-      // some segment may have reached numGroupsLimit: the first-seen pass decides which keys it kept
+    if (dq.mode == GB_HASH) HIP_TRY(hipMemcpyAsync(&overflow, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
+    if (limit_pass) {
       HIP_TRY(hipStreamSynchronize(st));
       if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
       const int64_t matched_docs = has_filter ? (int64_t)fin[32] : docs_in_work;
-      rc = group_limit(P, ws, st, matched_docs, &keys, &ov, &ol, &oh, &ngroups, &r.num_groups_limit_reached);
+      rc = group_limit(P, ws, st, matched_docs, &keys, &ov, &ol, &oh, &ngroups, &r.num_groups_limit_reached,
+                       (const int64_t *)offs);
       if (rc) return rc;
     }
     if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0 || P.order_terms.num_terms > 0)) {

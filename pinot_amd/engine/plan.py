@@ -573,9 +573,17 @@ class GpuCombineOperator:
             ng = r.num_groups
             m = 1 << max([p[4] for p in self.prims if p[0] == _lib.AGG_HLL] + [0])
             # (no groups: the library's arrays may be null)
-            vals = np.ctypeslib.as_array(r.values, shape=(ng * na,)).reshape(ng, na).copy() if ng * na else np.zeros((ng, na))
-            longs = (np.ctypeslib.as_array(r.long_values, shape=(ng * na,)).reshape(ng, na).copy() if ng * na
-                     else np.zeros((ng, na), np.int64))
+            if not self.query.group_by and ng == 1:
+                # one row: read its few slots through the pointers (a numpy view + copy costs ~6 us per array,
+                # on every query of the server loop)
+                vals = [[r.values[i] for i in range(na)]]
+                longs = [[r.long_values[i] for i in range(na)]]
+            else:
+                # as nested lists: the per-group loop below indexes them element by element
+                vals = (np.ctypeslib.as_array(r.values, shape=(ng * na,)).reshape(ng, na).tolist() if ng * na
+                        else [[0.0] * na for _ in range(ng)])
+                longs = (np.ctypeslib.as_array(r.long_values, shape=(ng * na,)).reshape(ng, na).tolist() if ng * na
+                         else [[0] * na for _ in range(ng)])
             hll = None
             if r.num_hll and ng:
                 hll = np.ctypeslib.as_array(r.hll_registers, shape=(ng * r.num_hll * m,)).reshape(ng, r.num_hll, m).copy()
@@ -589,11 +597,11 @@ class GpuCombineOperator:
             def prim_value(g, i):
                 f = self.prims[i][0]
                 if f == _lib.AGG_COUNT:
-                    return int(longs[g, i])
+                    return int(longs[g][i])
                 if f == _lib.AGG_SUM:
-                    return int(longs[g, i]) if exact[i] else float(vals[g, i])
+                    return int(longs[g][i]) if exact[i] else float(vals[g][i])
                 if f in (_lib.AGG_MIN, _lib.AGG_MAX):
-                    return float(vals[g, i])
+                    return float(vals[g][i])
                 return hll[g, hll_slot[i]].copy()
 
             def intermediates(g):
