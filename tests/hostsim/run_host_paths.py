@@ -47,6 +47,23 @@ for q in ("SELECT g, h, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTH
           "SELECT SUM(r), AVG(d), DISTINCTCOUNTHLL(g) FROM t WHERE h IN (1, 2) OR m > 0",
           "SELECT COUNT(*) FROM t WHERE NOT (h = 1 AND (g = 'k3' OR d < 0.5))"):
     pm.make_instance_plan(parse(q), gs).next_block()
+# filtered aggregations: several filter programs in one plan (per-entry staging, interleaved inverted words,
+# per-program statistics), and the descriptor checks of num_filter_programs / aggregation.program
+pm.make_instance_plan(parse("SELECT COUNT(*), SUM(m) FILTER(WHERE h IN (1, 2)), MIN(d) FILTER(WHERE h = 4 AND "
+                            "g <> 'k7'), DISTINCTCOUNTHLL(g) FILTER(WHERE m > 0) FROM t WHERE h <> 3"), gs).next_block()
+from pinot_amd.engine.plan import GpuCombineOperator  # noqa: E402
+from pinot_amd.query.context import FilterContext  # noqa: E402
+base = parse("SELECT COUNT(*), SUM(m) FROM t")
+flt = parse("SELECT COUNT(*) FROM t WHERE h = 1").filter
+for progs, aprog, gb in (([flt] * 9, [0, 8], False), ([flt, None], [0, 2], False), ([flt, None], [0, 1], True)):
+    q = parse("SELECT h, COUNT(*), SUM(m) FROM t GROUP BY h") if gb else base
+    op = GpuCombineOperator(q, gs, 100_000, programs=(progs, aprog))
+    try:
+        op.next_block()
+        raise SystemExit(f"descriptor accepted: {len(progs)} programs, {aprog}, group-by {gb}")
+    except _lib.PhipError:
+        pass
+    op.close()
 os.environ["PHIP_GB_HASH"] = "1"  # the hash-table group-by's host path (allocation, key decode)
 pm.make_instance_plan(parse("SELECT g, h, COUNT(*), SUM(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY g, h"), gs).next_block()
 del os.environ["PHIP_GB_HASH"]
