@@ -1903,7 +1903,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   int nbuf = 0, fbpc = 0;
   {
     const char *env = getenv("PHIP_FILTER_BPC");  // measurement override
-    const int want = env ? std::max(1, std::min(8, atoi(env))) : (conj_only ? 6 : 4);
+    int want = env ? std::max(1, std::min(8, atoi(env))) : (conj_only ? 6 : 4);
+    // A mid-sized scan (a few tiles per wave at the default) streams better with fewer, longer-lived waves and a
+    // deeper ring: each wave's ring prologue is paid once per range. Measured on SSB SF100 sorted Q1.1 (42K
+    // tiles): 6 -> 3 workgroups per CU, filter 0.074 -> 0.065 ms; the unsorted layout (293K tiles, 48 per wave)
+    // and small queries (every wave one or two tiles: latency) keep the default (tools/ab_env.sh, bpc A/B).
+    const int64_t kMinTilesPerWave = 12;
+    const int64_t waves_at = (int64_t)dev->num_cus * want * kFilterWaves;
+    if (!env && total_work >= 4 * waves_at)
+      while (want > 2 && total_work < kMinTilesPerWave * (int64_t)dev->num_cus * want * kFilterWaves) want--;
     const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * 128 * 2 : 0;  // filter.hip kFusedRing u16
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
       const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024 - 1024) / bpc - fring) / ((int64_t)kFilterWaves * stage_stride));
