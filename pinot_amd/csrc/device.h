@@ -163,7 +163,7 @@ struct DevFilter {
   int32_t xcd_walk;      // 1: XCD-sweep tile order (grid multiple of 8); 0: contiguous range per wave
   int32_t min_dma;       // min over segments of LDS-DMA wave-instructions per tile (vmcnt lower bound)
   int32_t probe;         // measurement only (PHIP_FILTER_PROBE): 1 = stream the tiles, skip the evaluation
-  int32_t pad_probe;
+  int32_t contig_inline;  // 1: range scans of the contiguous evaluator inline (0: through contig_scan_any; A/B)
   uint32_t *mask_out;    // optional: [total_work][64] lane-major tile masks
   uint64_t *partials;    // [num_blocks][2]: matched docs, entries scanned in filter
   uint64_t *seg_matched; // [num query segments]

@@ -422,8 +422,9 @@ __device__ __forceinline__ uint32_t contig_scan(const PHIP_LDS uint32_t *w, uint
   }
 }
 
-// The width / kind dispatch as a real call: its 93 unrolled bodies would otherwise be inlined into the
-// filter kernel and push it past the VGPR / SGPR budget (spills on every tile).
+// The width / kind dispatch of the set kinds as a real call: all 93 unrolled bodies inlined pushed the filter
+// kernel past the VGPR budget (spills on every tile). The 31 range bodies alone fit without spills and are
+// inlined (eval_leaf_contig): the call saves and restores its VGPRs through scratch on every tile.
 __device__ __noinline__ uint32_t contig_scan_any(const PHIP_LDS uint32_t *w, int B, int k, uint32_t LO, uint32_t SPAN,
                                                  uint64_t set, uint32_t myw, bool excl) {
   switch (B) {
@@ -439,7 +440,7 @@ __device__ __noinline__ uint32_t contig_scan_any(const PHIP_LDS uint32_t *w, int
 }
 
 __device__ __forceinline__ uint32_t eval_leaf_contig(cseg_t &seg, cnode_t *__restrict__ n, uint32_t valid,
-                                                     const Tile &t, uint32_t &scanned) {
+                                                     const Tile &t, uint32_t &scanned, bool inl) {
   const int lane = lane_id();
   const int kind = n->leaf_kind;
   if (kind == PHIP_LEAF_MATCH_ALL) return valid;
@@ -476,6 +477,14 @@ __device__ __forceinline__ uint32_t eval_leaf_contig(cseg_t &seg, cnode_t *__res
   const uint32_t LO = (uint32_t)n->lo << (32 - B);
   const uint32_t SPAN = (uint32_t)(n->hi - n->lo) << (32 - B);
   const int k = kind == PHIP_LEAF_DICT_RANGE ? 0 : (n->small_set ? 1 : 2);
+  if (inl && k == 0) {  // range scans inline (no call: its VGPR save / restore goes through scratch)
+    switch (B) {
+#define PHIP_CI(b) \
+  case b: return contig_scan<b, 0>(w, LO, SPAN, 0ull, 0u, false) & valid;
+      PHIP_B_CASES(PHIP_CI)
+#undef PHIP_CI
+    }
+  }
   const uint32_t myw = (k == 2 && lane < n->count) ? ((const PHIP_GLB uint32_t *)n->aux)[lane] : 0u;
   return contig_scan_any(w, B, k, LO, SPAN, n->set_mask, myw, n->exclusive != 0) & valid;
 }
@@ -483,7 +492,7 @@ __device__ __forceinline__ uint32_t eval_leaf_contig(cseg_t &seg, cnode_t *__res
 // The operand stack is a shift register (s0 = top): a push / pop is a handful of v_mov, not a scalar branch
 // tree on the stack pointer -- the interpreter's SALU / branch count per tile is what bounds this path.
 __device__ __forceinline__ uint32_t eval_filter_contig(cseg_t &seg, cnode_t *__restrict__ nodes, uint32_t valid,
-                                                       const Tile &t, uint32_t &scanned) {
+                                                       const Tile &t, uint32_t &scanned, bool inl) {
   uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
   int i = seg.node_begin;
   const int end = seg.node_end;
@@ -499,7 +508,7 @@ __device__ __forceinline__ uint32_t eval_filter_contig(cseg_t &seg, cnode_t *__r
           continue;
         }
       }
-      const uint32_t v = eval_leaf_contig(seg, n, valid, t, scanned);
+      const uint32_t v = eval_leaf_contig(seg, n, valid, t, scanned, inl);
       s5 = s4;
       s4 = s3;
       s3 = s2;
@@ -1048,7 +1057,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
       }
       scanned_t = (uint32_t)seg.conj * (uint32_t)tl.valid_docs;
     } else if (seg.contig) {
-      mask = eval_filter_contig(seg, nodes, contig_valid(tl.valid_docs, lane), tl, scanned_t);
+      mask = eval_filter_contig(seg, nodes, contig_valid(tl.valid_docs, lane), tl, scanned_t, q.contig_inline != 0);
       if (st) mask = contig_to_lane_major(mask);  // (popcounts do not care about the layout)
     } else {
       mask = seg.node_end > seg.node_begin ? eval_filter(seg, nodes, valid, tl, scanned_t) : valid;

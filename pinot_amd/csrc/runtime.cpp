@@ -1995,6 +1995,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   {
     const char *pe = getenv("PHIP_FILTER_PROBE");
     fq.probe = pe ? atoi(pe) : 0;
+    // range scans of the contiguous evaluator inline: the call's register save / restore through scratch cost
+    // 4-9 % of C4's filter kernel (tools/c4_ab.py, profiles/r02f_c4_inline_ab.log); "0" = the call (A/B)
+    const char *ie = getenv("PHIP_CONTIG_INLINE");
+    fq.contig_inline = ie ? atoi(ie) : 1;
   }
   fq.min_dma = 0;
   for (size_t i = 0; i < dsegs.size(); i++)
