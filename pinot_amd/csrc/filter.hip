@@ -940,7 +940,8 @@ __device__ __forceinline__ void cursor_issue(StageCursor<kS> &c, uint32_t lbase,
 
 template <bool kConjOnly, int NA>
 __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel(DevFilter q) {
-  constexpr int kS = kConjOnly ? (NA > 0 ? kMaxConj + kMaxAggStage : kMaxConj) : kMaxStage;
+  constexpr int kSConj = NA > 0 ? kMaxConj + kMaxAggStage : kMaxConj;
+  constexpr int kS = kConjOnly ? (kSConj < kMaxStage ? kSConj : kMaxStage) : kMaxStage;  // (DevSeg.stage size)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);

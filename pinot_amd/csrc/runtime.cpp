@@ -1850,7 +1850,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             const bool dense = seg_est[i] * (1024.0 / std::max(1, dc.bits)) >= kStreamValueMin;
             if (!(sv ? atoi(sv) != 0 : dense)) continue;
             const int32_t bytes = 256 * dc.bits;
-            if (ds.num_stage >= kMaxConj + kMaxAggStage || off + bytes + 2 * kStagePad > kSlotBudget) continue;
+            // (DevSeg.stage holds kMaxStage sources; the fused kernel's cursor takes up to kMaxConj + kMaxAggStage)
+            if (ds.num_stage >= std::min(kMaxStage, kMaxConj + kMaxAggStage) || off + bytes + 2 * kStagePad > kSlotBudget)
+              continue;
             dc.lds_off = off + kStagePad;
             ds.stage[ds.num_stage++] = {(const uint8_t *)dc.words, bytes, dc.lds_off};
             ds.num_dma += (int32_t)ceil_div(bytes, 1024);
