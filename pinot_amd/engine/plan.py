@@ -152,7 +152,8 @@ def compile_predicate(seg: GpuSegment, pred) -> object:
         fwd = (seg.num_docs * m.bits_per_element + 7) // 8
         inv_ok = os.environ.get("PINOT_AMD_INVERTED", "") == "always"
         if not inv_ok:
-            inv_ok = seg.inverted_bytes(column, ids) <= INVERTED_COST_RATIO * fwd
+            ratio = float(os.environ.get("PINOT_AMD_INVERTED_RATIO", INVERTED_COST_RATIO))  # (measurement override)
+            inv_ok = seg.inverted_bytes(column, ids) <= ratio * fwd
         if inv_ok:
             if ev.kind == "range":
                 return _Leaf(_lib.LEAF_INVERTED, column, ids=ids)
