@@ -173,7 +173,10 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
 // memory round trips instead of one per 64 matched docs. Lanes whose doc did not match load the
 // tile's first doc (always valid) and contribute the identity.
 // ------------------------------------------------------------------------------------------------
-constexpr int kBatch = 4;
+#ifndef PHIP_KBATCH
+#define PHIP_KBATCH 4  // (A/B builds override it)
+#endif
+constexpr int kBatch = PHIP_KBATCH;
 
 template <int U>
 __device__ __forceinline__ void batch_docs(int32_t doc, uint32_t act, int32_t safe, int32_t (&d)[U]) {

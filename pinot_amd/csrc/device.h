@@ -27,7 +27,10 @@ constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;
 // per-wave ring of matched doc ids (u32): GB_NONE batches up to 4 chunks (+ one group), the group-by walks
 // take one chunk at a time (their LDS goes to the table)
-constexpr int kRingAgg = 512;
+#ifndef PHIP_KBATCH
+#define PHIP_KBATCH 4  // agg_common.h kBatch (A/B builds override it)
+#endif
+constexpr int kRingAgg = 128 * PHIP_KBATCH;  // two batches of kBatch chunks
 constexpr int kRingGroup = 128;
 constexpr int ring_entries(int mode) { return mode == 0 ? kRingAgg : kRingGroup; }
 constexpr int kMaxAggStage = 4;      // staged aggregation columns
