@@ -1033,6 +1033,7 @@ struct Plan {
   // one segment, hash table, key space >= numGroupsLimit: the normal pass records every slot's first matched doc
   // (aggregate.hip seg_keys with one segment: the key is unchanged), so the limit pass starts from its table
   uint32_t *first_doc = nullptr;
+  bool total_events = true;  // record ev[0] / ev[3] (phip_result.device_ms); PHIP_TOTAL_EVENTS=0 skips them (A/B)
 };
 
 static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
@@ -2180,6 +2181,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.hslab = hslab;
   P.fo = fo;
   P.first_doc = (uint32_t *)first_doc;
+  if (const char *te = getenv("PHIP_TOTAL_EVENTS")) P.total_events = atoi(te) != 0;
   for (auto &e : P.ev) HIP_TRY(hipEventCreate(&e));
   {
     void *h = nullptr;
@@ -2215,7 +2217,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   const size_t filter_lds = P.filter_lds, agg_lds = P.agg_lds;
   const int64_t filter_nwords = P.filter_nwords;
   const bool filter_words = P.want_bitmap;
-  HIP_TRY(hipEventRecord(P.ev[0], st));
+  if (P.total_events) HIP_TRY(hipEventRecord(P.ev[0], st));
   // seg_matched and the HLL registers are zero between executions (finalize_all resets them); after a
   // failed execution they are cleared here
   const size_t hll_words = nhll && !group_by ? ((size_t)nhll << P.log2m) : 0;
@@ -2273,7 +2275,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
                                 filter_blocks, dev_kinds + naggs, (uint64_t *)seg_matched, P.nmatch, dq.hll_regs,
                                 (int)hll_words, P.pinned_dev, st));
   }
-  if (!group_by) HIP_TRY(hipEventRecord(P.ev[3], st));
+  if (!group_by && P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
   (void)fin_agg;
   (void)fin_filter;
   (void)fo;
@@ -2680,7 +2682,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       }
       if (nhll) HIP_TRY(hipMemcpyAsync(impl->hll.data(), oh, impl->hll.size(), hipMemcpyDeviceToHost, st));
     }
-    HIP_TRY(hipEventRecord(P.ev[3], st));
+    if (P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
     if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
     impl->keys.resize(ngroups * P.num_group_by);
@@ -2728,8 +2730,9 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     if (nhll) for (size_t i = 0; i < ((size_t)nhll << log2m); i++) impl->hll[i] = (uint8_t)hll_host[i];
   }
   float t_all = 0.f, t_scan = 0.f, t_filter = 0.f, t_agg = 0.f;
-  HIP_TRY(hipEventElapsedTime(&t_all, P.ev[0], P.ev[3]));
   HIP_TRY(hipEventElapsedTime(&t_scan, P.ev[1], P.ev[2]));
+  if (P.total_events) HIP_TRY(hipEventElapsedTime(&t_all, P.ev[0], P.ev[3]));
+  else t_all = t_scan;
   HIP_TRY(hipEventElapsedTime(&t_filter, P.ev[1], P.ev[4]));
   HIP_TRY(hipEventElapsedTime(&t_agg, P.ev[4], P.ev[2]));
   r.filter_kernel_ms = has_filter ? t_filter : 0.0;
