@@ -20,7 +20,8 @@ kernel from this round's rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE pa
 (profiles/<round>_traffic.json, tools/traffic.py), or null.
 
 cpu_baseline: oracle/cpu_scan.c, an OpenMP C restatement of Pinot's CPU server path ("restatement, not
-Pinot": no JVM here), over the SAME segments and queries, OMP_NUM_THREADS workers (16 on the GPU box).
+Pinot": no JVM here), over the SAME segments and queries, one worker per usable CPU (the affinity mask capped
+by the cgroup quota: oracle/cpu_baseline.usable_cpus).
 """
 import argparse
 import json
@@ -34,7 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROUND = "r02"
+ROUND = "r03"
 
 
 def load_layout(ssb, sf, world, rank, cols, seed, layout, keep_host):
@@ -84,7 +85,8 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
             ts = time.perf_counter()
             blk = run_query(q)
             lat[q].append((time.perf_counter() - ts) * 1e3)
-            kstats[q].append((blk.filter_kernel_ms, blk.agg_kernel_ms, blk.filter_bytes, blk.agg_bytes))
+            kstats[q].append((blk.filter_kernel_ms, blk.agg_kernel_ms, blk.filter_bytes, blk.agg_bytes,
+                               bool(getattr(blk, "fused", False))))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -98,34 +100,58 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
     return elapsed, lat, kstats
 
 
-def roofline(kstats, queries, traffic, layout):
-    """Per-kernel achieved bandwidth on algorithmic bytes; headline = the kernel with the most time."""
+# kernel families of one query execution: a plain filter launch, a filter launch that aggregated its own tiles
+# (fused), and a separate aggregation launch. The FETCH_SIZE x 2 correction (MI355X_MICROARCH.md §HBM) is
+# calibrated for wide coalesced streams only: the plain filter streams, the aggregation and fused launches
+# gather, so their `traffic` is the raw FETCH + WRITE (both figures are reported).
+STREAMING = {"filter_kernel"}
+
+
+def roofline(kstats, queries, traffic, layout, steps):
+    """Per-kernel achieved bandwidth on algorithmic bytes; headline = the kernel with the most time per step
+    (launches per step x mean launch time)."""
     kernels = {}
-    for name, ti, bi in (("filter_kernel", 0, 2), ("agg_kernel", 1, 3)):
-        ms = [s[ti] for q in queries for s in kstats[q]]
-        by = [s[bi] for q in queries for s in kstats[q]]
-        launches = sum(1 for x in ms if x > 0)
-        if not launches:
+    fams = {"filter_kernel": lambda s: (s[0] if not s[4] else 0.0, s[2]),
+            "fused_filter_agg": lambda s: (s[0] if s[4] else 0.0, s[2]),
+            "agg_kernel": lambda s: (s[1], s[3])}
+    for name, pick in fams.items():
+        ms, by, per_q = [], [], {}
+        for q in queries:
+            xs = [pick(s) for s in kstats[q]]
+            for t, b in xs:
+                if t > 0:
+                    ms.append(t)
+                    by.append(b)
+            per_q[q] = round(float(np.mean([t for t, _ in xs])), 4)
+        if not ms:
             continue
+        launches = len(ms)
         mean_ms = sum(ms) / launches
         mean_b = sum(by) / launches
         ach = mean_b / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
         tr = ((traffic or {}).get(layout) or {}).get(name)
-        kernels[name] = {"ms_per_launch": round(mean_ms, 4), "alg_bytes_per_launch": int(mean_b),
-                         "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                         "traffic_per_launch": tr,
-                         "traffic_frac": (round(tr / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
-                         "time_share": None, "per_query_ms": {q: round(float(np.mean([s[ti] for s in kstats[q]])), 4)
-                                                              for q in queries}}
-    tot = sum(k["ms_per_launch"] for k in kernels.values()) or 1.0
+        tsel = None
+        if isinstance(tr, dict):
+            tsel = tr["x2"] if name in STREAMING else tr["raw"]
+        kernels[name] = {"ms_per_launch": round(mean_ms, 4), "launches_per_step": round(launches / steps, 3),
+                         "ms_per_step": round(mean_ms * launches / steps, 4),
+                         "alg_bytes_per_launch": int(mean_b), "achieved": round(ach, 1),
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic_per_launch": tsel,
+                         "traffic_fetch_raw": tr.get("fetch_raw") if isinstance(tr, dict) else None,
+                         "traffic_fetch_x2": tr.get("x2") if isinstance(tr, dict) else None,
+                         "traffic_frac": (round(tsel / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tsel else None),
+                         "time_share": None, "per_query_ms": per_q}
+    tot = sum(k["ms_per_step"] for k in kernels.values()) or 1.0
     for k in kernels.values():
-        k["time_share"] = round(k["ms_per_launch"] / tot, 3)
-    dom = max(kernels, key=lambda k: kernels[k]["ms_per_launch"])
+        k["time_share"] = round(k["ms_per_step"] / tot, 3)
+    dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     d = kernels[dom]
     return {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": d["frac"], "traffic": d["traffic_per_launch"], "kernels": kernels,
             "bytes": "algorithmic bytes per launch (phip_result.filter_bytes / agg_bytes, SURVEY.md §8d) / mean "
-                     "launch time from HIP events on the library's stream; traffic = PMC HBM bytes per launch"}
+                     "launch time from HIP events on the library's stream; dominant = most device time per step "
+                     "(launches x mean); traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE for the "
+                     "streaming filter kernel, raw FETCH_SIZE + WRITE_SIZE for gathering kernels)"}
 
 
 def main():
@@ -184,13 +210,14 @@ def main():
         for s in gsegs:
             s.destroy()
         res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(gsegs),
-               "lat": lat, "roofline": roofline(kstats, queries, traffic, layout)}
+               "lat": lat, "roofline": roofline(kstats, queries, traffic, layout, args.steps)}
         if want_cpu and li == 0:
             from oracle import cpu_baseline
             v, threads, reps, el, _ = cpu_baseline.time_queries([qcs[q] for q in queries], raws, min_seconds=10.0)
             res["cpu"] = {"value": round(v / 1e9, 4), "unit": "G rows/s", "cores": threads, "kind": "port",
                           "sample": f"restatement, not Pinot: oracle/cpu_scan.c (OpenMP C restatement of the CPU "
-                                    f"server path, {threads} threads; host nproc = {os.cpu_count()}) running "
+                                    f"server path, {threads} threads = the usable CPUs: "
+                                    f"{cpu_baseline.usable_cpus()[1]}) running "
                                     f"{'+'.join(queries)} over the same {len(raws)} x {ssb.SEGMENT_ROWS}-row "
                                     f"SF{args.sf} {layout} segments, {reps} reps in {el:.1f} s"}
             del raws

@@ -229,7 +229,8 @@ typedef struct phip_result {
   double scan_kernel_ms; /* device time of the fused filter/aggregate kernel(s) */
   double device_ms;      /* device time of the whole query on the stream */
   int32_t num_groups_trimmed; /* 1 when the group set was trimmed to phip_query_desc.trim_size */
-  int32_t reserved;
+  int32_t fused;              /* 1 when the filter kernel aggregated its own tiles (one launch: filter_kernel_ms and
+                                 filter_bytes then cover both, agg_* are 0) */
   /* long_exact[a] = 1 when long_values[g*num_aggregations + a] holds the exact integer result (COUNT, and SUM
    * over INT/LONG inputs whose bound sum |value| stays below 2^62); 0 when the SUM accumulated in double like
    * SumAggregationFunction (a possible int64 overflow) -- values[] is then the only result. */
@@ -259,6 +260,10 @@ PHIP_API int32_t phip_shutdown(void);
 PHIP_API int32_t phip_device_count(int32_t *out_count);
 PHIP_API const char *phip_last_error(void);
 PHIP_API const char *phip_version(void);
+/* HIP_VERSION the library was built against and hipRuntimeGetVersion of the runtime it bound to (a process that
+ * also runs PyTorch-ROCm shares torch's bundled runtime; the loader refuses a major-version mismatch). No
+ * reference counterpart: a build/runtime sanity check of the FFM loader. */
+PHIP_API int32_t phip_runtime_versions(int32_t *out_built, int32_t *out_runtime);
 
 PHIP_API int32_t phip_segment_load(const phip_segment_desc *desc, uint64_t *out_handle);
 PHIP_API int32_t phip_segment_unload(uint64_t handle);

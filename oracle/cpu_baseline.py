@@ -130,10 +130,29 @@ class Prepared:
         return total, m.value
 
 
+def usable_cpus():
+    """(cpus this process may run on, how that was found): the affinity mask (os.sched_getaffinity), capped by
+    the cgroup CPU quota when one is set (a GPU box's share of a larger host: nproc shows the host's CPUs, the
+    quota how many of them the process gets). SURVEY.md §8(d): the CPU baseline runs one worker per such CPU,
+    as maxExecutionThreads = cores would (QueryMultiThreadingUtils.java:46-65)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        quota = None
+    n = min(aff, quota) if quota else aff
+    return n, f"sched_getaffinity {aff}, cgroup cpu.max quota {quota if quota else 'none'}, nproc {os.cpu_count()}"
+
+
 def time_queries(qcs, segments, threads=None, min_seconds=2.0, max_reps=100000):
-    """Runs every query over all segments with `threads` workers, repeated until min_seconds have passed;
-    returns (rows scanned per second, threads, reps, results). Rows = sum of numTotalDocs per query run."""
-    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    """Runs every query over all segments with `threads` workers (default: usable_cpus()), repeated until
+    min_seconds have passed; returns (rows scanned per second, threads, reps, results). Rows = sum of
+    numTotalDocs per query run."""
+    threads = threads or usable_cpus()[0]
     preps = [Prepared(q, segments) for q in qcs]
     rows_per_rep = sum(s.num_docs for s in segments) * len(preps)
     results = [p.run(threads) for p in preps]  # warm-up (page-in)

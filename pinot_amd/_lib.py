@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "phip_segment_load", "phip_segment_unload", "phip_segment_device_bytes", "phip_query",
     "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap", "phip_plan_create", "phip_plan_execute",
     "phip_plan_destroy", "phip_global_dictionary", "phip_plan_execute_partial", "phip_plan_finish",
+    "phip_runtime_versions",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -98,7 +99,7 @@ class Result(ctypes.Structure):
                 ("values", ctypes.POINTER(ctypes.c_double)), ("long_values", ctypes.POINTER(ctypes.c_int64)),
                 ("hll_registers", ctypes.POINTER(ctypes.c_uint8)), ("group_keys", ctypes.POINTER(ctypes.c_int32)),
                 ("scan_kernel_ms", ctypes.c_double), ("device_ms", ctypes.c_double),
-                ("num_groups_trimmed", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("num_groups_trimmed", ctypes.c_int32), ("fused", ctypes.c_int32),
                 ("long_exact", ctypes.POINTER(ctypes.c_int32)),
                 ("filter_kernel_ms", ctypes.c_double), ("agg_kernel_ms", ctypes.c_double),
                 ("filter_bytes", ctypes.c_int64), ("agg_bytes", ctypes.c_int64)]
@@ -129,22 +130,32 @@ class PhipError(RuntimeError):
 
 
 _lib = None
+_torch_first = False  # torch's HIP runtime was in the process before the library bound to one
 
 
-def load():
-    """Load libpinot_hip.so (fails loudly: there is no CPU fallback on the product path)."""
-    global _lib
+def load(with_torch: bool = False):
+    """Load libpinot_hip.so (fails loudly: there is no CPU fallback on the product path).
+
+    One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (same soname), so a process that also
+    uses torch on the GPU (RCCL merges, engine/distributed.py) must import torch BEFORE the library loads; the
+    library then binds to torch's runtime. ``with_torch`` (or PINOT_AMD_WITH_TORCH=1) does that import; a process
+    that already imported torch gets it implicitly. Plain users of the library skip torch's import and keep the
+    ROCm runtime the library was built against. Either way the runtime's major version must equal the build's
+    (phip_version reports both), else the load fails.
+    """
+    global _lib, _torch_first
+    import sys
+    want_torch = with_torch or os.environ.get("PINOT_AMD_WITH_TORCH") == "1"
     if _lib is not None:
+        if want_torch and not _torch_first:
+            raise RuntimeError("libpinot_hip.so was loaded before torch: its HIP runtime is not torch's. Import torch "
+                               "(or call pinot_amd._lib.load(with_torch=True)) before the first load")
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (same soname), so importing torch
-    # first makes the library bind to that copy. Loaded the other way round, the process would hold two
-    # runtimes and torch (RCCL merges, engine/distributed.py) would find no GPU.
-    try:
+    if want_torch:
         import torch  # noqa: F401
-    except ImportError:
-        pass
+    _torch_first = "torch" in sys.modules
     lib = ctypes.CDLL(LIB_PATH)
     i32, u64, i64 = ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64
     lib.phip_init.argtypes = [ctypes.POINTER(i32), i32]
@@ -183,6 +194,15 @@ def load():
     lib.phip_plan_execute_partial.restype = i32
     lib.phip_plan_finish.argtypes = [u64, ctypes.POINTER(Partial), ctypes.POINTER(ctypes.POINTER(Result))]
     lib.phip_plan_finish.restype = i32
+    built, runtime = ctypes.c_int32(0), ctypes.c_int32(0)
+    rv = getattr(lib, "phip_runtime_versions", None)  # (absent from round-2 builds used in A/B runs)
+    if rv is not None:
+        rv.argtypes = [ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        rv.restype = i32
+    if rv is not None and rv(ctypes.byref(built), ctypes.byref(runtime)) == PHIP_OK and runtime.value > 0:
+        if built.value // 10_000_000 != runtime.value // 10_000_000:  # HIP_VERSION = major*1e7 + minor*1e5 + patch
+            raise ImportError(f"libpinot_hip.so was built against HIP {built.value} but the process runs HIP "
+                              f"{runtime.value} (major versions differ)")
     _lib = lib
     return lib
 

@@ -252,11 +252,21 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
   int si = 0;
   int dict_si = -1;        // segment whose small dictionaries sit in the wave's stage area
   int t = xs + wid;
-  uint32_t m_next = 0;
-  if (mask != nullptr && t < xe) m_next = __builtin_nontemporal_load(mask + (size_t)t * 64 + lane);
+  // mask words of the next kMaskAhead tiles in flight (a sparse query skips most tiles: one load round trip
+  // per tile would bound the walk)
+  constexpr int kMaskAhead = 4;
+  uint32_t mq[kMaskAhead];
+#pragma unroll
+  for (int k = 0; k < kMaskAhead; k++)
+    mq[k] = (mask != nullptr && t + k * wx < xe) ? __builtin_nontemporal_load(mask + (size_t)(t + k * wx) * 64 + lane) : 0u;
   for (; t < xe; t += wx) {
-    const uint32_t m_raw = m_next;
-    if (mask != nullptr && t + wx < xe) m_next = __builtin_nontemporal_load(mask + (size_t)(t + wx) * 64 + lane);  // prefetch
+    const uint32_t m_raw = mq[0];
+#pragma unroll
+    for (int k = 0; k + 1 < kMaskAhead; k++) mq[k] = mq[k + 1];
+    {
+      const int tn = t + kMaskAhead * wx;
+      mq[kMaskAhead - 1] = (mask != nullptr && tn < xe) ? __builtin_nontemporal_load(mask + (size_t)tn * 64 + lane) : 0u;
+    }
     if (segs[si].work_begin + segs[si].num_work <= t) {
       if constexpr (MODE == GB_NONE) {
         if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
@@ -319,6 +329,42 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
       continue;
     }
     }
+    if constexpr (MODE == GB_NONE) {
+      // Matched docs -> the ring in doc order: the tile word is transposed to the contiguous layout (lane L
+      // = docs 32L .. 32L+31), every lane writes its docs at the wave prefix of the lanes' popcounts. This
+      // costs ~40 instructions plus the lane's own matches per tile; a pass per 64-doc group (ballot + rank
+      // + write for each of the 32 groups) cost ~320 on sparse tiles, most of the unsorted layout's walk.
+      if (ballot(m != 0) == 0) continue;
+      const uint32_t cw = lane_major_to_contig(m);
+      const uint32_t cnt = (uint32_t)__popc(cw);
+      const uint32_t incl = wave_incl_scan(cnt);
+      const int total = __builtin_amdgcn_readlane((int)incl, 63);
+      const int head0 = head;
+      const int32_t ldoc = doc0 + 32 * lane;
+      // all at once when the ring has room, else in quarter-tile pieces (16 lanes, <= 512 docs) each after
+      // draining the ring below one batch
+      const int npiece = head - tail + total <= R ? 1 : 4;
+      for (int p = 0; p < npiece; p++) {
+        const int lanes = 64 / npiece;
+        const int pend = __builtin_amdgcn_readlane((int)incl, lanes * p + lanes - 1);
+        if (lane >= lanes * p && lane < lanes * (p + 1)) {
+          uint32_t w = cw;
+          int pos = head0 + (int)(incl - cnt);
+          while (w) {
+            const int j = __builtin_clz(w);
+            w &= ~(0x80000000u >> j);
+            ring[pos & (R - 1)] = (uint32_t)(ldoc + j);
+            pos++;
+          }
+        }
+        head = head0 + pend;
+        while (head - tail >= 64 * kBatch) {
+          agg_ring_batch<NA>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0);
+          tail += 64 * kBatch;
+        }
+      }
+      continue;
+    }
     if (dense) {
       // every doc of the tile matched: consecutive chunks, coalesced column reads
       for (int c = 0; c < nvalid; c += 64) {
@@ -334,12 +380,7 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
         const uint64_t mm = ballot(b);
         if (b) ring[(head + mbcnt64(mm)) & (R - 1)] = (uint32_t)(doc0 + (31 - bit) * 64 + lane);
         head += __popcll(mm);
-        if constexpr (MODE == GB_NONE) {
-          if (head - tail >= 64 * kBatch) {
-            agg_ring_batch<NA>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0);
-            tail += 64 * kBatch;
-          }
-        } else if (head - tail >= 64) {
+        if (head - tail >= 64) {
           const int32_t doc = (int32_t)ring[(tail + lane) & (R - 1)];
           tail += 64;
           do_chunk<NA, MODE>(q, seg, doc, true, acc, hll_lds, tbl, hll_packed);

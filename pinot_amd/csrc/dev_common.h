@@ -149,4 +149,40 @@ __device__ __forceinline__ uint32_t valid_word(int32_t valid_docs, int lane) {
   return ngrp == 0 ? 0u : (~0u << (32 - ngrp));
 }
 
+// Transpose of the 32x32 bit matrix held by each 32-lane half (row = lane, Hacker's Delight transpose32 as 5
+// butterfly stages over ds_bpermute). It is an involution.
+__device__ __forceinline__ uint32_t transpose_halves(uint32_t a) {
+  const int lane = lane_id();
+  uint32_t m = 0x0000FFFFu;
+#pragma unroll
+  for (int j = 16; j != 0; j >>= 1, m ^= m << j) {
+    const uint32_t p = (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ j) << 2, (int)a);
+    if (lane & j) {
+      a ^= ((p ^ (a >> j)) & m) << j;
+    } else {
+      a ^= (a ^ (p >> j)) & m;
+    }
+  }
+  return a;
+}
+
+// Lane-major tile word (bit 31-g of lane l = doc 64g + l) -> contiguous word (bit 31-j of lane L = doc 32L + j):
+// the inverse of filter.hip contig_to_lane_major (transpose each half, then lane c takes lane 32(c&1) + c/2).
+__device__ __forceinline__ uint32_t lane_major_to_contig(uint32_t m) {
+  const int lane = lane_id();
+  const uint32_t a = transpose_halves(m);
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((32 * (lane & 1) + (lane >> 1)) << 2, (int)a);
+}
+
+// Inclusive prefix sum over the wave's 64 lanes.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, o);
+    v += lane >= o ? t : 0u;
+  }
+  return v;
+}
+
 }  // namespace phip

@@ -22,15 +22,17 @@ constexpr int kMaxHllRegs = 1 << 12;  // log2m <= 12 on the GPU path
 constexpr int kFilterBlock = 256;
 constexpr int kFilterWaves = kFilterBlock / kWave;
 constexpr int kMaxRing = 8;           // LDS-DMA ring slots per wave
+constexpr int kFusedRing = 512;       // fused aggregation: u16 tile-relative doc ids per wave (a quarter tile)
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;
-// per-wave ring of matched doc ids (u32): GB_NONE batches up to 4 chunks (+ one group), the group-by walks
-// take one chunk at a time (their LDS goes to the table)
+// per-wave ring of matched doc ids (u32): GB_NONE batches up to 4 chunks; a tile's docs enter it in
+// quarter-tile pieces of <= 512 after the ring was drained below one batch, so it holds one batch + 512; the
+// group-by walks take one chunk at a time (their LDS goes to the table)
 #ifndef PHIP_KBATCH
 #define PHIP_KBATCH 4  // agg_common.h kBatch (A/B builds override it)
 #endif
-constexpr int kRingAgg = 128 * PHIP_KBATCH;  // two batches of kBatch chunks
+constexpr int kRingAgg = PHIP_KBATCH <= 4 ? 1024 : 2048;  // power of two >= 64 * kBatch + 512
 constexpr int kRingGroup = 128;
 constexpr int ring_entries(int mode) { return mode == 0 ? kRingAgg : kRingGroup; }
 constexpr int kMaxAggStage = 4;      // staged aggregation columns
@@ -163,7 +165,8 @@ struct DevFilter {
   int32_t total_work;
   int32_t stage_stride;  // bytes of one ring slot (max over segments), multiple of 16
   int32_t nbuf;          // ring slots per wave (2..kMaxRing): nbuf-1 tiles in flight while one is evaluated
-  int32_t xcd_walk;      // 1: XCD-sweep tile order (grid multiple of 8); 0: contiguous range per wave
+  int32_t xcd_walk;      // 1: XCD-sweep tile order; 2: XCD ranges cut into contiguous per-wave ranges (grid multiple
+                         // of 8 for both); 0: contiguous range per wave
   int32_t min_dma;       // min over segments of LDS-DMA wave-instructions per tile (vmcnt lower bound)
   int32_t probe;         // measurement only (PHIP_FILTER_PROBE): 1 = stream the tiles, skip the evaluation
   int32_t contig_inline;  // 1: range scans of the contiguous evaluator inline (0: through contig_scan_any; A/B)

@@ -335,18 +335,7 @@ __device__ __forceinline__ uint32_t contig_valid(int32_t valid_docs, int lane) {
 // matrix (Hacker's Delight transpose32 with rows = lanes, 5 butterfly stages over ds_bpermute).
 __device__ __forceinline__ uint32_t contig_to_lane_major(uint32_t c) {
   const int lane = lane_id();
-  uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(((2 * (lane & 31)) | (lane >> 5)) << 2, (int)c);
-  uint32_t m = 0x0000FFFFu;
-#pragma unroll
-  for (int j = 16; j != 0; j >>= 1, m ^= m << j) {
-    const uint32_t p = (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ j) << 2, (int)a);
-    if (lane & j) {
-      a ^= ((p ^ (a >> j)) & m) << j;
-    } else {
-      a ^= (a ^ (p >> j)) & m;
-    }
-  }
-  return a;
+  return transpose_halves((uint32_t)__builtin_amdgcn_ds_bpermute(((2 * (lane & 31)) | (lane >> 5)) << 2, (int)c));
 }
 
 // One scan leaf over the lane's 32 docs: the B staged words of those docs in registers, field j cut from
@@ -741,16 +730,16 @@ __device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_
 
 // ------------------------------------------------------------------------------------------------
 // fused projection + aggregation (conjunctive programs without group-by / HLL). After a tile's mask is
-// known its matched docs are compacted into a per-wave LDS ring (mbcnt ranks, as the aggregation kernel
-// does) and projected 64 at a time, so a sparse tile costs one gather round trip instead of one per
-// group; the chunk is flushed at the end of the tile because columns staged in the tile's ring slot
-// (the filter columns, and value columns the host chose to stream) are read from LDS by tile-relative
-// doc. Dictionaries of <= 64 entries live one entry per lane (loaded when the wave enters a segment) and
-// are read with ds_bpermute; larger ones are gathered from HBM. Per-lane accumulators take their docs
-// in doc order, as agg_chunk does -- the aggregation kernel's walk without the mask round trip, the
-// re-read of the filter columns and a second launch.
+// known its matched docs are compacted into a per-wave LDS ring in doc order (the mask transposed to the
+// contiguous layout, lane ranks from a wave prefix sum, as the aggregation kernel does) and projected
+// kFusedBatch x 64 at a time with every load of the batch issued before the first use, so a sparse tile costs
+// one gather round trip. Columns staged in the tile's ring slot (the filter columns, and value columns the host
+// chose to stream) are read from LDS by tile-relative doc, so the ring is drained at the end of the tile.
+// Dictionaries of <= 64 entries live one entry per lane (loaded when the wave enters a segment) and are read
+// with ds_bpermute; larger ones are gathered from HBM -- the aggregation kernel's walk without the mask round
+// trip, the re-read of the filter columns and a second launch.
 // ------------------------------------------------------------------------------------------------
-constexpr int kFusedRing = 128;  // u16 tile-relative doc ids per wave (a partial chunk + one group)
+constexpr int kFusedBatch = 4;  // 64-doc chunks per gather round trip
 
 // The lane's share of a small dictionary: entry `lane` (64-bit image of the value), or 0.
 struct SmallDict {
@@ -782,38 +771,91 @@ __device__ __forceinline__ uint32_t fused_id(ccol_t &c, const Tile &t, int32_t t
   return decode_bits(c.words, (uint64_t)(uint32_t)(t.doc0 + td) * b, b);
 }
 
-__device__ __forceinline__ double fused_f64(ccol_t &c, const SmallDict &sd, const Tile &t, int32_t td) {
-  if (!c.has_dict) return raw_f64(c, t.doc0 + td);
-  const uint32_t id = fused_id(c, t, td);
+__device__ __forceinline__ uint64_t small_dict_bits(const SmallDict &sd, uint32_t id, bool wide) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.lo);
+  if (!wide) return lo;
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.hi) << 32) | lo;
+}
+
+// values of U docs as double: ids of all U first, then all U value loads (one round trip each)
+template <int U>
+__device__ __forceinline__ void fused_f64_u(ccol_t &c, const SmallDict &sd, const Tile &t, const int32_t (&td)[U],
+                                            double (&v)[U]) {
+  if (!c.has_dict) {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = raw_f64(c, t.doc0 + td[u]);
+    return;
+  }
+  uint32_t id[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) id[u] = fused_id(c, t, td[u]);
+  const int ty = c.type;
   if (sd.on) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.lo);
-    switch (c.type) {
-      case PHIP_TYPE_INT: return (double)(int32_t)lo;
-      case PHIP_TYPE_FLOAT: return (double)__uint_as_float(lo);
-      default: {
-        const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.hi) << 32) | lo;
-        return c.type == PHIP_TYPE_LONG ? (double)(int64_t)v : __longlong_as_double((long long)v);
-      }
+    const bool wide = ty == PHIP_TYPE_LONG || ty == PHIP_TYPE_DOUBLE;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t x = small_dict_bits(sd, id[u], wide);
+      v[u] = ty == PHIP_TYPE_INT ? (double)(int32_t)(uint32_t)x
+           : ty == PHIP_TYPE_FLOAT ? (double)__uint_as_float((uint32_t)x)
+           : ty == PHIP_TYPE_LONG ? (double)(int64_t)x : __longlong_as_double((long long)x);
     }
+    return;
   }
-  return dict_f64(c, id);
+  switch (ty) {
+    case PHIP_TYPE_INT:
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_GLB int32_t *)c.dict)[id[u]];
+      break;
+    case PHIP_TYPE_DOUBLE:
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB double *)c.dict)[id[u]];
+      break;
+    default:
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = dict_f64(c, id[u]);
+      break;
+  }
 }
 
-__device__ __forceinline__ int64_t fused_i64(ccol_t &c, const SmallDict &sd, const Tile &t, int32_t td) {
-  if (!c.has_dict) return raw_i64(c, t.doc0 + td);
-  const uint32_t id = fused_id(c, t, td);
+template <int U>
+__device__ __forceinline__ void fused_i64_u(ccol_t &c, const SmallDict &sd, const Tile &t, const int32_t (&td)[U],
+                                            int64_t (&v)[U]) {
+  if (!c.has_dict) {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = raw_i64(c, t.doc0 + td[u]);
+    return;
+  }
+  uint32_t id[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) id[u] = fused_id(c, t, td[u]);
+  const int ty = c.type;
   if (sd.on) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.lo);
-    if (c.type == PHIP_TYPE_INT) return (int64_t)(int32_t)lo;
-    const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.hi) << 32) | lo;
-    return (int64_t)v;  // (integral sums only see INT / LONG columns)
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t x = small_dict_bits(sd, id[u], ty != PHIP_TYPE_INT);
+      v[u] = ty == PHIP_TYPE_INT ? (int64_t)(int32_t)(uint32_t)x : (int64_t)x;  // (integral sums: INT / LONG only)
+    }
+    return;
   }
-  return dict_i64(c, id);
+  switch (ty) {
+    case PHIP_TYPE_INT:
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int32_t *)c.dict)[id[u]];
+      break;
+    case PHIP_TYPE_LONG:
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int64_t *)c.dict)[id[u]];
+      break;
+    default:
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = dict_i64(c, id[u]);
+      break;
+  }
 }
 
-// one chunk of up to 64 matched docs of the current tile (lane: tile-relative doc td, active flag)
-template <int NA>
-__device__ __forceinline__ void fused_chunk(cquery_t &aq, cseg_t &seg, const Tile &t, int32_t td, bool act,
+// U chunks of matched docs of the current tile (chunk u: lane's tile-relative doc td[u], active if bit u of act)
+template <int NA, int U>
+__device__ __forceinline__ void fused_batch(cquery_t &aq, cseg_t &seg, const Tile &t, const int32_t (&td)[U], uint32_t act,
                                             const SmallDict (&sda)[NA], const SmallDict (&sdb)[NA],
                                             uint64_t (&acc)[NA]) {
 #pragma unroll
@@ -822,29 +864,41 @@ __device__ __forceinline__ void fused_chunk(cquery_t &aq, cseg_t &seg, const Til
     cagg_t &ag = aq.aggs[a];
     const int kind = ag.acc;
     if (kind == ACC_COUNT) {
-      acc[a] += act ? 1ull : 0ull;
+      acc[a] += (uint64_t)__popc(act);
       continue;
     }
     ccol_t &ca = seg.cols[ag.col_a];
     if (kind == ACC_SUM_I64) {
-      int64_t x = fused_i64(ca, sda[a], t, td);
+      int64_t x[U];
+      fused_i64_u<U>(ca, sda[a], t, td, x);
       if (ag.expr != PHIP_EXPR_COLUMN) {
-        const int64_t y = fused_i64(seg.cols[ag.col_b], sdb[a], t, td);
-        x = ag.expr == PHIP_EXPR_ADD ? x + y : (ag.expr == PHIP_EXPR_SUB ? x - y : x * y);
+        int64_t y[U];
+        fused_i64_u<U>(seg.cols[ag.col_b], sdb[a], t, td, y);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          x[u] = ag.expr == PHIP_EXPR_ADD ? x[u] + y[u] : (ag.expr == PHIP_EXPR_SUB ? x[u] - y[u] : x[u] * y[u]);
       }
-      acc[a] += act ? (uint64_t)x : 0ull;
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[a] += ((act >> u) & 1u) ? (uint64_t)x[u] : 0ull;
     } else {
-      double x = fused_f64(ca, sda[a], t, td);
+      double x[U];
+      fused_f64_u<U>(ca, sda[a], t, td, x);
       if (ag.expr != PHIP_EXPR_COLUMN) {
-        const double y = fused_f64(seg.cols[ag.col_b], sdb[a], t, td);
-        x = ag.expr == PHIP_EXPR_ADD ? x + y : (ag.expr == PHIP_EXPR_SUB ? x - y : x * y);
+        double y[U];
+        fused_f64_u<U>(seg.cols[ag.col_b], sdb[a], t, td, y);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          x[u] = ag.expr == PHIP_EXPR_ADD ? x[u] + y[u] : (ag.expr == PHIP_EXPR_SUB ? x[u] - y[u] : x[u] * y[u]);
       }
-      const double cur = as_f64(acc[a]);
-      double nv;
-      if (kind == ACC_SUM_F64) nv = cur + (act ? x : 0.0);
-      else if (kind == ACC_MIN_F64) nv = fmin(cur, act ? x : __builtin_huge_val());
-      else nv = fmax(cur, act ? x : -__builtin_huge_val());
-      acc[a] = as_u64(nv);
+      double cur = as_f64(acc[a]);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const bool on = (act >> u) & 1u;
+        if (kind == ACC_SUM_F64) cur = cur + (on ? x[u] : 0.0);
+        else if (kind == ACC_MIN_F64) cur = fmin(cur, on ? x[u] : __builtin_huge_val());
+        else cur = fmax(cur, on ? x[u] : -__builtin_huge_val());
+      }
+      acc[a] = as_u64(cur);
     }
   }
 }
@@ -853,29 +907,42 @@ template <int NA>
 __device__ __forceinline__ void fused_tile(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
                                            PHIP_LDS uint16_t *ring, const SmallDict (&sda)[NA],
                                            const SmallDict (&sdb)[NA], uint64_t (&acc)[NA]) {
-  uint32_t any = wave_or32(mask);
-  if (any == 0) return;
+  if (ballot(mask != 0) == 0) return;
   const int lane = lane_id();
-  int head = 0, tail = 0;  // wave-uniform ring cursors
-  while (any) {
-    const int bit = 31 - __builtin_clz(any);
-    any &= ~(1u << bit);
-    const bool b = (mask >> bit) & 1u;
-    const uint64_t mm = ballot(b);
-    if (b) ring[(head + mbcnt64(mm)) & (kFusedRing - 1)] = (uint16_t)((31 - bit) * 64 + lane);
-    head += __popcll(mm);
-    if (head - tail >= 64) {
-      const int32_t td = ring[(tail + lane) & (kFusedRing - 1)];
-      tail += 64;
-      fused_chunk<NA>(aq, seg, t, td, true, sda, sdb, acc);
+  const uint32_t cw = lane_major_to_contig(mask);  // lane L: docs 32L .. 32L+31, bit 31-j = doc 32L+j
+  const uint32_t cnt = (uint32_t)__popc(cw);
+  const uint32_t incl = wave_incl_scan(cnt);
+  const int total = __builtin_amdgcn_readlane((int)incl, 63);
+  // the whole tile at once when it fits the ring, else quarter tiles (16 lanes, <= 512 docs)
+  const int npiece = total <= kFusedRing ? 1 : 4;
+  const int lanes = 64 / npiece;
+  for (int p = 0; p < npiece; p++) {
+    const int s = p == 0 ? 0 : __builtin_amdgcn_readlane((int)incl, lanes * p - 1);
+    const int e = __builtin_amdgcn_readlane((int)incl, lanes * p + lanes - 1);
+    if (e == s) continue;
+    if (lane >= lanes * p && lane < lanes * (p + 1)) {
+      uint32_t w = cw;
+      int pos = (int)(incl - cnt) - s;
+      while (w) {
+        const int j = __builtin_clz(w);
+        w &= ~(0x80000000u >> j);
+        ring[pos++] = (uint16_t)(32 * lane + j);
+      }
     }
+    const int n = e - s;
+    for (int c = 0; c < n; c += 64 * kFusedBatch) {
+      int32_t td[kFusedBatch];
+      uint32_t act = 0;
+#pragma unroll
+      for (int u = 0; u < kFusedBatch; u++) {
+        const bool on = c + 64 * u + lane < n;
+        td[u] = on ? (int32_t)ring[c + 64 * u + lane] : 0;
+        act |= on ? (1u << u) : 0u;
+      }
+      fused_batch<NA, kFusedBatch>(aq, seg, t, td, act, sda, sdb, acc);
+    }
+    __builtin_amdgcn_wave_barrier();  // ring reads done before the next piece's writes
   }
-  if (head > tail) {
-    const bool act = lane < head - tail;
-    const int32_t td = act ? (int32_t)ring[(tail + lane) & (kFusedRing - 1)] : 0;
-    fused_chunk<NA>(aq, seg, t, td, act, sda, sdb, acc);
-  }
-  __builtin_amdgcn_wave_barrier();  // ring reads done before the next tile's writes
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -946,13 +1013,23 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);
   int begin, end, step;
-  if (q.xcd_walk) {
+  if (q.xcd_walk == 1) {
     // XCD sweep (grid is a multiple of 8): the work list is cut into 8 ranges, one per XCD, and an
     // XCD's waves stride through its range together, so at any time they read neighbouring tiles
     const int x = blockIdx.x & 7, gx = gridDim.x >> 3;
     begin = (int)((int64_t)q.total_work * x / 8) + (int)(blockIdx.x >> 3) * kFilterWaves + wave;
     end = (int)((int64_t)q.total_work * (x + 1) / 8);
     step = gx * kFilterWaves;
+  } else if (q.xcd_walk == 2) {
+    // XCD ranges, each cut into contiguous per-wave ranges: a wave streams contiguous tiles (its ring
+    // prefetch stays sequential) and an XCD's waves stay inside 1/8 of the work list, so the dictionaries a
+    // fused aggregation gathers from belong to the few segments of that range (they stay in the XCD's L2)
+    const int x = blockIdx.x & 7, gx = gridDim.x >> 3;
+    const int64_t xs = (int64_t)q.total_work * x / 8, xe = (int64_t)q.total_work * (x + 1) / 8;
+    const int64_t nw = (int64_t)gx * kFilterWaves, w = (int64_t)(blockIdx.x >> 3) * kFilterWaves + wave;
+    begin = (int)(xs + (xe - xs) * w / nw);
+    end = (int)(xs + (xe - xs) * (w + 1) / nw);
+    step = 1;
   } else {
     // contiguous range per wave
     const int64_t waves_total = (int64_t)gridDim.x * kFilterWaves;

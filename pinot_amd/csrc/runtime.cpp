@@ -1828,10 +1828,18 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // (tools/ab_env.sh, profiles/r02_*): fused wins while the query has at most a few thousand work tiles
     // (Q1.2 / Q1.3 over the sorted layout: 0.112 -> 0.081 / 0.066 -> 0.057 ms p50) and loses beyond
     // (Q1.1 sorted, 44K tiles: 0.207 -> 0.270 ms; unsorted, 293K tiles: 1.6 -> 2.4 ms per step).
+    // Sparse queries fuse whatever their size: with few matched docs per tile the gathers inside the stream are
+    // rare, while a separate aggregation launch walks one mask per tile (estimated matches per work tile from the
+    // program's leaf selectivities: dict-id range widths / set sizes over the cardinality, sorted doc ranges).
     const char *fe = getenv("PHIP_FUSE");  // measurement override: "0" never, "1" always, unset = by size
     const int64_t kFuseMaxTiles = 8192;
+    double est_docs = 0.0;
+    for (size_t i = 0; i < dsegs.size(); i++) est_docs += seg_est[i] * dsegs[i].num_docs;
+    const double per_tile = est_docs / (double)std::max<int64_t>(1, total_work);
+    double fuse_per_tile = 16.0;
+    if (const char *fp = getenv("PHIP_FUSE_PER_TILE")) fuse_per_tile = atof(fp);  // measurement override
     bool fuse = conj_all && any_filter_prog && !group_by && nprog == 1 && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
-                (fe ? atoi(fe) != 0 : total_work <= kFuseMaxTiles);
+                (fe ? atoi(fe) != 0 : (total_work <= kFuseMaxTiles || per_tile <= fuse_per_tile));
     bool any_value = false;
     for (int a = 0; a < naggs; a++) any_value |= dq.aggs[a].acc != ACC_COUNT;
     if (fuse && any_value) {
@@ -1915,7 +1923,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const int64_t waves_at = (int64_t)dev->num_cus * want * kFilterWaves;
     if (!env && total_work >= 4 * waves_at)
       while (want > 2 && total_work < kMinTilesPerWave * (int64_t)dev->num_cus * want * kFilterWaves) want--;
-    const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * 128 * 2 : 0;  // filter.hip kFusedRing u16
+    const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * kFusedRing * 2 : 0;  // fused doc rings (u16)
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
       const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024 - 1024) / bpc - fring) / ((int64_t)kFilterWaves * stage_stride));
       if (nb >= 2) {
@@ -1925,9 +1933,12 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
     if (nbuf < 2) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
   }
-  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_naggs > 0 ? (size_t)kFilterWaves * 128 * 2 : 0);
-  const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "contig"
-  const bool xcd_walk = walk_env ? strcmp(walk_env, "xcd") == 0 : false;  // contig measured faster
+  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_naggs > 0 ? (size_t)kFilterWaves * kFusedRing * 2 : 0);
+  const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "xcdc" / "contig"
+  // contiguous per-wave ranges measured fastest for the plain filter; a fused aggregation's waves stay inside
+  // their XCD's eighth of the work (its dictionaries then stay in that XCD's L2)
+  int xcd_walk = fused_naggs > 0 ? 2 : 0;
+  if (walk_env) xcd_walk = !strcmp(walk_env, "xcd") ? 1 : (!strcmp(walk_env, "xcdc") ? 2 : 0);
   int filter_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)dev->num_cus * fbpc,
                                                                   ceil_div(total_work, kFilterWaves)));
   if (xcd_walk) filter_blocks = (int)round_up(std::max(filter_blocks, 8), 8);
@@ -1994,7 +2005,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   fq.total_work = (int32_t)total_work;
   fq.stage_stride = stage_stride;
   fq.nbuf = nbuf;
-  fq.xcd_walk = xcd_walk ? 1 : 0;
+  fq.xcd_walk = xcd_walk;
   {
     const char *pe = getenv("PHIP_FILTER_PROBE");
     fq.probe = pe ? atoi(pe) : 0;
@@ -2753,6 +2764,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     r.agg_bytes = ab;
   }
   if (P.fused_naggs > 0) {  // one kernel filtered and aggregated: it owns both times and both byte counts
+    r.fused = 1;
     r.filter_kernel_ms = t_filter + t_agg;
     r.agg_kernel_ms = 0.0;
     r.filter_bytes += r.agg_bytes;
@@ -2798,6 +2810,14 @@ extern "C" {
 
 PHIP_API const char *phip_last_error(void) { return g_err.c_str(); }
 PHIP_API const char *phip_version(void) { return "pinot_hip 0.1.0 gfx950"; }
+
+PHIP_API int32_t phip_runtime_versions(int32_t *out_built, int32_t *out_runtime) {
+  int rt = 0;
+  if (hipRuntimeGetVersion(&rt) != hipSuccess) rt = 0;
+  if (out_built) *out_built = HIP_VERSION;
+  if (out_runtime) *out_runtime = rt;
+  return PHIP_OK;
+}
 
 PHIP_API int32_t phip_device_count(int32_t *out_count) {
   int n = 0;

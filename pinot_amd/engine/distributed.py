@@ -51,115 +51,187 @@ def _stats_from(v) -> ExecutionStatistics:
     return ExecutionStatistics(*[int(x) for x in v])
 
 
-class _Slots:
-    """Layout of one row of intermediates across the four reduce operators."""
+# ---- one SUM and one MAX per merge ----------------------------------------------------------------
+# A row of intermediates is packed into a float64 SUM part and an int64 MAX part, so a merge is exactly two
+# all-reduces whatever the functions (the reference merges per function: SumAggregationFunction.merge `+`,
+# Min/Max `min`/`max`, HLL register max -- AggregationResultsBlockMerger.java:34-49):
+#   SUM   int64 values (COUNT, exact integer SUMs) as two doubles (v >> 32, v & 0xffffffff): each half sums
+#         exactly in a double over any realistic number of ranks (< 2^21), and the halves recombine to the exact
+#         integer; double SUMs as themselves; execution statistics (< 2^53) as doubles.
+#   MAX   MAX results as the order-preserving int64 image of the double (Double.compare order), MIN results as
+#         its bitwise complement (the order reversed, so MAX of it is the MIN), HLL registers one per slot, and
+#         per SUM slot a flag "this rank summed in double" (the int64 bound is per GPU): a SUM is exact only when
+#         no rank overflowed to double.
+def _f64_key(x: float) -> int:
+    u = int(np.array([x], "<f8").view(np.uint64)[0])
+    o = (~u & 0xFFFFFFFFFFFFFFFF) if u >> 63 else (u | (1 << 63))
+    return o - (1 << 63)  # signed image, same order
 
-    def __init__(self, aggregations, sample_row, integral_sums):
-        self.plan = []  # per function: list of (kind, index) where kind in int/fsum/min/max/hll
-        self.n = {"int": 0, "fsum": 0, "min": 0, "max": 0}
-        self.hll_m = 0
-        self.nhll = 0
-        for i, a in enumerate(aggregations):
+
+def _f64_from_key(k: int) -> float:
+    o = (int(k) + (1 << 63)) & 0xFFFFFFFFFFFFFFFF
+    u = (o & ((1 << 63) - 1)) if o >> 63 else (~o & 0xFFFFFFFFFFFFFFFF)
+    return float(np.array([u], np.uint64).view("<f8")[0])
+
+
+class _Layout:
+    """Where each function's intermediate lives in the SUM (float64) and MAX (int64) parts of a row."""
+
+    def __init__(self, aggregations, hll_m):
+        self.plan = []
+        self.nsum = 0
+        self.nmax = 0
+        for a in aggregations:
             f = a.function
             if f == "count":
-                self.plan.append([("int", self._take("int"))])
+                self.plan.append(("count", self._s(2)))
             elif f == "sum":
-                self.plan.append([("int", self._take("int"))] if integral_sums[i] else [("fsum", self._take("fsum"))])
-            elif f == "min":
-                self.plan.append([("min", self._take("min"))])
-            elif f == "max":
-                self.plan.append([("max", self._take("max"))])
+                self.plan.append(("sum", self._s(3), self._m(1)))
             elif f == "avg":
-                s = ("int", self._take("int")) if integral_sums[i] else ("fsum", self._take("fsum"))
-                self.plan.append([s, ("int", self._take("int"))])
+                self.plan.append(("avg", self._s(3), self._m(1), self._s(2)))
+            elif f == "min":
+                self.plan.append(("min", self._m(1)))
+            elif f == "max":
+                self.plan.append(("max", self._m(1)))
             elif f == "minmaxrange":
-                self.plan.append([("min", self._take("min")), ("max", self._take("max"))])
+                self.plan.append(("range", self._m(1), self._m(1)))
             elif f in _HLL_FUNCS:
-                m = len(sample_row[i]) if sample_row is not None else 1 << a.log2m
-                self.hll_m = m
-                self.plan.append([("hll", self.nhll)])
-                self.nhll += 1
+                m = hll_m or (1 << a.log2m)
+                self.plan.append(("hll", self._m(m), m))
             else:
                 raise NotImplementedError(f)
 
-    def _take(self, kind):
-        self.n[kind] += 1
-        return self.n[kind] - 1
+    def _s(self, n):
+        self.nsum += n
+        return self.nsum - n
 
-    def empty(self, rows):
-        return {"int": np.zeros((rows, self.n["int"]), np.int64),
-                "fsum": np.zeros((rows, self.n["fsum"]), np.float64),
-                "min": np.full((rows, self.n["min"]), np.inf),
-                "max": np.full((rows, self.n["max"]), -np.inf),
-                "hll": np.zeros((rows, self.nhll, max(self.hll_m, 1)), np.int32)}
+    def _m(self, n):
+        self.nmax += n
+        return self.nmax - n
 
-    def put(self, bufs, r, row):
-        for parts, v in zip(self.plan, row):
-            vals = v if len(parts) > 1 else (v,)
-            for (kind, j), x in zip(parts, vals):
-                if kind == "hll":
-                    bufs["hll"][r, j, :] = np.asarray(x, dtype=np.int32)
-                elif kind == "int":
-                    bufs["int"][r, j] = int(x)
-                else:
-                    bufs[kind][r, j] = float(x)
+    @staticmethod
+    def _put_int(sv, i, v):
+        v = int(v)
+        sv[i] = float(v >> 32)
+        sv[i + 1] = float(v & 0xFFFFFFFF)
 
-    def get(self, bufs, r):
+    @staticmethod
+    def _get_int(sv, i):
+        return (int(sv[i]) << 32) + int(sv[i + 1])
+
+    def _put_sum(self, sv, mv, i, j, v):
+        if isinstance(v, (int, np.integer)) and -(1 << 63) <= int(v) < (1 << 63):
+            self._put_int(sv, i, v)
+        else:
+            sv[i + 2] = float(v)
+            mv[j] = 1
+
+    def _get_sum(self, sv, mv, i, j):
+        exact = self._get_int(sv, i)
+        return float(exact) + float(sv[i + 2]) if mv[j] else exact
+
+    def put(self, sv, mv, row):
+        for p, v in zip(self.plan, row):
+            k = p[0]
+            if k == "count":
+                self._put_int(sv, p[1], v)
+            elif k == "sum":
+                self._put_sum(sv, mv, p[1], p[2], v)
+            elif k == "avg":
+                self._put_sum(sv, mv, p[1], p[2], v[0])
+                self._put_int(sv, p[3], v[1])
+            elif k == "min":
+                mv[p[1]] = ~_f64_key(float(v))
+            elif k == "max":
+                mv[p[1]] = _f64_key(float(v))
+            elif k == "range":
+                mv[p[1]] = ~_f64_key(float(v[0]))
+                mv[p[2]] = _f64_key(float(v[1]))
+            else:
+                r = np.asarray(v, dtype=np.int64)
+                mv[p[1]:p[1] + p[2]] = r
+
+    def empty_max(self, rows):
+        """MAX parts of rows no function touched: MIN = +inf, MAX = -inf (the functions' defaults)."""
+        mv = np.zeros((rows, self.nmax), np.int64)
+        for p in self.plan:
+            if p[0] == "min":
+                mv[:, p[1]] = ~_f64_key(float("inf"))
+            elif p[0] == "max":
+                mv[:, p[1]] = _f64_key(float("-inf"))
+            elif p[0] == "range":
+                mv[:, p[1]] = ~_f64_key(float("inf"))
+                mv[:, p[2]] = _f64_key(float("-inf"))
+        return mv
+
+    def get(self, sv, mv):
         out = []
-        for parts in self.plan:
-            vals = []
-            for kind, j in parts:
-                if kind == "hll":
-                    vals.append(bufs["hll"][r, j, :].astype(np.uint8))
-                elif kind == "int":
-                    vals.append(int(bufs["int"][r, j]))
-                else:
-                    vals.append(float(bufs[kind][r, j]))
-            out.append(tuple(vals) if len(parts) > 1 else vals[0])
+        for p in self.plan:
+            k = p[0]
+            if k == "count":
+                out.append(self._get_int(sv, p[1]))
+            elif k == "sum":
+                out.append(self._get_sum(sv, mv, p[1], p[2]))
+            elif k == "avg":
+                out.append((self._get_sum(sv, mv, p[1], p[2]), self._get_int(sv, p[3])))
+            elif k == "min":
+                out.append(_f64_from_key(~int(mv[p[1]])))
+            elif k == "max":
+                out.append(_f64_from_key(int(mv[p[1]])))
+            elif k == "range":
+                out.append((_f64_from_key(~int(mv[p[1]])), _f64_from_key(int(mv[p[2]]))))
+            else:
+                out.append(np.asarray(mv[p[1]:p[1] + p[2]]).astype(np.uint8))
         return out
 
 
-def _integral_sums(aggregations, rows):
-    """A SUM is exact-int64 when its intermediate is a Python int on every rank (see results.py)."""
-    out = []
-    for i, a in enumerate(aggregations):
-        if a.function == "sum":
-            out.append(all(isinstance(r[i], (int, np.integer)) for r in rows) if rows else False)
-        elif a.function == "avg":
-            out.append(all(isinstance(r[i][0], (int, np.integer)) for r in rows) if rows else False)
-        else:
-            out.append(False)
-    return out
-
-
-def _all_true(dist, group, flags: List[bool]) -> List[bool]:
+def _sum_max(dist, group, sv: np.ndarray, mv: np.ndarray):
+    """The merge's two collectives: float64 SUM of `sv` and int64 MAX of `mv`, staged through one host buffer
+    and one device buffer (a single copy each way)."""
     import torch
-    v = _reduce(dist, group, np.array([0 if f else 1 for f in flags] or [0], dtype=np.int64), dist.ReduceOp.SUM)
-    return [int(x) == 0 for x in v[:len(flags)]]
+    dev = _device(dist, group)
+    ns, nm = sv.size, mv.size
+    host = torch.empty(ns + nm, dtype=torch.float64, pin_memory=dev.type == "cuda")
+    hv = host.numpy()
+    hv[:ns] = sv.ravel()
+    hv[ns:].view(np.int64)[:] = mv.ravel()
+    d = host.to(dev, non_blocking=True)
+    if ns:
+        dist.all_reduce(d[:ns], op=dist.ReduceOp.SUM, group=group)
+    if nm:
+        dist.all_reduce(d[ns:].view(torch.int64), op=dist.ReduceOp.MAX, group=group)
+    out = d.cpu().numpy()
+    return out[:ns].reshape(sv.shape), out[ns:].view(np.int64).reshape(mv.shape)
 
 
-def _reduce_bufs(dist, group, bufs):
-    S, MIN, MAX = dist.ReduceOp.SUM, dist.ReduceOp.MIN, dist.ReduceOp.MAX
-    return {"int": _reduce(dist, group, bufs["int"], S), "fsum": _reduce(dist, group, bufs["fsum"], S),
-            "min": _reduce(dist, group, bufs["min"], MIN), "max": _reduce(dist, group, bufs["max"], MAX),
-            "hll": _reduce(dist, group, bufs["hll"], MAX)}
+def _hll_width(aggregations, rows):
+    for i, a in enumerate(aggregations):
+        if a.function in _HLL_FUNCS:
+            return len(rows[0][i]) if rows else 1 << a.log2m
+    return 0
 
 
 def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 22):
-    """Merge this rank's partial block with every other rank's; returns the merged block on every rank."""
+    """Merge this rank's partial block with every other rank's; returns the merged block on every rank.
+
+    Aggregation blocks: one float64 SUM + one int64 MAX all-reduce (_Layout). Group-by blocks: the key values
+    are exchanged once (all_gather_object) into node-global dictionaries, every rank scatters its groups into
+    the dense mixed-radix rows over those ids (column 0 least significant, as DictionaryBasedGroupKeyGenerator),
+    and the rows merge with the same SUM + MAX pair; above `max_dense_groups` the records are all-gathered and
+    merged by key instead."""
     if dist is None:
         import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return block
-    stats = _stats_from(_reduce(dist, group, _stats_vector(block.stats), dist.ReduceOp.SUM))
     aggs = block.aggregations
     if isinstance(block, AggregationResultsBlock):
-        integral = _all_true(dist, group, _integral_sums(aggs, [block.results]))
-        slots = _Slots(aggs, block.results, integral)
-        bufs = slots.empty(1)
-        slots.put(bufs, 0, block.results)
-        bufs = _reduce_bufs(dist, group, bufs)
-        return AggregationResultsBlock(aggs, slots.get(bufs, 0), stats)
+        lay = _Layout(aggs, _hll_width(aggs, [block.results]))
+        sv = np.zeros(6 + lay.nsum)
+        mv = lay.empty_max(1)[0]
+        sv[:6] = _stats_vector(block.stats)
+        lay.put(sv[6:], mv, block.results)
+        sv, mv = _sum_max(dist, group, sv, mv)
+        return AggregationResultsBlock(aggs, lay.get(sv[6:], mv), _stats_from(sv[:6]))
 
     # ---- group-by: node-global dictionaries over the key values --------------------------------
     keys = list(block.groups.keys())
@@ -167,47 +239,46 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
     world = dist.get_world_size(group)
     local_vals = [sorted({k[c] for k in keys}) for c in range(nk)]
     gathered = [None] * world
-    dist.all_gather_object(gathered, local_vals, group=group)
-    gdict = [sorted(set().union(*[g[c] for g in gathered])) for c in range(nk)]
+    dist.all_gather_object(gathered, (local_vals, _hll_width(aggs, list(block.groups.values()))), group=group)
+    gdict = [sorted(set().union(*[g[0][c] for g in gathered])) for c in range(nk)]
+    hll_m = max(g[1] for g in gathered)
     cards = [max(len(d), 1) for d in gdict]
     ndense = int(np.prod(cards, dtype=np.int64)) if nk else 1
-    limit = _reduce(dist, group, np.array([int(block.num_groups_limit_reached)], np.int64), dist.ReduceOp.MAX)
-    limit_reached = bool(limit[0])
-    rows = list(block.groups.values())
-    integral = _all_true(dist, group, _integral_sums(aggs, rows))
     if ndense > max_dense_groups:
         parts = [None] * world
-        dist.all_gather_object(parts, block.groups, group=group)
+        dist.all_gather_object(parts, (block.groups, _stats_vector(block.stats), bool(block.num_groups_limit_reached)),
+                               group=group)
         merged = {}
-        for p in parts:
+        for p, _, _ in parts:
             for k, v in p.items():
                 merged[k] = v if k not in merged else [merge_intermediate(a.function, x, y)
                                                        for a, x, y in zip(aggs, merged[k], v)]
-        return GroupByResultsBlock(aggs, block.group_by, merged, stats, limit_reached)
+        stats = _stats_from(np.sum([p[1] for p in parts], axis=0))
+        return GroupByResultsBlock(aggs, block.group_by, merged, stats, any(p[2] for p in parts))
     index = [{v: i for i, v in enumerate(d)} for d in gdict]
     strides = np.cumprod([1] + cards[:-1]).astype(np.int64)
-    sample = rows[0] if rows else None
-    # HLL width must agree on every rank even where this rank has no group
-    slots = _Slots(aggs, sample, integral)
-    for i, a in enumerate(aggs):
-        if a.function in _HLL_FUNCS:
-            slots.hll_m = 1 << a.log2m
-    bufs = slots.empty(ndense)
-    present = np.zeros(ndense, np.int64)
+    lay = _Layout(aggs, hll_m)
+    # SUM rows: [stats | presence count | row SUM parts]; MAX: [limit flag | row MAX parts]
+    sv = np.zeros(6 + ndense * (1 + lay.nsum))
+    mv = np.concatenate([np.array([int(block.num_groups_limit_reached)], np.int64), lay.empty_max(ndense).ravel()])
+    sv[:6] = _stats_vector(block.stats)
+    srows = sv[6:].reshape(ndense, 1 + lay.nsum)
+    mrows = mv[1:].reshape(ndense, lay.nmax)
     for k, v in block.groups.items():
         d = int(sum(index[c][k[c]] * strides[c] for c in range(nk)))
-        present[d] = 1
-        slots.put(bufs, d, v)
-    present = _reduce(dist, group, present, dist.ReduceOp.SUM)
-    bufs = _reduce_bufs(dist, group, bufs)
+        srows[d, 0] = 1.0
+        lay.put(srows[d, 1:], mrows[d], v)
+    sv, mv = _sum_max(dist, group, sv, mv)
+    srows = sv[6:].reshape(ndense, 1 + lay.nsum)
+    mrows = mv[1:].reshape(ndense, lay.nmax)
     groups = {}
-    for d in np.nonzero(present)[0]:
+    for d in np.nonzero(srows[:, 0])[0]:
         key, rem = [], int(d)
         for c in range(nk):
             key.append(gdict[c][rem % cards[c]])
             rem //= cards[c]
-        groups[tuple(key)] = slots.get(bufs, int(d))
-    return GroupByResultsBlock(aggs, block.group_by, groups, stats, limit_reached)
+        groups[tuple(key)] = lay.get(srows[d, 1:], mrows[d])
+    return GroupByResultsBlock(aggs, block.group_by, groups, _stats_from(sv[:6]), bool(mv[0]))
 
 
 # ------------------------------------------------------------------------------------------------------
@@ -367,44 +438,58 @@ def _rows_op(dist, group, table, rows, op):
     table[idx] = sub
 
 
-def allreduce_partial_table(table, hll, kinds, stats, dist, group=None):
+def allreduce_partial_table(table, hll, kinds, stats, dist, group=None, any_f64=None):
     """Merge this rank's dense partial table with every other rank's, in place (torch tensors on the
     communicator's device: RCCL over xGMI on the GPU server, gloo in CPU tests). `kinds` are the rows'
-    phip_partial row kinds (COUNT / SUM_I64 -> int64 SUM, SUM_F64 -> float64 SUM, MIN / MAX on the
-    order-preserving u64 image -> signed MIN / MAX after flipping the sign bit, HLL registers -> int32 MAX).
-    A row that is an exact int64 sum here but a double sum on another rank (the overflow bound is per
-    GPU) is converted to doubles first. Returns (merged kinds, merged stats)."""
+    phip_partial row kinds. One collective per reduce operator and type:
+      int64 SUM    COUNT / SUM_I64 rows and the six execution statistics, staged together;
+      float64 SUM  SUM_F64 rows;
+      int64 MAX    MAX rows as the signed image of their order-preserving u64 (sign bit flipped) and MIN rows as
+                   the complement of that image (order reversed, so the MAX of it is the MIN);
+      uint8 MAX    HLL registers (held as u32 by the library, exchanged as bytes).
+    A row that is an exact int64 sum here but a double sum on another rank (the overflow bound is per GPU) is
+    converted to doubles first: `any_f64[r]` says whether any rank holds row r in double (distributed_block
+    exchanges it with its shape check; None = exchange it here). Returns (merged kinds, merged stats)."""
     import torch
     from .. import _lib
-    S, MIN, MAX = dist.ReduceOp.SUM, dist.ReduceOp.MIN, dist.ReduceOp.MAX
+    S, MAX = dist.ReduceOp.SUM, dist.ReduceOp.MAX
     kinds = list(kinds)
     dev = table.device
-    f64 = torch.tensor([1 if k == _lib.ROW_SUM_F64 else 0 for k in kinds], dtype=torch.int64, device=dev)
-    dist.all_reduce(f64, op=MAX, group=group)
+    if any_f64 is None:
+        f64 = torch.tensor([1 if k == _lib.ROW_SUM_F64 else 0 for k in kinds], dtype=torch.int64, device=dev)
+        dist.all_reduce(f64, op=MAX, group=group)
+        any_f64 = [int(x) for x in f64.cpu().tolist()]
     for r, k in enumerate(kinds):
-        if k == _lib.ROW_SUM_I64 and int(f64[r]):
+        if k == _lib.ROW_SUM_I64 and any_f64[r]:
             table[r].copy_(table[r].to(torch.float64).view(torch.int64))
             kinds[r] = _lib.ROW_SUM_F64
     ints = [r for r, k in enumerate(kinds) if k in (_lib.ROW_COUNT, _lib.ROW_SUM_I64, _lib.ROW_HLL)]
     dbls = [r for r, k in enumerate(kinds) if k == _lib.ROW_SUM_F64]
     mins = [r for r, k in enumerate(kinds) if k == _lib.ROW_MIN]
     maxs = [r for r, k in enumerate(kinds) if k == _lib.ROW_MAX]
-    _rows_op(dist, group, table, ints, S)
-    if dbls:
-        tf = table.view(torch.float64)
-        _rows_op(dist, group, tf, dbls, S)
-    for rows, op in ((mins, MIN), (maxs, MAX)):
-        if rows:
-            for r in rows:
-                table[r].bitwise_xor_(_SIGN64)
-            _rows_op(dist, group, table, rows, op)
-            for r in rows:
-                table[r].bitwise_xor_(_SIGN64)
-    if hll is not None:
-        dist.all_reduce(hll, op=MAX, group=group)
+    ng = table.shape[1]
     st = torch.tensor(list(stats), dtype=torch.int64, device=dev)
-    dist.all_reduce(st, op=S, group=group)
-    return kinds, [int(x) for x in st.cpu().tolist()]
+    stage = torch.cat([table[ints].reshape(-1), st]) if ints else st
+    dist.all_reduce(stage, op=S, group=group)
+    if ints:
+        table[ints] = stage[:len(ints) * ng].view(len(ints), ng)
+    if dbls:
+        _rows_op(dist, group, table.view(torch.float64), dbls, S)
+    if mins or maxs:
+        rows = mins + maxs
+        sub = table[rows].bitwise_xor(_SIGN64)
+        nm = len(mins)
+        if nm:
+            sub[:nm] = sub[:nm].bitwise_not()
+        dist.all_reduce(sub, op=MAX, group=group)
+        if nm:
+            sub[:nm] = sub[:nm].bitwise_not()
+        table[rows] = sub.bitwise_xor(_SIGN64)
+    if hll is not None:
+        h8 = hll.to(torch.uint8)  # registers are <= 64: one byte each on the wire instead of four
+        dist.all_reduce(h8, op=MAX, group=group)
+        hll.copy_(h8)
+    return kinds, [int(x) for x in stage[-6:].cpu().tolist()]
 
 
 def distributed_block(op, dist=None, group=None, fallback_op=None):
@@ -415,8 +500,10 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
     it (the server-level trim runs once, after the merge). When any rank cannot hand out a dense table (hash
     key space, numGroupsLimit reached), every rank falls back to the record merge (allreduce_block) over
     `fallback_op` (an operator of the same query made with device_trim=False). Aggregation-only queries
-    all-reduce the few result slots (allreduce_block)."""
+    merge their result slots with one SUM and one MAX all-reduce (allreduce_block). A rank whose execution
+    raises tells the others through the shape check, so every rank raises instead of waiting in a collective."""
     import torch
+    from .. import _lib
     if dist is None:
         import torch.distributed as dist
     multi = dist.is_initialized() and dist.get_world_size(group) > 1
@@ -424,23 +511,36 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
         return op.next_block()
     if not getattr(op.query, "group_by", None) or not hasattr(op, "execute_partial"):
         return allreduce_block(op.next_block(), dist, group)
-    part = op.execute_partial()
+    _lib.load(with_torch=True)  # (torch's HIP runtime: the library must share it, _lib.load)
+    err = None
+    try:
+        part = op.execute_partial()
+    except Exception as e:  # noqa: BLE001 -- re-raised below, after the other ranks learned of it
+        part, err = None, e
     dev = _device(dist, group)
     shape = [0, 0, 0] if part is None or not part.global_keys else [1, part.num_groups, part.num_rows]
-    v = torch.tensor([1 - shape[0], shape[1], shape[2], -shape[1], -shape[2]], dtype=torch.int64, device=dev)
+    nrow = _lib.PARTIAL_MAX_ROWS
+    f64 = [1 if shape[0] and r < part.num_rows and part.row_kinds[r] == _lib.ROW_SUM_F64 else 0 for r in range(nrow)]
+    v = torch.tensor([1 if err is not None else 0, 1 - shape[0], shape[1], shape[2], -shape[1], -shape[2]] + f64,
+                     dtype=torch.int64, device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
     v = [int(x) for x in v.cpu().tolist()]
-    if v[0] == 0 and v[1] == -v[3] and v[2] == -v[4]:
+    if v[0]:
+        if err is not None:
+            raise err
+        raise RuntimeError("the query failed on another rank (distributed_block)")
+    if v[1] == 0 and v[2] == -v[4] and v[3] == -v[5]:
+        any_f64 = v[6:6 + part.num_rows]
         table, hll = partial_tensors(part)
         kinds = [part.row_kinds[r] for r in range(part.num_rows)]
         if table.device != dev:  # (gloo over host memory: stage through the host, CPU-communicator tests)
             t2, h2 = table.to(dev), (hll.to(dev) if hll is not None else None)
-            kinds, stats = allreduce_partial_table(t2, h2, kinds, list(part.stats), dist, group)
+            kinds, stats = allreduce_partial_table(t2, h2, kinds, list(part.stats), dist, group, any_f64)
             table.copy_(t2)
             if hll is not None:
                 hll.copy_(h2)
         else:
-            kinds, stats = allreduce_partial_table(table, hll, kinds, list(part.stats), dist, group)
+            kinds, stats = allreduce_partial_table(table, hll, kinds, list(part.stats), dist, group, any_f64)
         torch.cuda.current_stream(table.device).synchronize()
         for r, k in enumerate(kinds):
             part.row_kinds[r] = k

@@ -635,6 +635,7 @@ class GpuCombineOperator:
             blk.scan_kernel_ms = r.scan_kernel_ms
             blk.filter_kernel_ms, blk.agg_kernel_ms = r.filter_kernel_ms, r.agg_kernel_ms
             blk.filter_bytes, blk.agg_bytes = int(r.filter_bytes), int(r.agg_bytes)
+            blk.fused = bool(r.fused)
             return blk
         finally:
             lib.phip_result_free(res)

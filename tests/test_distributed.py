@@ -65,7 +65,10 @@ def _worker(rank, world, port, q, errs):
         qc.options["minServerGroupTrimSize"] = 20
         mine = [s for i, s in enumerate(segs) if i % world == rank]
         part, _ = executor.execute(qc, mine)
+        calls = _count_collectives(dist)
         merged = trim_groups(qc, allreduce_block(part, dist))
+        # one float64 SUM + one int64 MAX per merge, whatever the functions (DISTINCTCOUNTHLL, MIN, AVG ...)
+        assert sorted(calls) == [("max", "torch.int64"), ("sum", "torch.float64")], calls
         whole = trim_groups(qc, executor.execute(qc, segs)[0])
         if "DESC LIMIT 4" in q:
             assert len(whole.groups) == 20 and getattr(merged, "num_groups_trimmed", False)
@@ -83,6 +86,19 @@ def _worker(rank, world, port, q, errs):
         errs.put(f"rank {rank}: {type(e).__name__}: {e}")
     finally:
         dist.destroy_process_group()
+
+
+def _count_collectives(dist):
+    """Records (op, dtype) of every all_reduce the merge issues from here on."""
+    calls = []
+    orig = dist.all_reduce
+
+    def counted(t, op=None, group=None, **kw):
+        calls.append(("max" if op == dist.ReduceOp.MAX else ("sum" if op in (None, dist.ReduceOp.SUM) else str(op)),
+                      str(t.dtype)))
+        return orig(t, op=op if op is not None else dist.ReduceOp.SUM, group=group, **kw)
+    dist.all_reduce = counted
+    return calls
 
 
 def _free_port():
@@ -197,7 +213,15 @@ def _partial_worker(rank, world, port, f64_rank, errs):
         stats = [s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
                  s.num_total_docs, s.num_segments_processed, s.num_segments_matched]
         t, th = torch.from_numpy(table), torch.from_numpy(hll.reshape(-1))
-        kinds2, stats2 = allreduce_partial_table(t, th, kinds, stats, dist)
+        # the SUM_F64 flags as distributed_block exchanges them with its shape check
+        f = torch.tensor([1 if k == _lib.ROW_SUM_F64 else 0 for k in kinds], dtype=torch.int64)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        calls = _count_collectives(dist)
+        kinds2, stats2 = allreduce_partial_table(t, th, kinds, stats, dist, any_f64=f.tolist())
+        # one collective per (reduce operator, type): int64 SUM (counts, exact sums, statistics), float64 SUM,
+        # int64 MAX (MIN rows reversed), uint8 MAX (HLL registers)
+        assert sorted(calls) == sorted([("sum", "torch.int64"), ("sum", "torch.float64"), ("max", "torch.int64"),
+                                        ("max", "torch.uint8")]), calls
         whole, _ = executor.execute(qc, segs)
         assert stats2[0] == whole.stats.num_docs_scanned and stats2[3] == whole.stats.num_total_docs
         want_f64 = f64_rank is not None

@@ -1,9 +1,10 @@
 """HBM traffic per launch of the query kernels from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py.
 
 MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half of a wide coalesced stream's bytes on gfx950
-(128-B requests tallied at 64 B), so it is doubled; WRITE_SIZE (KB) is taken as is; the two counters need
-separate passes (TCC slots). Per kernel (filter_kernel, agg_kernel): bytes per launch = 2 x sum(FETCH_SIZE) /
-fetch-pass dispatches + sum(WRITE_SIZE) / write-pass dispatches. One pair of passes per bench layout.
+(128-B requests tallied at 64 B), so for a streaming kernel it is doubled; other access shapes are uncalibrated,
+so both figures are kept (raw and x2) and bench.py uses x2 only for the streaming filter kernel. WRITE_SIZE (KB)
+is taken as is; the two counters need separate passes (TCC slots). Per kernel family (filter_kernel,
+fused_filter_agg, agg_kernel): bytes per launch = sum over dispatches / dispatches. One pair of passes per layout.
 
   python tools/traffic.py --layout sorted <fetch_dir> <write_dir> [--layout unsorted <fetch_dir> <write_dir>]
          --queries Q1.1,Q1.2,Q1.3 --sf 100 -o profiles/r02_traffic.json
@@ -14,7 +15,18 @@ import glob
 import json
 import os
 
-KERNELS = ("filter_kernel", "agg_kernel")
+import re
+
+
+def family(kernel_name):
+    """filter_kernel (plain filter launch), fused_filter_agg (filter_kernel<C, NA> with NA > 0: it aggregated its
+    own tiles) or agg_kernel; None for the small kernels."""
+    m = re.search(r"phip::filter_kernel<(\w+), (\d+)>", kernel_name)
+    if m:
+        return "fused_filter_agg" if int(m.group(2)) > 0 else "filter_kernel"
+    if "phip::agg_kernel<" in kernel_name:
+        return "agg_kernel"
+    return None
 
 
 def per_kernel(d, counter):
@@ -24,10 +36,11 @@ def per_kernel(d, counter):
             for row in csv.DictReader(fh):
                 if row["Counter_Name"] != counter:
                     continue
-                for k in KERNELS:
-                    if f"phip::{k}<" in row["Kernel_Name"]:
-                        tot[k] = tot.get(k, 0.0) + float(row["Counter_Value"]) * 1024
-                        n[k] = n.get(k, 0) + 1
+                k = family(row["Kernel_Name"])
+                if k is None:
+                    continue
+                tot[k] = tot.get(k, 0.0) + float(row["Counter_Value"]) * 1024
+                n[k] = n.get(k, 0) + 1
     return tot, n
 
 
@@ -39,13 +52,20 @@ def main():
     ap.add_argument("-o", "--out", required=True)
     a = ap.parse_args()
     out = {"queries": a.queries.split(","), "sf": a.sf, "per_launch": {}, "dispatches": {},
-           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE passes (separate runs) over "
-                     "bench.py --layout <name>; HBM bytes per launch per kernel"}
+           "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes (separate runs) over bench.py --layout "
+                     "<name>; HBM bytes per launch per kernel family: raw = FETCH + WRITE, x2 = 2 x FETCH + "
+                     "WRITE (the gfx950 correction for wide coalesced streams)"}
     for name, fdir, wdir in a.layout:
         ft, fn = per_kernel(fdir, "FETCH_SIZE")
         wt, wn = per_kernel(wdir, "WRITE_SIZE")
-        out["per_launch"][name] = {k: int(2 * ft[k] / fn[k] + (wt.get(k, 0.0) / wn[k] if wn.get(k) else 0.0))
-                                   for k in ft if fn.get(k)}
+        pl = {}
+        for k in ft:
+            if not fn.get(k):
+                continue
+            f = ft[k] / fn[k]
+            w = wt.get(k, 0.0) / wn[k] if wn.get(k) else 0.0
+            pl[k] = {"fetch_raw": int(f), "write": int(w), "raw": int(f + w), "x2": int(2 * f + w)}
+        out["per_launch"][name] = pl
         out["dispatches"][name] = {"fetch": fn, "write": wn}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
