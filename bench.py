@@ -1,11 +1,14 @@
 """Headline benchmark: SSB SF100 flattened lineorder, Q1.1-Q1.3 (scan filter + SUM), per GPU.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; N>1 is launched by
-torch.distributed.run with one rank per GPU. A step = Q1.1 + Q1.2 + Q1.3, each one query over every
-segment resident on the rank (SF100 = 100 segments x 6M rows per GPU, weak scaling: rank r owns segments
-[100r, 100r+100) of an SF(100N) table). Partial aggregates of each query are merged across ranks with an
-RCCL all-reduce (the CombineOperator replacement's exchange step). value = rows scanned per second over the
-whole job (3 x 600M x N rows per step / max-over-ranks wall time of the K timed steps).
+torch.distributed.run with one rank per GPU. A step = Q1.1 + Q1.2 + Q1.3, each one query over 100 segments
+x 6M rows per GPU (SF100 per GPU, weak scaling). At N = 1 the rank holds exactly those 100 (BASELINE C2); at
+N > 1 each rank holds 125 segments of an SF(125N) table (N = 8: SF1000, BASELINE C5) and the step runs over
+the first 100 of them, while the C5 query (DISTINCTCOUNTHLL + GROUP BY) runs over all 125 per rank and is
+reported under "c5". Partial aggregates of each query are merged across ranks (the CombineOperator
+replacement's exchange step: one SUM + one MAX all-reduce per query, engine/distributed.py). value = rows
+scanned per second over the whole job (3 x 600M x N rows per step / max-over-ranks wall time of the K timed
+steps).
 
 Layout: rows sorted by LO_ORDERDATE, so D_YEAR / D_YEARMONTHNUM / D_WEEKNUMINYEAR carry
 sorted forward indexes and their predicates are doc ranges (SortedIndexBasedFilterOperator), exactly as
@@ -38,13 +41,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ROUND = "r03"
 
 
-def load_layout(ssb, sf, world, rank, cols, seed, layout, keep_host):
+def load_layout(ssb, seg_per_gpu, world, rank, cols, seed, layout, keep_host):
+    """This rank's segments [seg_per_gpu * rank, seg_per_gpu * (rank + 1)) of an SF(seg_per_gpu x world) table."""
     from pinot_amd.engine.segment import GpuSegment
-    seg_per_gpu = (sf * ssb.ROWS_PER_SF) // ssb.SEGMENT_ROWS
+    table_sf = seg_per_gpu * world * ssb.SEGMENT_ROWS // ssb.ROWS_PER_SF
     my_segs = list(range(rank * seg_per_gpu, (rank + 1) * seg_per_gpu))
     gsegs, raws = [], []
     for i in range(0, len(my_segs), 10):  # generate + load in chunks to bound host memory
-        for r in ssb.make_segments(sf * world, cols, seed=seed, segments=my_segs[i:i + 10], layout=layout):
+        for r in ssb.make_segments(table_sf, cols, seed=seed, segments=my_segs[i:i + 10], layout=layout):
             gsegs.append(GpuSegment(r))
             if keep_host:
                 raws.append(r)
@@ -53,6 +57,41 @@ def load_layout(ssb, sf, world, rank, cols, seed, layout, keep_host):
                     if not ci.metadata.is_sorted:  # reads sorted columns' doc ranges on the host (tiny)
                         ci.forward = b""
     return gsegs, raws
+
+
+def run_c5(args, dist, qc, gsegs, torch):
+    """BASELINE config C5: DISTINCTCOUNTHLL + GROUP BY over every segment of every rank, merged
+    across GPUs by distributed_block (node-global dictionaries registered once at load, the dense partial
+    tables all-reduced in place over RCCL, one collective per reduce operator and type). Returns wall seconds of
+    the K timed queries (max over ranks), per-query latencies and the merged block of the last query."""
+    from pinot_amd.engine.distributed import distributed_block, register_global_dictionaries
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    register_global_dictionaries(gsegs, [e.name for e in qc.group_by], dist)
+    op = GpuInstancePlanMaker().make_instance_plan(qc, gsegs)
+    fb = GpuInstancePlanMaker(device_trim=False).make_instance_plan(qc, gsegs)
+    for _ in range(args.warmup):
+        distributed_block(op, dist, fallback_op=fb)
+    lat = []
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    blk = None
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        blk = distributed_block(op, dist, fallback_op=fb)
+        lat.append((time.perf_counter() - ts) * 1e3)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    op.close()
+    fb.close()
+    return el, lat, blk
 
 
 def run_layout(args, dist, queries, qcs, gsegs, torch):
@@ -92,7 +131,7 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     for op in ops.values():
@@ -159,7 +198,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--sf", type=int, default=100, help="scale factor per GPU (SF100 = 600M rows)")
+    ap.add_argument("--segs-per-gpu", type=int, default=0,
+                    help="segments (6M rows each) per GPU: default 100 at one GPU (C2: SF100), 125 at N > 1 "
+                         "(N = 8: SF1000, BASELINE C5); Q1.x always runs over 100 of them per GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--c5", default="auto", choices=["auto", "on", "off"],
+                    help="also time the C5 query over all segments of all ranks (auto: at N > 1)")
     ap.add_argument("--queries", default="Q1.1,Q1.2,Q1.3")
     ap.add_argument("--layout", default="both", choices=["sorted", "unsorted", "both"],
                     help="headline = sorted (SURVEY.md §8d C2); both also measures the unsorted layout")
@@ -176,41 +220,60 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # (--dist-backend gloo with more ranks than GPUs rehearses the N > 1 path on a one-GPU box: ranks share a
+        # device and the merges stage through the host; the driver's runs use RCCL, one rank per GPU)
+        local_rank = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
     from pinot_amd import _lib
     import ctypes
-    dev = (ctypes.c_int32 * 1)(local_rank if world > 1 else 0)
+    dev = (ctypes.c_int32 * 1)(local_rank)
     _lib.check(_lib.load().phip_init(dev, 1))
 
     from pinot_amd.query.sql import parse
     from tools import ssb
 
     queries = args.queries.split(",")
-    cols = ssb.columns_for(queries)
+    seg_per_gpu = args.segs_per_gpu or (100 if world == 1 else 125)
+    head_segs = min(100, seg_per_gpu)  # C2's SF100 per GPU: weak scaling of the headline at exactly 100 per rank
+    want_c5 = args.c5 == "on" or (args.c5 == "auto" and world > 1)
+    cols = ssb.columns_for(queries + (["C5"] if want_c5 else []))
     qcs = {q: parse(ssb.SSB_QUERIES[q]) for q in queries}
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("queries") == queries and tj.get("sf") == args.sf:
+            if tj.get("queries") == queries and tj.get("sf") == 100:
                 traffic = tj.get("per_launch")
         except Exception:
             traffic = None
-    layouts = ["sorted", "unsorted"] if args.layout == "both" else [args.layout]
+    layouts = (["sorted", "unsorted"] if world == 1 else ["sorted"]) if args.layout == "both" else [args.layout]
     want_cpu = not args.no_cpu_baseline and rank == 0 and world == 1
     results = {}
     for li, layout in enumerate(layouts):
         t0 = time.time()
-        gsegs, raws = load_layout(ssb, args.sf, world, rank, cols, args.seed, layout, keep_host=want_cpu and li == 0)
+        gsegs, raws = load_layout(ssb, seg_per_gpu, world, rank, cols, args.seed, layout,
+                                  keep_host=want_cpu and li == 0)
         load_s = time.time() - t0
-        rows_per_rank = sum(s.num_docs for s in gsegs)
-        elapsed, lat, kstats = run_layout(args, dist, queries, qcs, gsegs, torch)
+        head = gsegs[:head_segs]
+        raws = raws[:head_segs]
+        rows_per_rank = sum(s.num_docs for s in head)
+        elapsed, lat, kstats = run_layout(args, dist, queries, qcs, head, torch)
+        res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(head),
+               "lat": lat, "roofline": roofline(kstats, queries, traffic, layout, args.steps)}
+        if want_c5 and li == 0:
+            qc5 = parse(ssb.SSB_QUERIES["C5"])
+            el5, lat5, blk5 = run_c5(args, dist, qc5, gsegs, torch)
+            rows5 = sum(s.num_docs for s in gsegs) * world
+            res["c5"] = {"query": ssb.SSB_QUERIES["C5"], "rows": rows5, "segments": len(gsegs) * world,
+                         "value": round(rows5 * args.steps / el5 / 1e9, 3), "unit": "G rows/s",
+                         "ms_per_query": round(el5 * 1e3 / args.steps, 3),
+                         "p50_latency_ms": round(float(np.median(lat5)), 3), "groups": len(blk5.groups),
+                         "merge": "distributed_block: node-global dictionaries, dense partial tables all-reduced "
+                                  "in place over RCCL (int64 SUM + uint8 MAX for this query)"}
         for s in gsegs:
             s.destroy()
-        res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(gsegs),
-               "lat": lat, "roofline": roofline(kstats, queries, traffic, layout, args.steps)}
         if want_cpu and li == 0:
             from oracle import cpu_baseline
             v, threads, reps, el, _ = cpu_baseline.time_queries([qcs[q] for q in queries], raws, min_seconds=10.0)
@@ -219,7 +282,7 @@ def main():
                                     f"server path, {threads} threads = the usable CPUs: "
                                     f"{cpu_baseline.usable_cpus()[1]}) running "
                                     f"{'+'.join(queries)} over the same {len(raws)} x {ssb.SEGMENT_ROWS}-row "
-                                    f"SF{args.sf} {layout} segments, {reps} reps in {el:.1f} s"}
+                                    f"SF{head_segs} {layout} segments, {reps} reps in {el:.1f} s"}
             del raws
         results[layout] = res
 
@@ -234,7 +297,7 @@ def main():
 
     value, ms_per_step = summary(head)
     out = {
-        "metric": "rows scanned/s (G) + p50 query latency, SSB flattened SF100, Q1.1-Q1.3",
+        "metric": "rows scanned/s (G) + p50 query latency, SSB flattened SF100/SF1000, 1-8 GPU",
         "value": round(value, 3),
         "unit": "G rows/s",
         "n_gpus": world,
@@ -246,8 +309,10 @@ def main():
         "vs_baseline": None,
         "dtype": "u32 dict ids / int64 sums",
         "data": "synthetic SSB-shaped (tools/ssbgen.c, seeded), Pinot segment encodings",
-        "config": {"workload": f"SSB SF{args.sf} flattened lineorder per GPU, {head['nseg']} segments x "
-                               f"{ssb.SEGMENT_ROWS} rows, queries {'+'.join(queries)}",
+        "config": {"workload": f"SSB SF{head['nseg']} flattened lineorder per GPU, {head['nseg']} segments x "
+                               f"{ssb.SEGMENT_ROWS} rows, queries {'+'.join(queries)}"
+                               + (f" (each rank holds {seg_per_gpu} segments of an SF{seg_per_gpu * world} table; "
+                                  f"C5 runs over all of them)" if want_c5 else ""),
                    "layout": f"{layouts[0]}" + (" by LO_ORDERDATE (SURVEY.md §8d C2)" if layouts[0] == "sorted" else ""),
                    "rows_per_gpu": head["rows_per_rank"], "parallelism": f"segment-sharded x{world}, RCCL all-reduce"},
         "p50_latency_ms": {q: round(float(np.median(head["lat"][q])), 3) for q in queries},
@@ -256,6 +321,8 @@ def main():
     }
     if "cpu" in head:
         out["cpu_baseline"] = head["cpu"]
+    if "c5" in head:
+        out["c5"] = head["c5"]
     if len(layouts) > 1:
         r = results[layouts[1]]
         v2, ms2 = summary(r)

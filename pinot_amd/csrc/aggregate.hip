@@ -330,17 +330,28 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
     }
     }
     if constexpr (MODE == GB_NONE) {
-      // Matched docs -> the ring in doc order: the tile word is transposed to the contiguous layout (lane L
-      // = docs 32L .. 32L+31), every lane writes its docs at the wave prefix of the lanes' popcounts. This
-      // costs ~40 instructions plus the lane's own matches per tile; a pass per 64-doc group (ballot + rank
-      // + write for each of the 32 groups) cost ~320 on sparse tiles, most of the unsorted layout's walk.
+      // Matched docs -> the ring: every lane writes its docs at the wave prefix (DPP scan) of the lanes'
+      // popcounts -- a few instructions plus the lane's own matches per tile; a pass per 64-doc group (ballot +
+      // rank + write for each of the 32 groups) cost ~320 on sparse tiles, most of the unsorted layout's walk.
+      // Lane-major order (lane l: docs 64g + l) when the tile holds few matches; a tile with at least a batch
+      // of them is first transposed to the contiguous layout (lane L: docs 32L .. 32L+31), so the ring is in doc
+      // order and a chunk's column reads are neighbours. Either way the order is a function of the data alone.
       if (ballot(m != 0) == 0) continue;
-      const uint32_t cw = lane_major_to_contig(m);
-      const uint32_t cnt = (uint32_t)__popc(cw);
-      const uint32_t incl = wave_incl_scan(cnt);
+      uint32_t cw = m;
+      uint32_t cnt = (uint32_t)__popc(cw);
+      uint32_t incl = wave_incl_scan(cnt);
       const int total = __builtin_amdgcn_readlane((int)incl, 63);
+      const bool doc_order = total >= 64 * kBatch;
+      int32_t ldoc = doc0 + lane;
+      int dstep = 64;
+      if (doc_order) {
+        cw = lane_major_to_contig(m);
+        cnt = (uint32_t)__popc(cw);
+        incl = wave_incl_scan(cnt);
+        ldoc = doc0 + 32 * lane;
+        dstep = 1;
+      }
       const int head0 = head;
-      const int32_t ldoc = doc0 + 32 * lane;
       // all at once when the ring has room, else in quarter-tile pieces (16 lanes, <= 512 docs) each after
       // draining the ring below one batch
       const int npiece = head - tail + total <= R ? 1 : 4;
@@ -353,7 +364,7 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
           while (w) {
             const int j = __builtin_clz(w);
             w &= ~(0x80000000u >> j);
-            ring[pos & (R - 1)] = (uint32_t)(ldoc + j);
+            ring[pos & (R - 1)] = (uint32_t)(ldoc + dstep * j);
             pos++;
           }
         }

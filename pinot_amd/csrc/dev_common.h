@@ -174,14 +174,16 @@ __device__ __forceinline__ uint32_t lane_major_to_contig(uint32_t m) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((32 * (lane & 1) + (lane >> 1)) << 2, (int)a);
 }
 
-// Inclusive prefix sum over the wave's 64 lanes.
+// Inclusive prefix sum over the wave's 64 lanes, in DPP (VALU) steps: row_shr 1/2/4/8 scan each 16-lane row,
+// row_bcast:15 / row_bcast:31 carry the row totals (GFX9 DPP; a disabled or out-of-row source reads as 0). Six
+// VALU ops instead of six dependent ds_bpermute round trips -- it runs once per tile of the aggregation walks.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)v, o);
-    v += lane >= o ? t : 0u;
-  }
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15, rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31, rows 2, 3
   return v;
 }
 

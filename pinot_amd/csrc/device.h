@@ -22,7 +22,9 @@ constexpr int kMaxHllRegs = 1 << 12;  // log2m <= 12 on the GPU path
 constexpr int kFilterBlock = 256;
 constexpr int kFilterWaves = kFilterBlock / kWave;
 constexpr int kMaxRing = 8;           // LDS-DMA ring slots per wave
-constexpr int kFusedRing = 512;       // fused aggregation: u16 tile-relative doc ids per wave (a quarter tile)
+constexpr int kFusedRingTile = 512;   // fused aggregation, per-tile mode: u16 tile-relative doc ids per wave
+constexpr int kFusedRingDefer = 1024; // fused aggregation, deferred mode: u32 segment doc ids per wave (one batch
+                                      // + a quarter tile)
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;
@@ -133,6 +135,10 @@ struct DevSeg {
   int32_t program;      // filter program of this entry: a plan with k programs (filtered aggregations) holds one
                         // entry per (segment, program), adjacent per segment; the aggregation kernel applies only
                         // the functions of that program (DevAgg.program) to its docs
+  int32_t fused_defer;  // fused aggregation, no value column streamed with the tile (sparse program): matched docs
+                        // collect across tiles in the wave's ring and their columns are gathered from HBM once
+                        // per kFusedBatch x 64 docs (the gathers do not stall the stream every tile)
+  int32_t pad_seg;
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
@@ -177,6 +183,8 @@ struct DevFilter {
   // each tile's matched docs itself, reading staged columns from the tile's ring slot (DevCol.lds_off)
   const struct DevAggQuery *agg;  // device copy of the aggregation descriptor, null = not fused
   uint64_t *agg_partials;         // [num_blocks][num_aggs]
+  int32_t fring_bytes;            // per-wave matched-doc ring (fused): 4 * kFusedRingDefer when a segment defers,
+  int32_t pad_f;                  // else 2 * kFusedRingTile
 };
 
 struct DevAgg {

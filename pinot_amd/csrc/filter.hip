@@ -764,10 +764,13 @@ __device__ __forceinline__ SmallDict load_small_dict(ccol_t &c) {
   return d;
 }
 
-// dict id of tile-relative doc td: from the staged words (LDS) or the forward index in HBM
+// dict id of tile-relative doc td: from the staged words (LDS) or the forward index in HBM (always HBM for the
+// deferred walk: its docs come from tiles whose ring slots are gone)
+template <bool kHbm = false>
 __device__ __forceinline__ uint32_t fused_id(ccol_t &c, const Tile &t, int32_t td) {
   const uint32_t b = (uint32_t)c.bits;
-  if (c.lds_off >= 0) return window_at((const PHIP_LDS uint32_t *)(t.stage + c.lds_off), td * (int32_t)b) >> (32 - b);
+  if (!kHbm && c.lds_off >= 0)
+    return window_at((const PHIP_LDS uint32_t *)(t.stage + c.lds_off), td * (int32_t)b) >> (32 - b);
   return decode_bits(c.words, (uint64_t)(uint32_t)(t.doc0 + td) * b, b);
 }
 
@@ -778,7 +781,7 @@ __device__ __forceinline__ uint64_t small_dict_bits(const SmallDict &sd, uint32_
 }
 
 // values of U docs as double: ids of all U first, then all U value loads (one round trip each)
-template <int U>
+template <int U, bool kHbm>
 __device__ __forceinline__ void fused_f64_u(ccol_t &c, const SmallDict &sd, const Tile &t, const int32_t (&td)[U],
                                             double (&v)[U]) {
   if (!c.has_dict) {
@@ -788,7 +791,7 @@ __device__ __forceinline__ void fused_f64_u(ccol_t &c, const SmallDict &sd, cons
   }
   uint32_t id[U];
 #pragma unroll
-  for (int u = 0; u < U; u++) id[u] = fused_id(c, t, td[u]);
+  for (int u = 0; u < U; u++) id[u] = fused_id<kHbm>(c, t, td[u]);
   const int ty = c.type;
   if (sd.on) {
     const bool wide = ty == PHIP_TYPE_LONG || ty == PHIP_TYPE_DOUBLE;
@@ -817,7 +820,7 @@ __device__ __forceinline__ void fused_f64_u(ccol_t &c, const SmallDict &sd, cons
   }
 }
 
-template <int U>
+template <int U, bool kHbm>
 __device__ __forceinline__ void fused_i64_u(ccol_t &c, const SmallDict &sd, const Tile &t, const int32_t (&td)[U],
                                             int64_t (&v)[U]) {
   if (!c.has_dict) {
@@ -827,7 +830,7 @@ __device__ __forceinline__ void fused_i64_u(ccol_t &c, const SmallDict &sd, cons
   }
   uint32_t id[U];
 #pragma unroll
-  for (int u = 0; u < U; u++) id[u] = fused_id(c, t, td[u]);
+  for (int u = 0; u < U; u++) id[u] = fused_id<kHbm>(c, t, td[u]);
   const int ty = c.type;
   if (sd.on) {
 #pragma unroll
@@ -854,7 +857,7 @@ __device__ __forceinline__ void fused_i64_u(ccol_t &c, const SmallDict &sd, cons
 }
 
 // U chunks of matched docs of the current tile (chunk u: lane's tile-relative doc td[u], active if bit u of act)
-template <int NA, int U>
+template <int NA, int U, bool kHbm>
 __device__ __forceinline__ void fused_batch(cquery_t &aq, cseg_t &seg, const Tile &t, const int32_t (&td)[U], uint32_t act,
                                             const SmallDict (&sda)[NA], const SmallDict (&sdb)[NA],
                                             uint64_t (&acc)[NA]) {
@@ -870,10 +873,10 @@ __device__ __forceinline__ void fused_batch(cquery_t &aq, cseg_t &seg, const Til
     ccol_t &ca = seg.cols[ag.col_a];
     if (kind == ACC_SUM_I64) {
       int64_t x[U];
-      fused_i64_u<U>(ca, sda[a], t, td, x);
+      fused_i64_u<U, kHbm>(ca, sda[a], t, td, x);
       if (ag.expr != PHIP_EXPR_COLUMN) {
         int64_t y[U];
-        fused_i64_u<U>(seg.cols[ag.col_b], sdb[a], t, td, y);
+        fused_i64_u<U, kHbm>(seg.cols[ag.col_b], sdb[a], t, td, y);
 #pragma unroll
         for (int u = 0; u < U; u++)
           x[u] = ag.expr == PHIP_EXPR_ADD ? x[u] + y[u] : (ag.expr == PHIP_EXPR_SUB ? x[u] - y[u] : x[u] * y[u]);
@@ -882,10 +885,10 @@ __device__ __forceinline__ void fused_batch(cquery_t &aq, cseg_t &seg, const Til
       for (int u = 0; u < U; u++) acc[a] += ((act >> u) & 1u) ? (uint64_t)x[u] : 0ull;
     } else {
       double x[U];
-      fused_f64_u<U>(ca, sda[a], t, td, x);
+      fused_f64_u<U, kHbm>(ca, sda[a], t, td, x);
       if (ag.expr != PHIP_EXPR_COLUMN) {
         double y[U];
-        fused_f64_u<U>(seg.cols[ag.col_b], sdb[a], t, td, y);
+        fused_f64_u<U, kHbm>(seg.cols[ag.col_b], sdb[a], t, td, y);
 #pragma unroll
         for (int u = 0; u < U; u++)
           x[u] = ag.expr == PHIP_EXPR_ADD ? x[u] + y[u] : (ag.expr == PHIP_EXPR_SUB ? x[u] - y[u] : x[u] * y[u]);
@@ -903,32 +906,68 @@ __device__ __forceinline__ void fused_batch(cquery_t &aq, cseg_t &seg, const Til
   }
 }
 
+// A tile's matched docs ranked by the wave prefix (DPP scan) of the lanes' popcounts: lane-major (lane l: docs
+// 64g + l) for a few matches, transposed to doc order (lane L: docs 32L .. 32L+31) from a batch on.
+struct TileRank {
+  uint32_t w;     // the lane's docs, bit 31-j = doc base + step * j
+  uint32_t excl;  // the lane's first rank
+  uint32_t incl;
+  int32_t base;   // tile-relative doc of bit 31
+  int32_t step;
+  int total;
+};
+__device__ __forceinline__ TileRank rank_tile(uint32_t mask) {
+  const int lane = lane_id();
+  TileRank r;
+  r.w = mask;
+  uint32_t cnt = (uint32_t)__popc(mask);
+  r.incl = wave_incl_scan(cnt);
+  r.total = __builtin_amdgcn_readlane((int)r.incl, 63);
+  r.base = lane;
+  r.step = 64;
+  if (r.total >= 64 * kFusedBatch) {
+    r.w = lane_major_to_contig(mask);
+    cnt = (uint32_t)__popc(r.w);
+    r.incl = wave_incl_scan(cnt);
+    r.base = 32 * lane;
+    r.step = 1;
+  }
+  r.excl = r.incl - cnt;
+  return r;
+}
+
+// the docs of lanes [l0, l1) at their ranks - sub, plus `add`
+template <typename T, int RING>
+__device__ __forceinline__ void write_ranked(const TileRank &r, int l0, int l1, int sub, int32_t add, PHIP_LDS T *ring) {
+  const int lane = lane_id();
+  if (lane >= l0 && lane < l1) {
+    uint32_t w = r.w;
+    int pos = (int)r.excl - sub;
+    while (w) {
+      const int j = __builtin_clz(w);
+      w &= ~(0x80000000u >> j);
+      ring[pos & (RING - 1)] = (T)(add + r.base + r.step * j);
+      pos++;
+    }
+  }
+}
+
+// per-tile mode: the tile's docs read from its ring slot (streamed value columns), drained before the next tile
 template <int NA>
 __device__ __forceinline__ void fused_tile(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
                                            PHIP_LDS uint16_t *ring, const SmallDict (&sda)[NA],
                                            const SmallDict (&sdb)[NA], uint64_t (&acc)[NA]) {
   if (ballot(mask != 0) == 0) return;
   const int lane = lane_id();
-  const uint32_t cw = lane_major_to_contig(mask);  // lane L: docs 32L .. 32L+31, bit 31-j = doc 32L+j
-  const uint32_t cnt = (uint32_t)__popc(cw);
-  const uint32_t incl = wave_incl_scan(cnt);
-  const int total = __builtin_amdgcn_readlane((int)incl, 63);
+  const TileRank r = rank_tile(mask);
   // the whole tile at once when it fits the ring, else quarter tiles (16 lanes, <= 512 docs)
-  const int npiece = total <= kFusedRing ? 1 : 4;
+  const int npiece = r.total <= kFusedRingTile ? 1 : 4;
   const int lanes = 64 / npiece;
   for (int p = 0; p < npiece; p++) {
-    const int s = p == 0 ? 0 : __builtin_amdgcn_readlane((int)incl, lanes * p - 1);
-    const int e = __builtin_amdgcn_readlane((int)incl, lanes * p + lanes - 1);
+    const int s = p == 0 ? 0 : __builtin_amdgcn_readlane((int)r.incl, lanes * p - 1);
+    const int e = __builtin_amdgcn_readlane((int)r.incl, lanes * p + lanes - 1);
     if (e == s) continue;
-    if (lane >= lanes * p && lane < lanes * (p + 1)) {
-      uint32_t w = cw;
-      int pos = (int)(incl - cnt) - s;
-      while (w) {
-        const int j = __builtin_clz(w);
-        w &= ~(0x80000000u >> j);
-        ring[pos++] = (uint16_t)(32 * lane + j);
-      }
-    }
+    write_ranked<uint16_t, kFusedRingTile>(r, lanes * p, lanes * (p + 1), s, 0, ring);
     const int n = e - s;
     for (int c = 0; c < n; c += 64 * kFusedBatch) {
       int32_t td[kFusedBatch];
@@ -939,9 +978,47 @@ __device__ __forceinline__ void fused_tile(cquery_t &aq, cseg_t &seg, const Tile
         td[u] = on ? (int32_t)ring[c + 64 * u + lane] : 0;
         act |= on ? (1u << u) : 0u;
       }
-      fused_batch<NA, kFusedBatch>(aq, seg, t, td, act, sda, sdb, acc);
+      fused_batch<NA, kFusedBatch, false>(aq, seg, t, td, act, sda, sdb, acc);
     }
     __builtin_amdgcn_wave_barrier();  // ring reads done before the next piece's writes
+  }
+}
+
+// deferred mode: kFusedBatch chunks of the ring (segment docs, columns from HBM)
+template <int NA>
+__device__ __forceinline__ void fused_flush(cquery_t &aq, cseg_t &seg, const PHIP_LDS uint32_t *ring, int tail, int n,
+                                            const SmallDict (&sda)[NA], const SmallDict (&sdb)[NA], uint64_t (&acc)[NA]) {
+  const int lane = lane_id();
+  int32_t d[kFusedBatch];
+  uint32_t act = 0;
+#pragma unroll
+  for (int u = 0; u < kFusedBatch; u++) {
+    const bool on = 64 * u + lane < n;
+    d[u] = on ? (int32_t)ring[(tail + 64 * u + lane) & (kFusedRingDefer - 1)] : 0;
+    act |= on ? (1u << u) : 0u;
+  }
+  const Tile tz{0, 0, nullptr};
+  fused_batch<NA, kFusedBatch, true>(aq, seg, tz, d, act, sda, sdb, acc);
+}
+
+// deferred mode: append the tile's matched docs; a full batch is projected at once
+template <int NA>
+__device__ __forceinline__ void fused_defer(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
+                                            PHIP_LDS uint32_t *ring, int &head, int &tail, const SmallDict (&sda)[NA],
+                                            const SmallDict (&sdb)[NA], uint64_t (&acc)[NA]) {
+  if (ballot(mask != 0) == 0) return;
+  const TileRank r = rank_tile(mask);
+  const int head0 = head;
+  const int npiece = head - tail + r.total <= kFusedRingDefer ? 1 : 4;
+  const int lanes = 64 / npiece;
+  for (int p = 0; p < npiece; p++) {
+    const int e = __builtin_amdgcn_readlane((int)r.incl, lanes * p + lanes - 1);
+    write_ranked<uint32_t, kFusedRingDefer>(r, lanes * p, lanes * (p + 1), -head0, t.doc0, ring);
+    head = head0 + e;
+    while (head - tail >= 64 * kFusedBatch) {
+      fused_flush<NA>(aq, seg, ring, tail, 64 * kFusedBatch, sda, sdb, acc);
+      tail += 64 * kFusedBatch;
+    }
   }
 }
 
@@ -1042,8 +1119,11 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   const int stride = q.stage_stride;
   PHIP_LDS uint8_t *ring = (PHIP_LDS uint8_t *)(smem + (size_t)wave * nbuf * stride);
   // fused aggregation: the wave's matched-doc ring sits after every wave's DMA ring
-  PHIP_LDS uint16_t *docring =
-      (PHIP_LDS uint16_t *)(smem + (size_t)kFilterWaves * nbuf * stride) + (NA > 0 ? wave * kFusedRing : 0);
+  PHIP_LDS uint8_t *docring_b = (PHIP_LDS uint8_t *)(smem + (size_t)kFilterWaves * nbuf * stride) +
+                                (NA > 0 ? (size_t)wave * q.fring_bytes : 0);
+  PHIP_LDS uint16_t *docring = (PHIP_LDS uint16_t *)docring_b;
+  PHIP_LDS uint32_t *deferring = (PHIP_LDS uint32_t *)docring_b;
+  int dhead = 0, dtail = 0;  // deferred ring cursors (wave-uniform)
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
 
   cseg_t *segs = (cseg_t *)q.segs;
@@ -1094,6 +1174,11 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   for (int t = begin; t < end; t += step, k++) {
     if (pf < end) PHIP_PREFETCH();
     if (t >= seg_end) {  // entering a new segment: flush the previous one's count
+      if constexpr (NA > 0) {  // the previous segment's deferred docs, before its small dictionaries go
+        if (si >= 0 && dhead > dtail)
+          fused_flush<NA>(*(cquery_t *)q.agg, segs[si], deferring, dtail, dhead - dtail, sda, sdb, acc);
+        dhead = dtail = 0;
+      }
       if (si >= 0) {
         const uint64_t m = wave_reduce_u64_add(lane_matched);
         lane_matched = 0;
@@ -1143,10 +1228,16 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     scanned += scanned_t;
     lane_matched += (uint32_t)__popc(mask);
     if (st) ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
-    if constexpr (NA > 0) fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, docring, sda, sdb, acc);
+    if constexpr (NA > 0) {
+      if (seg.fused_defer) fused_defer<NA>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail, sda, sdb, acc);
+      else fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, docring, sda, sdb, acc);
+    }
     slot = slot + 1 == nbuf ? 0 : slot + 1;
   }
 #undef PHIP_PREFETCH
+  if constexpr (NA > 0) {
+    if (si >= 0 && dhead > dtail) fused_flush<NA>(*(cquery_t *)q.agg, segs[si], deferring, dtail, dhead - dtail, sda, sdb, acc);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (si >= 0) {
     const uint64_t m = wave_reduce_u64_add(lane_matched);

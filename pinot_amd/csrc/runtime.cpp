@@ -1822,6 +1822,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   bool any_filter_prog = false;
   for (const DevSeg &ds : dsegs) any_filter_prog |= ds.node_end > ds.node_begin;
   int fused_naggs = 0;
+  bool any_defer = false;
   {
     // Fusion saves a launch, the mask round trip and the filter columns' re-read, but a streaming filter
     // wave that stops for a tile's projection gathers leaves its LDS-DMA ring idle. Measured on SSB SF100
@@ -1849,6 +1850,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       for (size_t i = 0; i < dsegs.size(); i++) {
         DevSeg &ds = dsegs[i];
         int32_t off = seg_off[i];
+        const int32_t nstage0 = ds.num_stage;
         for (int a = 0; a < naggs; a++) {
           const DevAgg &ag = dq.aggs[a];
           if (ag.acc == ACC_COUNT) continue;
@@ -1869,6 +1871,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
           }
         }
         stage_stride = std::max(stage_stride, off);
+        // nothing streamed with the tile: the matched docs collect across tiles (filter.hip fused_defer)
+        ds.fused_defer = ds.num_stage == nstage0 ? 1 : 0;
+        if (const char *fd = getenv("PHIP_FUSED_DEFER")) ds.fused_defer = ds.fused_defer && atoi(fd) != 0;  // A/B
+        any_defer |= ds.fused_defer != 0;
       }
     }
   }
@@ -1912,6 +1918,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // each wave the deepest ring that then fits the 160 KiB LDS (bytes in flight per CU =
   // blocks x 4 waves x (nbuf-1) x slot)
   int nbuf = 0, fbpc = 0;
+  const int32_t fring_bytes = any_defer ? 4 * kFusedRingDefer : 2 * kFusedRingTile;  // per wave (filter.hip)
   {
     const char *env = getenv("PHIP_FILTER_BPC");  // measurement override
     int want = env ? std::max(1, std::min(8, atoi(env))) : (conj_only ? 6 : 4);
@@ -1923,7 +1930,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const int64_t waves_at = (int64_t)dev->num_cus * want * kFilterWaves;
     if (!env && total_work >= 4 * waves_at)
       while (want > 2 && total_work < kMinTilesPerWave * (int64_t)dev->num_cus * want * kFilterWaves) want--;
-    const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * kFusedRing * 2 : 0;  // fused doc rings (u16)
+    const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * fring_bytes : 0;  // fused doc rings
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
       const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024 - 1024) / bpc - fring) / ((int64_t)kFilterWaves * stage_stride));
       if (nb >= 2) {
@@ -1933,7 +1940,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
     if (nbuf < 2) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
   }
-  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_naggs > 0 ? (size_t)kFilterWaves * kFusedRing * 2 : 0);
+  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_naggs > 0 ? (size_t)kFilterWaves * fring_bytes : 0);
   const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "xcdc" / "contig"
   // contiguous per-wave ranges measured fastest for the plain filter; a fused aggregation's waves stay inside
   // their XCD's eighth of the work (its dictionaries then stay in that XCD's L2)
@@ -2005,6 +2012,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   fq.total_work = (int32_t)total_work;
   fq.stage_stride = stage_stride;
   fq.nbuf = nbuf;
+  fq.fring_bytes = fring_bytes;
   fq.xcd_walk = xcd_walk;
   {
     const char *pe = getenv("PHIP_FILTER_PROBE");

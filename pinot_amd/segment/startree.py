@@ -268,3 +268,150 @@ def build_star_tree(config: StarTreeIndexConfig, dims_ids: Sequence[np.ndarray],
         meta = ColumnMetadata(col, dt, n, 0, 0, False, False, False)
         seg.columns[col] = ColumnIndexes(meta, _chunk_forward(vals[:n], dt))
     return StarTree(config, b.dimensions, root, b.num_nodes, seg, b.pairs)
+
+
+# ------------------------------------------------------------------------------------------------------
+# Pinot's on-disk star-tree (segment v3: star_tree_index + star_tree_index_map, metadata.properties startree.v2.*),
+# so that a server pins Pinot-written star-trees at load instead of rebuilding them.
+# ------------------------------------------------------------------------------------------------------
+STAR_TREE_MAGIC = 0xBADDA55B00DAD00D  # OffHeapStarTree.MAGIC_MARKER
+STAR_TREE_VERSION = 1                 # OffHeapStarTree.VERSION
+_NODE_INTS = 7                        # OffHeapStarTreeNode.NUM_SERIALIZABLE_FIELDS
+
+
+def parse_properties(text: str) -> Dict[str, List[str]]:
+    """metadata.properties / star_tree_index_map as Commons Configuration reads them: `key = value` lines,
+    `#` comments, a key may repeat (a list). Values are returned unescaped of the `\\uXXXX` forms."""
+    out: Dict[str, List[str]] = {}
+    for line in text.splitlines():
+        line = line.strip()
+        if not line or line.startswith("#") or line.startswith("!"):
+            continue
+        k, sep, v = line.partition("=")
+        if not sep:
+            continue
+        v = v.strip()
+        if "\\u" in v:
+            v = v.encode("latin-1", "backslashreplace").decode("unicode_escape")
+        out.setdefault(k.strip(), []).append(v)
+    return out
+
+
+def star_tree_metadata(props: Dict[str, List[str]]) -> List[dict]:
+    """StarTreeV2Metadata of every tree (SegmentMetadataImpl: startree.v2.count, startree.v2.<i>.total.docs /
+    split.order / function.column.pairs / skip.star.node.creation / max.leaf.records)."""
+    n = int(props.get("startree.v2.count", ["0"])[0])
+    out = []
+    for i in range(n):
+        p = f"startree.v2.{i}."
+        split = [x.strip() for v in props.get(p + "split.order", []) for x in v.split(",") if x.strip()]
+        pairs = [x.strip() for v in props.get(p + "function.column.pairs", []) for x in v.split(",") if x.strip()]
+        skip = [x.strip() for v in props.get(p + "skip.star.node.creation", []) for x in v.split(",") if x.strip()]
+        out.append({"total_docs": int(props[p + "total.docs"][0]), "split_order": split, "pairs": pairs,
+                    "skip": skip, "max_leaf_records": int(props.get(p + "max.leaf.records", [DEFAULT_MAX_LEAF_RECORDS])[0])})
+    return out
+
+
+def parse_star_tree_index_map(text: str) -> Dict[tuple, tuple]:
+    """star_tree_index_map (StarTreeIndexMapUtils): `<tree>.<column>.<STAR_TREE|FORWARD_INDEX>.OFFSET / .SIZE`
+    -> {(tree, column or None, type): (offset, size)}."""
+    raw: Dict[tuple, dict] = {}
+    for k, vs in parse_properties(text).items():
+        parts = k.split(".")
+        tree, field_ = int(parts[0]), parts[-1]
+        kind = parts[-2]
+        col = ".".join(parts[1:-2])
+        raw.setdefault((tree, None if col == "null" else col, kind), {})[field_] = int(vs[0])
+    return {key: (v["OFFSET"], v["SIZE"]) for key, v in raw.items()}
+
+
+def decode_off_heap_tree(buf: bytes):
+    """OffHeapStarTree (OffHeapStarTree.java:38-79, little-endian): magic, version, root node offset, dimension
+    names (id, utf-8 bytes), node count, then 7-int nodes (OffHeapStarTreeNode.java: dimension id, dimension value,
+    start doc, end doc (exclusive), aggregated doc, first child, last child; -1 = no child). Returns
+    (dimension names, root TreeNode, node count)."""
+    import struct
+    magic, version, root_off, ndims = struct.unpack_from("<QiiI", buf, 0)
+    if magic != STAR_TREE_MAGIC:
+        raise ValueError("invalid magic marker in star-tree data buffer")
+    if version != STAR_TREE_VERSION:
+        raise ValueError(f"star-tree version {version} is not {STAR_TREE_VERSION}")
+    off = 20
+    names: List[Optional[str]] = [None] * ndims
+    for _ in range(ndims):
+        did, nb = struct.unpack_from("<ii", buf, off)
+        off += 8
+        names[did] = bytes(buf[off:off + nb]).decode("utf-8")
+        off += nb
+    (num_nodes,) = struct.unpack_from("<i", buf, off)
+    off += 4
+    if off != root_off:
+        raise ValueError("star-tree header length mismatch")
+    if off + num_nodes * _NODE_INTS * 4 != len(buf):
+        raise ValueError("star-tree buffer size mismatch")
+    nd = np.frombuffer(buf, dtype="<i4", count=num_nodes * _NODE_INTS, offset=off).reshape(num_nodes, _NODE_INTS)
+    if num_nodes == 0:
+        raise ValueError("star-tree without nodes")
+
+    def make(i):
+        r = nd[i]
+        return TreeNode(int(r[0]), int(r[1]), int(r[2]), int(r[3]), int(r[4]))
+
+    nodes = [make(i) for i in range(num_nodes)]
+    # (the writer leaves the root's doc range unset, -1 / -1: it is the span of its non-star children)
+    for i in range(num_nodes):
+        first, last = int(nd[i, 5]), int(nd[i, 6])
+        if first < 0:
+            continue
+        if not (i < first <= last < num_nodes):
+            raise ValueError(f"star-tree node {i}: children [{first}, {last}] out of order")
+        kids = {}
+        for c in range(first, last + 1):
+            kids[nodes[c].dimension_value] = nodes[c]  # ALL (-1) is the star child (serialized first)
+        nodes[i].children = kids
+        nodes[i].child_dimension_id = int(nd[first, 0])
+    root = nodes[0]
+    if root.start_doc < 0 and root.children:
+        kids = [c for v, c in root.children.items() if v != ALL]
+        root.start_doc = min(c.start_doc for c in kids)
+        root.end_doc = max(c.end_doc for c in kids)
+    return [str(n) for n in names], root, num_nodes
+
+
+def read_pinot_star_trees(index: bytes, index_map: str, metadata: str, parent_columns, name: str = "startree"
+                          ) -> List[StarTree]:
+    """Every star-tree of a Pinot v3 segment directory, as the StarTree the GPU star-tree operator traverses
+    (StarTreeIndexReader.java: one buffer, the tree little-endian, forward indexes big-endian). The star-tree
+    documents become an ImmutableSegment: split-order dimensions as fixed-bit dict ids sharing the parent
+    column's dictionary (`parent_columns`: column -> ColumnIndexes of the segment), function-column pairs as
+    the raw chunk forward indexes Pinot wrote (count__* LONG, sum / min / max DOUBLE: the ValueAggregators'
+    result types)."""
+    from .creator import ColumnIndexes, ColumnMetadata, ImmutableSegment
+    metas = star_tree_metadata(parse_properties(metadata))
+    entries = parse_star_tree_index_map(index_map)
+    out = []
+    for i, m in enumerate(metas):
+        off, size = entries[(i, None, "STAR_TREE")]
+        dims, root, num_nodes = decode_off_heap_tree(index[off:off + size])
+        if dims != m["split_order"]:
+            raise ValueError(f"star-tree {i}: dimensions {dims} differ from the split order {m['split_order']}")
+        cfg = StarTreeIndexConfig(tuple(dims), tuple(m["pairs"]), tuple(m["skip"]), m["max_leaf_records"])
+        n = m["total_docs"]
+        seg = ImmutableSegment(f"{name}{i}", n)
+        for d in dims:
+            src = parent_columns[d].metadata
+            o, sz = entries[(i, d, "FORWARD_INDEX")]
+            want = (n * src.bits_per_element + 7) // 8
+            if sz < want:
+                raise ValueError(f"star-tree {i}: forward index of {d} holds {sz} bytes, {want} needed")
+            meta = ColumnMetadata(d, src.data_type, n, src.cardinality, src.bits_per_element, False, True, False,
+                                  src.string_width)
+            seg.columns[d] = ColumnIndexes(meta, bytes(index[o:o + sz]), parent_columns[d].dictionary, None)
+        pairs = cfg.pairs()
+        for f, c in pairs:
+            col = pair_column(f, c)
+            o, sz = entries[(i, col, "FORWARD_INDEX")]
+            dt = DataType.LONG if f == "count" else DataType.DOUBLE
+            seg.columns[col] = ColumnIndexes(ColumnMetadata(col, dt, n, 0, 0, False, False, False), bytes(index[o:o + sz]))
+        out.append(StarTree(cfg, list(dims), root, num_nodes, seg, pairs))
+    return out

@@ -171,3 +171,71 @@ def test_gpu_partial_inplace_rccl_world1(gpu_lib):
         dist.destroy_process_group()
         for s in segs:
             s.destroy()
+
+
+# ---- BASELINE config C5 through the sharded path ---------------------------------------------------------------
+def _c5_worker(rank, world, port, errs):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import executor
+        from pinot_amd.engine.distributed import distributed_block, register_global_dictionaries
+        from pinot_amd.engine.plan import GpuInstancePlanMaker
+        from pinot_amd.engine.segment import GpuSegment
+        from pinot_amd.query.sql import parse
+        from tools import ssb
+        qc = parse(ssb.SSB_QUERIES["C5"])
+        raws = ssb.make_segments(1, ssb.columns_for(["C5"]), segment_rows=1_000_000)  # SSB SF1, 6 segments
+        mine = [GpuSegment(s) for i, s in enumerate(raws) if i % world == rank]
+        register_global_dictionaries(mine, [e.name for e in qc.group_by], dist)
+        op = GpuInstancePlanMaker().make_instance_plan(qc, mine)
+        fb = GpuInstancePlanMaker(device_trim=False).make_instance_plan(qc, mine)
+        calls = []
+        orig = dist.all_reduce
+
+        def counted(t, op=None, group=None, **kw):
+            calls.append((str(op), str(t.dtype)))
+            return orig(t, op=op if op is not None else dist.ReduceOp.SUM, group=group, **kw)
+        dist.all_reduce = counted
+        merged = distributed_block(op, dist, fallback_op=fb)
+        dist.all_reduce = orig
+        # the device path: the shape check (int64 MAX), then the table -- counts + exact SUM + statistics as one
+        # int64 SUM, the HLL registers as one uint8 MAX
+        assert len(calls) == 3 and sorted(c[1] for c in calls) == ["torch.int64", "torch.int64", "torch.uint8"], calls
+        whole, _ = executor.execute(qc, raws)
+        assert len(whole.groups) == 35  # 7 years x the 5 nations of AMERICA
+        _compare(merged, whole, qc)
+        op.close()
+        fb.close()
+        for s in mine:
+            s.destroy()
+    except Exception as e:  # surfaced to the parent
+        import traceback
+        errs.put(f"rank {rank}: {type(e).__name__}: {e}\n{traceback.format_exc()}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_c5_sharded_world2(gpu_lib):
+    """BASELINE C5 (DISTINCTCOUNTHLL(LO_CUSTKEY) + SUM(LO_REVENUE - LO_SUPPLYCOST) GROUP BY D_YEAR, C_NATION) over
+    SSB SF1 split across two ranks: global dictionaries -> dense partial tables -> merge -> finish equals the
+    oracle over all six segments (registers and integer sums bit-exact)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errs = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c5_worker, args=(r, 2, port, errs)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=110)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not errs.empty():
+        msgs.append(errs.get())
+    assert not msgs, msgs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
