@@ -60,9 +60,11 @@
 /* ---- forward index encodings -------------------------------------------------------------- */
 #define PHIP_FWD_FIXED_BIT 0 /* FixedBitSVForwardIndexWriter: ceil(N*b/8) BE bytes, MSB first */
 #define PHIP_FWD_SORTED 1    /* SortedIndexReaderImpl: card x (start,end) BE int32, inclusive */
-#define PHIP_FWD_RAW_CHUNK 2 /* BaseChunkForwardIndexWriter v2/v3 fixed-width chunks: PASS_THROUGH, or SNAPPY / LZ4 /
-                              * LZ4_LENGTH_PREFIXED decoded on the GPU at load (ZSTANDARD / GZIP -> UNSUPPORTED);
-                              * v1 (4-int header, SNAPPY chunks: BaseChunkForwardIndexReader.java:86-95) as well */
+#define PHIP_FWD_RAW_CHUNK 2 /* BaseChunkForwardIndexWriter v2/v3 fixed-width chunks (and v4/v5 power-of-two chunks,
+                              * FixedBytePower2ChunkSVForwardIndexReader): PASS_THROUGH, or SNAPPY / LZ4 /
+                              * LZ4_LENGTH_PREFIXED / ZSTANDARD / GZIP decoded on the GPU at load (a malformed chunk
+                              * fails the load); v1 (4-int header, SNAPPY chunks: BaseChunkForwardIndexReader.java:86-95)
+                              * as well */
 
 typedef struct phip_column_desc {
   const char *name;
@@ -336,10 +338,14 @@ typedef struct phip_partial {
  * PHIP_ERR_UNSUPPORTED, with nothing to merge, for hash-table key spaces and when the GPU's distinct groups
  * reach numGroupsLimit (the per-segment first-seen limit needs the record path: phip_plan_execute). Until
  * phip_plan_finish the table belongs to the caller: it may all-reduce it in place (on any stream, synchronised
- * before phip_plan_finish). No other execution of the same plan may start in between. */
+ * before phip_plan_finish). No other execution of the same plan may start in between (the library refuses one
+ * with PHIP_ERR_INVALID until phip_plan_finish or phip_plan_abandon_partial). */
 PHIP_API int32_t phip_plan_execute_partial(uint64_t plan, phip_partial *out_partial);
 /* Compacts the (merged) partial table into a result exactly as phip_plan_execute would -- present groups,
  * the server-level trim (trim_size), statistics taken from merged->stats. */
 PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phip_result **out_result);
+/* Gives a pending partial table back without finishing it (the GPUs agreed to merge records instead). While a
+ * partial is pending, phip_plan_execute / phip_plan_execute_partial on the plan return PHIP_ERR_INVALID. */
+PHIP_API int32_t phip_plan_abandon_partial(uint64_t plan);
 
 #endif /* PINOT_HIP_H_ */

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "phip_segment_load", "phip_segment_unload", "phip_segment_device_bytes", "phip_query",
     "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap", "phip_plan_create", "phip_plan_execute",
     "phip_plan_destroy", "phip_global_dictionary", "phip_plan_execute_partial", "phip_plan_finish",
-    "phip_runtime_versions",
+    "phip_runtime_versions", "phip_plan_abandon_partial",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -194,6 +194,8 @@ def load(with_torch: bool = False):
     lib.phip_plan_execute_partial.restype = i32
     lib.phip_plan_finish.argtypes = [u64, ctypes.POINTER(Partial), ctypes.POINTER(ctypes.POINTER(Result))]
     lib.phip_plan_finish.restype = i32
+    lib.phip_plan_abandon_partial.argtypes = [u64]
+    lib.phip_plan_abandon_partial.restype = i32
     built, runtime = ctypes.c_int32(0), ctypes.c_int32(0)
     rv = getattr(lib, "phip_runtime_versions", None)  # (absent from round-2 builds used in A/B runs)
     if rv is not None:

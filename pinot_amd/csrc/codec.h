@@ -6,6 +6,9 @@
 // (java.util.zip.Deflater: RFC 1950 header, RFC 1951 deflate, Adler-32) followed by the uncompressed length
 // (4 bytes, big-endian); GzipDecompressor (:40-52) inflates it with java.util.zip.Inflater. inflate_zlib below
 // restates RFC 1950/1951 (stored, fixed and dynamic Huffman blocks; canonical codes decoded a bit at a time).
+// Its structure -- huff_build's over-subscribed / incomplete / complete return convention, huff_decode's
+// code / first / index walk and the length / distance base + extra-bit tables -- follows Mark Adler's puff.c
+// (zlib contrib/puff, Copyright (C) 2002-2013 Mark Adler, zlib licence), the reference inflater of RFC 1951.
 //
 // ZSTANDARD: ZstandardCompressor / ZstandardDecompressor (…/ZstandardCompressor.java, ZstandardDecompressor.java)
 // call zstd-jni Zstd.compress / Zstd.decompress: one RFC 8878 frame. zstd_decompress below restates the frame

@@ -374,11 +374,17 @@ static void release_lane(Device *dev, Lane *l) {
   dev->lane_cv.notify_one();
 }
 
+// Holds an execution lane for one execution. An execution that returns early (an error after kernels were
+// enqueued) leaves `done` false: the guard then drains the lane's stream before handing it back, so no kernel of
+// that execution can still be reading plan buffers that a later phip_plan_destroy frees.
 struct LaneGuard {
   Device *dev;
   Lane *lane = nullptr;
+  bool done = false;
   ~LaneGuard() {
-    if (lane) release_lane(dev, lane);
+    if (!lane) return;
+    if (!done) (void)hipStreamSynchronize(lane->stream);
+    release_lane(dev, lane);
   }
 };
 
@@ -2469,7 +2475,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         return fail(PHIP_ERR_INVALID, "phip_plan_finish: row %d kind %d (plan: %d)", 1 + a, k, own);
     }
   }
-  if (mode == EXEC_PARTIAL) P.partial_pending = false;
+  if (mode != EXEC_FINISH && P.partial_pending)  // the caller still owns the table (it may be all-reducing it)
+    return fail(PHIP_ERR_INVALID, "plan has a pending partial table: phip_plan_finish or phip_plan_abandon_partial first");
   HIP_TRY(hipSetDevice(dev->ordinal));
   LaneGuard lg{dev};
   {
@@ -2612,6 +2619,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       for (const auto &d : gb_dicts) part->global_keys &= d->global ? 1 : 0;
       P.partial_pending = true;
       P.clean = true;
+      lg.done = true;
       return PHIP_OK;
     }
     void *ov = nullptr, *ol = nullptr, *oh = nullptr;
@@ -2805,6 +2813,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   r.device_ms = t_all;
   P.clean = true;
   P.partial_pending = false;
+  lg.done = true;
   if (out_result) {
     *out_result = &impl.release()->pub;
   }
@@ -3007,6 +3016,15 @@ PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phi
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
   return execute_plan(*p, out_result, nullptr, EXEC_FINISH, nullptr, merged);
+}
+
+PHIP_API int32_t phip_plan_abandon_partial(uint64_t plan) {
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> xl(p->exec_mu);
+  p->partial_pending = false;  // the next execution zeroes and rewrites the table
+  return PHIP_OK;
 }
 
 PHIP_API int32_t phip_global_dictionary(int32_t device, const char *column, int32_t data_type, int32_t cardinality,

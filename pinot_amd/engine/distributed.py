@@ -547,5 +547,7 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
         for i, x in enumerate(stats):
             part.stats[i] = x
         return op.finish(part)
+    if part is not None:  # this rank's table was handed out but the ranks merge records: give it back
+        op.abandon_partial()
     blk = (fallback_op or op).next_block()
     return allreduce_block(blk, dist, group)

@@ -556,6 +556,12 @@ class GpuCombineOperator:
         _lib.check(rc)
         return part
 
+    def abandon_partial(self):
+        """Hands a pending partial table back unfinished (phip_plan_abandon_partial): the ranks agreed to merge
+        records instead, and the next execution of this plan rewrites the table."""
+        if getattr(self, "_plan", None):
+            _lib.check(_lib.load().phip_plan_abandon_partial(self._plan))
+
     def finish(self, merged):
         """Result block of the (merged) partial table: compaction, server-level trim, statistics of `merged`."""
         lib = _lib.load()
@@ -995,18 +1001,51 @@ class GpuCaseAggregationOperator:
         self.inner.close()
 
 
-class GpuInstancePlanMaker:
-    """``pinot.server.query.executor.plan.maker.class`` plug-in."""
+def use_gpu_option(query: QueryContext, default: bool) -> bool:
+    """The ``useGpu`` query option (``SET useGpu = true;`` / queryOptions), parsed as Java's
+    Boolean.parseBoolean (only a case-insensitive "true" is true); absent -> the plan maker's default."""
+    v = query.options.get("useGpu")
+    if v is None:
+        return default
+    return str(v).strip().lower() == "true"
 
-    def __init__(self, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT, device_trim: bool = True):
+
+class GpuInstancePlanMaker:
+    """``pinot.server.query.executor.plan.maker.class`` plug-in (INTEGRATION.md §3 is the Java
+    twin, a subclass of InstancePlanMakerImplV2).
+
+    Routing, as InstancePlanMakerImplV2.makeInstancePlan's override: the query option ``useGpu`` selects the GPU
+    operators; ``useGpu=false`` -- or a query outside the GPU subset (UnsupportedOnGpu) -- goes to
+    ``cpu_plan_maker.make_instance_plan`` (the reference's own CPU plan, ``super.makeInstancePlan``) when one
+    is configured, and raises UnsupportedOnGpu otherwise (this process has no CPU operators of its own).
+    ``default_use_gpu`` is the server-level default for queries that do not set the option: the Java twin
+    keeps the reference's default (CPU) and a GPU server flips it in its config; this host mirror is built
+    for GPU servers and defaults to True."""
+
+    def __init__(self, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT, device_trim: bool = True,
+                 cpu_plan_maker=None, default_use_gpu: bool = True):
         """device_trim=False: return every group (a rank of a multi-GPU server, whose partial groups must
         meet in ``distributed.allreduce_block`` BEFORE the server-level trim, ``reduce.trim_groups``)."""
         self.num_groups_limit = num_groups_limit
         self.device_trim = device_trim
+        self.cpu_plan_maker = cpu_plan_maker
+        self.default_use_gpu = default_use_gpu
 
     def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]):
         if isinstance(query, str):
             query = parse(query)
+        if not use_gpu_option(query, self.default_use_gpu):
+            if self.cpu_plan_maker is None:
+                raise UnsupportedOnGpu("useGpu=false: the query belongs to the CPU plan maker")
+            return self.cpu_plan_maker.make_instance_plan(query, segments)
+        if self.cpu_plan_maker is None:
+            return self._make_gpu_plan(query, segments)
+        try:
+            return self._make_gpu_plan(query, segments)
+        except UnsupportedOnGpu:
+            return self.cpu_plan_maker.make_instance_plan(query, segments)
+
+    def _make_gpu_plan(self, query: QueryContext, segments: Sequence[GpuSegment]):
         from .startree import GpuStarTreeOperator
         st = GpuStarTreeOperator.plan(query, segments, self.num_groups_limit)
         if st is not None:
