@@ -148,9 +148,12 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
   for (int a = 0; a < kMaxAggs; a++) {
     if (a >= q.num_aggs) break;
     cagg_t &ag = q.aggs[a];
+    if (ag.program != seg.program) continue;  // another filter program's function (wave-uniform)
     lds_u64 *slot = tbl + (1 + a) * G + key;
     switch (ag.acc) {
-      case ACC_COUNT: break;  // == row 0
+      case ACC_COUNT:  // == row 0, unless the programs count apart
+        if (q.own_count_rows) __hip_atomic_fetch_add(slot, 1ull, PHIP_RLX, PHIP_WG);
+        break;
       case ACC_SUM_I64: __hip_atomic_fetch_add(slot, (uint64_t)expr_i64(seg, ag, doc), PHIP_RLX, PHIP_WG); break;
       case ACC_SUM_F64:
         __hip_atomic_fetch_add((PHIP_LDS double *)slot, expr_f64(seg, ag, doc), PHIP_RLX, PHIP_WG);

@@ -141,9 +141,12 @@ __device__ __forceinline__ void group_update_global(cquery_t &q, cseg_t &seg, in
   for (int a = 0; a < kMaxAggs; a++) {
     if (a >= q.num_aggs) break;
     cagg_t &ag = q.aggs[a];
+    if (ag.program != seg.program) continue;  // another filter program's function (wave-uniform)
     glb_u64 *p = tbl + (1 + a) * G + slot;
     switch (ag.acc) {
-      case ACC_COUNT: break;
+      case ACC_COUNT:
+        if (q.own_count_rows) __hip_atomic_fetch_add(p, 1ull, PHIP_RLX, PHIP_AG);
+        break;
       case ACC_SUM_I64: __hip_atomic_fetch_add(p, (uint64_t)expr_i64(seg, ag, doc), PHIP_RLX, PHIP_AG); break;
       case ACC_SUM_F64:
         __hip_atomic_fetch_add((PHIP_GLB double *)p, expr_f64(seg, ag, doc), PHIP_RLX, PHIP_AG);
@@ -171,7 +174,11 @@ __device__ __forceinline__ void group_chunk_global(cquery_t &q, cseg_t &seg, int
 __device__ __forceinline__ void group_chunk_hash(cquery_t &q, cseg_t &seg, int32_t doc, bool act) {
   int64_t key = group_key(q, seg, doc);
   if (!act) return;
-  if (q.seg_keys) key = key * q.seg_key_mult + seg.seg_index;  // numGroupsLimit pass (limit.hip)
+  // numGroupsLimit pass (limit.hip): composite key per (segment, key) -- seg_index = program * segments +
+  // segment, so the modulo keeps the segment alone (the programs of a segment share its group generator) -- and
+  // the first-seen position: program (info order) major, doc minor, as FilteredGroupByOperator feeds the shared
+  // DictionaryBasedGroupKeyGenerator info by info (the host bounds programs x docs below 2^32)
+  if (q.seg_keys) key = key * q.seg_key_mult + seg.seg_index % q.seg_key_mult;
   const int64_t slot = hash_slot(q, (uint64_t)key);
   if (slot < 0) {
     __hip_atomic_fetch_or((glb_u32 *)q.hash_overflow, 1u, PHIP_RLX, PHIP_AG);
@@ -179,7 +186,8 @@ __device__ __forceinline__ void group_chunk_hash(cquery_t &q, cseg_t &seg, int32
   }
   if (q.seg_keys) {
     glb_u32 *fd = (glb_u32 *)q.first_doc + slot;
-    if (*fd > (uint32_t)doc) __hip_atomic_fetch_min(fd, (uint32_t)doc, PHIP_RLX, PHIP_AG);
+    const uint32_t pos = (uint32_t)seg.program * (uint32_t)seg.num_docs + (uint32_t)doc;
+    if (*fd > pos) __hip_atomic_fetch_min(fd, pos, PHIP_RLX, PHIP_AG);
   }
   group_update_global(q, seg, doc, slot);
 }
@@ -676,7 +684,7 @@ __global__ __launch_bounds__(256) void group_compact_kernel(const uint64_t *__re
 
 // Gather the aggregates of the compacted groups. table = [1 + naggs][ndense], row 0 = counts.
 __global__ void group_gather_kernel(const int64_t *__restrict__ keys, int64_t ngroups, int64_t ndense,
-                                    int32_t naggs, const int32_t *__restrict__ kinds,
+                                    int32_t naggs, int32_t own_count, const int32_t *__restrict__ kinds,
                                     const uint64_t *__restrict__ table, const uint32_t *__restrict__ hll, int32_t nhll,
                                     int32_t log2m, double *__restrict__ out_values, int64_t *__restrict__ out_longs,
                                     uint8_t *__restrict__ out_hll) {
@@ -688,7 +696,7 @@ __global__ void group_gather_kernel(const int64_t *__restrict__ keys, int64_t ng
       double d = 0.0;
       int64_t l = 0;
       switch (kind) {
-        case ACC_COUNT: l = (int64_t)table[key]; d = (double)l; break;
+        case ACC_COUNT: l = own_count ? (int64_t)v : (int64_t)table[key]; d = (double)l; break;
         case ACC_SUM_I64: l = (int64_t)v; d = (double)l; break;
         case ACC_SUM_F64: d = __longlong_as_double((long long)v); break;
         case ACC_MIN_F64:
@@ -798,12 +806,12 @@ hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t
   group_compact_kernel<<<(unsigned)nchunks, 256, 0, s>>>(counts, n, offsets, keys);
   return hipGetLastError();
 }
-hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs,
+hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs, int32_t own_count,
                                const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
                                int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s) {
   if (ngroups <= 0) return hipSuccess;
-  group_gather_kernel<<<grid_for(ngroups), 256, 0, s>>>(keys, ngroups, ndense, naggs, kinds, table, hll, nhll, log2m,
-                                                       vals, longs, hll_out);
+  group_gather_kernel<<<grid_for(ngroups), 256, 0, s>>>(keys, ngroups, ndense, naggs, own_count, kinds, table, hll, nhll,
+                                                       log2m, vals, longs, hll_out);
   return hipGetLastError();
 }
 

@@ -69,7 +69,12 @@ __device__ __forceinline__ uint64_t f64_ordered(double d) {
   uint64_t u = (uint64_t)__double_as_longlong(d);
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
+// The two table sentinels -- ~0 (a MIN row's initial value) and 0 (a MAX row's) -- are the images of two NaN bit
+// patterns no aggregation produces; a group that no doc of the function's filter program reached keeps them and
+// reads back as the holder defaults +inf / -inf (DoubleGroupByResultHolder, FILTER + GROUP BY).
 __host__ __device__ inline double f64_unordered(uint64_t u) {
+  if (u == ~0ull) return __builtin_huge_val();
+  if (u == 0ull) return -__builtin_huge_val();
   u = (u >> 63) ? (u & 0x7fffffffffffffffull) : ~u;
   union {
     uint64_t u;

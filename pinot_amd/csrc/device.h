@@ -240,7 +240,8 @@ struct DevAggQuery {
   int32_t seg_key_mult;
   uint32_t *first_doc;
   int32_t dense_min;  // GB_NONE + dense_batch: matched docs per 2048-doc tile from which the batched walk is used
-  int32_t pad_dense;
+  int32_t own_count_rows;  // group-by over several filter programs (FILTER + GROUP BY): every COUNT counts its own
+                           // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
 };
 
 // ORDER BY on group-by columns for the device trim (trim.hip)

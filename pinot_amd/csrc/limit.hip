@@ -81,7 +81,8 @@ __global__ void limit_heads_kernel(const uint64_t *__restrict__ k, int64_t n, in
 // it) into the compacted group layout of group_gather_kernel.
 __global__ void limit_reduce_kernel(const uint64_t *__restrict__ k, const int64_t *__restrict__ slot2, int64_t n,
                                     const int32_t *__restrict__ head, const int32_t *__restrict__ run, int64_t cap,
-                                    int32_t naggs, const int32_t *__restrict__ kinds, const uint64_t *__restrict__ table,
+                                    int32_t naggs, int32_t own_count, const int32_t *__restrict__ kinds,
+                                    const uint64_t *__restrict__ table,
                                     const uint32_t *__restrict__ hll, int32_t nhll, int32_t log2m,
                                     int64_t *__restrict__ keys_out, double *__restrict__ out_values,
                                     int64_t *__restrict__ out_longs, uint8_t *__restrict__ out_hll) {
@@ -107,7 +108,7 @@ __global__ void limit_reduce_kernel(const uint64_t *__restrict__ k, const int64_
       double d = 0.0;
       int64_t l = 0;
       switch (kind) {
-        case ACC_COUNT: l = (int64_t)cnt; d = (double)l; break;
+        case ACC_COUNT: l = own_count ? (int64_t)v : (int64_t)cnt; d = (double)l; break;
         case ACC_SUM_I64: l = (int64_t)v; d = (double)l; break;
         case ACC_SUM_F64: d = as_f64(v); break;
         case ACC_MIN_F64:
@@ -176,11 +177,12 @@ hipError_t launch_limit_runs(void *temp, size_t *scan_bytes, const uint64_t *k, 
 }
 
 hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t n, const int32_t *head, const int32_t *run,
-                               int64_t cap, int32_t naggs, const int32_t *kinds, const uint64_t *table,
-                               const uint32_t *hll, int32_t nhll, int32_t log2m, int64_t *keys_out, double *vals,
-                               int64_t *longs, uint8_t *hll_out, hipStream_t s) {
+                               int64_t cap, int32_t naggs, int32_t own_count, const int32_t *kinds,
+                               const uint64_t *table, const uint32_t *hll, int32_t nhll, int32_t log2m,
+                               int64_t *keys_out, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  limit_reduce_kernel<<<lim_grid(n), 256, 0, s>>>(k, slot2, n, head, run, cap, naggs, kinds, table, hll, nhll, log2m,
+  limit_reduce_kernel<<<lim_grid(n), 256, 0, s>>>(k, slot2, n, head, run, cap, naggs, own_count, kinds, table, hll,
+                                                  nhll, log2m,
                                                   keys_out, vals, longs, hll_out);
   return hipGetLastError();
 }

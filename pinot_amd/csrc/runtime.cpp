@@ -66,7 +66,7 @@ hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_
                               int64_t *offsets, hipStream_t s);
 hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *offsets, int64_t nchunks,
                                 int64_t *keys, hipStream_t s);
-hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs,
+hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs, int32_t own_count,
                                const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
                                int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_limit_prepare(const int64_t *slots, int64_t n, const uint64_t *hkeys, const uint32_t *first_doc,
@@ -80,9 +80,9 @@ hipError_t launch_limit_select(const uint64_t *sk_sorted, const int32_t *idx_sor
 hipError_t launch_limit_runs(void *temp, size_t *scan_bytes, const uint64_t *k, int64_t n, int32_t *head, int32_t *run,
                              hipStream_t s);
 hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t n, const int32_t *head, const int32_t *run,
-                               int64_t cap, int32_t naggs, const int32_t *kinds, const uint64_t *table,
-                               const uint32_t *hll, int32_t nhll, int32_t log2m, int64_t *keys_out, double *vals,
-                               int64_t *longs, uint8_t *hll_out, hipStream_t s);
+                               int64_t cap, int32_t naggs, int32_t own_count, const int32_t *kinds,
+                               const uint64_t *table, const uint32_t *hll, int32_t nhll, int32_t log2m,
+                               int64_t *keys_out, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s);
 }  // namespace phip
 
@@ -1052,8 +1052,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   if (q->num_segments > 1 && want_bitmap) return fail(PHIP_ERR_INVALID, "filter bitmap: one segment only");
   const int nprog = std::max(1, q->num_filter_programs);
   if (nprog > kMaxPrograms) return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d filter programs", kMaxPrograms);
-  if (nprog > 1 && (q->num_group_by > 0 || want_bitmap))
-    return fail(PHIP_ERR_UNSUPPORTED, "several filter programs: aggregation-only queries");
+  if (nprog > 1 && want_bitmap) return fail(PHIP_ERR_UNSUPPORTED, "several filter programs: no filter bitmap");
 
   std::vector<Segment *> segs(q->num_segments);
   Device *dev = nullptr;
@@ -1262,7 +1261,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     int c = q->group_by_columns[k];
     if (c < 0 || c >= ncols) return fail(PHIP_ERR_INVALID, "group-by column out of range");
     projected[c] = true;
-    proj_progs[c] |= 1u;
+    proj_progs[c] |= (1u << nprog) - 1;  // every program's docs generate groups (FilteredGroupByOperator infos)
   }
   int num_projected = 0;
   for (bool p : projected) num_projected += p ? 1 : 0;
@@ -1275,6 +1274,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   std::vector<std::vector<int32_t *>> gb_remap_dev;  // [k][seg]
   if (group_by) {
     dq.num_group_by = q->num_group_by;
+    dq.own_count_rows = nprog > 1 ? 1 : 0;
     int64_t stride = 1;
     for (int k = 0; k < q->num_group_by; k++) {
       int c = q->group_by_columns[k];
@@ -1835,18 +1835,20 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // (tools/ab_env.sh, profiles/r02_*): fused wins while the query has at most a few thousand work tiles
     // (Q1.2 / Q1.3 over the sorted layout: 0.112 -> 0.081 / 0.066 -> 0.057 ms p50) and loses beyond
     // (Q1.1 sorted, 44K tiles: 0.207 -> 0.270 ms; unsorted, 293K tiles: 1.6 -> 2.4 ms per step).
-    // Sparse queries fuse whatever their size: with few matched docs per tile the gathers inside the stream are
-    // rare, while a separate aggregation launch walks one mask per tile (estimated matches per work tile from the
-    // program's leaf selectivities: dict-id range widths / set sizes over the cardinality, sorted doc ranges).
+    // Fusing sparse queries whatever their size (estimated matches per work tile from the leaf selectivities) was
+    // measured slower: unsorted Q1.2 / Q1.3 (~1 match per tile, 293K tiles) 0.49 / 0.51 ms split vs 0.55 / 0.74 ms
+    // fused (profiles/r03b_fuse_sparse_ab.log: deferred or per-tile gathers, XCD or contiguous walk alike) -- the
+    // fused kernel's larger register / LDS footprint costs the stream more than the mask walk it saves. The rule
+    // stays as a measurement override (PHIP_FUSE_PER_TILE), off by default.
     const char *fe = getenv("PHIP_FUSE");  // measurement override: "0" never, "1" always, unset = by size
     const int64_t kFuseMaxTiles = 8192;
     double est_docs = 0.0;
     for (size_t i = 0; i < dsegs.size(); i++) est_docs += seg_est[i] * dsegs[i].num_docs;
     const double per_tile = est_docs / (double)std::max<int64_t>(1, total_work);
-    double fuse_per_tile = 16.0;
+    double fuse_per_tile = 0.0;
     if (const char *fp = getenv("PHIP_FUSE_PER_TILE")) fuse_per_tile = atof(fp);  // measurement override
     bool fuse = conj_all && any_filter_prog && !group_by && nprog == 1 && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
-                (fe ? atoi(fe) != 0 : (total_work <= kFuseMaxTiles || per_tile <= fuse_per_tile));
+                (fe ? atoi(fe) != 0 : (total_work <= kFuseMaxTiles || (fuse_per_tile > 0 && per_tile <= fuse_per_tile)));
     bool any_value = false;
     for (int a = 0; a < naggs; a++) any_value |= dq.aggs[a].acc != ACC_COUNT;
     if (fuse && any_value) {
@@ -2318,6 +2320,13 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   for (auto &d : P.gb_dicts) space *= d->card;
   if ((double)space * (double)S >= (double)((int64_t)1 << 62))
     return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: key space x %d segments exceeds 2^62", S);
+  {  // first-seen positions are program * num_docs + doc in 32 bits (aggregate.hip group_chunk_hash)
+    int64_t max_docs = 0;
+    for (int64_t d : P.seg_docs) max_docs = std::max(max_docs, d);
+    if ((int64_t)P.nprog * max_docs > (int64_t)UINT32_MAX)
+      return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: %d filter programs x %lld docs exceed 32-bit positions",
+                  P.nprog, (long long)max_docs);
+  }
   const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(matched, (int64_t)std::min<double>(
                                                                            (double)*ngroups * S, 9e18)));
   int64_t cap = 1024;
@@ -2438,7 +2447,7 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
       (nhll && (rc = ws.get("lim_hll_out", r1 * nhll * m_regs, &h_out))))
     return rc;
   HIP_TRY(launch_limit_reduce((const uint64_t *)k2b, (const int64_t *)s2b, kept, (const int32_t *)head,
-                              (const int32_t *)run, cap, naggs, (const int32_t *)(P.base + P.kinds_off),
+                              (const int32_t *)run, cap, naggs, P.dq.own_count_rows, (const int32_t *)(P.base + P.kinds_off),
                               (const uint64_t *)tab, (const uint32_t *)hll, nhll, P.log2m, (int64_t *)k_out,
                               (double *)v_out, (int64_t *)l_out, (uint8_t *)h_out, st));
   *keys = k_out;
@@ -2639,7 +2648,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         if (rc) return rc;
       }
       HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
-      HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, gather_kinds, (const uint64_t *)gtab,
+      HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, dq.own_count_rows, gather_kinds,
+                                  (const uint64_t *)gtab,
                                   (const uint32_t *)ghll, nhll, log2m, (double *)ov, (int64_t *)ol, (uint8_t *)oh, st));
       if (dq.mode == GB_HASH) HIP_TRY(launch_hash_keys((int64_t *)keys, ngroups, dq.gb_keys, st));
     }

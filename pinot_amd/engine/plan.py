@@ -413,7 +413,7 @@ class GpuCombineOperator:
         PHIP_ORDER_* terms; an ORDER BY outside that (HLL, post-aggregation expressions) returns every group
         (the broker's ORDER BY + LIMIT gives the same final rows)."""
         from .reduce import _agg_index
-        q = self.query
+        q = getattr(self, "trim_query", None) or self.query
         none = (-1, 0, 0, [], [])
         if not q.group_by or not q.order_by or not getattr(self, "device_trim", True):
             return none
@@ -434,7 +434,7 @@ class GpuCombineOperator:
                 terms.append((_lib.ORDER_GROUP_KEY, gb.index(str(ob.expression)), 0, desc))
                 continue
             i = _agg_index(q, ob.expression)
-            if i is None or q.aggregations[i].filter is not None:
+            if i is None or (q.aggregations[i].filter is not None and self.num_programs == 1):
                 return none
             f, sl = self.mapping[i]
             if f in ("sum", "min", "max", "count"):
@@ -770,22 +770,33 @@ class GpuFilteredGroupByOperator:
     """FilteredGroupByOperator (pinot-core/.../operator/query/FilteredGroupByOperator.java:110-176) over all
     segments. The infos of AggregationFunctionUtils.buildFilteredAggregationInfos (:312-400) -- one per distinct
     FILTER (main AND filter), then the main filter with the non-filtered functions, which a group-by always gets
-    so every group of the main filter exists (unless ``filteredAggregationsSkipEmptyGroups``) -- each run as one
-    GPU group-by over all segments (no device trim: the trim belongs after the merge). The reference shares one
-    group key generator across the infos; here the per-info group tables are merged by key, functions whose
-    filter never reached a group keep their holder default, and the server-level trim
-    (GroupByUtils / IndexedTable) runs on the merged block. numDocsScanned / post-filter entries are summed over
-    the infos (each projects the group-by columns + its functions' arguments).
+    so every group of the main filter exists (unless ``filteredAggregationsSkipEmptyGroups``) -- become the
+    filter programs of ONE GPU plan: one filter launch writes a tile mask per info, one aggregation launch keys
+    every info's docs into one shared dense key space (the shared DictionaryBasedGroupKeyGenerator) and applies
+    each function to its own info's docs only (phip_aggregation.program; COUNTs count their info's docs in their
+    own table row). A group's presence is the union over the infos; a function whose filter never reached a group
+    keeps its holder default (0 / +inf / -inf / empty registers, read back from the untouched table rows).
+    numDocsScanned / post-filter entries sum over the infos (each projects the group-by columns plus its
+    functions' arguments). The server-level trim runs on the device over the complete groups.
 
-    numGroupsLimit: the reference's shared generator numbers groups first-seen over info 0's docs, then
-    info 1's, ... in its HashMap order of the filters, so which groups survive a reached limit is not defined
-    by the query; when any info reaches the limit the operator raises UnsupportedOnGpu (PHIP_ERR_UNSUPPORTED:
-    the Java plan maker keeps its own CPU operator)."""
+    numGroupsLimit: the shared generator numbers groups first-seen over info 0's docs, then info 1's, ... per
+    segment; the device limit pass orders (segment, key) entries by (info, doc) exactly so. The info order is
+    the reference's for one filtered info (filtered infos first, the main info last); with several filtered
+    infos the reference iterates a HashMap of FilterContexts, whose order this restatement takes as
+    first-appearance in the query (the oracle does the same).
 
-    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
+    More than 8 infos or more than 8 primitive slots run one GPU group-by per info, merged by key on the host
+    (the round-2 path); that path raises UnsupportedOnGpu when an info reaches numGroupsLimit."""
+
+    _MAX_PROGRAMS = 8  # device.h kMaxPrograms
+    _MAX_SLOTS = 8     # device.h kMaxAggs
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int,
+                 device_trim: bool = True):
         self.query = query
         self.segments = list(segments)
         self.num_groups_limit = num_groups_limit
+        self.device_trim = device_trim
         main, infos = [], {}
         for i, ag in enumerate(query.aggregations):
             if ag.filter is None:
@@ -796,14 +807,33 @@ class GpuFilteredGroupByOperator:
         skip = str(query.options.get("filteredAggregationsSkipEmptyGroups", "false")).lower() == "true"
         if main or not skip:
             order.append((None, main))
-        self.parts = []
-        for flt, idxs in order:
+        filters = []
+        for flt, _ in order:
             if flt is None:
-                f = query.filter
+                filters.append(query.filter)
             elif query.filter is None:
-                f = flt
+                filters.append(flt)
             else:
-                f = FilterContext.AND(query.filter, flt)
+                filters.append(FilterContext.AND(query.filter, flt))
+        self.one_pass = None
+        self.parts = []
+        if len(order) <= self._MAX_PROGRAMS:
+            prog_of = {}
+            for p, (_, idxs) in enumerate(order):
+                for i in idxs:
+                    prog_of[i] = p
+            sub = QueryContext(query.table, [], [ag.unfiltered() for ag in query.aggregations], None,
+                               list(query.group_by), list(query.order_by), limit=query.limit,
+                               options=dict(query.options))
+            op = GpuCombineOperator(sub, self.segments, num_groups_limit,
+                                    programs=(filters, [prog_of[i] for i in range(len(query.aggregations))]))
+            if len(op.prims) <= self._MAX_SLOTS:
+                op.device_trim = device_trim
+                op.trim_query = query  # ORDER BY resolves against the FILTER'ed functions
+                self.one_pass = op
+                return
+            op.close()
+        for (flt, idxs), f in zip(order, filters):
             # an info without functions still generates its groups: a COUNT rides along and is dropped
             aggs = [query.aggregations[i].unfiltered() for i in idxs] or [AggregationInfo("count", None)]
             sub = QueryContext(query.table, [], aggs, f, list(query.group_by), limit=query.limit,
@@ -812,7 +842,17 @@ class GpuFilteredGroupByOperator:
             op.device_trim = False
             self.parts.append((idxs, op))
 
+    def _wrap(self, blk):
+        out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), blk.groups, blk.stats,
+                                  blk.num_groups_limit_reached)
+        out.num_groups_trimmed = getattr(blk, "num_groups_trimmed", False)
+        for k in GpuFilteredAggregationOperator._TIMES + ("fused",):
+            setattr(out, k, getattr(blk, k, 0))
+        return out
+
     def next_block(self):
+        if self.one_pass is not None:
+            return self._wrap(self.one_pass.next_block())
         from .reduce import trim_groups
         na = len(self.query.aggregations)
         stats = ExecutionStatistics()
@@ -821,8 +861,7 @@ class GpuFilteredGroupByOperator:
         device_ms = 0.0
         for (idxs, op), blk in zip(self.parts, _run_parts(self.parts)):
             if blk.num_groups_limit_reached:
-                raise UnsupportedOnGpu("numGroupsLimit reached by a FILTER + GROUP BY query (group numbering follows "
-                                       "the reference's filter HashMap order)")
+                raise UnsupportedOnGpu("numGroupsLimit reached by a FILTER + GROUP BY query of more than 8 infos")
             per_part.append((idxs, blk.groups))
             for k in blk.groups:
                 keys.setdefault(k, None)
@@ -845,11 +884,25 @@ class GpuFilteredGroupByOperator:
                     vals[i] = v[j] if v is not None else (dflt.copy() if isinstance(dflt, np.ndarray) else dflt)
         blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats, False)
         blk.num_groups_trimmed = False
-        blk = trim_groups(self.query, blk)
+        if self.device_trim:
+            blk = trim_groups(self.query, blk)
         blk.device_ms = device_ms
         return blk
 
+    # -- multi-GPU servers: the one-pass plan hands out its dense partial table like any group-by
+    def execute_partial(self):
+        return self.one_pass.execute_partial() if self.one_pass is not None else None
+
+    def abandon_partial(self):
+        if self.one_pass is not None:
+            self.one_pass.abandon_partial()
+
+    def finish(self, merged):
+        return self._wrap(self.one_pass.finish(merged))
+
     def close(self):
+        if self.one_pass is not None:
+            self.one_pass.close()
         for _, op in self.parts:
             op.close()
 
@@ -1055,7 +1108,7 @@ class GpuInstancePlanMaker:
             return GpuCaseAggregationOperator(query, segments, self.num_groups_limit)
         if any(ag.filter is not None for ag in query.aggregations):
             if query.group_by:
-                return GpuFilteredGroupByOperator(query, segments, self.num_groups_limit)
+                return GpuFilteredGroupByOperator(query, segments, self.num_groups_limit, self.device_trim)
             return GpuFilteredAggregationOperator(query, segments, self.num_groups_limit)
         op = GpuCombineOperator(query, segments, self.num_groups_limit)
         op.device_trim = self.device_trim

@@ -14,9 +14,11 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def gpu_lib():
-    """The product library on a GPU box; fails loudly (no CPU fallback) when it cannot load."""
+    """The product library on a GPU box; fails loudly (no CPU fallback) when it cannot load. Loaded after torch
+    (one HIP runtime per process, _lib.load): the distributed tests drive RCCL on the library's buffers, and the
+    test order must not decide which runtime the library binds to."""
     from pinot_amd import _lib
-    lib = _lib.load()
+    lib = _lib.load(with_torch=True)
     import ctypes
     n = ctypes.c_int32(0)
     lib.phip_device_count(ctypes.byref(n))

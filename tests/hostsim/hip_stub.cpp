@@ -120,7 +120,7 @@ hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *cc, in
 hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *, int64_t, int64_t *keys, hipStream_t) {
   int64_t o = 0; for (int64_t i = 0; i < n; i++) if (counts[i]) keys[o++] = i; return hipSuccess;
 }
-hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t naggs, const int32_t *, const uint64_t *,
+hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t naggs, int32_t, const int32_t *, const uint64_t *,
                                const uint32_t *, int32_t nhll, int32_t log2m, double *v, int64_t *l, uint8_t *h, hipStream_t) {
   memset(v, 0, ng * naggs * 8); memset(l, 0, ng * naggs * 8); if (nhll) memset(h, 0, ng * nhll * (1 << log2m)); return hipSuccess;
 }
@@ -140,6 +140,6 @@ hipError_t launch_limit_runs(void *, size_t *scan_bytes, const uint64_t *, int64
   *scan_bytes = 256; return hipSuccess;
 }
 hipError_t launch_limit_reduce(const uint64_t *, const int64_t *, int64_t, const int32_t *, const int32_t *, int64_t,
-                               int32_t, const int32_t *, const uint64_t *, const uint32_t *, int32_t, int32_t, int64_t *,
+                               int32_t, int32_t, const int32_t *, const uint64_t *, const uint32_t *, int32_t, int32_t, int64_t *,
                                double *, int64_t *, uint8_t *, hipStream_t) { return hipSuccess; }
 }  // namespace phip

@@ -55,17 +55,22 @@ from pinot_amd.engine.plan import GpuCombineOperator  # noqa: E402
 from pinot_amd.query.context import FilterContext  # noqa: E402
 base = parse("SELECT COUNT(*), SUM(m) FROM t")
 flt = parse("SELECT COUNT(*) FROM t WHERE h = 1").filter
-for progs, aprog, gb in (([flt] * 9, [0, 8], False), ([flt, None], [0, 2], False), ([flt, None], [0, 1], True)):
-    q = parse("SELECT h, COUNT(*), SUM(m) FROM t GROUP BY h") if gb else base
-    op = GpuCombineOperator(q, gs, 100_000, programs=(progs, aprog))
+for progs, aprog in (([flt] * 9, [0, 8]), ([flt, None], [0, 2])):
+    op = GpuCombineOperator(base, gs, 100_000, programs=(progs, aprog))
     try:
         op.next_block()
-        raise SystemExit(f"descriptor accepted: {len(progs)} programs, {aprog}, group-by {gb}")
+        raise SystemExit(f"descriptor accepted: {len(progs)} programs, {aprog}")
     except _lib.PhipError:
         pass
     op.close()
+# FILTER + GROUP BY: the infos as programs of one group-by plan (own COUNT rows), with and without device trim
+fgb = ("SELECT g, COUNT(*) FILTER(WHERE h = 1), SUM(m) FILTER(WHERE d < 0.5) s, MAX(d) FROM t WHERE h <> 3 "
+       "GROUP BY g ORDER BY s DESC LIMIT 3")
+pm.make_instance_plan(parse(fgb), gs).next_block()
+GpuInstancePlanMaker(device_trim=False).make_instance_plan(parse(fgb), gs).next_block()
 os.environ["PHIP_GB_HASH"] = "1"  # the hash-table group-by's host path (allocation, key decode)
 pm.make_instance_plan(parse("SELECT g, h, COUNT(*), SUM(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY g, h"), gs).next_block()
+pm.make_instance_plan(parse(fgb), gs).next_block()
 del os.environ["PHIP_GB_HASH"]
 for g in gs:
     g.destroy()

@@ -18,6 +18,9 @@ QUERIES = [
     "SELECT g, SUM(big), COUNT(*) FROM t GROUP BY g ORDER BY g LIMIT 100000",  # int64 on one rank, double on the other
     "SELECT h, MINMAXRANGE(d), SUM(m * h) FROM t WHERE h < 4 GROUP BY h ORDER BY h LIMIT 100000",
     "SELECT g, h, SUM(m) FROM t GROUP BY g, h ORDER BY SUM(m) DESC LIMIT 3",  # trim after the merge
+    # FILTER + GROUP BY: the infos are programs of one plan, its partial table merges like any other
+    "SELECT g, COUNT(*) FILTER(WHERE h = 1), SUM(m) FILTER(WHERE d > 0), MAX(d), COUNT(*) FROM t "
+    "GROUP BY g ORDER BY g LIMIT 100000",
 ]
 
 
@@ -81,6 +84,12 @@ def _worker(rank, world, port, q, limit, errs):
         fb = GpuInstancePlanMaker(num_groups_limit=limit, device_trim=False).make_instance_plan(qc, mine)
         part = op.execute_partial()
         assert (part is None) == (limit < 1000), "dense partial expected unless numGroupsLimit is hit"
+        if part is not None:
+            # the table is the caller's until finish / abandon: another execution of the plan is refused
+            from pinot_amd._lib import PhipError
+            with pytest.raises(PhipError):
+                op.execute_partial()
+            op.abandon_partial()
         merged = trim_groups(qc, distributed_block(op, dist, fallback_op=fb))
         whole = trim_groups(qc, executor.execute(qc, raws, num_groups_limit=limit)[0])
         if "DESC LIMIT 3" in q:

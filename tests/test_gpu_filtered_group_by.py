@@ -84,3 +84,48 @@ def test_gpu_filter_query_equals_twin(pair, ft):
 @pytest.mark.parametrize("sql", [q for p in FT_PAIRS for q in p] + EXTRA)
 def test_gpu_filtered_group_by_vs_oracle(sql, ft):
     _check_vs_oracle(sql, ft)
+
+
+# ---- one pass: the infos are filter programs of ONE group-by plan --------------------------------------------
+LIMIT_QUERIES = [
+    # one filtered info + the main info: the reference's info order (filtered first, main last) is defined
+    "SELECT STRING_COL, SUM(INT_COL) FILTER(WHERE BOOLEAN_COL = 1), COUNT(*), MAX(NO_INDEX_COL) FROM MyTable "
+    "GROUP BY STRING_COL",
+    # two filtered infos, COUNTs under different filters, HLL, groups over two columns
+    "SELECT STRING_COL, STATIC_INT_COL, COUNT(*) FILTER(WHERE INT_COL > 20000), COUNT(*) FILTER(WHERE NO_INDEX_COL "
+    "< 500), DISTINCTCOUNTHLL(INT_COL) FILTER(WHERE INT_COL > 20000), MIN(INT_COL) FROM MyTable "
+    "WHERE NO_INDEX_COL > 10 GROUP BY STRING_COL, STATIC_INT_COL",
+]
+
+
+@pytest.mark.parametrize("mode", ["dense", "hash"])
+@pytest.mark.parametrize("limit", [100_000, 37, 1])
+@pytest.mark.parametrize("sql", LIMIT_QUERIES, ids=["one-filter", "two-filters"])
+def test_gpu_filtered_group_by_one_pass_limit(sql, limit, mode, ft, monkeypatch):
+    """numGroupsLimit over the shared generator: per segment, groups first-seen over info 0's docs, then info 1's,
+    ...; later keys are dropped for every info (FilteredGroupByOperator.java:110-176 with one
+    DictionaryBasedGroupKeyGenerator). The GPU's limit pass orders (segment, key) entries by (info, doc)."""
+    if mode == "hash":
+        monkeypatch.setenv("PHIP_GB_HASH", "1")
+    qc = parse(sql)
+    op = GpuInstancePlanMaker(num_groups_limit=limit).make_instance_plan(qc, ft)
+    assert op.one_pass is not None and op.one_pass.num_programs >= 2
+    blk = op.next_block()
+    op.close()
+    oblk, exact = executor.execute(qc, [s.segment for s in ft], num_groups_limit=limit)
+    assert blk.num_groups_limit_reached == oblk.num_groups_limit_reached
+    assert blk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+    assert blk.stats.num_entries_scanned_post_filter == oblk.stats.num_entries_scanned_post_filter
+    assert set(blk.groups) == set(oblk.groups), (len(blk.groups), len(oblk.groups))
+    for k, v in blk.groups.items():
+        _assert_intermediates_equal(qc.aggregations, v, oblk.groups[k], exact[k])
+
+
+def test_gpu_filtered_group_by_skip_empty_groups_one_pass(ft):
+    """filteredAggregationsSkipEmptyGroups: no main info, so the groups are the union of the filtered infos'."""
+    sql = ("SET filteredAggregationsSkipEmptyGroups = true; SELECT STRING_COL, SUM(INT_COL) FILTER(WHERE INT_COL > "
+           "25000), COUNT(*) FILTER(WHERE BOOLEAN_COL = 1 AND INT_COL < 3000) FROM MyTable GROUP BY STRING_COL LIMIT 100000")
+    op = GpuInstancePlanMaker().make_instance_plan(parse(sql), ft)
+    assert op.one_pass is not None and op.one_pass.num_programs == 2
+    op.close()
+    _check_vs_oracle(sql, ft)
