@@ -191,7 +191,24 @@ typedef struct phip_query_desc {
    * (no group-by), at most 8 programs. 0 or 1 = one program. */
   int32_t num_filter_programs;
   const struct phip_order_term *order_terms;
+  /* Selection (row-returning) queries, the leaf of a multi-stage join (SelectionOnlyOperator,
+   * pinot-core/.../operator/query/SelectionOnlyOperator.java:40-170, and SelectionOnlyCombineOperator): when
+   * num_select > 0 (no aggregations, no group-by, one filter program) each segment keeps its first select_limit
+   * matched docs in doc order, the segments' rows are concatenated in query order up to select_limit rows, and
+   * every row holds the select expressions (phip_result.select_*). Statistics: numDocsScanned = the rows each
+   * segment kept, numEntriesScannedPostFilter = that x the distinct columns the expressions read. */
+  int32_t num_select;
+  int32_t reserved1;
+  const struct phip_select_expr *select;
+  int64_t select_limit;
 } phip_query_desc;
+
+typedef struct phip_select_expr {
+  int32_t expr;     /* PHIP_EXPR_*: a column, or a op b (evaluated in double, as the transform functions do) */
+  int32_t column_a; /* index into phip_query_desc.columns */
+  int32_t column_b;
+  int32_t reserved;
+} phip_select_expr;
 
 #define PHIP_ORDER_GROUP_KEY 0 /* group-by column `a` (GroupByExpressionExtractor) */
 #define PHIP_ORDER_VALUE 1     /* aggregations[a] as double: SUM / MIN / MAX / COUNT (AggregationFunctionExtractor) */
@@ -246,6 +263,15 @@ typedef struct phip_result {
   double agg_kernel_ms;
   int64_t filter_bytes;
   int64_t agg_bytes;
+  /* Selection queries (phip_query_desc.num_select > 0): num_rows rows of num_select columns, column-major 8-byte
+   * slots select_values[k * num_rows + r]; select_types[k] says how to read column k: PHIP_TYPE_INT / LONG = int64,
+   * PHIP_TYPE_FLOAT / DOUBLE = double bits (FLOAT values are exact floats; expressions are DOUBLE), PHIP_TYPE_STRING
+   * = id in a query-global dictionary (phip_result_select_dictionary). */
+  int64_t num_rows;
+  int32_t num_select;
+  int32_t reserved_select;
+  const int32_t *select_types;
+  const uint64_t *select_values;
 } phip_result;
 
 typedef struct phip_dictionary_view {
@@ -285,6 +311,10 @@ PHIP_API int32_t phip_plan_destroy(uint64_t plan);
 PHIP_API int32_t phip_result_dictionary(const phip_result *result, int32_t group_by_index,
                                         phip_dictionary_view *out_view);
 PHIP_API void phip_result_free(phip_result *result);
+
+/* Values of select column k of a selection result that holds STRING dictionary ids. */
+PHIP_API int32_t phip_result_select_dictionary(const phip_result *result, int32_t select_index,
+                                               phip_dictionary_view *out_view);
 
 /* Filter only, one segment: words_out receives ceil(num_docs/64) bitmap words. */
 PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *words_out, int64_t num_words);

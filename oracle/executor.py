@@ -465,6 +465,8 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
     from pinot_amd.engine.results import (AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock,
                                           merge_intermediate)
     from pinot_amd.query.context import columns_of
+    if query.is_selection:
+        return _execute_selection(query, segments), None
     stats = ExecutionStatistics()
     projected = set()
     for ag in query.aggregations:
@@ -515,7 +517,59 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
             else:
                 groups[k] = vals
                 exact_groups[k] = exs
-    return GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats, limit_reached), exact_groups
+    blk = GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats, limit_reached)
+    blk.key_types = [_STORED[int(segments[0].columns[e.name].metadata.data_type)] for e in query.group_by] \
+        if segments else None
+    return blk, exact_groups
+
+
+_STORED = {0: "INT", 1: "LONG", 2: "FLOAT", 3: "DOUBLE", 4: "STRING"}
+
+
+def _execute_selection(query, segments):
+    """SelectionOnlyOperator.getNextBlock (pinot-core/.../operator/query/SelectionOnlyOperator.java:130-170): per
+    segment the first LIMIT matched docs in doc order (numDocsScanned = the docs added, numEntriesScannedPostFilter =
+    that x the projected columns, :164-170), each row the select expressions (SelectionOperatorUtils
+    .extractExpressions, SELECT * = the columns sorted by name); SelectionOnlyCombineOperator concatenates the
+    segments' rows until LIMIT rows are held (segment order here). LIMIT 0 = EmptySelectionOperator (schema only)."""
+    from pinot_amd.engine.results import ExecutionStatistics, SelectionResultsBlock
+    from pinot_amd.query.context import Function, Identifier, columns_of
+    exprs = query.select_expressions(list(segments[0].columns) if segments else [])
+    names = [str(e) for e in exprs]
+    types = []
+    for e in exprs:
+        types.append(_STORED[int(segments[0].columns[e.name].metadata.data_type)] if isinstance(e, Identifier)
+                     else "DOUBLE")
+    projected = set()
+    for e in exprs:
+        projected.update(columns_of(e))
+    stats = ExecutionStatistics()
+    cols = [[] for _ in exprs]
+    nrows = 0
+    limit = int(query.limit)
+    for seg in segments:
+        stats.num_total_docs += seg.num_docs
+        stats.num_segments_processed += 1
+        if limit <= 0:
+            continue
+        os_ = OracleSegment(seg)
+        docs = np.nonzero(eval_filter(os_, query.filter))[0][:limit]
+        stats.num_docs_scanned += len(docs)
+        stats.num_entries_scanned_post_filter += len(docs) * len(projected)
+        stats.num_segments_matched += int(len(docs) > 0)
+        take = docs[:max(0, limit - nrows)]  # the combine keeps LIMIT rows in total
+        nrows += len(take)
+        for j, (e, t) in enumerate(zip(exprs, types)):
+            v = _expr_values(os_, e, take)
+            if t in ("INT", "LONG"):
+                cols[j].extend(int(x) for x in v)
+            elif t == "STRING":
+                cols[j].extend(str(x) for x in v)
+            elif t == "FLOAT":
+                cols[j].extend(float(np.float32(x)) for x in v)
+            else:
+                cols[j].extend(float(x) for x in np.asarray(v, dtype=np.float64))
+    return SelectionResultsBlock(names, types, cols, stats)
 
 
 def _execute_filtered(query, segments):
@@ -659,7 +713,10 @@ def _execute_filtered_group_by(query, segments, num_groups_limit):
             else:
                 groups[k] = vals
                 exact_groups[k] = exs
-    return GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats, limit_reached), exact_groups
+    blk = GroupByResultsBlock(query.aggregations, list(query.group_by), groups, stats, limit_reached)
+    blk.key_types = [_STORED[int(segments[0].columns[e.name].metadata.data_type)] for e in query.group_by] \
+        if segments else None
+    return blk, exact_groups
 
 
 def filter_mask(query, segment):

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "phip_segment_load", "phip_segment_unload", "phip_segment_device_bytes", "phip_query",
     "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap", "phip_plan_create", "phip_plan_execute",
     "phip_plan_destroy", "phip_global_dictionary", "phip_plan_execute_partial", "phip_plan_finish",
-    "phip_runtime_versions", "phip_plan_abandon_partial",
+    "phip_runtime_versions", "phip_plan_abandon_partial", "phip_result_select_dictionary",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -76,6 +76,11 @@ class OrderTerm(ctypes.Structure):
 ORDER_GROUP_KEY, ORDER_VALUE, ORDER_AVG, ORDER_RANGE = 0, 1, 2, 3
 
 
+class SelectExpr(ctypes.Structure):
+    _fields_ = [("expr", ctypes.c_int32), ("column_a", ctypes.c_int32), ("column_b", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
 class QueryDesc(ctypes.Structure):
     _fields_ = [("num_columns", ctypes.c_int32), ("num_segments", ctypes.c_int32),
                 ("columns", ctypes.POINTER(ctypes.c_char_p)), ("segments", ctypes.POINTER(ctypes.c_uint64)),
@@ -87,7 +92,9 @@ class QueryDesc(ctypes.Structure):
                 ("trim_size", ctypes.c_int64), ("num_order_by_keys", ctypes.c_int32), ("reserved0", ctypes.c_int32),
                 ("order_by_keys", ctypes.POINTER(ctypes.c_int32)),
                 ("num_order_terms", ctypes.c_int32), ("num_filter_programs", ctypes.c_int32),
-                ("order_terms", ctypes.POINTER(OrderTerm))]
+                ("order_terms", ctypes.POINTER(OrderTerm)),
+                ("num_select", ctypes.c_int32), ("reserved1", ctypes.c_int32),
+                ("select", ctypes.POINTER(SelectExpr)), ("select_limit", ctypes.c_int64)]
 
 
 class Result(ctypes.Structure):
@@ -102,7 +109,9 @@ class Result(ctypes.Structure):
                 ("num_groups_trimmed", ctypes.c_int32), ("fused", ctypes.c_int32),
                 ("long_exact", ctypes.POINTER(ctypes.c_int32)),
                 ("filter_kernel_ms", ctypes.c_double), ("agg_kernel_ms", ctypes.c_double),
-                ("filter_bytes", ctypes.c_int64), ("agg_bytes", ctypes.c_int64)]
+                ("filter_bytes", ctypes.c_int64), ("agg_bytes", ctypes.c_int64),
+                ("num_rows", ctypes.c_int64), ("num_select", ctypes.c_int32), ("reserved_select", ctypes.c_int32),
+                ("select_types", ctypes.POINTER(ctypes.c_int32)), ("select_values", ctypes.POINTER(ctypes.c_uint64))]
 
 
 class DictionaryView(ctypes.Structure):
@@ -178,6 +187,8 @@ def load(with_torch: bool = False):
     lib.phip_query.restype = i32
     lib.phip_result_dictionary.argtypes = [ctypes.POINTER(Result), i32, ctypes.POINTER(DictionaryView)]
     lib.phip_result_dictionary.restype = i32
+    lib.phip_result_select_dictionary.argtypes = [ctypes.POINTER(Result), i32, ctypes.POINTER(DictionaryView)]
+    lib.phip_result_select_dictionary.restype = i32
     lib.phip_result_free.argtypes = [ctypes.POINTER(Result)]
     lib.phip_result_free.restype = None
     lib.phip_filter_bitmap.argtypes = [ctypes.POINTER(QueryDesc), ctypes.POINTER(u64), i64]

@@ -244,6 +244,33 @@ struct DevAggQuery {
                            // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
 };
 
+// Selection (row-returning) queries (select.hip): SelectionOnlyOperator per segment + the combine's concatenation.
+constexpr int kMaxSelect = 16;  // select expressions per query
+enum SelKind : int32_t {
+  SEL_I64 = 0,  // INT / LONG column: the value as int64
+  SEL_F64 = 1,  // FLOAT / DOUBLE column, or an arithmetic expression (evaluated in double, as the transform
+                // functions do): the value as double bits
+  SEL_ID = 2,   // STRING column: the id in the query-global dictionary (DevCol.remap)
+};
+struct DevSelect {
+  int32_t expr;  // PHIP_EXPR_*
+  int32_t col_a;
+  int32_t col_b;
+  int32_t kind;  // SelKind
+};
+struct DevSelQuery {
+  const DevSeg *segs;
+  int32_t num_segs;
+  int32_t total_work;
+  const uint32_t *mask;      // [total_work][64] lane-major tile masks of the filter kernel; null = every doc
+  const int64_t *tile_off;   // [total_work + 1] exclusive prefix of matched docs per work tile
+  const int64_t *seg_base;   // [num_segs + 1] first output row of each entry (its kept rows follow in doc order)
+  int64_t limit;             // rows kept per segment (SelectionOnlyOperator._numRowsToKeep) and in total
+  int32_t num_select;
+  int32_t pad;
+  DevSelect sel[kMaxSelect];
+};
+
 // ORDER BY on group-by columns for the device trim (trim.hip)
 constexpr int kMaxOrderKeys = 8;
 struct KeyOrder {

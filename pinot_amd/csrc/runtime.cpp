@@ -69,6 +69,11 @@ hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t
 hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs, int32_t own_count,
                                const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
                                int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
+hipError_t launch_select_count(const DevSelQuery *q, int64_t total_work, int64_t *tile_cnt, hipStream_t s);
+hipError_t launch_select_scan(void *temp, size_t *temp_bytes, const int64_t *in, int64_t *out, int64_t n, hipStream_t s);
+hipError_t launch_select_bases(const DevSelQuery *q, int64_t *seg_base, int64_t *kept, int64_t *total, hipStream_t s);
+hipError_t launch_select_gather(const DevSelQuery *q, int64_t total_work, uint64_t *out, int64_t num_rows,
+                                hipStream_t s);
 hipError_t launch_limit_prepare(const int64_t *slots, int64_t n, const uint64_t *hkeys, const uint32_t *first_doc,
                                 int32_t nseg, uint64_t *sortkey, int32_t *idx, hipStream_t s);
 hipError_t launch_limit_bounds(const uint64_t *sk_sorted, int64_t n, int64_t *first, int64_t *last, hipStream_t s);
@@ -700,6 +705,9 @@ struct ResultImpl {
   std::vector<int32_t> keys;
   std::vector<int32_t> exact;
   std::vector<std::shared_ptr<Device::Remap>> dicts;
+  std::vector<uint64_t> sel_values;  // selection: [num_select][num_rows]
+  std::vector<int32_t> sel_types;
+  std::vector<std::shared_ptr<Device::Remap>> sel_dicts;  // per select column: query-global dictionary (STRING)
 };
 
 // validate a preorder subtree; returns index after it or -1
@@ -1039,6 +1047,16 @@ struct Plan {
   // one segment, hash table, key space >= numGroupsLimit: the normal pass records every slot's first matched doc
   // (aggregate.hip seg_keys with one segment: the key is unchanged), so the limit pass starts from its table
   uint32_t *first_doc = nullptr;
+  // selection queries (select.hip): descriptor in the blob, per-execution scratch (tile ranks, entry bases)
+  bool select = false;
+  int nsel = 0;
+  size_t sq_off = 0;
+  int64_t *sel_tile_cnt = nullptr, *sel_tile_off = nullptr, *sel_base = nullptr, *sel_kept = nullptr,
+          *sel_total = nullptr;
+  std::vector<int32_t> sel_types;
+  std::vector<std::shared_ptr<Device::Remap>> sel_dicts;
+  std::vector<int32_t> sel_bits, sel_width;  // per select column's projected bytes (algorithmic bytes)
+  float sel_filter_ms = 0.f;
   bool total_events = true;  // record ev[0] / ev[3] (phip_result.device_ms); PHIP_TOTAL_EVENTS=0 skips them (A/B)
 };
 
@@ -1263,6 +1281,57 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     projected[c] = true;
     proj_progs[c] |= (1u << nprog) - 1;  // every program's docs generate groups (FilteredGroupByOperator infos)
   }
+  // selection (SelectionOnlyOperator): expressions, output kinds, query-global dictionaries of STRING columns
+  const int nsel = q->num_select;
+  if (nsel < 0 || nsel > kMaxSelect) return fail(PHIP_ERR_UNSUPPORTED, "selection: at most %d expressions", kMaxSelect);
+  if (nsel > 0 && (naggs > 0 || q->num_group_by > 0 || nprog > 1 || want_bitmap || !q->select))
+    return fail(PHIP_ERR_INVALID, "selection: no aggregations, group-by or filter programs beside the expressions");
+  DevSelQuery sq;
+  memset(&sq, 0, sizeof(sq));
+  std::vector<int32_t> sel_types(nsel, 0);
+  std::vector<std::shared_ptr<Device::Remap>> sel_dicts(nsel), col_remap(ncols);
+  for (int k = 0; k < nsel; k++) {
+    const phip_select_expr &e = q->select[k];
+    if (e.expr < PHIP_EXPR_COLUMN || e.expr > PHIP_EXPR_MUL || e.column_a < 0 || e.column_a >= ncols ||
+        (e.expr != PHIP_EXPR_COLUMN && (e.column_b < 0 || e.column_b >= ncols)))
+      return fail(PHIP_ERR_INVALID, "select expression %d malformed", k);
+    DevSelect &d = sq.sel[k];
+    d.expr = e.expr;
+    d.col_a = e.column_a;
+    d.col_b = e.expr != PHIP_EXPR_COLUMN ? e.column_b : e.column_a;
+    for (int c : {e.column_a, e.expr != PHIP_EXPR_COLUMN ? e.column_b : -1}) {
+      if (c < 0) continue;
+      projected[c] = true;
+      const int t0 = segs[0]->cols[colidx[0][c]].type;
+      for (int s = 0; s < nseg; s++) {
+        const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
+        if (cs.type != t0) return fail(PHIP_ERR_UNSUPPORTED, "selection: column %s changes type across segments", q->columns[c]);
+        if (cs.type == PHIP_TYPE_STRING && (e.expr != PHIP_EXPR_COLUMN || cs.fwd_kind == PHIP_FWD_RAW_CHUNK))
+          return fail(PHIP_ERR_UNSUPPORTED, "selection: STRING column %s outside a dictionary-encoded projection",
+                      q->columns[c]);
+      }
+    }
+    const int t = segs[0]->cols[colidx[0][e.column_a]].type;
+    if (e.expr != PHIP_EXPR_COLUMN) {
+      d.kind = SEL_F64;
+      sel_types[k] = PHIP_TYPE_DOUBLE;
+    } else if (t == PHIP_TYPE_STRING) {
+      d.kind = SEL_ID;
+      sel_types[k] = PHIP_TYPE_STRING;
+      if (!col_remap[e.column_a]) {
+        std::vector<int> ci(nseg);
+        for (int s = 0; s < nseg; s++) ci[s] = colidx[s][e.column_a];
+        int32_t rc = build_remap(*dev, segs, ci, q->columns[e.column_a], col_remap[e.column_a]);
+        if (rc) return rc;
+      }
+      sel_dicts[k] = col_remap[e.column_a];
+    } else {
+      d.kind = (t == PHIP_TYPE_INT || t == PHIP_TYPE_LONG) ? SEL_I64 : SEL_F64;
+      sel_types[k] = t;
+    }
+  }
+  sq.num_select = nsel;
+  sq.limit = std::max<int64_t>(0, q->select_limit);
   int num_projected = 0;
   for (bool p : projected) num_projected += p ? 1 : 0;
 
@@ -1365,6 +1434,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       ds.cols[dq.aggs[a].col_a].hll = h;
     }
     for (int k = 0; k < q->num_group_by; k++) ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
+    for (int c = 0; c < ncols; c++)
+      if (col_remap[c]) ds.cols[c].remap = col_remap[c]->dev[s];
     if (sg.num_docs == 0) continue;
    // one entry per filter program (adjacent, so the programs of a segment read its columns back to back)
    for (int prog = 0; prog < nprog; prog++) {
@@ -1688,7 +1759,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   for (const DevSeg &ds : dsegs) has_filter |= ds.node_end > ds.node_begin;
   bool need_agg = group_by || nprog > 1;  // several programs: every COUNT is per program, in the aggregation walk
   for (int a = 0; a < naggs; a++) need_agg |= dq.aggs[a].acc != ACC_COUNT;
-  bool need_mask = has_filter && (need_agg || want_bitmap);
+  bool need_mask = has_filter && (need_agg || want_bitmap || nsel > 0);
   const int64_t kSlotBudget = 19 * 1024;  // bytes per ring slot
   int32_t stage_stride = 0;
   std::vector<double> seg_est(dsegs.size(), 1.0);
@@ -2002,6 +2073,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   kinds[naggs + 1] = ACC_COUNT;
   const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
   const size_t dq_off = blob.reserve(sizeof(DevAggQuery));  // written once every pointer is known
+  const size_t sq_off = nsel > 0 ? blob.reserve(sizeof(DevSelQuery)) : 0;
 
   void *dblob;
   int32_t rc = P.alloc(blob.data.size() + 64, &dblob);
@@ -2102,6 +2174,37 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   }
 
   memcpy(blob.data.data() + dq_off, &dq, sizeof(dq));
+  if (nsel > 0) {
+    void *sb;
+    const size_t nent = dsegs.size();
+    rc = P.alloc(((size_t)total_work + 1) * 16 + (2 * nent + 1) * 8 + 16, &sb);
+    if (rc) return rc;
+    P.sel_tile_cnt = (int64_t *)sb;
+    P.sel_tile_off = P.sel_tile_cnt + total_work + 1;
+    P.sel_base = P.sel_tile_off + total_work + 1;
+    P.sel_kept = P.sel_base + nent + 1;
+    P.sel_total = P.sel_kept + nent;
+    sq.segs = dev_segs;
+    sq.num_segs = (int32_t)nent;
+    sq.total_work = (int32_t)total_work;
+    sq.mask = has_filter ? (const uint32_t *)masks : nullptr;
+    sq.tile_off = P.sel_tile_off;
+    sq.seg_base = P.sel_base;
+    memcpy(blob.data.data() + sq_off, &sq, sizeof(sq));
+    P.select = true;
+    P.nsel = nsel;
+    P.sq_off = sq_off;
+    P.sel_types = sel_types;
+    P.sel_dicts = sel_dicts;
+    for (int k = 0; k < nsel; k++) {  // bytes one row reads per expression (first segment's widths)
+      for (int c : {sq.sel[k].col_a, sq.sel[k].expr != PHIP_EXPR_COLUMN ? sq.sel[k].col_b : -1}) {
+        if (c < 0) continue;
+        const ColumnStore &cs = segs[0]->cols[colidx[0][c]];
+        P.sel_bits.push_back(cs.fwd_kind == PHIP_FWD_RAW_CHUNK ? 0 : cs.bits);
+        P.sel_width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));
+      }
+    }
+  }
   // the descriptor blob goes up once, synchronously (its host copy dies with this function)
   HIP_TRY(hipMemcpyAsync(dblob, blob.data.data(), blob.data.size(), hipMemcpyHostToDevice, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -2458,6 +2561,47 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   return PHIP_OK;
 }
 
+// Selection (select.hip): after the filter launch, rank the matched docs per work tile, give each entry its rows
+// (first LIMIT in doc order, concatenated in segment order up to LIMIT) and gather the select expressions.
+// Blocks until the rows are in impl.sel_values; kept[e] receives each entry's kept rows (numDocsScanned).
+static int32_t execute_select(Plan &P, Workspace &ws, hipStream_t st, ResultImpl &impl, std::vector<int64_t> &kept,
+                              int64_t *num_rows, float *gather_ms) {
+  const DevSelQuery *dsq = (const DevSelQuery *)(P.base + P.sq_off);
+  const int64_t tw = P.total_work;
+  const size_t nent = P.dsegs.size();
+  int32_t rc;
+  int64_t tot[2] = {0, 0};
+  kept.assign(nent, 0);
+  *num_rows = 0;
+  *gather_ms = 0.f;
+  if (tw > 0) {
+    size_t tb = 0;
+    HIP_TRY(launch_select_scan(nullptr, &tb, nullptr, nullptr, tw + 1, st));
+    void *tmp;
+    if ((rc = ws.get("sel_scan", std::max<size_t>(tb, 16), &tmp))) return rc;
+    HIP_TRY(launch_select_count(dsq, tw, P.sel_tile_cnt, st));
+    HIP_TRY(launch_select_scan(tmp, &tb, P.sel_tile_cnt, P.sel_tile_off, tw + 1, st));
+    HIP_TRY(launch_select_bases(dsq, P.sel_base, P.sel_kept, P.sel_total, st));
+    HIP_TRY(hipMemcpyAsync(tot, P.sel_total, 16, hipMemcpyDeviceToHost, st));
+    if (nent) HIP_TRY(hipMemcpyAsync(kept.data(), P.sel_kept, nent * 8, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t rows = tot[0];
+  impl.sel_values.assign((size_t)rows * P.nsel, 0);
+  if (rows > 0) {
+    void *out;
+    if ((rc = ws.get("sel_out", (size_t)rows * P.nsel * 8, &out))) return rc;
+    HIP_TRY(hipEventRecord(P.ev[4], st));
+    HIP_TRY(launch_select_gather(dsq, tw, (uint64_t *)out, rows, st));
+    HIP_TRY(hipEventRecord(P.ev[2], st));
+    HIP_TRY(hipMemcpyAsync(impl.sel_values.data(), out, (size_t)rows * P.nsel * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipEventElapsedTime(gather_ms, P.ev[4], P.ev[2]));
+  }
+  *num_rows = rows;
+  return PHIP_OK;
+}
+
 // EXEC_FULL: one execution end to end (phip_plan_execute). EXEC_PARTIAL: the kernels up to the dense
 // group table, handed to the caller (phip_plan_execute_partial). EXEC_FINISH: compaction / trim / copy-out
 // of the caller-merged table (phip_plan_finish).
@@ -2734,6 +2878,16 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   } else {
     HIP_TRY(hipStreamSynchronize(st));
   }
+  // selection: the filter's tile masks -> rows (its own launches; event 2 / 4 then bracket the gather kernel)
+  std::vector<int64_t> sel_kept;
+  int64_t sel_rows = 0;
+  float sel_ms = 0.f;
+  if (P.select) {
+    float t_f = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t_f, P.ev[1], P.ev[4]));  // the filter launch, before the events are reused
+    if ((rc = execute_select(P, ws, st, *impl, sel_kept, &sel_rows, &sel_ms))) return rc;
+    P.sel_filter_ms = t_f;
+  }
   const int64_t matched = has_filter ? (int64_t)fin[32] : docs_in_work;
   if (filter_words && !has_filter) {  // no filter program: every doc of the (single) segment matches
     const int64_t n = dsegs.empty() ? 0 : dsegs[0].num_docs;
@@ -2821,6 +2975,32 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   r.long_exact = impl->exact.data();
   r.scan_kernel_ms = t_scan;
   r.device_ms = t_all;
+  if (P.select) {
+    // SelectionOnlyOperator statistics per segment: numDocsScanned = its kept rows, post-filter entries = that x the
+    // projected columns; a segment matched when it kept a row
+    int64_t docs = 0;
+    int32_t segs_matched = 0;
+    std::vector<int64_t> per_seg(nseg, 0);
+    for (size_t e = 0; e < dsegs.size(); e++) per_seg[dsegs[e].seg_index % nseg] += sel_kept[e];
+    for (int s = 0; s < nseg; s++) {
+      docs += per_seg[s];
+      segs_matched += per_seg[s] > 0 ? 1 : 0;
+    }
+    r.num_docs_scanned = docs;
+    r.num_entries_scanned_post_filter = docs * P.num_projected;
+    r.num_segments_matched = segs_matched;
+    r.num_rows = sel_rows;
+    r.num_select = P.nsel;
+    impl->sel_types = P.sel_types;
+    impl->sel_dicts = P.sel_dicts;
+    r.select_types = impl->sel_types.data();
+    r.select_values = impl->sel_values.data();
+    r.filter_kernel_ms = has_filter ? P.sel_filter_ms : 0.0;
+    r.agg_kernel_ms = sel_ms;  // the projection (gather) kernel
+    int64_t per_row = 8 * (int64_t)P.nsel;
+    for (size_t i = 0; i < P.sel_bits.size(); i++) per_row += P.sel_bits[i] ? ceil_div(P.sel_bits[i], 8) : P.sel_width[i];
+    r.agg_bytes = sel_rows * per_row;
+  }
   P.clean = true;
   P.partial_pending = false;
   lg.done = true;
@@ -3106,6 +3286,20 @@ PHIP_API int32_t phip_result_dictionary(const phip_result *result, int32_t k, ph
   return PHIP_OK;
 }
 
+PHIP_API int32_t phip_result_select_dictionary(const phip_result *result, int32_t k, phip_dictionary_view *out) {
+  if (!result || !out) return fail(PHIP_ERR_INVALID, "null argument");
+  const ResultImpl *impl = reinterpret_cast<const ResultImpl *>(result);
+  if (k < 0 || k >= (int)impl->sel_dicts.size() || !impl->sel_dicts[k])
+    return fail(PHIP_ERR_INVALID, "select column %d holds no dictionary ids", k);
+  const auto &d = impl->sel_dicts[k];
+  out->data_type = d->type;
+  out->cardinality = d->card;
+  out->string_width = d->width;
+  out->reserved = 0;
+  out->values = d->values.data();
+  return PHIP_OK;
+}
+
 PHIP_API void phip_result_free(phip_result *result) {
   if (result) delete reinterpret_cast<ResultImpl *>(result);
 }
@@ -3115,6 +3309,7 @@ PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *word
   phip_query_desc q = *query;
   q.num_aggregations = 0;
   q.num_group_by = 0;
+  q.num_select = 0;
   q.trim_size = 0;  // filter only: no groups to trim
   q.num_order_by_keys = 0;
   phip_result *r = nullptr;

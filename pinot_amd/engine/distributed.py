@@ -254,7 +254,9 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
                 merged[k] = v if k not in merged else [merge_intermediate(a.function, x, y)
                                                        for a, x, y in zip(aggs, merged[k], v)]
         stats = _stats_from(np.sum([p[1] for p in parts], axis=0))
-        return GroupByResultsBlock(aggs, block.group_by, merged, stats, any(p[2] for p in parts))
+        out = GroupByResultsBlock(aggs, block.group_by, merged, stats, any(p[2] for p in parts))
+        out.key_types = getattr(block, "key_types", None)
+        return out
     index = [{v: i for i, v in enumerate(d)} for d in gdict]
     strides = np.cumprod([1] + cards[:-1]).astype(np.int64)
     lay = _Layout(aggs, hll_m)
@@ -278,7 +280,9 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
             key.append(gdict[c][rem % cards[c]])
             rem //= cards[c]
         groups[tuple(key)] = lay.get(srows[d, 1:], mrows[d])
-    return GroupByResultsBlock(aggs, block.group_by, groups, _stats_from(sv[:6]), bool(mv[0]))
+    out = GroupByResultsBlock(aggs, block.group_by, groups, _stats_from(sv[:6]), bool(mv[0]))
+    out.key_types = getattr(block, "key_types", None)
+    return out
 
 
 # ------------------------------------------------------------------------------------------------------

@@ -10,6 +10,10 @@ blocks to the next stage as row blocks (pinot-query-runtime/.../runtime/operator
                                      (…/operator/utils/TypeUtils.java:40-60: Number.intValue / longValue / floatValue /
                                      doubleValue, toString for STRING)
 
+Selection leaves (the lineorder side of a joined SSB query: a filter plus a projection of join keys and metrics,
+SelectionOnlyOperator) arrive as SelectionResultsBlocks: composeSelectTransferableBlock (:505-560) maps the stage's
+select expressions onto the block's DataSchema columns (reordering when they differ) and converts the stored types.
+
 Rows follow the results blocks: AggregationResultsBlock.getRows (…/blocks/results/AggregationResultsBlock.java:99-101)
 is one row of intermediate results; GroupByResultsBlock.getRows (:173-183) is one row per group, group-by values
 then intermediates. Intermediates keep their single-stage types: SUM / MIN / MAX as DOUBLE (the library's exact
@@ -25,7 +29,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from .results import AggregationResultsBlock, GroupByResultsBlock
+from .results import AggregationResultsBlock, GroupByResultsBlock, SelectionResultsBlock
 
 # DataSchema.ColumnDataType stored types on this path
 INT, LONG, FLOAT, DOUBLE, STRING, OBJECT = "INT", "LONG", "FLOAT", "DOUBLE", "STRING", "OBJECT"
@@ -88,33 +92,52 @@ def _intermediate(function, v):
     return v
 
 
-def _key_type(v):
-    if isinstance(v, str):
-        return STRING
-    if isinstance(v, float):
-        return DOUBLE
-    return LONG if abs(int(v)) >= 2 ** 31 else INT
-
-
 def block_schema(block) -> DataSchema:
-    """The results block's own schema (group-by columns first, then one column per function)."""
+    """The results block's own schema (group-by columns first, then one column per function; a selection block's
+    DataSchema as it is). Group-by column types are the columns' stored types from the segment metadata
+    (GroupByResultsBlock's DataSchema: the group-by expressions' result types), never guessed from the values."""
+    if isinstance(block, SelectionResultsBlock):
+        return DataSchema(list(block.column_names), list(block.column_types))
     aggs = block.aggregations
     names = [a.result_column_name for a in aggs]
     types = [_stored_type(a.function) for a in aggs]
     if isinstance(block, GroupByResultsBlock):
         keys = [str(e) for e in block.group_by]
-        sample = next(iter(block.groups), None)
-        ktypes = [_key_type(v) for v in sample] if sample is not None else [STRING] * len(keys)
-        return DataSchema(keys + names, ktypes + types)
+        if block.key_types is None:
+            raise ValueError("group-by block without key types (the plan records them from the column metadata)")
+        return DataSchema(keys + names, list(block.key_types) + types)
     return DataSchema(names, types)
 
 
 def block_rows(block) -> List[list]:
     """BaseResultsBlock.getRows."""
+    if isinstance(block, SelectionResultsBlock):
+        return block.rows
     fns = [a.function for a in block.aggregations]
     if isinstance(block, AggregationResultsBlock):
         return [[_intermediate(f, v) for f, v in zip(fns, block.results)]]
     return [list(k) + [_intermediate(f, v) for f, v in zip(fns, vals)] for k, vals in block.groups.items()]
+
+
+def compose_select_transferable_block(block: SelectionResultsBlock, select_exprs, desired: DataSchema):
+    """composeSelectTransferableBlock (LeafStageTransferableBlockOperator.java:505-583): the column of every stage
+    select expression in the block's DataSchema; in order -> composeDirectTransferableBlock, else
+    composeColumnIndexedTransferableBlock (reorder, converting where the stored types differ)."""
+    index = {n: i for i, n in enumerate(block.column_names)}
+    idx = [index[str(e)] for e in select_exprs]
+    if idx == list(range(len(idx))) and len(idx) == len(block.column_names):
+        return compose_transferable_block(block, desired)
+    have = block.column_types
+    conv = [have[i] != t for i, t in zip(idx, desired.column_types)]
+    cols = [c.tolist() if hasattr(c, "tolist") else list(c) for c in block.columns]
+    rows = []
+    for r in range(block.num_rows):
+        row = []
+        for j, i in enumerate(idx):
+            v = cols[i][r]
+            row.append(convert(v, desired.column_types[j]) if conv[j] and v is not None else v)
+        rows.append(row)
+    return TransferableBlock(rows, desired)
 
 
 def compose_transferable_block(block, desired: DataSchema) -> TransferableBlock:
@@ -163,6 +186,11 @@ class GpuLeafStageOperator:
                            "totalDocs": s.num_total_docs,
                            "numGroupsLimitReached": bool(getattr(blk, "num_groups_limit_reached", False))}
             self._state = 1
+            if isinstance(blk, SelectionResultsBlock):
+                exprs = [e for e, _ in self.query.select]
+                if len(exprs) == 1 and str(exprs[0]) == "*":
+                    exprs = list(blk.column_names)
+                return compose_select_transferable_block(blk, exprs, self.desired or block_schema(blk))
             return compose_transferable_block(blk, self.desired or block_schema(blk))
         self._state = 2
         return TransferableBlock(None, None, is_end_of_stream=True, stats=dict(self._stats))

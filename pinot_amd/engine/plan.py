@@ -25,7 +25,7 @@ from ..query.context import (UNBOUNDED, AggregationInfo, FilterContext, Function
                              QueryContext, columns_of)
 from ..query.sql import parse
 from ..spi import DEFAULT_NUM_GROUPS_LIMIT, DataType
-from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock
+from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock, SelectionResultsBlock
 from .segment import GpuSegment
 
 
@@ -569,6 +569,11 @@ class GpuCombineOperator:
         _lib.check(lib.phip_plan_finish(self._plan, ctypes.byref(merged), ctypes.byref(res)))
         return self._block_from_result(res)
 
+    def key_types(self):
+        """Stored types of the group-by columns, from the column metadata (the group-by block's DataSchema)."""
+        return [_STORED[self.segments[0].column_metadata(e.name).data_type] for e in self.query.group_by] \
+            if self.segments else None
+
     def _block_from_result(self, res):
         lib = _lib.load()
         try:
@@ -637,6 +642,7 @@ class GpuCombineOperator:
                 blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
                                           bool(r.num_groups_limit_reached))
                 blk.num_groups_trimmed = bool(r.num_groups_trimmed)
+                blk.key_types = self.key_types()
             blk.device_ms = r.device_ms
             blk.scan_kernel_ms = r.scan_kernel_ms
             blk.filter_kernel_ms, blk.agg_kernel_ms = r.filter_kernel_ms, r.agg_kernel_ms
@@ -660,6 +666,106 @@ def _dictionary_lookup(dv, ids):
     dt = {DataType.INT: np.int32, DataType.LONG: np.int64, DataType.FLOAT: np.float32, DataType.DOUBLE: np.float64}[t]
     arr = np.ctypeslib.as_array(ctypes.cast(dv.values, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(card,))
     return arr[ids].tolist()
+
+
+_STORED = {DataType.INT: "INT", DataType.LONG: "LONG", DataType.FLOAT: "FLOAT", DataType.DOUBLE: "DOUBLE",
+           DataType.STRING: "STRING"}
+
+
+class GpuSelectionOperator(GpuCombineOperator):
+    """SelectionOnlyOperator (pinot-core/.../operator/query/SelectionOnlyOperator.java:40-170) over every segment,
+    with SelectionOnlyCombineOperator's merge (…/operator/combine/SelectionOnlyCombineOperator.java:30-70): per
+    segment the first LIMIT matched docs in doc order, projected to the select expressions; the segments' rows
+    concatenated in segment order up to LIMIT (the reference merges in completion order; which rows a LIMIT below
+    the matches keeps is thread-timing dependent there, segment order here). One filter launch, then the selection
+    kernels (select.hip) rank the matched docs and gather the columns; STRING columns come back as ids in a
+    query-global dictionary. Statistics as the reference's: numDocsScanned = the rows each segment kept,
+    numEntriesScannedPostFilter = that x the projected columns. numEntriesScannedInFilter is the full filter scan
+    (the reference's lazy scan stops at LIMIT; the known answers exclude it). LIMIT 0 is EmptySelectionOperator:
+    the schema, no rows, zero statistics. ORDER BY (SelectionOrderByOperator) is outside this operator."""
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int = 0):
+        if query.order_by and query.limit > 0:
+            raise UnsupportedOnGpu("selection ORDER BY (SelectionOrderByOperator)")
+        if not segments:
+            raise UnsupportedOnGpu("selection over no segments")
+        self.exprs = query.select_expressions(list(segments[0].segment.columns))
+        self.sel = []
+        for e in self.exprs:
+            e2 = _strip_cast(e)
+            if isinstance(e2, Identifier):
+                self.sel.append((_lib.EXPR_COLUMN, e2.name, None))
+            else:
+                self.sel.append(_gpu_expr(e2))
+        if len(self.sel) > 16:
+            raise UnsupportedOnGpu("selection of more than 16 expressions")
+        super().__init__(query, segments, num_groups_limit)
+        for _, a, b in self.sel:
+            for c in (a, b):
+                if c is not None and c not in self.columns:
+                    self.columns.append(c)
+        for s in self.segments:
+            for c in self.columns:
+                if not s.has_column(c):
+                    raise KeyError(f"segment {s.name} has no column {c}")
+        self.names = [str(e) for e in self.exprs]
+        self.types = []
+        for expr, a, _ in self.sel:
+            m = self.segments[0].column_metadata(a)
+            if expr == _lib.EXPR_COLUMN:
+                self.types.append(_STORED[m.data_type])
+            else:
+                self.types.append("DOUBLE")
+
+    def _desc(self, keep):
+        q = super()._desc(keep)
+        col_index = {c: i for i, c in enumerate(self.columns)}
+        arr = (_lib.SelectExpr * len(self.sel))()
+        for i, (expr, a, b) in enumerate(self.sel):
+            arr[i].expr = expr
+            arr[i].column_a = col_index[a]
+            arr[i].column_b = col_index[b] if b is not None else -1
+        keep.append(arr)
+        q.num_select = len(self.sel)
+        q.select = arr
+        q.select_limit = int(self.query.limit)
+        return q
+
+    def next_block(self):
+        if self.query.limit <= 0:  # EmptySelectionOperator: the data schema only
+            stats = ExecutionStatistics(0, 0, 0, sum(s.num_docs for s in self.segments), len(self.segments), 0)
+            return SelectionResultsBlock(self.names, self.types, [[] for _ in self.names], stats)
+        lib = _lib.load()
+        res = self.run_raw()
+        try:
+            r = res.contents
+            stats = ExecutionStatistics(r.num_docs_scanned, r.num_entries_scanned_in_filter,
+                                        r.num_entries_scanned_post_filter, r.num_total_docs,
+                                        r.num_segments_processed, r.num_segments_matched)
+            n, k = int(r.num_rows), int(r.num_select)
+            raw = (np.ctypeslib.as_array(r.select_values, shape=(k * n,)).reshape(k, n).copy() if n * k
+                   else np.zeros((k, 0), dtype=np.uint64))
+            cols = []
+            for j, t in enumerate(self.types):
+                v = raw[j]
+                if t in ("INT", "LONG"):
+                    cols.append(v.view(np.int64).astype(np.int32 if t == "INT" else np.int64))
+                elif t == "FLOAT":
+                    cols.append(v.view(np.float64).astype(np.float32))
+                elif t == "DOUBLE":
+                    cols.append(v.view(np.float64))
+                else:
+                    dv = _lib.DictionaryView()
+                    _lib.check(lib.phip_result_select_dictionary(res, j, ctypes.byref(dv)))
+                    cols.append(_dictionary_lookup(dv, v.view(np.int64)) if n else [])
+            blk = SelectionResultsBlock(self.names, list(self.types), cols, stats)
+            blk.device_ms = r.device_ms
+            blk.filter_kernel_ms, blk.agg_kernel_ms = r.filter_kernel_ms, r.agg_kernel_ms
+            blk.filter_bytes, blk.agg_bytes = int(r.filter_bytes), int(r.agg_bytes)
+            blk.fused = False
+            return blk
+        finally:
+            lib.phip_result_free(res)
 
 
 def _run_parts(parts):
@@ -846,6 +952,7 @@ class GpuFilteredGroupByOperator:
         out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), blk.groups, blk.stats,
                                   blk.num_groups_limit_reached)
         out.num_groups_trimmed = getattr(blk, "num_groups_trimmed", False)
+        out.key_types = getattr(blk, "key_types", None)
         for k in GpuFilteredAggregationOperator._TIMES + ("fused",):
             setattr(out, k, getattr(blk, k, 0))
         return out
@@ -884,6 +991,7 @@ class GpuFilteredGroupByOperator:
                     vals[i] = v[j] if v is not None else (dflt.copy() if isinstance(dflt, np.ndarray) else dflt)
         blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats, False)
         blk.num_groups_trimmed = False
+        blk.key_types = self.parts[0][1].key_types() if self.parts else None
         if self.device_trim:
             blk = trim_groups(self.query, blk)
         blk.device_ms = device_ms
@@ -1046,6 +1154,7 @@ class GpuCaseAggregationOperator:
         out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups,
                                   self._stats(blk.stats, counts), blk.num_groups_limit_reached)
         out.num_groups_trimmed = False
+        out.key_types = getattr(blk, "key_types", None)
         out = trim_groups(self.query, out)
         out.device_ms = getattr(blk, "device_ms", 0.0)
         return out
@@ -1104,6 +1213,8 @@ class GpuInstancePlanMaker:
         if st is not None:
             st.inner.device_trim = self.device_trim
             return st
+        if query.is_selection:
+            return GpuSelectionOperator(query, segments, self.num_groups_limit)
         if any(ag.argument is not None and _is_case(ag.argument) for ag in query.aggregations):
             return GpuCaseAggregationOperator(query, segments, self.num_groups_limit)
         if any(ag.filter is not None for ag in query.aggregations):

@@ -92,6 +92,8 @@ def reduce_blocks(query: QueryContext, blocks) -> ResultTable:
     stats = ExecutionStatistics()
     for b in blocks:
         stats.merge(b.stats)
+    if query.is_selection:
+        return _reduce_selection(query, blocks, stats)
     names = [_column_name(e, a) for e, a in query.select]
     if not query.group_by:
         merged = None
@@ -138,6 +140,29 @@ def reduce_blocks(query: QueryContext, blocks) -> ResultTable:
     records = records[:query.limit]
     rows = [[value_of(e, rec) for e, _ in query.select] for rec in records]
     return ResultTable(names, rows, stats, limit_reached)
+
+
+def _reduce_selection(query: QueryContext, blocks, stats) -> ResultTable:
+    """SelectionOnlyReducer (pinot-core/.../query/reduce/SelectionOnlyReducer): the servers' rows concatenated up to
+    LIMIT, each row mapped to the select list (SelectionOperatorUtils.getSelectionColumns: SELECT * keeps the data
+    schema's columns; duplicated expressions read the same schema column)."""
+    schema = next((b for b in blocks if b.column_names), None)
+    if schema is None:
+        return ResultTable([], [], stats)
+    index = {n: i for i, n in enumerate(schema.column_names)}
+    star = len(query.select) == 1 and str(query.select[0][0]) == "*"
+    if star:
+        names, picks = list(schema.column_names), list(range(len(schema.column_names)))
+    else:
+        names = [_column_name(e, a) for e, a in query.select]
+        picks = [index[str(e)] for e, _ in query.select]
+    rows = []
+    for b in blocks:
+        for r in b.rows:
+            if len(rows) >= query.limit:
+                break
+            rows.append([r[i] for i in picks])
+    return ResultTable(names, rows, stats)
 
 
 def trim_size(query: QueryContext) -> int:

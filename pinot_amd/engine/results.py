@@ -2,6 +2,7 @@
 
   AggregationResultsBlock  pinot-core/.../operator/blocks/results/AggregationResultsBlock.java:54-155
   GroupByResultsBlock      pinot-core/.../operator/blocks/results/GroupByResultsBlock.java:68-106
+  SelectionResultsBlock    pinot-core/.../operator/blocks/results/SelectionResultsBlock.java (DataSchema + rows)
   ExecutionStatistics      pinot-core/.../operator/ExecutionStatistics.java:42-45
 
 Intermediate results follow each function's intermediate type:
@@ -50,6 +51,30 @@ class GroupByResultsBlock:
     num_groups_limit_reached: bool = False
     device_ms: float = 0.0
     scan_kernel_ms: float = 0.0
+    key_types: Optional[List[str]] = None  # stored types of the group-by columns (column metadata: INT / LONG / ...)
+
+
+@dataclass
+class SelectionResultsBlock:
+    """Rows of a selection query: the DataSchema's column names are the select expressions' strings, its types the
+    columns' stored types (DOUBLE for arithmetic, the transform functions' result type). The values are held
+    column-wise (numpy arrays, or lists of str) -- a multi-stage leaf ships millions of rows -- and `rows` builds
+    the row lists on demand."""
+    column_names: List[str]
+    column_types: List[str]
+    columns: List[object]
+    stats: ExecutionStatistics = field(default_factory=ExecutionStatistics)
+    device_ms: float = 0.0
+    scan_kernel_ms: float = 0.0
+
+    @property
+    def num_rows(self) -> int:
+        return len(self.columns[0]) if self.columns else 0
+
+    @property
+    def rows(self) -> List[list]:
+        cols = [c.tolist() if isinstance(c, np.ndarray) else list(c) for c in self.columns]
+        return [list(r) for r in zip(*cols)] if cols else []
 
 
 def merge_intermediate(function: str, a, b):

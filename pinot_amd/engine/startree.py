@@ -381,6 +381,7 @@ class GpuStarTreeOperator:
             out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
                                       blk.num_groups_limit_reached)
             out.num_groups_trimmed = getattr(blk, "num_groups_trimmed", False)
+            out.key_types = getattr(blk, "key_types", None)
         for a in ("device_ms", "scan_kernel_ms", "filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes"):
             setattr(out, a, getattr(blk, a, 0))
         out.star_tree = True

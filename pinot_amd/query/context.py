@@ -178,3 +178,21 @@ class QueryContext:
     @property
     def is_group_by(self) -> bool:
         return bool(self.group_by)
+
+    @property
+    def is_selection(self) -> bool:
+        """A selection (row-returning) query: no aggregation, no group-by (QueryContext.isSelectionQuery)."""
+        return not self.aggregations and not self.group_by
+
+    def select_expressions(self, segment_columns=None):
+        """SelectionOperatorUtils.extractExpressions (pinot-core/.../query/selection/SelectionOperatorUtils.java:
+        83-124) without ORDER BY: the select expressions, deduplicated in order; SELECT * expands to the segment's
+        columns sorted by name (columns starting with '$' excluded)."""
+        exprs = [e for e, _ in self.select]
+        if len(exprs) == 1 and isinstance(exprs[0], Identifier) and exprs[0].name == "*":
+            return [Identifier(c) for c in sorted(c for c in (segment_columns or []) if not c.startswith("$"))]
+        out = []
+        for e in exprs:
+            if e not in out:
+                out.append(e)
+        return out

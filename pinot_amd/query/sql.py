@@ -295,6 +295,8 @@ class _Parser:
         return table, select, filt, group_by, order_by, limit
 
     def _select_item(self):
+        if self.accept("op", "*"):  # SELECT * (expanded per segment: SelectionOperatorUtils.extractExpressions)
+            return Identifier("*"), None
         e = self.expr()
         if self.peek()[0] == "ident" and str(self.peek()[1]).lower() == "filter":
             # agg(...) FILTER(WHERE ...) (CalciteSqlParser's FILTER clause -> filtered aggregation)
@@ -381,5 +383,8 @@ def parse(sql: str) -> QueryContext:
             if group_by and e not in group_by:
                 raise SqlError(f"select expression {e} is neither an aggregation nor a group-by expression")
     if not aggs and not group_by:
-        raise SqlError("selection / distinct queries are out of scope for the hot path")
+        # selection (SelectionOnlyOperator): columns and arithmetic over them; SELECT * stays a single '*'
+        for e, _ in select:
+            if isinstance(e, FilterClause) or (isinstance(e, Identifier) and e.name == "*" and len(select) > 1):
+                raise SqlError(f"select expression {e} in a selection query")
     return QueryContext(table, select, aggs, filt, group_by, resolved_order, limit, options)

@@ -253,6 +253,32 @@ def _fast_count_cases():
     return [(f"{FFC}:146-310", q, [[v]], None) for q, v in cases]
 
 
+SEL = "pinot-core/src/test/java/org/apache/pinot/queries/InnerSegmentSelectionSingleValueQueriesTest.java"
+
+
+def _selection_cases():
+    """Selection-only known answers over the ONE test_data-sv segment of the inner-segment tests: row count, the
+    first row's asserted columns, the schema's size and asserted types, (numDocsScanned,
+    numEntriesScannedPostFilter). numEntriesScannedInFilter depends on the lazy scan stopping at LIMIT (48204 at
+    :148) and is excluded."""
+    star, sel = "SELECT * FROM testTable", "SELECT column1, column5, column11 FROM testTable"
+    types = {"column1": "INT", "column11": "STRING"}
+    return [
+        {"ref": f"{SEL}:47-66", "query": star + " LIMIT 0", "num_rows": 0, "first": {}, "schema_size": 11,
+         "types": types, "stats": [0, 0]},
+        {"ref": f"{SEL}:68-83", "query": star + FILTER + " LIMIT 0", "num_rows": 0, "first": {}, "schema_size": 11,
+         "types": types, "stats": [0, 0]},
+        {"ref": f"{SEL}:119-141", "query": star, "num_rows": 10, "first": {"column1": 1578964907, "column11": "P"},
+         "schema_size": 11, "types": types, "stats": [10, 110]},
+        {"ref": f"{SEL}:143-164", "query": star + FILTER, "num_rows": 10,
+         "first": {"column1": 351823652, "column11": "t"}, "schema_size": 11, "types": types, "stats": [10, 110]},
+        {"ref": f"{SEL}:168-190", "query": sel, "num_rows": 10, "first": {"column1": 1578964907, "column11": "P"},
+         "schema_size": 3, "types": types, "stats": [10, 30]},
+        {"ref": f"{SEL}:192-212", "query": sel + FILTER, "num_rows": 10,
+         "first": {"column1": 351823652, "column11": "t"}, "schema_size": 3, "types": types, "stats": [10, 30]},
+    ]
+
+
 DOCSETS = "pinot-core/src/test/java/org/apache/pinot/core/operator/filter/"
 
 
@@ -285,7 +311,7 @@ def write_expected():
         cases.append({"ref": ref, "data": "test_data_sv", "query": q, "rows": rows, "stats": stats})
     for ref, q, rows, stats in _fast_count_cases():
         cases.append({"ref": ref, "data": "fast_filtered_count", "query": q, "rows": rows, "stats": stats})
-    out = {"queries": cases, "docsets": _docset_cases(),
+    out = {"queries": cases, "docsets": _docset_cases(), "selections": _selection_cases(),
            "note": "known answers transcribed from the reference's tests; see make_fixtures.py"}
     with open(os.path.join(HERE, "expected.json"), "w") as f:
         json.dump(out, f, indent=1)

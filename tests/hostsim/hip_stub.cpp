@@ -142,4 +142,13 @@ hipError_t launch_limit_runs(void *, size_t *scan_bytes, const uint64_t *, int64
 hipError_t launch_limit_reduce(const uint64_t *, const int64_t *, int64_t, const int32_t *, const int32_t *, int64_t,
                                int32_t, int32_t, const int32_t *, const uint64_t *, const uint32_t *, int32_t, int32_t, int64_t *,
                                double *, int64_t *, uint8_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_select_count(const DevSelQuery *, int64_t, int64_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_select_scan(void *, size_t *temp_bytes, const int64_t *, int64_t *, int64_t, hipStream_t) {
+  *temp_bytes = 256; return hipSuccess;
+}
+hipError_t launch_select_bases(const DevSelQuery *q, int64_t *, int64_t *kept, int64_t *total, hipStream_t) {
+  for (int e = 0; e < q->num_segs; e++) kept[e] = 0;
+  total[0] = total[1] = 0; return hipSuccess;
+}
+hipError_t launch_select_gather(const DevSelQuery *, int64_t, uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
 }  // namespace phip

@@ -16,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PAIRS = [("phip_column_desc", _lib.ColumnDesc), ("phip_segment_desc", _lib.SegmentDesc),
          ("phip_raw_range", _lib.RawRange), ("phip_filter_node", _lib.FilterNode),
          ("phip_aggregation", _lib.Aggregation), ("phip_query_desc", _lib.QueryDesc),
+         ("phip_select_expr", _lib.SelectExpr),
          ("phip_order_term", _lib.OrderTerm),
          ("phip_result", _lib.Result), ("phip_dictionary_view", _lib.DictionaryView),
          ("phip_partial", _lib.Partial)]
