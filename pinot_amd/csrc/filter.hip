@@ -101,6 +101,19 @@ __device__ __forceinline__ double raw_real_at(ccol_t &c, int32_t doc) {
   return c.type == PHIP_TYPE_DOUBLE ? ((const PHIP_GLB double *)c.raw)[doc] : (double)((const PHIP_GLB float *)c.raw)[doc];
 }
 
+// Membership in a raw IN list (RawValueBasedPredicateEvaluator's value set): the host sorts and deduplicates the
+// values (doubles without NaN, which IEEE equality never matches), so a doc costs log2(count) probes of the
+// L1-resident list instead of a scan of it.
+template <typename T>
+__device__ __forceinline__ bool sorted_contains(const PHIP_GLB T *set, int32_t count, T v) {
+  int32_t lo = 0, hi = count;  // first element >= v
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (set[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo < count && set[lo] == v;
+}
+
 __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__ n, uint32_t valid, const Tile &t,
                                               uint32_t &scanned) {
   const int lane = lane_id();
@@ -164,18 +177,14 @@ __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__
         if (kind == PHIP_LEAF_RAW_RANGE) {
           pass = v >= lo_i && v <= hi_i;
         } else {
-          pass = false;
-          for (int k = 0; k < n->count; k++) pass = pass || set_i[k] == v;
-          pass = pass != excl;
+          pass = sorted_contains(set_i, n->count, v) != excl;
         }
       } else {
         const double v = raw_real_at(c, doc);
         if (kind == PHIP_LEAF_RAW_RANGE) {
           pass = (lo_in ? v >= lo_f : v > lo_f) && (hi_in ? v <= hi_f : v < hi_f);
         } else {
-          pass = false;
-          for (int k = 0; k < n->count; k++) pass = pass || set_f[k] == v;
-          pass = pass != excl;
+          pass = sorted_contains(set_f, n->count, v) != excl;
         }
       }
       r = r + r + (uint32_t)pass;

@@ -739,8 +739,8 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
         err = "raw range leaf needs a phip_raw_range";
         return -1;
       }
-      if (n.leaf_kind == PHIP_LEAF_RAW_SET && (n.count % 2 != 0 || n.count > 2 * 1024)) {
-        err = "raw set leaf: count must be 2 x (values <= 1024)";
+      if (n.leaf_kind == PHIP_LEAF_RAW_SET && (n.count % 2 != 0 || n.count > 2 * (1 << 20))) {
+        err = "raw set leaf: count must be 2 x (values <= 2^20)";
         return -1;
       }
       if ((n.leaf_kind == PHIP_LEAF_DICT_SET || n.leaf_kind == PHIP_LEAF_INVERTED || n.leaf_kind == PHIP_LEAF_DOC_RANGES ||
@@ -1545,11 +1545,34 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             if (cs->fwd_kind != PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "raw leaf on dictionary column"); break; }
             if (cs->type == PHIP_TYPE_STRING) { rc = fail(PHIP_ERR_UNSUPPORTED, "raw STRING predicate"); break; }
             if (fn.leaf_kind == PHIP_LEAF_RAW_SET) {
-              dn.count = fn.count / 2;  // values
+              // the kernel binary-searches the values (filter.hip sorted_contains): sorted, distinct, and for
+              // FLOAT / DOUBLE columns without NaN (IEEE equality never matches it)
+              const int64_t nv = fn.count / 2;
+              std::vector<int64_t> vi;
+              std::vector<double> vf;
+              const bool real = cs->type == PHIP_TYPE_FLOAT || cs->type == PHIP_TYPE_DOUBLE;
+              for (int64_t k = 0; k < nv; k++) {
+                int64_t x;
+                memcpy(&x, fn.ids + 2 * k, 8);
+                if (!real) {
+                  vi.push_back(x);
+                } else {
+                  double d;
+                  memcpy(&d, &x, 8);
+                  if (d == d) vf.push_back(d);
+                }
+              }
+              std::sort(vi.begin(), vi.end());
+              vi.erase(std::unique(vi.begin(), vi.end()), vi.end());
+              std::sort(vf.begin(), vf.end());
+              vf.erase(std::unique(vf.begin(), vf.end()), vf.end());  // (-0.0 and 0.0 compare equal: one kept)
+              dn.count = (int32_t)(real ? vf.size() : vi.size());
               if (dn.count == 0) {
                 dn.leaf_kind = fn.exclusive ? PHIP_LEAF_MATCH_ALL : PHIP_LEAF_MATCH_NONE;
                 break;
               }
+              aux_fix.push_back({ni, real ? blob.add(vf.data(), vf.size() * 8) : blob.add(vi.data(), vi.size() * 8)});
+              break;
             }
             aux_fix.push_back({ni, blob.add(fn.ids, (size_t)fn.count * 4)});
             break;

@@ -72,6 +72,9 @@ def _doc_ranges_for(seg: GpuSegment, column: str, ev: predeval.DictPredicateEval
     return np.asarray(ranges, dtype=np.int32).reshape(-1)
 
 
+RAW_SET_MAX = 1 << 20  # values of a raw IN list (the descriptor blob carries them)
+
+
 def _raw_predicate(column, dt: DataType, pred):
     """Value-based leaf on a raw column (RawValueBasedPredicateEvaluatorFactory + ScanBasedFilterOperator):
     literals converted to the column type first (FLOAT literals rounded to float32, as Float.parseFloat);
@@ -119,11 +122,14 @@ def _raw_predicate(column, dt: DataType, pred):
             vals.append(x)
         elif float(x).is_integer():
             vals.append(int(v) if isinstance(v, int) else int(x))
-    if len(vals) > 1024:
-        raise UnsupportedOnGpu("raw IN list longer than 1024 values")
-    if not vals:
+    # the device binary-searches the list: sorted, distinct, no NaN (IEEE equality never matches it)
+    arr = np.unique(np.asarray(vals, dtype=np.float64 if real else np.int64))
+    if real:
+        arr = arr[~np.isnan(arr)]
+    if len(arr) > RAW_SET_MAX:
+        raise UnsupportedOnGpu(f"raw IN list longer than {RAW_SET_MAX} values")
+    if not len(arr):
         return _TRUE if exclusive else _FALSE
-    arr = np.asarray(vals, dtype=np.float64 if real else np.int64)
     return _Leaf(_lib.LEAF_RAW_SET, column, exclusive=exclusive, ids=arr.view(np.int32).copy())
 
 

@@ -496,6 +496,11 @@ RAW_FILTERS = [
     "ri BETWEEN -1000 AND 250000", "ri > 5.5 AND ri <= 100000", "ri IN (3, 7, 11, -5, 2.5)", "ri NOT IN (3, 7)",
     "rl >= 1099511627776 OR rl < -5", "rl = 42", "rf > 0.1 AND rf < 0.7", "rf = 0.25", "rf IN (0.1, 0.5)",
     "rd >= 0.5", "rd < 0.25 OR NOT (ri BETWEEN 0 AND 1000000 AND rd > 0.9)", "d IN (1, 2) AND rd <> 0.5",
+    # long raw IN lists (unsorted, with duplicates): binary search over the library's sorted copy
+    "ri IN (" + ", ".join(str(x) for x in np.random.default_rng(3).integers(-2000, 2_000_000, 3000)) + ")",
+    "rd NOT IN (" + ", ".join(f"{x:.3f}" for x in np.random.default_rng(4).random(2500)) + ")",
+    "rl IN (42, " + ", ".join(str(x) for x in np.random.default_rng(5).integers(-2 ** 41, 2 ** 41, 1500)) + ", 42)",
+    "rf IN (0.0, -0.0, 0.5, 0.25, 0.5)",
 ]
 
 
