@@ -21,7 +21,10 @@ fi
 step bench 600 python -u bench.py --steps 10 --warmup 3 "$@"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 B="--no-cpu-baseline --steps 10 --warmup 3 $*"
-step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 -u bench.py $B
+# one kernel-trace summary per layout, so the headline (sorted) kernels' averages read straight from their own file
+for L in sorted unsorted; do
+  step rocprof_$L 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
+done
 for L in sorted unsorted; do
   step pmcf_$L 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
   step pmcw_$L 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
