@@ -335,55 +335,4 @@ __device__ __forceinline__ void batch_expr_f64(cseg_t &s, cagg_t &a, const int32
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// finalize in the last workgroup (DevFinal): every workgroup makes its partial stores and atomics visible at agent
-// scope (the release of the classic last-block reduction), takes a ticket, and the workgroup holding the last ticket
-// acquires and runs finalize_all_kernel's work -- one wave per slot, lane-strided over the blocks in a fixed order and
-// a fixed shuffle tree (bitwise reproducible) -- then copies / zeroes the per-segment counts and the registers.
-// Reads go through agent-scope atomic loads, so no XCD's stale L2 line is read.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t coherent_load(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t coherent_load(const uint32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void fin_slot(const uint64_t *partials, int nblocks, int nslots, int kind, uint64_t *out,
-                                         int a) {
-  const int lane = lane_id();
-  const bool fp = kind == ACC_SUM_F64 || kind == ACC_MIN_F64 || kind == ACC_MAX_F64;
-  uint64_t v = fp ? acc_init(kind) : 0;
-  for (int b = lane; b < nblocks; b += 64) v = acc_combine(kind, v, coherent_load(partials + (int64_t)b * nslots + a));
-  if (fp) v = as_u64(wave_reduce_f64(as_f64(v), kind));
-  else v = wave_reduce_u64_add(v);
-  if (lane == 0) out[a] = v;
-}
-
-__device__ __forceinline__ void finalize_tail(const DevFinal *fp) {
-  __shared__ uint32_t ticket;
-  __threadfence();  // this thread's partial stores / atomics, released at agent scope
-  __syncthreads();
-  if (threadIdx.x == 0) ticket = atomicAdd(fp->counter, 1u);
-  __syncthreads();
-  if (ticket != gridDim.x - 1) return;
-  __threadfence();  // acquire: every other workgroup released before its ticket
-  const DevFinal &f = *fp;
-  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int s = wave; s < f.na + 2; s += nw) {
-    if (s < f.na) fin_slot(f.pa, f.nba, f.na, f.ka[s], f.out, s);
-    else if (f.pf != nullptr) fin_slot(f.pf, f.nbf, 2, f.kf[s - f.na], f.out + 32, s - f.na);
-  }
-  for (int i = threadIdx.x; i < f.nseg; i += blockDim.x) {
-    f.out[64 + i] = coherent_load(f.segm + i);
-    f.segm[i] = 0;
-  }
-  uint32_t *oh = (uint32_t *)(f.out + 64 + f.nseg);
-  for (int i = threadIdx.x; i < f.hll_words; i += blockDim.x) {
-    oh[i] = coherent_load(f.hll + i);
-    f.hll[i] = 0;
-  }
-  if (threadIdx.x == 0) *f.counter = 0;
-}
-
 }  // namespace phip

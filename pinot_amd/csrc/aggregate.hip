@@ -440,7 +440,6 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
     }
     for (int i = threadIdx.x; i < hll_words; i += kAggBlock)
       if (hll_lds[i]) __hip_atomic_fetch_max((glb_u32 *)q.hll_regs + i, (uint32_t)hll_lds[i], PHIP_RLX, PHIP_AG);
-    if (q.fin != nullptr) finalize_tail(q.fin);
   } else if constexpr (MODE == GB_LDS) {
     __syncthreads();
     glb_u64 *slab = (glb_u64 *)q.gb_table + (size_t)blockIdx.x * q.tbl_words;

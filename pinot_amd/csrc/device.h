@@ -163,22 +163,6 @@ struct DevNode {
                       // RAW_RANGE: phip_raw_range; RAW_SET: `count` int64 / double values
 };
 
-// The per-execution results of an aggregation-only plan (what finalize_all_kernel computes), produced instead by the
-// last workgroup of the plan's last kernel (agg_common.h finalize_tail): fixed-order reductions of the per-block
-// partials, the per-segment matched counts and the HLL registers, written into the plan's mapped pinned area and
-// the device counters zeroed for the next execution -- one launch and its dispatch gap fewer per query.
-struct DevFinal {
-  const uint64_t *pa;   // aggregation partials [nba][na], or null
-  const int32_t *ka;    // their accumulator kinds
-  const uint64_t *pf;   // filter partials [nbf][2] (matched docs, entries scanned), or null
-  const int32_t *kf;
-  uint64_t *segm;       // [nseg] matched docs per (program, segment) entry
-  uint32_t *hll;        // [hll_words] registers (aggregation only)
-  uint64_t *out;        // pinned: [0, na) slots, [32, 34) filter sums, [64, 64 + nseg) segm, then the registers
-  uint32_t *counter;    // workgroups done (the last one finalizes and resets it)
-  int32_t nba, na, nbf, nseg, hll_words, pad;
-};
-
 // Filter kernel launch (K1-K4 of SURVEY.md §2.4).
 struct DevFilter {
   const DevSeg *segs;
@@ -201,7 +185,6 @@ struct DevFilter {
   uint64_t *agg_partials;         // [num_blocks][num_aggs]
   int32_t fring_bytes;            // per-wave matched-doc ring (fused): 4 * kFusedRingDefer when a segment defers,
   int32_t pad_f;                  // else 2 * kFusedRingTile
-  const DevFinal *fin;            // non-null: this launch is the plan's last; its last workgroup finalizes
 };
 
 struct DevAgg {
@@ -259,7 +242,6 @@ struct DevAggQuery {
   int32_t dense_min;  // GB_NONE + dense_batch: matched docs per 2048-doc tile from which the batched walk is used
   int32_t own_count_rows;  // group-by over several filter programs (FILTER + GROUP BY): every COUNT counts its own
                            // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
-  const DevFinal *fin;     // GB_NONE: non-null when this launch is the plan's last (agg_common.h finalize_tail)
 };
 
 // Selection (row-returning) queries (select.hip): SelectionOnlyOperator per segment + the combine's concatenation.

@@ -1289,7 +1289,6 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
       }
     }
   }
-  if (q.fin != nullptr) finalize_tail(q.fin);
 }
 
 // ------------------------------------------------------------------------------------------------

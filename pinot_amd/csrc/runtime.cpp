@@ -1057,8 +1057,6 @@ struct Plan {
   std::vector<std::shared_ptr<Device::Remap>> sel_dicts;
   std::vector<int32_t> sel_bits, sel_width;  // per select column's projected bytes (algorithmic bytes)
   float sel_filter_ms = 0.f;
-  int fin_where = 0;                // 0: finalize_all launch, 1: the aggregation kernel's last workgroup, 2: the filter's
-  uint32_t *fin_counter = nullptr;  // its workgroup ticket counter
   bool total_events = true;  // record ev[0] / ev[3] (phip_result.device_ms); PHIP_TOTAL_EVENTS=0 skips them (A/B)
 };
 
@@ -2098,7 +2096,6 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   kinds[naggs + 1] = ACC_COUNT;
   const size_t kinds_off = blob.add(kinds.data(), kinds.size() * 4);
   const size_t dq_off = blob.reserve(sizeof(DevAggQuery));  // written once every pointer is known
-  const size_t fin_off = blob.reserve(sizeof(DevFinal));
   const size_t sq_off = nsel > 0 ? blob.reserve(sizeof(DevSelQuery)) : 0;
 
   void *dblob;
@@ -2199,56 +2196,6 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     if (rc) return rc;
   }
 
-  // pinned landing area of the per-execution results (device-visible, mapped): finalize writes straight into it
-  {
-    void *h = nullptr;
-    const size_t pbytes = (64 + (size_t)nmatch) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4;
-    HIP_TRY(hipHostMalloc(&h, pbytes, hipHostMallocMapped));
-    memset(h, 0, pbytes);
-    P.pinned = (uint64_t *)h;
-    void *dp = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
-    P.pinned_dev = (uint64_t *)dp;
-  }
-  // Finalize in the last workgroup of the plan's last kernel (agg_common.h finalize_tail) instead of a
-  // finalize_all launch: aggregation-only plans whose last kernel is the aggregation walk or the filter
-  // (count-only, fused, selection). PHIP_FOLD_FINAL=0 keeps the separate launch (measurement override).
-  {
-    const char *ff = getenv("PHIP_FOLD_FINAL");
-    const bool allow = !(ff && atoi(ff) == 0);
-    P.fin_where = 0;
-    if (allow && !group_by && total_work > 0) {
-      if (need_agg && fused_naggs == 0) P.fin_where = 1;
-      else if (has_filter) P.fin_where = 2;
-    }
-    if (P.fin_where) {
-      void *ctr;
-      rc = P.alloc(16, &ctr);
-      if (rc) return rc;
-      HIP_TRY(hipMemsetAsync(ctr, 0, 16, st));
-      P.fin_counter = (uint32_t *)ctr;
-      DevFinal df;
-      memset(&df, 0, sizeof(df));
-      const bool aggs_here = need_agg && naggs > 0;
-      df.pa = aggs_here ? (const uint64_t *)apart : nullptr;
-      df.nba = fused_naggs > 0 ? filter_blocks : agg_blocks;
-      df.na = aggs_here ? naggs : 0;
-      df.ka = (const int32_t *)(base + kinds_off);
-      df.pf = has_filter ? (const uint64_t *)fpart : nullptr;
-      df.nbf = filter_blocks;
-      df.kf = (const int32_t *)(base + kinds_off) + naggs;
-      df.segm = (uint64_t *)seg_matched;
-      df.nseg = nmatch;
-      df.hll = dq.hll_regs;
-      df.hll_words = nhll ? (nhll << log2m) : 0;
-      df.out = P.pinned_dev;
-      df.counter = P.fin_counter;
-      memcpy(blob.data.data() + fin_off, &df, sizeof(df));
-      const DevFinal *dfin = (const DevFinal *)(base + fin_off);
-      if (P.fin_where == 1) dq.fin = dfin;
-      else fq.fin = dfin;
-    }
-  }
   memcpy(blob.data.data() + dq_off, &dq, sizeof(dq));
   if (nsel > 0) {
     void *sb;
@@ -2389,6 +2336,17 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.first_doc = (uint32_t *)first_doc;
   if (const char *te = getenv("PHIP_TOTAL_EVENTS")) P.total_events = atoi(te) != 0;
   for (auto &e : P.ev) HIP_TRY(hipEventCreate(&e));
+  {
+    void *h = nullptr;
+    const size_t pbytes = (64 + (size_t)nmatch) * 8 + (size_t)std::max(nhll, 1) * (1 << 12) * 4;
+    // device-visible (mapped) pinned memory: finalize_all_kernel writes the results straight into it
+    HIP_TRY(hipHostMalloc(&h, pbytes, hipHostMallocMapped));
+    memset(h, 0, pbytes);
+    P.pinned = (uint64_t *)h;
+    void *dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
+    P.pinned_dev = (uint64_t *)dp;
+  }
   return PHIP_OK;
 }
 
@@ -2419,7 +2377,6 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (!P.clean) {
     HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)P.nmatch * 8, st));
     if (hll_words) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, hll_words * 4, st));
-    if (P.fin_counter) HIP_TRY(hipMemsetAsync(P.fin_counter, 0, 16, st));
   }
   P.clean = false;
   if (filter_words) HIP_TRY(hipMemsetAsync(fo, 0, (size_t)filter_nwords * 8, st));
@@ -2464,7 +2421,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
                                   filter_nwords, st));
   // every result lands in the plan's pinned buffer, written by the device: finals[64] | seg_matched[nmatch] | HLL
-  if (total_work > 0 && P.fin_where == 0) {
+  if (total_work > 0) {
     const bool aggs_here = need_agg && !group_by && naggs > 0;
     HIP_TRY(launch_finalize_all(aggs_here ? (const uint64_t *)apart : nullptr, fused ? filter_blocks : agg_blocks,
                                 aggs_here ? naggs : 0, dev_kinds, has_filter ? (const uint64_t *)fpart : nullptr,
