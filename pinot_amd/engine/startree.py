@@ -19,7 +19,7 @@ import numpy as np
 
 from ..query import predicate as predeval
 from ..query.context import AggregationInfo, FilterContext, Function, Identifier, OrderByExpression, QueryContext
-from ..segment.startree import ALL, pair_column
+from ..segment.startree import ALL, avg_count_column, pair_column
 from .results import AggregationResultsBlock, GroupByResultsBlock
 
 USE_SCAN_TO_TRAVERSE_NODES_THRESHOLD = 10  # StarTreeFilterOperator.java:108
@@ -278,7 +278,7 @@ def _remaining_filter(pmap, columns):
     return kids[0] if len(kids) == 1 else FilterContext.AND(*kids)
 
 
-_STAR_FUNCS = ("sum", "count", "min", "max")
+_STAR_FUNCS = ("sum", "count", "min", "max", "avg")
 
 
 def _pair_of(ag):
@@ -329,17 +329,31 @@ class GpuStarTreeOperator:
         from .plan import GpuCombineOperator
         self.query = query
         self.num_total_docs = sum(seg.num_docs for seg, _, _, _ in chosen)
-        inner_aggs = []
+        # per query function, the star-tree metric(s) it reads: SUM / MIN / MAX of their pair column, COUNT = SUM of
+        # count__*, AVG = SUM of its (sum, count) columns (AvgPair merge)
+        inner_aggs, self.slots = [], []
         for (f, c) in pairs:
-            col = Identifier(pair_column(f, c))
-            inner_aggs.append(AggregationInfo("sum" if f == "count" else f, col))
+            if f == "avg":
+                self.slots.append((len(inner_aggs), len(inner_aggs) + 1))
+                inner_aggs += [AggregationInfo("sum", Identifier(pair_column(f, c))),
+                               AggregationInfo("sum", Identifier(avg_count_column(c)))]
+                continue
+            self.slots.append((len(inner_aggs),))
+            inner_aggs.append(AggregationInfo("sum" if f == "count" else f, Identifier(pair_column(f, c))))
         mapping = {}
-        for ag, a in zip(query.aggregations, inner_aggs):
-            key = Function(ag.function, (ag.argument,) if ag.argument is not None else ())
-            mapping[str(key)] = Function(a.function, (a.argument,))
+        for ag, sl in zip(query.aggregations, self.slots):
+            if len(sl) == 1:
+                a = inner_aggs[sl[0]]
+                key = Function(ag.function, (ag.argument,) if ag.argument is not None else ())
+                mapping[str(key)] = Function(a.function, (a.argument,))
+        # ORDER BY an AVG has no single inner metric: the device trim is skipped and the operator trims its outer
+        # groups on the host (reduce.trim_groups), exactly as the combine's IndexedTable would
+        self.host_trim = any(f == "avg" for f, _ in pairs) and bool(query.order_by)
         order = []
         for ob in query.order_by:
             e = ob.expression
+            if self.host_trim:
+                break
             if str(e) in mapping:
                 order.append(OrderByExpression(mapping[str(e)], ob.ascending))
             elif isinstance(e, Function) and e.name == "count":
@@ -366,8 +380,12 @@ class GpuStarTreeOperator:
 
     def _outer(self, vals):
         out = []
-        for f, v in zip(self.functions, vals):
-            out.append(int(v) if f == "count" else float(v))
+        for f, sl in zip(self.functions, self.slots):
+            if f == "avg":
+                out.append((float(vals[sl[0]]), int(vals[sl[1]])))
+            else:
+                v = vals[sl[0]]
+                out.append(int(v) if f == "count" else float(v))
         return out
 
     def next_block(self):
@@ -382,6 +400,9 @@ class GpuStarTreeOperator:
                                       blk.num_groups_limit_reached)
             out.num_groups_trimmed = getattr(blk, "num_groups_trimmed", False)
             out.key_types = getattr(blk, "key_types", None)
+            if self.host_trim and self.inner.device_trim:
+                from .reduce import trim_groups
+                out = trim_groups(self.query, out)
         for a in ("device_ms", "scan_kernel_ms", "filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes"):
             setattr(out, a, getattr(blk, a, 0))
         out.star_tree = True

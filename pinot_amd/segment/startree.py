@@ -15,8 +15,10 @@ Restates the reference's single-tree builder
 
 STAR is stored as dictionary id 0 in the star-tree forward index (StarTreeV2Constants.STAR_IN_FORWARD_INDEX = 0),
 and ALL (-1) names the star child. Metric columns are named like AggregationFunctionColumnPair.toColumnName
-(``sum__col``, ``count__*``, ``min__col``, ``max__col``) and hold the aggregated values the ValueAggregators
-produce (SUM / MIN / MAX as DOUBLE, COUNT as LONG). The star-tree documents form an ordinary
+(``sum__col``, ``count__*``, ``min__col``, ``max__col``, ``avg__col``) and hold the aggregated values the
+ValueAggregators produce (SUM / MIN / MAX as DOUBLE, COUNT as LONG). AvgValueAggregator's AvgPair (sum, count) is held
+as two numeric columns, ``avg__col`` (the DOUBLE sum) and ``avg__col$count`` (the LONG count), so the GPU sums both
+like any metric instead of decoding serialized pairs. The star-tree documents form an ordinary
 ImmutableSegment (dimension columns share the parent segment's dictionaries), so the GPU loads and scans them with
 the same kernels as any segment.
 """
@@ -31,7 +33,7 @@ STAR_IN_FORWARD_INDEX = 0  # StarTreeV2Constants.java:39
 ALL = -1                   # StarTreeNode.ALL
 DEFAULT_MAX_LEAF_RECORDS = 10_000  # StarTreeV2BuilderConfig.DEFAULT_MAX_LEAF_RECORDS
 
-_PAIR_FUNCS = ("sum", "count", "min", "max")
+_PAIR_FUNCS = ("sum", "count", "min", "max", "avg")
 
 
 @dataclass(frozen=True)
@@ -50,7 +52,7 @@ class StarTreeIndexConfig:
             f, _, c = p.partition("__")
             f = f.lower()
             if f not in _PAIR_FUNCS:
-                raise ValueError(f"star-tree function {f} is outside the GPU subset (SUM/COUNT/MIN/MAX)")
+                raise ValueError(f"star-tree function {f} is outside the GPU subset (SUM/COUNT/MIN/MAX/AVG)")
             if f == "count":
                 c = "*"
             if (f, c) not in out:
@@ -76,6 +78,23 @@ class TreeNode:
 def pair_column(f, c):
     """AggregationFunctionColumnPair.toColumnName."""
     return f"{f}__{c}"
+
+
+def avg_count_column(c):
+    """The count half of an AVG pair's (sum, count) (AvgPair.getCount)."""
+    return f"avg__{c}$count"
+
+
+def metric_slots(pairs):
+    """Per function-column pair, its stored metrics as (column name, aggregation kind): AVG expands to its sum and
+    its count (AvgValueAggregator.applyRawValue: sum += value, count += 1)."""
+    out = []
+    for f, c in pairs:
+        if f == "avg":
+            out += [(pair_column(f, c), "sum", c), (avg_count_column(c), "count", c)]
+        else:
+            out.append((pair_column(f, c), f, c))
+    return out
 
 
 @dataclass
@@ -143,17 +162,18 @@ class _Builder:
         self.dimensions = list(config.dimensions_split_order)
         self.k = len(self.dimensions)
         self.pairs = config.pairs()
-        self.funcs = [f for f, _ in self.pairs]
+        self.slots = metric_slots(self.pairs)
+        self.funcs = [k for _, k, _ in self.slots]
         self.skip = {self.dimensions.index(d) for d in config.skip_star_node_creation}
         self.max_leaf = int(config.max_leaf_records)
         n = len(dims_ids[0]) if dims_ids else 0
         D = np.stack([np.asarray(a, dtype=np.int32) for a in dims_ids], axis=1) if self.k else np.zeros((n, 0), np.int32)
         M = []
-        for f, c in self.pairs:
-            if f == "count":
-                M.append(np.ones(n, dtype=np.int64))     # CountValueAggregator: 1 per raw record
+        for _, k, c in self.slots:
+            if k == "count":
+                M.append(np.ones(n, dtype=np.int64))     # CountValueAggregator / AvgPair count: 1 per raw record
             else:
-                M.append(np.asarray(metric_values[c], dtype=np.float64))  # Sum/Min/Max: doubleValue()
+                M.append(np.asarray(metric_values[c], dtype=np.float64))  # Sum/Min/Max/Avg sum: doubleValue()
         # sortAndAggregateSegmentRecords: sort by the dimensions in split order, merge equal ones
         order = np.lexsort(D.T[::-1]) if self.k else np.arange(n)
         dims, mets = _aggregate_runs(D[order], [m[order] for m in M], self.funcs)
@@ -262,9 +282,8 @@ def build_star_tree(config: StarTreeIndexConfig, dims_ids: Sequence[np.ndarray],
         meta = ColumnMetadata(dim, m.data_type, n, m.cardinality, m.bits_per_element, False, True, False,
                               m.string_width)
         seg.columns[dim] = ColumnIndexes(meta, pack_bits(ids, m.bits_per_element), src.dictionary, None)
-    for (f, c), vals in zip(b.pairs, b.rec.mets):
-        dt = DataType.LONG if f == "count" else DataType.DOUBLE
-        col = pair_column(f, c)
+    for (col, k, _), vals in zip(b.slots, b.rec.mets):
+        dt = DataType.LONG if k == "count" else DataType.DOUBLE
         meta = ColumnMetadata(col, dt, n, 0, 0, False, False, False)
         seg.columns[col] = ColumnIndexes(meta, _chunk_forward(vals[:n], dt))
     return StarTree(config, b.dimensions, root, b.num_nodes, seg, b.pairs)
@@ -409,6 +428,8 @@ def read_pinot_star_trees(index: bytes, index_map: str, metadata: str, parent_co
             seg.columns[d] = ColumnIndexes(meta, bytes(index[o:o + sz]), parent_columns[d].dictionary, None)
         pairs = cfg.pairs()
         for f, c in pairs:
+            if f == "avg":  # AvgValueAggregator writes serialized AvgPair bytes (a var-byte chunk index)
+                raise ValueError(f"star-tree {i}: AVG pairs are serialized AvgPair bytes, not read here")
             col = pair_column(f, c)
             o, sz = entries[(i, col, "FORWARD_INDEX")]
             dt = DataType.LONG if f == "count" else DataType.DOUBLE

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 EXTRA = [
     "SELECT d2, d4, SUM(m2), COUNT(*) FROM t GROUP BY d2, d4 ORDER BY SUM(m2) DESC, d4 LIMIT 5",
     "SELECT d1, d3, MAX(m) FROM t WHERE d2 BETWEEN 'v02' AND 'v08' GROUP BY d1, d3 ORDER BY d3 DESC, d1 LIMIT 7",
+    "SELECT d2, d4, AVG(m), COUNT(*) FROM t GROUP BY d2, d4 ORDER BY AVG(m) DESC, d2, d4 LIMIT 6",  # host trim
 ]
 
 

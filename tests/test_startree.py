@@ -14,7 +14,7 @@ from pinot_amd.segment.creator import SegmentCreator
 from pinot_amd.segment.startree import ALL, STAR_IN_FORWARD_INDEX, StarTreeIndexConfig
 from pinot_amd.spi import DataType
 
-PAIRS = ["SUM__m", "COUNT__*", "MIN__m", "MAX__m", "SUM__m2"]
+PAIRS = ["SUM__m", "COUNT__*", "MIN__m", "MAX__m", "SUM__m2", "AVG__m", "AVG__m2"]
 
 
 def make_segment(seed=3, n=40_000, max_leaf=50, skip=(), name="st"):
@@ -42,6 +42,9 @@ QUERIES = [
     "SELECT SUM(m), COUNT(*) FROM t WHERE d4 <> 7 AND d2 <> 'v02'",       # all children match: star nodes
     "SELECT SUM(m) FROM t WHERE d3 = 1",                                 # always false: no star-tree
     "SELECT d1, d2, d3, d4, COUNT(*) FROM t WHERE d2 = 'v05' GROUP BY d1, d2, d3, d4",
+    # AVG from its (sum, count) pair columns (AvgValueAggregator)
+    "SELECT AVG(m), SUM(m), AVG(m2) FROM t WHERE d1 = 2",
+    "SELECT d2, AVG(m2), COUNT(*) FROM t WHERE d4 < 100 GROUP BY d2",
 ]
 
 
@@ -64,17 +67,25 @@ def _star_answer(qc, seg):
         if rf is not None:
             mask &= executor.eval_filter(os_, rf)
     docs = np.nonzero(mask)[0]
-    inner = []
+    inner, slots = [], []
     for ag in qc.aggregations:
         f, c = st._pair_of(ag)
-        inner.append(AggregationInfo("sum" if f == "count" else f, Identifier(f"{f}__{c}")))
+        if f == "avg":  # the AvgPair halves
+            slots.append((len(inner), len(inner) + 1))
+            inner += [AggregationInfo("sum", Identifier(f"avg__{c}")), AggregationInfo("sum", Identifier(f"avg__{c}$count"))]
+        else:
+            slots.append((len(inner),))
+            inner.append(AggregationInfo("sum" if f == "count" else f, Identifier(f"{f}__{c}")))
+
+    def outer(vals):
+        return [(vals[s[0]], vals[s[1]]) if len(s) == 2 else vals[s[0]] for s in slots]
     if not qc.group_by:
-        return [executor._agg_segment(os_, a, docs)[0] for a in inner], len(docs)
+        return outer([executor._agg_segment(os_, a, docs)[0] for a in inner]), len(docs)
     iq = parse("SELECT COUNT(*) FROM t")
     iq.group_by = list(qc.group_by)
     iq.aggregations = inner
     groups, _, _ = executor._group_segment(os_, iq, docs, None) if len(docs) else ({}, {}, False)
-    return groups, len(docs)
+    return {k: outer(v) for k, v in groups.items()}, len(docs)
 
 
 def _tree_invariants(tree):
@@ -116,12 +127,13 @@ def test_star_tree_equals_scan(max_leaf, skip):
             assert "d3 = 1" in sql  # StarTreeUtils: an always-false predicate keeps the scan path
             continue
         assert ndocs <= tree.docs.num_docs
+        flat = lambda xs: [float(y) for x in xs for y in (x if isinstance(x, tuple) else (x,))]  # noqa: E731
         if not qc.group_by:
-            assert [float(x) for x in got] == [float(x) for x in want.results], sql
+            assert flat(got) == flat(want.results), sql
         else:
             assert set(got) == set(want.groups), sql
             for k, v in want.groups.items():
-                assert [float(x) for x in got[k]] == [float(x) for x in v], (sql, k)
+                assert flat(got[k]) == flat(v), (sql, k)
 
 
 def test_star_tree_fit_rules():
@@ -132,5 +144,6 @@ def test_star_tree_fit_rules():
     pm = st.predicate_map(view, parse("SELECT COUNT(*) FROM t WHERE m > 3").filter)
     assert not set(pm) <= set(seg.star_trees[0].dimensions)  # isFitForStarTree: predicate column not a dimension
     assert st.predicate_map(view, parse("SELECT COUNT(*) FROM t WHERE d1 >= 0").filter) == {}  # always true
-    assert st._pair_of(parse("SELECT AVG(m) FROM t").aggregations[0]) is None
+    assert st._pair_of(parse("SELECT AVG(m) FROM t").aggregations[0]) == ("avg", "m")
+    assert st._pair_of(parse("SELECT DISTINCTCOUNTHLL(m) FROM t").aggregations[0]) is None
     assert st._pair_of(parse("SELECT SUM(m) FILTER(WHERE d1 = 1) FROM t").aggregations[0]) is None
