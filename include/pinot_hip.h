@@ -60,6 +60,8 @@
 /* ---- forward index encodings -------------------------------------------------------------- */
 #define PHIP_FWD_FIXED_BIT 0 /* FixedBitSVForwardIndexWriter: ceil(N*b/8) BE bytes, MSB first */
 #define PHIP_FWD_SORTED 1    /* SortedIndexReaderImpl: card x (start,end) BE int32, inclusive */
+#define PHIP_FWD_HLL_REGISTERS 3 /* per doc 2^bits_per_value u8 HyperLogLog registers (a star-tree DISTINCTCOUNTHLL
+                                  * function-column pair): DISTINCTCOUNTHLL max-merges them; no other use */
 #define PHIP_FWD_RAW_CHUNK 2 /* BaseChunkForwardIndexWriter v2/v3 fixed-width chunks (and v4/v5 power-of-two chunks,
                               * FixedBytePower2ChunkSVForwardIndexReader): PASS_THROUGH, or SNAPPY / LZ4 /
                               * LZ4_LENGTH_PREFIXED / ZSTANDARD / GZIP decoded on the GPU at load (a malformed chunk

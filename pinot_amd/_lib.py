@@ -16,7 +16,7 @@ PHIP_ERR_UNSUPPORTED = 3
 PHIP_ERR_NOT_FOUND = 4
 PHIP_ERR_NO_DEVICE = 5
 
-FWD_FIXED_BIT, FWD_SORTED, FWD_RAW_CHUNK = 0, 1, 2
+FWD_FIXED_BIT, FWD_SORTED, FWD_RAW_CHUNK, FWD_HLL_REGISTERS = 0, 1, 2, 3
 NODE_LEAF, NODE_AND, NODE_OR, NODE_NOT = 0, 1, 2, 3
 LEAF_MATCH_ALL, LEAF_MATCH_NONE, LEAF_DICT_RANGE, LEAF_DICT_SET, LEAF_DOC_RANGES, LEAF_INVERTED, LEAF_RAW_RANGE, \
     LEAF_RAW_SET = range(8)

@@ -91,6 +91,23 @@ __device__ __forceinline__ void lds_hll_max(lds_u32 *words, uint32_t reg, uint32
   }
 }
 
+// HLL register rows (a star-tree DISTINCTCOUNTHLL pair, DevCol.hll_rows): the doc's 2^hll_rows registers, each
+// nonzero one handed to f(register, rho) -- the register-wise max merge of HyperLogLog.merge.
+template <typename F>
+__device__ __forceinline__ void hll_row_each(ccol_t &c, int32_t doc, F &&f) {
+  const int words = (1 << c.hll_rows) >> 2;
+  const PHIP_GLB uint32_t *row = (const PHIP_GLB uint32_t *)c.raw + (int64_t)doc * words;
+  for (int w = 0; w < words; w++) {
+    const uint32_t x = row[w];
+    if (!x) continue;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t rho = (x >> (8 * b)) & 0xffu;
+      if (rho) f(4 * w + b, rho);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // per-chunk work: 64 lanes = up to 64 matched docs of one segment (inactive lanes carry doc 0, a valid
 // doc, so every load stays in bounds, and contribute the identity)
@@ -111,8 +128,13 @@ __device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc,
       acc[a] += act ? (uint64_t)v : 0ull;
     } else if (kind == ACC_HLL) {
       ccol_t &c = seg.cols[ag.col_a];
-      const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
-      if (act) __hip_atomic_fetch_max(&hll_lds[(ag.hll_slot << q.log2m) + (h >> 8)], h & 0xffu, PHIP_RLX, PHIP_WG);
+      lds_u32 *regs = hll_lds + (ag.hll_slot << q.log2m);
+      if (c.hll_rows) {
+        if (act) hll_row_each(c, doc, [&](int r, uint32_t rho) { __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_WG); });
+      } else {
+        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+        if (act) __hip_atomic_fetch_max(&regs[h >> 8], h & 0xffu, PHIP_RLX, PHIP_WG);
+      }
     } else {
       const double v = expr_f64(seg, ag, doc);
       const double cur = as_f64(acc[a]);
@@ -162,8 +184,13 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
       case ACC_MAX_F64: __hip_atomic_fetch_max(slot, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_WG); break;
       case ACC_HLL: {
         ccol_t &c = seg.cols[ag.col_a];
-        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
-        lds_hll_max(hll_packed + ((((int64_t)ag.hll_slot * G + key) << q.log2m) >> 2), h >> 8, h & 0xffu);
+        lds_u32 *regs = hll_packed + ((((int64_t)ag.hll_slot * G + key) << q.log2m) >> 2);
+        if (c.hll_rows) {
+          hll_row_each(c, doc, [&](int r, uint32_t rho) { lds_hll_max(regs, (uint32_t)r, rho); });
+        } else {
+          const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+          lds_hll_max(regs, h >> 8, h & 0xffu);
+        }
         break;
       }
     }

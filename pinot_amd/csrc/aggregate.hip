@@ -46,6 +46,13 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
       batch_expr_i64<U>(seg, ag, d, sa, sb, v);
 #pragma unroll
       for (int u = 0; u < U; u++) acc[a] += ((act >> u) & 1u) ? (uint64_t)v[u] : 0ull;
+    } else if (kind == ACC_HLL && seg.cols[ag.col_a].hll_rows) {
+      ccol_t &c = seg.cols[ag.col_a];
+      lds_u32 *regs = hll_lds + (ag.hll_slot << q.log2m);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if ((act >> u) & 1u)
+          hll_row_each(c, d[u], [&](int r, uint32_t rho) { __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_WG); });
     } else if (kind == ACC_HLL) {
       ccol_t &c = seg.cols[ag.col_a];
       uint32_t id[U];
@@ -155,9 +162,16 @@ __device__ __forceinline__ void group_update_global(cquery_t &q, cseg_t &seg, in
       case ACC_MAX_F64: __hip_atomic_fetch_max(p, f64_ordered(expr_f64(seg, ag, doc)), PHIP_RLX, PHIP_AG); break;
       case ACC_HLL: {
         ccol_t &c = seg.cols[ag.col_a];
-        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
-        glb_u32 *r = (glb_u32 *)q.gb_hll + (((int64_t)ag.hll_slot * G + slot) << q.log2m) + (h >> 8);
-        if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
+        glb_u32 *regs = (glb_u32 *)q.gb_hll + (((int64_t)ag.hll_slot * G + slot) << q.log2m);
+        if (c.hll_rows) {
+          hll_row_each(c, doc, [&](int r, uint32_t rho) {
+            if (regs[r] < rho) __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_AG);
+          });
+        } else {
+          const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+          glb_u32 *r = regs + (h >> 8);
+          if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
+        }
         break;
       }
     }

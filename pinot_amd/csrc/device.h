@@ -78,7 +78,7 @@ struct DevCol {
   int32_t type;      // PHIP_TYPE_*
   int32_t has_dict;  // 1: dictionary-encoded; 0: raw
   int32_t lds_off;   // filter kernel: byte offset of this column's tile region in the stage slot, -1 = not staged
-  int32_t pad;
+  int32_t hll_rows;  // > 0: `raw` holds 2^hll_rows u8 HLL registers per doc (star-tree DISTINCTCOUNTHLL pair)
 };
 
 // One source the filter wave copies into its LDS stage slot for every tile (LDS-DMA, 1 KiB per

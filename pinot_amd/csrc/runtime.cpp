@@ -291,6 +291,7 @@ struct Container {
 struct ColumnStore {
   std::string name;
   int32_t type = 0, fwd_kind = 0, card = 0, bits = 0, string_width = 0;
+  int32_t hll_log2m = 0;      // PHIP_FWD_HLL_REGISTERS: 2^hll_log2m u8 registers per doc in `raw`
   uint32_t *words = nullptr;  // fixed-bit dict ids (also synthesised for sorted columns)
   void *dict = nullptr;       // LE typed dictionary (numeric)
   void *raw = nullptr;        // LE raw values
@@ -304,6 +305,11 @@ struct ColumnStore {
   std::vector<int64_t> inv_begin;  // card+1 into inv_conts
   std::vector<Container> inv_conts;
 };
+// No dictionary: a raw chunk forward index, or the HLL register rows of a star-tree DISTINCTCOUNTHLL pair
+static inline bool no_dict(const ColumnStore &c) {
+  return c.fwd_kind == PHIP_FWD_RAW_CHUNK || c.fwd_kind == PHIP_FWD_HLL_REGISTERS;
+}
+
 
 struct Segment {
   uint64_t handle = 0;
@@ -504,8 +510,22 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
   const int64_t n = seg.num_docs;
   if (c.data_type < PHIP_TYPE_INT || c.data_type > PHIP_TYPE_STRING)
     return fail(PHIP_ERR_INVALID, "column %s: bad data type %d", c.name, c.data_type);
-  const bool dict = c.fwd_kind != PHIP_FWD_RAW_CHUNK;
-  if (dict) {
+  if (c.fwd_kind < PHIP_FWD_FIXED_BIT || c.fwd_kind > PHIP_FWD_HLL_REGISTERS)
+    return fail(PHIP_ERR_INVALID, "column %s: bad forward kind %d", c.name, c.fwd_kind);
+  const bool dict = c.fwd_kind == PHIP_FWD_FIXED_BIT || c.fwd_kind == PHIP_FWD_SORTED;
+  if (c.fwd_kind == PHIP_FWD_HLL_REGISTERS) {
+    // a star-tree DISTINCTCOUNTHLL pair: per doc 2^log2m u8 registers, copied as they are
+    const int lg = c.bits_per_value;
+    if (lg < 4 || lg > 12 || c.forward_bytes != ((uint64_t)n << lg) || (n > 0 && !c.forward))
+      return fail(PHIP_ERR_INVALID, "column %s: HLL registers need num_docs x 2^log2m bytes (log2m %d)", c.name, lg);
+    void *p;
+    int32_t rc = dev_alloc(seg, std::max<uint64_t>(c.forward_bytes, 16), &p);
+    if (rc) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(p, c.forward, c.forward_bytes, hipMemcpyHostToDevice, st));
+    cs.raw = p;
+    cs.hll_log2m = lg;
+    cs.card = 0;
+  } else if (dict) {
     if (c.cardinality <= 0) return fail(PHIP_ERR_INVALID, "column %s: cardinality must be > 0", c.name);
     const int w = c.data_type == PHIP_TYPE_STRING ? c.string_width : type_width(c.data_type);
     if (w <= 0 || c.dictionary == nullptr || c.dictionary_bytes != (uint64_t)w * c.cardinality)
@@ -845,7 +865,7 @@ int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::
   int width = type == PHIP_TYPE_STRING ? c0.string_width : type_width(type);
   for (size_t i = 0; i < segs.size(); i++) {
     const ColumnStore &c = segs[i]->cols[colidx[i]];
-    if (c.fwd_kind == PHIP_FWD_RAW_CHUNK) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s", name.c_str());
+    if (no_dict(c)) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s", name.c_str());
     if (c.type != type) return fail(PHIP_ERR_INVALID, "column %s has different types across segments", name.c_str());
     if (type == PHIP_TYPE_STRING) width = std::max(width, c.string_width);
   }
@@ -1140,12 +1160,21 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         if (!(ca.type == PHIP_TYPE_INT || ca.type == PHIP_TYPE_LONG)) integral = false;
         if (ca.type == PHIP_TYPE_STRING && ag.function != PHIP_AGG_HLL)
           return fail(PHIP_ERR_INVALID, "numeric aggregation over STRING column %s", ca.name.c_str());
+        if (ca.fwd_kind == PHIP_FWD_HLL_REGISTERS) {  // star-tree HLL pair: DISTINCTCOUNTHLL of the column only
+          if (ag.function != PHIP_AGG_HLL || ag.expr != PHIP_EXPR_COLUMN)
+            return fail(PHIP_ERR_INVALID, "HLL register column %s outside DISTINCTCOUNTHLL", ca.name.c_str());
+          if (ag.log2m != ca.hll_log2m)
+            return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL log2m %d over registers of log2m %d", ag.log2m,
+                        ca.hll_log2m);
+        }
         if (ag.function == PHIP_AGG_HLL && ca.fwd_kind == PHIP_FWD_RAW_CHUNK)
           return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over raw column %s", ca.name.c_str());
         if (ag.expr != PHIP_EXPR_COLUMN) {
           const ColumnStore &cb = segs[s]->cols[colidx[s][ag.column_b]];
           if (!(cb.type == PHIP_TYPE_INT || cb.type == PHIP_TYPE_LONG)) integral = false;
           if (cb.type == PHIP_TYPE_STRING) return fail(PHIP_ERR_INVALID, "numeric expression over STRING column");
+          if (cb.fwd_kind == PHIP_FWD_HLL_REGISTERS)
+            return fail(PHIP_ERR_INVALID, "expression over the HLL register column %s", cb.name.c_str());
         }
       }
     }
@@ -1195,7 +1224,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         for (int c : {ag.column_a, ag.expr != PHIP_EXPR_COLUMN ? ag.column_b : -1}) {
           if (c < 0) continue;
           const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-          if (cs.fwd_kind == PHIP_FWD_RAW_CHUNK) continue;
+          if (no_dict(cs)) continue;
           const int64_t w = ag.function == PHIP_AGG_HLL ? 4 : ((cs.type == PHIP_TYPE_LONG || cs.type == PHIP_TYPE_DOUBLE) ? 8 : 4);
           max_dict = std::max<int64_t>(max_dict, (int64_t)cs.card * w);
         }
@@ -1223,7 +1252,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         bool any_dict = false;
         for (int s = 0; s < nseg; s++) {
           const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-          if (cs.fwd_kind == PHIP_FWD_RAW_CHUNK) continue;
+          if (no_dict(cs)) continue;
           any_dict = true;
           bits = std::max(bits, cs.bits);
         }
@@ -1253,7 +1282,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       bool numeric = true;
       for (int s = 0; s < nseg; s++) {
         const ColumnStore &cs = segs[s]->cols[colidx[s][cols[k]]];
-        if (cs.fwd_kind == PHIP_FWD_RAW_CHUNK) continue;
+        if (no_dict(cs)) continue;
         if (cs.type == PHIP_TYPE_STRING) numeric = false;
         const int64_t w = (cs.type == PHIP_TYPE_LONG || cs.type == PHIP_TYPE_DOUBLE) ? 8 : 4;
         bytes = std::max<int64_t>(bytes, (int64_t)cs.card * w);
@@ -1306,6 +1335,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       for (int s = 0; s < nseg; s++) {
         const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
         if (cs.type != t0) return fail(PHIP_ERR_UNSUPPORTED, "selection: column %s changes type across segments", q->columns[c]);
+        if (cs.fwd_kind == PHIP_FWD_HLL_REGISTERS)
+          return fail(PHIP_ERR_INVALID, "selection of the HLL register column %s", q->columns[c]);
         if (cs.type == PHIP_TYPE_STRING && (e.expr != PHIP_EXPR_COLUMN || cs.fwd_kind == PHIP_FWD_RAW_CHUNK))
           return fail(PHIP_ERR_UNSUPPORTED, "selection: STRING column %s outside a dictionary-encoded projection",
                       q->columns[c]);
@@ -1422,12 +1453,14 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dc.bits = cs.bits;
       dc.card = cs.card;
       dc.type = cs.type;
-      dc.has_dict = cs.fwd_kind != PHIP_FWD_RAW_CHUNK;
+      dc.has_dict = !no_dict(cs);
+      dc.hll_rows = cs.hll_log2m;
       dc.lds_off = -1;
     }
     for (int a = 0; a < naggs; a++) {
       if (dq.aggs[a].acc != ACC_HLL) continue;
       ColumnStore &cs = sg.cols[colidx[s][dq.aggs[a].col_a]];
+      if (cs.fwd_kind == PHIP_FWD_HLL_REGISTERS) continue;  // the register rows are the column's raw values
       uint32_t *h;
       int32_t rc = ensure_hll(cs, dq.aggs[a].log2m, &h);
       if (rc) return rc;
@@ -1475,14 +1508,14 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         if (cs) dn.bits = cs->bits;
         switch (fn.leaf_kind) {
           case PHIP_LEAF_DICT_RANGE:
-            if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "dict leaf on raw column"); break; }
+            if (no_dict(*cs)) { rc = fail(PHIP_ERR_INVALID, "dict leaf on raw column"); break; }
             dn.lo = std::max(0, fn.lo);
             dn.hi = std::min(cs->card, fn.hi);
             if (dn.hi <= dn.lo) dn.leaf_kind = PHIP_LEAF_MATCH_NONE;
             else if (dn.lo == 0 && dn.hi == cs->card) dn.leaf_kind = PHIP_LEAF_MATCH_ALL;
             break;
           case PHIP_LEAF_DICT_SET: {
-            if (cs->fwd_kind == PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "dict leaf on raw column"); break; }
+            if (no_dict(*cs)) { rc = fail(PHIP_ERR_INVALID, "dict leaf on raw column"); break; }
             std::vector<uint32_t> bits(ceil_div(cs->card, 32) + 1, 0);
             int32_t n_in = 0, mn = INT32_MAX, mx = -1;
             for (int k = 0; k < fn.count; k++) {
@@ -1542,7 +1575,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
           }
           case PHIP_LEAF_RAW_RANGE:
           case PHIP_LEAF_RAW_SET:
-            if (cs->fwd_kind != PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "raw leaf on dictionary column"); break; }
+            if (cs->fwd_kind != PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "raw leaf on a column without raw values"); break; }
             if (cs->type == PHIP_TYPE_STRING) { rc = fail(PHIP_ERR_UNSUPPORTED, "raw STRING predicate"); break; }
             if (fn.leaf_kind == PHIP_LEAF_RAW_SET) {
               // the kernel binary-searches the values (filter.hip sorted_contains): sorted, distinct, and for
@@ -2006,7 +2039,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     pc.progs = proj_progs[c];
     for (int s = 0; s < nseg; s++) {
       const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-      const bool raw = cs.fwd_kind == PHIP_FWD_RAW_CHUNK;
+      const bool raw = no_dict(cs);
       pc.bits.push_back(raw ? 0 : cs.bits);
       pc.card.push_back(raw ? 0 : cs.card);
       pc.width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));  // STRING: remap / HLL entry
@@ -2223,7 +2256,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       for (int c : {sq.sel[k].col_a, sq.sel[k].expr != PHIP_EXPR_COLUMN ? sq.sel[k].col_b : -1}) {
         if (c < 0) continue;
         const ColumnStore &cs = segs[0]->cols[colidx[0][c]];
-        P.sel_bits.push_back(cs.fwd_kind == PHIP_FWD_RAW_CHUNK ? 0 : cs.bits);
+        P.sel_bits.push_back(no_dict(cs) ? 0 : cs.bits);
         P.sel_width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));
       }
     }

@@ -71,14 +71,20 @@ def hash_values(values, data_type: DataType) -> np.ndarray:
     return _mix_long(arr.astype(np.float64).view(np.int64))
 
 
-def registers_of_hashes(h: np.ndarray, log2m: int) -> np.ndarray:
-    """HyperLogLog.offerHashed over all hashes -> registers (uint8)."""
+def register_rho(h: np.ndarray, log2m: int):
+    """HyperLogLog.offerHashed of each hash: (register index, rho) per hash."""
     h = h.astype(np.uint32)
     j = (h >> np.uint32(32 - log2m)).astype(np.int64)
     w = (h << np.uint32(log2m)) | np.uint32((1 << (log2m - 1)) + 1)
     # rho = number of leading zeros of w (32-bit) + 1
     _, bitlen = np.frexp(w.astype(np.float64))  # exact bit length for w < 2^53
     rho = (32 - bitlen.astype(np.int64)) + 1
+    return j, rho
+
+
+def registers_of_hashes(h: np.ndarray, log2m: int) -> np.ndarray:
+    """HyperLogLog.offerHashed over all hashes -> registers (uint8)."""
+    j, rho = register_rho(h, log2m)
     regs = np.zeros(1 << log2m, dtype=np.uint8)
     np.maximum.at(regs, j, rho.astype(np.uint8))
     return regs

@@ -33,14 +33,16 @@ class GpuSegment:
             keep.append(name)
             d.name = name
             d.data_type = int(m.data_type)
-            if not m.has_dictionary:
+            if getattr(m, "hll_log2m", 0):  # star-tree DISTINCTCOUNTHLL pair: register rows
+                d.fwd_kind = _lib.FWD_HLL_REGISTERS
+            elif not m.has_dictionary:
                 d.fwd_kind = _lib.FWD_RAW_CHUNK
             elif m.is_sorted:
                 d.fwd_kind = _lib.FWD_SORTED
             else:
                 d.fwd_kind = _lib.FWD_FIXED_BIT
             d.cardinality = m.cardinality
-            d.bits_per_value = m.bits_per_element
+            d.bits_per_value = m.hll_log2m if getattr(m, "hll_log2m", 0) else m.bits_per_element
             d.string_width = m.string_width
             for attr, buf in (("forward", ci.forward), ("dictionary", ci.dictionary), ("inverted", ci.inverted)):
                 if buf is None:

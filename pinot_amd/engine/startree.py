@@ -19,7 +19,7 @@ import numpy as np
 
 from ..query import predicate as predeval
 from ..query.context import AggregationInfo, FilterContext, Function, Identifier, OrderByExpression, QueryContext
-from ..segment.startree import ALL, avg_count_column, pair_column
+from ..segment.startree import ALL, STAR_HLL_LOG2M, avg_count_column, pair_column
 from .results import AggregationResultsBlock, GroupByResultsBlock
 
 USE_SCAN_TO_TRAVERSE_NODES_THRESHOLD = 10  # StarTreeFilterOperator.java:108
@@ -278,7 +278,7 @@ def _remaining_filter(pmap, columns):
     return kids[0] if len(kids) == 1 else FilterContext.AND(*kids)
 
 
-_STAR_FUNCS = ("sum", "count", "min", "max", "avg")
+_STAR_FUNCS = ("sum", "count", "min", "max", "avg", "distinctcounthll")
 
 
 def _pair_of(ag):
@@ -288,6 +288,8 @@ def _pair_of(ag):
     if ag.function == "count":
         return ("count", "*")
     if not isinstance(ag.argument, Identifier):
+        return None
+    if ag.function == "distinctcounthll" and ag.log2m != STAR_HLL_LOG2M:  # the pair's HyperLogLog is log2m 8
         return None
     return (ag.function, ag.argument.name)
 
@@ -339,6 +341,9 @@ class GpuStarTreeOperator:
                                AggregationInfo("sum", Identifier(avg_count_column(c)))]
                 continue
             self.slots.append((len(inner_aggs),))
+            if f == "distinctcounthll":  # max-merge of the documents' register rows
+                inner_aggs.append(AggregationInfo(f, Identifier(pair_column(f, c)), STAR_HLL_LOG2M))
+                continue
             inner_aggs.append(AggregationInfo("sum" if f == "count" else f, Identifier(pair_column(f, c))))
         mapping = {}
         for ag, sl in zip(query.aggregations, self.slots):
@@ -383,6 +388,8 @@ class GpuStarTreeOperator:
         for f, sl in zip(self.functions, self.slots):
             if f == "avg":
                 out.append((float(vals[sl[0]]), int(vals[sl[1]])))
+            elif f == "distinctcounthll":
+                out.append(vals[sl[0]])
             else:
                 v = vals[sl[0]]
                 out.append(int(v) if f == "count" else float(v))

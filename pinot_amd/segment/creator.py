@@ -94,6 +94,7 @@ class ColumnMetadata:
     has_dictionary: bool
     has_inverted_index: bool
     string_width: int = 0  # bytes per padded STRING dictionary entry
+    hll_log2m: int = 0     # > 0: a star-tree DISTINCTCOUNTHLL pair column -- per doc 2^log2m u8 HLL registers
 
 
 @dataclass
@@ -259,7 +260,8 @@ class SegmentCreator:
                     if d not in self._ids:
                         raise ValueError(f"star-tree dimension {d} must be a dictionary-encoded column")
                 seg.star_trees.append(build_star_tree(cfg, [self._ids[d] for d in dims], [seg.columns[d] for d in dims],
-                                                      raw, f"{self.name}.startree{i}"))
+                                                      raw, f"{self.name}.startree{i}",
+                                                      {name: dt for name, dt, _ in self._cols}))
         return seg
 
     def _build_column(self, name, dt, vals, n) -> ColumnIndexes:

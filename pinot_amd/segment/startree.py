@@ -18,7 +18,10 @@ and ALL (-1) names the star child. Metric columns are named like AggregationFunc
 (``sum__col``, ``count__*``, ``min__col``, ``max__col``, ``avg__col``) and hold the aggregated values the
 ValueAggregators produce (SUM / MIN / MAX as DOUBLE, COUNT as LONG). AvgValueAggregator's AvgPair (sum, count) is held
 as two numeric columns, ``avg__col`` (the DOUBLE sum) and ``avg__col$count`` (the LONG count), so the GPU sums both
-like any metric instead of decoding serialized pairs. The star-tree documents form an ordinary
+like any metric instead of decoding serialized pairs. DistinctCountHLLValueAggregator's HyperLogLog (log2m 8, the
+default) is held as its registers: ``distinctcounthll__col`` stores 256 u8 registers per star-tree document (the
+register-wise max of its raw documents' (register, rho) offers), which the GPU max-merges per matched document
+(PHIP_FWD_HLL_REGISTERS) instead of deserializing clearspring HyperLogLog bytes. The star-tree documents form an ordinary
 ImmutableSegment (dimension columns share the parent segment's dictionaries), so the GPU loads and scans them with
 the same kernels as any segment.
 """
@@ -33,7 +36,8 @@ STAR_IN_FORWARD_INDEX = 0  # StarTreeV2Constants.java:39
 ALL = -1                   # StarTreeNode.ALL
 DEFAULT_MAX_LEAF_RECORDS = 10_000  # StarTreeV2BuilderConfig.DEFAULT_MAX_LEAF_RECORDS
 
-_PAIR_FUNCS = ("sum", "count", "min", "max", "avg")
+_PAIR_FUNCS = ("sum", "count", "min", "max", "avg", "distinctcounthll")
+STAR_HLL_LOG2M = 8  # DistinctCountHLLValueAggregator: HyperLogLog(log2m = 8) unless configured
 
 
 @dataclass(frozen=True)
@@ -52,7 +56,8 @@ class StarTreeIndexConfig:
             f, _, c = p.partition("__")
             f = f.lower()
             if f not in _PAIR_FUNCS:
-                raise ValueError(f"star-tree function {f} is outside the GPU subset (SUM/COUNT/MIN/MAX/AVG)")
+                raise ValueError(f"star-tree function {f} is outside the GPU subset (SUM/COUNT/MIN/MAX/AVG/"
+                                 f"DISTINCTCOUNTHLL)")
             if f == "count":
                 c = "*"
             if (f, c) not in out:
@@ -92,6 +97,8 @@ def metric_slots(pairs):
     for f, c in pairs:
         if f == "avg":
             out += [(pair_column(f, c), "sum", c), (avg_count_column(c), "count", c)]
+        elif f == "distinctcounthll":
+            out.append((pair_column(f, c), "hll", c))
         else:
             out.append((pair_column(f, c), f, c))
     return out
@@ -117,7 +124,9 @@ class _Records:
         self.k = k
         self.n = 0
         self.dims = np.zeros((cap, k), dtype=np.int32)
-        self.mets = [np.zeros(cap, dtype=dt) for dt in metric_dtypes]
+        # metric_dtypes: a dtype, or (dtype, row width) for register rows
+        self.mets = [np.zeros((cap, dt[1]), dtype=dt[0]) if isinstance(dt, tuple) else np.zeros(cap, dtype=dt)
+                     for dt in metric_dtypes]
 
     def append(self, dims, mets):
         m = len(dims)
@@ -127,7 +136,7 @@ class _Records:
             nd[:self.n] = self.dims[:self.n]
             self.dims = nd
             for i, a in enumerate(self.mets):
-                na = np.zeros(cap, dtype=a.dtype)
+                na = np.zeros((cap,) + a.shape[1:], dtype=a.dtype)
                 na[:self.n] = a[:self.n]
                 self.mets[i] = na
         self.dims[self.n:self.n + m] = dims
@@ -138,7 +147,8 @@ class _Records:
 
 def _aggregate_runs(dims, mets, funcs):
     """Sorted records -> one record per run of equal dimensions, metrics merged in record order
-    (ValueAggregator.applyAggregatedValue: SUM/COUNT add, MIN/MAX compare)."""
+    (ValueAggregator.applyAggregatedValue: SUM/COUNT add, MIN/MAX compare, HLL register-wise max; raw HLL records
+    arrive as packed (register << 8 | rho) offers and leave as register rows)."""
     n = len(dims)
     if n == 0:
         return dims, mets
@@ -151,13 +161,19 @@ def _aggregate_runs(dims, mets, funcs):
             out.append(np.add.reduceat(v, starts))
         elif f == "min":
             out.append(np.minimum.reduceat(v, starts))
+        elif f == "hll" and v.ndim == 1:  # raw offers -> one register row per run
+            run = np.cumsum(change) - 1
+            rows = np.zeros((len(starts), 1 << STAR_HLL_LOG2M), dtype=np.uint8)
+            np.maximum.at(rows, (run, (v >> 8).astype(np.int64)), (v & 0xFF).astype(np.uint8))
+            out.append(rows)
         else:
-            out.append(np.maximum.reduceat(v, starts))
+            out.append(np.maximum.reduceat(v, starts, axis=0))
     return dims[starts], out
 
 
 class _Builder:
-    def __init__(self, config, dims_ids, metric_values):
+    def __init__(self, config, dims_ids, metric_values, metric_types=None):
+        metric_types = metric_types or {}
         self.cfg = config
         self.dimensions = list(config.dimensions_split_order)
         self.k = len(self.dimensions)
@@ -172,12 +188,21 @@ class _Builder:
         for _, k, c in self.slots:
             if k == "count":
                 M.append(np.ones(n, dtype=np.int64))     # CountValueAggregator / AvgPair count: 1 per raw record
+            elif k == "hll":  # DistinctCountHLLValueAggregator.getInitialAggregatedValue: offer the raw value
+                from ..engine.hll import hash_values, register_rho
+                from ..spi import DataType as _DT
+                vals = metric_values[c]
+                dt = _DT.STRING if (len(vals) and isinstance(vals[0], str)) else (
+                    _DT.LONG if np.asarray(vals).dtype.kind in "iu" else _DT.DOUBLE)
+                j, rho = register_rho(hash_values(vals, metric_types.get(c, dt)), STAR_HLL_LOG2M)
+                M.append((j << 8 | rho).astype(np.int32))
             else:
                 M.append(np.asarray(metric_values[c], dtype=np.float64))  # Sum/Min/Max/Avg sum: doubleValue()
         # sortAndAggregateSegmentRecords: sort by the dimensions in split order, merge equal ones
         order = np.lexsort(D.T[::-1]) if self.k else np.arange(n)
         dims, mets = _aggregate_runs(D[order], [m[order] for m in M], self.funcs)
-        self.rec = _Records(self.k, [m.dtype for m in M], cap=max(2 * len(dims), 16))
+        self.rec = _Records(self.k, [(m.dtype, m.shape[1]) if m.ndim == 2 else m.dtype for m in mets],
+                            cap=max(2 * len(dims), 16))
         self.rec.append(dims, mets)
         self.num_nodes = 1
         self.root = TreeNode(start_doc=0, end_doc=self.rec.n)
@@ -227,21 +252,21 @@ class _Builder:
         mets = []
         for f, m in zip(self.funcs, self.rec.mets):
             seg = m[start:end]
-            mets.append(seg.sum() if f in ("sum", "count") else (seg.min() if f == "min" else seg.max()))
+            mets.append(seg.sum() if f in ("sum", "count") else (seg.min() if f == "min" else seg.max(axis=0)))
         return dims, mets
 
     def _append_aggregated(self, node, dims, mets):
         dims = dims.copy()
         dims[node.dimension_id + 1:] = STAR_IN_FORWARD_INDEX
         node.aggregated_doc = self.rec.n
-        self.rec.append(dims[None, :], [np.asarray([v]) for v in mets])
+        self.rec.append(dims[None, :], [np.asarray(v)[None] for v in mets])
 
     def _aggregated_docs(self, node):
         """createAggregatedDocs (BaseSingleTreeBuilder.java:414-455); returns the node's aggregated record."""
         if node.children is None:
             if node.start_doc == node.end_doc - 1:
                 node.aggregated_doc = node.start_doc
-                return self.rec.dims[node.start_doc].copy(), [m[node.start_doc] for m in self.rec.mets]
+                return self.rec.dims[node.start_doc].copy(), [m[node.start_doc].copy() for m in self.rec.mets]
             dims, mets = self._merge_range(node.start_doc, node.end_doc)
             self._append_aggregated(node, dims, mets)
             return dims, mets
@@ -259,19 +284,20 @@ class _Builder:
             if acc_d is None:
                 acc_d, acc_m = d.copy(), list(m)
             else:
-                acc_m = [(a + b) if f in ("sum", "count") else (min(a, b) if f == "min" else max(a, b))
+                acc_m = [(a + b) if f in ("sum", "count") else
+                         (min(a, b) if f == "min" else (np.maximum(a, b) if f == "hll" else max(a, b)))
                          for f, a, b in zip(self.funcs, acc_m, m)]
         self._append_aggregated(node, acc_d, acc_m)
         return acc_d, acc_m
 
 
 def build_star_tree(config: StarTreeIndexConfig, dims_ids: Sequence[np.ndarray], dim_columns, metric_values,
-                    name: str) -> StarTree:
+                    name: str, metric_types=None) -> StarTree:
     """Builds one star-tree over a segment: ``dims_ids`` = the dict ids of every split-order dimension,
     ``dim_columns`` = their ColumnIndexes (dictionaries and metadata are shared with the star-tree docs),
     ``metric_values`` = column -> raw values for the SUM / MIN / MAX pairs."""
     from .creator import ColumnIndexes, ColumnMetadata, ImmutableSegment, _chunk_forward, pack_bits
-    b = _Builder(config, dims_ids, metric_values)
+    b = _Builder(config, dims_ids, metric_values, metric_types or {})
     root = b.build()
     n = b.rec.n
     seg = ImmutableSegment(name, n)
@@ -283,6 +309,10 @@ def build_star_tree(config: StarTreeIndexConfig, dims_ids: Sequence[np.ndarray],
                               m.string_width)
         seg.columns[dim] = ColumnIndexes(meta, pack_bits(ids, m.bits_per_element), src.dictionary, None)
     for (col, k, _), vals in zip(b.slots, b.rec.mets):
+        if k == "hll":  # register rows, 2^log2m bytes per star-tree document
+            meta = ColumnMetadata(col, DataType.LONG, n, 0, 0, False, False, False, 0, STAR_HLL_LOG2M)
+            seg.columns[col] = ColumnIndexes(meta, np.ascontiguousarray(vals[:n], dtype=np.uint8).tobytes())
+            continue
         dt = DataType.LONG if k == "count" else DataType.DOUBLE
         meta = ColumnMetadata(col, dt, n, 0, 0, False, False, False)
         seg.columns[col] = ColumnIndexes(meta, _chunk_forward(vals[:n], dt))
@@ -428,8 +458,8 @@ def read_pinot_star_trees(index: bytes, index_map: str, metadata: str, parent_co
             seg.columns[d] = ColumnIndexes(meta, bytes(index[o:o + sz]), parent_columns[d].dictionary, None)
         pairs = cfg.pairs()
         for f, c in pairs:
-            if f == "avg":  # AvgValueAggregator writes serialized AvgPair bytes (a var-byte chunk index)
-                raise ValueError(f"star-tree {i}: AVG pairs are serialized AvgPair bytes, not read here")
+            if f in ("avg", "distinctcounthll"):  # serialized AvgPair / HyperLogLog bytes (var-byte chunk indexes)
+                raise ValueError(f"star-tree {i}: {f.upper()} pairs are serialized objects, not read here")
             col = pair_column(f, c)
             o, sz = entries[(i, col, "FORWARD_INDEX")]
             dt = DataType.LONG if f == "count" else DataType.DOUBLE

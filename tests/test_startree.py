@@ -14,7 +14,8 @@ from pinot_amd.segment.creator import SegmentCreator
 from pinot_amd.segment.startree import ALL, STAR_IN_FORWARD_INDEX, StarTreeIndexConfig
 from pinot_amd.spi import DataType
 
-PAIRS = ["SUM__m", "COUNT__*", "MIN__m", "MAX__m", "SUM__m2", "AVG__m", "AVG__m2"]
+PAIRS = ["SUM__m", "COUNT__*", "MIN__m", "MAX__m", "SUM__m2", "AVG__m", "AVG__m2", "DISTINCTCOUNTHLL__m",
+         "DISTINCTCOUNTHLL__d2"]
 
 
 def make_segment(seed=3, n=40_000, max_leaf=50, skip=(), name="st"):
@@ -45,6 +46,9 @@ QUERIES = [
     # AVG from its (sum, count) pair columns (AvgValueAggregator)
     "SELECT AVG(m), SUM(m), AVG(m2) FROM t WHERE d1 = 2",
     "SELECT d2, AVG(m2), COUNT(*) FROM t WHERE d4 < 100 GROUP BY d2",
+    # DISTINCTCOUNTHLL from the register rows (DistinctCountHLLValueAggregator): registers equal the scan's exactly
+    "SELECT DISTINCTCOUNTHLL(m), DISTINCTCOUNTHLL(d2), COUNT(*) FROM t WHERE d3 BETWEEN 30 AND 90",
+    "SELECT d1, DISTINCTCOUNTHLL(m), SUM(m) FROM t WHERE d2 <> 'v04' GROUP BY d1",
 ]
 
 
@@ -70,6 +74,9 @@ def _star_answer(qc, seg):
     inner, slots = [], []
     for ag in qc.aggregations:
         f, c = st._pair_of(ag)
+        if f == "distinctcounthll":  # register rows: max over the matched star-tree documents
+            slots.append(("hll", f"distinctcounthll__{c}"))
+            continue
         if f == "avg":  # the AvgPair halves
             slots.append((len(inner), len(inner) + 1))
             inner += [AggregationInfo("sum", Identifier(f"avg__{c}")), AggregationInfo("sum", Identifier(f"avg__{c}$count"))]
@@ -77,15 +84,29 @@ def _star_answer(qc, seg):
             slots.append((len(inner),))
             inner.append(AggregationInfo("sum" if f == "count" else f, Identifier(f"{f}__{c}")))
 
-    def outer(vals):
-        return [(vals[s[0]], vals[s[1]]) if len(s) == 2 else vals[s[0]] for s in slots]
+    def rows(col):
+        return np.frombuffer(tree.docs.columns[col].forward, dtype=np.uint8).reshape(tree.docs.num_docs, -1)
+
+    def outer(vals, sel):
+        out = []
+        for s in slots:
+            if s[0] == "hll":
+                r = rows(s[1])[sel]
+                out.append(r.max(axis=0) if len(r) else np.zeros(r.shape[1], np.uint8))
+            else:
+                out.append((vals[s[0]], vals[s[1]]) if len(s) == 2 else vals[s[0]])
+        return out
     if not qc.group_by:
-        return outer([executor._agg_segment(os_, a, docs)[0] for a in inner]), len(docs)
+        return outer([executor._agg_segment(os_, a, docs)[0] for a in inner], docs), len(docs)
     iq = parse("SELECT COUNT(*) FROM t")
     iq.group_by = list(qc.group_by)
-    iq.aggregations = inner
+    iq.aggregations = inner or [AggregationInfo("count", None)]
     groups, _, _ = executor._group_segment(os_, iq, docs, None) if len(docs) else ({}, {}, False)
-    return {k: outer(v) for k, v in groups.items()}, len(docs)
+    gkey = [tuple(k) for k in zip(*[os_.values(e.name)[docs] for e in qc.group_by])]
+    members = {}
+    for i, k in enumerate(gkey):
+        members.setdefault(tuple(x.item() if hasattr(x, "item") else x for x in k), []).append(docs[i])
+    return {k: outer(v, np.asarray(members[k], dtype=np.int64)) for k, v in groups.items()}, len(docs)
 
 
 def _tree_invariants(tree):
@@ -127,7 +148,7 @@ def test_star_tree_equals_scan(max_leaf, skip):
             assert "d3 = 1" in sql  # StarTreeUtils: an always-false predicate keeps the scan path
             continue
         assert ndocs <= tree.docs.num_docs
-        flat = lambda xs: [float(y) for x in xs for y in (x if isinstance(x, tuple) else (x,))]  # noqa: E731
+        flat = lambda xs: [float(y) for x in xs for y in (x if isinstance(x, (tuple, np.ndarray)) else (x,))]  # noqa: E731
         if not qc.group_by:
             assert flat(got) == flat(want.results), sql
         else:
@@ -145,5 +166,6 @@ def test_star_tree_fit_rules():
     assert not set(pm) <= set(seg.star_trees[0].dimensions)  # isFitForStarTree: predicate column not a dimension
     assert st.predicate_map(view, parse("SELECT COUNT(*) FROM t WHERE d1 >= 0").filter) == {}  # always true
     assert st._pair_of(parse("SELECT AVG(m) FROM t").aggregations[0]) == ("avg", "m")
-    assert st._pair_of(parse("SELECT DISTINCTCOUNTHLL(m) FROM t").aggregations[0]) is None
+    assert st._pair_of(parse("SELECT DISTINCTCOUNTHLL(m) FROM t").aggregations[0]) == ("distinctcounthll", "m")
+    assert st._pair_of(parse("SELECT DISTINCTCOUNTHLL(m, 10) FROM t").aggregations[0]) is None  # log2m 8 pairs only
     assert st._pair_of(parse("SELECT SUM(m) FILTER(WHERE d1 = 1) FROM t").aggregations[0]) is None
