@@ -27,11 +27,15 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Bits [off, off+bits) of the MSB-first stream held in words (u32, bit 31 first).
+// Bits [off, off+bits) of the MSB-first stream held in words (u32, bit 31 first). The two words of the window come
+// in ONE dword-aligned global_load_dwordx2 (one L2 request unless it straddles a line; two dword loads were two
+// requests per doc on the sparse gathers of the aggregation walks).
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ uint32_t decode_bits(const uint32_t *words_generic, uint64_t off, uint32_t bits) {
   // streamed once: non-temporal, so the words do not evict the dictionaries the gathers re-read
-  const PHIP_GLB uint32_t *p = (const PHIP_GLB uint32_t *)words_generic + (off >> 5);
-  const uint64_t win = ((uint64_t)__builtin_nontemporal_load(p) << 32) | (uint64_t)__builtin_nontemporal_load(p + 1);
+  const PHIP_GLB u32x2_a4 *p = (const PHIP_GLB u32x2_a4 *)((const PHIP_GLB uint32_t *)words_generic + (off >> 5));
+  const u32x2_a4 v = __builtin_nontemporal_load(p);
+  const uint64_t win = ((uint64_t)v.x << 32) | (uint64_t)v.y;
   return (uint32_t)((win << (off & 31)) >> (64 - bits));
 }
 

@@ -96,6 +96,7 @@ struct StageSrc {
 #endif
 constexpr int kMaxConj = PHIP_MAX_CONJ;
 constexpr int kConjSparseMax = 6;     // default per-lane bound of the sparse conjunction walk
+constexpr double kConjSparseSel = 1.0 / 16;  // ... taken only when the first leaf's selectivity is at most this
 struct ConjLeaf {
   int32_t lds_off;  // staged region in the ring slot
   int32_t bits;

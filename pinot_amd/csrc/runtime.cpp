@@ -1908,6 +1908,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       ds.conj = (int32_t)conj.size();
       ds.conj_sparse = 1;
       for (size_t i = 1; i < conj.size(); i++) ds.conj_sparse &= conj[i].second.kind == 0 ? 1 : 0;
+      // the per-doc walk pays when the first leaf leaves ~2 docs per lane; at a selectivity of 1/7 (unsorted SSB
+      // Q1.1's D_YEAR) tiles often pass the per-tile bound yet the walk is slower than the dense leaves (filter kernel
+      // 0.32 -> 0.30 ms without it, profiles/r03f_unsorted_filter_knobs_ab.log), so it needs a selective first leaf
+      if (conj.empty() || conj[0].first > kConjSparseSel) ds.conj_sparse = 0;
       if (getenv("PHIP_NO_SPARSE")) ds.conj_sparse = 0;  // measurement override
       // the value is the per-lane passing-doc bound under which the sparse walk is taken
       if (ds.conj_sparse) {
