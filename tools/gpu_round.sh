@@ -30,6 +30,12 @@ for L in sorted unsorted; do
   step pmcw_$L 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
 done
 step pmcsq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmcsq_$TAG -o run -- python3 -u bench.py $B --layout unsorted
+# the headline's dominant kernel (sorted Q1.1's aggregation): instruction mix, waits, L2 hits / misses
+B1="--no-cpu-baseline --steps 5 --warmup 2 --layout sorted --queries Q1.1"
+step pmcq11sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU --output-format csv -d gpurun_out/pmcq11sq_$TAG -o run -- python3 -u bench.py $B1
+step pmcq11tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/pmcq11tcc_$TAG -o run -- python3 -u bench.py $B1
+python3 tools/pmc_summary.py gpurun_out/pmcq11sq_$TAG > gpurun_out/pmcq11sq_$TAG.txt 2>&1 || true
+python3 tools/pmc_summary.py gpurun_out/pmcq11tcc_$TAG > gpurun_out/pmcq11tcc_$TAG.txt 2>&1 || true
 python3 tools/traffic.py --layout sorted gpurun_out/pmcf_${TAG}_sorted gpurun_out/pmcw_${TAG}_sorted \
   --layout unsorted gpurun_out/pmcf_${TAG}_unsorted gpurun_out/pmcw_${TAG}_unsorted \
   --queries Q1.1,Q1.2,Q1.3 --sf 100 -o gpurun_out/traffic_$TAG.json
