@@ -115,6 +115,12 @@ typedef struct phip_segment_desc {
  * FLOAT/DOUBLE columns -- (RAW_SET, xor exclusive). */
 #define PHIP_LEAF_RAW_RANGE 6
 #define PHIP_LEAF_RAW_SET 7
+/* Raw STRING columns (var-byte chunks): the values compared in String.compareTo order. ids points at `count` int32
+ * words: RAW_STRING_RANGE = [lo_len][hi_len][lo_inclusive][hi_inclusive][lo UTF-8 bytes][hi UTF-8 bytes], a length
+ * of -1 = unbounded (StringRawValueBasedRangePredicateEvaluator, RangePredicateEvaluatorFactory.java); RAW_STRING_SET
+ * = [n][n + 1 byte offsets][the n values' UTF-8 bytes] (raw EQ / NOT_EQ / IN / NOT_IN, xor exclusive). */
+#define PHIP_LEAF_RAW_STRING_RANGE 8
+#define PHIP_LEAF_RAW_STRING_SET 9
 
 typedef struct phip_raw_range {
   int64_t lo_int, hi_int; /* INT/LONG columns: lo_int <= v <= hi_int */
@@ -200,7 +206,11 @@ typedef struct phip_query_desc {
    * every row holds the select expressions (phip_result.select_*). Statistics: numDocsScanned = the rows each
    * segment kept, numEntriesScannedPostFilter = that x the distinct columns the expressions read. */
   int32_t num_select;
-  int32_t reserved1;
+  /* Programs whose filter scans count in num_entries_scanned_in_filter: bit p = program p; 0 = every program.
+   * A CASE aggregation's branch programs re-evaluate the query's filter AND a WHEN condition, while the
+   * reference scans each original filter once (CaseTransformFunction evaluates the WHENs in the transform,
+   * pinot-core/.../transform/function/CaseTransformFunction.java): only those programs count. */
+  uint32_t stats_programs;
   const struct phip_select_expr *select;
   int64_t select_limit;
 } phip_query_desc;

@@ -79,6 +79,8 @@ class OracleSegment:
             m = ci.metadata
             if m.has_dictionary:
                 v = self.dictionary(c)[self.dict_ids(c)]
+            elif int(m.data_type) == 4:
+                v = _read_var_byte_chunk(ci.forward, self.num_docs)
             else:
                 v = _read_raw_chunk(ci.forward, int(m.data_type), self.num_docs)
             self._vals[c] = v
@@ -144,6 +146,67 @@ def _read_raw_chunk(buf, dtype, n):
     return np.concatenate(parts).astype(_NATIVE[dtype]) if parts else np.zeros(0, _NATIVE[dtype])
 
 
+def _zstd_content_size(body: bytes) -> int:
+    """Frame_Content_Size of a zstd frame (RFC 8878 §3.1.1.1): zstd-jni writes it, and the decoder sizes its output
+    with it."""
+    fhd = body[4]
+    fcs_flag, single, did_flag = fhd >> 6, (fhd >> 5) & 1, fhd & 3
+    p = 5 + (0 if single else 1) + (0, 1, 2, 4)[did_flag]
+    size = (1 if single else 0, 2, 4, 8)[fcs_flag]
+    if size == 0:
+        raise ValueError("zstd frame without a content size")
+    v = int.from_bytes(body[p:p + size], "little")
+    return v + 256 if size == 2 else v
+
+
+def _read_var_byte_chunk(buf, n):
+    """VarByteChunkSVForwardIndexReader (pinot-segment-local/.../readers/forward/VarByteChunkSVForwardIndexReader.java
+    :80-112,176-217) over v1..v3 var-byte chunks: chunk k spans [offset_k, offset_{k+1}) (the last to the end of the
+    buffer) and decodes to numDocsPerChunk BE int start offsets + the values' UTF-8 bytes; a row ends where the next
+    row starts, or at the chunk's end for its last row and for the last row of a partial chunk (absent rows hold 0)."""
+    version, num_chunks, per_chunk, longest = [int(x) for x in np.frombuffer(buf, ">i4", 4)]
+    if version > 1:
+        total, comp, data_hdr = [int(x) for x in np.frombuffer(buf, ">i4", 3, offset=16)]
+    else:  # v1: 4-int header, SNAPPY chunks, offsets from byte 16 (BaseChunkForwardIndexReader.java:86-95)
+        total, comp, data_hdr = n, 1, 16
+    assert version in (1, 2, 3) and total == n and comp in (0, 1, 2, 3, 4, 5), (version, total, comp)
+    offs = np.frombuffer(buf, dtype=">i4" if version <= 2 else ">i8", count=num_chunks, offset=data_hdr)
+    raw = np.frombuffer(buf, dtype=np.uint8)
+    cap = per_chunk * (4 + longest)
+    out = []
+    for k in range(num_chunks):
+        end = int(offs[k + 1]) if k + 1 < num_chunks else len(buf)
+        body = bytes(buf[int(offs[k]):end])
+        if comp == 0:
+            chunk = body
+        elif comp == 5:
+            import zlib
+            chunk = zlib.decompress(body[:-4])
+            assert len(chunk) == int.from_bytes(body[-4:], "big")
+        elif comp == 2:
+            import pyarrow as pa
+            chunk = pa.Codec("zstd").decompress(body, decompressed_size=_zstd_content_size(body), asbytes=True)
+        else:
+            src = np.frombuffer(body, dtype=np.uint8)
+            dst = np.empty(max(cap, 1), dtype=np.uint8)
+            got = _oracle_lib().oracle_chunk_decode(comp, src.ctypes.data, len(src), dst.ctypes.data, cap)
+            assert got >= 0, f"chunk {k}: malformed (type {comp})"
+            chunk = dst[:got].tobytes()
+        starts = np.frombuffer(chunk, dtype=">i4", count=per_chunk)
+        for r in range(min(per_chunk, n - k * per_chunk)):
+            s = int(starts[r])
+            e = int(starts[r + 1]) if r + 1 < per_chunk else 0
+            if e == 0:
+                e = len(chunk)
+            out.append(chunk[s:e].decode("utf-8"))
+    return np.array(out, dtype=object)
+
+
+def java_string_key(s: str) -> bytes:
+    """String.compareTo order: UTF-16 code units (surrogate pairs sort below U+E000..U+FFFF)."""
+    return s.encode("utf-16-be", "surrogatepass")
+
+
 # ----------------------------------------------------------------------------------- filter
 def _literal(m, lit):
     """Literal converted to the column type (the reference parses predicate values per data type)."""
@@ -156,6 +219,17 @@ def _literal(m, lit):
 
 def _pred_on_values(pred, vals, m):
     t = pred.type
+    if int(m.data_type) == 4 and not m.has_dictionary and t == "RANGE":
+        # raw STRING: StringRawValueBasedRangePredicateEvaluator compares with String.compareTo
+        keys = [java_string_key(v) for v in vals]
+        ok = np.ones(len(vals), dtype=bool)
+        if pred.lower != "*":
+            lo = java_string_key(str(pred.lower))
+            ok &= np.array([(k >= lo) if pred.lower_inclusive else (k > lo) for k in keys], dtype=bool)
+        if pred.upper != "*":
+            hi = java_string_key(str(pred.upper))
+            ok &= np.array([(k <= hi) if pred.upper_inclusive else (k < hi) for k in keys], dtype=bool)
+        return ok
     if t in ("EQ", "NOT_EQ", "IN", "NOT_IN"):
         lits = [_literal(m, v) for v in pred.values]
         hit = np.zeros(len(vals), dtype=bool)

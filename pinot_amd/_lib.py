@@ -19,7 +19,7 @@ PHIP_ERR_NO_DEVICE = 5
 FWD_FIXED_BIT, FWD_SORTED, FWD_RAW_CHUNK, FWD_HLL_REGISTERS = 0, 1, 2, 3
 NODE_LEAF, NODE_AND, NODE_OR, NODE_NOT = 0, 1, 2, 3
 LEAF_MATCH_ALL, LEAF_MATCH_NONE, LEAF_DICT_RANGE, LEAF_DICT_SET, LEAF_DOC_RANGES, LEAF_INVERTED, LEAF_RAW_RANGE, \
-    LEAF_RAW_SET = range(8)
+    LEAF_RAW_SET, LEAF_RAW_STRING_RANGE, LEAF_RAW_STRING_SET = range(10)
 
 
 class RawRange(ctypes.Structure):
@@ -93,7 +93,7 @@ class QueryDesc(ctypes.Structure):
                 ("order_by_keys", ctypes.POINTER(ctypes.c_int32)),
                 ("num_order_terms", ctypes.c_int32), ("num_filter_programs", ctypes.c_int32),
                 ("order_terms", ctypes.POINTER(OrderTerm)),
-                ("num_select", ctypes.c_int32), ("reserved1", ctypes.c_int32),
+                ("num_select", ctypes.c_int32), ("stats_programs", ctypes.c_uint32),
                 ("select", ctypes.POINTER(SelectExpr)), ("select_limit", ctypes.c_int64)]
 
 

@@ -79,6 +79,7 @@ struct DevCol {
   int32_t has_dict;  // 1: dictionary-encoded; 0: raw
   int32_t lds_off;   // filter kernel: byte offset of this column's tile region in the stage slot, -1 = not staged
   int32_t hll_rows;  // > 0: `raw` holds 2^hll_rows u8 HLL registers per doc (star-tree DISTINCTCOUNTHLL pair)
+  const uint64_t *str_off;  // raw STRING: doc d's UTF-8 bytes are raw[str_off[d] .. str_off[d+1])
 };
 
 // One source the filter wave copies into its LDS stage slot for every tile (LDS-DMA, 1 KiB per
@@ -177,6 +178,7 @@ struct DevFilter {
   int32_t min_dma;       // min over segments of LDS-DMA wave-instructions per tile (vmcnt lower bound)
   int32_t probe;         // measurement only (PHIP_FILTER_PROBE): 1 = stream the tiles, skip the evaluation
   int32_t contig_inline;  // 1: range scans of the contiguous evaluator inline (0: through contig_scan_any; A/B)
+  uint32_t stats_programs;  // programs whose scans count as entries scanned in filter (bit p = program p)
   uint32_t *mask_out;    // optional: [total_work][64] lane-major tile masks
   uint64_t *partials;    // [num_blocks][2]: matched docs, entries scanned in filter
   uint64_t *seg_matched; // [num query segments]

@@ -114,6 +114,66 @@ __device__ __forceinline__ bool sorted_contains(const PHIP_GLB T *set, int32_t c
   return lo < count && set[lo] == v;
 }
 
+// String.compareTo order (UTF-16 code units) over UTF-8 bytes: lead bytes 0xEE / 0xEF (U+E000..U+FFFF) rank after
+// the 4-byte leads 0xF0..0xF4 (supplementary characters = surrogate pairs in UTF-16); every other byte keeps its order
+// (the host sorts RAW_STRING sets the same way, runtime.cpp java_str_cmp)
+__device__ __forceinline__ uint32_t java_order_byte(uint32_t b) { return (b == 0xEEu || b == 0xEFu) ? b + 8u : b; }
+__device__ __forceinline__ int java_str_cmp(const PHIP_GLB uint8_t *a, uint32_t al, const PHIP_GLB uint8_t *b,
+                                            uint32_t bl) {
+  const uint32_t m = al < bl ? al : bl;
+  for (uint32_t i = 0; i < m; i++) {
+    const uint32_t x = a[i], y = b[i];
+    if (x != y) return java_order_byte(x) < java_order_byte(y) ? -1 : 1;
+  }
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+// Raw STRING leaf: doc d's UTF-8 bytes [str_off[d], str_off[d+1]) against the bounds (RAW_STRING_RANGE) or a sorted
+// value list (RAW_STRING_SET, binary search); payload layouts in pinot_hip.h
+__device__ __noinline__ uint32_t eval_raw_string(ccol_t &c, cnode_t *__restrict__ n, uint32_t valid, const Tile &t) {
+  const int lane = lane_id();
+  const PHIP_GLB uint8_t *bytes = (const PHIP_GLB uint8_t *)c.raw;
+  const PHIP_GLB uint64_t *off = (const PHIP_GLB uint64_t *)c.str_off;
+  const PHIP_GLB int32_t *w = (const PHIP_GLB int32_t *)n->aux;
+  const PHIP_GLB uint8_t *wb = (const PHIP_GLB uint8_t *)n->aux;
+  const bool range = n->leaf_kind == PHIP_LEAF_RAW_STRING_RANGE;
+  const int32_t lo_len = range ? w[0] : 0, hi_len = range ? w[1] : 0;
+  const bool lo_in = range && w[2] != 0, hi_in = range && w[3] != 0;
+  const uint32_t nv = range ? 0u : (uint32_t)w[0];
+  const PHIP_GLB uint32_t *vo = (const PHIP_GLB uint32_t *)(w + 1);
+  const PHIP_GLB uint8_t *vb = wb + 4 * (2 + (size_t)nv);
+  const bool excl = n->exclusive != 0;
+  const int32_t last = t.valid_docs - 1;
+  uint32_t r = 0;
+  for (int g = 0; g < kTileGroups; g++) {
+    const int32_t doc = t.doc0 + min(g * 64 + lane, last);
+    const uint64_t s0 = off[doc];
+    const uint32_t len = (uint32_t)(off[doc + 1] - s0);
+    const PHIP_GLB uint8_t *v = bytes + s0;
+    bool pass;
+    if (range) {
+      pass = true;
+      if (lo_len >= 0) {
+        const int cmp = java_str_cmp(v, len, wb + 16, (uint32_t)lo_len);
+        pass = lo_in ? cmp >= 0 : cmp > 0;
+      }
+      if (pass && hi_len >= 0) {
+        const int cmp = java_str_cmp(v, len, wb + 16 + (lo_len > 0 ? lo_len : 0), (uint32_t)hi_len);
+        pass = hi_in ? cmp <= 0 : cmp < 0;
+      }
+    } else {
+      uint32_t lo = 0, hi = nv;  // first value >= the doc's
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (java_str_cmp(v, len, vb + vo[mid], vo[mid + 1] - vo[mid]) > 0) lo = mid + 1; else hi = mid;
+      }
+      pass = (lo < nv && java_str_cmp(v, len, vb + vo[lo], vo[lo + 1] - vo[lo]) == 0) != excl;
+    }
+    r = r + r + (uint32_t)pass;
+  }
+  return r & valid;
+}
+
 __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__ n, uint32_t valid, const Tile &t,
                                               uint32_t &scanned) {
   const int lane = lane_id();
@@ -154,6 +214,10 @@ __device__ __forceinline__ uint32_t eval_leaf(cseg_t &seg, cnode_t *__restrict__
     }
     if (n->exclusive) r = ~r;
     return valid & r;
+  }
+  if (kind == PHIP_LEAF_RAW_STRING_RANGE || kind == PHIP_LEAF_RAW_STRING_SET) {
+    scanned += (uint32_t)t.valid_docs;
+    return eval_raw_string(seg.cols[n->column], n, valid, t);
   }
   if (kind == PHIP_LEAF_RAW_RANGE || kind == PHIP_LEAF_RAW_SET) {
     // value-based scan of a raw column (RawValueBasedPredicateEvaluator): one coalesced load per 64 docs
@@ -1234,7 +1298,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     } else {
       mask = seg.node_end > seg.node_begin ? eval_filter(seg, nodes, valid, tl, scanned_t) : valid;
     }
-    scanned += scanned_t;
+    if ((q.stats_programs >> seg.program) & 1u) scanned += scanned_t;  // (wave-uniform)
     lane_matched += (uint32_t)__popc(mask);
     if (st) ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
     if constexpr (NA > 0) {

@@ -1,4 +1,6 @@
 // load.hip -- one-time layout transforms at segment load (phip_segment_load, runtime.cpp).
+#include <hipcub/hipcub.hpp>
+
 #include "codec.h"
 #include "dev_common.h"
 
@@ -234,7 +236,7 @@ template <int kCodec, int kEntry>
 __global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restrict__ blob,
                                                           const RawChunk *__restrict__ chunks, int32_t nchunks,
                                                           int32_t out_cap, int32_t in_cap, uint8_t *__restrict__ out,
-                                                          int32_t *__restrict__ err) {
+                                                          int32_t *__restrict__ err, int32_t *__restrict__ sizes) {
   extern __shared__ __align__(16) uint8_t lds[];
   uint8_t *lout = lds;
   uint8_t *lin = lds + out_cap;
@@ -261,7 +263,17 @@ __global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restr
       got = decode_chunk<kCodec>(in, n, lout, usize, lane);
     }
     __syncthreads();
-    if (got != usize) {
+    if (kEntry == 1) {
+      // var-byte chunk (VarByteChunkForwardIndexWriter): its decoded size is the chunk's own, usize the bound
+      if (got < 0 || got > usize) {
+        if (lane == 0) atomicMax(err, c + 1);
+      } else {
+        if (lane == 0) sizes[c] = got;
+        uint32_t *o = (uint32_t *)(out + dst);
+        const uint32_t *w = (const uint32_t *)lout;
+        for (int i = lane; i < (got + 3) / 4; i += 64) o[i] = w[i];  // bytes as stored (no swap)
+      }
+    } else if (got != usize) {
       if (lane == 0) atomicMax(err, c + 1);
     } else if (kEntry == 8) {
       uint64_t *o = (uint64_t *)(out + dst);
@@ -280,18 +292,21 @@ __global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restr
 template <int kCodec>
 static hipError_t launch_chunk_decode_codec(int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
                                             int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err,
-                                            hipStream_t s) {
+                                            int32_t *sizes, hipStream_t s) {
   const int grid = nchunks < (1 << 20) ? nchunks : (1 << 20);
+  const void *fn = entry == 8 ? (const void *)chunk_decode_kernel<kCodec, 8>
+                 : entry == 4 ? (const void *)chunk_decode_kernel<kCodec, 4>
+                              : (const void *)chunk_decode_kernel<kCodec, 1>;
   if (lds > 65536) {  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
-    hipError_t e = hipFuncSetAttribute(entry == 8 ? (const void *)chunk_decode_kernel<kCodec, 8>
-                                                  : (const void *)chunk_decode_kernel<kCodec, 4>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
     if (e != hipSuccess) return e;
   }
   if (entry == 8)
-    chunk_decode_kernel<kCodec, 8><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, in_cap, out, err);
+    chunk_decode_kernel<kCodec, 8><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, in_cap, out, err, sizes);
+  else if (entry == 4)
+    chunk_decode_kernel<kCodec, 4><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, in_cap, out, err, sizes);
   else
-    chunk_decode_kernel<kCodec, 4><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, in_cap, out, err);
+    chunk_decode_kernel<kCodec, 1><<<grid, 64, lds, s>>>(blob, chunks, nchunks, out_cap, in_cap, out, err, sizes);
   return hipGetLastError();
 }
 
@@ -303,16 +318,98 @@ size_t chunk_decode_extra_lds(int codec, int32_t out_cap) {
 }
 
 hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
-                               int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s) {
+                               int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err, int32_t *sizes,
+                               hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
+  if (entry != 1 && entry != 4 && entry != 8) return hipErrorInvalidValue;
   switch (codec) {
-    case 1: return launch_chunk_decode_codec<1>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
-    case 2: return launch_chunk_decode_codec<2>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
-    case 3: return launch_chunk_decode_codec<3>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
-    case 4: return launch_chunk_decode_codec<4>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
-    case 5: return launch_chunk_decode_codec<5>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, s);
+    case 1: return launch_chunk_decode_codec<1>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, sizes, s);
+    case 2: return launch_chunk_decode_codec<2>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, sizes, s);
+    case 3: return launch_chunk_decode_codec<3>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, sizes, s);
+    case 4: return launch_chunk_decode_codec<4>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, sizes, s);
+    case 5: return launch_chunk_decode_codec<5>(entry, blob, chunks, nchunks, out_cap, in_cap, lds, out, err, sizes, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Raw STRING columns: var-byte chunks (VarByteChunkForwardIndexWriter.java:37-158 -- per chunk numDocsPerChunk BE
+// int start offsets, then the values' UTF-8 bytes) -> one contiguous byte array + u64 doc offsets, so a predicate
+// reads doc d as bytes [off[d], off[d+1]). chunk_base / chunk_size locate each chunk in `stage` (the forward
+// index's own bytes for PASS_THROUGH, the decoded chunks otherwise).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t be32_bytes(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+// [start, end) of doc d inside its chunk (VarByteChunkSVForwardIndexReader.getValueEndOffset, :176-217): the next
+// row's start, or the chunk's end for its last row and for the last row of a partial chunk (absent rows hold 0)
+__device__ __forceinline__ bool varbyte_span(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
+                                             int32_t per_chunk, int64_t d, uint64_t &src, uint32_t &len) {
+  const int64_t k = d / per_chunk;
+  const int32_t r = (int32_t)(d - k * per_chunk);
+  const uint8_t *c = stage + chunk_base[k];
+  const uint32_t size = (uint32_t)chunk_size[k];
+  const uint32_t start = be32_bytes(c + 4 * r);
+  uint32_t end = r + 1 < per_chunk ? be32_bytes(c + 4 * (r + 1)) : 0u;
+  if (end == 0) end = size;
+  const uint32_t hdr = 4u * (uint32_t)per_chunk;
+  if ((uint64_t)hdr > size || start < hdr || end < start || end > size) return false;
+  src = chunk_base[k] + start;
+  len = end - start;
+  return true;
+}
+
+__global__ void varbyte_lengths_kernel(const uint8_t *__restrict__ stage, const uint64_t *__restrict__ chunk_base,
+                                       const int32_t *__restrict__ chunk_size, int32_t per_chunk, int64_t n,
+                                       uint64_t *__restrict__ len, int32_t *__restrict__ err) {
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d > n) return;
+  if (d == n) {
+    len[n] = 0;  // (the exclusive scan's total)
+    return;
+  }
+  uint64_t src;
+  uint32_t l;
+  if (!varbyte_span(stage, chunk_base, chunk_size, per_chunk, d, src, l)) {
+    atomicMax(err, 1);
+    l = 0;
+  }
+  len[d] = l;
+}
+
+__global__ void varbyte_copy_kernel(const uint8_t *__restrict__ stage, const uint64_t *__restrict__ chunk_base,
+                                    const int32_t *__restrict__ chunk_size, int32_t per_chunk, int64_t n,
+                                    const uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  uint64_t src;
+  uint32_t l;
+  if (!varbyte_span(stage, chunk_base, chunk_size, per_chunk, d, src, l)) return;  // (the lengths pass failed the load)
+  const uint64_t o = off[d];
+  for (uint32_t i = 0; i < l; i++) out[o + i] = stage[src + i];
+}
+
+// lengths of docs 0..n-1 (len[n] = 0) and their exclusive scan into off[0..n]; temp == null: scan size query only
+hipError_t launch_varbyte_offsets(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
+                                  int32_t per_chunk, int64_t n, uint64_t *len, uint64_t *off, void *temp,
+                                  size_t *temp_bytes, int32_t *err, hipStream_t s) {
+  if (temp == nullptr) return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, len, off, n + 1, s);
+  const int threads = 256;
+  const int64_t blocks = (n + 1 + threads - 1) / threads;
+  varbyte_lengths_kernel<<<(unsigned)blocks, threads, 0, s>>>(stage, chunk_base, chunk_size, per_chunk, n, len, err);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, len, off, n + 1, s);
+}
+
+hipError_t launch_varbyte_copy(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
+                               int32_t per_chunk, int64_t n, const uint64_t *off, uint8_t *out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int threads = 256;
+  varbyte_copy_kernel<<<(unsigned)((n + threads - 1) / threads), threads, 0, s>>>(stage, chunk_base, chunk_size,
+                                                                                   per_chunk, n, off, out);
+  return hipGetLastError();
 }
 
 }  // namespace phip

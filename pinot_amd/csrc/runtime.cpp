@@ -41,7 +41,8 @@ hipError_t launch_trim_gather(const int32_t *order, int64_t k, int32_t naggs, in
                               const double *vals, const int64_t *longs, const uint8_t *hll, int64_t *keys_out,
                               double *vals_out, int64_t *longs_out, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
-                               int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err, hipStream_t s);
+                               int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err, int32_t *sizes,
+                               hipStream_t s);
 size_t chunk_decode_extra_lds(int codec, int32_t out_cap);
 hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32_t *ids_tmp, int64_t n, int32_t bits,
                                    uint32_t *words, int64_t nwords, hipStream_t s);
@@ -89,6 +90,11 @@ hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t 
                                const uint64_t *table, const uint32_t *hll, int32_t nhll, int32_t log2m,
                                int64_t *keys_out, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s);
+hipError_t launch_varbyte_offsets(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
+                                  int32_t per_chunk, int64_t n, uint64_t *len, uint64_t *off, void *temp,
+                                  size_t *temp_bytes, int32_t *err, hipStream_t s);
+hipError_t launch_varbyte_copy(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
+                               int32_t per_chunk, int64_t n, const uint64_t *off, uint8_t *out, hipStream_t s);
 }  // namespace phip
 
 using namespace phip;
@@ -294,7 +300,9 @@ struct ColumnStore {
   int32_t hll_log2m = 0;      // PHIP_FWD_HLL_REGISTERS: 2^hll_log2m u8 registers per doc in `raw`
   uint32_t *words = nullptr;  // fixed-bit dict ids (also synthesised for sorted columns)
   void *dict = nullptr;       // LE typed dictionary (numeric)
-  void *raw = nullptr;        // LE raw values
+  void *raw = nullptr;        // LE raw values (raw STRING: the values' UTF-8 bytes, back to back)
+  uint64_t *str_off = nullptr;  // raw STRING: num_docs + 1 byte offsets into raw
+  uint64_t str_total = 0;       // raw STRING: bytes of all values
   std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
   std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
   std::map<int, uint32_t *> hll;      // per log2m
@@ -499,6 +507,128 @@ static int32_t parse_inverted(const phip_column_desc &c, ColumnStore &cs, Segmen
   return PHIP_OK;
 }
 
+// Raw STRING column: VarByteChunkForwardIndexWriter v1..v3 (VarByteChunkForwardIndexWriter.java:37-158 over the
+// BaseChunkForwardIndexWriter header and chunk table; per chunk numDocsPerChunk BE int start offsets, then the
+// values' UTF-8 bytes; VarByteChunkSVForwardIndexReader.java:80-217 reads them) -> the values back to back in HBM
+// plus num_docs + 1 u64 offsets, built on the GPU (load.hip): compressed chunks are decoded by the same kernel as
+// fixed-width ones (their decoded size is their own, at most the writer's chunk buffer), then a lengths pass, an
+// exclusive scan and a copy. The V4 / V5 var-byte writers (a different chunk layout) are outside the GPU path.
+static int32_t load_varbyte(const phip_column_desc &c, Segment &seg, ColumnStore &cs, hipStream_t st,
+                            std::vector<void *> &temps) {
+  const int64_t n = seg.num_docs;
+  const uint8_t *h = c.forward;
+  if (h == nullptr || c.forward_bytes < 16) return fail(PHIP_ERR_INVALID, "column %s: chunk header truncated", c.name);
+  const int32_t version = (int32_t)be32(h), num_chunks = (int32_t)be32(h + 4), per_chunk = (int32_t)be32(h + 8);
+  const int32_t longest = (int32_t)be32(h + 12);
+  int32_t total = (int32_t)n, comp = 1, data_hdr = 16;  // v1: 4-int header, SNAPPY chunks, int offsets from byte 16
+  if (version < 1 || version > 3)
+    return fail(PHIP_ERR_UNSUPPORTED, "column %s: var-byte chunk version %d (the GPU path reads v1..v3)", c.name, version);
+  if (version > 1) {
+    if (c.forward_bytes < 28) return fail(PHIP_ERR_INVALID, "column %s: chunk header truncated", c.name);
+    total = (int32_t)be32(h + 16);
+    comp = (int32_t)be32(h + 20);
+    data_hdr = (int32_t)be32(h + 24);
+  }
+  if (comp < 0 || comp > 5) return fail(PHIP_ERR_INVALID, "column %s: unknown chunk compression type %d", c.name, comp);
+  if (total != n || per_chunk <= 0 || longest < 0 || num_chunks != ceil_div(n, per_chunk))
+    return fail(PHIP_ERR_INVALID, "column %s: bad var-byte chunk header", c.name);
+  const int osz = version <= 2 ? 4 : 8;
+  const uint64_t hdr_end = (uint64_t)data_hdr + (uint64_t)num_chunks * osz;
+  if (data_hdr < (version > 1 ? 28 : 16) || hdr_end > c.forward_bytes)
+    return fail(PHIP_ERR_INVALID, "column %s: chunk offsets truncated", c.name);
+  // the writer's chunk buffer: numDocsPerChunk x (4 + lengthOfLongestEntry) (VarByteChunkForwardIndexWriter.java:69-71)
+  const uint64_t max_u = (uint64_t)per_chunk * (4 + (uint64_t)longest);
+  if (max_u >= (1ull << 31)) return fail(PHIP_ERR_INVALID, "column %s: var-byte chunk of %llu bytes", c.name, (unsigned long long)max_u);
+  auto chunk_off = [&](int32_t k) -> uint64_t { return osz == 4 ? be32(h + data_hdr + 4 * k) : be64(h + data_hdr + 8 * k); };
+  std::vector<uint64_t> base(std::max(num_chunks, 1), 0);
+  std::vector<int32_t> size(std::max(num_chunks, 1), 0);
+  std::vector<RawChunk> chunks(std::max(num_chunks, 1));
+  const uint64_t first = num_chunks > 0 ? chunk_off(0) : hdr_end;
+  uint32_t max_c = 0;
+  for (int32_t k = 0; k < num_chunks; k++) {
+    const uint64_t off = chunk_off(k), end = k + 1 < num_chunks ? chunk_off(k + 1) : c.forward_bytes;
+    if (off < hdr_end || end < off || end > c.forward_bytes || end - off >= (1ull << 31))
+      return fail(PHIP_ERR_INVALID, "column %s: chunk %d offsets out of order", c.name, k);
+    if (comp == 0 && end - off > max_u) return fail(PHIP_ERR_INVALID, "column %s: chunk %d exceeds its header", c.name, k);
+    base[k] = off - first;
+    size[k] = (int32_t)(end - off);
+    chunks[k].src = off - first;
+    chunks[k].csize = (uint32_t)(end - off);
+    chunks[k].usize = (uint32_t)max_u;
+    max_c = std::max(max_c, chunks[k].csize);
+  }
+  const uint64_t blob_bytes = c.forward_bytes - first;
+  void *blob, *dbase, *dsize, *err;
+  HIP_TRY(hipMalloc(&blob, blob_bytes + 16));
+  temps.push_back(blob);
+  HIP_TRY(hipMalloc(&dbase, base.size() * 8));
+  temps.push_back(dbase);
+  HIP_TRY(hipMalloc(&dsize, size.size() * 4));
+  temps.push_back(dsize);
+  HIP_TRY(hipMalloc(&err, 4));
+  temps.push_back(err);
+  HIP_TRY(hipMemsetAsync(err, 0, 4, st));
+  if (blob_bytes) HIP_TRY(hipMemcpyAsync(blob, h + first, blob_bytes, hipMemcpyHostToDevice, st));
+  const uint8_t *stage = (const uint8_t *)blob;
+  if (comp != 0 && num_chunks > 0) {
+    const uint64_t stride = (uint64_t)round_up((int64_t)max_u, 16);
+    for (int32_t k = 0; k < num_chunks; k++) {
+      base[k] = (uint64_t)k * stride;
+      chunks[k].dst = base[k];
+    }
+    const uint32_t out_cap = (uint32_t)stride;
+    const uint32_t in_cap = (uint32_t)round_up(max_c + 8, 16);
+    const size_t lds = out_cap + in_cap + chunk_decode_extra_lds(comp, (int32_t)out_cap);
+    if (lds > 163840 - 1024)
+      return fail(PHIP_ERR_UNSUPPORTED, "column %s: var-byte chunks of %u -> %llu bytes exceed the 159 KiB LDS decode window",
+                  c.name, max_c, (unsigned long long)max_u);
+    void *dec, *table;
+    HIP_TRY(hipMalloc(&dec, stride * num_chunks + 16));
+    temps.push_back(dec);
+    HIP_TRY(hipMalloc(&table, sizeof(RawChunk) * num_chunks));
+    temps.push_back(table);
+    HIP_TRY(hipMemcpyAsync(table, chunks.data(), sizeof(RawChunk) * num_chunks, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_chunk_decode(comp, 1, (const uint8_t *)blob, (const RawChunk *)table, num_chunks, (int32_t)out_cap,
+                                (int32_t)in_cap, lds, (uint8_t *)dec, (int32_t *)err, (int32_t *)dsize, st));
+    int32_t bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, err, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (bad) return fail(PHIP_ERR_INVALID, "column %s: malformed compressed chunk %d (type %d)", c.name, bad - 1, comp);
+    stage = (const uint8_t *)dec;
+  } else {
+    HIP_TRY(hipMemcpyAsync(dsize, size.data(), size.size() * 4, hipMemcpyHostToDevice, st));
+  }
+  HIP_TRY(hipMemcpyAsync(dbase, base.data(), base.size() * 8, hipMemcpyHostToDevice, st));
+  void *off, *len, *temp;
+  int32_t rc = dev_alloc(seg, (size_t)(n + 1) * 8, &off);
+  if (rc) return rc;
+  HIP_TRY(hipMalloc(&len, (size_t)(n + 1) * 8));
+  temps.push_back(len);
+  size_t temp_bytes = 0;
+  HIP_TRY(launch_varbyte_offsets(stage, (const uint64_t *)dbase, (const int32_t *)dsize, per_chunk, n, (uint64_t *)len,
+                                 (uint64_t *)off, nullptr, &temp_bytes, (int32_t *)err, st));
+  HIP_TRY(hipMalloc(&temp, std::max<size_t>(temp_bytes, 16)));
+  temps.push_back(temp);
+  HIP_TRY(launch_varbyte_offsets(stage, (const uint64_t *)dbase, (const int32_t *)dsize, per_chunk, n, (uint64_t *)len,
+                                 (uint64_t *)off, temp, &temp_bytes, (int32_t *)err, st));
+  int32_t bad = 0;
+  uint64_t nbytes = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&nbytes, (uint64_t *)off + n, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (bad) return fail(PHIP_ERR_INVALID, "column %s: var-byte row offsets outside their chunk", c.name);
+  void *bytes;
+  rc = dev_alloc(seg, nbytes + 16, &bytes);
+  if (rc) return rc;
+  HIP_TRY(launch_varbyte_copy(stage, (const uint64_t *)dbase, (const int32_t *)dsize, per_chunk, n, (const uint64_t *)off,
+                              (uint8_t *)bytes, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  cs.raw = bytes;
+  cs.str_off = (uint64_t *)off;
+  cs.str_total = nbytes;
+  return PHIP_OK;
+}
+
 static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t st, std::vector<void *> &temps) {
   ColumnStore cs;
   if (!c.name) return fail(PHIP_ERR_INVALID, "column without name");
@@ -594,9 +724,11 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
       int32_t rc2 = parse_inverted(c, cs, seg, st);
       if (rc2) return rc2;
     }
+  } else if (c.data_type == PHIP_TYPE_STRING) {
+    int32_t rc = load_varbyte(c, seg, cs, st, temps);
+    if (rc) return rc;
   } else {
     // raw fixed-width chunk forward index (BaseChunkForwardIndexWriter.java:40-160)
-    if (c.data_type == PHIP_TYPE_STRING) return fail(PHIP_ERR_UNSUPPORTED, "raw STRING columns are not on the GPU path");
     const uint8_t *h = c.forward;
     if (c.forward_bytes < 16) return fail(PHIP_ERR_INVALID, "column %s: chunk header truncated", c.name);
     int32_t version = (int32_t)be32(h), num_chunks = (int32_t)be32(h + 4), per_chunk = (int32_t)be32(h + 8);
@@ -672,7 +804,7 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
       HIP_TRY(hipMemcpyAsync(blob, h + first, blob_bytes, hipMemcpyHostToDevice, st));
       HIP_TRY(hipMemcpyAsync(table, chunks.data(), sizeof(RawChunk) * num_chunks, hipMemcpyHostToDevice, st));
       HIP_TRY(launch_chunk_decode(comp, entry, (const uint8_t *)blob, (const RawChunk *)table, num_chunks,
-                                  (int32_t)out_cap, (int32_t)in_cap, lds, (uint8_t *)p, (int32_t *)err, st));
+                                  (int32_t)out_cap, (int32_t)in_cap, lds, (uint8_t *)p, (int32_t *)err, nullptr, st));
       int32_t bad = 0;
       HIP_TRY(hipMemcpyAsync(&bad, err, 4, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
@@ -745,7 +877,7 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
   int after;
   switch (n.op) {
     case PHIP_NODE_LEAF:
-      if (n.leaf_kind < PHIP_LEAF_MATCH_ALL || n.leaf_kind > PHIP_LEAF_RAW_SET) {
+      if (n.leaf_kind < PHIP_LEAF_MATCH_ALL || n.leaf_kind > PHIP_LEAF_RAW_STRING_SET) {
         err = "bad leaf kind";
         return -1;
       }
@@ -761,6 +893,11 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
       }
       if (n.leaf_kind == PHIP_LEAF_RAW_SET && (n.count % 2 != 0 || n.count > 2 * (1 << 20))) {
         err = "raw set leaf: count must be 2 x (values <= 2^20)";
+        return -1;
+      }
+      if ((n.leaf_kind == PHIP_LEAF_RAW_STRING_RANGE && (n.ids == nullptr || n.count < 4 || n.count > (1 << 24))) ||
+          (n.leaf_kind == PHIP_LEAF_RAW_STRING_SET && (n.ids == nullptr || n.count < 2 || n.count > (1 << 26)))) {
+        err = "raw STRING leaf: count words of bounds / values (<= 2^24 / 2^26)";
         return -1;
       }
       if ((n.leaf_kind == PHIP_LEAF_DICT_SET || n.leaf_kind == PHIP_LEAF_INVERTED || n.leaf_kind == PHIP_LEAF_DOC_RANGES ||
@@ -1079,6 +1216,84 @@ struct Plan {
   float sel_filter_ms = 0.f;
   bool total_events = true;  // record ev[0] / ev[3] (phip_result.device_ms); PHIP_TOTAL_EVENTS=0 skips them (A/B)
 };
+
+// String.compareTo order (UTF-16 code units) over UTF-8 bytes: the lead bytes 0xEE / 0xEF (U+E000..U+FFFF) rank
+// after the 4-byte leads 0xF0..0xF4 (supplementary characters, i.e. surrogate pairs 0xD800..0xDFFF in UTF-16); every
+// other byte keeps its order. The kernel compares the same way (filter.hip java_str_cmp).
+static inline int java_order_byte(uint8_t b) { return (b == 0xEE || b == 0xEF) ? b + 8 : b; }
+static int java_str_cmp(const uint8_t *a, size_t al, const uint8_t *b, size_t bl) {
+  const size_t m = std::min(al, bl);
+  for (size_t i = 0; i < m; i++)
+    if (a[i] != b[i]) return java_order_byte(a[i]) < java_order_byte(b[i]) ? -1 : 1;
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+// RAW_RANGE / RAW_SET leaf on a raw STRING column (StringRawValueBasedRangePredicateEvaluator / the raw EQ / IN
+// evaluators of RangePredicateEvaluatorFactory.java / InPredicateEvaluatorFactory.java). phip_filter_node.ids holds
+// `count` int32 words: RAW_SET = [n][n + 1 byte offsets][the values' UTF-8 bytes]; RAW_RANGE = [lo_len][hi_len]
+// [lo_inclusive][hi_inclusive][lo bytes][hi bytes], a length of -1 = unbounded. The set is sorted in String order and
+// deduplicated here, so the kernel binary-searches it.
+struct AuxFix {  // a leaf's node.aux = device base of the plan's blob + off
+  size_t node;
+  size_t off;
+};
+
+static int32_t raw_string_leaf(const phip_filter_node &fn, DevNode &dn, Blob &blob, std::vector<AuxFix> &aux_fix,
+                               size_t ni) {
+  if (fn.ids == nullptr || fn.count < 1) return fail(PHIP_ERR_INVALID, "raw STRING leaf without its values");
+  const int64_t wb = (int64_t)fn.count * 4;
+  const uint8_t *w = (const uint8_t *)fn.ids;
+  if (fn.leaf_kind == PHIP_LEAF_RAW_STRING_RANGE) {
+    if (fn.count < 4) return fail(PHIP_ERR_INVALID, "raw STRING range: truncated bounds");
+    const int32_t lo_len = fn.ids[0], hi_len = fn.ids[1];
+    if (lo_len < -1 || hi_len < -1 || 16 + (int64_t)std::max(lo_len, 0) + std::max(hi_len, 0) > wb)
+      return fail(PHIP_ERR_INVALID, "raw STRING range: bound lengths %d / %d exceed the leaf's %d words", lo_len, hi_len, fn.count);
+    aux_fix.push_back({ni, blob.add(fn.ids, (size_t)(16 + std::max(lo_len, 0) + std::max(hi_len, 0)))});
+    return PHIP_OK;
+  }
+  const int64_t nv = fn.ids[0];
+  if (nv < 0 || (1 + nv + 1) * 4 > wb) return fail(PHIP_ERR_INVALID, "raw STRING set: %lld values in %d words", (long long)nv, fn.count);
+  const int64_t data0 = (2 + nv) * 4;
+  std::vector<std::pair<const uint8_t *, size_t>> vals;
+  vals.reserve(nv);
+  for (int64_t k = 0; k < nv; k++) {
+    const int64_t s = (uint32_t)fn.ids[1 + k], e = (uint32_t)fn.ids[2 + k];
+    if (e < s || data0 + e > wb) return fail(PHIP_ERR_INVALID, "raw STRING set: value %lld outside the leaf", (long long)k);
+    vals.push_back({w + data0 + s, (size_t)(e - s)});
+  }
+  auto less = [](const std::pair<const uint8_t *, size_t> &a, const std::pair<const uint8_t *, size_t> &b) {
+    return java_str_cmp(a.first, a.second, b.first, b.second) < 0;
+  };
+  std::sort(vals.begin(), vals.end(), less);
+  vals.erase(std::unique(vals.begin(), vals.end(),
+                         [](const std::pair<const uint8_t *, size_t> &a, const std::pair<const uint8_t *, size_t> &b) {
+                           return java_str_cmp(a.first, a.second, b.first, b.second) == 0;
+                         }),
+             vals.end());
+  if (vals.empty()) {
+    dn.leaf_kind = fn.exclusive ? PHIP_LEAF_MATCH_ALL : PHIP_LEAF_MATCH_NONE;
+    return PHIP_OK;
+  }
+  // device payload: [n][n + 1 offsets] then the bytes, in order
+  std::vector<uint32_t> out(2 + vals.size());
+  out[0] = (uint32_t)vals.size();
+  size_t pos = 0;
+  for (size_t k = 0; k < vals.size(); k++) {
+    out[1 + k] = (uint32_t)pos;
+    pos += vals[k].second;
+  }
+  out[1 + vals.size()] = (uint32_t)pos;
+  std::vector<uint8_t> payload(out.size() * 4 + pos);
+  memcpy(payload.data(), out.data(), out.size() * 4);
+  pos = out.size() * 4;
+  for (const auto &v : vals) {
+    if (v.second) memcpy(payload.data() + pos, v.first, v.second);
+    pos += v.second;
+  }
+  dn.count = (int32_t)vals.size();
+  aux_fix.push_back({ni, blob.add(payload.data(), payload.size())});
+  return PHIP_OK;
+}
 
 static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
 
@@ -1417,10 +1632,6 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // ---- staging blob: segments, nodes, leaf aux ------------------------------------------------
   Blob blob;
   std::vector<DevNode> nodes;
-  struct AuxFix {
-    size_t node;
-    size_t off;
-  };
   std::vector<AuxFix> aux_fix;  // node.aux = dev_base + off
   struct InvLeaf {
     size_t node;
@@ -1455,6 +1666,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dc.type = cs.type;
       dc.has_dict = !no_dict(cs);
       dc.hll_rows = cs.hll_log2m;
+      dc.str_off = cs.str_off;
       dc.lds_off = -1;
     }
     for (int a = 0; a < naggs; a++) {
@@ -1576,7 +1788,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
           case PHIP_LEAF_RAW_RANGE:
           case PHIP_LEAF_RAW_SET:
             if (cs->fwd_kind != PHIP_FWD_RAW_CHUNK) { rc = fail(PHIP_ERR_INVALID, "raw leaf on a column without raw values"); break; }
-            if (cs->type == PHIP_TYPE_STRING) { rc = fail(PHIP_ERR_UNSUPPORTED, "raw STRING predicate"); break; }
+            if (cs->type == PHIP_TYPE_STRING) { rc = fail(PHIP_ERR_INVALID, "STRING column: use the RAW_STRING leaves"); break; }
             if (fn.leaf_kind == PHIP_LEAF_RAW_SET) {
               // the kernel binary-searches the values (filter.hip sorted_contains): sorted, distinct, and for
               // FLOAT / DOUBLE columns without NaN (IEEE equality never matches it)
@@ -1608,6 +1820,14 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
               break;
             }
             aux_fix.push_back({ni, blob.add(fn.ids, (size_t)fn.count * 4)});
+            break;
+          case PHIP_LEAF_RAW_STRING_RANGE:
+          case PHIP_LEAF_RAW_STRING_SET:
+            if (cs->fwd_kind != PHIP_FWD_RAW_CHUNK || cs->type != PHIP_TYPE_STRING || cs->str_off == nullptr) {
+              rc = fail(PHIP_ERR_INVALID, "raw STRING leaf on column %s, which holds no raw STRING values", cs->name.c_str());
+              break;
+            }
+            rc = raw_string_leaf(fn, dn, blob, aux_fix, ni);
             break;
           case PHIP_LEAF_INVERTED:
             if (cs->inv_begin.empty()) { rc = fail(PHIP_ERR_INVALID, "column %s has no inverted index", cs->name.c_str()); break; }
@@ -2033,6 +2253,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         per_tile += 256;
       } else if (dn.leaf_kind == PHIP_LEAF_RAW_RANGE || dn.leaf_kind == PHIP_LEAF_RAW_SET) {
         per_tile += (int64_t)kTileDocs * type_width(ds.cols[dn.column].type);
+      } else if (dn.leaf_kind == PHIP_LEAF_RAW_STRING_RANGE || dn.leaf_kind == PHIP_LEAF_RAW_STRING_SET) {
+        // the doc offsets + the values' bytes (this segment's mean length)
+        const int s = ds.seg_index % nseg;
+        const ColumnStore &cs = segs[s]->cols[colidx[s][dn.column]];
+        per_tile += (int64_t)kTileDocs * 8 + (int64_t)(kTileDocs * cs.str_total / std::max<int64_t>(segs[s]->num_docs, 1));
       }
     }
     P.filter_bytes += per_tile * ds.num_work;
@@ -2162,6 +2387,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const char *ie = getenv("PHIP_CONTIG_INLINE");
     fq.contig_inline = ie ? atoi(ie) : 1;
   }
+  fq.stats_programs = q->stats_programs ? (uint32_t)q->stats_programs : 0xffffffffu;
   fq.min_dma = 0;
   for (size_t i = 0; i < dsegs.size(); i++)
     fq.min_dma = i == 0 ? dsegs[i].num_dma : std::min(fq.min_dma, dsegs[i].num_dma);

@@ -75,12 +75,40 @@ def _doc_ranges_for(seg: GpuSegment, column: str, ev: predeval.DictPredicateEval
 RAW_SET_MAX = 1 << 20  # values of a raw IN list (the descriptor blob carries them)
 
 
+def _raw_string_predicate(column, pred):
+    """Value-based leaf on a raw STRING column (RangePredicateEvaluatorFactory's StringRawValueBasedRange-
+    PredicateEvaluator: String.compareTo against the bounds; the raw EQ / IN evaluators: equality). Literals become
+    their string form; the payload layouts are pinot_hip.h's RAW_STRING_RANGE / RAW_STRING_SET (the library sorts
+    and deduplicates the set)."""
+    def words(b: bytes) -> np.ndarray:
+        return np.frombuffer(b + b"\0" * (-len(b) % 4), dtype=np.int32).copy()
+
+    if pred.type == "RANGE":
+        lo = None if pred.lower == UNBOUNDED else str(pred.lower).encode("utf-8")
+        hi = None if pred.upper == UNBOUNDED else str(pred.upper).encode("utf-8")
+        head = np.array([-1 if lo is None else len(lo), -1 if hi is None else len(hi),
+                         int(bool(pred.lower_inclusive)), int(bool(pred.upper_inclusive))], dtype=np.int32)
+        return _Leaf(_lib.LEAF_RAW_STRING_RANGE, column, ids=np.concatenate([head, words((lo or b"") + (hi or b""))]))
+    exclusive = pred.type in ("NOT_EQ", "NOT_IN")
+    vals = sorted({str(v).encode("utf-8") for v in pred.values})
+    if len(vals) > RAW_SET_MAX:
+        raise UnsupportedOnGpu(f"raw IN list longer than {RAW_SET_MAX} values")
+    if not vals:
+        return _TRUE if exclusive else _FALSE
+    offs = np.zeros(len(vals) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(v) for v in vals])
+    if offs[-1] >= 1 << 31:
+        raise UnsupportedOnGpu("raw STRING IN list over 2 GiB")
+    head = np.concatenate([[len(vals)], offs]).astype(np.int32)
+    return _Leaf(_lib.LEAF_RAW_STRING_SET, column, exclusive=exclusive, ids=np.concatenate([head, words(b"".join(vals))]))
+
+
 def _raw_predicate(column, dt: DataType, pred):
     """Value-based leaf on a raw column (RawValueBasedPredicateEvaluatorFactory + ScanBasedFilterOperator):
     literals converted to the column type first (FLOAT literals rounded to float32, as Float.parseFloat);
     integral ranges folded to closed integer intervals."""
     if dt == DataType.STRING:
-        raise UnsupportedOnGpu(f"predicate on raw STRING column {column}")
+        return _raw_string_predicate(column, pred)
     real = dt in (DataType.FLOAT, DataType.DOUBLE)
 
     def conv(v):
@@ -322,6 +350,7 @@ class GpuCombineOperator:
             if not isinstance(e, Identifier):
                 raise UnsupportedOnGpu(f"group-by expression {e}")
         self.num_programs = len(programs[0]) if programs is not None else 1
+        self.stats_programs = 0  # phip_query_desc.stats_programs: 0 = every program's scans count
         self.prims, self.mapping = plan_aggregations(query.aggregations, programs[1] if programs is not None else None)
         if programs is not None:
             # program-major, as filter_offsets lays them out: program p of segment s at p * nseg + s
@@ -379,6 +408,7 @@ class GpuCombineOperator:
         keep.append(arr)
         q.filter_nodes = arr
         q.num_filter_programs = self.num_programs
+        q.stats_programs = self.stats_programs
         aggs = (_lib.Aggregation * max(len(self.prims), 1))()
         for i, (f, expr, ca, cb, log2m, prog) in enumerate(self.prims):
             aggs[i].function = f
@@ -774,6 +804,13 @@ class GpuSelectionOperator(GpuCombineOperator):
             lib.phip_result_free(res)
 
 
+def _stats_mask(keys, stats_filters) -> int:
+    """phip_query_desc.stats_programs for programs keyed by ``keys`` (their FILTER clauses, in program order)."""
+    if stats_filters is None:
+        return 0
+    return sum(1 << p for p, k in enumerate(keys) if k in stats_filters) or (1 << 31)  # (no program 31: none)
+
+
 def _run_parts(parts):
     """The per-info operators of a filtered query, in info order (FilteredAggregationOperator runs its infos one
     after another too). Running them on concurrent execution lanes from a thread pool was measured slower on C1
@@ -796,7 +833,10 @@ class GpuFilteredAggregationOperator:
     _MAX_SLOTS = 8     # device.h kMaxAggs
     _TIMES = ("device_ms", "scan_kernel_ms", "filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes")
 
-    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int):
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int,
+                 stats_filters=None):
+        """stats_filters: the FILTER clauses (None = unfiltered) whose programs count in numEntriesScannedInFilter
+        (default: all) -- GpuCaseAggregationOperator's original filters, not its CASE-branch programs."""
         if query.group_by:
             raise UnsupportedOnGpu("FILTER clause with GROUP BY (FilteredGroupByOperator)")
         self.query = query
@@ -820,13 +860,16 @@ class GpuFilteredAggregationOperator:
                                limit=query.limit, options=dict(query.options))
             op = GpuCombineOperator(sub, self.segments, num_groups_limit,
                                     programs=(filters, [order.index(ag.filter) for ag in query.aggregations]))
+            op.stats_programs = _stats_mask(order, stats_filters)
             if len(op.prims) <= self._MAX_SLOTS:
                 self.one_pass = op
                 return
-        for f, idxs in zip(filters, groups.values()):
+        self.part_counts = []
+        for (key, idxs), f in zip(groups.items(), filters):
             sub = QueryContext(query.table, [], [query.aggregations[i].unfiltered() for i in idxs], f, [],
                                limit=query.limit, options=dict(query.options))
             self.parts.append((idxs, GpuCombineOperator(sub, self.segments, num_groups_limit)))
+            self.part_counts.append(stats_filters is None or key in stats_filters)
 
     def next_block(self):
         if self.one_pass is not None:
@@ -838,12 +881,12 @@ class GpuFilteredAggregationOperator:
         results = [None] * len(self.query.aggregations)
         stats = ExecutionStatistics()
         times = dict.fromkeys(self._TIMES, 0)
-        for (idxs, op), blk in zip(self.parts, _run_parts(self.parts)):
+        for (idxs, op), blk, counts in zip(self.parts, _run_parts(self.parts), self.part_counts):
             for j, i in enumerate(idxs):
                 results[i] = blk.results[j]
             s = blk.stats
             stats.num_docs_scanned += s.num_docs_scanned
-            stats.num_entries_scanned_in_filter += s.num_entries_scanned_in_filter
+            stats.num_entries_scanned_in_filter += s.num_entries_scanned_in_filter if counts else 0
             stats.num_entries_scanned_post_filter += s.num_entries_scanned_post_filter
             stats.num_total_docs = s.num_total_docs
             stats.num_segments_processed = s.num_segments_processed
@@ -904,7 +947,7 @@ class GpuFilteredGroupByOperator:
     _MAX_SLOTS = 8     # device.h kMaxAggs
 
     def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int,
-                 device_trim: bool = True):
+                 device_trim: bool = True, stats_filters=None):
         self.query = query
         self.segments = list(segments)
         self.num_groups_limit = num_groups_limit
@@ -929,6 +972,7 @@ class GpuFilteredGroupByOperator:
                 filters.append(FilterContext.AND(query.filter, flt))
         self.one_pass = None
         self.parts = []
+        self.part_counts = []
         if len(order) <= self._MAX_PROGRAMS:
             prog_of = {}
             for p, (_, idxs) in enumerate(order):
@@ -939,6 +983,7 @@ class GpuFilteredGroupByOperator:
                                options=dict(query.options))
             op = GpuCombineOperator(sub, self.segments, num_groups_limit,
                                     programs=(filters, [prog_of[i] for i in range(len(query.aggregations))]))
+            op.stats_programs = _stats_mask([flt for flt, _ in order], stats_filters)
             if len(op.prims) <= self._MAX_SLOTS:
                 op.device_trim = device_trim
                 op.trim_query = query  # ORDER BY resolves against the FILTER'ed functions
@@ -953,6 +998,7 @@ class GpuFilteredGroupByOperator:
             op = GpuCombineOperator(sub, self.segments, num_groups_limit)
             op.device_trim = False
             self.parts.append((idxs, op))
+            self.part_counts.append(stats_filters is None or flt in stats_filters)
 
     def _wrap(self, blk):
         out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), blk.groups, blk.stats,
@@ -972,7 +1018,7 @@ class GpuFilteredGroupByOperator:
         per_part = []
         keys = {}
         device_ms = 0.0
-        for (idxs, op), blk in zip(self.parts, _run_parts(self.parts)):
+        for (idxs, op), blk, counts in zip(self.parts, _run_parts(self.parts), self.part_counts):
             if blk.num_groups_limit_reached:
                 raise UnsupportedOnGpu("numGroupsLimit reached by a FILTER + GROUP BY query of more than 8 infos")
             per_part.append((idxs, blk.groups))
@@ -980,7 +1026,7 @@ class GpuFilteredGroupByOperator:
                 keys.setdefault(k, None)
             s = blk.stats
             stats.num_docs_scanned += s.num_docs_scanned
-            stats.num_entries_scanned_in_filter += s.num_entries_scanned_in_filter
+            stats.num_entries_scanned_in_filter += s.num_entries_scanned_in_filter if counts else 0
             stats.num_entries_scanned_post_filter += s.num_entries_scanned_post_filter
             stats.num_total_docs = s.num_total_docs
             stats.num_segments_processed = s.num_segments_processed
@@ -1109,10 +1155,15 @@ class GpuCaseAggregationOperator:
             inner_options.pop("filteredAggregationsSkipEmptyGroups", None)  # the CASE query's groups = main filter's
         self.inner_query = QueryContext(query.table, [], inner, query.filter, list(query.group_by), [],
                                         limit=query.limit, options=inner_options)
+        # numEntriesScannedInFilter: the scans of the original filters' programs only (the hidden COUNT(*) slots'),
+        # not those of the CASE-branch programs, which re-evaluate the filter AND a WHEN condition
+        stats_filters = set(per_filter)
         if query.group_by:
-            self.inner = GpuFilteredGroupByOperator(self.inner_query, segments, num_groups_limit)
+            self.inner = GpuFilteredGroupByOperator(self.inner_query, segments, num_groups_limit,
+                                                    stats_filters=stats_filters)
         else:
-            self.inner = GpuFilteredAggregationOperator(self.inner_query, segments, num_groups_limit)
+            self.inner = GpuFilteredAggregationOperator(self.inner_query, segments, num_groups_limit,
+                                                        stats_filters=stats_filters)
 
     def _fold(self, vals):
         out = []

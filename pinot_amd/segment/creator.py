@@ -12,8 +12,9 @@ maps), so the C-ABI receives exactly what ``ImmutableSegmentLoader`` would hand 
                    SegmentColumnarIndexCreator.java:589)
                  - sorted dict column: card x (startDocId, endDocId) BE int32, inclusive
                    (SortedIndexReaderImpl.java:114-116)
-                 - raw (no-dictionary) fixed-width column: chunk format v2/v3 PASS_THROUGH
+                 - raw (no-dictionary) fixed-width column: chunk format v2..v5, any ChunkCompressionType
                    (BaseChunkForwardIndexWriter.java:40-160)
+                 - raw STRING column: var-byte chunks v2 / v3 (VarByteChunkForwardIndexWriter.java:37-158)
 * inverted index (card+1) BE u32 absolute offsets + portable Roaring bitmaps
                  (BitmapInvertedIndexWriter.java:35-156)
 """
@@ -214,6 +215,38 @@ def _chunk_forward(values: np.ndarray, dt: DataType, docs_per_chunk: int = 1000,
     return header + offs + b"".join(chunks)
 
 
+def _var_byte_forward(values, docs_per_chunk: int = 1000, version: int = 3, compression: str = "PASS_THROUGH") -> bytes:
+    """Var-byte chunk forward index of a raw STRING column (VarByteChunkForwardIndexWriter.java:37-158 over the
+    BaseChunkForwardIndexWriter header): the 7-int header with lengthOfLongestEntry as the entry size, the chunk
+    offsets, then per chunk -- through its codec -- numDocsPerChunk BE int start offsets (0 for the absent rows of a
+    partial chunk) followed by the values' UTF-8 bytes. The chunk ends at its last value (the writer flips its buffer
+    at the write position)."""
+    if version not in (2, 3):
+        raise ValueError(f"illegal chunk writer version {version} for variable-length values")
+    codec = CHUNK_COMPRESSION[compression]
+    enc = [str(s).encode("utf-8") for s in np.asarray(values).tolist()]
+    n = len(enc)
+    longest = max((len(e) for e in enc), default=0)
+    num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
+    off_size = 4 if version == 2 else 8
+    header = np.array([version, num_chunks, docs_per_chunk, longest, n, codec, 7 * 4], dtype=">i4").tobytes()
+    offsets, chunks = [], []
+    pos = 7 * 4 + num_chunks * off_size
+    for c in range(num_chunks):
+        rows = enc[c * docs_per_chunk:(c + 1) * docs_per_chunk]
+        starts = np.zeros(docs_per_chunk, dtype=">i4")
+        p = docs_per_chunk * 4
+        for j, e in enumerate(rows):
+            starts[j] = p
+            p += len(e)
+        body = _compress_chunk(starts.tobytes() + b"".join(rows), codec)
+        offsets.append(pos)
+        chunks.append(body)
+        pos += len(body)
+    offs = np.asarray(offsets, dtype=">i4" if version == 2 else ">i8").tobytes()
+    return header + offs + b"".join(chunks)
+
+
 class SegmentCreator:
     """Builds an ImmutableSegment from column arrays (``SegmentIndexCreationDriverImpl`` role)."""
 
@@ -266,9 +299,10 @@ class SegmentCreator:
 
     def _build_column(self, name, dt, vals, n) -> ColumnIndexes:
         if name in self.raw:
-            if dt == DataType.STRING:
-                raise NotImplementedError("raw STRING forward index is out of scope")
             meta = ColumnMetadata(name, dt, n, 0, 0, False, False, False)
+            if dt == DataType.STRING:
+                return ColumnIndexes(meta, _var_byte_forward(vals, self.docs_per_chunk, min(self.raw_version, 3),
+                                                             self.compression.get(name, "PASS_THROUGH")))
             return ColumnIndexes(meta, _chunk_forward(vals, dt, self.docs_per_chunk, self.raw_version,
                                                       self.compression.get(name, "PASS_THROUGH")))
         uniq, ids = _sorted_unique(vals, dt)

@@ -62,7 +62,11 @@ hipError_t launch_trim_order_terms(const double *, const int64_t *, const OrderT
 }
 hipError_t launch_trim_gather(const int32_t *, int64_t, int32_t, int64_t, const int64_t *, const double *, const int64_t *,
                               const uint8_t *, int64_t *, double *, int64_t *, uint8_t *, hipStream_t) { return hipSuccess; }
-hipError_t launch_chunk_decode(int, int, const uint8_t *, const RawChunk *, int32_t, int32_t, int32_t, size_t, uint8_t *, int32_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_chunk_decode(int, int, const uint8_t *, const RawChunk *, int32_t, int32_t, int32_t, size_t, uint8_t *, int32_t *, int32_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_varbyte_offsets(const uint8_t *, const uint64_t *, const int32_t *, int32_t, int64_t, uint64_t *, uint64_t *,
+                                  void *, size_t *temp_bytes, int32_t *, hipStream_t) { *temp_bytes = 64; return hipSuccess; }
+hipError_t launch_varbyte_copy(const uint8_t *, const uint64_t *, const int32_t *, int32_t, int64_t, const uint64_t *, uint8_t *,
+                               hipStream_t) { return hipSuccess; }
 size_t chunk_decode_extra_lds(int, int32_t) { return 0; }
 hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }

@@ -129,3 +129,29 @@ def test_gpu_filtered_group_by_skip_empty_groups_one_pass(ft):
     assert op.one_pass is not None and op.one_pass.num_programs == 2
     op.close()
     _check_vs_oracle(sql, ft)
+
+
+# ---- CASE statistics: one scan per original filter -------------------------------------------------------------
+CASE_STATS_TWINS = [
+    # an unfiltered CASE query is a plain AggregationOperator: numEntriesScannedInFilter = its WHERE's scan
+    (EXTRA[3], "SELECT SUM(INT_COL) FROM MyTable WHERE INT_COL > 100"),
+    # CASE under a FILTER + unfiltered CASE functions, grouped: one info per original filter, as the twin's
+    (EXTRA[2], "SELECT SUM(INT_COL) FILTER(WHERE BOOLEAN_COL = 0), SUM(INT_COL) FROM MyTable GROUP BY STATIC_INT_COL"),
+    ("SELECT SUM(CASE WHEN NO_INDEX_COL < 5000 THEN INT_COL ELSE 0 END) FROM MyTable WHERE NO_INDEX_COL > 10 "
+     "AND INT_COL < 29000", "SELECT SUM(INT_COL) FROM MyTable WHERE NO_INDEX_COL > 10 AND INT_COL < 29000"),
+]
+
+
+@pytest.mark.parametrize("pair", CASE_STATS_TWINS, ids=["where", "filter-group-by", "two-leaf-where"])
+def test_gpu_case_entries_scanned_in_filter(pair, ft):
+    """The reference evaluates the WHENs in the transform (CaseTransformFunction), so a CASE query scans each
+    original filter once; the GPU's branch programs (filter AND WHEN) must not add their scans
+    (phip_query_desc.stats_programs). The twin without CASE has the same original filters."""
+    pm = GpuInstancePlanMaker()
+    counts = []
+    for sql in pair:
+        op = pm.make_instance_plan(parse(sql), ft)
+        blk = op.next_block()
+        op.close()
+        counts.append(blk.stats.num_entries_scanned_in_filter)
+    assert counts[0] == counts[1], counts
