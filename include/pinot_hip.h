@@ -66,7 +66,8 @@
                               * FixedBytePower2ChunkSVForwardIndexReader): PASS_THROUGH, or SNAPPY / LZ4 /
                               * LZ4_LENGTH_PREFIXED / ZSTANDARD / GZIP decoded on the GPU at load (a malformed chunk
                               * fails the load); v1 (4-int header, SNAPPY chunks: BaseChunkForwardIndexReader.java:86-95)
-                              * as well */
+                              * as well. A STRING column: VarByteChunkForwardIndexWriter v1..v3 chunks (per chunk
+                              * numDocsPerChunk BE int start offsets, then the UTF-8 bytes), any codec */
 
 typedef struct phip_column_desc {
   const char *name;

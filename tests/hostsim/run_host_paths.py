@@ -72,6 +72,33 @@ os.environ["PHIP_GB_HASH"] = "1"  # the hash-table group-by's host path (allocat
 pm.make_instance_plan(parse("SELECT g, h, COUNT(*), SUM(m), DISTINCTCOUNTHLL(m) FROM t GROUP BY g, h"), gs).next_block()
 pm.make_instance_plan(parse(fgb), gs).next_block()
 del os.environ["PHIP_GB_HASH"]
+# raw STRING columns: var-byte chunk parsing at load (every codec; the stub decodes nothing), RAW_STRING leaves
+# (the library's sorted, deduplicated set copy; range bounds), CASE statistics programs
+rs = []
+for k, codec in enumerate(("PASS_THROUGH", "SNAPPY", "ZSTANDARD", "GZIP")):
+    c = SegmentCreator(f"rs{k}", no_dictionary_columns=["s"], raw_compression={"s": codec}, docs_per_chunk=97)
+    c.add_column("s", DataType.STRING, np.array([["", "a", "ab", "\U0001F600", "\uffff", "b" * 30][x]
+                                                for x in rng.integers(0, 6, 3001 + k)]))
+    c.add_column("h", DataType.INT, rng.integers(0, 5, 3001 + k))
+    rs.append(GpuSegment(c.build()))
+in_list = ", ".join(f"'v{i}'" for i in range(3000)) + ", 'a', 'a', ''"
+for q in (f"SELECT COUNT(*), SUM(h) FROM t WHERE s IN ({in_list})",
+          "SELECT COUNT(*) FROM t WHERE s NOT IN ('a', 'ab') AND h > 1",
+          "SELECT COUNT(*) FROM t WHERE s BETWEEN 'a' AND '\uffff' OR s < ''",
+          "SELECT COUNT(*) FROM t WHERE s > 'a'",
+          "SELECT SUM(CASE WHEN s = 'a' THEN h ELSE 0 END), COUNT(*) FROM t WHERE h <> 2"):
+    pm.make_instance_plan(parse(q), rs).next_block()
+from pinot_amd.engine.plan import _Leaf  # noqa: E402
+op = GpuCombineOperator(parse("SELECT COUNT(*) FROM t WHERE s = 'a'"), rs[:1], 100_000)
+op.trees = [_Leaf(_lib.LEAF_RAW_STRING_SET, "s", ids=np.array([2, 0, 5, 3], dtype=np.int32))]  # offsets past the end
+try:
+    op.next_block()
+    raise SystemExit("malformed RAW_STRING_SET accepted")
+except _lib.PhipError:
+    pass
+op.close()
+for g in rs:
+    g.destroy()
 for g in gs:
     g.destroy()
 for s in segs.values():
