@@ -128,7 +128,8 @@ __device__ __forceinline__ int decode_chunk(const uint8_t *__restrict__ in, int 
       ulen |= (b & 0x7fu) << shift;
       if (!(b & 0x80u)) break;
     }
-    if (ulen != (uint32_t)cap) return -1;
+    if (ulen > (uint32_t)cap) return -1;  // (fixed-width chunks: the kernel then checks ulen = docs x entry)
+    cap = (int)ulen;
     while (ip < n) {
       uint32_t tag = lds_byte(in, ip++);
       uint32_t len, off;
@@ -173,7 +174,7 @@ __device__ __forceinline__ int decode_chunk(const uint8_t *__restrict__ in, int 
       }
       op += (int)len;
     }
-    return op;
+    return op == cap ? op : -1;
   }
   // LZ4 block format
   while (ip < n) {
@@ -289,6 +290,46 @@ __global__ __launch_bounds__(64) void chunk_decode_kernel(const uint8_t *__restr
   }
 }
 
+// Var-byte chunks larger than the LDS window (Pinot's derived 1 MiB chunks, long strings): the same decoders with
+// the compressed bytes read from and the output written to HBM -- one single-wave workgroup per chunk, the sequence
+// parse wave-uniform, literal / match copies by the 64 lanes with a workgroup barrier between dependent copies
+// (a single-wave workgroup stays on one CU, whose L1 the barrier's fences keep coherent for it); the entropy codecs
+// run on lane 0 with their workspace in LDS and the zstd literal buffer in HBM scratch.
+template <int kCodec>
+__global__ __launch_bounds__(64) void chunk_decode_global_kernel(const uint8_t *__restrict__ blob,
+                                                                 const RawChunk *__restrict__ chunks, int32_t nchunks,
+                                                                 uint8_t *__restrict__ out, int32_t *__restrict__ err,
+                                                                 int32_t *__restrict__ sizes, uint8_t *__restrict__ lits,
+                                                                 uint64_t lits_stride) {
+  __shared__ __align__(16) uint8_t ws[kCodec == 2 ? ((codec::kZstdWs + 15) & ~15) : (kCodec == 5 ? ((codec::kInflateWs + 15) & ~15) : 16)];
+  __shared__ int32_t got_s;
+  const int lane = threadIdx.x;
+  for (int32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint8_t *in = blob + chunks[c].src;
+    uint8_t *o = out + chunks[c].dst;
+    const int n = (int)chunks[c].csize, cap = (int)chunks[c].usize;
+    int got;
+    if (kCodec == 2 || kCodec == 5) {
+      if (lane == 0)
+        got_s = kCodec == 5 ? codec::pinot_gzip_chunk(in, n, o, cap, ws)
+                            : codec::zstd_decompress(in, n, o, cap, lits + (uint64_t)c * lits_stride, cap, ws);
+      __syncthreads();
+      got = got_s;
+    } else if (kCodec == 4) {
+      const int want = n < 4 ? -2 : (int)(lds_byte(in, 0) | (lds_byte(in, 1) << 8) | (lds_byte(in, 2) << 16) | (lds_byte(in, 3) << 24));
+      got = n < 4 ? -1 : decode_chunk<3>(in + 4, n - 4, o, cap, lane);
+      if (got != want) got = -1;
+    } else {
+      got = decode_chunk<kCodec>(in, n, o, cap, lane);
+    }
+    if (lane == 0) {
+      if (got < 0 || got > cap) atomicMax(err, c + 1);
+      else sizes[c] = got;
+    }
+    __syncthreads();
+  }
+}
+
 template <int kCodec>
 static hipError_t launch_chunk_decode_codec(int entry, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks,
                                             int32_t out_cap, int32_t in_cap, size_t lds, uint8_t *out, int32_t *err,
@@ -388,6 +429,21 @@ __global__ void varbyte_copy_kernel(const uint8_t *__restrict__ stage, const uin
   if (!varbyte_span(stage, chunk_base, chunk_size, per_chunk, d, src, l)) return;  // (the lengths pass failed the load)
   const uint64_t o = off[d];
   for (uint32_t i = 0; i < l; i++) out[o + i] = stage[src + i];
+}
+
+hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
+                                      int32_t *err, int32_t *sizes, uint8_t *lits, uint64_t lits_stride, hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+  const int grid = nchunks < (1 << 20) ? nchunks : (1 << 20);
+  switch (codec) {
+    case 1: chunk_decode_global_kernel<1><<<grid, 64, 0, s>>>(blob, chunks, nchunks, out, err, sizes, lits, lits_stride); break;
+    case 2: chunk_decode_global_kernel<2><<<grid, 64, 0, s>>>(blob, chunks, nchunks, out, err, sizes, lits, lits_stride); break;
+    case 3: chunk_decode_global_kernel<3><<<grid, 64, 0, s>>>(blob, chunks, nchunks, out, err, sizes, lits, lits_stride); break;
+    case 4: chunk_decode_global_kernel<4><<<grid, 64, 0, s>>>(blob, chunks, nchunks, out, err, sizes, lits, lits_stride); break;
+    case 5: chunk_decode_global_kernel<5><<<grid, 64, 0, s>>>(blob, chunks, nchunks, out, err, sizes, lits, lits_stride); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // lengths of docs 0..n-1 (len[n] = 0) and their exclusive scan into off[0..n]; temp == null: scan size query only

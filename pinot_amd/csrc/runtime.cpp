@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cmath>
 #include <cstdarg>
@@ -90,6 +91,8 @@ hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t 
                                const uint64_t *table, const uint32_t *hll, int32_t nhll, int32_t log2m,
                                int64_t *keys_out, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
 hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s);
+hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
+                                      int32_t *err, int32_t *sizes, uint8_t *lits, uint64_t lits_stride, hipStream_t s);
 hipError_t launch_varbyte_offsets(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
                                   int32_t per_chunk, int64_t n, uint64_t *len, uint64_t *off, void *temp,
                                   size_t *temp_bytes, int32_t *err, hipStream_t s);
@@ -579,17 +582,24 @@ static int32_t load_varbyte(const phip_column_desc &c, Segment &seg, ColumnStore
     const uint32_t out_cap = (uint32_t)stride;
     const uint32_t in_cap = (uint32_t)round_up(max_c + 8, 16);
     const size_t lds = out_cap + in_cap + chunk_decode_extra_lds(comp, (int32_t)out_cap);
-    if (lds > 163840 - 1024)
-      return fail(PHIP_ERR_UNSUPPORTED, "column %s: var-byte chunks of %u -> %llu bytes exceed the 159 KiB LDS decode window",
-                  c.name, max_c, (unsigned long long)max_u);
     void *dec, *table;
     HIP_TRY(hipMalloc(&dec, stride * num_chunks + 16));
     temps.push_back(dec);
     HIP_TRY(hipMalloc(&table, sizeof(RawChunk) * num_chunks));
     temps.push_back(table);
     HIP_TRY(hipMemcpyAsync(table, chunks.data(), sizeof(RawChunk) * num_chunks, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_chunk_decode(comp, 1, (const uint8_t *)blob, (const RawChunk *)table, num_chunks, (int32_t)out_cap,
-                                (int32_t)in_cap, lds, (uint8_t *)dec, (int32_t *)err, (int32_t *)dsize, st));
+    if (lds <= 163840 - 1024) {  // the chunk and its output in LDS (as fixed-width chunks)
+      HIP_TRY(launch_chunk_decode(comp, 1, (const uint8_t *)blob, (const RawChunk *)table, num_chunks, (int32_t)out_cap,
+                                  (int32_t)in_cap, lds, (uint8_t *)dec, (int32_t *)err, (int32_t *)dsize, st));
+    } else {  // beyond the LDS window (e.g. Pinot's derived 1 MiB chunks): decoded from and into HBM
+      void *lits = nullptr;
+      if (comp == 2) {
+        HIP_TRY(hipMalloc(&lits, stride * num_chunks + 16));
+        temps.push_back(lits);
+      }
+      HIP_TRY(launch_chunk_decode_global(comp, (const uint8_t *)blob, (const RawChunk *)table, num_chunks, (uint8_t *)dec,
+                                         (int32_t *)err, (int32_t *)dsize, (uint8_t *)lits, stride, st));
+    }
     int32_t bad = 0;
     HIP_TRY(hipMemcpyAsync(&bad, err, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2916,12 +2926,18 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   }
   if (mode != EXEC_FINISH && P.partial_pending)  // the caller still owns the table (it may be all-reducing it)
     return fail(PHIP_ERR_INVALID, "plan has a pending partial table: phip_plan_finish or phip_plan_abandon_partial first");
+  // measurement only (PHIP_HOST_TRACE=1): host microseconds per phase of this call, one stderr line per execution
+  static const bool host_trace = getenv("PHIP_HOST_TRACE") != nullptr;
+  using hclock = std::chrono::steady_clock;
+  hclock::time_point ht[5];
+  if (host_trace) ht[0] = hclock::now();
   HIP_TRY(hipSetDevice(dev->ordinal));
   LaneGuard lg{dev};
   {
     int32_t lrc = acquire_lane(dev, &lg.lane);
     if (lrc) return lrc;
   }
+  if (host_trace) ht[1] = hclock::now();
   hipStream_t st = lg.lane->stream;
   Workspace &ws = lg.lane->ws;
   // Opt-in (PHIP_GRAPH=1): replay a captured hipGraph from the second execution on. Measured on
@@ -2950,6 +2966,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     int32_t rc = enqueue_plan(P, st);
     if (rc) return rc;
   }
+  if (host_trace) ht[2] = hclock::now();
   if (mode != EXEC_FINISH) {
     P.executions++;
     if (P.total_work == 0) {  // no kernel ran: nothing matched, no registers set
@@ -3164,6 +3181,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   } else {
     HIP_TRY(hipStreamSynchronize(st));
   }
+  if (host_trace) ht[3] = hclock::now();
   // selection: the filter's tile masks -> rows (its own launches; event 2 / 4 then bracket the gather kernel)
   std::vector<int64_t> sel_kept;
   int64_t sel_rows = 0;
@@ -3292,6 +3310,12 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   lg.done = true;
   if (out_result) {
     *out_result = &impl.release()->pub;
+  }
+  if (host_trace) {
+    ht[4] = hclock::now();
+    auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(ht[b] - ht[a]).count(); };
+    fprintf(stderr, "phip_host_trace lane %.1f enqueue %.1f sync %.1f result %.1f total %.1f device %.1f\n", us(0, 1),
+            us(1, 2), us(2, 3), us(3, 4), us(0, 4), 1000.0 * r.device_ms);
   }
   return PHIP_OK;
 }
