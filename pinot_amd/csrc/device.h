@@ -80,7 +80,10 @@ struct DevCol {
   int32_t lds_off;   // filter kernel: byte offset of this column's tile region in the stage slot, -1 = not staged
   int32_t hll_rows;  // > 0: `raw` holds 2^hll_rows u8 HLL registers per doc (star-tree DISTINCTCOUNTHLL pair)
   const uint64_t *str_off;  // raw STRING: doc d's UTF-8 bytes are raw[str_off[d] .. str_off[d+1])
+  const uint32_t *planes;   // bit-sliced copy of `words` (bits <= kBitSliceMaxBits), or null: per 2048-doc tile,
+                            // plane k (bit bits-1-k of the id) as 64 lane words, bit 31-g of lane l = doc 64g + l
 };
+constexpr int kBitSliceMaxBits = 12;
 
 // One source the filter wave copies into its LDS stage slot for every tile (LDS-DMA, 1 KiB per
 // wave-instruction): a fixed-bit filter column (256*b bytes per 2048-doc tile) or the dense doc words of
@@ -101,10 +104,10 @@ constexpr double kConjSparseSel = 1.0 / 16;  // ... taken only when the first le
 struct ConjLeaf {
   int32_t lds_off;  // staged region in the ring slot
   int32_t bits;
-  int32_t kind;     // 0: dict-id range, 1: dict-id set over card <= 64
-  uint32_t lo;      // range: lo << (32 - bits)
-  uint32_t span;    // range: (hi - lo) << (32 - bits)
-  int32_t pad;
+  int32_t kind;     // 0: dict-id range, 1: dict-id set over card <= 64, 2: dict-id range over the bit-sliced planes
+  uint32_t lo;      // range: lo << (32 - bits); bit-sliced: the first id of the range
+  uint32_t span;    // range: (hi - lo) << (32 - bits); bit-sliced: the last id of the range (inclusive)
+  int32_t pad;      // bit-sliced: 1 = lower bound to test, 2 = upper bound to test
   uint64_t set_mask;
 };
 
@@ -140,7 +143,8 @@ struct DevSeg {
   int32_t fused_defer;  // fused aggregation, no value column streamed with the tile (sparse program): matched docs
                         // collect across tiles in the wave's ring and their columns are gathered from HBM once
                         // per kFusedBatch x 64 docs (the gathers do not stall the stream every tile)
-  int32_t pad_seg;
+  int32_t conj_bs;      // 1: every conj leaf is a bit-sliced range (kind 2, staged planes); the AND is computed in
+                        // the lane-major tile layout directly
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
   DevCol cols[kMaxQueryColumns];
@@ -179,6 +183,7 @@ struct DevFilter {
   int32_t probe;         // measurement only (PHIP_FILTER_PROBE): 1 = stream the tiles, skip the evaluation
   int32_t contig_inline;  // 1: range scans of the contiguous evaluator inline (0: through contig_scan_any; A/B)
   uint32_t stats_programs;  // programs whose scans count as entries scanned in filter (bit p = program p)
+  int32_t mask_nt;          // tile masks stored non-temporally (PHIP_MASK_NT measurement switch)
   uint32_t *mask_out;    // optional: [total_work][64] lane-major tile masks
   uint64_t *partials;    // [num_blocks][2]: matched docs, entries scanned in filter
   uint64_t *seg_matched; // [num query segments]

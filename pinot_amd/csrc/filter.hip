@@ -792,7 +792,77 @@ __device__ __forceinline__ uint32_t eval_conj_p(cseg_t &seg, const PHIP_LDS uint
   return to_lane_major<P>(r);
 }
 
+// Bit-sliced range leaf (ConjLeaf kind 2) over the lane's B plane words, most significant plane first: x >= lo and
+// x <= hi for the lane's 32 docs at once, comparing MSB first (gt / eq and lt / eq flags, BitWeaving/V). The
+// bounds are wave-uniform, so each plane costs one or two bitwise ops per side; lo == hi is an equality (one op per
+// plane).
+template <int B>
+__device__ __forceinline__ uint32_t bs_range(const PHIP_LDS uint32_t *pl, uint32_t lo, uint32_t hi, int sides) {
+  const int lane = lane_id();
+  uint32_t x[B];
+#pragma unroll
+  for (int k = 0; k < B; k++) x[k] = pl[64 * k + lane];
+  if (sides == 3 && lo == hi) {
+    uint32_t eq = ~0u;
+#pragma unroll
+    for (int k = 0; k < B; k++) eq &= ((lo >> (B - 1 - k)) & 1u) ? x[k] : ~x[k];
+    return eq;
+  }
+  uint32_t r = ~0u;
+  if (sides & 1) {  // x >= lo
+    uint32_t gt = 0u, eq = ~0u;
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      if ((lo >> (B - 1 - k)) & 1u) {
+        eq &= x[k];
+      } else {
+        gt |= eq & x[k];
+        eq &= ~x[k];
+      }
+    }
+    r = gt | eq;
+  }
+  if (sides & 2) {  // x <= hi
+    uint32_t lt = 0u, eq = ~0u;
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      if ((hi >> (B - 1 - k)) & 1u) {
+        lt |= eq & ~x[k];
+        eq &= x[k];
+      } else {
+        eq &= ~x[k];
+      }
+    }
+    r &= lt | eq;
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint32_t bs_range_any(const PHIP_LDS uint32_t *pl, int bits, uint32_t lo, uint32_t hi,
+                                              int sides) {
+  switch (bits) {
+#define PHIP_BSR(b) \
+  case b: return bs_range<b>(pl, lo, hi, sides);
+    PHIP_BSR(1) PHIP_BSR(2) PHIP_BSR(3) PHIP_BSR(4) PHIP_BSR(5) PHIP_BSR(6) PHIP_BSR(7) PHIP_BSR(8) PHIP_BSR(9)
+    PHIP_BSR(10) PHIP_BSR(11) PHIP_BSR(12)
+#undef PHIP_BSR
+  }
+  return 0u;
+}
+
+// AND of the bit-sliced range leaves, already lane-major (no transpose)
+__device__ __forceinline__ uint32_t eval_conj_bs(cseg_t &seg, const PHIP_LDS uint8_t *slot) {
+  uint32_t r = ~0u;
+  for (int i = 0; i < seg.conj; i++) {
+    const PHIP_CAS ConjLeaf &L = seg.conj_leaf[i];
+    r &= bs_range_any((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.lo, L.span, L.pad);
+    if (ballot(r != 0) == 0) break;  // every doc already rejected (AndDocIdSet short-circuit)
+  }
+  return r;
+}
+
 __device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_t *slot, uint32_t valid) {
+  if (seg.conj_bs) return valid & eval_conj_bs(seg, slot);
   switch (seg.conj_p) {
     case 8: return valid & eval_conj_p<8>(seg, slot);
     case 4: return valid & eval_conj_p<4>(seg, slot);
@@ -1300,7 +1370,11 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
     }
     if ((q.stats_programs >> seg.program) & 1u) scanned += scanned_t;  // (wave-uniform)
     lane_matched += (uint32_t)__popc(mask);
-    if (st) ((PHIP_GLB uint32_t *)q.mask_out)[(size_t)t * 64 + lane] = mask;
+    if (st) {
+      PHIP_GLB uint32_t *mo = (PHIP_GLB uint32_t *)q.mask_out + (size_t)t * 64 + lane;
+      if (q.mask_nt) __builtin_nontemporal_store(mask, mo);
+      else *mo = mask;
+    }
     if constexpr (NA > 0) {
       if (seg.fused_defer) fused_defer<NA>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail, sda, sdb, acc);
       else fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, docring, sda, sdb, acc);

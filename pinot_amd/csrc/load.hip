@@ -374,6 +374,45 @@ hipError_t launch_chunk_decode(int codec, int entry, const uint8_t *blob, const 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Bit-sliced copy of a fixed-bit forward index (the BitWeaving/V layout) for the range leaves of the conjunctive
+// filter: per 2048-doc tile, plane k (k = 0: the id's most significant bit) is 64 lane words with bit 31-g of lane
+// l = that bit of doc 64g + l -- the tile-mask layout, so a range test over a lane's 32 docs costs a few bitwise
+// operations per plane instead of three per doc. One wave per tile; padded docs decode from the guard words.
+// ------------------------------------------------------------------------------------------------
+template <int B>
+__global__ __launch_bounds__(256) void bitslice_kernel(const uint32_t *__restrict__ words, int64_t ntiles,
+                                                       uint32_t *__restrict__ planes) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= ntiles) return;
+  uint32_t pl[B];
+#pragma unroll
+  for (int k = 0; k < B; k++) pl[k] = 0;
+  for (int g = 0; g < 32; g++) {
+    const uint64_t doc = (uint64_t)t * 2048 + 64 * g + lane;
+    const uint32_t id = decode_bits(words, doc * B, B);
+#pragma unroll
+    for (int k = 0; k < B; k++) pl[k] |= ((id >> (B - 1 - k)) & 1u) << (31 - g);
+  }
+#pragma unroll
+  for (int k = 0; k < B; k++) planes[((size_t)t * B + k) * 64 + lane] = pl[k];
+}
+
+hipError_t launch_bitslice(const uint32_t *words, int32_t bits, int64_t ntiles, uint32_t *planes, hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)((ntiles + 3) / 4);
+  switch (bits) {
+#define PHIP_BSL(b) \
+  case b: bitslice_kernel<b><<<grid, 256, 0, s>>>(words, ntiles, planes); break;
+    PHIP_BSL(1) PHIP_BSL(2) PHIP_BSL(3) PHIP_BSL(4) PHIP_BSL(5) PHIP_BSL(6) PHIP_BSL(7) PHIP_BSL(8) PHIP_BSL(9)
+    PHIP_BSL(10) PHIP_BSL(11) PHIP_BSL(12)
+#undef PHIP_BSL
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Raw STRING columns: var-byte chunks (VarByteChunkForwardIndexWriter.java:37-158 -- per chunk numDocsPerChunk BE
 // int start offsets, then the values' UTF-8 bytes) -> one contiguous byte array + u64 doc offsets, so a predicate
 // reads doc d as bytes [off[d], off[d+1]). chunk_base / chunk_size locate each chunk in `stage` (the forward

@@ -93,6 +93,7 @@ hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t 
 hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s);
 hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
                                       int32_t *err, int32_t *sizes, uint8_t *lits, uint64_t lits_stride, hipStream_t s);
+hipError_t launch_bitslice(const uint32_t *words, int32_t bits, int64_t ntiles, uint32_t *planes, hipStream_t s);
 hipError_t launch_varbyte_offsets(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
                                   int32_t per_chunk, int64_t n, uint64_t *len, uint64_t *off, void *temp,
                                   size_t *temp_bytes, int32_t *err, hipStream_t s);
@@ -306,6 +307,7 @@ struct ColumnStore {
   void *raw = nullptr;        // LE raw values (raw STRING: the values' UTF-8 bytes, back to back)
   uint64_t *str_off = nullptr;  // raw STRING: num_docs + 1 byte offsets into raw
   uint64_t str_total = 0;       // raw STRING: bytes of all values
+  uint32_t *planes = nullptr;   // bit-sliced copy of words (fixed-bit columns of <= kBitSliceMaxBits bits)
   std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
   std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
   std::map<int, uint32_t *> hll;      // per log2m
@@ -705,6 +707,16 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
                     (unsigned long long)c.forward_bytes, (unsigned long long)need);
       HIP_TRY(hipMemcpyAsync(cs.words, c.forward, need, hipMemcpyHostToDevice, st));
       HIP_TRY(launch_bswap32(cs.words, ceil_div(need, 4), st));
+      // the bit-sliced copy for conjunctive range leaves (load.hip bitslice_kernel): 256 x bits bytes per tile,
+      // as many as the packed words -- narrow columns only (a range costs ~4 ops per plane per 32 docs there)
+      if (cs.bits <= kBitSliceMaxBits && getenv("PHIP_NO_BITSLICE_LOAD") == nullptr) {
+        const int64_t ntiles = ceil_div(std::max<int64_t>(n, 1), kTileDocs);
+        void *pp;
+        rc = dev_alloc(seg, (size_t)ntiles * cs.bits * 256, &pp);
+        if (rc) return rc;
+        cs.planes = (uint32_t *)pp;
+        HIP_TRY(launch_bitslice(cs.words, cs.bits, ntiles, cs.planes, st));
+      }
     } else if (c.fwd_kind == PHIP_FWD_SORTED) {
       if (c.forward_bytes != 8ull * c.cardinality)
         return fail(PHIP_ERR_INVALID, "column %s: sorted index must be card x 8 bytes", c.name);
@@ -1677,6 +1689,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dc.has_dict = !no_dict(cs);
       dc.hll_rows = cs.hll_log2m;
       dc.str_off = cs.str_off;
+      dc.planes = cs.planes;
       dc.lds_off = -1;
     }
     for (int a = 0; a < naggs; a++) {
@@ -2063,9 +2076,43 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       return lds_off;
     };
     int32_t inv_region = -2;  // -2: not added yet, -1: did not fit
+    // A program that is an AND of dict-id ranges (plus single sorted-index ranges) over columns with a bit-sliced
+    // copy stages the planes instead of the packed words and takes the bit-sliced conjunctive path (filter.hip
+    // eval_conj_bs); the packed words stay the source of every other use (values, the interpreter paths)
+    bool bs = getenv("PHIP_NO_BITSLICE") == nullptr && ds.node_end > ds.node_begin;
+    for (int i = ds.node_begin; i < ds.node_end && bs; i++) {
+      const DevNode &dn = nodes[i];
+      if (dn.op == DOP_AND || (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_MATCH_ALL)) continue;
+      if (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_DOC_RANGES && dn.count == 1) continue;
+      bs = dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_DICT_RANGE && ds.cols[dn.column].planes != nullptr;
+    }
+    if (bs) {  // every column's planes must fit the slot (else the packed words, as the interpreter reads them)
+      std::vector<int> cols_seen;
+      int64_t need = 0;
+      for (int i = ds.node_begin; i < ds.node_end; i++) {
+        const DevNode &dn = nodes[i];
+        if (dn.op != DOP_LEAF || dn.leaf_kind != PHIP_LEAF_DICT_RANGE) continue;
+        if (std::find(cols_seen.begin(), cols_seen.end(), dn.column) != cols_seen.end()) continue;
+        cols_seen.push_back(dn.column);
+        need += 256ll * ds.cols[dn.column].bits + 2 * kStagePad;
+      }
+      bs = (int)cols_seen.size() <= kMaxStage && need <= kSlotBudget;
+    }
+    std::vector<std::pair<int, int32_t>> bs_regions;  // column -> its planes' region
     for (int i = ds.node_begin; i < ds.node_end; i++) {
       DevNode &dn = nodes[i];
       if (dn.op != DOP_LEAF) continue;
+      if (bs && dn.leaf_kind == PHIP_LEAF_DICT_RANGE) {
+        const DevCol &dc = ds.cols[dn.column];
+        int32_t r = -2;
+        for (const auto &p : bs_regions) r = p.first == dn.column ? p.second : r;
+        if (r == -2) {
+          r = add_region((const uint8_t *)dc.planes, 256 * dc.bits);
+          bs_regions.push_back({dn.column, r});
+        }
+        dn.lds_off = r;  // (fits: checked above)
+        continue;
+      }
       if (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || dn.leaf_kind == PHIP_LEAF_DICT_SET) {
         DevCol &dc = ds.cols[dn.column];
         if (dc.lds_off < 0) dc.lds_off = add_region((const uint8_t *)dc.words, 256 * dc.bits);
@@ -2113,7 +2160,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       L.lds_off = dn.lds_off;
       L.bits = dn.bits;
       double sel;
-      if (dn.leaf_kind == PHIP_LEAF_DICT_RANGE) {
+      if (bs) {  // (every leaf a DICT_RANGE whose planes are staged)
+        L.kind = 2;
+        L.lo = (uint32_t)dn.lo;
+        L.span = (uint32_t)(dn.hi - 1);
+        L.pad = (dn.lo > 0 ? 1 : 0) | (dn.hi < card ? 2 : 0);  // (ids >= card never occur)
+        sel = double(dn.hi - dn.lo) / card;
+      } else if (dn.leaf_kind == PHIP_LEAF_DICT_RANGE) {
         L.kind = 0;
         L.lo = (uint32_t)dn.lo << (32 - dn.bits);
         L.span = (uint32_t)(dn.hi - dn.lo) << (32 - dn.bits);
@@ -2136,7 +2189,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       std::stable_sort(conj.begin(), conj.end(),
                        [](const std::pair<double, ConjLeaf> &a, const std::pair<double, ConjLeaf> &b) { return a.first < b.first; });
       ds.conj = (int32_t)conj.size();
-      ds.conj_sparse = 1;
+      ds.conj_bs = bs ? 1 : 0;
+      ds.conj_sparse = bs ? 0 : 1;
       for (size_t i = 1; i < conj.size(); i++) ds.conj_sparse &= conj[i].second.kind == 0 ? 1 : 0;
       // the per-doc walk pays when the first leaf leaves ~2 docs per lane; at a selectivity of 1/7 (unsorted SSB
       // Q1.1's D_YEAR) tiles often pass the per-tile bound yet the walk is slower than the dense leaves (filter kernel
@@ -2306,7 +2360,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       while (want > 2 && total_work < kMinTilesPerWave * (int64_t)dev->num_cus * want * kFilterWaves) want--;
     const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * fring_bytes : 0;  // fused doc rings
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
-      const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024 - 1024) / bpc - fring) / ((int64_t)kFilterWaves * stage_stride));
+      // a workgroup's share of the CU's 160 KiB, less 256 B for the kernel's static LDS (block partials)
+      const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024) / bpc - 256 - fring) / ((int64_t)kFilterWaves * stage_stride));
       if (nb >= 2) {
         nbuf = (int)nb;
         fbpc = bpc;
@@ -2398,6 +2453,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     fq.contig_inline = ie ? atoi(ie) : 1;
   }
   fq.stats_programs = q->stats_programs ? (uint32_t)q->stats_programs : 0xffffffffu;
+  {
+    const char *mn = getenv("PHIP_MASK_NT");  // measurement switch: non-temporal tile-mask stores
+    fq.mask_nt = mn ? atoi(mn) : 0;
+  }
   fq.min_dma = 0;
   for (size_t i = 0; i < dsegs.size(); i++)
     fq.min_dma = i == 0 ? dsegs[i].num_dma : std::min(fq.min_dma, dsegs[i].num_dma);
