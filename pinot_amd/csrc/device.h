@@ -104,7 +104,8 @@ constexpr double kConjSparseSel = 1.0 / 16;  // ... taken only when the first le
 struct ConjLeaf {
   int32_t lds_off;  // staged region in the ring slot
   int32_t bits;
-  int32_t kind;     // 0: dict-id range, 1: dict-id set over card <= 64, 2: dict-id range over the bit-sliced planes
+  int32_t kind;     // 0: dict-id range, 1: dict-id set over card <= 64, 2: dict-id range over the bit-sliced planes,
+                    // 3: a few ids (set_mask) over the bit-sliced planes
   uint32_t lo;      // range: lo << (32 - bits); bit-sliced: the first id of the range
   uint32_t span;    // range: (hi - lo) << (32 - bits); bit-sliced: the last id of the range (inclusive)
   int32_t pad;      // bit-sliced: 1 = lower bound to test, 2 = upper bound to test

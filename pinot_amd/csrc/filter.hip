@@ -838,11 +838,30 @@ __device__ __forceinline__ uint32_t bs_range(const PHIP_LDS uint32_t *pl, uint32
   return r;
 }
 
+// a few ids (set bits of `set`, wave-uniform): OR of equalities
+template <int B>
+__device__ __forceinline__ uint32_t bs_set(const PHIP_LDS uint32_t *pl, uint64_t set) {
+  const int lane = lane_id();
+  uint32_t x[B];
+#pragma unroll
+  for (int k = 0; k < B; k++) x[k] = pl[64 * k + lane];
+  uint32_t r = 0u;
+  while (set) {
+    const uint32_t id = (uint32_t)__builtin_ctzll(set);
+    set &= set - 1;
+    uint32_t eq = ~0u;
+#pragma unroll
+    for (int k = 0; k < B; k++) eq &= ((id >> (B - 1 - k)) & 1u) ? x[k] : ~x[k];
+    r |= eq;
+  }
+  return r;
+}
+
 __device__ __forceinline__ uint32_t bs_range_any(const PHIP_LDS uint32_t *pl, int bits, uint32_t lo, uint32_t hi,
-                                              int sides) {
+                                              int sides, int kind, uint64_t set) {
   switch (bits) {
 #define PHIP_BSR(b) \
-  case b: return bs_range<b>(pl, lo, hi, sides);
+  case b: return kind == 3 ? bs_set<(b < 7 ? b : 6)>(pl, set) : bs_range<b>(pl, lo, hi, sides);
     PHIP_BSR(1) PHIP_BSR(2) PHIP_BSR(3) PHIP_BSR(4) PHIP_BSR(5) PHIP_BSR(6) PHIP_BSR(7) PHIP_BSR(8) PHIP_BSR(9)
     PHIP_BSR(10) PHIP_BSR(11) PHIP_BSR(12)
 #undef PHIP_BSR
@@ -855,7 +874,7 @@ __device__ __forceinline__ uint32_t eval_conj_bs(cseg_t &seg, const PHIP_LDS uin
   uint32_t r = ~0u;
   for (int i = 0; i < seg.conj; i++) {
     const PHIP_CAS ConjLeaf &L = seg.conj_leaf[i];
-    r &= bs_range_any((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.lo, L.span, L.pad);
+    r &= bs_range_any((const PHIP_LDS uint32_t *)(slot + L.lds_off), L.bits, L.lo, L.span, L.pad, L.kind, L.set_mask);
     if (ballot(r != 0) == 0) break;  // every doc already rejected (AndDocIdSet short-circuit)
   }
   return r;

@@ -1255,6 +1255,15 @@ static int java_str_cmp(const uint8_t *a, size_t al, const uint8_t *b, size_t bl
 // `count` int32 words: RAW_SET = [n][n + 1 byte offsets][the values' UTF-8 bytes]; RAW_RANGE = [lo_len][hi_len]
 // [lo_inclusive][hi_inclusive][lo bytes][hi bytes], a length of -1 = unbounded. The set is sorted in String order and
 // deduplicated here, so the kernel binary-searches it.
+// An IN / EQ set the bit-sliced conjunction tests as an OR of equalities: a dictionary of <= 64 ids (the leaf's
+// set_mask) and at most kBitSliceSetMax of them in the set (each costs one op per plane)
+constexpr int kBitSliceSetMax = 4;
+static bool bs_small_set(const DevNode &dn, const DevCol &dc) {
+  if (!dn.small_set || dc.card > 64) return false;
+  const uint64_t in_dict = dc.card >= 64 ? ~0ull : ((1ull << dc.card) - 1);
+  return __builtin_popcountll(dn.set_mask & in_dict) <= kBitSliceSetMax;
+}
+
 struct AuxFix {  // a leaf's node.aux = device base of the plan's blob + off
   size_t node;
   size_t off;
@@ -2084,14 +2093,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       const DevNode &dn = nodes[i];
       if (dn.op == DOP_AND || (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_MATCH_ALL)) continue;
       if (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_DOC_RANGES && dn.count == 1) continue;
-      bs = dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_DICT_RANGE && ds.cols[dn.column].planes != nullptr;
+      bs = dn.op == DOP_LEAF && ds.cols[dn.column].planes != nullptr &&
+           (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || (dn.leaf_kind == PHIP_LEAF_DICT_SET && bs_small_set(dn, ds.cols[dn.column])));
     }
     if (bs) {  // every column's planes must fit the slot (else the packed words, as the interpreter reads them)
       std::vector<int> cols_seen;
       int64_t need = 0;
       for (int i = ds.node_begin; i < ds.node_end; i++) {
         const DevNode &dn = nodes[i];
-        if (dn.op != DOP_LEAF || dn.leaf_kind != PHIP_LEAF_DICT_RANGE) continue;
+        if (dn.op != DOP_LEAF || (dn.leaf_kind != PHIP_LEAF_DICT_RANGE && dn.leaf_kind != PHIP_LEAF_DICT_SET)) continue;
         if (std::find(cols_seen.begin(), cols_seen.end(), dn.column) != cols_seen.end()) continue;
         cols_seen.push_back(dn.column);
         need += 256ll * ds.cols[dn.column].bits + 2 * kStagePad;
@@ -2102,7 +2112,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     for (int i = ds.node_begin; i < ds.node_end; i++) {
       DevNode &dn = nodes[i];
       if (dn.op != DOP_LEAF) continue;
-      if (bs && dn.leaf_kind == PHIP_LEAF_DICT_RANGE) {
+      if (bs && (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || dn.leaf_kind == PHIP_LEAF_DICT_SET)) {
         const DevCol &dc = ds.cols[dn.column];
         int32_t r = -2;
         for (const auto &p : bs_regions) r = p.first == dn.column ? p.second : r;
@@ -2160,7 +2170,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       L.lds_off = dn.lds_off;
       L.bits = dn.bits;
       double sel;
-      if (bs) {  // (every leaf a DICT_RANGE whose planes are staged)
+      if (bs && dn.leaf_kind == PHIP_LEAF_DICT_SET) {  // (a few ids of a dictionary of <= 64: bs_small_set)
+        L.kind = 3;
+        L.set_mask = dn.set_mask & (card >= 64 ? ~0ull : ((1ull << card) - 1));
+        sel = double(__builtin_popcountll(L.set_mask)) / card;
+      } else if (bs) {  // (every other leaf a DICT_RANGE whose planes are staged)
         L.kind = 2;
         L.lo = (uint32_t)dn.lo;
         L.span = (uint32_t)(dn.hi - 1);
