@@ -2093,8 +2093,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       const DevNode &dn = nodes[i];
       if (dn.op == DOP_AND || (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_MATCH_ALL)) continue;
       if (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_DOC_RANGES && dn.count == 1) continue;
-      bs = dn.op == DOP_LEAF && ds.cols[dn.column].planes != nullptr &&
-           (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || (dn.leaf_kind == PHIP_LEAF_DICT_SET && bs_small_set(dn, ds.cols[dn.column])));
+      bs = dn.op == DOP_LEAF && (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || dn.leaf_kind == PHIP_LEAF_DICT_SET) &&
+           ds.cols[dn.column].planes != nullptr &&
+           (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || bs_small_set(dn, ds.cols[dn.column]));
     }
     if (bs) {  // every column's planes must fit the slot (else the packed words, as the interpreter reads them)
       std::vector<int> cols_seen;
