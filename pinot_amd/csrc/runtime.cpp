@@ -1259,7 +1259,8 @@ static int java_str_cmp(const uint8_t *a, size_t al, const uint8_t *b, size_t bl
 // set_mask) and at most kBitSliceSetMax of them in the set (each costs one op per plane)
 constexpr int kBitSliceSetMax = 4;
 static bool bs_small_set(const DevNode &dn, const DevCol &dc) {
-  if (!dn.small_set || dc.card > 64) return false;
+  const bool on = getenv("PHIP_BS_SETS") != nullptr;  // opt-in until measured on the GPU (read per plan)
+  if (!on || !dn.small_set || dc.card > 64) return false;
   const uint64_t in_dict = dc.card >= 64 ? ~0ull : ((1ull << dc.card) - 1);
   return __builtin_popcountll(dn.set_mask & in_dict) <= kBitSliceSetMax;
 }

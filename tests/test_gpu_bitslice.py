@@ -53,11 +53,16 @@ def segs(gpu_lib):
         g.destroy()
 
 
+@pytest.mark.parametrize("sets", [False, True], ids=["ranges", "bs-sets"])
 @pytest.mark.parametrize("flt", _filters())
-def test_gpu_bitsliced_doc_sets(flt, segs, monkeypatch):
+def test_gpu_bitsliced_doc_sets(flt, sets, segs, monkeypatch):
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     from tests.test_gpu_parity import _assert_intermediates_equal, _words_from_mask
     raws, gs = segs
+    if sets:  # IN sets on the planes too (opt-in: PHIP_BS_SETS, read when a plan is prepared)
+        if " IN " not in flt:
+            pytest.skip("no IN set")
+        monkeypatch.setenv("PHIP_BS_SETS", "1")
     qc = parse(f"SELECT COUNT(*), SUM(m) FROM t WHERE {flt}")
     for raw, g in zip(raws, gs):
         want = _words_from_mask(executor.eval_filter(OracleSegment(raw), qc.filter))
