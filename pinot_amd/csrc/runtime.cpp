@@ -2278,8 +2278,18 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const double per_tile = est_docs / (double)std::max<int64_t>(1, total_work);
     double fuse_per_tile = 0.0;
     if (const char *fp = getenv("PHIP_FUSE_PER_TILE")) fuse_per_tile = atof(fp);  // measurement override
+    // Large scans fuse too since the bit-sliced conjunction (round 3): its light evaluation leaves the wave time to
+    // gather a deferred batch of matched docs' values, and the split's mask round trip is gone -- unsorted SSB
+    // Q1.1 / Q1.2 / Q1.3 p50 0.64 / 0.476 / 0.487 -> 0.62 / 0.385 / 0.476 ms, sorted Q1.1 unchanged
+    // (profiles/r03n_fuse_large_ab.log). Their value columns are gathered, not streamed with every tile (streaming
+    // LO_EXTENDEDPRICE over 293K tiles: 1.4 ms). PHIP_FUSE_LARGE=0 restores the size rule alone.
+    const bool big = total_work > kFuseMaxTiles;
+    const char *fl = getenv("PHIP_FUSE_LARGE");  // measurement override
+    bool bs_all = true;  // (the P-layout conjunction's heavier evaluation keeps the size rule)
+    for (const DevSeg &ds : dsegs) bs_all &= ds.conj == 0 || ds.conj_bs != 0;
+    const bool fuse_large = (fl ? atoi(fl) != 0 : true) && bs_all;
     bool fuse = conj_all && any_filter_prog && !group_by && nprog == 1 && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
-                (fe ? atoi(fe) != 0 : (total_work <= kFuseMaxTiles || (fuse_per_tile > 0 && per_tile <= fuse_per_tile)));
+                (fe ? atoi(fe) != 0 : (!big || fuse_large || (fuse_per_tile > 0 && per_tile <= fuse_per_tile)));
     bool any_value = false;
     for (int a = 0; a < naggs; a++) any_value |= dq.aggs[a].acc != ACC_COUNT;
     if (fuse && any_value) {
@@ -2298,7 +2308,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             DevCol &dc = ds.cols[c];
             if (!dc.has_dict || dc.lds_off >= 0) continue;
             const bool dense = seg_est[i] * (1024.0 / std::max(1, dc.bits)) >= kStreamValueMin;
-            if (!(sv ? atoi(sv) != 0 : dense)) continue;
+            if (!(sv ? atoi(sv) != 0 : (dense && !big))) continue;
             const int32_t bytes = 256 * dc.bits;
             // (DevSeg.stage holds kMaxStage sources; the fused kernel's cursor takes up to kMaxConj + kMaxAggStage)
             if (ds.num_stage >= std::min(kMaxStage, kMaxConj + kMaxAggStage) || off + bytes + 2 * kStagePad > kSlotBudget)
