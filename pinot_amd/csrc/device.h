@@ -23,8 +23,8 @@ constexpr int kFilterBlock = 256;
 constexpr int kFilterWaves = kFilterBlock / kWave;
 constexpr int kMaxRing = 8;           // LDS-DMA ring slots per wave
 constexpr int kFusedRingTile = 512;   // fused aggregation, per-tile mode: u16 tile-relative doc ids per wave
-constexpr int kFusedRingDefer = 1024; // fused aggregation, deferred mode: u32 segment doc ids per wave (one batch
-                                      // + a quarter tile)
+constexpr int kFusedRingDefer = 512;  // fused aggregation, deferred mode: u32 segment doc ids per wave (one batch
+                                      // + an eighth of a tile)
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;

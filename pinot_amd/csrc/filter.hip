@@ -1171,7 +1171,9 @@ __device__ __forceinline__ void fused_defer(cquery_t &aq, cseg_t &seg, const Til
   if (ballot(mask != 0) == 0) return;
   const TileRank r = rank_tile(mask);
   const int head0 = head;
-  const int npiece = head - tail + r.total <= kFusedRingDefer ? 1 : 4;
+  // the whole tile when the ring has room, else eighth tiles (8 lanes, <= 256 docs) each after draining the ring below
+  // one batch (< 256 pending + 256 <= kFusedRingDefer)
+  const int npiece = head - tail + r.total <= kFusedRingDefer ? 1 : 8;
   const int lanes = 64 / npiece;
   for (int p = 0; p < npiece; p++) {
     const int e = __builtin_amdgcn_readlane((int)r.incl, lanes * p + lanes - 1);
