@@ -2382,7 +2382,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // and small queries (every wave one or two tiles: latency) keep the default (tools/ab_env.sh, bpc A/B).
     const int64_t kMinTilesPerWave = 12;
     const int64_t waves_at = (int64_t)dev->num_cus * want * kFilterWaves;
-    if (!env && total_work >= 4 * waves_at)
+    // (a fused launch keeps the full width: its waves also wait on gathers -- sorted Q1.1 fused 0.201 -> 0.187 ms at
+    // 6 instead of 3 workgroups per CU, profiles/r03p_fused_bpc_ab.log)
+    if (!env && total_work >= 4 * waves_at && fused_naggs == 0)
       while (want > 2 && total_work < kMinTilesPerWave * (int64_t)dev->num_cus * want * kFilterWaves) want--;
     const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * fring_bytes : 0;  // fused doc rings
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
