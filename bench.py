@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROUND = "r03"
+ROUND = "r04"
 
 
 def load_layout(ssb, seg_per_gpu, world, rank, cols, seed, layout, keep_host):
@@ -134,9 +134,36 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # one more execution per query, outside the timed region: this rank's answers, checked against the CPU
+    # restatement on the same segments (check_parity)
+    answers = {q: ops[q].next_block() for q in queries}
     for op in ops.values():
         op.close()
-    return elapsed, lat, kstats
+    return elapsed, lat, kstats, answers
+
+
+def check_parity(queries, qcs, answers, raws, dist, torch):
+    """Every query's GPU answer on this rank (exact int64 SUM, numDocsScanned) against oracle/cpu_scan.c over the
+    same segments (its SUM is a double sum of integer products, exact below 2^53), outside the timed region; the
+    ranks agree on the verdict with one MIN all-reduce. Returns (ok, per-query detail)."""
+    from oracle import cpu_baseline
+    detail = {}
+    ok = True
+    threads = cpu_baseline.usable_cpus()[0]
+    for q in queries:
+        total, matched = cpu_baseline.Prepared(qcs[q], raws).run(threads)
+        blk = answers[q]
+        got = blk.results[0]
+        good = (isinstance(got, int) and abs(total) < 2 ** 53 and got == int(total)
+                and blk.stats.num_docs_scanned == matched)
+        ok &= good
+        detail[q] = {"sum": got, "cpu_sum": int(total), "docs": blk.stats.num_docs_scanned, "cpu_docs": matched,
+                     "equal": good}
+    if dist is not None:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item())
+    return ok, detail
 
 
 # kernel families of one query execution: a plain filter launch, a filter launch that aggregated its own tiles
@@ -208,6 +235,8 @@ def main():
     ap.add_argument("--layout", default="both", choices=["sorted", "unsorted", "both"],
                     help="headline = sorted (SURVEY.md §8d C2); both also measures the unsorted layout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the check of every query's answer against oracle/cpu_scan.c on the same segments")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", f"{ROUND}_traffic.json"),
                     help="HBM bytes per launch per kernel and layout from rocprofv3 --pmc passes (tools/traffic.py)")
     ap.add_argument("--seed", type=int, default=42)
@@ -254,14 +283,16 @@ def main():
     for li, layout in enumerate(layouts):
         t0 = time.time()
         gsegs, raws = load_layout(ssb, seg_per_gpu, world, rank, cols, args.seed, layout,
-                                  keep_host=want_cpu and li == 0)
+                                  keep_host=not args.no_parity or (want_cpu and li == 0))
         load_s = time.time() - t0
         head = gsegs[:head_segs]
         raws = raws[:head_segs]
         rows_per_rank = sum(s.num_docs for s in head)
-        elapsed, lat, kstats = run_layout(args, dist, queries, qcs, head, torch)
+        elapsed, lat, kstats, answers = run_layout(args, dist, queries, qcs, head, torch)
         res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(head),
                "lat": lat, "roofline": roofline(kstats, queries, traffic, layout, args.steps)}
+        if not args.no_parity:
+            res["parity"] = check_parity(queries, qcs, answers, raws, dist, torch)
         if want_c5 and li == 0:
             qc5 = parse(ssb.SSB_QUERIES["C5"])
             el5, lat5, blk5 = run_c5(args, dist, qc5, gsegs, torch)
@@ -274,6 +305,8 @@ def main():
                                   "in place over RCCL (int64 SUM + uint8 MAX for this query)"}
         for s in gsegs:
             s.destroy()
+        if not (want_cpu and li == 0):
+            del raws
         if want_cpu and li == 0:
             from oracle import cpu_baseline
             v, threads, reps, el, _ = cpu_baseline.time_queries([qcs[q] for q in queries], raws, min_seconds=10.0)
@@ -321,6 +354,13 @@ def main():
     }
     if "cpu" in head:
         out["cpu_baseline"] = head["cpu"]
+    if not args.no_parity:
+        ok = all(results[l]["parity"][0] for l in layouts)
+        out["parity"] = "checked" if ok else "MISMATCH"
+        out["parity_detail"] = {
+            "against": "oracle/cpu_scan.c on the same segments, every rank, outside the timed region: exact int64 "
+                       "SUM == the CPU's (integer-valued) double SUM, numDocsScanned == its matched docs",
+            **{l: results[l]["parity"][1] for l in layouts}}
     if "c5" in head:
         out["c5"] = head["c5"]
     if len(layouts) > 1:

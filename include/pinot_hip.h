@@ -285,6 +285,11 @@ typedef struct phip_result {
   int32_t reserved_select;
   const int32_t *select_types;
   const uint64_t *select_values;
+  /* Per segment of the query (num_segments_processed entries): the docs that passed its filter, summed over the
+   * filter programs -- the docs its GroupByOperator keyed, so min(this, key space, numGroupsLimit) bounds the
+   * group records the segment hands the combine (GroupByCombineOperator.java:128-157; the plan maker's
+   * minSegmentGroupTrimSize / groupTrimThreshold checks). For a phip_plan_finish result: this GPU's. */
+  const int64_t *segment_docs_matched;
 } phip_result;
 
 typedef struct phip_dictionary_view {

@@ -529,13 +529,50 @@ def _hll_group_registers(os_, col, docs, gid, ng, log2m):
 DEFAULT_NUM_GROUPS_LIMIT = 100_000  # InstancePlanMakerImplV2.java:78
 
 
-def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
+def _order_value(query, expr, key, vals):
+    """TableResizer's extractors (pinot-core/.../data/table/TableResizer.java:90-125): a group-by column's value, or an
+    aggregation's final result (extractFinalResult: COUNT / SUM / MIN / MAX as numbers, AVG = sum / count with -inf
+    for an empty group, MINMAXRANGE = max - min)."""
+    from pinot_amd.query.context import Function
+    gb = [str(e) for e in query.group_by]
+    if str(expr) in gb:
+        return key[gb.index(str(expr))]
+    for i, ag in enumerate(query.aggregations):
+        if isinstance(expr, Function) and expr.name == ag.function and ag.filter is None and \
+                (ag.function == "count" or (expr.args and expr.args[0] == ag.argument)):
+            v = vals[i]
+            if ag.function in ("count", "sum", "min", "max"):
+                return float(v)
+            if ag.function == "avg":
+                return float(v[0]) / v[1] if v[1] else float("-inf")
+            if ag.function == "minmaxrange":
+                return float(v[1]) - float(v[0])
+            break
+    raise NotImplementedError(f"oracle segment trim: ORDER BY {expr}")
+
+
+def _segment_trim(query, groups, exact, trim):
+    """GroupByOperator's segment-level trim (pinot-core/.../operator/query/GroupByOperator.java:118-133,
+    TableResizer.trimInSegmentResults): more than ``trim`` groups keep the top ``trim`` by the ORDER BY. Ties at the
+    boundary: the lowest mixed-radix group key (column 0 least significant), the GPU's rule (the reference's pick is
+    priority-queue order dependent)."""
+    if len(groups) <= trim:
+        return groups, exact
+    recs = sorted(groups.items(), key=lambda kv: tuple(reversed(kv[0])))
+    for ob in reversed(query.order_by):
+        recs.sort(key=lambda kv: _order_value(query, ob.expression, kv[0], kv[1]), reverse=not ob.ascending)
+    keep = [k for k, _ in recs[:trim]]
+    return {k: groups[k] for k in keep}, {k: exact[k] for k in keep}
+
+
+def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT, min_segment_group_trim_size=None):
     """Server-side execution over ImmutableSegments -> (results block, exact_sums).
 
     Group-by keeps, per segment, the first ``num_groups_limit`` distinct keys in doc order and drops the
     docs of later new keys (IntGroupIdMap.getGroupId returns INVALID_ID once the map holds
     groupIdUpperBound keys, DictionaryBasedGroupKeyGenerator.java:153-174,1023-1048); the block is flagged
-    when a segment's group count reaches the limit (GroupByOperator.java:116)."""
+    when a segment's group count reaches the limit (GroupByOperator.java:116). ``min_segment_group_trim_size``
+    (> 0, with ORDER BY): each segment's groups are trimmed before the merge (GroupByOperator.java:118-133)."""
     from pinot_amd.engine.results import (AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock,
                                           merge_intermediate)
     from pinot_amd.query.context import columns_of
@@ -582,6 +619,9 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT):
             continue
         seg_groups, seg_exact, reached = _group_segment(os_, query, docs, num_groups_limit)
         limit_reached |= reached
+        if query.order_by and min_segment_group_trim_size is not None and min_segment_group_trim_size > 0:
+            trim = max(5 * int(query.limit), min_segment_group_trim_size)  # GroupByUtils.getTableCapacity
+            seg_groups, seg_exact = _segment_trim(query, seg_groups, seg_exact, trim)
         for k, vals in seg_groups.items():
             exs = seg_exact[k]
             if k in groups:

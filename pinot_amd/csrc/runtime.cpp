@@ -882,6 +882,7 @@ struct ResultImpl {
   std::vector<uint64_t> sel_values;  // selection: [num_select][num_rows]
   std::vector<int32_t> sel_types;
   std::vector<std::shared_ptr<Device::Remap>> sel_dicts;  // per select column: query-global dictionary (STRING)
+  std::vector<int64_t> seg_docs;  // per segment: matched docs summed over the filter programs
 };
 
 // validate a preorder subtree; returns index after it or -1
@@ -3353,6 +3354,11 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     r.num_segments_processed = (int32_t)st6[4];
     r.num_segments_matched = (int32_t)st6[5];
   }
+  impl->seg_docs.assign(std::max(nseg, 1), 0);
+  for (int s = 0; s < nseg; s++)
+    for (int p = 0; p < P.nprog; p++)
+      impl->seg_docs[s] += has_filter ? (int64_t)segm[p * nseg + s] : P.slot_docs[p * nseg + s];
+  r.segment_docs_matched = impl->seg_docs.data();
   r.num_aggregations = naggs;
   r.num_groups = group_by ? ngroups : 1;
   r.num_group_by = P.num_group_by;

@@ -515,9 +515,10 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
         return op.next_block()
     if not getattr(op.query, "group_by", None) or not hasattr(op, "execute_partial"):
         return allreduce_block(op.next_block(), dist, group)
-    _lib.load(with_torch=True)  # (torch's HIP runtime: the library must share it, _lib.load)
     err = None
+    part = None
     try:
+        _lib.load(with_torch=True)  # (torch's HIP runtime: the library must share it, _lib.load)
         part = op.execute_partial()
     except Exception as e:  # noqa: BLE001 -- re-raised below, after the other ranks learned of it
         part, err = None, e
@@ -530,27 +531,36 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
     v = [int(x) for x in v.cpu().tolist()]
     if v[0]:
+        if part is not None:  # the plan must not stay blocked behind a table nobody will finish
+            op.abandon_partial()
         if err is not None:
             raise err
         raise RuntimeError("the query failed on another rank (distributed_block)")
     if v[1] == 0 and v[2] == -v[4] and v[3] == -v[5]:
-        any_f64 = v[6:6 + part.num_rows]
-        table, hll = partial_tensors(part)
-        kinds = [part.row_kinds[r] for r in range(part.num_rows)]
-        if table.device != dev:  # (gloo over host memory: stage through the host, CPU-communicator tests)
-            t2, h2 = table.to(dev), (hll.to(dev) if hll is not None else None)
-            kinds, stats = allreduce_partial_table(t2, h2, kinds, list(part.stats), dist, group, any_f64)
-            table.copy_(t2)
-            if hll is not None:
-                hll.copy_(h2)
-        else:
-            kinds, stats = allreduce_partial_table(table, hll, kinds, list(part.stats), dist, group, any_f64)
-        torch.cuda.current_stream(table.device).synchronize()
-        for r, k in enumerate(kinds):
-            part.row_kinds[r] = k
-        for i, x in enumerate(stats):
-            part.stats[i] = x
-        return op.finish(part)
+        try:
+            any_f64 = v[6:6 + part.num_rows]
+            table, hll = partial_tensors(part)
+            kinds = [part.row_kinds[r] for r in range(part.num_rows)]
+            if table.device != dev:  # (gloo over host memory: stage through the host, CPU-communicator tests)
+                t2, h2 = table.to(dev), (hll.to(dev) if hll is not None else None)
+                kinds, stats = allreduce_partial_table(t2, h2, kinds, list(part.stats), dist, group, any_f64)
+                table.copy_(t2)
+                if hll is not None:
+                    hll.copy_(h2)
+            else:
+                kinds, stats = allreduce_partial_table(table, hll, kinds, list(part.stats), dist, group, any_f64)
+            torch.cuda.current_stream(table.device).synchronize()
+            for r, k in enumerate(kinds):
+                part.row_kinds[r] = k
+            for i, x in enumerate(stats):
+                part.stats[i] = x
+            return op.finish(part)
+        except BaseException:
+            try:  # a failed merge or finish leaves the table pending: hand it back so the plan runs again
+                op.abandon_partial()
+            except Exception:  # noqa: BLE001 -- the original error is the one to report
+                pass
+            raise
     if part is not None:  # this rank's table was handed out but the ranks merge records: give it back
         op.abandon_partial()
     blk = (fallback_op or op).next_block()

@@ -12,8 +12,10 @@
                          with one phip_query call.
 """
 import ctypes
+import dataclasses
 import math
 import os
+import re
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Union
 
@@ -24,8 +26,10 @@ from ..query import predicate as predeval
 from ..query.context import (UNBOUNDED, AggregationInfo, FilterContext, Function, Identifier, Literal,
                              QueryContext, columns_of)
 from ..query.sql import parse
-from ..spi import DEFAULT_NUM_GROUPS_LIMIT, DataType
-from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock, SelectionResultsBlock
+from ..spi import (DEFAULT_GROUPBY_TRIM_THRESHOLD, DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE,
+                   DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE, DEFAULT_NUM_GROUPS_LIMIT, MAX_TRIM_THRESHOLD, DataType)
+from .results import (AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock, SelectionResultsBlock,
+                      merge_intermediate)
 from .segment import GpuSegment
 
 
@@ -453,7 +457,11 @@ class GpuCombineOperator:
         none = (-1, 0, 0, [], [])
         if not q.group_by or not q.order_by or not getattr(self, "device_trim", True):
             return none
-        min_trim = int(q.options.get("minServerGroupTrimSize", 5000))
+        seg_trim = getattr(self, "segment_trim", None)
+        if seg_trim is not None:  # one segment's GroupByOperator trim (minSegmentGroupTrimSize > 0)
+            min_trim = seg_trim
+        else:
+            min_trim = int(q.options.get("minServerGroupTrimSize", DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE))
         if min_trim <= 0:  # trim disabled (GroupByUtils.java:108)
             return none
         trim = min(max(5 * int(q.limit), min_trim), 2 ** 31 - 1)
@@ -681,6 +689,9 @@ class GpuCombineOperator:
                 blk.key_types = self.key_types()
             blk.device_ms = r.device_ms
             blk.scan_kernel_ms = r.scan_kernel_ms
+            nseg = r.num_segments_processed
+            blk.segment_docs_matched = ([r.segment_docs_matched[i] for i in range(nseg)]
+                                        if self.query.group_by and r.segment_docs_matched else None)
             blk.filter_kernel_ms, blk.agg_kernel_ms = r.filter_kernel_ms, r.agg_kernel_ms
             blk.filter_bytes, blk.agg_bytes = int(r.filter_bytes), int(r.agg_bytes)
             blk.fused = bool(r.fused)
@@ -1007,6 +1018,7 @@ class GpuFilteredGroupByOperator:
         out.key_types = getattr(blk, "key_types", None)
         for k in GpuFilteredAggregationOperator._TIMES + ("fused",):
             setattr(out, k, getattr(blk, k, 0))
+        out.segment_docs_matched = getattr(blk, "segment_docs_matched", None)
         return out
 
     def next_block(self):
@@ -1045,8 +1057,9 @@ class GpuFilteredGroupByOperator:
         blk.num_groups_trimmed = False
         blk.key_types = self.parts[0][1].key_types() if self.parts else None
         if self.device_trim:
-            blk = trim_groups(self.query, blk)
+            blk = trim_groups(self.query, blk, getattr(self, "segment_trim", None))
         blk.device_ms = device_ms
+        blk.segment_docs_matched = None  # (summed per info below it: the checks take the segments' docs instead)
         return blk
 
     # -- multi-GPU servers: the one-pass plan hands out its dense partial table like any group-by
@@ -1212,12 +1225,211 @@ class GpuCaseAggregationOperator:
                                   self._stats(blk.stats, counts), blk.num_groups_limit_reached)
         out.num_groups_trimmed = False
         out.key_types = getattr(blk, "key_types", None)
-        out = trim_groups(self.query, out)
+        out = trim_groups(self.query, out, getattr(self, "segment_trim", None))
         out.device_ms = getattr(blk, "device_ms", 0.0)
+        out.segment_docs_matched = getattr(blk, "segment_docs_matched", None)
         return out
 
     def close(self):
         self.inner.close()
+
+
+# ------------------------------------------------------------------------------ query options
+class QueryOptionError(ValueError):
+    """A malformed query option (QueryOptionsUtils's IllegalArgumentException: a BadQueryRequest)."""
+
+
+_INT = re.compile(r"[+-]?[0-9]+\Z")
+
+
+def _int_option(options, key, min_value=None):
+    """QueryOptionsUtils.uncheckedParseInt / checkedParseInt (pinot-common/.../utils/config/QueryOptionsUtils.java:
+    366-402): Integer.parseInt of the option, at least ``min_value`` when given; None when absent."""
+    v = options.get(key)
+    if v is None:
+        return None
+    v = str(v)
+    if not _INT.match(v) or not -(1 << 31) <= int(v) < (1 << 31):
+        raise QueryOptionError(f"{key} must be an integer, got: {v}")
+    x = int(v)
+    if min_value is not None and x < min_value:
+        raise QueryOptionError(f"{key} must be a number between {min_value} and 2^31-1, got: {v}")
+    return x
+
+
+def _bool_option(options, key) -> bool:
+    """Boolean.parseBoolean of a query option (only a case-insensitive "true" is true)."""
+    return str(options.get(key, "")).strip().lower() == "true"
+
+
+def table_capacity(limit: int, min_num_groups: int) -> int:
+    """GroupByUtils.getTableCapacity (pinot-core/.../util/GroupByUtils.java:55-58): max(limit * 5, minNumGroups)."""
+    by_limit = int(limit) * 5
+    return (1 << 31) - 1 if by_limit > (1 << 31) - 1 else max(by_limit, int(min_num_groups))
+
+
+def indexed_table_trim_threshold(trim_size: int, trim_threshold: int) -> int:
+    """GroupByUtils.getIndexedTableTrimThreshold (:60-70): trim disabled (Integer.MAX_VALUE) when the threshold is
+    non-positive or above 10^9 or trimSize above 5 x 10^8; else max(threshold, 2 x trimSize)."""
+    if trim_threshold <= 0 or trim_threshold > MAX_TRIM_THRESHOLD or trim_size > MAX_TRIM_THRESHOLD // 2:
+        return (1 << 31) - 1
+    return max(trim_threshold, 2 * trim_size)
+
+
+def _source_segments(op):
+    """The segments (GpuSegment) an operator's per-segment GroupByOperators key: the star-tree documents for a
+    star-tree operator, the inner operator's for a CASE operator."""
+    return list(op.segments) if hasattr(op, "segments") else list(op.inner.segments)
+
+
+def _set_segment_trim(op, n):
+    """Make ``op`` (an operator over ONE segment) trim its groups as that segment's GroupByOperator would with
+    minSegmentGroupTrimSize = n: keep the top getTableCapacity(limit, n) by the ORDER BY."""
+    op.segment_trim = n
+    for attr in ("one_pass", "inner"):
+        sub = getattr(op, attr, None)
+        if isinstance(sub, GpuCombineOperator):
+            sub.segment_trim = n
+
+
+class GpuGroupByCombineOperator:
+    """The result-changing group-by options of the combine, over any group-by operator of the plan maker:
+
+      minSegmentGroupTrimSize  GroupByOperator.getNextBlock (pinot-core/.../operator/query/GroupByOperator.java:
+                               118-133): with ORDER BY and a positive size, a segment holding more than
+                               trimSize = getTableCapacity(limit, size) groups keeps only its top trimSize
+                               (TableResizer.trimInSegmentResults) before the combine merges it.
+      groupTrimThreshold       the combine's IndexedTable resizes to the server trimSize whenever it holds
+                               getIndexedTableTrimThreshold(trimSize, threshold) records
+                               (SimpleIndexedTable.upsert; GroupByUtils.java:60-70,130-145).
+
+    The all-segment GPU operator answers first. Per segment s it reports the docs its filter passed; its group
+    records are at most b_s = min(matched docs, key space, numGroupsLimit). When every b_s is within the segment
+    trimSize no segment trims, and the one-launch answer is the reference's; otherwise the query runs once per
+    segment (each plan trimming its own groups on the device, top trimSize by the ORDER BY) and the blocks merge
+    on the host, as the combine merges them. A combine that can reach the trim threshold with records of two or
+    more segments resizes mid-merge, and which partial values then survive depends on the order the reference's
+    worker threads upsert in (ConcurrentIndexedTable): that query raises UnsupportedOnGpu so the plan maker
+    answers it on the CPU (a one-segment combine holds every group once with its exact value, so its resizes keep
+    the exact top trimSize: the GPU answers it)."""
+
+    def __init__(self, query: QueryContext, inner, make_op):
+        self.query = query
+        self.inner = inner
+        self.make_op = make_op
+        self.segments = _source_segments(inner)
+        o = query.options
+        self.limit = int(o.get("numGroupsLimit", DEFAULT_NUM_GROUPS_LIMIT))
+        min_seg = int(o.get("minSegmentGroupTrimSize", DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE))
+        self.min_seg = min_seg if (query.order_by and min_seg > 0) else None
+        self.seg_trim = table_capacity(query.limit, min_seg) if self.min_seg else None
+        min_srv = int(o.get("minServerGroupTrimSize", DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE))
+        srv_trim = table_capacity(query.limit, min_srv) if min_srv > 0 else (1 << 31) - 1
+        thr = int(o.get("groupTrimThreshold", DEFAULT_GROUPBY_TRIM_THRESHOLD))
+        self.threshold = indexed_table_trim_threshold(srv_trim, thr) if query.order_by else (1 << 31) - 1
+        self.key_space = []
+        for seg in self.segments:
+            ks = 1
+            for e in query.group_by:
+                m = seg.column_metadata(e.name)
+                ks *= m.cardinality if m.has_dictionary else max(seg.num_docs, 1)
+            self.key_space.append(ks)
+        self.per_segment = None
+
+    @staticmethod
+    def needed(query: QueryContext) -> bool:
+        """Whether either option can change the result of ``query`` (its options resolved by the plan maker)."""
+        if not query.group_by or not query.order_by:
+            return False
+        o = query.options
+        if int(o.get("minSegmentGroupTrimSize", DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE)) > 0:
+            return True
+        min_srv = int(o.get("minServerGroupTrimSize", DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE))
+        srv_trim = table_capacity(query.limit, min_srv) if min_srv > 0 else (1 << 31) - 1
+        thr = int(o.get("groupTrimThreshold", DEFAULT_GROUPBY_TRIM_THRESHOLD))
+        return indexed_table_trim_threshold(srv_trim, thr) < (1 << 31) - 1
+
+    def _bounds(self, blk):
+        docs = getattr(blk, "segment_docs_matched", None)
+        if docs is None or len(docs) != len(self.segments):
+            docs = [s.num_docs for s in self.segments]
+        return [min(int(d), ks, self.limit) for d, ks in zip(docs, self.key_space)]
+
+    def _check_threshold(self, records):
+        nonempty = sum(1 for r in records if r > 0)
+        if nonempty >= 2 and sum(records) >= self.threshold:
+            raise UnsupportedOnGpu(
+                f"the combine can reach its trim threshold ({self.threshold} records from {nonempty} segments): "
+                "which partial groups survive depends on the reference's thread interleaving")
+
+    def _run_per_segment(self):
+        from .reduce import trim_groups
+        if self.per_segment is None:
+            self.per_segment = []
+            for seg in self.segments:
+                op = self.make_op([seg])
+                _set_segment_trim(op, self.min_seg)
+                self.per_segment.append(op)
+        blocks = [op.next_block() for op in self.per_segment]
+        self._check_threshold([len(b.groups) for b in blocks])
+        aggs = self.query.aggregations
+        groups, stats, reached = {}, ExecutionStatistics(), False
+        times = dict.fromkeys(GpuFilteredAggregationOperator._TIMES, 0)
+        for b in blocks:  # GroupByCombineOperator: every segment's records upserted into one table
+            for k, v in b.groups.items():
+                groups[k] = v if k not in groups else [merge_intermediate(a.function, x, y)
+                                                       for a, x, y in zip(aggs, groups[k], v)]
+            stats.merge(b.stats)
+            reached |= bool(b.num_groups_limit_reached)
+            for k in times:
+                times[k] += getattr(b, k, 0) or 0
+        out = GroupByResultsBlock(aggs, list(self.query.group_by), groups, stats, reached)
+        out.key_types = getattr(blocks[0], "key_types", None) if blocks else None
+        out.num_groups_trimmed = False
+        out = trim_groups(self.query, out)  # the server-level trim of the combine
+        for k, v in times.items():
+            setattr(out, k, v)
+        out.segment_trimmed = True
+        return out
+
+    def next_block(self):
+        blk = self.inner.next_block()
+        bounds = self._bounds(blk)
+        if self.seg_trim is not None and any(b > self.seg_trim for b in bounds):
+            return self._run_per_segment()
+        if self.seg_trim is not None:
+            bounds = [min(b, self.seg_trim) for b in bounds]
+        self._check_threshold(bounds)
+        return blk
+
+    def close(self):
+        self.inner.close()
+        for op in self.per_segment or []:
+            op.close()
+
+    def __getattr__(self, name):
+        # the inner operator's surface (execute_partial / finish for a multi-GPU server's merge, key_types, ...);
+        # a multi-GPU merge applies neither check: its combine spans the GPUs (DESIGN.md §5)
+        if name == "inner":
+            raise AttributeError(name)
+        return getattr(self.inner, name)
+
+
+class GpuPlanWithCpuFallback:
+    """A GPU operator whose execution may still refuse the query (UnsupportedOnGpu from next_block: the combine's
+    trim threshold): the configured CPU plan maker's operator answers it instead."""
+
+    def __init__(self, gpu_op, cpu_plan_maker, query, segments):
+        self.gpu_op, self.cpu_plan_maker, self.query, self.segments = gpu_op, cpu_plan_maker, query, segments
+
+    def next_block(self):
+        try:
+            return self.gpu_op.next_block()
+        except UnsupportedOnGpu:
+            return self.cpu_plan_maker.make_instance_plan(self.query, self.segments).next_block()
+
+    def close(self):
+        self.gpu_op.close()
 
 
 def use_gpu_option(query: QueryContext, default: bool) -> bool:
@@ -1242,13 +1454,50 @@ class GpuInstancePlanMaker:
     for GPU servers and defaults to True."""
 
     def __init__(self, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT, device_trim: bool = True,
-                 cpu_plan_maker=None, default_use_gpu: bool = True):
+                 cpu_plan_maker=None, default_use_gpu: bool = True,
+                 min_segment_group_trim_size: int = DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE,
+                 min_server_group_trim_size: int = DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE,
+                 group_trim_threshold: int = DEFAULT_GROUPBY_TRIM_THRESHOLD):
         """device_trim=False: return every group (a rank of a multi-GPU server, whose partial groups must
-        meet in ``distributed.allreduce_block`` BEFORE the server-level trim, ``reduce.trim_groups``)."""
+        meet in ``distributed.allreduce_block`` BEFORE the server-level trim, ``reduce.trim_groups``).
+        The remaining arguments are the server's instance config (InstancePlanMakerImplV2.init,
+        InstancePlanMakerImplV2.java:108-140): query options override them per query (applyQueryOptions)."""
+        if group_trim_threshold <= 0:  # (InstancePlanMakerImplV2.java:133-134)
+            raise ValueError(f"Invalid configurable: groupByTrimThreshold: {group_trim_threshold} must be positive")
         self.num_groups_limit = num_groups_limit
         self.device_trim = device_trim
         self.cpu_plan_maker = cpu_plan_maker
         self.default_use_gpu = default_use_gpu
+        self.min_segment_group_trim_size = min_segment_group_trim_size
+        self.min_server_group_trim_size = min_server_group_trim_size
+        self.group_trim_threshold = group_trim_threshold
+
+    def apply_query_options(self, query: QueryContext) -> QueryContext:
+        """InstancePlanMakerImplV2.applyQueryOptions (pinot-core/.../plan/maker/InstancePlanMakerImplV2.java:
+        230-300): for a group-by query, numGroupsLimit (a positive int), minSegmentGroupTrimSize,
+        minServerGroupTrimSize and groupTrimThreshold from the query options, else the server's values, written into
+        a copy of the query's options (the reference's QueryContext setters). A malformed option raises
+        QueryOptionError (the reference's BadQueryRequest). Options whose semantics the GPU operators do not have
+        raise UnsupportedOnGpu: enableNullHandling (null value vectors, QueryContext.java:597) and the
+        server-returns-final-result modes (their blocks carry final, not intermediate, results)."""
+        o = query.options
+        if _bool_option(o, "enableNullHandling"):
+            raise UnsupportedOnGpu("enableNullHandling: null handling is not on the GPU path")
+        for k in ("serverReturnFinalResult", "serverReturnFinalResultKeyUnpartitioned"):
+            if _bool_option(o, k):
+                raise UnsupportedOnGpu(f"{k}: the GPU operators return intermediate results")
+        if not (query.aggregations and query.group_by):
+            return query
+        opts = dict(o)
+        v = _int_option(o, "numGroupsLimit", 1)
+        opts["numGroupsLimit"] = str(v if v is not None else self.num_groups_limit)
+        v = _int_option(o, "minSegmentGroupTrimSize")
+        opts["minSegmentGroupTrimSize"] = str(v if v is not None else self.min_segment_group_trim_size)
+        v = _int_option(o, "minServerGroupTrimSize")
+        opts["minServerGroupTrimSize"] = str(v if v is not None else self.min_server_group_trim_size)
+        v = _int_option(o, "groupTrimThreshold")
+        opts["groupTrimThreshold"] = str(v if v is not None else self.group_trim_threshold)
+        return dataclasses.replace(query, options=opts)
 
     def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]):
         if isinstance(query, str):
@@ -1260,24 +1509,36 @@ class GpuInstancePlanMaker:
         if self.cpu_plan_maker is None:
             return self._make_gpu_plan(query, segments)
         try:
-            return self._make_gpu_plan(query, segments)
+            op = self._make_gpu_plan(query, segments)
         except UnsupportedOnGpu:
             return self.cpu_plan_maker.make_instance_plan(query, segments)
+        if isinstance(op, GpuGroupByCombineOperator):
+            return GpuPlanWithCpuFallback(op, self.cpu_plan_maker, query, segments)
+        return op
 
     def _make_gpu_plan(self, query: QueryContext, segments: Sequence[GpuSegment]):
+        query = self.apply_query_options(query)
+        op = self._make_operator(query, segments)
+        if self.device_trim and GpuGroupByCombineOperator.needed(query):
+            op = GpuGroupByCombineOperator(query, op, lambda segs: self._make_operator(query, segs))
+        return op
+
+    def _make_operator(self, query: QueryContext, segments: Sequence[GpuSegment]):
         from .startree import GpuStarTreeOperator
-        st = GpuStarTreeOperator.plan(query, segments, self.num_groups_limit)
+        limit = int(query.options["numGroupsLimit"]) if "numGroupsLimit" in query.options and query.group_by \
+            else self.num_groups_limit
+        st = GpuStarTreeOperator.plan(query, segments, limit)
         if st is not None:
             st.inner.device_trim = self.device_trim
             return st
         if query.is_selection:
-            return GpuSelectionOperator(query, segments, self.num_groups_limit)
+            return GpuSelectionOperator(query, segments, limit)
         if any(ag.argument is not None and _is_case(ag.argument) for ag in query.aggregations):
-            return GpuCaseAggregationOperator(query, segments, self.num_groups_limit)
+            return GpuCaseAggregationOperator(query, segments, limit)
         if any(ag.filter is not None for ag in query.aggregations):
             if query.group_by:
-                return GpuFilteredGroupByOperator(query, segments, self.num_groups_limit, self.device_trim)
-            return GpuFilteredAggregationOperator(query, segments, self.num_groups_limit)
-        op = GpuCombineOperator(query, segments, self.num_groups_limit)
+                return GpuFilteredGroupByOperator(query, segments, limit, self.device_trim)
+            return GpuFilteredAggregationOperator(query, segments, limit)
+        op = GpuCombineOperator(query, segments, limit)
         op.device_trim = self.device_trim
         return op

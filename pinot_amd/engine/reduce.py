@@ -165,19 +165,22 @@ def _reduce_selection(query: QueryContext, blocks, stats) -> ResultTable:
     return ResultTable(names, rows, stats)
 
 
-def trim_size(query: QueryContext) -> int:
-    """GroupByUtils.getTableCapacity(limit, minServerGroupTrimSize) (GroupByUtils.java:55-58,96-140); 0 = no trim."""
-    min_trim = int(query.options.get("minServerGroupTrimSize", 5000))
+def trim_size(query: QueryContext, min_trim=None) -> int:
+    """GroupByUtils.getTableCapacity(limit, minServerGroupTrimSize) (GroupByUtils.java:55-58,96-140); 0 = no trim.
+    ``min_trim``: a segment's minSegmentGroupTrimSize instead (GroupByOperator.java:118-133)."""
+    if min_trim is None:
+        min_trim = int(query.options.get("minServerGroupTrimSize", 5000))
     if not query.group_by or not query.order_by or min_trim <= 0:
         return 0
     return min(max(5 * int(query.limit), min_trim), 2 ** 31 - 1)
 
 
-def trim_groups(query: QueryContext, block):
+def trim_groups(query: QueryContext, block, min_trim=None):
     """Server-level trim on the host (IndexedTable.finish -> TableResizer.getTopRecords): the merged
     group-by block of a multi-GPU server keeps its top trimSize groups by the full ORDER BY. Ties at the
-    boundary keep the smallest keys (the reference's choice is heap-order dependent)."""
-    k = trim_size(query)
+    boundary keep the smallest keys (the reference's choice is heap-order dependent). ``min_trim``: the
+    segment-level trim of one segment's block (minSegmentGroupTrimSize, TableResizer.trimInSegmentResults)."""
+    k = trim_size(query, min_trim)
     if not k or len(block.groups) <= k:
         return block
     gb_index = {str(e): i for i, e in enumerate(query.group_by)}

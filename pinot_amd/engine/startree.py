@@ -409,8 +409,9 @@ class GpuStarTreeOperator:
             out.key_types = getattr(blk, "key_types", None)
             if self.host_trim and self.inner.device_trim:
                 from .reduce import trim_groups
-                out = trim_groups(self.query, out)
-        for a in ("device_ms", "scan_kernel_ms", "filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes"):
+                out = trim_groups(self.query, out, getattr(self, "segment_trim", None))
+        for a in ("device_ms", "scan_kernel_ms", "filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes",
+                  "segment_docs_matched"):
             setattr(out, a, getattr(blk, a, 0))
         out.star_tree = True
         return out

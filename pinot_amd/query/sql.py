@@ -352,6 +352,15 @@ def _collect_aggs(expr, out, flt=None):
 _SET = re.compile(r"\s*SET\s+([A-Za-z_][A-Za-z0-9_.]*)\s*=\s*('(?:[^']|'')*'|[^;]*?)\s*;", re.IGNORECASE)
 
 
+# CommonConstants.Broker.Request.QueryOptionKey names this path reads: SET keys resolve to them case-insensitively
+# (QueryOptionsUtils.resolveCaseInsensitiveOptions, pinot-common/.../utils/config/QueryOptionsUtils.java:80-95)
+QUERY_OPTION_KEYS = ("useGpu", "numGroupsLimit", "minSegmentGroupTrimSize", "minServerGroupTrimSize",
+                     "groupTrimThreshold", "enableNullHandling", "filteredAggregationsSkipEmptyGroups", "useStarTree",
+                     "serverReturnFinalResult", "serverReturnFinalResultKeyUnpartitioned",
+                     "maxInitialResultHolderCapacity", "minInitialIndexedTableCapacity", "timeoutMs")
+_OPTION_RESOLVER = {k.lower(): k for k in QUERY_OPTION_KEYS}
+
+
 def parse(sql: str) -> QueryContext:
     """SQL -> QueryContext; leading ``SET key = value;`` statements become query options (as the broker's
     CalciteSqlParser.compileToPinotQuery collects them)."""
@@ -361,7 +370,8 @@ def parse(sql: str) -> QueryContext:
         if not m:
             break
         v = m.group(2)
-        options[m.group(1)] = v[1:-1].replace("''", "'") if v.startswith("'") else v
+        key = _OPTION_RESOLVER.get(m.group(1).lower(), m.group(1))
+        options[key] = v[1:-1].replace("''", "'") if v.startswith("'") else v
         sql = sql[m.end():]
     table, select, filt, group_by, order_by, limit = _Parser(sql).query()
     aggs = []

@@ -47,6 +47,12 @@ MAX_DOC_PER_CALL = 10_000
 # pinot-core/.../plan/maker/InstancePlanMakerImplV2.java:74,78
 DEFAULT_MAX_INITIAL_RESULT_HOLDER_CAPACITY = 10_000
 DEFAULT_NUM_GROUPS_LIMIT = 100_000
+# InstancePlanMakerImplV2 server defaults (pinot-core/.../plan/maker/InstancePlanMakerImplV2.java:80-96) and
+# GroupByUtils.MAX_TRIM_THRESHOLD (pinot-core/.../util/GroupByUtils.java:40)
+DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE = -1
+DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE = 5000
+DEFAULT_GROUPBY_TRIM_THRESHOLD = 1_000_000
+MAX_TRIM_THRESHOLD = 1_000_000_000
 # pinot-spi/src/main/java/org/apache/pinot/spi/utils/CommonConstants.java:117
 DEFAULT_HYPERLOGLOG_LOG2M = 8
 
