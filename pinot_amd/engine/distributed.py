@@ -563,5 +563,15 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
             raise
     if part is not None:  # this rank's table was handed out but the ranks merge records: give it back
         op.abandon_partial()
-    blk = (fallback_op or op).next_block()
+    err = None
+    try:
+        blk = (fallback_op or op).next_block()
+    except Exception as e:  # noqa: BLE001 -- every rank learns of it before raising (no rank left in a collective)
+        blk, err = None, e
+    f = torch.tensor([1 if err is not None else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
+    if int(f.item()):
+        if err is not None:
+            raise err
+        raise RuntimeError("the query failed on another rank (distributed_block record merge)")
     return allreduce_block(blk, dist, group)

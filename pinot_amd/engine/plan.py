@@ -948,8 +948,8 @@ class GpuFilteredGroupByOperator:
     numGroupsLimit: the shared generator numbers groups first-seen over info 0's docs, then info 1's, ... per
     segment; the device limit pass orders (segment, key) entries by (info, doc) exactly so. The info order is
     the reference's for one filtered info (filtered infos first, the main info last); with several filtered
-    infos the reference iterates a HashMap of FilterContexts, whose order this restatement takes as
-    first-appearance in the query (the oracle does the same).
+    infos the reference iterates a HashMap of FilterContexts, so which keys survive a reached limit is not defined
+    by the query: such an execution raises UnsupportedOnGpu (the plan maker's CPU operator answers it).
 
     More than 8 infos or more than 8 primitive slots run one GPU group-by per info, merged by key on the host
     (the round-2 path); that path raises UnsupportedOnGpu when an info reaches numGroupsLimit."""
@@ -970,6 +970,7 @@ class GpuFilteredGroupByOperator:
             else:
                 infos.setdefault(ag.filter, []).append(i)
         order = list(infos.items())
+        self.num_filtered_infos = len(order)
         skip = str(query.options.get("filteredAggregationsSkipEmptyGroups", "false")).lower() == "true"
         if main or not skip:
             order.append((None, main))
@@ -1023,7 +1024,13 @@ class GpuFilteredGroupByOperator:
 
     def next_block(self):
         if self.one_pass is not None:
-            return self._wrap(self.one_pass.next_block())
+            blk = self.one_pass.next_block()
+            if blk.num_groups_limit_reached and self.num_filtered_infos >= 2:
+                # which keys a segment keeps past the limit depends on the order the shared generator sees the infos
+                # in, and the reference iterates a HashMap of FilterContexts: not defined by the query
+                raise UnsupportedOnGpu("numGroupsLimit reached by a FILTER + GROUP BY query with two or more "
+                                       "filtered infos (the reference's info order is HashMap order)")
+            return self._wrap(blk)
         from .reduce import trim_groups
         na = len(self.query.aggregations)
         stats = ExecutionStatistics()
@@ -1416,8 +1423,9 @@ class GpuGroupByCombineOperator:
 
 
 class GpuPlanWithCpuFallback:
-    """A GPU operator whose execution may still refuse the query (UnsupportedOnGpu from next_block: the combine's
-    trim threshold): the configured CPU plan maker's operator answers it instead."""
+    """A GPU group-by operator whose execution may still refuse the query (UnsupportedOnGpu from next_block: the
+    combine's trim threshold, numGroupsLimit reached under several FILTER infos): the configured CPU plan maker's
+    operator answers it instead."""
 
     def __init__(self, gpu_op, cpu_plan_maker, query, segments):
         self.gpu_op, self.cpu_plan_maker, self.query, self.segments = gpu_op, cpu_plan_maker, query, segments
@@ -1512,7 +1520,7 @@ class GpuInstancePlanMaker:
             op = self._make_gpu_plan(query, segments)
         except UnsupportedOnGpu:
             return self.cpu_plan_maker.make_instance_plan(query, segments)
-        if isinstance(op, GpuGroupByCombineOperator):
+        if query.group_by:  # (a group-by execution may still refuse: trim threshold, several infos at the limit)
             return GpuPlanWithCpuFallback(op, self.cpu_plan_maker, query, segments)
         return op
 

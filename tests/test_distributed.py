@@ -281,3 +281,87 @@ def test_float_order_keys_round_trip():
         want = np.array([-np.inf, -2.25, -0.0, 0.0, 1e-30, 3.5, np.inf, np.nan], code)
         assert np.array_equal(got.view(np.uint64 if code == "<f8" else np.uint32),
                               want.view(np.uint64 if code == "<f8" else np.uint32))
+
+
+class _StubPlan:
+    """A group-by operator's partial-table protocol without a GPU: execute_partial hands out a table (or raises on
+    the failing rank), and while one is pending the plan refuses to run, as libpinot_hip.so does
+    (runtime.cpp: PHIP_ERR_INVALID until phip_plan_finish / phip_plan_abandon_partial)."""
+
+    def __init__(self, fail_partial=False, fail_block=False):
+        from types import SimpleNamespace
+        self.query = SimpleNamespace(group_by=["g"])
+        self.fail_partial, self.fail_block = fail_partial, fail_block
+        self.pending = False
+        self.abandoned = 0
+
+    def execute_partial(self):
+        if self.pending:
+            raise RuntimeError("pending partial table")
+        if self.fail_partial:
+            raise ValueError("execution failed on this rank")
+        self.pending = True
+        from types import SimpleNamespace
+        return SimpleNamespace(global_keys=0, num_groups=0, num_rows=0)  # (local key order: records merge)
+
+    def abandon_partial(self):
+        self.pending = False
+        self.abandoned += 1
+
+    def next_block(self):
+        if self.pending:
+            raise RuntimeError("pending partial table")
+        if self.fail_block:
+            raise ValueError("record path failed on this rank")
+        from pinot_amd.engine.results import ExecutionStatistics, GroupByResultsBlock
+        return GroupByResultsBlock([], ["g"], {}, ExecutionStatistics(), False)
+
+
+def _failure_worker(rank, world, port, where, errs):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pinot_amd import _lib
+        from pinot_amd.engine.distributed import distributed_block
+        _lib.load = lambda *a, **k: None  # (no library on a CPU host: the protocol is what is tested)
+        op = _StubPlan(fail_partial=(where == "partial" and rank == 0), fail_block=(where == "records" and rank == 0))
+        try:
+            distributed_block(op, dist)
+            raise AssertionError("every rank must raise when one rank fails")
+        except (ValueError, RuntimeError) as e:
+            assert (rank == 0) == isinstance(e, ValueError), repr(e)
+        assert not op.pending, "a surviving rank's plan must not stay blocked behind its partial table"
+        if rank != 0 or where == "records":
+            assert op.abandoned == 1
+        op.fail_partial = op.fail_block = False
+        distributed_block(op, dist)  # the plans execute again afterwards, on every rank
+    except Exception as e:  # surfaced to the parent
+        import traceback
+        errs.put(f"rank {rank}: {type(e).__name__}: {e}\n{traceback.format_exc()}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("where", ["partial", "records"])
+def test_distributed_block_rank_failure_world2_gloo(where):
+    """when one rank's execution raises (its partial table, or the record-merge fallback), every rank
+    raises instead of waiting in a collective, and every surviving rank hands its pending partial table back, so
+    its plan runs again afterwards."""
+    ctx = mp.get_context("spawn")
+    errs = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failure_worker, args=(r, 2, port, where, errs)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not errs.empty():
+        msgs.append(errs.get())
+    assert not msgs, msgs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

@@ -110,9 +110,17 @@ def test_gpu_filtered_group_by_one_pass_limit(sql, limit, mode, ft, monkeypatch)
     qc = parse(sql)
     op = GpuInstancePlanMaker(num_groups_limit=limit).make_instance_plan(qc, ft)
     assert op.one_pass is not None and op.one_pass.num_programs >= 2
+    oblk, exact = executor.execute(qc, [s.segment for s in ft], num_groups_limit=limit)
+    if op.num_filtered_infos >= 2 and oblk.num_groups_limit_reached:
+        # two filtered infos: the reference's info order is HashMap order, so the kept keys are not defined by
+        # the query -- the GPU refuses the execution (the Java plan maker answers on the CPU)
+        from pinot_amd.engine.plan import UnsupportedOnGpu
+        with pytest.raises(UnsupportedOnGpu):
+            op.next_block()
+        op.close()
+        return
     blk = op.next_block()
     op.close()
-    oblk, exact = executor.execute(qc, [s.segment for s in ft], num_groups_limit=limit)
     assert blk.num_groups_limit_reached == oblk.num_groups_limit_reached
     assert blk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
     assert blk.stats.num_entries_scanned_post_filter == oblk.stats.num_entries_scanned_post_filter
