@@ -111,6 +111,230 @@ __device__ __forceinline__ void agg_ring_batch(cquery_t &q, cseg_t &seg, const l
   agg_docs<NA, kBatch>(q, seg, d, act, nullptr, 0, false, acc, hll_lds);
 }
 
+// ------------------------------------------------------------------------------------------------
+// batched group-by walk (GB_LDS / GB_GLOBAL, dense_batch): kBatch chunks of 64 ring entries per round trip.
+// Every key column's ids of the batch are issued together, then every remap gather, then per aggregation
+// both input columns' ids together and then both dictionary gathers: per 256 matched docs the key costs two
+// dependent round trips and each aggregation two more, where the one-chunk walk paid them per 64 docs
+// (DictionaryBasedGroupKeyGenerator.java:285-414 keys, DoubleGroupByResultHolder.java:94-98 holders).
+// ------------------------------------------------------------------------------------------------
+template <int U>
+__device__ __forceinline__ void batch_ids_hbm(ccol_t &c, const int32_t (&d)[U], uint32_t (&id)[U]) {
+  const uint32_t b = (uint32_t)c.bits;
+#pragma unroll
+  for (int u = 0; u < U; u++) id[u] = decode_bits(c.words, (uint64_t)(uint32_t)d[u] * b, b);
+}
+
+template <int U>
+__device__ __forceinline__ void batch_group_keys(cquery_t &q, cseg_t &seg, const int32_t (&d)[U], int32_t (&key)[U]) {
+  uint32_t id[kMaxGroupBy][U];
+#pragma unroll
+  for (int k = 0; k < kMaxGroupBy; k++) {
+#pragma unroll
+    for (int u = 0; u < U; u++) id[k][u] = 0;
+    if (k < q.num_group_by) batch_ids_hbm<U>(seg.cols[q.gb_cols[k]], d, id[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxGroupBy; k++) {
+    if (k < q.num_group_by) {
+      ccol_t &c = seg.cols[q.gb_cols[k]];
+      if (c.remap) {
+#pragma unroll
+        for (int u = 0; u < U; u++) id[k][u] = (uint32_t)((const PHIP_GLB int32_t *)c.remap)[id[k][u]];
+      }
+    }
+  }
+  // (GB_LDS / GB_GLOBAL key spaces are below 2^31: 32-bit keys and strides)
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    int32_t kk = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxGroupBy; k++)
+      if (k < q.num_group_by) kk += (int32_t)id[k][u] * (int32_t)q.gb_stride[k];
+    key[u] = kk;
+  }
+}
+
+// Values of a batch from ids already loaded (dictionary columns) or from the raw column.
+template <int U>
+__device__ __forceinline__ void batch_vals_i64(ccol_t &c, const int32_t (&d)[U], const uint32_t (&id)[U],
+                                               int64_t (&v)[U]) {
+  if (c.has_dict) {
+    if (c.type == PHIP_TYPE_INT) {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int32_t *)c.dict)[id[u]];
+    } else if (c.type == PHIP_TYPE_LONG) {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB int64_t *)c.dict)[id[u]];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = dict_i64(c, id[u]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = raw_i64(c, d[u]);
+  }
+}
+template <int U>
+__device__ __forceinline__ void batch_vals_f64(ccol_t &c, const int32_t (&d)[U], const uint32_t (&id)[U],
+                                               double (&v)[U]) {
+  if (c.has_dict) {
+    if (c.type == PHIP_TYPE_INT) {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = (double)((const PHIP_GLB int32_t *)c.dict)[id[u]];
+    } else if (c.type == PHIP_TYPE_DOUBLE) {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = ((const PHIP_GLB double *)c.dict)[id[u]];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = dict_f64(c, id[u]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = raw_f64(c, d[u]);
+  }
+}
+
+// expr_i64 / expr_f64 over a batch: both inputs' ids in flight together, then both gathers.
+template <int U>
+__device__ __forceinline__ void batch_expr2_i64(cseg_t &s, cagg_t &a, const int32_t (&d)[U], int64_t (&x)[U]) {
+  ccol_t &ca = s.cols[a.col_a];
+  const bool two = a.expr != PHIP_EXPR_COLUMN;
+  uint32_t ia[U], ib[U];
+  if (ca.has_dict) batch_ids_hbm<U>(ca, d, ia);
+  if (two && s.cols[a.col_b].has_dict) batch_ids_hbm<U>(s.cols[a.col_b], d, ib);
+  batch_vals_i64<U>(ca, d, ia, x);
+  if (!two) return;
+  int64_t y[U];
+  batch_vals_i64<U>(s.cols[a.col_b], d, ib, y);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (a.expr == PHIP_EXPR_ADD) x[u] = x[u] + y[u];
+    else if (a.expr == PHIP_EXPR_SUB) x[u] = x[u] - y[u];
+    else x[u] = x[u] * y[u];
+  }
+}
+template <int U>
+__device__ __forceinline__ void batch_expr2_f64(cseg_t &s, cagg_t &a, const int32_t (&d)[U], double (&x)[U]) {
+  ccol_t &ca = s.cols[a.col_a];
+  const bool two = a.expr != PHIP_EXPR_COLUMN;
+  uint32_t ia[U], ib[U];
+  if (ca.has_dict) batch_ids_hbm<U>(ca, d, ia);
+  if (two && s.cols[a.col_b].has_dict) batch_ids_hbm<U>(s.cols[a.col_b], d, ib);
+  batch_vals_f64<U>(ca, d, ia, x);
+  if (!two) return;
+  double y[U];
+  batch_vals_f64<U>(s.cols[a.col_b], d, ib, y);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (a.expr == PHIP_EXPR_ADD) x[u] = x[u] + y[u];
+    else if (a.expr == PHIP_EXPR_SUB) x[u] = x[u] - y[u];
+    else x[u] = x[u] * y[u];
+  }
+}
+
+// One table word update: LDS atomics for the workgroup's table, agent-scope atomics for the HBM table.
+template <int MODE>
+__device__ __forceinline__ void tbl_add_u64(cquery_t &q, lds_u64 *tbl, int64_t i, uint64_t v) {
+  if constexpr (MODE == GB_LDS) __hip_atomic_fetch_add(&tbl[i], v, PHIP_RLX, PHIP_WG);
+  else __hip_atomic_fetch_add(&((glb_u64 *)q.gb_table)[i], v, PHIP_RLX, PHIP_AG);
+}
+template <int MODE>
+__device__ __forceinline__ void tbl_add_f64(cquery_t &q, lds_u64 *tbl, int64_t i, double v) {
+  if constexpr (MODE == GB_LDS) __hip_atomic_fetch_add((PHIP_LDS double *)&tbl[i], v, PHIP_RLX, PHIP_WG);
+  else __hip_atomic_fetch_add((PHIP_GLB double *)&((glb_u64 *)q.gb_table)[i], v, PHIP_RLX, PHIP_AG);
+}
+template <int MODE>
+__device__ __forceinline__ void tbl_minmax(cquery_t &q, lds_u64 *tbl, int64_t i, uint64_t v, bool is_min) {
+  if constexpr (MODE == GB_LDS) {
+    if (is_min) __hip_atomic_fetch_min(&tbl[i], v, PHIP_RLX, PHIP_WG);
+    else __hip_atomic_fetch_max(&tbl[i], v, PHIP_RLX, PHIP_WG);
+  } else {
+    glb_u64 *p = &((glb_u64 *)q.gb_table)[i];
+    if (is_min) __hip_atomic_fetch_min(p, v, PHIP_RLX, PHIP_AG);
+    else __hip_atomic_fetch_max(p, v, PHIP_RLX, PHIP_AG);
+  }
+}
+template <int MODE>
+__device__ __forceinline__ void tbl_hll(cquery_t &q, lds_u32 *hll_packed, int slot, int64_t key, uint32_t reg,
+                                        uint32_t rho) {
+  const int64_t G = q.num_groups;
+  if constexpr (MODE == GB_LDS) {
+    lds_hll_max(hll_packed + ((((int64_t)slot * G + key) << q.log2m) >> 2), reg, rho);
+  } else {
+    glb_u32 *r = (glb_u32 *)q.gb_hll + (((int64_t)slot * G + key) << q.log2m) + reg;
+    if (*r < rho) __hip_atomic_fetch_max(r, rho, PHIP_RLX, PHIP_AG);
+  }
+}
+
+constexpr int kRingGB = kRingGroupBatch;
+
+template <int MODE>
+__device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const lds_u32 *ring, int tail, int n,
+                                                 lds_u64 *tbl, lds_u32 *hll_packed) {
+  constexpr int U = kBatch;
+  const int lane = lane_id();
+  int32_t d[U];
+  uint32_t act = 0;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const bool on = 64 * u + lane < n;
+    d[u] = on ? (int32_t)ring[(tail + 64 * u + lane) & (kRingGB - 1)] : 0;  // (doc 0: a valid doc, no effect)
+    act |= on ? (1u << u) : 0u;
+  }
+  int32_t key[U];
+  batch_group_keys<U>(q, seg, d, key);
+  const int64_t G = q.num_groups;
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if ((act >> u) & 1u) tbl_add_u64<MODE>(q, tbl, key[u], 1ull);
+  for (int a = 0; a < kMaxAggs; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    if (ag.program != seg.program) continue;  // another filter program's function (wave-uniform)
+    const int kind = ag.acc;
+    const int64_t row = (int64_t)(1 + a) * G;
+    if (kind == ACC_COUNT) {  // == row 0, unless the programs count apart
+      if (q.own_count_rows) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if ((act >> u) & 1u) tbl_add_u64<MODE>(q, tbl, row + key[u], 1ull);
+      }
+    } else if (kind == ACC_HLL) {
+      ccol_t &c = seg.cols[ag.col_a];
+      if (c.hll_rows) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if ((act >> u) & 1u)
+            hll_row_each(c, d[u], [&](int r, uint32_t rho) { tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], r, rho); });
+      } else {
+        uint32_t id[U], h[U];
+        batch_ids_hbm<U>(c, d, id);
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll)[id[u]];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if ((act >> u) & 1u) tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], h[u] >> 8, h[u] & 0xffu);
+      }
+    } else if (kind == ACC_SUM_I64) {
+      int64_t v[U];
+      batch_expr2_i64<U>(seg, ag, d, v);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if ((act >> u) & 1u) tbl_add_u64<MODE>(q, tbl, row + key[u], (uint64_t)v[u]);
+    } else {
+      double v[U];
+      batch_expr2_f64<U>(seg, ag, d, v);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (!((act >> u) & 1u)) continue;
+        if (kind == ACC_SUM_F64) tbl_add_f64<MODE>(q, tbl, row + key[u], v[u]);
+        else tbl_minmax<MODE>(q, tbl, row + key[u], f64_ordered(v[u]), kind == ACC_MIN_F64);
+      }
+    }
+  }
+}
+
 // GB_HASH: linear probing from a 64-bit finaliser of the key; a slot is claimed by CAS(empty -> key).
 // Plain loads may see a stale "empty" (the CAS then returns the owner) but never a wrong key, because
 // a slot changes at most once.
@@ -222,14 +446,18 @@ __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, 
 // kDense: the batched dense-tile walk is compiled in (host: dq.dense_batch). Without it the kernel is
 // the per-64-doc ring walk alone -- its smaller code and register footprint measured 8-10 % faster on
 // the sparse SSB Q1.x aggregations than a kernel that merely skips the batched path at run time.
+// For GB_LDS / GB_GLOBAL, kDense selects the batched group-by walk (group_ring_batch) instead.
 template <int NA, int MODE, bool kDense>
-__global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr) {
+__global__ __launch_bounds__(kAggBlock, (MODE == GB_LDS || MODE == GB_GLOBAL) && kDense ? 6 : 1)
+void agg_kernel(const DevAggQuery *qptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cquery_t &q = *(cquery_t *)qptr;
   const int lane = lane_id();
   const int wave = uniform(threadIdx.x >> 6);
   PHIP_LDS unsigned char *lds = (PHIP_LDS unsigned char *)smem;
-  constexpr int R = ring_entries(MODE);
+  constexpr bool kGbBatch = (MODE == GB_LDS || MODE == GB_GLOBAL) && kDense;
+  constexpr bool kRingFill = MODE == GB_NONE || kGbBatch;  // matched docs enter the ring by a wave prefix scan
+  constexpr int R = ring_entries(MODE, kGbBatch);
   lds_u32 *ring = (lds_u32 *)lds + wave * R;
   PHIP_LDS unsigned char *stage = lds + kAggWaves * R * 4;  // GB_NONE dense-tile staging
   PHIP_LDS unsigned char *stg = stage + wave * q.stage_bytes;
@@ -292,6 +520,8 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
     if (segs[si].work_begin + segs[si].num_work <= t) {
       if constexpr (MODE == GB_NONE) {
         if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
+      } else if constexpr (kGbBatch) {
+        if (head > tail) group_ring_batch<MODE>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
       } else if (head > tail) {  // leftover (< 64) matched docs of the previous segment
         const bool act = lane < head - tail;
         const int32_t doc = act ? (int32_t)ring[(tail + lane) & (R - 1)] : 0;
@@ -351,7 +581,7 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
       continue;
     }
     }
-    if constexpr (MODE == GB_NONE) {
+    if constexpr (kRingFill) {
       // Matched docs -> the ring: every lane writes its docs at the wave prefix (DPP scan) of the lanes'
       // popcounts -- a few instructions plus the lane's own matches per tile; a pass per 64-doc group (ballot +
       // rank + write for each of the 32 groups) cost ~320 on sparse tiles, most of the unsorted layout's walk.
@@ -374,9 +604,9 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
         dstep = 1;
       }
       const int head0 = head;
-      // all at once when the ring has room, else in quarter-tile pieces (16 lanes, <= 512 docs) each after
-      // draining the ring below one batch
-      const int npiece = head - tail + total <= R ? 1 : 4;
+      // all at once when the ring has room, else in quarter-tile pieces (16 lanes, <= 512 docs; eighths of <= 256
+      // docs in the group-by walk's smaller ring) each after draining the ring below one batch
+      const int npiece = head - tail + total <= R ? 1 : (kGbBatch ? 8 : 4);
       for (int p = 0; p < npiece; p++) {
         const int lanes = 64 / npiece;
         const int pend = __builtin_amdgcn_readlane((int)incl, lanes * p + lanes - 1);
@@ -392,7 +622,8 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
         }
         head = head0 + pend;
         while (head - tail >= 64 * kBatch) {
-          agg_ring_batch<NA>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0);
+          if constexpr (kGbBatch) group_ring_batch<MODE>(q, seg, ring, tail, 64 * kBatch, tbl, hll_packed);
+          else agg_ring_batch<NA>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0);
           tail += 64 * kBatch;
         }
       }
@@ -423,6 +654,8 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
   }
   if constexpr (MODE == GB_NONE) {
     if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
+  } else if constexpr (kGbBatch) {
+    if (head > tail) group_ring_batch<MODE>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
   } else if (head > tail) {
     const bool act = lane < head - tail;
     const int32_t doc = act ? (int32_t)ring[(tail + lane) & (R - 1)] : 0;
@@ -449,11 +682,12 @@ __global__ __launch_bounds__(kAggBlock) void agg_kernel(const DevAggQuery *qptr)
         const int kind = q.aggs[a].acc;
         uint64_t v = part[0][a];
         for (int w = 1; w < kAggWaves; w++) v = acc_combine(kind, v, part[w][a]);
-        q.partials[(size_t)blockIdx.x * q.num_aggs + a] = v;
+        coherent_store(q.partials + (size_t)blockIdx.x * q.num_aggs + a, v);  // (read by the finalizing workgroup)
       }
     }
     for (int i = threadIdx.x; i < hll_words; i += kAggBlock)
       if (hll_lds[i]) __hip_atomic_fetch_max((glb_u32 *)q.hll_regs + i, (uint32_t)hll_lds[i], PHIP_RLX, PHIP_AG);
+    if (q.fin != nullptr) finalize_tail(q.fin);
   } else if constexpr (MODE == GB_LDS) {
     __syncthreads();
     glb_u64 *slab = (glb_u64 *)q.gb_table + (size_t)blockIdx.x * q.tbl_words;
@@ -760,8 +994,11 @@ static hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hi
 
 // q: host copy (for the variant choice); dq: the same descriptor in device memory.
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s) {
-  if (q.mode == GB_LDS) return launch_agg_t<1, GB_LDS>(dq, nblocks, lds, s);
-  if (q.mode == GB_GLOBAL) return launch_agg_t<1, GB_GLOBAL>(dq, nblocks, lds, s);
+  if (q.mode == GB_LDS)
+    return q.dense_batch ? launch_agg_t<1, GB_LDS, true>(dq, nblocks, lds, s) : launch_agg_t<1, GB_LDS>(dq, nblocks, lds, s);
+  if (q.mode == GB_GLOBAL)
+    return q.dense_batch ? launch_agg_t<1, GB_GLOBAL, true>(dq, nblocks, lds, s)
+                         : launch_agg_t<1, GB_GLOBAL>(dq, nblocks, lds, s);
   if (q.mode == GB_HASH) return launch_agg_t<1, GB_HASH>(dq, nblocks, lds, s);
   if (q.dense_batch) {
     if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE, true>(dq, nblocks, lds, s);

@@ -36,7 +36,12 @@ constexpr int kAggWaves = kAggBlock / kWave;
 #endif
 constexpr int kRingAgg = PHIP_KBATCH <= 4 ? 1024 : 2048;  // power of two >= 64 * kBatch + 512
 constexpr int kRingGroup = 128;
-constexpr int ring_entries(int mode) { return mode == 0 ? kRingAgg : kRingGroup; }
+// the batched group-by walk (GB_LDS / GB_GLOBAL, DevAggQuery::dense_batch): kBatch chunks per gather round
+// trip like GB_NONE, a tile entering in eighth-tile pieces of <= 256 docs (its LDS goes to the table)
+constexpr int kRingGroupBatch = PHIP_KBATCH <= 4 ? 512 : 1024;  // power of two >= 64 * kBatch + 256
+constexpr int ring_entries(int mode, bool batched = false) {
+  return mode == 0 ? kRingAgg : (batched ? kRingGroupBatch : kRingGroup);
+}
 constexpr int kMaxAggStage = 4;      // staged aggregation columns
 constexpr int kAggStageBudget = 4096; // LDS bytes per wave for them
 constexpr int kAggLdsDict = 1024;     // dictionaries up to this many bytes are copied next to them
@@ -105,7 +110,8 @@ struct ConjLeaf {
   int32_t lds_off;  // staged region in the ring slot
   int32_t bits;
   int32_t kind;     // 0: dict-id range, 1: dict-id set over card <= 64, 2: dict-id range over the bit-sliced planes,
-                    // 3: a few ids (set_mask) over the bit-sliced planes
+                    // 3: a few ids (set_mask) over the bit-sliced planes, 4: OR of <= 4 id runs over the bit-sliced
+                    // planes (runs 0 / 1 in set_mask's halves, run 2 in lo, run 3 in span, pad = number of runs)
   uint32_t lo;      // range: lo << (32 - bits); bit-sliced: the first id of the range
   uint32_t span;    // range: (hi - lo) << (32 - bits); bit-sliced: the last id of the range (inclusive)
   int32_t pad;      // bit-sliced: 1 = lower bound to test, 2 = upper bound to test
@@ -165,9 +171,28 @@ struct DevNode {
   int32_t small_set;  // DICT_SET with card <= 64: membership in set_mask
   int32_t aux_stride; // INVERTED: u64 words per 2048-doc tile in aux (32 x the entry's inverted leaves, interleaved)
   uint64_t set_mask;
+  int32_t bs_nruns;   // DICT_SET: its ids (complement taken when exclusive) as 1..kBitSliceRuns runs of consecutive ids,
+  uint32_t bs_runs[4];  // run r = [bs_runs[r] & 0xffff, bs_runs[r] >> 16] (the bit-sliced conjunction's OR of ranges);
+                        // 0 = more runs than that
   const void *aux;    // DICT_SET: u32 bitset over dict ids; DOC_RANGES: int32 pairs;
                       // INVERTED: u64 doc bitmap words of the segment (materialised);
                       // RAW_RANGE: phip_raw_range; RAW_SET: `count` int64 / double values
+};
+
+// The per-execution results of an aggregation-only plan (what finalize_all_kernel computes), produced instead by the
+// last workgroup of the plan's last kernel (agg_common.h finalize_tail): fixed-order reductions of the per-block
+// partials, the per-segment matched counts and the HLL registers, written into the plan's mapped pinned area and
+// the device counters zeroed for the next execution -- one launch and its dispatch gap fewer per query.
+struct DevFinal {
+  const uint64_t *pa;   // aggregation partials [nba][na], or null
+  const int32_t *ka;    // their accumulator kinds
+  const uint64_t *pf;   // filter partials [nbf][2] (matched docs, entries scanned), or null
+  const int32_t *kf;
+  uint64_t *segm;       // [nseg] matched docs per (program, segment) entry
+  uint32_t *hll;        // [hll_words] registers (aggregation only)
+  uint64_t *out;        // pinned: [0, na) slots, [32, 34) filter sums, [64, 64 + nseg) segm, then the registers
+  uint32_t *counter;    // workgroups done (the last one finalizes and resets it)
+  int32_t nba, na, nbf, nseg, hll_words, pad;
 };
 
 // Filter kernel launch (K1-K4 of SURVEY.md §2.4).
@@ -194,6 +219,7 @@ struct DevFilter {
   uint64_t *agg_partials;         // [num_blocks][num_aggs]
   int32_t fring_bytes;            // per-wave matched-doc ring (fused): 4 * kFusedRingDefer when a segment defers,
   int32_t pad_f;                  // else 2 * kFusedRingTile
+  const DevFinal *fin;            // non-null: this launch is the plan's last; its last workgroup finalizes
 };
 
 struct DevAgg {
@@ -221,7 +247,8 @@ struct DevAggQuery {
   // group-by
   int32_t num_group_by;
   int32_t gb_cols[kMaxGroupBy];
-  int32_t dense_batch;    // GB_NONE: dense tiles take the batched lane-major walk (small dictionaries)
+  int32_t dense_batch;    // GB_NONE: dense tiles take the batched lane-major walk (small dictionaries);
+                          // GB_LDS / GB_GLOBAL: the batched group-by walk (kBatch chunks per gather round trip)
   int64_t gb_stride[kMaxGroupBy];  // mixed radix, column 0 least significant
   int64_t num_groups;     // dense key space size
   int32_t tbl_words;      // GB_LDS: u64 words of one workgroup table = num_groups * (1 + num_aggs)
@@ -251,6 +278,7 @@ struct DevAggQuery {
   int32_t dense_min;  // GB_NONE + dense_batch: matched docs per 2048-doc tile from which the batched walk is used
   int32_t own_count_rows;  // group-by over several filter programs (FILTER + GROUP BY): every COUNT counts its own
                            // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
+  const DevFinal *fin;     // GB_NONE: non-null when this launch is the plan's last (agg_common.h finalize_tail)
 };
 
 // Selection (row-returning) queries (select.hip): SelectionOnlyOperator per segment + the combine's concatenation.

@@ -857,11 +857,38 @@ __device__ __forceinline__ uint32_t bs_set(const PHIP_LDS uint32_t *pl, uint64_t
   return r;
 }
 
+// OR of n <= 4 runs of ids (ConjLeaf kind 4: runs 0 / 1 in the two halves of `set`, run 2 in lo, run 3 in hi; a run
+// is [r & 0xffff, r >> 16]): one plane load, each run an equality or a two-sided BitWeaving/V comparison.
+template <int B>
+__device__ __forceinline__ uint32_t bs_runs(const PHIP_LDS uint32_t *pl, uint64_t set, uint32_t r2, uint32_t r3, int n) {
+  const int lane = lane_id();
+  uint32_t x[B];
+#pragma unroll
+  for (int k = 0; k < B; k++) x[k] = pl[64 * k + lane];
+  uint32_t res = 0u;
+  for (int j = 0; j < n; j++) {
+    const uint32_t run = j == 0 ? (uint32_t)set : (j == 1 ? (uint32_t)(set >> 32) : (j == 2 ? r2 : r3));
+    const uint32_t a = run & 0xffffu, b = run >> 16;
+    uint32_t gt = 0u, lt = 0u, eqa = ~0u, eqb = ~0u;
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const uint32_t ba = (a >> (B - 1 - k)) & 1u, bb = (b >> (B - 1 - k)) & 1u;
+      if (ba) eqa &= x[k];
+      else { gt |= eqa & x[k]; eqa &= ~x[k]; }
+      if (bb) { lt |= eqb & ~x[k]; eqb &= x[k]; }
+      else eqb &= ~x[k];
+    }
+    res |= (gt | eqa) & (lt | eqb);  // a <= x <= b
+  }
+  return res;
+}
+
 __device__ __forceinline__ uint32_t bs_range_any(const PHIP_LDS uint32_t *pl, int bits, uint32_t lo, uint32_t hi,
                                               int sides, int kind, uint64_t set) {
   switch (bits) {
 #define PHIP_BSR(b) \
-  case b: return kind == 3 ? bs_set<(b < 7 ? b : 6)>(pl, set) : bs_range<b>(pl, lo, hi, sides);
+  case b: return kind == 4 ? bs_runs<b>(pl, set, lo, hi, sides) \
+               : kind == 3 ? bs_set<(b < 7 ? b : 6)>(pl, set) : bs_range<b>(pl, lo, hi, sides);
     PHIP_BSR(1) PHIP_BSR(2) PHIP_BSR(3) PHIP_BSR(4) PHIP_BSR(5) PHIP_BSR(6) PHIP_BSR(7) PHIP_BSR(8) PHIP_BSR(9)
     PHIP_BSR(10) PHIP_BSR(11) PHIP_BSR(12)
 #undef PHIP_BSR
@@ -1422,7 +1449,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
   if (threadIdx.x < 2) {
     uint64_t v = 0;
     for (int w = 0; w < kFilterWaves; w++) v += part[w][threadIdx.x];
-    q.partials[(size_t)blockIdx.x * 2 + threadIdx.x] = v;
+    coherent_store(q.partials + (size_t)blockIdx.x * 2 + threadIdx.x, v);  // (read by the finalizing workgroup)
   }
   if constexpr (NA > 0) {  // fused aggregation: per-block partials, reduced in a fixed order by finalize
     cquery_t &aq = *(cquery_t *)q.agg;
@@ -1444,10 +1471,11 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel
         const int kind = aq.aggs[a].acc;
         uint64_t v = apart[0][a];
         for (int w = 1; w < kFilterWaves; w++) v = acc_combine(kind, v, apart[w][a]);
-        q.agg_partials[(size_t)blockIdx.x * aq.num_aggs + a] = v;
+        coherent_store(q.agg_partials + (size_t)blockIdx.x * aq.num_aggs + a, v);
       }
     }
   }
+  if (q.fin != nullptr) finalize_tail(q.fin);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1238,6 +1238,9 @@ struct Plan {
   std::vector<int32_t> sel_bits, sel_width;  // per select column's projected bytes (algorithmic bytes)
   float sel_filter_ms = 0.f;
   bool total_events = true;  // record ev[0] / ev[3] (phip_result.device_ms); PHIP_TOTAL_EVENTS=0 skips them (A/B)
+  bool split_event = true;   // record ev[4] between a filter and a separate aggregation launch
+  bool fold_final = false;   // the last kernel's last workgroup finalizes (no finalize_all launch)
+  uint32_t *fin_counter = nullptr;  // its ticket counter (device)
 };
 
 // String.compareTo order (UTF-16 code units) over UTF-8 bytes: the lead bytes 0xEE / 0xEF (U+E000..U+FFFF) rank
@@ -1264,6 +1267,14 @@ static bool bs_small_set(const DevNode &dn, const DevCol &dc) {
   if (!on || !dn.small_set || dc.card > 64) return false;
   const uint64_t in_dict = dc.card >= 64 ? ~0ull : ((1ull << dc.card) - 1);
   return __builtin_popcountll(dn.set_mask & in_dict) <= kBitSliceSetMax;
+}
+
+// An IN / NOT IN set of any dictionary whose ids form at most 4 runs of consecutive ids (DevNode.bs_runs): the
+// bit-sliced conjunction tests it as an OR of plane ranges (equalities for one-id runs). PHIP_BS_RUNS=0 disables it.
+static bool bs_runs_set(const DevNode &dn) {
+  const char *e = getenv("PHIP_BS_RUNS");  // (read per plan, as the tests switch it)
+  const bool off = e != nullptr && atoi(e) == 0;
+  return !off && dn.leaf_kind == PHIP_LEAF_DICT_SET && dn.bs_nruns > 0;
 }
 
 struct AuxFix {  // a leaf's node.aux = device base of the plan's blob + off
@@ -1775,6 +1786,21 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             if (rc) break;
             // a contiguous id set (or its complement within the dictionary) is a dict-id range
             const bool contiguous = n_in > 0 && mx - mn + 1 == n_in;
+            if (cs->bits <= kBitSliceMaxBits) {  // the matching ids as runs (the bit-sliced conjunction ORs <= 4)
+              int nr = 0;
+              bool prev = false;
+              for (int id = 0; id <= cs->card && nr <= 4; id++) {
+                const bool in = id < cs->card && (((bits[id >> 5] >> (id & 31)) & 1u) != 0) != (fn.exclusive != 0);
+                if (in && !prev) {
+                  if (nr < 4) dn.bs_runs[nr] = (uint32_t)id;
+                  nr++;
+                } else if (!in && prev && nr <= 4) {
+                  dn.bs_runs[nr - 1] |= (uint32_t)(id - 1) << 16;
+                }
+                prev = in;
+              }
+              dn.bs_nruns = nr <= 4 && cs->card <= 65536 ? nr : 0;
+            }
             if (n_in == 0) {
               dn.leaf_kind = fn.exclusive ? PHIP_LEAF_MATCH_ALL : PHIP_LEAF_MATCH_NONE;
             } else if (n_in == cs->card) {
@@ -2097,7 +2123,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       if (dn.op == DOP_LEAF && dn.leaf_kind == PHIP_LEAF_DOC_RANGES && dn.count == 1) continue;
       bs = dn.op == DOP_LEAF && (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || dn.leaf_kind == PHIP_LEAF_DICT_SET) &&
            ds.cols[dn.column].planes != nullptr &&
-           (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || bs_small_set(dn, ds.cols[dn.column]));
+           (dn.leaf_kind == PHIP_LEAF_DICT_RANGE || bs_small_set(dn, ds.cols[dn.column]) || bs_runs_set(dn));
     }
     if (bs) {  // every column's planes must fit the slot (else the packed words, as the interpreter reads them)
       std::vector<int> cols_seen;
@@ -2163,7 +2189,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         continue;
       }
       if (dn.op != DOP_LEAF || dn.lds_off < 0 ||
-          !(dn.leaf_kind == PHIP_LEAF_DICT_RANGE || (dn.leaf_kind == PHIP_LEAF_DICT_SET && dn.small_set))) {
+          !(dn.leaf_kind == PHIP_LEAF_DICT_RANGE || (dn.leaf_kind == PHIP_LEAF_DICT_SET && dn.small_set) ||
+            (bs && bs_runs_set(dn)))) {
         ok = false;
         break;
       }
@@ -2173,7 +2200,16 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       L.lds_off = dn.lds_off;
       L.bits = dn.bits;
       double sel;
-      if (bs && dn.leaf_kind == PHIP_LEAF_DICT_SET) {  // (a few ids of a dictionary of <= 64: bs_small_set)
+      if (bs && dn.leaf_kind == PHIP_LEAF_DICT_SET && bs_runs_set(dn)) {  // OR of <= 4 id runs over the planes
+        L.kind = 4;
+        L.set_mask = (uint64_t)dn.bs_runs[0] | ((uint64_t)dn.bs_runs[1] << 32);
+        L.lo = dn.bs_runs[2];
+        L.span = dn.bs_runs[3];
+        L.pad = dn.bs_nruns;
+        int64_t n = 0;
+        for (int r = 0; r < dn.bs_nruns; r++) n += (int64_t)(dn.bs_runs[r] >> 16) - (dn.bs_runs[r] & 0xffff) + 1;
+        sel = double(n) / card;
+      } else if (bs && dn.leaf_kind == PHIP_LEAF_DICT_SET) {  // (a few ids of a dictionary of <= 64: bs_small_set)
         L.kind = 3;
         L.set_mask = dn.set_mask & (card >= 64 ? ~0ull : ((1ull << card) - 1));
         sel = double(__builtin_popcountll(L.set_mask)) / card;
@@ -2411,6 +2447,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // ---- aggregation kernel configuration (aggregate.hip) -----------------------------------------
   dq.log2m = log2m;
   if (dq.mode != GB_HASH) dq.mode = group_by ? GB_GLOBAL : GB_NONE;
+  if (group_by) dq.dense_batch = 0;  // (set below for GB_LDS: the batched group-by walk)
   const int m_regs = nhll ? (1 << log2m) : 0;
   size_t agg_lds = (size_t)kAggWaves * ring_entries(dq.mode) * 4 + (size_t)kAggWaves * dq.stage_bytes;
   int agg_bpc = 4;
@@ -2433,7 +2470,23 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const char *force = getenv("PHIP_GB_MODE");  // measurement override: "lds" / "global"
     bool use_lds = table_bytes <= 128 * 1024;
     if (force && !strcmp(force, "global")) use_lds = false;
-    if (force && !strcmp(force, "lds") && table_bytes <= 150 * 1024) use_lds = true;
+    if (force && !strcmp(force, "lds") && (int64_t)agg_lds + round_up(table_bytes, 16) <= 159 * 1024) use_lds = true;
+    // The batched walk (aggregate.hip group_ring_batch: kBatch chunks per gather round trip) for LDS tables, the
+    // one-chunk walk for HBM tables: measured on SSB SF100 (tools/gb_ab.py, profiles/r04b_gb_ab.log) the LDS
+    // group-bys gain (Q2.1 aggregation 0.45 -> 0.34 ms, Q2.2 0.20 -> 0.19, Q4.1 0.63 -> 0.56) and the sparse HBM-table
+    // ones lose (Q3.2 0.30 -> 0.36, Q4.3 0.10 -> 0.15: the larger kernel keeps fewer waves resident for their latency;
+    // profiles/r04c_gb_ab.log).
+    // Its larger ring must not cost a resident workgroup (C5: 3 -> 2 per CU made it 16 % slower, Q4.2 2 -> 1 6 %).
+    const char *gbb = getenv("PHIP_GB_BATCH");  // measurement override: "0" / "1"
+    const int64_t tb = round_up(table_bytes, 16);
+    const int64_t ring_extra = (int64_t)kAggWaves * (kRingGroupBatch - kRingGroup) * 4;
+    auto bpc_of = [&](int64_t lds) { return std::max<int64_t>(1, std::min<int64_t>(4, (160 * 1024 - 1024) / lds)); };
+    bool batched = use_lds && bpc_of((int64_t)agg_lds + ring_extra + tb) >= bpc_of((int64_t)agg_lds + tb);
+    if (gbb) batched = atoi(gbb) != 0;
+    if (use_lds && (int64_t)agg_lds + ring_extra + tb > 159 * 1024) batched = false;
+    dq.dense_batch = batched ? 1 : 0;
+    agg_lds = (size_t)kAggWaves * ring_entries(dq.mode == GB_HASH ? GB_HASH : GB_LDS, batched) * 4 +
+              (size_t)kAggWaves * dq.stage_bytes;
     if (use_lds) {
       dq.mode = GB_LDS;
       dq.tbl_words = (int32_t)tbl_words;
@@ -2696,6 +2749,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.fo = fo;
   P.first_doc = (uint32_t *)first_doc;
   if (const char *te = getenv("PHIP_TOTAL_EVENTS")) P.total_events = atoi(te) != 0;
+  // ev[4] only between two launches (selection plans time their gather with it, execute_select)
+  P.split_event = P.select || (P.has_filter && P.need_agg && P.fused_naggs == 0);
+  if (const char *se = getenv("PHIP_SPLIT_EVENT")) P.split_event = P.split_event || atoi(se) != 0;  // A/B
   for (auto &e : P.ev) HIP_TRY(hipEventCreate(&e));
   {
     void *h = nullptr;
@@ -2707,6 +2763,43 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     void *dp = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
     P.pinned_dev = (uint64_t *)dp;
+  }
+  // Finalize in the last workgroup of the plan's last kernel (agg_common.h finalize_tail) for aggregation-only plans:
+  // the finalize_all launch and its dispatch gap go. PHIP_FOLD_FINAL=0 keeps the launch (A/B).
+  const char *ff = getenv("PHIP_FOLD_FINAL");
+  if (!group_by && !P.select && !want_bitmap && total_work > 0 && (has_filter || need_agg) && (!ff || atoi(ff) != 0)) {
+    const bool fused = fused_naggs > 0;
+    const bool agg_last = need_agg && !fused;
+    const bool aggs_here = need_agg && naggs > 0;
+    DevFinal f;
+    memset(&f, 0, sizeof(f));
+    f.pa = aggs_here ? (const uint64_t *)apart : nullptr;
+    f.ka = (const int32_t *)(base + kinds_off);
+    f.nba = fused ? filter_blocks : agg_blocks;
+    f.na = aggs_here ? naggs : 0;
+    f.pf = has_filter ? (const uint64_t *)fpart : nullptr;
+    f.kf = (const int32_t *)(base + kinds_off) + naggs;
+    f.nbf = filter_blocks;
+    f.segm = (uint64_t *)seg_matched;
+    f.nseg = nmatch;
+    f.hll = dq.hll_regs;
+    f.hll_words = nhll ? (int32_t)((size_t)nhll << log2m) : 0;
+    f.out = P.pinned_dev;
+    void *fb;
+    rc = P.alloc(sizeof(DevFinal) + 64, &fb);
+    if (rc) return rc;
+    f.counter = (uint32_t *)((uint8_t *)fb + round_up(sizeof(DevFinal), 16));
+    HIP_TRY(hipMemsetAsync(f.counter, 0, 4, st));
+    HIP_TRY(hipMemcpyAsync(fb, &f, sizeof(f), hipMemcpyHostToDevice, st));
+    P.fin_counter = f.counter;
+    if (agg_last) {
+      P.dq.fin = (const DevFinal *)fb;
+      HIP_TRY(hipMemcpyAsync(base + dq_off, &P.dq, sizeof(DevAggQuery), hipMemcpyHostToDevice, st));
+    } else {
+      P.fq.fin = (const DevFinal *)fb;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    P.fold_final = true;
   }
   return PHIP_OK;
 }
@@ -2738,6 +2831,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (!P.clean) {
     HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)P.nmatch * 8, st));
     if (hll_words) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, hll_words * 4, st));
+    if (P.fin_counter) HIP_TRY(hipMemsetAsync(P.fin_counter, 0, 4, st));
   }
   P.clean = false;
   if (filter_words) HIP_TRY(hipMemsetAsync(fo, 0, (size_t)filter_nwords * 8, st));
@@ -2763,7 +2857,9 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   const bool fused = P.fused_naggs > 0;
   if (has_filter && total_work > 0)
     HIP_TRY(launch_filter(fq, conj_only, P.fused_naggs, filter_blocks, filter_lds, st));
-  HIP_TRY(hipEventRecord(P.ev[4], st));
+  // (a plan of one kernel -- fused, or a filter or aggregation alone -- needs no split event: every timing marker on
+  // the queue is a barrier packet the command processor waits on, a few microseconds of a 25-us query)
+  if (P.split_event) HIP_TRY(hipEventRecord(P.ev[4], st));
   if (need_agg && total_work > 0 && !fused)
     HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
   HIP_TRY(hipEventRecord(P.ev[2], st));
@@ -2782,7 +2878,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
                                   filter_nwords, st));
   // every result lands in the plan's pinned buffer, written by the device: finals[64] | seg_matched[nmatch] | HLL
-  if (total_work > 0) {
+  if (total_work > 0 && !P.fold_final) {
     const bool aggs_here = need_agg && !group_by && naggs > 0;
     HIP_TRY(launch_finalize_all(aggs_here ? (const uint64_t *)apart : nullptr, fused ? filter_blocks : agg_blocks,
                                 aggs_here ? naggs : 0, dev_kinds, has_filter ? (const uint64_t *)fpart : nullptr,
@@ -3316,8 +3412,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   HIP_TRY(hipEventElapsedTime(&t_scan, P.ev[1], P.ev[2]));
   if (P.total_events) HIP_TRY(hipEventElapsedTime(&t_all, P.ev[0], P.ev[3]));
   else t_all = t_scan;
-  HIP_TRY(hipEventElapsedTime(&t_filter, P.ev[1], P.ev[4]));
-  HIP_TRY(hipEventElapsedTime(&t_agg, P.ev[4], P.ev[2]));
+  if (P.split_event) {
+    HIP_TRY(hipEventElapsedTime(&t_filter, P.ev[1], P.ev[4]));
+    HIP_TRY(hipEventElapsedTime(&t_agg, P.ev[4], P.ev[2]));
+  } else if (has_filter && !(need_agg && !P.fused_naggs)) {
+    t_filter = t_scan;  // the one kernel between ev[1] and ev[2] is the filter (fused or not)
+  } else {
+    t_agg = t_scan;
+  }
   r.filter_kernel_ms = has_filter ? t_filter : 0.0;
   r.agg_kernel_ms = need_agg ? t_agg : 0.0;
   r.filter_bytes = has_filter ? P.filter_bytes : 0;

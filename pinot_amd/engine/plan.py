@@ -235,13 +235,47 @@ def compile_filter(seg: GpuSegment, fc: Optional[FilterContext]):
     if fc.type == "OR":
         if any(_is_const(k, _TRUE) for k in kids):
             return _TRUE
-        kids = [k for k in kids if not _is_const(k, _FALSE)]
+        kids = _merge_or_leaves([k for k in kids if not _is_const(k, _FALSE)])
         if not kids:
             return _FALSE
         if len(kids) == 1:
             return kids[0]
         return _Node(_lib.NODE_OR, kids)
     raise ValueError(fc.type)
+
+
+def _leaf_ids(leaf):
+    if leaf.kind == _lib.LEAF_DICT_RANGE:
+        return np.arange(leaf.lo, leaf.hi, dtype=np.int32)
+    return np.asarray(leaf.ids, dtype=np.int32)
+
+
+def _merge_or_leaves(kids):
+    """OR of EQ / IN / range leaves on one dictionary column -> one leaf over the union of their dict ids, as the
+    reference's broker rewrites an OR of EQ / IN predicates on one column into one IN (MergeEqInFilterOptimizer,
+    pinot-core/.../query/optimizer/filter/MergeEqInFilterOptimizer.java:40-120): a scan leaf (DICT_SET; the library
+    turns a contiguous id set into a range) when every merged leaf scans, an inverted leaf when every one reads the
+    inverted index. Exclusive (NOT_EQ / NOT_IN) leaves stay apart. The doc set is the OR's."""
+    scan = (_lib.LEAF_DICT_RANGE, _lib.LEAF_DICT_SET)
+    groups, order = {}, []
+    for k in kids:
+        fam = None
+        if isinstance(k, _Leaf) and k.column is not None and not k.exclusive:
+            fam = "scan" if k.kind in scan else ("inv" if k.kind == _lib.LEAF_INVERTED else None)
+        key = (k.column, fam) if fam else id(k)
+        if key not in groups:
+            groups[key] = []
+            order.append(key)
+        groups[key].append(k)
+    out = []
+    for key in order:
+        g = groups[key]
+        if len(g) == 1 or not isinstance(key, tuple):
+            out.extend(g)
+            continue
+        ids = np.unique(np.concatenate([_leaf_ids(k) for k in g])).astype(np.int32)
+        out.append(_Leaf(_lib.LEAF_DICT_SET if key[1] == "scan" else _lib.LEAF_INVERTED, key[0], ids=ids))
+    return out
 
 
 def _flatten(tree, col_index, out, keep):
@@ -627,7 +661,14 @@ class GpuCombineOperator:
                                         r.num_segments_processed, r.num_segments_matched)
             na = r.num_aggregations
             ng = r.num_groups
-            m = 1 << max([p[4] for p in self.prims if p[0] == _lib.AGG_HLL] + [0])
+            plan = getattr(self, "_decode_plan", None)
+            if plan is None:  # per operator, once: HLL width and slots (the server loop decodes every execution)
+                hs = {}
+                for i, p in enumerate(self.prims):
+                    if p[0] == _lib.AGG_HLL:
+                        hs[i] = len(hs)
+                plan = self._decode_plan = (1 << max([p[4] for p in self.prims if p[0] == _lib.AGG_HLL] + [0]), hs)
+            m, hll_slot = plan
             # (no groups: the library's arrays may be null)
             if not self.query.group_by and ng == 1:
                 # one row: read its few slots through the pointers (a numpy view + copy costs ~6 us per array,
@@ -643,10 +684,6 @@ class GpuCombineOperator:
             hll = None
             if r.num_hll and ng:
                 hll = np.ctypeslib.as_array(r.hll_registers, shape=(ng * r.num_hll * m,)).reshape(ng, r.num_hll, m).copy()
-            hll_slot = {}
-            for i, p in enumerate(self.prims):
-                if p[0] == _lib.AGG_HLL:
-                    hll_slot[i] = len(hll_slot)
             # long_exact[a]: the library kept an exact int64 sum (else it summed in double: int64 overflow bound)
             exact = [bool(r.long_exact[i]) for i in range(na)] if na else []
 

@@ -89,3 +89,61 @@ def test_bitsliced_sets(b):
     for _ in range(50):
         s = sorted(set(int(x) for x in rng.integers(0, card, rng.integers(1, 5))))
         assert np.array_equal(bs_set(pl, b, s), lane_major(np.isin(ids, s))), (b, s)
+
+
+def bs_runs(pl, b, runs):
+    """filter.hip bs_runs: OR over runs [a, b] of (gt | eq_a) & (lt | eq_b), both bounds tested in one plane pass."""
+    full = np.uint32(0xFFFFFFFF)
+    res = np.zeros(64, np.uint32)
+    for a, z in runs:
+        gt, lt = np.zeros(64, np.uint32), np.zeros(64, np.uint32)
+        eqa, eqb = np.full(64, full, np.uint32), np.full(64, full, np.uint32)
+        for k in range(b):
+            if (a >> (b - 1 - k)) & 1:
+                eqa &= pl[k]
+            else:
+                gt |= eqa & pl[k]
+                eqa &= ~pl[k]
+            if (z >> (b - 1 - k)) & 1:
+                lt |= eqb & ~pl[k]
+                eqb &= pl[k]
+            else:
+                eqb &= ~pl[k]
+        res |= (gt | eqa) & (lt | eqb)
+    return res
+
+
+def id_runs(ids_in, card, exclusive):
+    """runtime.cpp DICT_SET -> DevNode.bs_runs: the matching ids (complemented when exclusive) as runs."""
+    member = np.zeros(card, bool)
+    member[list(ids_in)] = True
+    if exclusive:
+        member = ~member
+    runs, start = [], None
+    for i in range(card + 1):
+        on = i < card and member[i]
+        if on and start is None:
+            start = i
+        elif not on and start is not None:
+            runs.append((start, i - 1))
+            start = None
+    return runs
+
+
+@pytest.mark.parametrize("b", [1, 3, 5, 8, 10, 12])
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_bitsliced_id_runs(b, exclusive):
+    """IN / NOT IN sets of at most 4 runs (OR of EQ predicates merged into one IN, SSB Q3.3's two cities, Q4.1's
+    P_MFGR pair): the OR of plane ranges equals membership for every doc."""
+    rng = np.random.default_rng(100 + b)
+    card = max(2, (1 << b) - int(rng.integers(0, 2)))
+    ids = rng.integers(0, card, 2048)
+    pl = planes(ids, b)
+    for _ in range(60):
+        n = int(rng.integers(1, min(card, 9)))
+        chosen = set(int(x) for x in rng.choice(card, n, replace=False))
+        runs = id_runs(chosen, card, exclusive)
+        if not runs or len(runs) > 4:
+            continue
+        want = lane_major(np.isin(ids, list(chosen)) != exclusive)
+        assert np.array_equal(bs_runs(pl, b, runs), want), (b, sorted(chosen), exclusive, runs)

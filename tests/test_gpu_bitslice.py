@@ -39,7 +39,22 @@ def _filters():
             "c4 = 8 AND c6 BETWEEN 20 AND 80 AND c7 > 100 AND c8 < 300 AND c10 >= 1000 AND c11 < 5000",
             # IN sets of <= 4 ids over a dictionary of <= 64 (OR of equalities on the planes), and ones that are not
             "c3 IN (-4, 8, 14)", "c5 IN (-7, 2, 89) AND c2 = -1 AND c9 > 500", "c6 IN (-7, 182) AND c4 BETWEEN 5 AND 20",
-            "c6 NOT IN (-7, 182) AND c4 > 5", "c6 IN (-7, -4, -1, 2, 5, 8) AND c3 < 8"]
+            "c6 NOT IN (-7, 182) AND c4 > 5", "c6 IN (-7, -4, -1, 2, 5, 8) AND c3 < 8",
+            # OR of EQ / IN / ranges on one column, merged into one IN (MergeEqInFilterOptimizer) and tested on the
+            # planes as an OR of <= 4 id runs (ConjLeaf kind 4) over dictionaries of any size up to 12 bits
+            "(c8 = 8 OR c8 = 80) AND c5 < 40", "(c12 = -4 OR c12 = 2000 OR c12 = 8990) AND c3 > 2",
+            "(c10 BETWEEN 100 AND 200 OR c10 = 2000) AND c7 < 300", "c9 NOT IN (-7, 500) AND c6 > 50",
+            "(c11 = 5 OR c11 IN (11, 14, 17)) AND c4 < 20", "c8 IN (-7, 2, 89, 300, 500) AND c2 = -1",
+            "(c7 = -7 OR c7 = 374) AND (c9 = 20 OR c9 = 1000)"]
+    return out
+
+
+def _cases():
+    out = []
+    for f in _filters():
+        out += [pytest.param(f, "default", id=f"{f}-default"), pytest.param(f, "no-runs", id=f"{f}-no-runs")]
+        if " IN " in f:  # IN sets of <= 64-entry dictionaries as ids on the planes (opt-in PHIP_BS_SETS)
+            out.append(pytest.param(f, "bs-sets", id=f"{f}-bs-sets"))
     return out
 
 
@@ -53,16 +68,16 @@ def segs(gpu_lib):
         g.destroy()
 
 
-@pytest.mark.parametrize("sets", [False, True], ids=["ranges", "bs-sets"])
-@pytest.mark.parametrize("flt", _filters())
-def test_gpu_bitsliced_doc_sets(flt, sets, segs, monkeypatch):
+@pytest.mark.parametrize("flt,mode", _cases())
+def test_gpu_bitsliced_doc_sets(flt, mode, segs, monkeypatch):
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     from tests.test_gpu_parity import _assert_intermediates_equal, _words_from_mask
     raws, gs = segs
-    if sets:  # IN sets on the planes too (opt-in: PHIP_BS_SETS, read when a plan is prepared)
-        if " IN " not in flt:
-            pytest.skip("no IN set")
+    if mode == "bs-sets":  # IN sets on the planes as id masks (opt-in: PHIP_BS_SETS, read when a plan is prepared)
         monkeypatch.setenv("PHIP_BS_SETS", "1")
+        monkeypatch.setenv("PHIP_BS_RUNS", "0")
+    elif mode == "no-runs":  # sets off the planes: the packed-word conjunction or the interpreter
+        monkeypatch.setenv("PHIP_BS_RUNS", "0")
     qc = parse(f"SELECT COUNT(*), SUM(m) FROM t WHERE {flt}")
     for raw, g in zip(raws, gs):
         want = _words_from_mask(executor.eval_filter(OracleSegment(raw), qc.filter))

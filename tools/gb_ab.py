@@ -1,0 +1,96 @@
+"""A/B of library settings on the SSB group-by configs (C3 Q2.x-Q4.x, C5) inside ONE process: the SF100 segments
+are generated and loaded once, then every query is planned and timed under each setting (environment variables
+the library reads at plan creation, e.g. PHIP_GB_BATCH=0 / PHIP_GB_MODE=global). Prints one JSON line per
+(query, setting): p50 wall, mean filter / aggregation kernel ms (HIP events), groups; and checks that every
+setting returns the same groups and values (exact for integer results, 1e-9 relative for doubles).
+
+usage: python tools/gb_ab.py --queries Q2.1,Q3.1,C5 --set "" --set PHIP_GB_BATCH=0 [--sf 100] [--reps 20]"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _same(a, b):
+    if isinstance(a, (list, tuple)):
+        return all(_same(x, y) for x, y in zip(a, b))
+    if isinstance(a, np.ndarray):
+        return np.array_equal(a, b)
+    if isinstance(a, float) or isinstance(b, float):
+        return a == b or abs(a - b) <= 1e-9 * max(abs(a), abs(b))
+    return a == b
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--queries", default="Q2.1,Q2.2,Q2.3,Q3.1,Q3.2,Q3.3,Q3.4,Q4.1,Q4.2,Q4.3,C5")
+    ap.add_argument("--set", action="append", default=None, help="space-separated NAME=VALUE settings ('' = none)")
+    ap.add_argument("--sf", type=int, default=100)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    args = ap.parse_args()
+    sets = args.set if args.set is not None else [""]
+    from pinot_amd import _lib
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    from pinot_amd.engine.segment import GpuSegment
+    from pinot_amd.query.sql import parse
+    from tools import ssb
+    _lib.check(_lib.load().phip_init((ctypes.c_int32 * 1)(0), 1))
+    queries = args.queries.split(",")
+    cols = ssb.columns_for(queries)
+    nseg = (args.sf * ssb.ROWS_PER_SF) // ssb.SEGMENT_ROWS
+    gsegs = []
+    t0 = time.time()
+    for i in range(0, nseg, 10):
+        for r in ssb.make_segments(args.sf, cols, seed=42, segments=range(i, min(nseg, i + 10))):
+            gsegs.append(GpuSegment(r))
+            for ci in r.columns.values():
+                if not ci.metadata.is_sorted:
+                    ci.forward = b""
+    print(json.dumps({"loaded_segments": len(gsegs), "load_s": round(time.time() - t0, 1)}), flush=True)
+    base_env = dict(os.environ)
+    for q in queries:
+        qc = parse(ssb.SSB_QUERIES[q])
+        ref = None
+        for st in sets:
+            os.environ.clear()
+            os.environ.update(base_env)
+            for kv in st.split():
+                k, v = kv.split("=", 1)
+                os.environ[k] = v
+            op = GpuInstancePlanMaker().make_instance_plan(qc, gsegs)
+            wall, fk, ak = [], [], []
+            blk = None
+            for i in range(args.warmup + args.reps):
+                ts = time.perf_counter()
+                blk = op.next_block()
+                te = time.perf_counter()
+                if i >= args.warmup:
+                    wall.append((te - ts) * 1e3)
+                    fk.append(getattr(blk, "filter_kernel_ms", 0.0) or 0.0)
+                    ak.append(getattr(blk, "agg_kernel_ms", 0.0) or 0.0)
+            op.close()
+            groups = blk.groups
+            same = None
+            if ref is None:
+                ref = groups
+            else:
+                same = set(ref) == set(groups) and all(_same(ref[k], groups[k]) for k in ref)
+            print(json.dumps({"query": q, "set": st, "p50_ms": round(float(np.median(wall)), 4),
+                              "filter_ms": round(float(np.mean(fk)), 4), "agg_ms": round(float(np.mean(ak)), 4),
+                              "groups": len(groups), "docs": blk.stats.num_docs_scanned,
+                              "fused": bool(getattr(blk, "fused", False)), "same_as_first": same}), flush=True)
+    os.environ.clear()
+    os.environ.update(base_env)
+    for g in gsegs:
+        g.destroy()
+
+
+if __name__ == "__main__":
+    main()
