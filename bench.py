@@ -6,7 +6,8 @@ x 6M rows per GPU (SF100 per GPU, weak scaling). At N = 1 the rank holds exactly
 N > 1 each rank holds 125 segments of an SF(125N) table (N = 8: SF1000, BASELINE C5) and the step runs over
 the first 100 of them, while the C5 query (DISTINCTCOUNTHLL + GROUP BY) runs over all 125 per rank and is
 reported under "c5". Partial aggregates of each query are merged across ranks (the CombineOperator
-replacement's exchange step: one SUM + one MAX all-reduce per query, engine/distributed.py). value = rows
+replacement's exchange step, engine/distributed.distributed_block: each GPU's one-group partial table -- rows and
+statistics in device memory -- all-reduced in place over RCCL, one int64 SUM collective for Q1.x). value = rows
 scanned per second over the whole job (3 x 600M x N rows per step / max-over-ranks wall time of the K timed
 steps).
 
@@ -96,19 +97,15 @@ def run_c5(args, dist, qc, gsegs, torch):
 
 def run_layout(args, dist, queries, qcs, gsegs, torch):
     """Warm-up, then exactly args.steps timed steps bracketed by barrier + synchronize on both sides."""
-    from pinot_amd.engine.distributed import allreduce_block
+    from pinot_amd.engine.distributed import distributed_block
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     pm = GpuInstancePlanMaker()
     ops = {q: pm.make_instance_plan(qcs[q], gsegs) for q in queries}
 
     def run_query(q):
-        blk = ops[q].next_block()
-        if dist is not None:  # the exchange step: RCCL all-reduce of the partial blocks
-            merged = allreduce_block(blk, dist)
-            for k in ("filter_kernel_ms", "agg_kernel_ms", "filter_bytes", "agg_bytes", "scan_kernel_ms"):
-                setattr(merged, k, getattr(blk, k, 0))
-            return merged
-        return blk
+        if dist is not None:  # the exchange step: the partial tables all-reduced in place on the GPUs (RCCL)
+            return distributed_block(ops[q], dist)  # (the merged block carries this GPU's kernel times)
+        return ops[q].next_block()
 
     for _ in range(args.warmup):
         for q in queries:

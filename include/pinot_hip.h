@@ -380,9 +380,21 @@ typedef struct phip_partial {
   /* This GPU's execution statistics (phip_result order: docs scanned, entries scanned in filter, entries
    * scanned post filter, total docs, segments processed, segments matched); summed over GPUs by the caller. */
   int64_t stats[6];
+  /* Aggregation-only plans (num_groups = 1): the same six statistics as int64 in DEVICE memory right after the
+   * table's last row (stats_dev = table + num_rows), so one int64 SUM all-reduce covers the table's integer rows and
+   * them; phip_plan_finish then reads the merged statistics from there. NULL for group-by partials (stats[] holds
+   * them). */
+  int64_t *stats_dev;
+  /* 1: hll holds u8 registers ([num_hll][G][1 << log2m] bytes: the all-reduce MAX runs on them directly); 0: u32. */
+  int32_t hll_u8;
+  int32_t reserved_partial;
 } phip_partial;
 
-/* Runs a dense group-by plan up to its partial table and returns it (the kernels have completed). Returns
+/* Runs a dense group-by plan up to its partial table and returns it (the kernels have completed). An
+ * aggregation-only plan (AggregationResultsBlockMerger.java:34-49's inputs) hands out a one-group table: row 0 =
+ * matched docs, row 1 + a = aggregation a in its row kind's encoding (MIN / MAX as the order-preserving u64 image),
+ * the statistics in stats_dev and u8 HLL registers -- all in device memory, so GPUs merge them with RCCL
+ * all-reduces and no host copy. Returns
  * PHIP_ERR_UNSUPPORTED, with nothing to merge, for hash-table key spaces and when the GPU's distinct groups
  * reach numGroupsLimit (the per-segment first-seen limit needs the record path: phip_plan_execute). Until
  * phip_plan_finish the table belongs to the caller: it may all-reduce it in place (on any stream, synchronised

@@ -130,7 +130,8 @@ class Partial(ctypes.Structure):
                 ("log2m", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("table", ctypes.c_void_p), ("hll", ctypes.c_void_p),
                 ("row_kinds", ctypes.c_int32 * PARTIAL_MAX_ROWS), ("global_keys", ctypes.c_int32),
-                ("stats", ctypes.c_int64 * 6)]
+                ("stats", ctypes.c_int64 * 6), ("stats_dev", ctypes.c_void_p), ("hll_u8", ctypes.c_int32),
+                ("reserved_partial", ctypes.c_int32)]
 
 
 class PhipError(RuntimeError):

@@ -1173,6 +1173,7 @@ struct Plan {
       if (e) (void)hipEventDestroy(e);
     for (void *p : allocs) (void)hipFree(p);
     if (pinned) (void)hipHostFree(pinned);
+    if (pstage) (void)hipHostFree(pstage);
   }
   // configuration
   DevAggQuery dq;
@@ -1224,6 +1225,13 @@ struct Plan {
   hipStream_t graph_stream = nullptr;  // the lane stream the graph was captured on
   bool clean = false;  // device seg_matched / HLL registers are zero (finalize_all reset them last time)
   bool partial_pending = false;  // phip_plan_execute_partial handed the table out; phip_plan_finish is next
+  // aggregation-only partials: [1 + naggs] u64 rows + 6 int64 statistics (device), u8 HLL registers (device), and a
+  // pinned staging area for their one H2D / D2H copy each
+  uint64_t *ptab = nullptr;
+  uint8_t *phll = nullptr;
+  uint64_t *pstage = nullptr;
+  double part_times[5] = {0, 0, 0, 0, 0};  // the partial's execution: scan, device, filter, agg kernel ms; fused
+  int64_t part_bytes[2] = {0, 0};           // its filter / agg bytes (reported again by phip_plan_finish)
   // one segment, hash table, key space >= numGroupsLimit: the normal pass records every slot's first matched doc
   // (aggregate.hip seg_keys with one segment: the key is unchanged), so the limit pass starts from its table
   uint32_t *first_doc = nullptr;
@@ -3096,8 +3104,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   Device *dev = P.dev;
   std::lock_guard<std::mutex> xlock(P.exec_mu);
   if (mode != EXEC_FULL && (!P.group_by || P.dq.mode == GB_HASH))
-    return fail(PHIP_ERR_UNSUPPORTED, "partial tables: dense group-by plans only (this plan: %s)",
-                P.group_by ? "hash-table key space" : "no group-by");
+    return fail(PHIP_ERR_UNSUPPORTED, "partial tables: dense group-by and aggregation plans only (this plan: %s)",
+                P.group_by ? "hash-table key space" : "selection");
   if (mode == EXEC_FINISH) {
     if (!P.partial_pending) return fail(PHIP_ERR_INVALID, "phip_plan_finish without a pending phip_plan_execute_partial");
     if (merged->num_groups != P.dq.num_groups || merged->num_rows != 1 + P.naggs || merged->table != (uint64_t *)P.gtab)
@@ -3515,6 +3523,181 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   return PHIP_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Aggregation-only partials (the cross-GPU merge of AggregationResultsBlockMerger.java:34-49 on the device): one
+// execution, then the result slots encoded as a one-group partial table in device memory -- row 0 matched docs, row
+// 1 + a slot a (COUNT / exact SUM as int64, double SUM as its bits, MIN / MAX as the order-preserving image), the six
+// statistics after the last row, HLL registers as u8 -- uploaded with one copy from a pinned staging area.
+// ------------------------------------------------------------------------------------------------
+static inline uint64_t f64_ordered_host(double d) {  // dev_common.h f64_ordered
+  uint64_t u;
+  memcpy(&u, &d, 8);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+static inline double f64_unordered_host(uint64_t u) {  // dev_common.h f64_unordered (sentinels: +/-inf)
+  if (u == ~0ull) return HUGE_VAL;
+  if (u == 0ull) return -HUGE_VAL;
+  u = (u >> 63) ? (u & 0x7fffffffffffffffull) : ~u;
+  double d;
+  memcpy(&d, &u, 8);
+  return d;
+}
+
+static int32_t agg_partial_buffers(Plan &P) {
+  if (P.ptab) return PHIP_OK;
+  const size_t rows = (size_t)(1 + P.naggs) + 6;
+  const size_t hbytes = (size_t)P.nhll << (P.nhll ? P.log2m : 0);
+  void *t, *h = nullptr, *st;
+  int32_t rc = P.alloc(rows * 8 + 64, &t);
+  if (rc) return rc;
+  if (hbytes && (rc = P.alloc(hbytes + 64, &h))) return rc;
+  HIP_TRY(hipHostMalloc(&st, rows * 8 + hbytes + 64, hipHostMallocDefault));
+  P.ptab = (uint64_t *)t;
+  P.phll = (uint8_t *)h;
+  P.pstage = (uint64_t *)st;
+  return PHIP_OK;
+}
+
+static int32_t execute_agg_partial(Plan &P, phip_partial *part) {
+  if (P.select || P.naggs > kMaxAggs) return fail(PHIP_ERR_UNSUPPORTED, "partial tables: not for selection plans");
+  phip_result *res = nullptr;
+  int32_t rc = execute_plan(P, &res, nullptr, EXEC_FULL);  // (refuses while a partial is pending)
+  if (rc) return rc;
+  std::unique_ptr<phip_result, void (*)(phip_result *)> hold(res, [](phip_result *r) {
+    delete reinterpret_cast<ResultImpl *>(r);
+  });
+  std::lock_guard<std::mutex> xlock(P.exec_mu);
+  if (P.partial_pending) return fail(PHIP_ERR_INVALID, "plan has a pending partial table");
+  if ((rc = agg_partial_buffers(P))) return rc;
+  const int na = P.naggs;
+  const size_t rows = (size_t)(1 + na);
+  uint64_t *h = P.pstage;
+  h[0] = (uint64_t)res->num_docs_scanned;
+  for (int a = 0; a < na; a++) {
+    const int k = P.dq.aggs[a].acc;
+    const double v = res->values[a];
+    uint64_t w;
+    if (k == ACC_COUNT || k == ACC_SUM_I64) w = (uint64_t)res->long_values[a];
+    else if (k == ACC_SUM_F64) memcpy(&w, &v, 8);
+    else if (k == ACC_MIN_F64 || k == ACC_MAX_F64) w = f64_ordered_host(v);
+    else w = 0;  // (HLL: the registers travel in phll)
+    h[1 + a] = w;
+  }
+  const int64_t st6[6] = {res->num_docs_scanned, res->num_entries_scanned_in_filter,
+                          res->num_entries_scanned_post_filter, res->num_total_docs, res->num_segments_processed,
+                          res->num_segments_matched};
+  memcpy(h + rows, st6, sizeof(st6));
+  const size_t hbytes = (size_t)P.nhll << (P.nhll ? P.log2m : 0);
+  if (hbytes) memcpy((uint8_t *)(h + rows + 6), res->hll_registers, hbytes);
+  HIP_TRY(hipSetDevice(P.dev->ordinal));
+  LaneGuard lg{P.dev};
+  if ((rc = acquire_lane(P.dev, &lg.lane))) return rc;
+  hipStream_t st = lg.lane->stream;
+  HIP_TRY(hipMemcpyAsync(P.ptab, h, (rows + 6) * 8, hipMemcpyHostToDevice, st));
+  if (hbytes) HIP_TRY(hipMemcpyAsync(P.phll, h + rows + 6, hbytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  lg.done = true;
+  memset(part, 0, sizeof(*part));
+  part->num_groups = 1;
+  part->num_rows = (int32_t)rows;
+  part->num_hll = P.nhll;
+  part->log2m = P.nhll ? P.log2m : 0;
+  part->device = P.dev->ordinal;
+  part->table = P.ptab;
+  part->hll = (uint32_t *)P.phll;
+  part->hll_u8 = 1;
+  part->row_kinds[0] = PHIP_ROW_COUNT;
+  for (int a = 0; a < na; a++) part->row_kinds[1 + a] = P.dq.aggs[a].acc;
+  memcpy(part->stats, st6, sizeof(st6));
+  part->stats_dev = (int64_t *)(P.ptab + rows);
+  P.part_times[0] = res->scan_kernel_ms;
+  P.part_times[1] = res->device_ms;
+  P.part_times[2] = res->filter_kernel_ms;
+  P.part_times[3] = res->agg_kernel_ms;
+  P.part_times[4] = res->fused;
+  P.part_bytes[0] = res->filter_bytes;
+  P.part_bytes[1] = res->agg_bytes;
+  part->global_keys = 1;  // (one group: nothing to key)
+  P.partial_pending = true;
+  return PHIP_OK;
+}
+
+static int32_t finish_agg_partial(Plan &P, const phip_partial *merged, phip_result **out_result) {
+  std::lock_guard<std::mutex> xlock(P.exec_mu);
+  if (!P.partial_pending) return fail(PHIP_ERR_INVALID, "phip_plan_finish without a pending phip_plan_execute_partial");
+  const int na = P.naggs;
+  const size_t rows = (size_t)(1 + na);
+  if (merged->table != P.ptab || merged->num_rows != (int32_t)rows || merged->num_groups != 1)
+    return fail(PHIP_ERR_INVALID, "phip_plan_finish: partial does not belong to this plan");
+  for (int a = 0; a < na; a++) {
+    const int k = merged->row_kinds[1 + a], own = P.dq.aggs[a].acc;
+    if (k != own && !(own == ACC_SUM_I64 && k == ACC_SUM_F64))
+      return fail(PHIP_ERR_INVALID, "phip_plan_finish: row %d kind %d (plan: %d)", 1 + a, k, own);
+  }
+  const size_t hbytes = (size_t)P.nhll << (P.nhll ? P.log2m : 0);
+  uint64_t *h = P.pstage;
+  HIP_TRY(hipSetDevice(P.dev->ordinal));
+  LaneGuard lg{P.dev};
+  int32_t rc = acquire_lane(P.dev, &lg.lane);
+  if (rc) return rc;
+  hipStream_t st = lg.lane->stream;
+  HIP_TRY(hipMemcpyAsync(h, P.ptab, (rows + 6) * 8, hipMemcpyDeviceToHost, st));
+  if (hbytes) HIP_TRY(hipMemcpyAsync(h + rows + 6, P.phll, hbytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  lg.done = true;
+  auto impl = std::make_unique<ResultImpl>();
+  phip_result &r = impl->pub;
+  memset(&r, 0, sizeof(r));
+  const int64_t *st6 = merged->stats_dev ? (const int64_t *)(h + rows) : merged->stats;
+  r.num_docs_scanned = st6[0];
+  r.num_entries_scanned_in_filter = st6[1];
+  r.num_entries_scanned_post_filter = st6[2];
+  r.num_total_docs = st6[3];
+  r.num_segments_processed = (int32_t)st6[4];
+  r.num_segments_matched = (int32_t)st6[5];
+  impl->values.resize(std::max(na, 1));
+  impl->longs.resize(std::max(na, 1));
+  impl->exact.resize(std::max(na, 1), 0);
+  for (int a = 0; a < na; a++) {
+    const int k = merged->row_kinds[1 + a];
+    const uint64_t w = h[1 + a];
+    double d = 0.0;
+    int64_t l = 0;
+    if (k == ACC_COUNT || k == ACC_SUM_I64) {
+      l = (int64_t)w;
+      d = (double)l;
+    } else if (k == ACC_SUM_F64) {
+      memcpy(&d, &w, 8);
+    } else if (k == ACC_MIN_F64 || k == ACC_MAX_F64) {
+      d = f64_unordered_host(w);
+    }
+    impl->values[a] = d;
+    impl->longs[a] = l;
+    impl->exact[a] = (k == ACC_COUNT || k == ACC_SUM_I64) ? 1 : 0;
+  }
+  impl->hll.assign((const uint8_t *)(h + rows + 6), (const uint8_t *)(h + rows + 6) + hbytes);
+  impl->seg_docs.assign(1, 0);
+  r.num_aggregations = na;
+  r.num_groups = 1;
+  r.num_hll = P.nhll;
+  r.values = impl->values.data();
+  r.long_values = impl->longs.data();
+  r.hll_registers = impl->hll.data();
+  r.group_keys = impl->keys.data();
+  r.long_exact = impl->exact.data();
+  r.segment_docs_matched = impl->seg_docs.data();
+  r.scan_kernel_ms = P.part_times[0];  // (this GPU's execution of the partial)
+  r.device_ms = P.part_times[1];
+  r.filter_kernel_ms = P.part_times[2];
+  r.agg_kernel_ms = P.part_times[3];
+  r.fused = (int32_t)P.part_times[4];
+  r.filter_bytes = P.part_bytes[0];
+  r.agg_bytes = P.part_bytes[1];
+  P.partial_pending = false;
+  *out_result = &impl.release()->pub;
+  return PHIP_OK;
+}
+
 // ================================================================================================
 // C ABI
 // ================================================================================================
@@ -3701,6 +3884,7 @@ PHIP_API int32_t phip_plan_execute_partial(uint64_t plan, phip_partial *out_part
   Plan *p;
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
+  if (!p->group_by) return execute_agg_partial(*p, out_partial);
   return execute_plan(*p, nullptr, nullptr, EXEC_PARTIAL, out_partial, nullptr);
 }
 
@@ -3710,6 +3894,7 @@ PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phi
   Plan *p;
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
+  if (!p->group_by) return finish_agg_partial(*p, merged, out_result);
   return execute_plan(*p, out_result, nullptr, EXEC_FINISH, nullptr, merged);
 }
 

@@ -496,6 +496,65 @@ def allreduce_partial_table(table, hll, kinds, stats, dist, group=None, any_f64=
     return kinds, [int(x) for x in stage[-6:].cpu().tolist()]
 
 
+def _finish_agg_via_host(op, part, dist, group, any_f64):
+    """The aggregation partial merged over a CPU communicator (gloo tests on one GPU): table + statistics + registers
+    staged through host tensors, then copied back before phip_plan_finish."""
+    import torch
+    dev = torch.device("cuda", part.device)
+    nr = part.num_rows
+    buf = torch.as_tensor(_DeviceArray(part.table, (nr + 6,), "<i8"), device=dev)
+    hb = buf.cpu()
+    kinds = [part.row_kinds[r] for r in range(nr)]
+    t2 = hb[:nr].view(nr, 1).clone()
+    kinds2, stats = allreduce_partial_table(t2, None, kinds, hb[nr:].tolist(), dist, group, any_f64)
+    hb[:nr] = t2.view(-1)
+    hb[nr:] = torch.tensor(stats, dtype=torch.int64)
+    buf.copy_(hb)
+    if part.num_hll:
+        h = torch.as_tensor(_DeviceArray(part.hll, (part.num_hll << part.log2m,), "|u1"), device=dev)
+        hh = h.cpu()
+        dist.all_reduce(hh, op=dist.ReduceOp.MAX, group=group)
+        h.copy_(hh)
+    torch.cuda.current_stream(dev).synchronize()
+    for r, k in enumerate(kinds2):
+        part.row_kinds[r] = k
+    return op.finish(part)
+
+
+def allreduce_aggregation_partial(part, dist, group=None, any_f64=None):
+    """Merge an aggregation-only plan's one-group partial (phip_plan_execute_partial) across ranks in place, on the
+    device: when every row sums as int64 (COUNT, exact SUMs -- SSB Q1.x) the rows and the statistics after them are
+    one contiguous int64 SUM all-reduce, plus one uint8 MAX for HLL registers; other mixes go through
+    allreduce_partial_table (one collective per reduce operator) with the statistics staged from the host."""
+    import torch
+    from .. import _lib
+    dev = torch.device("cuda", part.device)
+    nr = part.num_rows
+    kinds = [part.row_kinds[r] for r in range(nr)]
+    if any_f64 is None:
+        any_f64 = [0] * nr
+    hll = None
+    if part.num_hll:
+        hll = torch.as_tensor(_DeviceArray(part.hll, (part.num_hll << part.log2m,), "|u1"), device=dev)
+    if all(k in (_lib.ROW_COUNT, _lib.ROW_SUM_I64, _lib.ROW_HLL) for k in kinds) and not any(any_f64[:nr]):
+        buf = torch.as_tensor(_DeviceArray(part.table, (nr + 6,), "<i8"), device=dev)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        if hll is not None:
+            dist.all_reduce(hll, op=dist.ReduceOp.MAX, group=group)
+        torch.cuda.current_stream(dev).synchronize()
+        return
+    table = torch.as_tensor(_DeviceArray(part.table, (nr, 1), "<i8"), device=dev)
+    kinds2, stats = allreduce_partial_table(table, None, kinds, list(part.stats), dist, group, any_f64)
+    if hll is not None:
+        dist.all_reduce(hll, op=dist.ReduceOp.MAX, group=group)
+    torch.cuda.current_stream(dev).synchronize()
+    for r, k in enumerate(kinds2):
+        part.row_kinds[r] = k
+    for i, x in enumerate(stats):
+        part.stats[i] = x
+    part.stats_dev = None  # (phip_plan_finish takes the host statistics)
+
+
 def distributed_block(op, dist=None, group=None, fallback_op=None):
     """This rank's share of a query merged with every other rank's; every rank returns the merged block.
 
@@ -513,7 +572,7 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
     multi = dist.is_initialized() and dist.get_world_size(group) > 1
     if not multi:
         return op.next_block()
-    if not getattr(op.query, "group_by", None) or not hasattr(op, "execute_partial"):
+    if not hasattr(op, "execute_partial"):
         return allreduce_block(op.next_block(), dist, group)
     err = None
     part = None
@@ -539,6 +598,11 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
     if v[1] == 0 and v[2] == -v[4] and v[3] == -v[5]:
         try:
             any_f64 = v[6:6 + part.num_rows]
+            if not getattr(op.query, "group_by", None):  # aggregation-only: the one-group table, merged in place
+                if _device(dist, group).type != "cuda":  # (gloo over host memory: stage through the host)
+                    return _finish_agg_via_host(op, part, dist, group, any_f64)
+                allreduce_aggregation_partial(part, dist, group, any_f64)
+                return op.finish(part)
             table, hll = partial_tensors(part)
             kinds = [part.row_kinds[r] for r in range(part.num_rows)]
             if table.device != dev:  # (gloo over host memory: stage through the host, CPU-communicator tests)

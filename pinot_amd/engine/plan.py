@@ -622,8 +622,10 @@ class GpuCombineOperator:
     def execute_partial(self):
         """Runs the plan up to this GPU's dense partial group table (phip_plan_execute_partial). Returns the
         _lib.Partial (device pointers), or None when the plan cannot hand one out (hash-table key space,
-        numGroupsLimit reached on this GPU) -- the caller then merges records instead."""
-        if not self.query.group_by:
+        numGroupsLimit reached on this GPU; an aggregation the non-scan operator answers from dictionaries, whose
+        statistics differ) -- the caller then merges records instead. Aggregation-only plans hand out a one-group
+        table (rows + statistics + u8 HLL registers in device memory, include/pinot_hip.h)."""
+        if not self.query.group_by and self._non_scan_fit():
             return None
         lib = _lib.load()
         self.run_raw(prepare_only=True)

@@ -248,3 +248,111 @@ def test_gpu_c5_sharded_world2(gpu_lib):
         msgs.append(errs.get())
     assert not msgs, msgs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+# ---- aggregation-only queries: the one-group partial table merged on the device ---------------------------------
+AGG_QUERIES = [
+    "SELECT COUNT(*), SUM(m), SUM(h) FROM t WHERE h < 5",  # every row an int64 sum: one SUM collective
+    "SELECT MIN(d), MAX(m), SUM(d), AVG(h), DISTINCTCOUNTHLL(h), MINMAXRANGE(d), COUNT(*) FROM t WHERE m > 0",
+    "SELECT SUM(big), COUNT(*) FROM t",  # int64 on one rank, double on the other (the overflow bound is per GPU)
+]
+
+
+def _agg_worker(rank, world, port, q, errs):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import executor
+        from pinot_amd.engine.distributed import distributed_block
+        from pinot_amd.engine.plan import GpuInstancePlanMaker
+        from pinot_amd.engine.segment import GpuSegment
+        from pinot_amd.query.sql import parse
+        raws = _segments()
+        mine = [GpuSegment(s) for i, s in enumerate(raws) if i % world == rank]
+        qc = parse(q)
+        op = GpuInstancePlanMaker().make_instance_plan(qc, mine)
+        for _ in range(2):  # (the plan executes again after a merge)
+            merged = distributed_block(op, dist)
+            whole, _ = executor.execute(qc, raws)
+            assert merged.stats.num_docs_scanned == whole.stats.num_docs_scanned
+            assert merged.stats.num_total_docs == whole.stats.num_total_docs
+            assert merged.stats.num_segments_matched == whole.stats.num_segments_matched
+            for x, y in zip(merged.results, whole.results):
+                assert _close(x, y), (q, x, y)
+        op.close()
+        for s in mine:
+            s.destroy()
+    except Exception as e:  # surfaced to the parent
+        import traceback
+        errs.put(f"rank {rank}: {type(e).__name__}: {e}\n{traceback.format_exc()}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("q", AGG_QUERIES)
+def test_gpu_distributed_aggregation_world2(q, gpu_lib):
+    """Aggregation-only queries over two ranks through phip_plan_execute_partial's one-group table (rows, statistics,
+    u8 HLL registers) -> merge -> phip_plan_finish: equal to the oracle over all segments (AggregationResultsBlockMerger
+    semantics: sums add, MIN / MAX / registers take the extreme, statistics add)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errs = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agg_worker, args=(r, 2, port, q, errs)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=100)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not errs.empty():
+        msgs.append(errs.get())
+    assert not msgs, msgs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+@pytest.mark.parametrize("q", AGG_QUERIES[:2])
+def test_gpu_aggregation_partial_inplace_rccl_world1(q, gpu_lib):
+    """RCCL all-reduces directly on an aggregation plan's device partial (rows + statistics, u8 registers), then
+    phip_plan_finish: equals phip_plan_execute on the same plan; an all-int64 query is ONE collective."""
+    import torch.distributed as dist
+    from pinot_amd.engine.distributed import allreduce_aggregation_partial
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    from pinot_amd.engine.segment import GpuSegment
+    from pinot_amd.query.sql import parse
+    raws = _segments()
+    segs = [GpuSegment(s) for s in raws]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        qc = parse(q)
+        op = GpuInstancePlanMaker().make_instance_plan(qc, segs)
+        ref = op.next_block()
+        part = op.execute_partial()
+        assert part is not None and part.num_groups == 1 and part.stats_dev and part.hll_u8 == 1
+        calls = []
+        orig = dist.all_reduce
+
+        def counted(t, op=None, group=None, **kw):
+            calls.append(str(t.dtype))
+            return orig(t, op=op if op is not None else dist.ReduceOp.SUM, group=group, **kw)
+        dist.all_reduce = counted
+        allreduce_aggregation_partial(part, dist)
+        dist.all_reduce = orig
+        if q == AGG_QUERIES[0]:
+            assert calls == ["torch.int64"], calls
+        blk = op.finish(part)
+        assert blk.stats.num_docs_scanned == ref.stats.num_docs_scanned
+        assert blk.stats.num_segments_matched == ref.stats.num_segments_matched
+        for x, y in zip(blk.results, ref.results):
+            assert _close(x, y), (x, y)
+        op.close()
+    finally:
+        dist.destroy_process_group()
+        for s in segs:
+            s.destroy()
