@@ -122,7 +122,7 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
             blk = run_query(q)
             lat[q].append((time.perf_counter() - ts) * 1e3)
             kstats[q].append((blk.filter_kernel_ms, blk.agg_kernel_ms, blk.filter_bytes, blk.agg_bytes,
-                               bool(getattr(blk, "fused", False))))
+                               bool(getattr(blk, "fused", False)), int(getattr(blk, "stream_bytes", 0) or 0)))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -164,45 +164,65 @@ def check_parity(queries, qcs, answers, raws, dist, torch):
 
 
 # kernel families of one query execution: a plain filter launch, a filter launch that aggregated its own tiles
-# (fused), and a separate aggregation launch. The FETCH_SIZE x 2 correction (MI355X_MICROARCH.md §HBM) is
-# calibrated for wide coalesced streams only: the plain filter streams, the aggregation and fused launches
-# gather, so their `traffic` is the raw FETCH + WRITE (both figures are reported).
-STREAMING = {"filter_kernel"}
-
-
-def roofline(kstats, queries, traffic, layout, steps):
+# (fused), and a separate aggregation launch.
+#
+# Traffic (MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies a wide stream's 128-B requests at 64 B; other shapes are to be
+# calibrated in the kernel's own access pattern). profiles/<round>_traffic.json holds each family's raw FETCH_SIZE
+# and WRITE_SIZE per launch and `stream_factor` = the streamed bytes / FETCH_SIZE of the SAME filter kernel run as a
+# stream-only probe (PHIP_FILTER_PROBE=1 PHIP_FUSE=0: its bytes are known exactly). A launch's traffic is then its
+# streamed bytes (exact) + the rest of its FETCH at face value (gathers: 64-B requests) + WRITE -- never below the
+# bytes it must stream. `touched` (profiles/<round>_touched.json, tools/touched_lines.py) is the floor of a gathering
+# launch at 64-B line granularity: the streamed bytes + every line holding a matched doc's id or value.
+def roofline(kstats, queries, traffic, touched, layout, steps):
     """Per-kernel achieved bandwidth on algorithmic bytes; headline = the kernel with the most time per step
     (launches per step x mean launch time)."""
     kernels = {}
-    fams = {"filter_kernel": lambda s: (s[0] if not s[4] else 0.0, s[2]),
-            "fused_filter_agg": lambda s: (s[0] if s[4] else 0.0, s[2]),
-            "agg_kernel": lambda s: (s[1], s[3])}
+    fams = {"filter_kernel": lambda s: (s[0] if not s[4] else 0.0, s[2], s[5], False),
+            "fused_filter_agg": lambda s: (s[0] if s[4] else 0.0, s[2], s[5], True),
+            "agg_kernel": lambda s: (s[1], s[3], 0, True)}
+    tj = (traffic or {}).get("per_launch", {}).get(layout) or {}
+    factor = (traffic or {}).get("stream_factor")
+    tq = ((touched or {}).get("per_query") or {}).get(layout) or {}
     for name, pick in fams.items():
-        ms, by, per_q = [], [], {}
+        ms, by, sb, per_q, floor = [], [], [], {}, []
         for q in queries:
             xs = [pick(s) for s in kstats[q]]
-            for t, b in xs:
+            for t, b, st, gathers in xs:
                 if t > 0:
                     ms.append(t)
                     by.append(b)
-            per_q[q] = round(float(np.mean([t for t, _ in xs])), 4)
+                    sb.append(st)
+                    if q in tq:
+                        floor.append(st + (tq[q]["touched_bytes"] if gathers else 0))
+            per_q[q] = round(float(np.mean([x[0] for x in xs])), 4)
         if not ms:
             continue
         launches = len(ms)
         mean_ms = sum(ms) / launches
         mean_b = sum(by) / launches
+        mean_stream = sum(sb) / launches
         ach = mean_b / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
-        tr = ((traffic or {}).get(layout) or {}).get(name)
-        tsel = None
+        tr = tj.get(name)
+        tsel, method = None, None
         if isinstance(tr, dict):
-            tsel = tr["x2"] if name in STREAMING else tr["raw"]
+            if factor:
+                gather_fetch = max(0.0, tr["fetch_raw"] - mean_stream / factor)
+                tsel = int(mean_stream + gather_fetch + tr["write"])
+                method = f"streamed bytes (exact) + FETCH beyond stream/{factor:.3f} (calibrated) + WRITE"
+            else:
+                tsel = tr["x2"] if name == "filter_kernel" else tr["raw"]
+                method = "uncalibrated: FETCH x2 + WRITE (streaming) / FETCH + WRITE (gathering)"
+        fl = int(sum(floor) / len(floor)) if len(floor) == launches else None
+
+        def frac(b):
+            return round(b / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if b else None
         kernels[name] = {"ms_per_launch": round(mean_ms, 4), "launches_per_step": round(launches / steps, 3),
                          "ms_per_step": round(mean_ms * launches / steps, 4),
-                         "alg_bytes_per_launch": int(mean_b), "achieved": round(ach, 1),
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic_per_launch": tsel,
+                         "alg_bytes_per_launch": int(mean_b), "stream_bytes_per_launch": int(mean_stream),
+                         "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic_per_launch": tsel, "traffic_frac": frac(tsel), "traffic_method": method,
                          "traffic_fetch_raw": tr.get("fetch_raw") if isinstance(tr, dict) else None,
-                         "traffic_fetch_x2": tr.get("x2") if isinstance(tr, dict) else None,
-                         "traffic_frac": (round(tsel / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tsel else None),
+                         "touched_floor_per_launch": fl, "touched_frac": frac(fl),
                          "time_share": None, "per_query_ms": per_q}
     tot = sum(k["ms_per_step"] for k in kernels.values()) or 1.0
     for k in kernels.values():
@@ -213,8 +233,8 @@ def roofline(kstats, queries, traffic, layout, steps):
             "frac": d["frac"], "traffic": d["traffic_per_launch"], "kernels": kernels,
             "bytes": "algorithmic bytes per launch (phip_result.filter_bytes / agg_bytes, SURVEY.md §8d) / mean "
                      "launch time from HIP events on the library's stream; dominant = most device time per step "
-                     "(launches x mean); traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE for the "
-                     "streaming filter kernel, raw FETCH_SIZE + WRITE_SIZE for gathering kernels)"}
+                     "(launches x mean); traffic = PMC HBM bytes per launch, calibrated (traffic_method); "
+                     "touched_floor = streamed bytes + the 64-B lines a launch's gathers must move"}
 
 
 def main():
@@ -236,6 +256,8 @@ def main():
                     help="skip the check of every query's answer against oracle/cpu_scan.c on the same segments")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", f"{ROUND}_traffic.json"),
                     help="HBM bytes per launch per kernel and layout from rocprofv3 --pmc passes (tools/traffic.py)")
+    ap.add_argument("--touched-json", default=os.path.join(ROOT, "profiles", f"{ROUND}_touched.json"),
+                    help="64-B lines the gathers touch per query and layout (tools/touched_lines.py)")
     ap.add_argument("--seed", type=int, default=42)
     args = ap.parse_args()
 
@@ -271,9 +293,18 @@ def main():
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("queries") == queries and tj.get("sf") == 100:
-                traffic = tj.get("per_launch")
+                traffic = tj
         except Exception:
             traffic = None
+    touched = None
+    if os.path.exists(args.touched_json):
+        try:
+            with open(args.touched_json) as f:
+                tj = json.load(f)
+            if tj.get("queries") == queries and tj.get("sf") == 100:
+                touched = tj
+        except Exception:
+            touched = None
     layouts = (["sorted", "unsorted"] if world == 1 else ["sorted"]) if args.layout == "both" else [args.layout]
     want_cpu = not args.no_cpu_baseline and rank == 0 and world == 1
     results = {}
@@ -287,7 +318,7 @@ def main():
         rows_per_rank = sum(s.num_docs for s in head)
         elapsed, lat, kstats, answers = run_layout(args, dist, queries, qcs, head, torch)
         res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(head),
-               "lat": lat, "roofline": roofline(kstats, queries, traffic, layout, args.steps)}
+               "lat": lat, "roofline": roofline(kstats, queries, traffic, touched, layout, args.steps)}
         if not args.no_parity:
             res["parity"] = check_parity(queries, qcs, answers, raws, dist, torch)
         if want_c5 and li == 0:

@@ -290,6 +290,9 @@ typedef struct phip_result {
    * group records the segment hands the combine (GroupByCombineOperator.java:128-157; the plan maker's
    * minSegmentGroupTrimSize / groupTrimThreshold checks). For a phip_plan_finish result: this GPU's. */
   const int64_t *segment_docs_matched;
+  /* The part of filter_bytes the filter launch STREAMS (the staged tiles' words, LDS-DMA); for a fused launch
+   * filter_bytes also holds its gathers (agg_bytes folded in). The traffic calibration separates the two. */
+  int64_t stream_bytes;
 } phip_result;
 
 typedef struct phip_dictionary_view {

@@ -361,26 +361,35 @@ def _exact_sum(ex):
     return int(sum(int(x) for x in ex.tolist()))
 
 
+def _hll_hash(L, v, t):
+    """clearspring MurmurHash of one value as DistinctCountHLLAggregationFunction offers it (dictionary values and
+    raw values alike, DistinctCountHLLAggregationFunction.java:106-145,457-466)."""
+    if t == 4:
+        b = v.encode("utf-8")
+        arr = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
+        return L.oracle_murmur_hash_bytes(arr.ctypes.data, len(b), -1)
+    if t in (0, 1):
+        return L.oracle_murmur_hash_long(int(v))
+    if t == 2:
+        return L.oracle_murmur_hash_long(int(np.float32(v).view(np.int32)))
+    return L.oracle_murmur_hash_long(int(np.float64(v).view(np.int64)))
+
+
+def _distinct_values(vals, t):
+    """(distinct values, inverse): FLOAT / DOUBLE by bit pattern (-0.0 and 0.0 are two values to the hash)."""
+    if t in (2, 3):
+        bits = np.asarray(vals, dtype=np.float32 if t == 2 else np.float64).view(np.int32 if t == 2 else np.int64)
+        ub, inv = np.unique(bits, return_inverse=True)
+        return ub.view(np.float32 if t == 2 else np.float64), inv
+    return np.unique(vals, return_inverse=True)
+
+
 def _hll_registers(os_, col, docs, log2m):
     L = _oracle_lib()
     regs = np.zeros(1 << log2m, dtype=np.uint8)
-    m = os_.meta(col)
-    ids = np.unique(os_.dict_ids(col)[docs])
-    d = os_.dictionary(col)
-    t = int(m.data_type)
-    for i in ids.tolist():
-        v = d[i]
-        if t == 4:
-            b = v.encode("utf-8")
-            arr = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
-            x = L.oracle_murmur_hash_bytes(arr.ctypes.data, len(b), -1)
-        elif t in (0, 1):
-            x = L.oracle_murmur_hash_long(int(v))
-        elif t == 2:
-            x = L.oracle_murmur_hash_long(int(np.float32(v).view(np.int32)))
-        else:
-            x = L.oracle_murmur_hash_long(int(np.float64(v).view(np.int64)))
-        L.oracle_hll_offer_hashed(regs.ctypes.data, log2m, x)
+    t = int(os_.meta(col).data_type)
+    for v in _distinct_values(os_.values(col)[docs], t)[0].tolist():  # (each distinct value once: order-free max)
+        L.oracle_hll_offer_hashed(regs.ctypes.data, log2m, _hll_hash(L, v, t))
     return regs
 
 
@@ -496,29 +505,16 @@ def _group_aggregate(os_, ag, docs, gid, ng):
 
 
 def _hll_group_registers(os_, col, docs, gid, ng, log2m):
-    """Registers per group: every distinct matched dictionary value offered once (order-free max)."""
+    """Registers per group: every distinct matched value offered once (order-free max)."""
     L = _oracle_lib()
-    ids = os_.dict_ids(col)[docs]
-    uid, uinv = np.unique(ids, return_inverse=True)
-    reg_of = np.empty(len(uid), dtype=np.int64)
-    rho_of = np.empty(len(uid), dtype=np.uint8)
-    d = os_.dictionary(col)
     t = int(os_.meta(col).data_type)
+    uval, uinv = _distinct_values(os_.values(col)[docs], t)
+    reg_of = np.empty(len(uval), dtype=np.int64)
+    rho_of = np.empty(len(uval), dtype=np.uint8)
     one = np.zeros(1 << log2m, dtype=np.uint8)
-    for j, i in enumerate(uid.tolist()):
+    for j, v in enumerate(uval.tolist()):
         one[:] = 0
-        v = d[i]
-        if t == 4:
-            b = v.encode("utf-8")
-            arr = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
-            x = L.oracle_murmur_hash_bytes(arr.ctypes.data, len(b), -1)
-        elif t in (0, 1):
-            x = L.oracle_murmur_hash_long(int(v))
-        elif t == 2:
-            x = L.oracle_murmur_hash_long(int(np.float32(v).view(np.int32)))
-        else:
-            x = L.oracle_murmur_hash_long(int(np.float64(v).view(np.int64)))
-        L.oracle_hll_offer_hashed(one.ctypes.data, log2m, x)
+        L.oracle_hll_offer_hashed(one.ctypes.data, log2m, _hll_hash(L, v, t))
         r = int(np.nonzero(one)[0][0])
         reg_of[j], rho_of[j] = r, one[r]
     regs = np.zeros((ng, 1 << log2m), dtype=np.uint8)

@@ -112,7 +112,7 @@ class Result(ctypes.Structure):
                 ("filter_bytes", ctypes.c_int64), ("agg_bytes", ctypes.c_int64),
                 ("num_rows", ctypes.c_int64), ("num_select", ctypes.c_int32), ("reserved_select", ctypes.c_int32),
                 ("select_types", ctypes.POINTER(ctypes.c_int32)), ("select_values", ctypes.POINTER(ctypes.c_uint64)),
-                ("segment_docs_matched", ctypes.POINTER(ctypes.c_int64))]
+                ("segment_docs_matched", ctypes.POINTER(ctypes.c_int64)), ("stream_bytes", ctypes.c_int64)]
 
 
 class DictionaryView(ctypes.Structure):

@@ -108,6 +108,43 @@ __device__ __forceinline__ void hll_row_each(ccol_t &c, int32_t doc, F &&f) {
   }
 }
 
+// HyperLogLog entry ((register << 8) | rho) of a raw numeric column's value at doc: clearspring MurmurHash.hashLong of
+// the value as DistinctCountHLLAggregationFunction offers raw values (java.lang.Integer / Long widened, FLOAT / DOUBLE
+// by their bits -- the same mapping ensure_hll applies to dictionary values).
+__device__ __forceinline__ int32_t murmur_hash_long_dev(int64_t data) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = 0;
+  uint32_t k = (uint32_t)data * m;
+  k ^= k >> 24;
+  h ^= k * m;
+  k = (uint32_t)((uint64_t)data >> 32) * m;
+  k ^= k >> 24;
+  h *= m;
+  h ^= k * m;
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+__device__ __forceinline__ uint32_t hll_entry_raw(ccol_t &c, int32_t doc, int log2m) {
+  int64_t x;
+  switch (c.type) {
+    case PHIP_TYPE_INT: x = ((const PHIP_GLB int32_t *)c.raw)[doc]; break;
+    case PHIP_TYPE_LONG: x = ((const PHIP_GLB int64_t *)c.raw)[doc]; break;
+    case PHIP_TYPE_FLOAT: x = ((const PHIP_GLB int32_t *)c.raw)[doc]; break;
+    default: x = ((const PHIP_GLB int64_t *)c.raw)[doc]; break;
+  }
+  const uint32_t ux = (uint32_t)murmur_hash_long_dev(x);
+  const uint32_t j = ux >> (32 - log2m);
+  const uint32_t w = (ux << log2m) | ((1u << (log2m - 1)) + 1u);
+  return (j << 8) | ((uint32_t)__builtin_clz(w) + 1u);
+}
+// the entry of doc's value in column c: the per-dictionary-id table, or hashed from the raw value
+__device__ __forceinline__ uint32_t hll_entry(ccol_t &c, int32_t doc, int log2m) {
+  if (!c.has_dict) return hll_entry_raw(c, doc, log2m);
+  return ((const PHIP_GLB uint32_t *)c.hll)[col_dict_id(c, doc)];
+}
+
 // ------------------------------------------------------------------------------------------------
 // per-chunk work: 64 lanes = up to 64 matched docs of one segment (inactive lanes carry doc 0, a valid
 // doc, so every load stays in bounds, and contribute the identity)
@@ -132,7 +169,7 @@ __device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc,
       if (c.hll_rows) {
         if (act) hll_row_each(c, doc, [&](int r, uint32_t rho) { __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_WG); });
       } else {
-        const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+        const uint32_t h = hll_entry(c, doc, q.log2m);
         if (act) __hip_atomic_fetch_max(&regs[h >> 8], h & 0xffu, PHIP_RLX, PHIP_WG);
       }
     } else {
@@ -148,17 +185,23 @@ __device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc,
 }
 
 // Dense group key of one doc: mixed radix over query-global dict ids, column 0 least significant
-// (DictionaryBasedGroupKeyGenerator.java:314,322,345,442).
+// (DictionaryBasedGroupKeyGenerator.java:314,322,345,442); a raw INT / LONG column contributes value - gb_base.
 __device__ __forceinline__ int64_t group_key(cquery_t &q, cseg_t &seg, int32_t doc) {
   int64_t key = 0;
   for (int k = 0; k < q.num_group_by; k++) {
     ccol_t &c = seg.cols[q.gb_cols[k]];
-    const uint32_t id = col_dict_id(c, doc);
-    const int32_t gid = c.remap ? ((const PHIP_GLB int32_t *)c.remap)[id] : (int32_t)id;
-    key += (int64_t)gid * q.gb_stride[k];
+    int64_t gid;
+    if (!c.has_dict) {
+      gid = raw_i64(c, doc) - c.gb_base;
+    } else {
+      const uint32_t id = col_dict_id(c, doc);
+      gid = c.remap ? ((const PHIP_GLB int32_t *)c.remap)[id] : (int32_t)id;
+    }
+    key += gid * q.gb_stride[k];
   }
   return key;
 }
+
 
 // GB_LDS: table rows in LDS (row 0 counts, row 1+a aggregation a), packed HLL registers in LDS.
 __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_t doc, bool act, lds_u64 *tbl,
@@ -188,7 +231,7 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
         if (c.hll_rows) {
           hll_row_each(c, doc, [&](int r, uint32_t rho) { lds_hll_max(regs, (uint32_t)r, rho); });
         } else {
-          const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+          const uint32_t h = hll_entry(c, doc, q.log2m);
           lds_hll_max(regs, h >> 8, h & 0xffu);
         }
         break;
@@ -382,12 +425,24 @@ __device__ __forceinline__ uint32_t coherent_load(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+constexpr int kFinLoads = 32;  // blocks per lane whose partials are loaded in one round trip (64 x 32 = 2048 blocks)
 __device__ __forceinline__ void fin_slot(const uint64_t *partials, int nblocks, int nslots, int kind, uint64_t *out,
                                          int a) {
   const int lane = lane_id();
   const bool fp = kind == ACC_SUM_F64 || kind == ACC_MIN_F64 || kind == ACC_MAX_F64;
   uint64_t v = fp ? acc_init(kind) : 0;
-  for (int b = lane; b < nblocks; b += 64) v = acc_combine(kind, v, coherent_load(partials + (int64_t)b * nslots + a));
+  // every load of the lane issued before the first combine (coherent loads reach the device coherence point: one
+  // dependent round trip per block would cost ~20 of them)
+  uint64_t w[kFinLoads];
+#pragma unroll
+  for (int i = 0; i < kFinLoads; i++) {
+    const int b = lane + 64 * i;
+    w[i] = b < nblocks ? coherent_load(partials + (int64_t)b * nslots + a) : (fp ? acc_init(kind) : 0);
+  }
+#pragma unroll
+  for (int i = 0; i < kFinLoads; i++) v = acc_combine(kind, v, w[i]);
+  for (int b = lane + 64 * kFinLoads; b < nblocks; b += 64)
+    v = acc_combine(kind, v, coherent_load(partials + (int64_t)b * nslots + a));
   if (fp) v = as_u64(wave_reduce_f64(as_f64(v), kind));
   else v = wave_reduce_u64_add(v);
   if (lane == 0) out[a] = v;

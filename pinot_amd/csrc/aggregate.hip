@@ -55,11 +55,16 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
           hll_row_each(c, d[u], [&](int r, uint32_t rho) { __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_WG); });
     } else if (kind == ACC_HLL) {
       ccol_t &c = seg.cols[ag.col_a];
-      uint32_t id[U];
-      batch_ids<U>(c, d, sa, id);
       uint32_t h[U];
+      if (!c.has_dict) {  // raw values, hashed per doc
 #pragma unroll
-      for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll)[id[u]];
+        for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], q.log2m);
+      } else {
+        uint32_t id[U];
+        batch_ids<U>(c, d, sa, id);
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll)[id[u]];
+      }
 #pragma unroll
       for (int u = 0; u < U; u++)
         if ((act >> u) & 1u)
@@ -132,13 +137,21 @@ __device__ __forceinline__ void batch_group_keys(cquery_t &q, cseg_t &seg, const
   for (int k = 0; k < kMaxGroupBy; k++) {
 #pragma unroll
     for (int u = 0; u < U; u++) id[k][u] = 0;
-    if (k < q.num_group_by) batch_ids_hbm<U>(seg.cols[q.gb_cols[k]], d, id[k]);
+    if (k < q.num_group_by) {
+      ccol_t &c = seg.cols[q.gb_cols[k]];
+      if (c.has_dict) {
+        batch_ids_hbm<U>(c, d, id[k]);
+      } else {  // raw INT / LONG: value - gb_base (below 2^31 here: an LDS / HBM table's key space)
+#pragma unroll
+        for (int u = 0; u < U; u++) id[k][u] = (uint32_t)(raw_i64(c, d[u]) - c.gb_base);
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < kMaxGroupBy; k++) {
     if (k < q.num_group_by) {
       ccol_t &c = seg.cols[q.gb_cols[k]];
-      if (c.remap) {
+      if (c.has_dict && c.remap) {
 #pragma unroll
         for (int u = 0; u < U; u++) id[k][u] = (uint32_t)((const PHIP_GLB int32_t *)c.remap)[id[k][u]];
       }
@@ -307,6 +320,13 @@ __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const
         for (int u = 0; u < U; u++)
           if ((act >> u) & 1u)
             hll_row_each(c, d[u], [&](int r, uint32_t rho) { tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], r, rho); });
+      } else if (!c.has_dict) {  // raw values, hashed per doc
+        uint32_t h[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], q.log2m);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if ((act >> u) & 1u) tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], h[u] >> 8, h[u] & 0xffu);
       } else {
         uint32_t id[U], h[U];
         batch_ids_hbm<U>(c, d, id);
@@ -392,7 +412,7 @@ __device__ __forceinline__ void group_update_global(cquery_t &q, cseg_t &seg, in
             if (regs[r] < rho) __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_AG);
           });
         } else {
-          const uint32_t h = ((const glb_u32 *)c.hll)[col_dict_id(c, doc)];
+          const uint32_t h = hll_entry(c, doc, q.log2m);
           glb_u32 *r = regs + (h >> 8);
           if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
         }

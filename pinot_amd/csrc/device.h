@@ -87,6 +87,7 @@ struct DevCol {
   const uint64_t *str_off;  // raw STRING: doc d's UTF-8 bytes are raw[str_off[d] .. str_off[d+1])
   const uint32_t *planes;   // bit-sliced copy of `words` (bits <= kBitSliceMaxBits), or null: per 2048-doc tile,
                             // plane k (bit bits-1-k of the id) as 64 lane words, bit 31-g of lane l = doc 64g + l
+  int64_t gb_base;          // raw INT / LONG group-by column: its key id = value - gb_base
 };
 constexpr int kBitSliceMaxBits = 12;
 

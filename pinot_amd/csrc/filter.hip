@@ -1273,8 +1273,11 @@ __device__ __forceinline__ void cursor_issue(StageCursor<kS> &c, uint32_t lbase,
   }
 }
 
+#ifndef PHIP_FUSED_WAVES
+#define PHIP_FUSED_WAVES 6  // waves per SIMD the fused launches are compiled for (A/B builds override it)
+#endif
 template <bool kConjOnly, int NA>
-__global__ __launch_bounds__(kFilterBlock, kConjOnly ? 6 : 4) void filter_kernel(DevFilter q) {
+__global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVES : 6) : 4) void filter_kernel(DevFilter q) {
   constexpr int kSConj = NA > 0 ? kMaxConj + kMaxAggStage : kMaxConj;
   constexpr int kS = kConjOnly ? (kSConj < kMaxStage ? kSConj : kMaxStage) : kMaxStage;  // (DevSeg.stage size)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -276,6 +276,8 @@ struct Device {
     int32_t type = 0;
     int32_t width = 0;
     bool global = false;          // the column's registered node-global dictionary
+    bool raw = false;             // a raw INT / LONG column: id = value - raw_base (values not materialised)
+    int64_t raw_base = 0;
     std::vector<uint8_t> values;  // LE typed or fixed-width strings
     ~Remap() {
       for (auto *p : dev)
@@ -1023,6 +1025,33 @@ int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::
   r->type = type;
   r->global = gd != nullptr;
   int width = type == PHIP_TYPE_STRING ? c0.string_width : type_width(type);
+  if (no_dict(c0) && c0.fwd_kind == PHIP_FWD_RAW_CHUNK && (type == PHIP_TYPE_INT || type == PHIP_TYPE_LONG)) {
+    // A raw INT / LONG column (NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator,
+    // DefaultGroupByExecutor.java:106-116): its values themselves are the key dimension -- id = value - min over the
+    // query's segments (the load-time value ranges), value order = id order -- and a result's dictionary holds only
+    // the values its groups use (execute_plan). No global dictionary: a multi-GPU merge takes the record path.
+    if (gd) return fail(PHIP_ERR_INVALID, "column %s is raw: it has no global dictionary", name.c_str());
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (size_t i = 0; i < segs.size(); i++) {
+      const ColumnStore &c = segs[i]->cols[colidx[i]];
+      if (!no_dict(c) || c.fwd_kind != PHIP_FWD_RAW_CHUNK || c.type != type)
+        return fail(PHIP_ERR_UNSUPPORTED, "group-by on column %s: raw in some segments only", name.c_str());
+      if (!c.has_range) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s without a value range", name.c_str());
+      if (segs[i]->num_docs == 0) continue;
+      lo = std::min(lo, c.vmin);
+      hi = std::max(hi, c.vmax);
+    }
+    if (lo > hi) lo = hi = 0;
+    if ((long double)hi - (long double)lo + 1 > (long double)INT32_MAX)
+      return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s: value range above 2^31", name.c_str());
+    r->raw = true;
+    r->raw_base = lo;
+    r->card = (int32_t)(hi - lo + 1);
+    r->dev.assign(segs.size(), nullptr);
+    dev.remaps[key] = r;
+    out = r;
+    return PHIP_OK;
+  }
   for (size_t i = 0; i < segs.size(); i++) {
     const ColumnStore &c = segs[i]->cols[colidx[i]];
     if (no_dict(c)) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s", name.c_str());
@@ -1231,7 +1260,7 @@ struct Plan {
   uint8_t *phll = nullptr;
   uint64_t *pstage = nullptr;
   double part_times[5] = {0, 0, 0, 0, 0};  // the partial's execution: scan, device, filter, agg kernel ms; fused
-  int64_t part_bytes[2] = {0, 0};           // its filter / agg bytes (reported again by phip_plan_finish)
+  int64_t part_bytes[3] = {0, 0, 0};        // its filter / agg / stream bytes (reported again by phip_plan_finish)
   // one segment, hash table, key space >= numGroupsLimit: the normal pass records every slot's first matched doc
   // (aggregate.hip seg_keys with one segment: the key is unchanged), so the limit pass starts from its table
   uint32_t *first_doc = nullptr;
@@ -1434,8 +1463,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL log2m %d over registers of log2m %d", ag.log2m,
                         ca.hll_log2m);
         }
-        if (ag.function == PHIP_AGG_HLL && ca.fwd_kind == PHIP_FWD_RAW_CHUNK)
-          return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over raw column %s", ca.name.c_str());
+        // raw numeric columns offer their values directly (DistinctCountHLLAggregationFunction.java:106-145): the
+        // kernels hash each matched doc's value (agg_common.h hll_entry_raw); raw STRING values stay on the CPU
+        if (ag.function == PHIP_AGG_HLL && ca.fwd_kind == PHIP_FWD_RAW_CHUNK && ca.type == PHIP_TYPE_STRING)
+          return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over raw STRING column %s", ca.name.c_str());
         if (ag.expr != PHIP_EXPR_COLUMN) {
           const ColumnStore &cb = segs[s]->cols[colidx[s][ag.column_b]];
           if (!(cb.type == PHIP_TYPE_INT || cb.type == PHIP_TYPE_LONG)) integral = false;
@@ -1726,12 +1757,16 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       if (dq.aggs[a].acc != ACC_HLL) continue;
       ColumnStore &cs = sg.cols[colidx[s][dq.aggs[a].col_a]];
       if (cs.fwd_kind == PHIP_FWD_HLL_REGISTERS) continue;  // the register rows are the column's raw values
+      if (no_dict(cs)) continue;  // raw values: hashed per doc on the device
       uint32_t *h;
       int32_t rc = ensure_hll(cs, dq.aggs[a].log2m, &h);
       if (rc) return rc;
       ds.cols[dq.aggs[a].col_a].hll = h;
     }
-    for (int k = 0; k < q->num_group_by; k++) ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
+    for (int k = 0; k < q->num_group_by; k++) {
+      ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
+      if (gb_dicts[k]->raw) ds.cols[q->group_by_columns[k]].gb_base = gb_dicts[k]->raw_base;
+    }
     for (int c = 0; c < ncols; c++)
       if (col_remap[c]) ds.cols[c].remap = col_remap[c]->dev[s];
     if (sg.num_docs == 0) continue;
@@ -3370,6 +3405,34 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       }
     }
     impl->dicts = gb_dicts;  // (num_groups_limit_reached was set by group_limit, before any trim)
+    for (int k = 0; k < P.num_group_by; k++) {
+      if (!gb_dicts[k]->raw) continue;
+      // a raw column's result dictionary: the values its groups use, ascending; group keys re-pointed at it
+      std::vector<int32_t> used;
+      used.reserve(ngroups);
+      for (int64_t g = 0; g < ngroups; g++) used.push_back(impl->keys[g * P.num_group_by + k]);
+      std::sort(used.begin(), used.end());
+      used.erase(std::unique(used.begin(), used.end()), used.end());
+      auto rd = std::make_shared<Device::Remap>();
+      rd->type = gb_dicts[k]->type;
+      rd->card = (int32_t)used.size();
+      const int w = type_width(rd->type);
+      rd->values.resize(used.size() * w);
+      for (size_t i = 0; i < used.size(); i++) {
+        const int64_t v = gb_dicts[k]->raw_base + used[i];
+        if (w == 4) {
+          const int32_t v4 = (int32_t)v;
+          memcpy(rd->values.data() + 4 * i, &v4, 4);
+        } else {
+          memcpy(rd->values.data() + 8 * i, &v, 8);
+        }
+      }
+      for (int64_t g = 0; g < ngroups; g++) {
+        int32_t &id = impl->keys[g * P.num_group_by + k];
+        id = (int32_t)(std::lower_bound(used.begin(), used.end(), id) - used.begin());
+      }
+      impl->dicts[k] = rd;
+    }
   } else {
     HIP_TRY(hipStreamSynchronize(st));
   }
@@ -3431,6 +3494,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   r.filter_kernel_ms = has_filter ? t_filter : 0.0;
   r.agg_kernel_ms = need_agg ? t_agg : 0.0;
   r.filter_bytes = has_filter ? P.filter_bytes : 0;
+  r.stream_bytes = r.filter_bytes;
   if (need_agg) {
     int64_t ab = 0;
     for (int s = 0; s < nseg; s++) {
@@ -3617,6 +3681,7 @@ static int32_t execute_agg_partial(Plan &P, phip_partial *part) {
   P.part_times[4] = res->fused;
   P.part_bytes[0] = res->filter_bytes;
   P.part_bytes[1] = res->agg_bytes;
+  P.part_bytes[2] = res->stream_bytes;
   part->global_keys = 1;  // (one group: nothing to key)
   P.partial_pending = true;
   return PHIP_OK;
@@ -3693,6 +3758,7 @@ static int32_t finish_agg_partial(Plan &P, const phip_partial *merged, phip_resu
   r.fused = (int32_t)P.part_times[4];
   r.filter_bytes = P.part_bytes[0];
   r.agg_bytes = P.part_bytes[1];
+  r.stream_bytes = P.part_bytes[2];
   P.partial_pending = false;
   *out_result = &impl.release()->pub;
   return PHIP_OK;

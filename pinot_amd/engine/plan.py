@@ -733,6 +733,7 @@ class GpuCombineOperator:
                                         if self.query.group_by and r.segment_docs_matched else None)
             blk.filter_kernel_ms, blk.agg_kernel_ms = r.filter_kernel_ms, r.agg_kernel_ms
             blk.filter_bytes, blk.agg_bytes = int(r.filter_bytes), int(r.agg_bytes)
+            blk.stream_bytes = int(r.stream_bytes)
             blk.fused = bool(r.fused)
             return blk
         finally:

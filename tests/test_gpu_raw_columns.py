@@ -1,0 +1,112 @@
+"""Group-by keys and DISTINCTCOUNTHLL over raw (no-dictionary) columns on the GPU.
+
+  group-by   NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator
+             (DefaultGroupByExecutor.java:106-116): a raw INT / LONG column keys by its values; on the GPU the key
+             dimension is value - min over the query's segments (value order = key order), mixed with dictionary
+             columns' global ids, and a result's dictionary holds only the values its groups use.
+  HLL        DistinctCountHLLAggregationFunction over raw INT / LONG / FLOAT / DOUBLE values (:106-145): every matched
+             doc's value hashed on the device (clearspring MurmurHash.hashLong, the dictionary path's mapping).
+
+Every block equals the oracle's (values read from the raw chunks: an independent route)."""
+import numpy as np
+import pytest
+
+from oracle import executor
+from pinot_amd.engine.reduce import reduce_blocks, trim_groups
+from pinot_amd.query.sql import parse
+from pinot_amd.segment.creator import SegmentCreator
+from pinot_amd.spi import DataType
+from tests import fixtures
+from tests.test_gpu_limits import _check, _gpu, _segs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def raw_segments(gpu_lib):
+    """Three ragged segments; r* columns raw (no dictionary), d* dictionary-encoded; value ranges differ per segment
+    (negative LONGs, a segment whose INT range sits inside another's)."""
+    rng = np.random.default_rng(31)
+    raws = []
+    for s, n in enumerate((20_000, 33_333, 4097)):
+        c = SegmentCreator(f"raw{s}", no_dictionary_columns=["ri", "rl", "rf", "rd", "rm"])
+        c.add_column("ri", DataType.INT, rng.integers(-50 + 7 * s, 60 + 3 * s, n).astype(np.int32))
+        c.add_column("rl", DataType.LONG, rng.integers(-3_000_000_000, -2_999_990_000, n) + 1_000_000 * s)
+        c.add_column("rf", DataType.FLOAT, np.round(rng.normal(0, 5, n), 1).astype(np.float32))
+        c.add_column("rd", DataType.DOUBLE, np.round(rng.normal(0, 50, n), 2))
+        c.add_column("rm", DataType.LONG, rng.integers(-10 ** 9, 10 ** 9, n))
+        c.add_column("dk", DataType.STRING, np.array([f"k{x}" for x in rng.integers(0, 9 + s, n)]))
+        c.add_column("f", DataType.INT, rng.integers(0, 100, n))
+        raws.append(c.build())
+    segs = _segs(raws)
+    yield raws, segs
+    for g in segs:
+        g.destroy()
+
+
+RAW_GROUP_BY = [
+    "SELECT ri, COUNT(*), SUM(rm), MAX(rd) FROM t GROUP BY ri LIMIT 100000",
+    "SELECT rl, COUNT(*), MIN(ri) FROM t WHERE f < 30 GROUP BY rl LIMIT 100000",
+    "SELECT dk, ri, SUM(rm), DISTINCTCOUNTHLL(rl) FROM t WHERE f >= 10 GROUP BY dk, ri LIMIT 100000",
+    "SELECT ri, dk, COUNT(*) FROM t GROUP BY ri, dk ORDER BY COUNT(*) DESC, ri, dk LIMIT 7",  # device trim
+    "SELECT ri, SUM(rm) FROM t GROUP BY ri ORDER BY ri DESC LIMIT 5",  # key-order trim over raw values
+]
+
+
+@pytest.mark.parametrize("mode", ["auto", "hash"])
+@pytest.mark.parametrize("sql", RAW_GROUP_BY)
+def test_gpu_group_by_raw_columns(sql, mode, raw_segments, monkeypatch):
+    monkeypatch.setenv("PHIP_GB_HASH", "1" if mode == "hash" else "0")
+    raws, segs = raw_segments
+    qc = parse(sql)
+    qc.options["minServerGroupTrimSize"] = "3"  # (so the ORDER BY queries trim on the device)
+    op = _gpu().make_instance_plan(qc, segs)
+    gblk = op.next_block()
+    op.close()
+    oblk, exact = executor.execute(qc, raws)
+    if getattr(gblk, "num_groups_trimmed", False):
+        oblk = trim_groups(qc, oblk)
+    _check(qc, gblk, oblk, exact)
+    assert gblk.key_types == oblk.key_types
+    got, want = reduce_blocks(qc, [gblk]).rows, reduce_blocks(qc, [oblk]).rows
+    if not qc.order_by:
+        got, want = sorted(got), sorted(want)
+    assert fixtures.rows_match(got, want)
+
+
+@pytest.mark.parametrize("limit", [1, 25])
+def test_gpu_group_by_raw_num_groups_limit(limit, raw_segments):
+    """numGroupsLimit over a raw key: per segment the first `limit` values in doc order (the no-dictionary
+    generators' first-seen map, like the dictionary ones)."""
+    raws, segs = raw_segments
+    qc = parse("SELECT ri, COUNT(*), SUM(rm) FROM t GROUP BY ri LIMIT 100000")
+    gblk = _gpu(num_groups_limit=limit).make_instance_plan(qc, segs).next_block()
+    oblk, exact = executor.execute(qc, raws, num_groups_limit=limit)
+    assert oblk.num_groups_limit_reached
+    _check(qc, gblk, oblk, exact)
+
+
+RAW_HLL = [
+    "SELECT DISTINCTCOUNTHLL(ri), DISTINCTCOUNTHLL(rl), DISTINCTCOUNTHLL(rf), DISTINCTCOUNTHLL(rd) FROM t",
+    "SELECT DISTINCTCOUNTHLL(rm), COUNT(*) FROM t WHERE f < 40",
+    "SELECT dk, DISTINCTCOUNTHLL(rd), DISTINCTCOUNTHLL(ri) FROM t GROUP BY dk LIMIT 100000",
+    "SELECT DISTINCTCOUNTHLL(rl, 12), SUM(ri) FROM t WHERE f BETWEEN 20 AND 80",
+]
+
+
+@pytest.mark.parametrize("sql", RAW_HLL)
+def test_gpu_distinctcounthll_raw_columns(sql, raw_segments):
+    """Registers bit-exact against the oracle's offers of the raw values (aggregation and group-by walks)."""
+    raws, segs = raw_segments
+    qc = parse(sql)
+    gblk = _gpu().make_instance_plan(qc, segs).next_block()
+    oblk, exact = executor.execute(qc, raws)
+    if qc.group_by:
+        _check(qc, gblk, oblk, exact)
+    else:
+        from tests.test_gpu_parity import _assert_intermediates_equal
+        _assert_intermediates_equal(qc.aggregations, gblk.results, oblk.results, exact)
+    got, want = reduce_blocks(qc, [gblk]).rows, reduce_blocks(qc, [oblk]).rows
+    if not qc.order_by:  # (no ORDER BY: the broker's rows come in table order; compare as sets)
+        got, want = sorted(got), sorted(want)
+    assert got == want

@@ -47,6 +47,9 @@ def per_kernel(d, counter):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layout", nargs=3, action="append", metavar=("NAME", "FETCH_DIR", "WRITE_DIR"), required=True)
+    ap.add_argument("--calib", nargs=2, metavar=("FETCH_DIR", "BENCH_LOG"),
+                    help="FETCH_SIZE pass over a stream-only probe run of bench.py (PHIP_FILTER_PROBE=1 PHIP_FUSE=0) and "
+                         "that run's JSON line: stream_factor = the filter kernel's streamed bytes / its FETCH_SIZE")
     ap.add_argument("--queries", required=True)
     ap.add_argument("--sf", type=int, default=100)
     ap.add_argument("-o", "--out", required=True)
@@ -67,6 +70,20 @@ def main():
             pl[k] = {"fetch_raw": int(f), "write": int(w), "raw": int(f + w), "x2": int(2 * f + w)}
         out["per_launch"][name] = pl
         out["dispatches"][name] = {"fetch": fn, "write": wn}
+    if a.calib:
+        ft, fn = per_kernel(a.calib[0], "FETCH_SIZE")
+        line = [l for l in open(a.calib[1]) if l.startswith("{")][-1]
+        j = json.loads(line)
+        ks = (j.get("roofline") or {}).get("kernels", {})
+        if "filter_kernel" not in ks or not fn.get("filter_kernel"):
+            raise SystemExit("calibration run has no plain filter_kernel launches")
+        stream = ks["filter_kernel"]["stream_bytes_per_launch"]
+        fetch = ft["filter_kernel"] / fn["filter_kernel"]
+        out["stream_factor"] = round(stream / fetch, 4)
+        out["calibration"] = {"run": "bench.py PHIP_FILTER_PROBE=1 PHIP_FUSE=0 (stream-only filter launches: the "
+                                     "staged tiles' bytes are known exactly)",
+                              "stream_bytes_per_launch": int(stream), "fetch_size_per_launch": int(fetch),
+                              "layout": j.get("config", {}).get("layout")}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
