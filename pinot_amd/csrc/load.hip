@@ -68,6 +68,27 @@ hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32
   return hipGetLastError();
 }
 
+// Doc-order values of a dictionary column with a large dictionary: vals[d] = dict[id(d)] (4- or 8-byte entries).
+// A projection then reads one coalesced-by-doc value instead of the doc's id bits plus a dependent gather into a
+// dictionary that does not stay in L2.
+template <typename T>
+__global__ void materialize_kernel(const uint32_t *__restrict__ words, int32_t bits, const T *__restrict__ dict,
+                                   int64_t n, T *__restrict__ vals) {
+  for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x)
+    vals[d] = dict[decode_bits(words, (uint64_t)d * (uint32_t)bits, (uint32_t)bits)];
+}
+hipError_t launch_materialize(const uint32_t *words, int32_t bits, const void *dict, int32_t width, int64_t n,
+                              void *vals, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (width == 4)
+    materialize_kernel<uint32_t><<<grid_for(n, 256, 8192), 256, 0, s>>>(words, bits, (const uint32_t *)dict, n,
+                                                                         (uint32_t *)vals);
+  else
+    materialize_kernel<uint64_t><<<grid_for(n, 256, 8192), 256, 0, s>>>(words, bits, (const uint64_t *)dict, n,
+                                                                         (uint64_t *)vals);
+  return hipGetLastError();
+}
+
 // Value range of a raw INT / LONG column (LE, resident), for the plan-time int64 overflow bound of
 // integer SUMs (SumAggregationFunction adds in double and never wraps, :76-101). out = {min, max},
 // preset to {INT64_MAX, INT64_MIN} by the caller.

@@ -94,6 +94,8 @@ hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *
 hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
                                       int32_t *err, int32_t *sizes, uint8_t *lits, uint64_t lits_stride, hipStream_t s);
 hipError_t launch_bitslice(const uint32_t *words, int32_t bits, int64_t ntiles, uint32_t *planes, hipStream_t s);
+hipError_t launch_materialize(const uint32_t *words, int32_t bits, const void *dict, int32_t width, int64_t n,
+                              void *vals, hipStream_t s);
 hipError_t launch_varbyte_offsets(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
                                   int32_t per_chunk, int64_t n, uint64_t *len, uint64_t *off, void *temp,
                                   size_t *temp_bytes, int32_t *err, hipStream_t s);
@@ -310,6 +312,7 @@ struct ColumnStore {
   uint64_t *str_off = nullptr;  // raw STRING: num_docs + 1 byte offsets into raw
   uint64_t str_total = 0;       // raw STRING: bytes of all values
   uint32_t *planes = nullptr;   // bit-sliced copy of words (fixed-bit columns of <= kBitSliceMaxBits bits)
+  void *vals = nullptr;         // numeric dictionary column: doc-order LE values (ensure_vals), made on first use
   std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
   std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
   std::map<int, uint32_t *> hll;      // per log2m
@@ -1167,6 +1170,30 @@ int32_t ensure_hll(ColumnStore &c, int log2m, uint32_t **out) {
   return PHIP_OK;
 }
 
+// Doc-order values of a numeric dictionary column (load.hip materialize_kernel), made the first time a plan projects
+// the column as a plain value (see use_vals in phip_plan_create) and kept with the segment: num_docs x 4 / 8 bytes.
+// Plan creation holds the device's mutex, so two plans never build one column's values at once.
+constexpr int64_t kMaterializeMinDict = 1 << 20;
+static int64_t materialize_min_dict() {
+  const char *e = getenv("PHIP_MATERIALIZE_MIN_DICT");  // measurement override (bytes of dictionary)
+  return e ? atoll(e) : kMaterializeMinDict;
+}
+static bool vals_eligible(const ColumnStore &c, int64_t min_dict) {
+  if (no_dict(c) || c.words == nullptr || c.dict == nullptr || c.type == PHIP_TYPE_STRING) return false;
+  return (int64_t)c.card * type_width(c.type) >= min_dict;
+}
+static int32_t ensure_vals(Segment &sg, ColumnStore &c, hipStream_t st, bool *made) {
+  if (c.vals != nullptr) return PHIP_OK;
+  const int w = type_width(c.type);
+  void *p;
+  int32_t rc = dev_alloc(sg, (size_t)std::max<int32_t>(sg.num_docs, 1) * w, &p);
+  if (rc) return rc;
+  HIP_TRY(launch_materialize(c.words, c.bits, c.dict, w, sg.num_docs, p, st));
+  c.vals = p;
+  *made = true;
+  return PHIP_OK;
+}
+
 int acc_kind_for(const phip_aggregation &a, bool integral) {
   switch (a.function) {
     case PHIP_AGG_COUNT: return ACC_COUNT;
@@ -1508,6 +1535,49 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
   }
   dq.num_hll = nhll;
+  // Plain values of SUM / MIN / MAX (no filter leaf, group-by key or HLL reads the column) whose dictionary is
+  // large read the segment's doc-order values: one load by doc instead of the doc's id bits plus a dependent
+  // gather into a dictionary that does not stay in the XCD's L2 (~1M distinct prices per segment: random lines
+  // from the Infinity Cache). The kernels take such a column as a raw one (DevCol.has_dict = 0).
+  std::vector<bool> use_vals(ncols, false);
+  const int64_t vals_min = materialize_min_dict();
+  {
+    const char *me = getenv("PHIP_MATERIALIZE");  // measurement override: "0" = ids + dictionary gathers
+    if (!(me && atoi(me) == 0) && !want_bitmap && vals_min >= 0) {
+      for (int a = 0; a < naggs; a++) {
+        const phip_aggregation &ag = q->aggregations[a];
+        if (ag.function == PHIP_AGG_SUM || ag.function == PHIP_AGG_MIN || ag.function == PHIP_AGG_MAX) {
+          use_vals[ag.column_a] = true;
+          if (ag.expr != PHIP_EXPR_COLUMN) use_vals[ag.column_b] = true;
+        }
+      }
+      for (int a = 0; a < naggs; a++)
+        if (q->aggregations[a].function == PHIP_AGG_HLL) use_vals[q->aggregations[a].column_a] = false;
+      for (int k = 0; k < q->num_group_by; k++)
+        if (q->group_by_columns[k] >= 0 && q->group_by_columns[k] < ncols) use_vals[q->group_by_columns[k]] = false;
+      if (q->filter_offsets && q->filter_nodes)
+        for (int i = q->filter_offsets[0]; i < q->filter_offsets[nprog * nseg]; i++) {
+          const phip_filter_node &fn = q->filter_nodes[i];
+          if (fn.op == PHIP_NODE_LEAF && fn.column >= 0 && fn.column < ncols) use_vals[fn.column] = false;
+        }
+    }
+    bool made = false;
+    for (int c = 0; c < ncols; c++) {
+      if (!use_vals[c]) continue;
+      for (int s = 0; s < nseg; s++) {
+        ColumnStore &cs = segs[s]->cols[colidx[s][c]];
+        if (!vals_eligible(cs, vals_min)) continue;
+        int32_t rc = ensure_vals(*segs[s], cs, st, &made);
+        if (rc) return rc;
+      }
+    }
+    if (made) HIP_TRY(hipStreamSynchronize(st));
+  }
+  // column c of segment s read as raw values (no dictionary, or its doc-order values above)
+  auto as_raw = [&](int s, int c) -> bool {
+    const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
+    return no_dict(cs) || (use_vals[c] && cs.vals != nullptr && vals_eligible(cs, vals_min));
+  };
   // Batched dense-tile walk (aggregate.hip agg_batch) only when every dictionary the aggregations
   // gather from is small enough to stay cache-resident. Gathers from a large dictionary (~1M distinct
   // prices per segment) are bound by random lines from the Infinity Cache, and more of them in flight
@@ -1522,7 +1592,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         for (int c : {ag.column_a, ag.expr != PHIP_EXPR_COLUMN ? ag.column_b : -1}) {
           if (c < 0) continue;
           const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-          if (no_dict(cs)) continue;
+          if (as_raw(s, c)) continue;
           const int64_t w = ag.function == PHIP_AGG_HLL ? 4 : ((cs.type == PHIP_TYPE_LONG || cs.type == PHIP_TYPE_DOUBLE) ? 8 : 4);
           max_dict = std::max<int64_t>(max_dict, (int64_t)cs.card * w);
         }
@@ -1550,7 +1620,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         bool any_dict = false;
         for (int s = 0; s < nseg; s++) {
           const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-          if (no_dict(cs)) continue;
+          if (as_raw(s, c)) continue;
           any_dict = true;
           bits = std::max(bits, cs.bits);
         }
@@ -1580,7 +1650,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       bool numeric = true;
       for (int s = 0; s < nseg; s++) {
         const ColumnStore &cs = segs[s]->cols[colidx[s][cols[k]]];
-        if (no_dict(cs)) continue;
+        if (as_raw(s, cols[k])) continue;
         if (cs.type == PHIP_TYPE_STRING) numeric = false;
         const int64_t w = (cs.type == PHIP_TYPE_LONG || cs.type == PHIP_TYPE_DOUBLE) ? 8 : 4;
         bytes = std::max<int64_t>(bytes, (int64_t)cs.card * w);
@@ -1748,6 +1818,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dc.card = cs.card;
       dc.type = cs.type;
       dc.has_dict = !no_dict(cs);
+      if (dc.has_dict && as_raw(s, c)) {  // doc-order values of a value-only column
+        dc.raw = cs.vals;
+        dc.has_dict = 0;
+      }
       dc.hll_rows = cs.hll_log2m;
       dc.str_off = cs.str_off;
       dc.planes = cs.planes;
@@ -2438,7 +2512,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     pc.progs = proj_progs[c];
     for (int s = 0; s < nseg; s++) {
       const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-      const bool raw = no_dict(cs);
+      const bool raw = as_raw(s, c);
       pc.bits.push_back(raw ? 0 : cs.bits);
       pc.card.push_back(raw ? 0 : cs.card);
       pc.width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));  // STRING: remap / HLL entry
@@ -2808,9 +2882,12 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     P.pinned_dev = (uint64_t *)dp;
   }
   // Finalize in the last workgroup of the plan's last kernel (agg_common.h finalize_tail) for aggregation-only plans:
-  // the finalize_all launch and its dispatch gap go. PHIP_FOLD_FINAL=0 keeps the launch (A/B).
+  // the finalize_all launch and its dispatch gap go, but every workgroup then takes a ticket from one device-scope
+  // counter, and those atomics serialise at the memory side: measured on SSB SF100 sorted (tools/host_ab.sh,
+  // profiles/r04f_host_ab.log) the fused kernel grows 13-50 us and the step 0.346 -> 0.421 ms. Off by default;
+  // PHIP_FOLD_FINAL=1 folds (A/B).
   const char *ff = getenv("PHIP_FOLD_FINAL");
-  if (!group_by && !P.select && !want_bitmap && total_work > 0 && (has_filter || need_agg) && (!ff || atoi(ff) != 0)) {
+  if (!group_by && !P.select && !want_bitmap && total_work > 0 && (has_filter || need_agg) && ff && atoi(ff) != 0) {
     const bool fused = fused_naggs > 0;
     const bool agg_last = need_agg && !fused;
     const bool aggs_here = need_agg && naggs > 0;

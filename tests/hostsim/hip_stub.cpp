@@ -66,6 +66,9 @@ hipError_t launch_chunk_decode(int, int, const uint8_t *, const RawChunk *, int3
 hipError_t launch_chunk_decode_global(int, const uint8_t *, const RawChunk *, int32_t, uint8_t *, int32_t *, int32_t *, uint8_t *,
                                       uint64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_bitslice(const uint32_t *, int32_t, int64_t, uint32_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_materialize(const uint32_t *, int32_t, const void *, int32_t, int64_t, void *, hipStream_t) {
+  return hipSuccess;
+}
 hipError_t launch_varbyte_offsets(const uint8_t *, const uint64_t *, const int32_t *, int32_t, int64_t, uint64_t *, uint64_t *,
                                   void *, size_t *temp_bytes, int32_t *, hipStream_t) { *temp_bytes = 64; return hipSuccess; }
 hipError_t launch_varbyte_copy(const uint8_t *, const uint64_t *, const int32_t *, int32_t, int64_t, const uint64_t *, uint8_t *,

@@ -89,3 +89,23 @@ def test_gpu_fused_ssb_q1(layout, fuse, gpu_lib, monkeypatch):
     finally:
         for s in segs:
             s.destroy()
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+@pytest.mark.parametrize("sql", QUERIES)
+def test_gpu_folded_finalize(sql, fuse, fused_segments, monkeypatch):
+    """PHIP_FOLD_FINAL=1: the last workgroup of the plan's last kernel finalizes (agg_common.h finalize_tail,
+    one device-scope ticket per workgroup) instead of a finalize launch -- same answers."""
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    from tests.test_gpu_parity import _assert_intermediates_equal
+    monkeypatch.setenv("PHIP_FUSE", fuse)
+    monkeypatch.setenv("PHIP_FOLD_FINAL", "1")
+    raws, segs = fused_segments
+    qc = parse(sql)
+    op = GpuInstancePlanMaker().make_instance_plan(qc, segs)
+    oblk, ex = executor.execute(qc, raws)
+    for _ in range(3):  # (the ticket counter resets between executions)
+        blk = op.next_block()
+        assert blk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+        _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
+    op.close()

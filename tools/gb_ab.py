@@ -4,7 +4,8 @@ the library reads at plan creation, e.g. PHIP_GB_BATCH=0 / PHIP_GB_MODE=global).
 (query, setting): p50 wall, mean filter / aggregation kernel ms (HIP events), groups; and checks that every
 setting returns the same groups and values (exact for integer results, 1e-9 relative for doubles).
 
-usage: python tools/gb_ab.py --queries Q2.1,Q3.1,C5 --set "" --set PHIP_GB_BATCH=0 [--sf 100] [--reps 20]"""
+usage: python tools/gb_ab.py --queries Q2.1,Q3.1,C5 --set "" --set PHIP_GB_BATCH=0 [--sf 100] [--reps 20]
+       [--layout sorted]   (the Q1.x configs too: any SSB query name works)"""
 import argparse
 import ctypes
 import json
@@ -34,6 +35,7 @@ def main():
     ap.add_argument("--sf", type=int, default=100)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--layout", default="unsorted")
     args = ap.parse_args()
     sets = args.set if args.set is not None else [""]
     from pinot_amd import _lib
@@ -48,7 +50,8 @@ def main():
     gsegs = []
     t0 = time.time()
     for i in range(0, nseg, 10):
-        for r in ssb.make_segments(args.sf, cols, seed=42, segments=range(i, min(nseg, i + 10))):
+        for r in ssb.make_segments(args.sf, cols, seed=42, segments=range(i, min(nseg, i + 10)),
+                                   layout=args.layout):
             gsegs.append(GpuSegment(r))
             for ci in r.columns.values():
                 if not ci.metadata.is_sorted:
@@ -76,7 +79,9 @@ def main():
                     fk.append(getattr(blk, "filter_kernel_ms", 0.0) or 0.0)
                     ak.append(getattr(blk, "agg_kernel_ms", 0.0) or 0.0)
             op.close()
-            groups = blk.groups
+            groups = getattr(blk, "groups", None)
+            if groups is None:  # aggregation only: one row
+                groups = {(): list(blk.results)}
             same = None
             if ref is None:
                 ref = groups

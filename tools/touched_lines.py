@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--queries", default="Q1.1,Q1.2,Q1.3")
     ap.add_argument("--segs", type=int, default=100)
     ap.add_argument("-o", "--out", required=True)
+    ap.add_argument("--materialize-min", type=int, default=1 << 20,
+                    help="dictionary bytes from which a value-only column reads doc-order values (-1: never)")
     args = ap.parse_args()
     from pinot_amd import _lib
     from pinot_amd.engine.plan import GpuCombineOperator, plan_aggregations
@@ -44,9 +46,11 @@ def main():
     _lib.check(_lib.load().phip_init((ctypes.c_int32 * 1)(0), 1))
     queries = args.queries.split(",")
     cols = ssb.columns_for(queries)
-    out = {"queries": queries, "sf": 100, "line_bytes": 64, "per_query": {},
+    out = {"queries": queries, "sf": 100, "line_bytes": 64, "per_query": {}, "materialize_min": args.materialize_min,
            "method": "per segment: distinct 64-B lines of each projected column's fixed-bit words holding a matched "
-                     "doc's id bits, + distinct 64-B dictionary lines of the matched ids (phip_filter_bitmap docs)"}
+                     "doc's id bits, + distinct 64-B dictionary lines of the matched ids (phip_filter_bitmap docs); "
+                     "a value-only column with a dictionary of >= materialize_min bytes: the lines of its doc-order "
+                     "values instead"}
     for layout in args.layout or ["sorted"]:
         res = {q: {"id_line_bytes": 0, "dict_line_bytes": 0, "matched": 0} for q in queries}
         for i in range(0, args.segs, 10):
@@ -71,6 +75,14 @@ def main():
                             if not m.has_dictionary:
                                 res[q]["id_line_bytes"] += 8 * len(docs)
                                 continue
+                            w = 4 if int(m.data_type) in (0, 2) else 8
+                            where = ssb.SSB_QUERIES[q].upper().split("WHERE", 1)[-1].split("GROUP BY")[0]
+                            if (args.materialize_min >= 0 and m.cardinality * w >= args.materialize_min
+                                    and c.upper() not in where):
+                                # a value-only column with a large dictionary: its doc-order values
+                                # (runtime.cpp ensure_vals), no dictionary gather
+                                res[q]["id_line_bytes"] += 64 * lines_of(docs, 8 * w)
+                                continue
                             b = m.bits_per_element
                             res[q]["id_line_bytes"] += 64 * lines_of(docs, b)
                             ids = np.frombuffer(raw.columns[c].forward, dtype=np.uint8)
@@ -82,7 +94,6 @@ def main():
                                 pos = bitpos + k
                                 bit = (padded[pos >> 3] >> (7 - (pos & 7))) & 1
                                 vals = (vals << 1) | bit
-                            w = 4 if int(m.data_type) in (0, 2) else 8
                             res[q]["dict_line_bytes"] += 64 * int(len(np.unique((vals * w) >> 6)))
                 g.destroy()
         for q in queries:
