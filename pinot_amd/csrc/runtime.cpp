@@ -2414,6 +2414,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   for (const DevSeg &ds : dsegs) any_filter_prog |= ds.node_end > ds.node_begin;
   int fused_naggs = 0;
   bool any_defer = false;
+  std::vector<bool> ids_streamed((size_t)nseg * ncols, false);  // (segment, column): fused tiles stream its ids
   {
     // Fusion saves a launch, the mask round trip and the filter columns' re-read, but a streaming filter
     // wave that stops for a tile's projection gathers leaves its LDS-DMA ring idle. Measured on SSB SF100
@@ -2460,13 +2461,25 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
           for (int c : {ag.col_a, ag.expr != PHIP_EXPR_COLUMN ? ag.col_b : -1}) {
             if (c < 0) continue;
             DevCol &dc = ds.cols[c];
-            if (!dc.has_dict || dc.lds_off >= 0) continue;
-            const bool dense = seg_est[i] * (1024.0 / std::max(1, dc.bits)) >= kStreamValueMin;
+            if (dc.lds_off >= 0) continue;
+            // a column read through its doc-order values (as_raw) streams its packed ids instead when the tiles are
+            // dense enough: fewer bytes per tile than the values, and no per-doc load at all
+            const int sidx = ds.seg_index % nseg;
+            const ColumnStore &cs = segs[sidx]->cols[colidx[sidx][c]];
+            const bool via_vals = !dc.has_dict && !no_dict(cs);
+            if (!dc.has_dict && !via_vals) continue;
+            const int32_t bits = via_vals ? cs.bits : dc.bits;
+            const bool dense = seg_est[i] * (1024.0 / std::max(1, bits)) >= kStreamValueMin;
             if (!(sv ? atoi(sv) != 0 : (dense && !big))) continue;
-            const int32_t bytes = 256 * dc.bits;
+            const int32_t bytes = 256 * bits;
             // (DevSeg.stage holds kMaxStage sources; the fused kernel's cursor takes up to kMaxConj + kMaxAggStage)
             if (ds.num_stage >= std::min(kMaxStage, kMaxConj + kMaxAggStage) || off + bytes + 2 * kStagePad > kSlotBudget)
               continue;
+            if (via_vals) {
+              dc.has_dict = 1;
+              dc.raw = cs.raw;
+              ids_streamed[(size_t)sidx * ncols + c] = true;
+            }
             dc.lds_off = off + kStagePad;
             ds.stage[ds.num_stage++] = {(const uint8_t *)dc.words, bytes, dc.lds_off};
             ds.num_dma += (int32_t)ceil_div(bytes, 1024);
@@ -2512,7 +2525,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     pc.progs = proj_progs[c];
     for (int s = 0; s < nseg; s++) {
       const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-      const bool raw = as_raw(s, c);
+      const bool raw = as_raw(s, c) && !ids_streamed[(size_t)s * ncols + c];
       pc.bits.push_back(raw ? 0 : cs.bits);
       pc.card.push_back(raw ? 0 : cs.card);
       pc.width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));  // STRING: remap / HLL entry

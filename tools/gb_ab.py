@@ -90,6 +90,7 @@ def main():
             print(json.dumps({"query": q, "set": st, "p50_ms": round(float(np.median(wall)), 4),
                               "filter_ms": round(float(np.mean(fk)), 4), "agg_ms": round(float(np.mean(ak)), 4),
                               "groups": len(groups), "docs": blk.stats.num_docs_scanned,
+                              "filter_bytes": getattr(blk, "filter_bytes", None), "agg_bytes": getattr(blk, "agg_bytes", None),
                               "fused": bool(getattr(blk, "fused", False)), "same_as_first": same}), flush=True)
     os.environ.clear()
     os.environ.update(base_env)
