@@ -425,7 +425,7 @@ __device__ __forceinline__ uint32_t coherent_load(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr int kFinLoads = 32;  // blocks per lane whose partials are loaded in one round trip (64 x 32 = 2048 blocks)
+constexpr int kFinLoads = 8;  // blocks per lane whose partials are loaded in one round trip (64 x 32 = 2048 blocks)
 __device__ __forceinline__ void fin_slot(const uint64_t *partials, int nblocks, int nslots, int kind, uint64_t *out,
                                          int a) {
   const int lane = lane_id();
