@@ -83,6 +83,11 @@ typedef struct phip_column_desc {
   uint64_t dictionary_bytes;
   const uint8_t *inverted; /* (card+1) BE u32 offsets + portable Roaring bitmaps, or NULL */
   uint64_t inverted_bytes;
+  /* Null value vector (NullValueVectorReaderImpl: `<column>.bitmap.nullvalue`, one portable Roaring bitmap of the
+   * docs whose value is null; NullValueVectorCreator writes it only when some doc is null), or NULL. Kept in HBM as
+   * dense doc words for PHIP_LEAF_NULL leaves. */
+  const uint8_t *null_vector;
+  uint64_t null_vector_bytes;
 } phip_column_desc;
 
 typedef struct phip_segment_desc {
@@ -122,6 +127,11 @@ typedef struct phip_segment_desc {
  * = [n][n + 1 byte offsets][the n values' UTF-8 bytes] (raw EQ / NOT_EQ / IN / NOT_IN, xor exclusive). */
 #define PHIP_LEAF_RAW_STRING_RANGE 8
 #define PHIP_LEAF_RAW_STRING_SET 9
+/* The column's null value vector (IS NULL: BitmapBasedFilterOperator over NullValueVectorReader.getNullBitmap,
+ * FilterPlanNode.java:294-307; exclusive = IS NOT NULL). A column without a null vector matches no doc (all docs when
+ * exclusive). With enableNullHandling the host composes these with the other leaves (BaseColumnFilterOperator's
+ * trues AND NOT nulls, the And / Or / Not operators' getFalses), so the library needs nothing else for nulls. */
+#define PHIP_LEAF_NULL 10
 
 typedef struct phip_raw_range {
   int64_t lo_int, hi_int; /* INT/LONG columns: lo_int <= v <= hi_int */
@@ -259,7 +269,8 @@ typedef struct phip_result {
   const uint8_t *hll_registers;
   const int32_t *group_keys;
   double scan_kernel_ms; /* device time of the fused filter/aggregate kernel(s) */
-  double device_ms;      /* device time of the whole query on the stream */
+  double device_ms;      /* device time of the query's filter / aggregation kernels (whole sequence incl. memsets and
+                          * finalize when PHIP_TOTAL_EVENTS=1: two more timing markers, ~4 us each on the queue) */
   int32_t num_groups_trimmed; /* 1 when the group set was trimmed to phip_query_desc.trim_size */
   int32_t fused;              /* 1 when the filter kernel aggregated its own tiles (one launch: filter_kernel_ms and
                                  filter_bytes then cover both, agg_* are 0) */

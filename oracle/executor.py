@@ -86,6 +86,22 @@ class OracleSegment:
             self._vals[c] = v
         return v
 
+    def nulls(self, c):
+        """Null value vector of column c as a doc mask (NullValueVectorReaderImpl.getNullBitmap; all False when the
+        column has none)."""
+        out = np.zeros(self.num_docs, dtype=bool)
+        nv = getattr(self.seg.columns[c], "null_vector", None)
+        if nv:
+            buf = np.frombuffer(nv, dtype=np.uint8)
+            docs = np.empty(max(self.num_docs, 1), dtype=np.int32)
+            n = _oracle_lib().oracle_roaring_decode(buf.ctypes.data, len(buf), docs.ctypes.data, len(docs))
+            assert n >= 0, "bad null vector"
+            out[docs[:n]] = True
+        return out
+
+    def has_nulls(self, c):
+        return bool(getattr(self.seg.columns[c], "null_vector", None))
+
     def inverted_docs(self, c, dict_id):
         ci = self.seg.columns[c]
         card = ci.metadata.cardinality
@@ -246,10 +262,70 @@ def _pred_on_values(pred, vals, m):
     return ok
 
 
-def eval_filter(os_: OracleSegment, fc):
+def _always(os_, pred):
+    """PredicateEvaluator.isAlwaysTrue / isAlwaysFalse of a dictionary column's predicate (every / no dictionary
+    value matches); raw-column evaluators are neither."""
+    m = os_.meta(pred.column)
+    if not m.has_dictionary:
+        return None
+    hit = _pred_on_values(pred, os_.dictionary(pred.column), m)
+    return True if hit.all() else (False if not hit.any() else None)
+
+
+def eval_filter3(os_: OracleSegment, fc):
+    """enableNullHandling: (trues, falses, nulls) doc masks of a filter, per the reference operators --
+    BaseColumnFilterOperator (trues exclude the column's nulls, nulls = its null bitmap), BaseFilterOperator.getFalses
+    (NOT(trues OR nulls)), FilterOperatorUtils' always-true leaf over a null column (a bitmap operator: trues = not
+    null, no nulls), EmptyFilterOperator, IS [NOT] NULL (bitmap operators, no nulls), AndFilterOperator /
+    OrFilterOperator (falses = NOT(AND / OR of trues_i OR nulls_i), no nulls) and NotFilterOperator (trues and falses
+    swapped)."""
+    n = os_.num_docs
+    none = np.zeros(n, dtype=bool)
+    if fc.type == "CONSTANT":
+        t = np.full(n, bool(fc.constant))
+        return t, ~t, none
+    if fc.type == "PREDICATE":
+        pred = fc.predicate
+        col = pred.column
+        if pred.type in ("IS_NULL", "IS_NOT_NULL"):
+            t = os_.nulls(col) if pred.type == "IS_NULL" else ~os_.nulls(col)
+            return t, ~t, none
+        p = eval_filter(os_, fc)
+        if not os_.has_nulls(col):
+            return p, ~p, none
+        nul = os_.nulls(col)
+        a = _always(os_, pred)
+        if a is False:
+            return none.copy(), np.ones(n, dtype=bool), none
+        if a is True:
+            return ~nul, nul, none
+        t = p & ~nul
+        return t, ~(t | nul), nul
+    if fc.type == "NOT":
+        t, f, _ = eval_filter3(os_, fc.children[0])
+        return f, t, none
+    parts = [eval_filter3(os_, c) for c in fc.children]
+    if fc.type == "AND":
+        t = np.ones(n, dtype=bool)
+        either = np.ones(n, dtype=bool)
+        for ti, _, ni in parts:
+            t &= ti
+            either &= ti | ni
+        return t, ~either, none
+    t = np.zeros(n, dtype=bool)
+    either = np.zeros(n, dtype=bool)
+    for ti, _, ni in parts:
+        t |= ti
+        either |= ti | ni
+    return t, ~either, none
+
+
+def eval_filter(os_: OracleSegment, fc, null_handling=False):
     n = os_.num_docs
     if fc is None:
         return np.ones(n, dtype=bool)
+    if null_handling:
+        return eval_filter3(os_, fc)[0]
     if fc.type == "AND":
         m = np.ones(n, dtype=bool)
         for c in fc.children:
@@ -266,6 +342,10 @@ def eval_filter(os_: OracleSegment, fc):
         return np.full(n, bool(fc.constant))
     pred = fc.predicate
     col = pred.column
+    if pred.type == "IS_NULL":
+        return os_.nulls(col)
+    if pred.type == "IS_NOT_NULL":
+        return ~os_.nulls(col)
     m = os_.meta(col)
     if m.has_dictionary and (m.is_sorted or (m.has_inverted_index and pred.type != "RANGE")):
         dict_match = _pred_on_values(pred, os_.dictionary(col), m)
@@ -393,9 +473,24 @@ def _hll_registers(os_, col, docs, log2m):
     return regs
 
 
-def _agg_segment(os_, ag, docs):
-    """Intermediate result of one aggregation over matched docs (ascending) of one segment."""
+_NULLABLE = ("sum", "min", "max", "avg", "minmaxrange", "count")
+
+
+def _agg_segment(os_, ag, docs, null_handling=False):
+    """Intermediate result of one aggregation over matched docs (ascending) of one segment. null_handling: a nullable
+    function skips the docs where any column of its argument is null and is None (null) when none is left
+    (NullableSingleInputAggregationFunction.foldNotNull; COUNT(col) counts the rest)."""
     f = ag.function
+    if null_handling and f in _NULLABLE and ag.argument is not None:
+        from pinot_amd.query.context import columns_of
+        keep = np.ones(len(docs), dtype=bool)
+        for c in columns_of(ag.argument):
+            keep &= ~os_.nulls(c)[docs]
+        docs = docs[keep]
+        if f == "count":
+            return len(docs), None
+        if len(docs) == 0:
+            return None, None
     if f == "count":
         return len(docs), None
     if f in ("distinctcounthll", "distinctcountrawhll"):
@@ -581,10 +676,11 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT, min_segm
             projected.update(columns_of(ag.argument))
     for e in query.group_by:
         projected.update(columns_of(e))
+    nh = str(query.options.get("enableNullHandling", "false")).strip().lower() == "true"
     per_seg = []
     for seg in segments:
         os_ = OracleSegment(seg)
-        mask = eval_filter(os_, query.filter)
+        mask = eval_filter(os_, query.filter, nh)
         docs = np.nonzero(mask)[0]
         stats.num_docs_scanned += len(docs)
         stats.num_total_docs += seg.num_docs
@@ -592,21 +688,31 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT, min_segm
         stats.num_segments_processed += 1
         stats.num_segments_matched += int(len(docs) > 0)
         per_seg.append((os_, docs))
+    if nh and query.group_by:
+        cols = set()
+        for ag in query.aggregations:
+            if ag.function in _NULLABLE and ag.argument is not None:
+                cols.update(columns_of(ag.argument))
+        for e in query.group_by:
+            cols.update(columns_of(e))
+        if any(ag.filter is not None for ag in query.aggregations) or any(
+                os_.has_nulls(c) for os_, _ in per_seg for c in cols):
+            raise NotImplementedError("null group keys / per-group null results (not restated)")
     if any(ag.filter is not None for ag in query.aggregations):
         if query.group_by:
             return _execute_filtered_group_by(query, segments, num_groups_limit)
-        return _execute_filtered(query, segments)
+        return _execute_filtered(query, segments, nh)
     if not query.group_by:
         results, exact = None, None
         for os_, docs in per_seg:
-            r = [_agg_segment(os_, ag, docs) for ag in query.aggregations]
+            r = [_agg_segment(os_, ag, docs, nh) for ag in query.aggregations]
             vals = [x[0] for x in r]
             exs = [x[1] for x in r]
             if results is None:
                 results, exact = vals, exs
             else:
+                exact = [_merge_exact(a, b, x, y) for a, b, x, y in zip(exact, exs, results, vals)]
                 results = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(query.aggregations, results, vals)]
-                exact = [(a + b) if a is not None and b is not None else None for a, b in zip(exact, exs)]
         return AggregationResultsBlock(query.aggregations, results, stats), exact
     groups, exact_groups = {}, {}
     limit_reached = False
@@ -663,7 +769,8 @@ def _execute_selection(query, segments):
         if limit <= 0:
             continue
         os_ = OracleSegment(seg)
-        docs = np.nonzero(eval_filter(os_, query.filter))[0][:limit]
+        nh = str(query.options.get("enableNullHandling", "false")).strip().lower() == "true"
+        docs = np.nonzero(eval_filter(os_, query.filter, nh))[0][:limit]
         stats.num_docs_scanned += len(docs)
         stats.num_entries_scanned_post_filter += len(docs) * len(projected)
         stats.num_segments_matched += int(len(docs) > 0)
@@ -682,7 +789,16 @@ def _execute_selection(query, segments):
     return SelectionResultsBlock(names, types, cols, stats)
 
 
-def _execute_filtered(query, segments):
+def _merge_exact(ea, eb, va, vb):
+    """Exact integer sums of two partials (None: no exact sum); a null partial (va / vb None) adds nothing."""
+    if va is None:
+        return eb
+    if vb is None:
+        return ea
+    return (ea + eb) if ea is not None and eb is not None else None
+
+
+def _execute_filtered(query, segments, null_handling=False):
     """FilteredAggregationOperator (pinot-core/.../operator/query/FilteredAggregationOperator.java:67-113):
     aggregations grouped by their FILTER (unfiltered ones under the main filter), each group evaluated
     over main AND its filter; numDocsScanned / post-filter entries summed over the groups
@@ -698,10 +814,10 @@ def _execute_filtered(query, segments):
     first = True
     for seg in segments:
         os_ = OracleSegment(seg)
-        base = eval_filter(os_, query.filter)
+        base = eval_filter(os_, query.filter, null_handling)
         scanned = 0
         for flt, idxs in infos.items():
-            mask = base if flt is None else (base & eval_filter(os_, flt))
+            mask = base if flt is None else (base & eval_filter(os_, flt, null_handling))
             docs = np.nonzero(mask)[0]
             proj = set()
             for i in idxs:
@@ -711,12 +827,12 @@ def _execute_filtered(query, segments):
             stats.num_entries_scanned_post_filter += len(docs) * len(proj)
             for i in idxs:
                 ag = query.aggregations[i]
-                v, ex = _agg_segment(os_, ag, docs)
+                v, ex = _agg_segment(os_, ag, docs, null_handling)
                 if first:
                     results[i], exact[i] = v, ex
                 else:
+                    exact[i] = _merge_exact(exact[i], ex, results[i], v)
                     results[i] = merge_intermediate(ag.function, results[i], v)
-                    exact[i] = exact[i] + ex if exact[i] is not None and ex is not None else None
         first = False
         stats.num_docs_scanned += scanned
         stats.num_total_docs += seg.num_docs

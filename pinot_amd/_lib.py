@@ -19,7 +19,7 @@ PHIP_ERR_NO_DEVICE = 5
 FWD_FIXED_BIT, FWD_SORTED, FWD_RAW_CHUNK, FWD_HLL_REGISTERS = 0, 1, 2, 3
 NODE_LEAF, NODE_AND, NODE_OR, NODE_NOT = 0, 1, 2, 3
 LEAF_MATCH_ALL, LEAF_MATCH_NONE, LEAF_DICT_RANGE, LEAF_DICT_SET, LEAF_DOC_RANGES, LEAF_INVERTED, LEAF_RAW_RANGE, \
-    LEAF_RAW_SET, LEAF_RAW_STRING_RANGE, LEAF_RAW_STRING_SET = range(10)
+    LEAF_RAW_SET, LEAF_RAW_STRING_RANGE, LEAF_RAW_STRING_SET, LEAF_NULL = range(11)
 
 
 class RawRange(ctypes.Structure):
@@ -48,7 +48,8 @@ class ColumnDesc(ctypes.Structure):
                 ("string_width", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("forward", ctypes.c_void_p), ("forward_bytes", ctypes.c_uint64),
                 ("dictionary", ctypes.c_void_p), ("dictionary_bytes", ctypes.c_uint64),
-                ("inverted", ctypes.c_void_p), ("inverted_bytes", ctypes.c_uint64)]
+                ("inverted", ctypes.c_void_p), ("inverted_bytes", ctypes.c_uint64),
+                ("null_vector", ctypes.c_void_p), ("null_vector_bytes", ctypes.c_uint64)]
 
 
 class SegmentDesc(ctypes.Structure):

@@ -313,6 +313,8 @@ struct ColumnStore {
   uint64_t str_total = 0;       // raw STRING: bytes of all values
   uint32_t *planes = nullptr;   // bit-sliced copy of words (fixed-bit columns of <= kBitSliceMaxBits bits)
   void *vals = nullptr;         // numeric dictionary column: doc-order LE values (ensure_vals), made on first use
+  uint64_t *nulls = nullptr;    // null value vector as dense doc words (load_null_vector), or null: no null doc
+  int64_t null_count = 0;
   std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
   std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
   std::map<int, uint32_t *> hll;      // per log2m
@@ -514,6 +516,87 @@ static int32_t parse_inverted(const phip_column_desc &c, ColumnStore &cs, Segmen
   if (rc) return rc;
   cs.inv_blob = (uint8_t *)p;
   HIP_TRY(hipMemcpyAsync(cs.inv_blob, b + off_bytes, blob, hipMemcpyHostToDevice, st));
+  return PHIP_OK;
+}
+
+// Null value vector (NullValueVectorReaderImpl: one portable Roaring bitmap, NullValueVectorCreator.java:83-92) ->
+// dense doc words in HBM, the inverted leaves' layout (bit d % 64 of u64 word d / 64), padded to whole 2048-doc tiles
+// so a PHIP_LEAF_NULL leaf stages 256 bytes per tile like any bitmap leaf. Decoded on the host once at load.
+static int32_t load_null_vector(const phip_column_desc &c, ColumnStore &cs, Segment &seg, hipStream_t st) {
+  const uint8_t *bm = c.null_vector;
+  const uint64_t len = c.null_vector_bytes;
+  const int64_t n = seg.num_docs;
+  if (len < 8) return fail(PHIP_ERR_INVALID, "column %s: null vector truncated", c.name);
+  const uint32_t cookie = le32(bm);
+  int32_t size;
+  uint64_t pos;
+  const uint8_t *runflags = nullptr;
+  if ((cookie & 0xFFFF) == 12347) {
+    size = (int32_t)(cookie >> 16) + 1;
+    runflags = bm + 4;
+    pos = 4 + (uint64_t)(size + 7) / 8;
+  } else if (cookie == 12346) {
+    size = (int32_t)le32(bm + 4);
+    pos = 8;
+  } else {
+    return fail(PHIP_ERR_INVALID, "column %s: null vector bad cookie %u", c.name, cookie);
+  }
+  if (size < 0 || pos + 4ull * size > len) return fail(PHIP_ERR_INVALID, "column %s: null vector header", c.name);
+  const uint8_t *hdr = bm + pos;
+  pos += 4ull * size;
+  const bool has_off = runflags == nullptr || size >= 4;
+  const uint8_t *offs = bm + pos;
+  if (has_off) pos += 4ull * size;
+  if (pos > len) return fail(PHIP_ERR_INVALID, "column %s: null vector header", c.name);
+  const int64_t nwords = round_up(std::max<int64_t>(n, 1), kTileDocs) / 64;
+  std::vector<uint64_t> words((size_t)nwords, 0);
+  int64_t count = 0;
+  auto set = [&](int64_t d) -> bool {
+    if (d < 0 || d >= n) return false;
+    words[(size_t)(d >> 6)] |= 1ull << (d & 63);
+    count++;
+    return true;
+  };
+  for (int32_t k = 0; k < size; k++) {
+    const int64_t key = le16(hdr + 4 * k);
+    const int32_t ccard = (int32_t)le16(hdr + 4 * k + 2) + 1;
+    const bool is_run = runflags && ((runflags[k >> 3] >> (k & 7)) & 1);
+    if (has_off) pos = le32(offs + 4 * k);
+    const int64_t base = key << 16;
+    if (is_run) {
+      if (pos + 2 > len) return fail(PHIP_ERR_INVALID, "column %s: null vector container overflow", c.name);
+      const int32_t nruns = le16(bm + pos);
+      if (pos + 2 + 4ull * nruns > len) return fail(PHIP_ERR_INVALID, "column %s: null vector run overflow", c.name);
+      for (int32_t r = 0; r < nruns; r++) {
+        const int64_t s0 = le16(bm + pos + 2 + 4 * r), l = le16(bm + pos + 4 + 4 * r);
+        for (int64_t d = base + s0; d <= base + s0 + l; d++)
+          if (!set(d)) return fail(PHIP_ERR_INVALID, "column %s: null doc beyond numDocs", c.name);
+      }
+      pos += 2 + 4ull * nruns;
+    } else if (ccard <= 4096) {
+      if (pos + 2ull * ccard > len) return fail(PHIP_ERR_INVALID, "column %s: null vector array overflow", c.name);
+      for (int32_t i = 0; i < ccard; i++)
+        if (!set(base + le16(bm + pos + 2 * i))) return fail(PHIP_ERR_INVALID, "column %s: null doc beyond numDocs", c.name);
+      pos += 2ull * ccard;
+    } else {
+      if (pos + 8192 > len) return fail(PHIP_ERR_INVALID, "column %s: null vector bitmap overflow", c.name);
+      for (int32_t w = 0; w < 1024; w++) {
+        uint64_t x = 0;
+        for (int b = 0; b < 8; b++) x |= (uint64_t)bm[pos + 8 * w + b] << (8 * b);
+        for (; x; x &= x - 1)
+          if (!set(base + 64 * w + __builtin_ctzll(x))) return fail(PHIP_ERR_INVALID, "column %s: null doc beyond numDocs", c.name);
+      }
+      pos += 8192;
+    }
+  }
+  if (count == 0) return PHIP_OK;  // (an empty bitmap: no null vector, as the creator never writes one)
+  void *p;
+  int32_t rc = dev_alloc(seg, (size_t)nwords * 8, &p);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(p, words.data(), (size_t)nwords * 8, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));  // (the host words go out of scope)
+  cs.nulls = (uint64_t *)p;
+  cs.null_count = count;
   return PHIP_OK;
 }
 
@@ -851,6 +934,10 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
       cs.has_range = true;
     }
   }
+  if (c.null_vector != nullptr && c.null_vector_bytes > 0) {
+    int32_t rc = load_null_vector(c, cs, seg, st);
+    if (rc) return rc;
+  }
   seg.by_name[cs.name] = (int)seg.cols.size();
   seg.cols.push_back(std::move(cs));
   return PHIP_OK;
@@ -905,7 +992,7 @@ int validate_tree(const phip_filter_node *nodes, int begin, int end, int idx, in
   int after;
   switch (n.op) {
     case PHIP_NODE_LEAF:
-      if (n.leaf_kind < PHIP_LEAF_MATCH_ALL || n.leaf_kind > PHIP_LEAF_RAW_STRING_SET) {
+      if (n.leaf_kind < PHIP_LEAF_MATCH_ALL || n.leaf_kind > PHIP_LEAF_NULL) {
         err = "bad leaf kind";
         return -1;
       }
@@ -1301,7 +1388,9 @@ struct Plan {
   std::vector<std::shared_ptr<Device::Remap>> sel_dicts;
   std::vector<int32_t> sel_bits, sel_width;  // per select column's projected bytes (algorithmic bytes)
   float sel_filter_ms = 0.f;
-  bool total_events = true;  // record ev[0] / ev[3] (phip_result.device_ms); PHIP_TOTAL_EVENTS=0 skips them (A/B)
+  // record ev[0] / ev[3] around the whole sequence (phip_result.device_ms): off by default -- every timing marker is a
+  // barrier packet the command processor waits on (~4 us each, r04 host A/B); PHIP_TOTAL_EVENTS=1 records them
+  bool total_events = false;
   bool split_event = true;   // record ev[4] between a filter and a separate aggregation launch
   bool fold_final = false;   // the last kernel's last workgroup finalizes (no finalize_all launch)
   uint32_t *fin_counter = nullptr;  // its ticket counter (device)
@@ -2006,6 +2095,19 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             }
             rc = raw_string_leaf(fn, dn, blob, aux_fix, ni);
             break;
+          case PHIP_LEAF_NULL:
+            // the column's resident null doc words, read like an inverted leaf's words (one 256-byte region per tile)
+            if (cs->nulls == nullptr) {
+              dn.leaf_kind = fn.exclusive ? PHIP_LEAF_MATCH_ALL : PHIP_LEAF_MATCH_NONE;
+              dn.exclusive = 0;
+              break;
+            }
+            dn.leaf_kind = PHIP_LEAF_INVERTED;
+            dn.aux = cs->nulls;
+            dn.aux_stride = 32;
+            dn.count = 0;
+            dn.bits = 0;
+            break;
           case PHIP_LEAF_INVERTED:
             if (cs->inv_begin.empty()) { rc = fail(PHIP_ERR_INVALID, "column %s has no inverted index", cs->name.c_str()); break; }
             {
@@ -2273,6 +2375,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         DevCol &dc = ds.cols[dn.column];
         if (dc.lds_off < 0) dc.lds_off = add_region((const uint8_t *)dc.words, 256 * dc.bits);
         dn.lds_off = dc.lds_off;
+      } else if (dn.leaf_kind == PHIP_LEAF_INVERTED && dn.aux != nullptr && node_inv_leaves[i] == 0) {
+        dn.lds_off = add_region((const uint8_t *)dn.aux, 256);  // a null vector: the column's own resident words
       } else if (dn.leaf_kind == PHIP_LEAF_INVERTED && dn.aux != nullptr) {
         // the entry's interleaved inverted words: one region of L x 256 bytes per tile, leaf j at 256 j
         if (inv_region == -2) {

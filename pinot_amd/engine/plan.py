@@ -23,7 +23,7 @@ import numpy as np
 
 from .. import _lib
 from ..query import predicate as predeval
-from ..query.context import (UNBOUNDED, AggregationInfo, FilterContext, Function, Identifier, Literal,
+from ..query.context import (UNBOUNDED, AggregationInfo, FilterContext, Function, Identifier, Literal, Predicate,
                              QueryContext, columns_of)
 from ..query.sql import parse
 from ..spi import (DEFAULT_GROUPBY_TRIM_THRESHOLD, DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE,
@@ -168,8 +168,19 @@ def _raw_predicate(column, dt: DataType, pred):
 INVERTED_COST_RATIO = 0.5  # decode bytes allowed per forward-index byte (measured: tools/configs_bench.py C4)
 
 
+def _null_leaf(seg: GpuSegment, column: str, exclusive: bool = False):
+    """IS NULL (exclusive: IS NOT NULL) over the column's null value vector: BitmapBasedFilterOperator on
+    NullValueVectorReader.getNullBitmap(), or EmptyFilterOperator / MatchAllFilterOperator for a column without one
+    (FilterPlanNode.java:294-307)."""
+    if seg.has_null_vector(column):
+        return _Leaf(_lib.LEAF_NULL, column, exclusive=exclusive)
+    return _TRUE if exclusive else _FALSE
+
+
 def compile_predicate(seg: GpuSegment, pred) -> object:
     column = pred.column
+    if pred.type in ("IS_NULL", "IS_NOT_NULL"):
+        return _null_leaf(seg, column, pred.type == "IS_NOT_NULL")
     m = seg.column_metadata(column)
     if not m.has_dictionary:
         return _raw_predicate(column, m.data_type, pred)
@@ -201,10 +212,82 @@ def compile_predicate(seg: GpuSegment, pred) -> object:
     return _Leaf(_lib.LEAF_DICT_SET, column, exclusive=ev.exclusive, ids=np.asarray(ev.ids, dtype=np.int32))
 
 
-def compile_filter(seg: GpuSegment, fc: Optional[FilterContext]):
-    """FilterContext -> leaf/node tree for one segment, constants folded (FilterPlanNode.java:197-229)."""
+def _fold_and(kids):
+    if any(_is_const(k, _FALSE) for k in kids):
+        return _FALSE
+    kids = [k for k in kids if not _is_const(k, _TRUE)]
+    if not kids:
+        return _TRUE
+    return kids[0] if len(kids) == 1 else _Node(_lib.NODE_AND, kids)
+
+
+def _fold_or(kids):
+    if any(_is_const(k, _TRUE) for k in kids):
+        return _TRUE
+    kids = [k for k in kids if not _is_const(k, _FALSE)]
+    if not kids:
+        return _FALSE
+    return kids[0] if len(kids) == 1 else _Node(_lib.NODE_OR, kids)
+
+
+def _fold_not(k):
+    if _is_const(k, _TRUE):
+        return _FALSE
+    if _is_const(k, _FALSE):
+        return _TRUE
+    if isinstance(k, _Leaf) and k.kind in (_lib.LEAF_DICT_SET, _lib.LEAF_INVERTED, _lib.LEAF_RAW_SET, _lib.LEAF_NULL):
+        return _Leaf(k.kind, k.column, k.lo, k.hi, not k.exclusive, k.ids)
+    return _Node(_lib.NODE_NOT, [k])
+
+
+def _three_valued(seg: GpuSegment, fc: FilterContext):
+    """(trues, falses, nulls) trees of a filter under enableNullHandling (nulls None = EmptyDocIdSet):
+      column leaf      BaseColumnFilterOperator: trues = p AND NOT null(c), nulls = null(c), falses = NOT(trues OR
+                       nulls) = NOT p AND NOT null(c) (BaseColumnFilterOperator.java:45-80, BaseFilterOperator.java:
+                       104-122); an always-true predicate is BitmapBasedFilterOperator(null bitmap, exclusive), an
+                       always-false one EmptyFilterOperator (FilterOperatorUtils.java:75-88): no nulls of their own
+      IS [NOT] NULL    BitmapBasedFilterOperator: no nulls
+      AND / OR         trues = AND / OR of the trues; falses = NOT(AND / OR of (trues_i OR nulls_i)); no nulls
+                       (AndFilterOperator.java:60-86, OrFilterOperator.java:59-85)
+      NOT              trues = the child's falses, falses = its trues (NotFilterOperator.java:52-60)"""
+    if fc.type == "CONSTANT":
+        t = _TRUE if fc.constant else _FALSE
+        return t, _fold_not(t), None
+    if fc.type == "PREDICATE":
+        pred = fc.predicate
+        p = compile_predicate(seg, pred)
+        if pred.type in ("IS_NULL", "IS_NOT_NULL") or not seg.has_null_vector(pred.column):
+            return p, _fold_not(p), None
+        n, nn = _null_leaf(seg, pred.column), _null_leaf(seg, pred.column, True)
+        if _is_const(p, _FALSE):
+            return _FALSE, _TRUE, None
+        if _is_const(p, _TRUE):
+            return nn, n, None
+        return _fold_and([p, nn]), _fold_and([_fold_not(p), nn]), n
+    if fc.type == "NOT":
+        t, f, _ = _three_valued(seg, fc.children[0])
+        return f, t, None
+    parts = [_three_valued(seg, c) for c in fc.children]
+    either = [t if nl is None else _fold_or([t, nl]) for t, _, nl in parts]
+    if fc.type == "AND":
+        return _fold_and([t for t, _, _ in parts]), _fold_not(_fold_and(either)), None
+    if fc.type == "OR":
+        return _fold_or([t for t, _, _ in parts]), _fold_not(_fold_or(either)), None
+    raise ValueError(fc.type)
+
+
+def null_handling_enabled(query: QueryContext) -> bool:
+    """QueryContext.isNullHandlingEnabled (the enableNullHandling query option, QueryContext.java:597)."""
+    return str(query.options.get("enableNullHandling", "false")).strip().lower() == "true"
+
+
+def compile_filter(seg: GpuSegment, fc: Optional[FilterContext], null_handling: bool = False):
+    """FilterContext -> leaf/node tree for one segment, constants folded (FilterPlanNode.java:197-229).
+    null_handling: the docs where the filter is TRUE under three-valued logic (_three_valued)."""
     if fc is None:
         return _TRUE
+    if null_handling:
+        return _three_valued(seg, fc)[0]
     if fc.type == "PREDICATE":
         return compile_predicate(seg, fc.predicate)
     if fc.type == "CONSTANT":
@@ -215,7 +298,7 @@ def compile_filter(seg: GpuSegment, fc: Optional[FilterContext]):
             return _FALSE
         if _is_const(c, _FALSE):
             return _TRUE
-        if isinstance(c, _Leaf) and c.kind in (_lib.LEAF_DICT_SET, _lib.LEAF_INVERTED, _lib.LEAF_RAW_SET):
+        if isinstance(c, _Leaf) and c.kind in (_lib.LEAF_DICT_SET, _lib.LEAF_INVERTED, _lib.LEAF_RAW_SET, _lib.LEAF_NULL):
             return _Leaf(c.kind, c.column, c.lo, c.hi, not c.exclusive, c.ids)
         return _Node(_lib.NODE_NOT, [c])
     kids = [compile_filter(seg, c) for c in fc.children]
@@ -390,15 +473,16 @@ class GpuCombineOperator:
         self.num_programs = len(programs[0]) if programs is not None else 1
         self.stats_programs = 0  # phip_query_desc.stats_programs: 0 = every program's scans count
         self.prims, self.mapping = plan_aggregations(query.aggregations, programs[1] if programs is not None else None)
+        nh = null_handling_enabled(query)
         if programs is not None:
             # program-major, as filter_offsets lays them out: program p of segment s at p * nseg + s
-            self.trees = [compile_filter(s, f) for f in programs[0] for s in self.segments]
+            self.trees = [compile_filter(s, f, nh) for f in programs[0] for s in self.segments]
         elif segment_filters is None:
-            self.trees = [compile_filter(s, query.filter) for s in self.segments]
+            self.trees = [compile_filter(s, query.filter, nh) for s in self.segments]
         else:
             self.trees = []
             for s, (flt, ranges) in zip(self.segments, segment_filters):
-                t = compile_filter(s, flt)
+                t = compile_filter(s, flt, nh)
                 if ranges is not None:
                     if len(ranges) == 0 or _is_const(t, _FALSE):
                         t = _FALSE
@@ -574,9 +658,13 @@ class GpuCombineOperator:
     def _non_scan_fit(self):
         if self.query.group_by or not all(_is_const(t, _TRUE) for t in self.trees):
             return False
+        nh = null_handling_enabled(self.query)
         for ag in self.query.aggregations:
             if ag.function not in self._NON_SCAN:
                 return False
+            if nh and ag.argument is not None and (not isinstance(ag.argument, Identifier) or any(
+                    s.has_null_vector(ag.argument.name) for s in self.segments)):
+                return False  # (AggregationPlanNode.hasNullValues, :104,125-150)
             if ag.function == "count":
                 continue
             if not isinstance(ag.argument, Identifier):
@@ -1489,6 +1577,144 @@ def use_gpu_option(query: QueryContext, default: bool) -> bool:
     return str(v).strip().lower() == "true"
 
 
+def _query_columns(query: QueryContext):
+    cols = set()
+    if query.filter is not None:
+        cols.update(query.filter.columns())
+    for ag in query.aggregations:
+        if ag.argument is not None:
+            cols.update(columns_of(ag.argument))
+        if ag.filter is not None:
+            cols.update(ag.filter.columns())
+    for e in query.group_by:
+        cols.update(columns_of(e))
+    for e, _ in query.select:
+        cols.update(c for c in columns_of(e) if c != "*")
+    return cols
+
+
+def _has_nulls(query: QueryContext, segments) -> bool:
+    """enableNullHandling with a null value vector on any column the query reads in any segment: the star-tree
+    then stays unused, as StarTreeUtils.isFitForStarTree decides per segment (StarTreeUtils.java:380-400)."""
+    if not null_handling_enabled(query):
+        return False
+    cols = _query_columns(query)
+    return any(s.has_null_vector(c) for s in segments for c in cols if s.has_column(c))
+
+
+_NULLABLE = ("sum", "min", "max", "avg", "minmaxrange", "count")  # NullableSingleInputAggregationFunction subclasses
+
+
+def _null_handling_operator(query: QueryContext, segments, limit):
+    """enableNullHandling (QueryContext.isNullHandlingEnabled). The filter side needs nothing here: every
+    GpuCombineOperator compiles its programs three-valued (_three_valued). This picks the aggregation side:
+      * aggregation only -> GpuNullHandlingAggregationOperator;
+      * group-by: the GPU operators when no group-by column and no nullable function's column has a null vector in
+        any segment (every group then holds docs with non-null values: the results are the plain ones); else the
+        null group keys (DefaultGroupByExecutor's no-dictionary generators) and per-group null results are not
+        on the GPU path: UnsupportedOnGpu. FILTER clauses and CASE with GROUP BY likewise;
+      * selection: the selected columns must be null-free (the reference returns nulls for null values);
+    None = the regular operators apply."""
+    def null_cols(exprs):
+        cols = set()
+        for e in exprs:
+            cols.update(c for c in columns_of(e) if c != "*")
+        return {c for c in cols if any(s.has_column(c) and s.has_null_vector(c) for s in segments)}
+
+    if any(ag.argument is not None and _is_case(ag.argument) for ag in query.aggregations):
+        raise UnsupportedOnGpu("enableNullHandling with CASE aggregations")
+    if query.is_selection:
+        if null_cols([e for e, _ in query.select]):
+            raise UnsupportedOnGpu("enableNullHandling: selected columns with null values")
+        return None
+    nullable_args = [ag.argument for ag in query.aggregations if ag.function in _NULLABLE and ag.argument is not None]
+    if query.group_by:
+        if any(ag.filter is not None for ag in query.aggregations):
+            raise UnsupportedOnGpu("enableNullHandling with FILTER clauses and GROUP BY")
+        if null_cols(list(query.group_by)) or null_cols(nullable_args):
+            raise UnsupportedOnGpu("enableNullHandling: group-by / aggregated columns with null values")
+        return None
+    return GpuNullHandlingAggregationOperator(query, segments, limit, null_cols(nullable_args))
+
+
+class GpuNullHandlingAggregationOperator:
+    """Aggregation-only query under enableNullHandling (AggregationOperator / FilteredAggregationOperator with
+    NullableSingleInputAggregationFunction: SUM / MIN / MAX / AVG / MINMAXRANGE skip the null values of their
+    argument -- of every column it reads, BaseTransformFunction's OR of the arguments' null bitmaps -- and their
+    result is null when no non-null value was aggregated (SumAggregationFunction.java:55-160, AvgAggregationFunction
+    .java:170-186); COUNT(col) counts the non-null values (CountAggregationFunction.java:44-160); COUNT(*) and
+    DISTINCTCOUNTHLL (not nullable) are unchanged).
+
+    On the GPU every nullable function over columns with null vectors becomes a filtered aggregation over
+    ``its filter AND col IS NOT NULL ...`` plus a hidden COUNT(*) of the same program, and every original info gets a
+    hidden COUNT(*) of its docs: one plan of filter programs (GpuFilteredAggregationOperator). A result whose count is
+    0 is None. The statistics are the reference's: numDocsScanned and post-filter entries from the original infos'
+    counts (each info projects its functions' input columns), filter scans of the original infos' programs only."""
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int, null_cols):
+        self.query = query
+        keys = []
+        for ag in query.aggregations:
+            if ag.filter not in keys:
+                keys.append(ag.filter)
+        aggs = []
+        counts = {}
+
+        def count_for(flt):
+            if flt not in counts:
+                counts[flt] = len(aggs)
+                aggs.append(AggregationInfo("count", None, 8, flt))
+            return counts[flt]
+
+        self.info_count = {k: count_for(k) for k in keys}
+        self.slots = []  # per original aggregation: (its value's index, the index of its non-null count or None)
+        for ag in query.aggregations:
+            if ag.function not in _NULLABLE or ag.argument is None:
+                self.slots.append((len(aggs), None))
+                aggs.append(ag)
+                continue
+            cols = [c for c in columns_of(ag.argument) if c in null_cols]
+            flt = ag.filter
+            if cols:
+                nn = [FilterContext.PRED(Predicate("IS_NOT_NULL", Identifier(c))) for c in cols]
+                parts = ([flt] if flt is not None else []) + nn
+                flt = parts[0] if len(parts) == 1 else FilterContext.AND(*parts)
+            if ag.function == "count":
+                self.slots.append((count_for(flt), None))
+                continue
+            self.slots.append((len(aggs), count_for(flt)))
+            aggs.append(AggregationInfo(ag.function, ag.argument, ag.log2m, flt))
+        sub = QueryContext(query.table, [], aggs, query.filter, [], limit=query.limit, options=dict(query.options))
+        if any(a.filter is not None for a in aggs):
+            self.op = GpuFilteredAggregationOperator(sub, segments, num_groups_limit, stats_filters=set(keys))
+        else:
+            self.op = GpuCombineOperator(sub, segments, num_groups_limit)
+        self.proj = {}
+        for ag in query.aggregations:
+            cols = self.proj.setdefault(ag.filter, set())
+            if ag.argument is not None:
+                cols.update(columns_of(ag.argument))
+
+    def next_block(self):
+        blk = self.op.next_block()
+        res = blk.results
+        out = []
+        for vi, ci in self.slots:
+            out.append(None if ci is not None and res[ci] == 0 else res[vi])
+        stats = dataclasses.replace(blk.stats)
+        if not (isinstance(self.op, GpuCombineOperator) and self.op._non_scan_fit()):
+            stats.num_docs_scanned = sum(int(res[i]) for i in self.info_count.values())
+            stats.num_entries_scanned_post_filter = sum(int(res[i]) * len(self.proj[k])
+                                                        for k, i in self.info_count.items())
+        o = AggregationResultsBlock(self.query.aggregations, out, stats)
+        for k in GpuFilteredAggregationOperator._TIMES:
+            setattr(o, k, getattr(blk, k, 0))
+        return o
+
+    def close(self):
+        self.op.close()
+
+
 class GpuInstancePlanMaker:
     """``pinot.server.query.executor.plan.maker.class`` plug-in (INTEGRATION.md §3 is the Java
     twin, a subclass of InstancePlanMakerImplV2).
@@ -1526,11 +1752,10 @@ class GpuInstancePlanMaker:
         minServerGroupTrimSize and groupTrimThreshold from the query options, else the server's values, written into
         a copy of the query's options (the reference's QueryContext setters). A malformed option raises
         QueryOptionError (the reference's BadQueryRequest). Options whose semantics the GPU operators do not have
-        raise UnsupportedOnGpu: enableNullHandling (null value vectors, QueryContext.java:597) and the
-        server-returns-final-result modes (their blocks carry final, not intermediate, results)."""
+        raise UnsupportedOnGpu: the server-returns-final-result modes (their blocks carry final, not intermediate,
+        results). enableNullHandling is _make_operator's (GpuNullHandlingAggregationOperator)."""
         o = query.options
-        if _bool_option(o, "enableNullHandling"):
-            raise UnsupportedOnGpu("enableNullHandling: null handling is not on the GPU path")
+        _bool_option(o, "enableNullHandling")  # (validated: the operators read it, null_handling_enabled)
         for k in ("serverReturnFinalResult", "serverReturnFinalResultKeyUnpartitioned"):
             if _bool_option(o, k):
                 raise UnsupportedOnGpu(f"{k}: the GPU operators return intermediate results")
@@ -1575,7 +1800,11 @@ class GpuInstancePlanMaker:
         from .startree import GpuStarTreeOperator
         limit = int(query.options["numGroupsLimit"]) if "numGroupsLimit" in query.options and query.group_by \
             else self.num_groups_limit
-        st = GpuStarTreeOperator.plan(query, segments, limit)
+        if null_handling_enabled(query):
+            op = _null_handling_operator(query, segments, limit)
+            if op is not None:
+                return op
+        st = GpuStarTreeOperator.plan(query, segments, limit) if not _has_nulls(query, segments) else None
         if st is not None:
             st.inner.device_trim = self.device_trim
             return st

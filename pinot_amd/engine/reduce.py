@@ -44,7 +44,9 @@ def hll_cardinality(regs: np.ndarray) -> int:
 
 
 def final_result(function: str, v):
-    """AggregationFunction.extractFinalResult."""
+    """AggregationFunction.extractFinalResult (a null intermediate stays null)."""
+    if v is None:
+        return None
     if function == "count":
         return int(v)
     if function == "sum":
@@ -73,17 +75,24 @@ def _agg_index(query: QueryContext, expr):
     flt = None
     if isinstance(expr, FilterClause):
         expr, flt = expr.function, expr.filter
+    if not isinstance(expr, Function):
+        return None
+    for i, a in enumerate(query.aggregations):  # exact argument first (COUNT(col) under enableNullHandling)
+        if expr.name == a.function and a.filter == flt and expr.args and expr.args[0] == a.argument:
+            return i
     for i, a in enumerate(query.aggregations):
-        if isinstance(expr, Function) and expr.name == a.function and a.filter == flt:
-            if a.function == "count" or (expr.args and expr.args[0] == a.argument):
-                return i
+        if expr.name == a.function == "count" and a.filter == flt and a.argument is None:
+            return i
     return None
 
 
-def _column_name(expr, alias):
+def _column_name(expr, alias, query=None):
     if alias:
         return alias
     if isinstance(expr, Function) and expr.name == "count":
+        i = _agg_index(query, expr) if query is not None else None
+        if i is not None and query.aggregations[i].argument is not None:
+            return f"count({query.aggregations[i].argument})"  # (enableNullHandling: CountAggregationFunction.java:64-66)
         return "count(*)"
     return str(expr)
 
@@ -94,7 +103,7 @@ def reduce_blocks(query: QueryContext, blocks) -> ResultTable:
         stats.merge(b.stats)
     if query.is_selection:
         return _reduce_selection(query, blocks, stats)
-    names = [_column_name(e, a) for e, a in query.select]
+    names = [_column_name(e, a, query) for e, a in query.select]
     if not query.group_by:
         merged = None
         for b in blocks:
@@ -154,7 +163,7 @@ def _reduce_selection(query: QueryContext, blocks, stats) -> ResultTable:
     if star:
         names, picks = list(schema.column_names), list(range(len(schema.column_names)))
     else:
-        names = [_column_name(e, a) for e, a in query.select]
+        names = [_column_name(e, a, query) for e, a in query.select]
         picks = [index[str(e)] for e, _ in query.select]
     rows = []
     for b in blocks:

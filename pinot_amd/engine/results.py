@@ -78,7 +78,13 @@ class SelectionResultsBlock:
 
 
 def merge_intermediate(function: str, a, b):
-    """AggregationFunction.merge for the functions on the path."""
+    """AggregationFunction.merge for the functions on the path. None is a null intermediate result (enableNullHandling:
+    no non-null value aggregated); merging it keeps the other side (SumAggregationFunction.merge under null handling,
+    :240-250, and the other nullable functions alike)."""
+    if a is None:
+        return b
+    if b is None:
+        return a
     if function == "count":
         return a + b
     if function == "sum":

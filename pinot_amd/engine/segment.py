@@ -44,7 +44,8 @@ class GpuSegment:
             d.cardinality = m.cardinality
             d.bits_per_value = m.hll_log2m if getattr(m, "hll_log2m", 0) else m.bits_per_element
             d.string_width = m.string_width
-            for attr, buf in (("forward", ci.forward), ("dictionary", ci.dictionary), ("inverted", ci.inverted)):
+            for attr, buf in (("forward", ci.forward), ("dictionary", ci.dictionary), ("inverted", ci.inverted),
+                              ("null_vector", getattr(ci, "null_vector", None))):
                 if buf is None:
                     setattr(d, attr, None)
                     setattr(d, attr + "_bytes", 0)
@@ -72,6 +73,12 @@ class GpuSegment:
     # ---- host-side readers (DataSource equivalents) -----------------------------------------
     def column_metadata(self, column):
         return self.segment.columns[column].metadata
+
+    def has_null_vector(self, column) -> bool:
+        """The column has a null value vector, i.e. some doc is null (NullValueVectorCreator writes none otherwise;
+        DataSource.getNullValueVector() != null)."""
+        ci = self.segment.columns.get(column)
+        return ci is not None and bool(getattr(ci, "null_vector", None))
 
     def has_column(self, column):
         return column in self.segment.columns

@@ -76,6 +76,8 @@ class PredicateType:
     IN = "IN"
     NOT_IN = "NOT_IN"
     RANGE = "RANGE"
+    IS_NULL = "IS_NULL"          # the column's null value vector (FilterPlanNode.java:294-307)
+    IS_NOT_NULL = "IS_NOT_NULL"
 
 
 UNBOUNDED = "*"  # RangePredicate.UNBOUNDED
@@ -146,8 +148,12 @@ class AggregationInfo:
 
     @property
     def result_column_name(self) -> str:
-        """AggregationFunction.getResultColumnName(): lower-case function name + argument."""
-        base = "count(*)" if self.function == "count" else f"{self.function}({self.argument})"
+        """AggregationFunction.getResultColumnName(): lower-case function name + argument; COUNT(col) keeps its
+        argument only under enableNullHandling (the argument is then set: CountAggregationFunction.java:44-66)."""
+        if self.function == "count":
+            base = "count(*)" if self.argument is None else f"count({self.argument})"
+        else:
+            base = f"{self.function}({self.argument})"
         return base if self.filter is None else f"{base} FILTER(WHERE {self.filter})"
 
     def unfiltered(self) -> "AggregationInfo":

@@ -4,7 +4,7 @@ The reference compiles SQL with Calcite (CalciteSqlParser, pinot-common/.../sql/
 PinotQuery, then QueryContextConverterUtils builds a QueryContext. This is a recursive-descent
 parser for the subset the parity tests and SSB use: SELECT <aggregations / group columns>
 FROM t [WHERE <boolean expr>] [GROUP BY ...] [ORDER BY ...] [LIMIT n], with predicates
-=, <>, !=, <, <=, >, >=, [NOT] BETWEEN, [NOT] IN and NOT/AND/OR, and +, -, *, / and CAST in
+=, <>, !=, <, <=, >, >=, [NOT] BETWEEN, [NOT] IN, IS [NOT] NULL and NOT/AND/OR, and +, -, *, / and CAST in
 expressions. The reference optimizer's flattening of nested AND/OR
 (pinot-core/.../query/optimizer/filter/FlattenAndOrFilterOptimizer.java) is applied.
 """
@@ -21,7 +21,7 @@ _TOKEN = re.compile(r"""\s*(?:
 )""", re.VERBOSE)
 
 _KEYWORDS = {"select", "from", "where", "group", "by", "order", "limit", "and", "or", "not", "between",
-             "in", "asc", "desc", "as", "cast", "option", "case", "when", "then", "else", "end"}
+             "in", "asc", "desc", "as", "cast", "option", "case", "when", "then", "else", "end", "is", "null"}
 
 
 class SqlError(ValueError):
@@ -217,7 +217,7 @@ class _Parser:
                 depth -= 1
                 if depth == 0:
                     return False
-            elif depth == 1 and k == "kw" and v in ("and", "or", "not", "between", "in"):
+            elif depth == 1 and k == "kw" and v in ("and", "or", "not", "between", "in", "is"):
                 return True
             elif depth == 1 and k == "op" and v in ("=", "<>", "!=", "<", "<=", ">", ">="):
                 return True
@@ -231,6 +231,10 @@ class _Parser:
 
     def predicate(self):
         lhs = self.expr()
+        if self.accept("kw", "is"):  # IS [NOT] NULL (Predicate.Type.IS_NULL / IS_NOT_NULL)
+            neg = bool(self.accept("kw", "not"))
+            self.expect("kw", "null")
+            return FilterContext.PRED(Predicate(PredicateType.IS_NOT_NULL if neg else PredicateType.IS_NULL, lhs))
         neg = bool(self.accept("kw", "not"))
         if self.accept("kw", "between"):
             lo = self._lit()
@@ -325,15 +329,19 @@ class _Parser:
         return OrderByExpression(e, asc)
 
 
-def _collect_aggs(expr, out, flt=None):
+def _collect_aggs(expr, out, flt=None, null_handling=False):
     if isinstance(expr, FilterClause):
-        _collect_aggs(expr.function, out, expr.filter)
+        _collect_aggs(expr.function, out, expr.filter, null_handling)
         return
     if isinstance(expr, Function):
         if expr.name in SUPPORTED_AGGREGATIONS:
             arg = None
             if expr.name == "count":
-                arg = None
+                # COUNT(col) counts the non-null values under enableNullHandling (an identifier or a function
+                # argument; COUNT(*) and COUNT(literal) stay COUNT(*): CountAggregationFunction.java:44-52)
+                a0 = expr.args[0] if expr.args else None
+                if null_handling and a0 is not None and not isinstance(a0, Literal) and a0 != Identifier("*"):
+                    arg = a0
             else:
                 if len(expr.args) < 1:
                     raise SqlError(f"{expr.name} needs an argument")
@@ -346,7 +354,7 @@ def _collect_aggs(expr, out, flt=None):
                 out.append(info)
             return
         for a in expr.args:
-            _collect_aggs(a, out)
+            _collect_aggs(a, out, None, null_handling)
 
 
 _SET = re.compile(r"\s*SET\s+([A-Za-z_][A-Za-z0-9_.]*)\s*=\s*('(?:[^']|'')*'|[^;]*?)\s*;", re.IGNORECASE)
@@ -375,8 +383,9 @@ def parse(sql: str) -> QueryContext:
         sql = sql[m.end():]
     table, select, filt, group_by, order_by, limit = _Parser(sql).query()
     aggs = []
+    nh = str(options.get("enableNullHandling", "false")).strip().lower() == "true"
     for e, _ in select:
-        _collect_aggs(e, aggs)
+        _collect_aggs(e, aggs, None, nh)
     # ORDER BY may reference aggregations absent from the select list (InterSegmentGroupBy tests)
     alias_map = {a: e for e, a in select if a}
     resolved_order = []
@@ -384,7 +393,7 @@ def parse(sql: str) -> QueryContext:
         e = ob.expression
         if isinstance(e, Identifier) and e.name in alias_map:
             e = alias_map[e.name]
-        _collect_aggs(e, aggs)
+        _collect_aggs(e, aggs, None, nh)
         resolved_order.append(OrderByExpression(e, ob.ascending))
     for e, _ in select:
         if isinstance(e, FilterClause):

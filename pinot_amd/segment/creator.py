@@ -84,6 +84,11 @@ def inverted_index_bytes(ids: np.ndarray, card: int, run_optimize: bool = True, 
     return offsets.astype(">u4").tobytes() + b"".join(bitmaps)
 
 
+# FieldSpec's default null values of dimension fields (pinot-spi/.../data/FieldSpec.java:75-81)
+DEFAULT_NULL_VALUES = {DataType.INT: -2 ** 31, DataType.LONG: -2 ** 63, DataType.FLOAT: float("-inf"),
+                       DataType.DOUBLE: float("-inf"), DataType.STRING: "null"}
+
+
 @dataclass
 class ColumnMetadata:
     name: str
@@ -104,6 +109,7 @@ class ColumnIndexes:
     forward: bytes
     dictionary: Optional[bytes] = None
     inverted: Optional[bytes] = None
+    null_vector: Optional[bytes] = None  # portable Roaring bitmap of the null docs (NullValueVectorCreator), or None
 
 
 @dataclass
@@ -266,12 +272,26 @@ class SegmentCreator:
         self.star_tree_configs = list(star_tree_configs)
         self._cols = []
         self._ids = {}
+        self._nulls = {}
 
-    def add_column(self, name: str, data_type: DataType, values):
+    def add_column(self, name: str, data_type: DataType, values, nulls=None, null_value=None):
+        """nulls: optional bool mask of the docs whose value is null. Those docs store the field's default null value
+        (``null_value``, else FieldSpec's dimension default: Integer.MIN_VALUE, Long.MIN_VALUE, -inf, "null";
+        FieldSpec.java:75-81) in every index, and the column gets a null value vector (NullValueVectorCreator: the
+        Roaring bitmap of the null doc ids, written only when some doc is null, :83-92)."""
         if data_type == DataType.STRING:
-            arr = np.asarray(values, dtype=np.str_)
+            arr = np.asarray(values, dtype=object if nulls is not None else np.str_)
         else:
-            arr = np.asarray(values, dtype=data_type.numpy)
+            arr = np.asarray(values, dtype=object if nulls is not None else data_type.numpy)
+        if nulls is not None:
+            mask = np.asarray(nulls, dtype=bool)
+            if len(mask) != len(arr):
+                raise ValueError(f"column {name}: {len(mask)} null flags for {len(arr)} values")
+            fill = null_value if null_value is not None else DEFAULT_NULL_VALUES[data_type]
+            arr = np.where(mask, fill, arr)
+            arr = np.asarray(arr, dtype=np.str_ if data_type == DataType.STRING else data_type.numpy)
+            if mask.any():
+                self._nulls[name] = np.nonzero(mask)[0]
         self._cols.append((name, data_type, arr))
         return self
 
@@ -284,6 +304,8 @@ class SegmentCreator:
             if len(vals) != n:
                 raise ValueError(f"column {name}: {len(vals)} values, expected {n}")
             seg.columns[name] = self._build_column(name, dt, vals, n)
+            if name in self._nulls:
+                seg.columns[name].null_vector = roaring.serialize(self._nulls[name], self.run_optimize)
         if self.star_tree_configs:
             from .startree import build_star_tree
             raw = {name: vals for name, _, vals in self._cols}

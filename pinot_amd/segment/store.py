@@ -7,11 +7,12 @@ bytes, exactly as Pinot wrote them). Two directory layouts exist:
 * v1 / v2 (FilePerIndexDirectory, pinot-segment-local/.../segment/store/FilePerIndexDirectory.java:184-199):
   one file per index, named by V1Constants (pinot-segment-spi/.../V1Constants.java:34-45):
   ``<col>.dict``, ``<col>.sv.unsorted.fwd`` (fixed-bit dict ids), ``<col>.sv.sorted.fwd`` (doc ranges),
-  ``<col>.sv.raw.fwd`` (fixed-byte chunks), ``<col>.bitmap.inv`` (Roaring inverted index);
+  ``<col>.sv.raw.fwd`` (fixed-byte chunks), ``<col>.bitmap.inv`` (Roaring inverted index), ``<col>.bitmap.nullvalue``
+  (the null value vector: one Roaring bitmap, NullValueVectorCreator.java:83-92);
 * v3 (SingleFileIndexDirectory.java:72-73,165-185,225-310): ``v3/columns.psf`` holds every buffer,
   each preceded by the 8-byte magic 0xdeadbeefdeafbead; ``v3/index_map`` records
   ``<col>.<index>.startOffset`` / ``.size`` (size includes the magic) for the index ids
-  ``dictionary``, ``forward_index``, ``inverted_index``.
+  ``dictionary``, ``forward_index``, ``inverted_index``, ``nullvalue_vector``.
 
 Column metadata comes from ``metadata.properties`` (ColumnMetadataImpl.fromPropertiesConfiguration,
 pinot-segment-spi/.../index/metadata/ColumnMetadataImpl.java:200-260): cardinality, bitsPerElement,
@@ -28,7 +29,9 @@ from .creator import ColumnIndexes, ColumnMetadata, ImmutableSegment
 
 MAGIC_MARKER = 0xDEADBEEFDEAFBEAD
 _EXT = {"dictionary": ".dict", "sorted": ".sv.sorted.fwd", "unsorted": ".sv.unsorted.fwd", "raw": ".sv.raw.fwd",
-        "inverted": ".bitmap.inv"}
+        "inverted": ".bitmap.inv", "nullvalue": ".bitmap.nullvalue"}
+# v3 index ids (StandardIndexes.java: "dictionary", "forward_index", "inverted_index", "nullvalue_vector")
+_INDEX_ID = {"dictionary": "dictionary", "inverted": "inverted_index", "nullvalue": "nullvalue_vector"}
 _TYPES = {"INT": DataType.INT, "LONG": DataType.LONG, "FLOAT": DataType.FLOAT, "DOUBLE": DataType.DOUBLE,
           "STRING": DataType.STRING}
 
@@ -98,7 +101,7 @@ def read_segment_dir(path: str) -> ImmutableSegment:
             blob = f.read()
 
         def buf(col, kind):
-            index = {"dictionary": "dictionary", "inverted": "inverted_index"}.get(kind, "forward_index")
+            index = _INDEX_ID.get(kind, "forward_index")
             start = imap.get(f"{col}.{index}.startOffset")
             if start is None:
                 return None
@@ -127,7 +130,7 @@ def read_segment_dir(path: str) -> ImmutableSegment:
         if not has_dict:
             fwd = buf(col, "raw")
             meta = ColumnMetadata(col, dt, num_docs, 0, 0, False, False, False)
-            seg.columns[col] = ColumnIndexes(meta, fwd)
+            seg.columns[col] = ColumnIndexes(meta, fwd, null_vector=buf(col, "nullvalue"))
             continue
         dictionary = buf(col, "dictionary")
         fwd = buf(col, "sorted") if is_sorted else buf(col, "unsorted")
@@ -135,7 +138,7 @@ def read_segment_dir(path: str) -> ImmutableSegment:
             fwd = buf(col, "unsorted") if is_sorted else buf(col, "sorted")
         inv = buf(col, "inverted")
         meta = ColumnMetadata(col, dt, num_docs, card, bits, is_sorted, True, inv is not None, width)
-        seg.columns[col] = ColumnIndexes(meta, fwd, dictionary, inv)
+        seg.columns[col] = ColumnIndexes(meta, fwd, dictionary, inv, buf(col, "nullvalue"))
     return seg
 
 
@@ -161,9 +164,11 @@ def write_segment_dir(seg: ImmutableSegment, path: str, version: int = 3) -> str
             parts.append(("dictionary", ci.dictionary))
         if ci.inverted is not None:
             parts.append(("inverted", ci.inverted))
+        if ci.null_vector is not None:
+            parts.append(("nullvalue", ci.null_vector))
         for kind, data in parts:
             if version == 3:
-                index = {"dictionary": "dictionary", "inverted": "inverted_index"}.get(kind, "forward_index")
+                index = _INDEX_ID.get(kind, "forward_index")
                 imap.append(f"{col}.{index}.startOffset = {len(psf)}")
                 imap.append(f"{col}.{index}.size = {len(data) + 8}")
                 psf += struct.pack(">Q", MAGIC_MARKER) + data

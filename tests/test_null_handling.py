@@ -1,0 +1,211 @@
+"""Null value vectors and enableNullHandling, host side (no GPU): the SQL front end (IS [NOT] NULL, COUNT(col)), the
+segment writer / directory round trip of ``<column>.bitmap.nullvalue``, the oracle's three-valued filters and
+null-skipping aggregations against hand-derived answers and the reference's NullEnabledQueriesTest known answers, and
+the plan's three-valued filter trees (plan._three_valued) evaluated on the host against the oracle.
+
+The GPU parity of the same semantics is tests/test_gpu_null_handling.py."""
+import numpy as np
+import pytest
+
+from oracle import executor
+from pinot_amd import _lib
+from pinot_amd.engine import plan
+from pinot_amd.engine.reduce import reduce_blocks
+from pinot_amd.query.sql import parse
+from pinot_amd.segment import roaring
+from pinot_amd.segment.creator import DEFAULT_NULL_VALUES, SegmentCreator
+from pinot_amd.segment.dictionary import Dictionary
+from pinot_amd.segment.store import read_segment_dir, write_segment_dir
+from pinot_amd.spi import DataType
+
+
+def _seg(name="n0"):
+    """x: INT with nulls at docs 1, 3, 6; y: INT, no nulls; s: STRING with a null at doc 2; r: raw LONG with nulls."""
+    c = SegmentCreator(name, no_dictionary_columns=["r"])
+    c.add_column("x", DataType.INT, [5, 0, 7, 0, 5, 9, 0, 1], nulls=[0, 1, 0, 1, 0, 0, 1, 0])
+    c.add_column("y", DataType.INT, [1, 1, 2, 2, 3, 3, 1, 2])
+    c.add_column("s", DataType.STRING, ["a", "b", "", "a", "c", "b", "a", "c"], nulls=[0, 0, 1, 0, 0, 0, 0, 0])
+    c.add_column("r", DataType.LONG, [10, 20, 30, 40, 50, 60, 70, 80], nulls=[1, 0, 0, 0, 0, 0, 0, 1])
+    return c.build()
+
+
+# ----------------------------------------------------------------------------------------------- SQL
+def test_sql_is_null_and_count_column():
+    q = parse("SELECT COUNT(*) FROM t WHERE x IS NULL OR NOT (y IS NOT NULL)")
+    p0 = q.filter.children[0].predicate
+    assert (p0.type, p0.column) == ("IS_NULL", "x")
+    assert q.filter.children[1].type == "NOT" and q.filter.children[1].children[0].predicate.type == "IS_NOT_NULL"
+    # COUNT(col) keeps its argument only under enableNullHandling (CountAggregationFunction.java:44-66)
+    assert parse("SELECT COUNT(x) FROM t").aggregations[0].argument is None
+    q = parse("SET enableNullHandling = true; SELECT COUNT(x), COUNT(*), COUNT(1) FROM t")
+    assert [a.result_column_name for a in q.aggregations] == ["count(x)", "count(*)"]
+
+
+# ----------------------------------------------------------------------------------------------- segment
+def test_creator_stores_default_null_values_and_the_vector():
+    seg = _seg()
+    os_ = executor.OracleSegment(seg)
+    assert os_.nulls("x").tolist() == [False, True, False, True, False, False, True, False]
+    assert os_.values("x")[[1, 3, 6]].tolist() == [DEFAULT_NULL_VALUES[DataType.INT]] * 3  # FieldSpec defaults
+    assert os_.values("s")[2] == "null" and os_.values("r")[0] == -2 ** 63
+    assert seg.columns["y"].null_vector is None  # (NullValueVectorCreator writes no file without a null)
+    assert not os_.nulls("y").any()
+    assert seg.columns["x"].null_vector == roaring.serialize([1, 3, 6])
+
+
+@pytest.mark.parametrize("version", [1, 3])
+def test_segment_directory_round_trip_keeps_null_vectors(tmp_path, version):
+    seg = _seg()
+    back = read_segment_dir(write_segment_dir(seg, str(tmp_path / f"v{version}"), version=version))
+    for c in ("x", "s", "r", "y"):
+        assert back.columns[c].null_vector == seg.columns[c].null_vector
+
+
+# ----------------------------------------------------------------------------------------------- oracle
+def _mask(seg, where, nh=True):
+    return executor.eval_filter(executor.OracleSegment(seg), parse(f"SELECT COUNT(*) FROM t WHERE {where}").filter, nh)
+
+
+def _docs(m):
+    return np.nonzero(m)[0].tolist()
+
+
+def test_oracle_three_valued_filters_hand_derived():
+    seg = _seg()  # x = [5, N, 7, N, 5, 9, N, 1], y = [1, 1, 2, 2, 3, 3, 1, 2]
+    assert _docs(_mask(seg, "x = 5")) == [0, 4]
+    assert _docs(_mask(seg, "x <> 5")) == [2, 5, 7]                 # nulls are not "not 5"
+    assert _docs(_mask(seg, "NOT (x = 5)")) == [2, 5, 7]            # falses of the leaf: NOT x=5 AND NOT null
+    assert _docs(_mask(seg, "x = 5", nh=False)) == [0, 4]
+    assert _docs(_mask(seg, "NOT (x = 5)", nh=False)) == [1, 2, 3, 5, 6, 7]  # two-valued: nulls hold MIN_VALUE
+    assert _docs(_mask(seg, "x IS NULL")) == [1, 3, 6]
+    assert _docs(_mask(seg, "NOT (x IS NULL)")) == [0, 2, 4, 5, 7]
+    # AND falses = NOT(AND of (trues OR nulls)): NOT(x = 5 AND y = 1) -> docs with a definite false
+    assert _docs(_mask(seg, "NOT (x = 5 AND y = 1)")) == [2, 3, 4, 5, 7]
+    # OR falses = NOT(OR of (trues OR nulls)): NOT(x = 7 OR y = 3) -> docs where both are definitely false
+    assert _docs(_mask(seg, "NOT (x = 7 OR y = 3)")) == [0, 7]
+    # x >= 0 does not match the stored null value (Integer.MIN_VALUE): a scan leaf, falses = NOT p AND NOT null
+    assert _docs(_mask(seg, "x >= 0")) == [0, 2, 4, 5, 7]
+    assert _docs(_mask(seg, "NOT (x >= 0)")) == []
+    # an always-true predicate over a column with nulls is a bitmap operator: trues = not null, NOT gives the nulls
+    assert _docs(_mask(seg, "x <> 12345")) == [0, 2, 4, 5, 7]
+    assert _docs(_mask(seg, "NOT (x <> 12345)")) == [1, 3, 6]
+    # an always-false one is EmptyFilterOperator: NOT matches every doc, nulls included
+    assert _docs(_mask(seg, "NOT (x = 12345)")) == list(range(8))
+    # nested NOT: the inner AND has no nulls of its own (AndFilterOperator.getNulls is empty)
+    assert _docs(_mask(seg, "NOT (NOT (x = 5 AND y = 1))")) == [0]
+
+
+@pytest.mark.parametrize("dt,base", [(DataType.INT, 7), (DataType.LONG, -3), (DataType.FLOAT, 5.5),
+                                     (DataType.DOUBLE, -1.25)])
+def test_oracle_null_enabled_known_answers(dt, base):
+    """NullEnabledQueriesTest.testQueries (pinot-core/src/test/.../queries/NullEnabledQueriesTest.java:93-122,
+    473-495): 1000 records per segment, record i holds base + i when i is even and null otherwise; over 4 segment
+    copies COUNT(col) = 4 x 500, MIN = base, MAX = base + 998, AVG = the mean of the non-null values, SUM = 4 x their
+    sum."""
+    vals = np.array([base + i for i in range(1000)])
+    nulls = np.arange(1000) % 2 == 1
+    raws = []
+    for k in range(4):
+        c = SegmentCreator(f"ne{k}")
+        c.add_column("col", dt, vals, nulls=nulls)
+        raws.append(c.build())
+    q = parse("SET enableNullHandling = true; SELECT COUNT(col) AS count, MIN(col) AS min, MAX(col) AS max, "
+              "AVG(col) AS avg, SUM(col) AS sum FROM testTable LIMIT 1000")
+    blk, _ = executor.execute(q, raws)
+    row = reduce_blocks(q, [blk]).rows[0]
+    s = float(sum(base + i for i in range(0, 1000, 2)))
+    assert row[0] == 4 * 500
+    assert abs(row[1] - base) < 1e-1 and abs(row[2] - (base + 998)) < 1e-1
+    assert abs(row[3] - s / 500) < 1e-1 and abs(row[4] - 4 * s) < 1e-1
+
+
+def test_oracle_null_results_when_nothing_non_null_is_aggregated():
+    seg = _seg()
+    q = parse("SET enableNullHandling = true; SELECT SUM(x), MIN(x), COUNT(x), COUNT(*), AVG(r), MAX(x) "
+              "FILTER (WHERE y = 3) FROM t WHERE x IS NULL")
+    blk, _ = executor.execute(q, [seg, seg])
+    assert blk.results[0] is None and blk.results[1] is None and blk.results[5] is None
+    assert blk.results[2] == 0 and blk.results[3] == 6
+    assert blk.results[4] == (260.0, 6)  # r is null at docs 0 and 7 only: 20 + 40 + 70 per segment copy
+    assert reduce_blocks(q, [blk]).rows[0] == [None, None, 0, 6, 260.0 / 6, None]
+    # SUM(x * y): a doc is skipped when either column is null
+    q = parse("SET enableNullHandling = true; SELECT SUM(x * y), SUM(r) FROM t")
+    blk, ex = executor.execute(q, [seg])
+    assert ex[0] == 5 * 1 + 7 * 2 + 5 * 3 + 9 * 3 + 1 * 2 and ex[1] == 20 + 30 + 40 + 50 + 60 + 70
+
+
+# ----------------------------------------------------------------------------------------------- plan trees
+class _HostSeg:
+    """The GpuSegment surface compile_predicate reads, over an ImmutableSegment (no device)."""
+
+    def __init__(self, seg):
+        self.segment = seg
+        self.name = seg.name
+        self.num_docs = seg.num_docs
+
+    def column_metadata(self, c):
+        return self.segment.columns[c].metadata
+
+    def dictionary(self, c):
+        ci = self.segment.columns[c]
+        m = ci.metadata
+        return Dictionary(ci.dictionary, m.data_type, m.cardinality, m.string_width)
+
+    def has_null_vector(self, c):
+        return bool(self.segment.columns[c].null_vector)
+
+    def sorted_doc_range(self, c, d):
+        p = np.frombuffer(self.segment.columns[c].forward, dtype=">i4").reshape(-1, 2)
+        return int(p[d, 0]), int(p[d, 1])
+
+
+def _eval_tree(os_, t):
+    """Host evaluation of a compiled leaf/node tree (the library's leaf semantics)."""
+    n = os_.num_docs
+    if isinstance(t, plan._Node):
+        kids = [_eval_tree(os_, c) for c in t.children]
+        if t.op == _lib.NODE_NOT:
+            return ~kids[0]
+        out = kids[0].copy()
+        for k in kids[1:]:
+            out = (out & k) if t.op == _lib.NODE_AND else (out | k)
+        return out
+    if t.kind == _lib.LEAF_MATCH_ALL:
+        return np.ones(n, dtype=bool)
+    if t.kind == _lib.LEAF_MATCH_NONE:
+        return np.zeros(n, dtype=bool)
+    if t.kind == _lib.LEAF_NULL:
+        m = os_.nulls(t.column)
+    elif t.kind == _lib.LEAF_DICT_RANGE:
+        ids = os_.dict_ids(t.column)
+        m = (ids >= t.lo) & (ids < t.hi)
+    elif t.kind == _lib.LEAF_DICT_SET:
+        m = np.isin(os_.dict_ids(t.column), t.ids)
+    elif t.kind == _lib.LEAF_RAW_RANGE:  # (integral raw column: lo_int <= v <= hi_int)
+        rr = _lib.RawRange.from_buffer_copy(np.asarray(t.ids, dtype=np.int32).tobytes())
+        v = os_.values(t.column)
+        m = (v >= rr.lo_int) & (v <= rr.hi_int)
+    elif t.kind == _lib.LEAF_DOC_RANGES:
+        m = np.zeros(n, dtype=bool)
+        for a, b in np.asarray(t.ids).reshape(-1, 2):
+            m[a:b + 1] = True
+        return m
+    else:
+        raise AssertionError(f"leaf kind {t.kind} not expected here")
+    return ~m if t.exclusive else m
+
+
+WHERES = ["x = 5", "x <> 5", "NOT (x = 5)", "x IS NULL", "x IS NOT NULL", "NOT (x IS NOT NULL)", "x >= 0",
+          "NOT (x >= 0)", "NOT (x = 12345)", "NOT (x <> 12345)", "x <> 12345 AND y = 1", "NOT (r > 30)", "x IN (5, 9) AND y = 3", "NOT (x = 5 AND y = 1)", "NOT (x = 7 OR y = 3)",
+          "NOT (NOT (x = 5 AND y = 1))", "s = 'a' OR x > 6", "NOT (s = 'a' OR x > 6)", "s IS NULL OR x IS NULL",
+          "NOT (s IN ('a', 'b') AND NOT (x BETWEEN 1 AND 7))", "y = 2 AND NOT (x = 7)"]
+
+
+@pytest.mark.parametrize("nh", [True, False])
+@pytest.mark.parametrize("where", WHERES)
+def test_plan_three_valued_trees_match_the_oracle(where, nh):
+    seg = _seg()
+    fc = parse(f"SELECT COUNT(*) FROM t WHERE {where}").filter
+    tree = plan.compile_filter(_HostSeg(seg), fc, nh)
+    os_ = executor.OracleSegment(seg)
+    assert _docs(_eval_tree(os_, tree)) == _docs(executor.eval_filter(os_, fc, nh)), where

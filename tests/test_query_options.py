@@ -75,8 +75,7 @@ class _CpuMaker:
         return SimpleNamespace(next_block=lambda: "cpu-block", close=lambda: None)
 
 
-@pytest.mark.parametrize("opt", ["enableNullHandling = true", "enableNullHandling = 'TRUE'",
-                                 "serverReturnFinalResult = true", "serverReturnFinalResultKeyUnpartitioned = true"])
+@pytest.mark.parametrize("opt", ["serverReturnFinalResult = true", "serverReturnFinalResultKeyUnpartitioned = true"])
 def test_options_outside_the_gpu_semantics_fall_back(opt):
     sql = f"SET {opt}; SELECT a, COUNT(*) FROM t GROUP BY a"
     with pytest.raises(UnsupportedOnGpu):

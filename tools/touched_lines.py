@@ -49,8 +49,8 @@ def main():
     out = {"queries": queries, "sf": 100, "line_bytes": 64, "per_query": {}, "materialize_min": args.materialize_min,
            "method": "per segment: distinct 64-B lines of each projected column's fixed-bit words holding a matched "
                      "doc's id bits, + distinct 64-B dictionary lines of the matched ids (phip_filter_bitmap docs); "
-                     "a value-only column with a dictionary of >= materialize_min bytes: the lines of its doc-order "
-                     "values instead"}
+                     "a value-only column with a dictionary of >= materialize_min bytes: the fewer of those and the "
+                     "lines of its doc-order values"}
     for layout in args.layout or ["sorted"]:
         res = {q: {"id_line_bytes": 0, "dict_line_bytes": 0, "matched": 0} for q in queries}
         for i in range(0, args.segs, 10):
@@ -76,15 +76,7 @@ def main():
                                 res[q]["id_line_bytes"] += 8 * len(docs)
                                 continue
                             w = 4 if int(m.data_type) in (0, 2) else 8
-                            where = ssb.SSB_QUERIES[q].upper().split("WHERE", 1)[-1].split("GROUP BY")[0]
-                            if (args.materialize_min >= 0 and m.cardinality * w >= args.materialize_min
-                                    and c.upper() not in where):
-                                # a value-only column with a large dictionary: its doc-order values
-                                # (runtime.cpp ensure_vals), no dictionary gather
-                                res[q]["id_line_bytes"] += 64 * lines_of(docs, 8 * w)
-                                continue
                             b = m.bits_per_element
-                            res[q]["id_line_bytes"] += 64 * lines_of(docs, b)
                             ids = np.frombuffer(raw.columns[c].forward, dtype=np.uint8)
                             # the matched docs' dict ids (MSB-first fixed-bit stream)
                             bitpos = docs.astype(np.int64) * b
@@ -94,7 +86,19 @@ def main():
                                 pos = bitpos + k
                                 bit = (padded[pos >> 3] >> (7 - (pos & 7))) & 1
                                 vals = (vals << 1) | bit
-                            res[q]["dict_line_bytes"] += 64 * int(len(np.unique((vals * w) >> 6)))
+                            via_ids = 64 * lines_of(docs, b) + 64 * int(len(np.unique((vals * w) >> 6)))
+                            where = ssb.SSB_QUERIES[q].upper().split("WHERE", 1)[-1].split("GROUP BY")[0]
+                            if (args.materialize_min >= 0 and m.cardinality * w >= args.materialize_min
+                                    and c.upper() not in where):
+                                # a value-only column with a large dictionary also has doc-order values (runtime.cpp
+                                # ensure_vals): the floor is the cheaper of the two routes
+                                via_vals = 64 * lines_of(docs, 8 * w)
+                                res[q]["value_line_bytes"] = res[q].get("value_line_bytes", 0) + via_vals
+                                res[q]["ids_dict_line_bytes"] = res[q].get("ids_dict_line_bytes", 0) + via_ids
+                                res[q]["id_line_bytes"] += min(via_vals, via_ids)
+                                continue
+                            res[q]["id_line_bytes"] += 64 * lines_of(docs, b)
+                            res[q]["dict_line_bytes"] += via_ids - 64 * lines_of(docs, b)
                 g.destroy()
         for q in queries:
             res[q]["touched_bytes"] = res[q]["id_line_bytes"] + res[q]["dict_line_bytes"]
