@@ -1682,7 +1682,8 @@ class GpuNullHandlingAggregationOperator:
             if ag.function == "count":
                 self.slots.append((count_for(flt), None))
                 continue
-            self.slots.append((len(aggs), count_for(flt)))
+            ci = count_for(flt)
+            self.slots.append((len(aggs), ci))
             aggs.append(AggregationInfo(ag.function, ag.argument, ag.log2m, flt))
         sub = QueryContext(query.table, [], aggs, query.filter, [], limit=query.limit, options=dict(query.options))
         if any(a.filter is not None for a in aggs):

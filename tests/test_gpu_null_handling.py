@@ -125,7 +125,7 @@ def test_gpu_null_handling_selection_of_null_free_columns(null_segments):
     qc = parse(NH + "SELECT g, k FROM t WHERE NOT (d = 5 OR s = 'v2') LIMIT 200")
     blk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
     oblk, _ = executor.execute(qc, raws)
-    assert blk.rows() == oblk.rows()
+    assert blk.rows == oblk.rows
 
 
 @pytest.mark.parametrize("dt,base", [(DataType.INT, 7), (DataType.DOUBLE, -1.25)])
