@@ -141,6 +141,7 @@ __device__ __forceinline__ uint32_t hll_entry_raw(ccol_t &c, int32_t doc, int lo
 }
 // the entry of doc's value in column c: the per-dictionary-id table, or hashed from the raw value
 __device__ __forceinline__ uint32_t hll_entry(ccol_t &c, int32_t doc, int log2m) {
+  if (c.hll_doc != nullptr) return ((const PHIP_GLB uint32_t *)c.hll_doc)[doc];
   if (!c.has_dict) return hll_entry_raw(c, doc, log2m);
   return ((const PHIP_GLB uint32_t *)c.hll)[col_dict_id(c, doc)];
 }

@@ -16,6 +16,8 @@
 //              per-workgroup slab and reduced in a fixed order by slab_reduce_kernel (bitwise
 //              reproducible, no global atomics);
 //   GB_GLOBAL  one dense table in HBM updated with global atomics (large key spaces).
+#include <hip/hip_ext.h>
+
 #include "agg_common.h"
 
 namespace phip {
@@ -56,7 +58,10 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
     } else if (kind == ACC_HLL) {
       ccol_t &c = seg.cols[ag.col_a];
       uint32_t h[U];
-      if (!c.has_dict) {  // raw values, hashed per doc
+      if (c.hll_doc != nullptr) {  // doc-order entries
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
+      } else if (!c.has_dict) {  // raw values, hashed per doc
 #pragma unroll
         for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], q.log2m);
       } else {
@@ -320,10 +325,15 @@ __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const
         for (int u = 0; u < U; u++)
           if ((act >> u) & 1u)
             hll_row_each(c, d[u], [&](int r, uint32_t rho) { tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], r, rho); });
-      } else if (!c.has_dict) {  // raw values, hashed per doc
+      } else if (c.hll_doc != nullptr || !c.has_dict) {  // doc-order entries, or raw values hashed per doc
         uint32_t h[U];
+        if (c.hll_doc != nullptr) {
 #pragma unroll
-        for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], q.log2m);
+          for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], q.log2m);
+        }
 #pragma unroll
         for (int u = 0; u < U; u++)
           if ((act >> u) & 1u) tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], h[u] >> 8, h[u] & 0xffu);
@@ -1001,35 +1011,42 @@ static inline int grid_for(int64_t n, int per_block = 256, int cap = 4096) {
 }
 
 template <int NA, int MODE, bool D = false>
-static hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s) {
+static hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0 = nullptr,
+                               hipEvent_t e1 = nullptr) {
   if (lds > 65536) {
     // once per instantiation (a magic static: thread-safe under concurrent queries)
     static const hipError_t configured =
         hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
     if (configured != hipSuccess) return configured;
   }
+  if (e0 != nullptr) {  // timing carried by the dispatch packet itself (hipExtLaunchKernel)
+    void *args[] = {(void *)&q};
+    return hipExtLaunchKernel((const void *)agg_kernel<NA, MODE, D>, dim3(nblocks), dim3(kAggBlock), args, lds, s, e0,
+                              e1, 0);
+  }
   agg_kernel<NA, MODE, D><<<nblocks, kAggBlock, lds, s>>>(q);
   return hipGetLastError();
 }
 
 // q: host copy (for the variant choice); dq: the same descriptor in device memory.
-hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s) {
+hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0,
+                      hipEvent_t e1) {
   if (q.mode == GB_LDS)
-    return q.dense_batch ? launch_agg_t<1, GB_LDS, true>(dq, nblocks, lds, s) : launch_agg_t<1, GB_LDS>(dq, nblocks, lds, s);
+    return q.dense_batch ? launch_agg_t<1, GB_LDS, true>(dq, nblocks, lds, s, e0, e1) : launch_agg_t<1, GB_LDS>(dq, nblocks, lds, s, e0, e1);
   if (q.mode == GB_GLOBAL)
-    return q.dense_batch ? launch_agg_t<1, GB_GLOBAL, true>(dq, nblocks, lds, s)
-                         : launch_agg_t<1, GB_GLOBAL>(dq, nblocks, lds, s);
-  if (q.mode == GB_HASH) return launch_agg_t<1, GB_HASH>(dq, nblocks, lds, s);
+    return q.dense_batch ? launch_agg_t<1, GB_GLOBAL, true>(dq, nblocks, lds, s, e0, e1)
+                         : launch_agg_t<1, GB_GLOBAL>(dq, nblocks, lds, s, e0, e1);
+  if (q.mode == GB_HASH) return launch_agg_t<1, GB_HASH>(dq, nblocks, lds, s, e0, e1);
   if (q.dense_batch) {
-    if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE, true>(dq, nblocks, lds, s);
-    if (q.num_aggs <= 2) return launch_agg_t<2, GB_NONE, true>(dq, nblocks, lds, s);
-    if (q.num_aggs <= 4) return launch_agg_t<4, GB_NONE, true>(dq, nblocks, lds, s);
-    return launch_agg_t<8, GB_NONE, true>(dq, nblocks, lds, s);
+    if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE, true>(dq, nblocks, lds, s, e0, e1);
+    if (q.num_aggs <= 2) return launch_agg_t<2, GB_NONE, true>(dq, nblocks, lds, s, e0, e1);
+    if (q.num_aggs <= 4) return launch_agg_t<4, GB_NONE, true>(dq, nblocks, lds, s, e0, e1);
+    return launch_agg_t<8, GB_NONE, true>(dq, nblocks, lds, s, e0, e1);
   }
-  if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE>(dq, nblocks, lds, s);
-  if (q.num_aggs <= 2) return launch_agg_t<2, GB_NONE>(dq, nblocks, lds, s);
-  if (q.num_aggs <= 4) return launch_agg_t<4, GB_NONE>(dq, nblocks, lds, s);
-  return launch_agg_t<8, GB_NONE>(dq, nblocks, lds, s);
+  if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE>(dq, nblocks, lds, s, e0, e1);
+  if (q.num_aggs <= 2) return launch_agg_t<2, GB_NONE>(dq, nblocks, lds, s, e0, e1);
+  if (q.num_aggs <= 4) return launch_agg_t<4, GB_NONE>(dq, nblocks, lds, s, e0, e1);
+  return launch_agg_t<8, GB_NONE>(dq, nblocks, lds, s, e0, e1);
 }
 
 hipError_t launch_slab_reduce(const uint64_t *slab, int32_t nslabs, int32_t tbl_words, int64_t G, const int32_t *kinds,

@@ -88,6 +88,7 @@ struct DevCol {
   const uint32_t *planes;   // bit-sliced copy of `words` (bits <= kBitSliceMaxBits), or null: per 2048-doc tile,
                             // plane k (bit bits-1-k of the id) as 64 lane words, bit 31-g of lane l = doc 64g + l
   int64_t gb_base;          // raw INT / LONG group-by column: its key id = value - gb_base
+  const uint32_t *hll_doc;  // DISTINCTCOUNTHLL: doc-order copy of `hll` (entry of doc d = hll[id(d)]), or null
 };
 constexpr int kBitSliceMaxBits = 12;
 

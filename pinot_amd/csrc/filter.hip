@@ -16,6 +16,8 @@
 // materialisation; AND / OR / NOT (AndDocIdSet / OrDocIdSet / NotDocIdSet) are one VALU op per lane.
 // The tile's 64 lane words (256 B, one coalesced store) go to the aggregation kernel when the query
 // projects anything; COUNT-only queries stop here (FastFilteredCountOperator.java:66-78).
+#include <hip/hip_ext.h>
+
 #include "agg_common.h"
 
 namespace phip {
@@ -1574,12 +1576,18 @@ hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *group
 }
 
 template <bool C, int NA>
-static hipError_t launch_filter_t(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s) {
+static hipError_t launch_filter_t(const DevFilter &q, int nblocks, size_t lds_bytes, hipStream_t s, hipEvent_t e0,
+                                  hipEvent_t e1) {
   if (lds_bytes > 65536) {
     // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup); once, thread-safe (magic static)
     static const hipError_t configured = hipFuncSetAttribute((const void *)filter_kernel<C, NA>,
                                                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
     if (configured != hipSuccess) return configured;
+  }
+  if (e0 != nullptr) {  // timing carried by the dispatch packet itself (no barrier packets around it)
+    void *args[] = {(void *)&q};
+    return hipExtLaunchKernel((const void *)filter_kernel<C, NA>, dim3(nblocks), dim3(kFilterBlock), args, lds_bytes, s,
+                              e0, e1, 0);
   }
   filter_kernel<C, NA><<<nblocks, kFilterBlock, lds_bytes, s>>>(q);
   return hipGetLastError();
@@ -1588,13 +1596,14 @@ static hipError_t launch_filter_t(const DevFilter &q, int nblocks, size_t lds_by
 // conj_only: every segment's program takes the conjunctive fast path (the interpreter is compiled
 // out, which frees registers for more resident waves); fused_naggs > 0: the aggregation runs inside
 // (q.agg set, conj_only required)
+// (e0 / e1: optional start / stop events recorded by the kernel's own dispatch, hipExtLaunchKernel)
 hipError_t launch_filter(const DevFilter &q, bool conj_only, int fused_naggs, int nblocks, size_t lds_bytes,
-                         hipStream_t s) {
-  if (!conj_only) return launch_filter_t<false, 0>(q, nblocks, lds_bytes, s);
-  if (fused_naggs <= 0) return launch_filter_t<true, 0>(q, nblocks, lds_bytes, s);
-  if (fused_naggs <= 1) return launch_filter_t<true, 1>(q, nblocks, lds_bytes, s);
-  if (fused_naggs <= 2) return launch_filter_t<true, 2>(q, nblocks, lds_bytes, s);
-  return launch_filter_t<true, 4>(q, nblocks, lds_bytes, s);
+                         hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  if (!conj_only) return launch_filter_t<false, 0>(q, nblocks, lds_bytes, s, e0, e1);
+  if (fused_naggs <= 0) return launch_filter_t<true, 0>(q, nblocks, lds_bytes, s, e0, e1);
+  if (fused_naggs <= 1) return launch_filter_t<true, 1>(q, nblocks, lds_bytes, s, e0, e1);
+  if (fused_naggs <= 2) return launch_filter_t<true, 2>(q, nblocks, lds_bytes, s, e0, e1);
+  return launch_filter_t<true, 4>(q, nblocks, lds_bytes, s, e0, e1);
 }
 
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,

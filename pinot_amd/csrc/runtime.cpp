@@ -50,10 +50,11 @@ hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
 hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *groups, int32_t ngroups, hipStream_t s);
 hipError_t launch_filter(const DevFilter &q, bool conj_only, int fused_naggs, int nblocks, size_t lds_bytes,
-                         hipStream_t s);
+                         hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_masks_to_words(const uint32_t *masks, int32_t tile0, int32_t ntiles, uint64_t *words, int64_t nwords,
                                  hipStream_t s);
-hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s);
+hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hipStream_t s);
 hipError_t launch_slab_reduce(const uint64_t *slab, int32_t nslabs, int32_t tbl_words, int64_t G, const int32_t *kinds,
                               uint64_t *out, const uint32_t *hslab, int32_t hll_words, uint32_t *hout, hipStream_t s);
@@ -318,6 +319,7 @@ struct ColumnStore {
   std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
   std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
   std::map<int, uint32_t *> hll;      // per log2m
+  std::map<int, uint32_t *> hll_doc;  // per log2m: doc-order copy of hll (ensure_hll_doc), in the segment's allocations
   bool has_range = false;             // INT / LONG: value range (plan-time overflow bound of integer sums)
   int64_t vmin = 0, vmax = 0;
   // inverted index
@@ -1269,6 +1271,26 @@ static bool vals_eligible(const ColumnStore &c, int64_t min_dict) {
   if (no_dict(c) || c.words == nullptr || c.dict == nullptr || c.type == PHIP_TYPE_STRING) return false;
   return (int64_t)c.card * type_width(c.type) >= min_dict;
 }
+// Doc-order DISTINCTCOUNTHLL entries (entry of doc d = the per-dictionary-id table's entry of its id): made the first
+// time a plan aggregates the column with that log2m, when the table is too large to stay in L2 (>= 1 MiB, e.g. ~3M
+// LO_CUSTKEY ids per segment: a 12 MB table gathered at random once per matched doc).
+static int32_t ensure_hll_doc(Segment &sg, ColumnStore &c, int log2m, const uint32_t *table, hipStream_t st, bool *made,
+                              uint32_t **out) {
+  auto it = c.hll_doc.find(log2m);
+  if (it != c.hll_doc.end()) {
+    *out = it->second;
+    return PHIP_OK;
+  }
+  void *p;
+  int32_t rc = dev_alloc(sg, (size_t)std::max<int32_t>(sg.num_docs, 1) * 4, &p);
+  if (rc) return rc;
+  HIP_TRY(launch_materialize(c.words, c.bits, table, 4, sg.num_docs, p, st));
+  c.hll_doc[log2m] = (uint32_t *)p;
+  *out = (uint32_t *)p;
+  *made = true;
+  return PHIP_OK;
+}
+
 static int32_t ensure_vals(Segment &sg, ColumnStore &c, hipStream_t st, bool *made) {
   if (c.vals != nullptr) return PHIP_OK;
   const int w = type_width(c.type);
@@ -1889,6 +1911,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   int64_t total_docs = 0;
   std::vector<DevSeg> dsegs;  // (segment, program) entries with work only, segment-major
   dsegs.reserve((size_t)nseg * nprog);
+  bool hll_made = false;
+  std::vector<bool> hll_doc_used((size_t)nseg * ncols, false);  // (segment, column): HLL entries read by doc
+  const char *hde = getenv("PHIP_HLL_DOC");  // measurement override: "0" = gather the per-id table
+  const char *mze = getenv("PHIP_MATERIALIZE");
+  const bool hll_doc_on = !(hde && atoi(hde) == 0) && !(mze && atoi(mze) == 0) && !want_bitmap;
   for (int s = 0; s < nseg; s++) {
     Segment &sg = *segs[s];
     total_docs += sg.num_docs;
@@ -1925,6 +1952,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       int32_t rc = ensure_hll(cs, dq.aggs[a].log2m, &h);
       if (rc) return rc;
       ds.cols[dq.aggs[a].col_a].hll = h;
+      if (hll_doc_on && cs.words != nullptr && (int64_t)cs.card * 4 >= vals_min && vals_min >= 0) {
+        uint32_t *hd;
+        rc = ensure_hll_doc(sg, cs, dq.aggs[a].log2m, h, st, &hll_made, &hd);
+        if (rc) return rc;
+        ds.cols[dq.aggs[a].col_a].hll_doc = hd;
+        hll_doc_used[(size_t)s * ncols + dq.aggs[a].col_a] = true;
+      }
     }
     for (int k = 0; k < q->num_group_by; k++) {
       ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
@@ -2202,6 +2236,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     dsegs.push_back(ds);
    }
   }
+  if (hll_made) HIP_TRY(hipStreamSynchronize(st));
   if (total_work > INT32_MAX / 2) return fail(PHIP_ERR_UNSUPPORTED, "too many tiles in one query");
   dq.total_work = (int32_t)total_work;
   if (group_by && gb_key_space > ((int64_t)1 << 22)) {
@@ -2629,7 +2664,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     pc.progs = proj_progs[c];
     for (int s = 0; s < nseg; s++) {
       const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-      const bool raw = as_raw(s, c) && !ids_streamed[(size_t)s * ncols + c];
+      const bool raw = (as_raw(s, c) && !ids_streamed[(size_t)s * ncols + c]) || hll_doc_used[(size_t)s * ncols + c];
       pc.bits.push_back(raw ? 0 : cs.bits);
       pc.card.push_back(raw ? 0 : cs.card);
       pc.width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));  // STRING: remap / HLL entry
@@ -3090,16 +3125,22 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     }
     if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
-  HIP_TRY(hipEventRecord(P.ev[1], st));
   const bool fused = P.fused_naggs > 0;
+  // A plan of one kernel (fused, or a filter or an aggregation alone) has its timing events recorded by the kernel's
+  // own dispatch packet (hipExtLaunchKernel): every separate marker is a barrier packet the command processor waits
+  // on, a few microseconds of a 20-us query. Two kernels keep the markers (ev[4] splits them).
+  const int nkern = (has_filter ? 1 : 0) + (need_agg && !fused ? 1 : 0);
+  const char *xe = getenv("PHIP_EXT_EVENTS");  // measurement override: "0" = separate markers
+  const bool ext_events = total_work > 0 && nkern == 1 && !P.split_event && !(xe && atoi(xe) == 0);
+  hipEvent_t e0 = ext_events ? P.ev[1] : nullptr, e1 = ext_events ? P.ev[2] : nullptr;
+  if (!ext_events) HIP_TRY(hipEventRecord(P.ev[1], st));
   if (has_filter && total_work > 0)
-    HIP_TRY(launch_filter(fq, conj_only, P.fused_naggs, filter_blocks, filter_lds, st));
-  // (a plan of one kernel -- fused, or a filter or aggregation alone -- needs no split event: every timing marker on
-  // the queue is a barrier packet the command processor waits on, a few microseconds of a 25-us query)
+    HIP_TRY(launch_filter(fq, conj_only, P.fused_naggs, filter_blocks, filter_lds, st, e0, e1));
+  // (a plan of one kernel -- fused, or a filter or aggregation alone -- needs no split event)
   if (P.split_event) HIP_TRY(hipEventRecord(P.ev[4], st));
   if (need_agg && total_work > 0 && !fused)
-    HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st));
-  HIP_TRY(hipEventRecord(P.ev[2], st));
+    HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st, e0, e1));
+  if (!ext_events) HIP_TRY(hipEventRecord(P.ev[2], st));
   if (group_by && dq.mode == GB_LDS && total_work > 0)
     HIP_TRY(launch_slab_reduce((const uint64_t *)slab, agg_blocks, dq.tbl_words, dq.num_groups, dev_kinds,
                                (uint64_t *)gtab, (const uint32_t *)hslab, nhll ? dq.hll_words : 0, (uint32_t *)ghll, st));

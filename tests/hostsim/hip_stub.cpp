@@ -77,14 +77,16 @@ size_t chunk_decode_extra_lds(int, int32_t) { return 0; }
 hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }
 hipError_t launch_roaring_or(const RoaringTask *, const RoaringGroup *, int32_t, hipStream_t) { return hipSuccess; }
-hipError_t launch_filter(const DevFilter &q, bool, int fused_naggs, int nblocks, size_t, hipStream_t) {
+hipError_t launch_filter(const DevFilter &q, bool, int fused_naggs, int nblocks, size_t, hipStream_t, hipEvent_t,
+                         hipEvent_t) {
   memset(q.partials, 0, (size_t)nblocks * 2 * 8);
   if (fused_naggs > 0) memset(q.agg_partials, 0, (size_t)nblocks * fused_naggs * 8);
   if (q.mask_out) memset(q.mask_out, 0, (size_t)q.total_work * 64 * 4);
   return hipSuccess;
 }
 hipError_t launch_masks_to_words(const uint32_t *, int32_t, int32_t, uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
-hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *, int nblocks, size_t, hipStream_t) {
+hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *, int nblocks, size_t, hipStream_t, hipEvent_t,
+                      hipEvent_t) {
   if (q.mode == GB_NONE) memset(q.partials, 0, (size_t)nblocks * q.num_aggs * 8);
   else if (q.mode == GB_GLOBAL) q.gb_table[0] = 1;  // one non-empty group
   else if (q.mode == GB_HASH) { q.gb_table[0] = 1; q.gb_keys[0] = 0; }  // slot 0 holds key 0

@@ -3,7 +3,8 @@ SUM / MIN / MAX operand with a large dictionary is read as one value per doc ins
 gather. Every path that projects values (fused filter+aggregation, the aggregation kernel's dense and sparse walks,
 LDS / HBM / hash group-by tables, filtered aggregations) must give the oracle's answers with the values on
 (PHIP_MATERIALIZE_MIN_DICT=0: every numeric dictionary), at the default threshold, and off (PHIP_MATERIALIZE=0);
-columns a filter or group-by also reads keep their ids."""
+columns a filter or group-by also reads keep their ids. DISTINCTCOUNTHLL over a large dictionary reads doc-order
+registers entries (ensure_hll_doc) the same way: registers bit-exact."""
 import numpy as np
 import pytest
 
@@ -47,12 +48,16 @@ AGG = [
     "SELECT SUM(p), MAX(d) FROM t",                                             # no filter
     "SELECT SUM(p), COUNT(*) FROM t WHERE p < 500000000 AND g = 2",             # p also filtered: ids
     "SELECT SUM(p) FILTER (WHERE f < 10), MAX(l) FILTER (WHERE g = 3), COUNT(*) FROM t WHERE q > 5",
+    "SELECT DISTINCTCOUNTHLL(p), COUNT(*) FROM t WHERE f < 30",                # doc-order HLL entries
+    "SELECT DISTINCTCOUNTHLL(l, 10), DISTINCTCOUNTHLL(q), SUM(p) FROM t WHERE g <> 4",
 ]
 GROUP_BY = [
     "SELECT g, SUM(p), MAX(d), COUNT(*) FROM t WHERE f < 50 GROUP BY g LIMIT 1000",
     "SELECT g, q, SUM(l), MIN(p) FROM t GROUP BY g, q LIMIT 100000",
     "SELECT f, SUM(p * q) FROM t WHERE g < 5 GROUP BY f ORDER BY SUM(p * q) DESC LIMIT 10",
     "SELECT p, COUNT(*) FROM t WHERE f < 3 GROUP BY p LIMIT 100000",               # p a key: ids
+    "SELECT g, DISTINCTCOUNTHLL(p), SUM(l) FROM t WHERE f < 60 GROUP BY g LIMIT 100",  # HLL in an LDS table
+    "SELECT g, q, DISTINCTCOUNTHLL(l) FROM t GROUP BY g, q LIMIT 100000",
 ]
 
 
