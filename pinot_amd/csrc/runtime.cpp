@@ -3126,12 +3126,12 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
   const bool fused = P.fused_naggs > 0;
-  // A plan of one kernel (fused, or a filter or an aggregation alone) has its timing events recorded by the kernel's
-  // own dispatch packet (hipExtLaunchKernel): every separate marker is a barrier packet the command processor waits
-  // on, a few microseconds of a 20-us query. Two kernels keep the markers (ev[4] splits them).
+  // Opt-in (PHIP_EXT_EVENTS=1): a one-kernel plan's timing events recorded by the kernel's own dispatch packet
+  // (hipExtLaunchKernel) instead of two barrier-packet markers. Measured on the sorted headline it costs more than it
+  // saves: enqueue 7.0 -> 9.8 us per query, step 0.286 -> 0.304 ms (profiles/r04p_host_ab.log).
   const int nkern = (has_filter ? 1 : 0) + (need_agg && !fused ? 1 : 0);
-  const char *xe = getenv("PHIP_EXT_EVENTS");  // measurement override: "0" = separate markers
-  const bool ext_events = total_work > 0 && nkern == 1 && !P.split_event && !(xe && atoi(xe) == 0);
+  const char *xe = getenv("PHIP_EXT_EVENTS");
+  const bool ext_events = total_work > 0 && nkern == 1 && !P.split_event && xe && atoi(xe) != 0;
   hipEvent_t e0 = ext_events ? P.ev[1] : nullptr, e1 = ext_events ? P.ev[2] : nullptr;
   if (!ext_events) HIP_TRY(hipEventRecord(P.ev[1], st));
   if (has_filter && total_work > 0)

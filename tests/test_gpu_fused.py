@@ -109,3 +109,20 @@ def test_gpu_folded_finalize(sql, fuse, fused_segments, monkeypatch):
         assert blk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
         _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
     op.close()
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_gpu_ext_launch_events(fuse, fused_segments, monkeypatch):
+    """PHIP_EXT_EVENTS=1: a one-kernel plan's timing events ride on its dispatch packet (hipExtLaunchKernel) -- same
+    answers, a positive kernel time."""
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    from tests.test_gpu_parity import _assert_intermediates_equal
+    monkeypatch.setenv("PHIP_FUSE", fuse)
+    monkeypatch.setenv("PHIP_EXT_EVENTS", "1")
+    raws, segs = fused_segments
+    for sql in (QUERIES[0], QUERIES[3], "SELECT COUNT(*) FROM t WHERE f < 20"):
+        qc = parse(sql)
+        blk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
+        oblk, ex = executor.execute(qc, raws)
+        _assert_intermediates_equal(qc.aggregations, blk.results, oblk.results, ex)
+        assert (blk.filter_kernel_ms or 0) + (blk.agg_kernel_ms or 0) > 0

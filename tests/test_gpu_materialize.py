@@ -49,7 +49,7 @@ AGG = [
     "SELECT SUM(p), COUNT(*) FROM t WHERE p < 500000000 AND g = 2",             # p also filtered: ids
     "SELECT SUM(p) FILTER (WHERE f < 10), MAX(l) FILTER (WHERE g = 3), COUNT(*) FROM t WHERE q > 5",
     "SELECT DISTINCTCOUNTHLL(p), COUNT(*) FROM t WHERE f < 30",                # doc-order HLL entries
-    "SELECT DISTINCTCOUNTHLL(l, 10), DISTINCTCOUNTHLL(q), SUM(p) FROM t WHERE g <> 4",
+    "SELECT DISTINCTCOUNTHLL(l, 10), DISTINCTCOUNTHLL(q, 10), SUM(p) FROM t WHERE g <> 4",
 ]
 GROUP_BY = [
     "SELECT g, SUM(p), MAX(d), COUNT(*) FROM t WHERE f < 50 GROUP BY g LIMIT 1000",
