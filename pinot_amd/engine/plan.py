@@ -806,10 +806,21 @@ class GpuCombineOperator:
                     dv = _lib.DictionaryView()
                     _lib.check(lib.phip_result_dictionary(res, k, ctypes.byref(dv)))
                     cols.append(_dictionary_lookup(dv, keys[:, k]) if ng else [])
-                groups = {}
-                for g in range(ng):
-                    key = tuple(cols[k][g] for k in range(nk))
-                    groups[key] = intermediates(g)
+                # column-wise (one list per primitive, then per function), zipped into the groups' lists: the
+                # per-group Python work is a few list operations (280 groups: 0.25 -> ~0.05 ms)
+                prim_cols = []
+                for i, p in enumerate(self.prims):
+                    f = p[0]
+                    if f == _lib.AGG_COUNT or (f == _lib.AGG_SUM and exact[i]):
+                        prim_cols.append([int(row[i]) for row in longs])
+                    elif f in (_lib.AGG_SUM, _lib.AGG_MIN, _lib.AGG_MAX):
+                        prim_cols.append([float(row[i]) for row in vals])
+                    else:
+                        prim_cols.append([hll[g, hll_slot[i]].copy() for g in range(ng)])
+                fcols = [list(zip(prim_cols[sl[0]], prim_cols[sl[1]])) if fn in ("avg", "minmaxrange") else prim_cols[sl]
+                         for fn, sl in self.mapping]
+                gkeys = list(zip(*cols)) if nk else [()] * ng
+                groups = dict(zip(gkeys, map(list, zip(*fcols)))) if fcols else {k: [] for k in gkeys}
                 blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
                                           bool(r.num_groups_limit_reached))
                 blk.num_groups_trimmed = bool(r.num_groups_trimmed)
