@@ -434,16 +434,16 @@ __device__ __forceinline__ void fin_slot(const uint64_t *partials, int nblocks, 
   uint64_t v = fp ? acc_init(kind) : 0;
   // every load of the lane issued before the first combine (coherent loads reach the device coherence point: one
   // dependent round trip per block would cost ~20 of them)
-  uint64_t w[kFinLoads];
+  for (int b0 = 0; b0 < nblocks; b0 += 64 * kFinLoads) {  // (1280 blocks: 3 round trips, not 13)
+    uint64_t w[kFinLoads];
 #pragma unroll
-  for (int i = 0; i < kFinLoads; i++) {
-    const int b = lane + 64 * i;
-    w[i] = b < nblocks ? coherent_load(partials + (int64_t)b * nslots + a) : (fp ? acc_init(kind) : 0);
+    for (int i = 0; i < kFinLoads; i++) {
+      const int b = b0 + lane + 64 * i;
+      w[i] = b < nblocks ? coherent_load(partials + (int64_t)b * nslots + a) : (fp ? acc_init(kind) : 0);
+    }
+#pragma unroll
+    for (int i = 0; i < kFinLoads; i++) v = acc_combine(kind, v, w[i]);
   }
-#pragma unroll
-  for (int i = 0; i < kFinLoads; i++) v = acc_combine(kind, v, w[i]);
-  for (int b = lane + 64 * kFinLoads; b < nblocks; b += 64)
-    v = acc_combine(kind, v, coherent_load(partials + (int64_t)b * nslots + a));
   if (fp) v = as_u64(wave_reduce_f64(as_f64(v), kind));
   else v = wave_reduce_u64_add(v);
   if (lane == 0) out[a] = v;
@@ -453,9 +453,23 @@ __device__ __forceinline__ void finalize_tail(const DevFinal *fp) {
   __shared__ uint32_t ticket;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores / atomics acknowledged
   __syncthreads();
-  if (threadIdx.x == 0) ticket = __hip_atomic_fetch_add(fp->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // Two-level ticket: a workgroup counts itself in its shard (blockIdx % kFinShards, one 64-B line each), the one that
+  // completes a shard counts the shard at the top; the completer of the last shard finalizes. One device-scope
+  // counter taking every workgroup's add serialised them at the memory side (r04f: +13-50 us per launch).
+  if (threadIdx.x == 0) {
+    const uint32_t k = blockIdx.x % kFinShards;
+    const uint32_t nk = min((uint32_t)kFinShards, gridDim.x);
+    const uint32_t in_shard = (gridDim.x - k + kFinShards - 1) / kFinShards;
+    uint32_t *sc = fp->counter + 16 * (1 + k);
+    uint32_t last = 0;
+    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_shard - 1) {
+      __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(fp->counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nk - 1 ? 1u : 0u;
+    }
+    ticket = last;
+  }
   __syncthreads();
-  if (ticket != gridDim.x - 1) return;
+  if (ticket == 0) return;
   const DevFinal &f = *fp;
   const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int s = wave; s < f.na + 2; s += nw) {

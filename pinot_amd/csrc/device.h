@@ -185,6 +185,8 @@ struct DevNode {
 // last workgroup of the plan's last kernel (agg_common.h finalize_tail): fixed-order reductions of the per-block
 // partials, the per-segment matched counts and the HLL registers, written into the plan's mapped pinned area and
 // the device counters zeroed for the next execution -- one launch and its dispatch gap fewer per query.
+constexpr int kFinShards = 16;
+constexpr size_t kFinCounterBytes = 64 * (1 + kFinShards);
 struct DevFinal {
   const uint64_t *pa;   // aggregation partials [nba][na], or null
   const int32_t *ka;    // their accumulator kinds
@@ -193,7 +195,8 @@ struct DevFinal {
   uint64_t *segm;       // [nseg] matched docs per (program, segment) entry
   uint32_t *hll;        // [hll_words] registers (aggregation only)
   uint64_t *out;        // pinned: [0, na) slots, [32, 34) filter sums, [64, 64 + nseg) segm, then the registers
-  uint32_t *counter;    // workgroups done (the last one finalizes and resets it)
+  uint32_t *counter;    // [0]: shards complete; [16 (1 + k)]: workgroups done in shard k (blockIdx % kFinShards),
+                        // each on its own 64-B line; the last shard's completer finalizes and resets them
   int32_t nba, na, nbf, nseg, hll_words, pad;
 };
 

@@ -3058,10 +3058,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     f.hll_words = nhll ? (int32_t)((size_t)nhll << log2m) : 0;
     f.out = P.pinned_dev;
     void *fb;
-    rc = P.alloc(sizeof(DevFinal) + 64, &fb);
+    rc = P.alloc(round_up(sizeof(DevFinal), 64) + kFinCounterBytes, &fb);
     if (rc) return rc;
-    f.counter = (uint32_t *)((uint8_t *)fb + round_up(sizeof(DevFinal), 16));
-    HIP_TRY(hipMemsetAsync(f.counter, 0, 4, st));
+    f.counter = (uint32_t *)((uint8_t *)fb + round_up(sizeof(DevFinal), 64));
+    HIP_TRY(hipMemsetAsync(f.counter, 0, kFinCounterBytes, st));
     HIP_TRY(hipMemcpyAsync(fb, &f, sizeof(f), hipMemcpyHostToDevice, st));
     P.fin_counter = f.counter;
     if (agg_last) {
@@ -3103,7 +3103,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (!P.clean) {
     HIP_TRY(hipMemsetAsync(seg_matched, 0, (size_t)P.nmatch * 8, st));
     if (hll_words) HIP_TRY(hipMemsetAsync(dq.hll_regs, 0, hll_words * 4, st));
-    if (P.fin_counter) HIP_TRY(hipMemsetAsync(P.fin_counter, 0, 4, st));
+    if (P.fin_counter) HIP_TRY(hipMemsetAsync(P.fin_counter, 0, kFinCounterBytes, st));
   }
   P.clean = false;
   if (filter_words) HIP_TRY(hipMemsetAsync(fo, 0, (size_t)filter_nwords * 8, st));
