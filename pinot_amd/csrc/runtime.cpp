@@ -3036,10 +3036,12 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // Finalize in the last workgroup of the plan's last kernel (agg_common.h finalize_tail) for aggregation-only plans:
   // the finalize_all launch and its dispatch gap go. With one device-scope ticket counter the workgroups' atomics
   // serialised at the memory side (the fused kernel grew 13-50 us, step 0.346 -> 0.421 ms, profiles/r04f_host_ab.log);
-  // with the two-level sharded ticket the kernel grows 4-6 us and the step gains 3 % (0.280 / 0.286 -> 0.272 / 0.278
-  // ms, profiles/r04w_host_ab.log). PHIP_FOLD_FINAL=0 keeps the finalize launch (A/B).
+  // with the two-level sharded ticket the step gains 2-3 % (host probe 0.280 / 0.286 -> 0.272 / 0.278 ms,
+  // profiles/r04w_host_ab.log; bench 0.284 -> 0.278 ms, profiles/r04x_bench.log), but every workgroup now waits for
+  // its partials' acknowledgement and a ticket before it retires, and the fused kernel itself grows 11 % (sorted Q1.1
+  // 0.135 -> 0.150 ms): its own roofline fraction drops more than the step gains. Opt-in (PHIP_FOLD_FINAL=1).
   const char *ff = getenv("PHIP_FOLD_FINAL");
-  if (!group_by && !P.select && !want_bitmap && total_work > 0 && (has_filter || need_agg) && (!ff || atoi(ff) != 0)) {
+  if (!group_by && !P.select && !want_bitmap && total_work > 0 && (has_filter || need_agg) && ff && atoi(ff) != 0) {
     const bool fused = fused_naggs > 0;
     const bool agg_last = need_agg && !fused;
     const bool aggs_here = need_agg && naggs > 0;

@@ -95,8 +95,8 @@ def test_gpu_fused_ssb_q1(layout, fuse, gpu_lib, monkeypatch):
 @pytest.mark.parametrize("fuse", ["0", "1"])
 @pytest.mark.parametrize("sql", QUERIES)
 def test_gpu_folded_finalize(sql, fuse, fold, fused_segments, monkeypatch):
-    """PHIP_FOLD_FINAL=1 (default): the last workgroup of the plan's last kernel finalizes (agg_common.h finalize_tail,
-    a two-level sharded ticket) instead of a finalize launch; 0 keeps the launch -- same answers."""
+    """PHIP_FOLD_FINAL=1: the last workgroup of the plan's last kernel finalizes (agg_common.h finalize_tail, a
+    two-level sharded ticket) instead of a finalize launch; 0 (default) keeps the launch -- same answers."""
     from pinot_amd.engine.plan import GpuInstancePlanMaker
     from tests.test_gpu_parity import _assert_intermediates_equal
     monkeypatch.setenv("PHIP_FUSE", fuse)
