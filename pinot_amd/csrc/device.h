@@ -23,7 +23,10 @@ constexpr int kFilterBlock = 256;
 constexpr int kFilterWaves = kFilterBlock / kWave;
 constexpr int kMaxRing = 8;           // LDS-DMA ring slots per wave
 constexpr int kFusedRingTile = 512;   // fused aggregation, per-tile mode: u16 tile-relative doc ids per wave
-constexpr int kFusedRingDefer = 512;  // fused aggregation, deferred mode: u32 segment doc ids per wave (one batch
+#ifndef PHIP_FUSED_RING_DEFER
+#define PHIP_FUSED_RING_DEFER 512  // (A/B builds override it)
+#endif
+constexpr int kFusedRingDefer = PHIP_FUSED_RING_DEFER;  // fused aggregation, deferred mode: u32 segment doc ids per wave (one batch
                                       // + an eighth of a tile)
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;

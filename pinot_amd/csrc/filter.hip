@@ -930,7 +930,10 @@ __device__ __forceinline__ uint32_t eval_conj(cseg_t &seg, const PHIP_LDS uint8_
 // with ds_bpermute; larger ones are gathered from HBM -- the aggregation kernel's walk without the mask round
 // trip, the re-read of the filter columns and a second launch.
 // ------------------------------------------------------------------------------------------------
-constexpr int kFusedBatch = 4;  // 64-doc chunks per gather round trip
+#ifndef PHIP_FUSED_BATCH
+#define PHIP_FUSED_BATCH 4  // (A/B builds override it)
+#endif
+constexpr int kFusedBatch = PHIP_FUSED_BATCH;  // 64-doc chunks per gather round trip
 
 // The lane's share of a small dictionary: entry `lane` (64-bit image of the value), or 0.
 struct SmallDict {
