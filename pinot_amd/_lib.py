@@ -4,6 +4,7 @@ This is the Python twin of the Java FFM binding shown in INTEGRATION.md. The pro
 no CPU fallback: if the library cannot be loaded, or no GPU is present, calls raise.
 """
 import ctypes
+import struct
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -114,6 +115,12 @@ class Result(ctypes.Structure):
                 ("num_rows", ctypes.c_int64), ("num_select", ctypes.c_int32), ("reserved_select", ctypes.c_int32),
                 ("select_types", ctypes.POINTER(ctypes.c_int32)), ("select_values", ctypes.POINTER(ctypes.c_uint64)),
                 ("segment_docs_matched", ctypes.POINTER(ctypes.c_int64)), ("stream_bytes", ctypes.c_int64)]
+
+
+# phip_result's scalar image in one read (the aggregation-only fast path of plan._block_from_result): the fields in
+# declaration order, natural alignment (checked against ctypes below)
+RESULT_IMAGE = struct.Struct("<4q4iq2i4Q2d2iQ2d3q2i3Qq")
+assert RESULT_IMAGE.size == ctypes.sizeof(Result)
 
 
 class DictionaryView(ctypes.Structure):
