@@ -1,0 +1,67 @@
+"""The aggregation-only fast decode of phip_result (plan.GpuCombineOperator._aggregation_block over one
+_lib.RESULT_IMAGE read) against the values the library laid out, on a host-built result (no GPU): exact int64 sums
+and counts, double sums / MIN / MAX, AVG and MINMAXRANGE pairs, statistics and kernel fields; HLL and group-by
+results fall back to the general path (None)."""
+import ctypes
+from types import SimpleNamespace
+
+from pinot_amd import _lib
+from pinot_amd.engine.plan import GpuCombineOperator, plan_aggregations
+from pinot_amd.query.sql import parse
+
+
+def _result(vals, longs, exact, nhll=0, ngroups=1):
+    r = _lib.Result()
+    n = len(vals)
+    keep = [(ctypes.c_double * n)(*vals), (ctypes.c_int64 * n)(*longs), (ctypes.c_int32 * n)(*exact)]
+    r.num_docs_scanned, r.num_entries_scanned_in_filter, r.num_entries_scanned_post_filter = 11, 22, 33
+    r.num_total_docs, r.num_segments_processed, r.num_segments_matched = 44, 5, 4
+    r.num_aggregations, r.num_groups, r.num_hll = n, ngroups, nhll
+    r.values = ctypes.cast(keep[0], ctypes.POINTER(ctypes.c_double))
+    r.long_values = ctypes.cast(keep[1], ctypes.POINTER(ctypes.c_int64))
+    r.long_exact = ctypes.cast(keep[2], ctypes.POINTER(ctypes.c_int32))
+    r.filter_kernel_ms, r.agg_kernel_ms, r.device_ms, r.scan_kernel_ms = 0.25, 0.5, 0.75, 0.125
+    r.filter_bytes, r.agg_bytes, r.stream_bytes, r.fused = 1000, 2000, 900, 1
+    return r, keep
+
+
+def test_aggregation_fast_decode():
+    qc = parse("SELECT COUNT(*), SUM(a), SUM(b), MIN(b), AVG(a), MINMAXRANGE(b) FROM t")
+    prims, mapping = plan_aggregations(qc.aggregations)
+    # prims: COUNT, SUM(a), SUM(b), MIN(b), MAX(b) (AVG / MINMAXRANGE share the SUM / COUNT / MIN slots)
+    kinds = [p[0] for p in prims]
+    vals = [0.0] * len(prims)
+    longs = [0] * len(prims)
+    exact = [0] * len(prims)
+    for i, (k, col) in enumerate((p[0], p[2]) for p in prims):
+        if k == _lib.AGG_COUNT:
+            longs[i] = 1234
+        elif k == _lib.AGG_SUM and col == "a":
+            longs[i], exact[i], vals[i] = 2 ** 60 + 7, 1, float(2 ** 60 + 7)
+        elif k == _lib.AGG_SUM:
+            vals[i] = 12.5
+        elif k == _lib.AGG_MIN:
+            vals[i] = -3.0
+        else:
+            vals[i] = 9.0
+    r, keep = _result(vals, longs, exact)
+    op = SimpleNamespace(prims=prims, mapping=mapping, query=qc)
+    blk = GpuCombineOperator._aggregation_block(op, ctypes.pointer(r))
+    assert blk.results == [1234, 2 ** 60 + 7, 12.5, -3.0, (2 ** 60 + 7, 1234), (-3.0, 9.0)]
+    assert isinstance(blk.results[1], int) and isinstance(blk.results[2], float)
+    s = blk.stats
+    assert (s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter, s.num_total_docs,
+            s.num_segments_processed, s.num_segments_matched) == (11, 22, 33, 44, 5, 4)
+    assert (blk.filter_kernel_ms, blk.agg_kernel_ms, blk.device_ms, blk.scan_kernel_ms) == (0.25, 0.5, 0.75, 0.125)
+    assert (blk.filter_bytes, blk.agg_bytes, blk.stream_bytes, blk.fused) == (1000, 2000, 900, True)
+    assert _lib.AGG_HLL not in kinds
+
+
+def test_fast_decode_leaves_hll_and_groups_to_the_general_path():
+    qc = parse("SELECT COUNT(*) FROM t")
+    prims, mapping = plan_aggregations(qc.aggregations)
+    op = SimpleNamespace(prims=prims, mapping=mapping, query=qc)
+    r, keep = _result([0.0], [5], [0], nhll=1)
+    assert GpuCombineOperator._aggregation_block(op, ctypes.pointer(r)) is None
+    r, keep = _result([0.0], [5], [0], ngroups=3)
+    assert GpuCombineOperator._aggregation_block(op, ctypes.pointer(r)) is None
