@@ -3547,17 +3547,23 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     // some segment may have reached numGroupsLimit: the first-seen pass decides which keys it kept (and the
     // normal pass's compaction would be thrown away)
     const bool limit_pass = mode == EXEC_FULL && P.num_groups_limit > 0 && ngroups >= P.num_groups_limit;
+    // the compacted keys, values, exact sums and registers of the groups back to back in one buffer (one copy out)
+    auto contiguous_out = [&](const char *name, int64_t n, void **k, void **v, void **l, void **h) -> int32_t {
+      void *base;
+      const size_t kb = (size_t)n * 8, vb = (size_t)n * naggs * 8, hb = (size_t)n * nhll * m_regs;
+      int32_t rc2 = ws.get(name, std::max<size_t>(kb + 2 * vb + hb, 16), &base);
+      if (rc2) return rc2;
+      *k = base;
+      *v = (uint8_t *)base + kb;
+      *l = (uint8_t *)base + kb + vb;
+      *h = nhll ? (uint8_t *)base + kb + 2 * vb : nullptr;
+      return PHIP_OK;
+    };
+    bool out_contig = false;
     if (!limit_pass) {
-      rc = ws.get("gb_keys", (size_t)std::max<int64_t>(ngroups, 1) * 8, &keys);
+      rc = contiguous_out("gb_out", ngroups, &keys, &ov, &ol, &oh);
       if (rc) return rc;
-      rc = ws.get("gb_out_vals", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ov);
-      if (rc) return rc;
-      rc = ws.get("gb_out_longs", (size_t)std::max<int64_t>(ngroups * naggs, 1) * 8, &ol);
-      if (rc) return rc;
-      if (nhll) {
-        rc = ws.get("gb_out_hll", (size_t)std::max<int64_t>(ngroups, 1) * nhll * m_regs, &oh);
-        if (rc) return rc;
-      }
+      out_contig = true;
       HIP_TRY(launch_group_compact((const uint64_t *)gtab, dq.num_groups, (const int64_t *)offs, nchunks, (int64_t *)keys, st));
       HIP_TRY(launch_group_gather((const int64_t *)keys, ngroups, dq.num_groups, naggs, dq.own_count_rows, gather_kinds,
                                   (const uint64_t *)gtab,
@@ -3598,10 +3604,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       void *scratch, *k2, *v2, *l2, *h2 = nullptr;
       const int64_t k = P.trim_size;
       if ((rc = ws.get("trim_scratch", sbytes, &scratch))) return rc;
-      if ((rc = ws.get("trim_keys", (size_t)k * 8, &k2))) return rc;
-      if ((rc = ws.get("trim_vals", (size_t)k * std::max(naggs, 1) * 8, &v2))) return rc;
-      if ((rc = ws.get("trim_longs", (size_t)k * std::max(naggs, 1) * 8, &l2))) return rc;
-      if (nhll && (rc = ws.get("trim_hll", (size_t)k * nhll * m_regs, &h2))) return rc;
+      if ((rc = contiguous_out("trim_out", k, &k2, &v2, &l2, &h2))) return rc;
       if (terms)
         HIP_TRY(launch_trim_order_terms((const double *)ov, (const int64_t *)keys, &ot, ngroups, naggs, scratch, &sbytes,
                                         &order, st));
@@ -3617,12 +3620,18 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       oh = h2;
       ngroups = k;
       r.num_groups_trimmed = 1;
+      out_contig = true;
     }
     std::vector<int64_t> hkeys(ngroups);
     impl->values.resize(ngroups * naggs);
     impl->longs.resize(ngroups * naggs);
     impl->hll.resize((size_t)ngroups * nhll * m_regs);
-    if (ngroups) {
+    const size_t kb = (size_t)ngroups * 8, vb = (size_t)ngroups * naggs * 8, hb = impl->hll.size();
+    std::vector<uint8_t> staged;
+    if (ngroups && out_contig) {  // one copy of the contiguous outputs (each small copy is its own command)
+      staged.resize(kb + 2 * vb + hb);
+      HIP_TRY(hipMemcpyAsync(staged.data(), keys, staged.size(), hipMemcpyDeviceToHost, st));
+    } else if (ngroups) {
       HIP_TRY(hipMemcpyAsync(hkeys.data(), keys, ngroups * 8, hipMemcpyDeviceToHost, st));
       if (naggs) {
         HIP_TRY(hipMemcpyAsync(impl->values.data(), ov, ngroups * naggs * 8, hipMemcpyDeviceToHost, st));
@@ -3632,6 +3641,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     }
     if (P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (!staged.empty()) {
+      memcpy(hkeys.data(), staged.data(), kb);
+      if (vb) {
+        memcpy(impl->values.data(), staged.data() + kb, vb);
+        memcpy(impl->longs.data(), staged.data() + kb + vb, vb);
+      }
+      if (hb) memcpy(impl->hll.data(), staged.data() + kb + 2 * vb, hb);
+    }
     if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
     impl->keys.resize(ngroups * P.num_group_by);
     for (int64_t g = 0; g < ngroups; g++) {
