@@ -20,8 +20,10 @@ from pinot_amd.spi import DataType
 
 
 def _seg(name="n0"):
-    """x: INT with nulls at docs 1, 3, 6; y: INT, no nulls; s: STRING with a null at doc 2; r: raw LONG with nulls."""
-    c = SegmentCreator(name, no_dictionary_columns=["r"])
+    """x: INT with nulls at docs 1, 3, 6; y: INT, no nulls; s: STRING with a null at doc 2 (inverted index); r: raw
+    LONG with nulls; o: sorted INT with a null at doc 0 (its stored Integer.MIN_VALUE keeps it sorted)."""
+    c = SegmentCreator(name, no_dictionary_columns=["r"], inverted_index_columns=["s"])
+    c.add_column("o", DataType.INT, [0, 1, 1, 2, 3, 3, 4, 9], nulls=[1, 0, 0, 0, 0, 0, 0, 0])
     c.add_column("x", DataType.INT, [5, 0, 7, 0, 5, 9, 0, 1], nulls=[0, 1, 0, 1, 0, 0, 1, 0])
     c.add_column("y", DataType.INT, [1, 1, 2, 2, 3, 3, 1, 2])
     c.add_column("s", DataType.STRING, ["a", "b", "", "a", "c", "b", "a", "c"], nulls=[0, 0, 1, 0, 0, 0, 0, 0])
@@ -154,6 +156,12 @@ class _HostSeg:
     def has_null_vector(self, c):
         return bool(self.segment.columns[c].null_vector)
 
+    def inverted_bytes(self, c, dict_ids):
+        ci = self.segment.columns[c]
+        off = np.frombuffer(ci.inverted[:4 * (ci.metadata.cardinality + 1)], dtype=">u4").astype(np.int64)
+        ids = np.asarray(dict_ids, dtype=np.int64)
+        return int((off[ids + 1] - off[ids]).sum())
+
     def sorted_doc_range(self, c, d):
         p = np.frombuffer(self.segment.columns[c].forward, dtype=">i4").reshape(-1, 2)
         return int(p[d, 0]), int(p[d, 1])
@@ -181,6 +189,10 @@ def _eval_tree(os_, t):
         m = (ids >= t.lo) & (ids < t.hi)
     elif t.kind == _lib.LEAF_DICT_SET:
         m = np.isin(os_.dict_ids(t.column), t.ids)
+    elif t.kind == _lib.LEAF_INVERTED:
+        m = np.zeros(n, dtype=bool)
+        for d in np.asarray(t.ids).tolist():
+            m[os_.inverted_docs(t.column, int(d))] = True
     elif t.kind == _lib.LEAF_RAW_RANGE:  # (integral raw column: lo_int <= v <= hi_int)
         rr = _lib.RawRange.from_buffer_copy(np.asarray(t.ids, dtype=np.int32).tobytes())
         v = os_.values(t.column)
@@ -198,7 +210,9 @@ def _eval_tree(os_, t):
 WHERES = ["x = 5", "x <> 5", "NOT (x = 5)", "x IS NULL", "x IS NOT NULL", "NOT (x IS NOT NULL)", "x >= 0",
           "NOT (x >= 0)", "NOT (x = 12345)", "NOT (x <> 12345)", "x <> 12345 AND y = 1", "NOT (r > 30)", "x IN (5, 9) AND y = 3", "NOT (x = 5 AND y = 1)", "NOT (x = 7 OR y = 3)",
           "NOT (NOT (x = 5 AND y = 1))", "s = 'a' OR x > 6", "NOT (s = 'a' OR x > 6)", "s IS NULL OR x IS NULL",
-          "NOT (s IN ('a', 'b') AND NOT (x BETWEEN 1 AND 7))", "y = 2 AND NOT (x = 7)"]
+          "NOT (s IN ('a', 'b') AND NOT (x BETWEEN 1 AND 7))", "y = 2 AND NOT (x = 7)",
+          "o BETWEEN 1 AND 3", "NOT (o BETWEEN 1 AND 3)", "NOT (o > 2 OR s = 'c')", "o IS NULL OR s IS NULL",
+          "NOT (s = 'b')", "s <> 'zz'", "NOT (s <> 'zz')"]
 
 
 @pytest.mark.parametrize("nh", [True, False])
