@@ -229,9 +229,15 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
         sv = np.zeros(6 + lay.nsum)
         mv = lay.empty_max(1)[0]
         sv[:6] = _stats_vector(block.stats)
-        lay.put(sv[6:], mv, block.results)
-        sv, mv = _sum_max(dist, group, sv, mv)
-        return AggregationResultsBlock(aggs, lay.get(sv[6:], mv), _stats_from(sv[:6]))
+        # a null intermediate (enableNullHandling: nothing non-null aggregated) contributes the function's identity,
+        # and a presence flag per function (MAX over the ranks) says whether any rank had a value
+        ident = lay.get(np.zeros(lay.nsum), lay.empty_max(1)[0])
+        lay.put(sv[6:], mv, [ident[i] if v is None else v for i, v in enumerate(block.results)])
+        present = np.array([v is not None for v in block.results], dtype=np.int64)
+        sv, mv = _sum_max(dist, group, sv, np.concatenate([mv, present]))
+        vals = lay.get(sv[6:], mv[:lay.nmax])
+        vals = [v if mv[lay.nmax + i] else None for i, v in enumerate(vals)]
+        return AggregationResultsBlock(aggs, vals, _stats_from(sv[:6]))
 
     # ---- group-by: node-global dictionaries over the key values --------------------------------
     keys = list(block.groups.keys())

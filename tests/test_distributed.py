@@ -365,3 +365,50 @@ def test_distributed_block_rank_failure_world2_gloo(where):
         msgs.append(errs.get())
     assert not msgs, msgs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _null_worker(rank, world, port, errs):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pinot_amd.engine.distributed import allreduce_block
+        from pinot_amd.engine.results import AggregationResultsBlock, ExecutionStatistics
+        from pinot_amd.query.sql import parse
+        q = parse("SET enableNullHandling = true; SELECT SUM(a), MIN(a), AVG(a), COUNT(a), MAX(b), SUM(c) FROM t")
+        # rank 0 aggregated no non-null value of a / b; rank 1 has values; c is null everywhere
+        if rank == 0:
+            res = [None, None, None, 0, None, None]
+        else:
+            res = [7, -2.5, (7, 2), 2, 11.0, None]
+        blk = AggregationResultsBlock(q.aggregations, res, ExecutionStatistics(3, 0, 3, 10, 1, 1))
+        out = allreduce_block(blk, dist)
+        assert out.results == [7, -2.5, (7, 2), 2, 11.0, None], out.results
+        assert out.stats.num_docs_scanned == 6 and out.stats.num_total_docs == 20
+    except Exception as e:  # surfaced to the parent
+        import traceback
+        errs.put(f"rank {rank}: {type(e).__name__}: {e}\n{traceback.format_exc()}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_block_null_intermediates_world2_gloo():
+    """enableNullHandling across ranks: a rank's null intermediate adds nothing (the nullable functions' merge keeps
+    the other side), and a function null on every rank stays null."""
+    ctx = mp.get_context("spawn")
+    errs = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_null_worker, args=(r, 2, port, errs)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not errs.empty():
+        msgs.append(errs.get())
+    assert not msgs, msgs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
