@@ -134,7 +134,10 @@ hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t
 }
 hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t naggs, int32_t, const int32_t *, const uint64_t *,
                                const uint32_t *, int32_t nhll, int32_t log2m, double *v, int64_t *l, uint8_t *h, hipStream_t) {
-  memset(v, 0, ng * naggs * 8); memset(l, 0, ng * naggs * 8); if (nhll) memset(h, 0, ng * nhll * (1 << log2m)); return hipSuccess;
+  // a pattern (not zeros), so the host side's unpacking of the compacted outputs is checked (run_host_paths.py)
+  for (int64_t i = 0; i < ng * naggs; i++) { v[i] = 0.25 + (double)i; l[i] = 1000 + i; }
+  if (nhll) for (int64_t i = 0; i < ng * nhll * (1 << log2m); i++) h[i] = (uint8_t)(i * 3 + 1);
+  return hipSuccess;
 }
 hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hipStream_t) {
   for (int64_t i = 0; i < n; i++) slots[i] = (int64_t)keys[slots[i]];

@@ -47,6 +47,24 @@ for q in ("SELECT g, h, COUNT(*), SUM(m), SUM(d), MIN(d), MAX(m), DISTINCTCOUNTH
           "SELECT SUM(r), AVG(d), DISTINCTCOUNTHLL(g) FROM t WHERE h IN (1, 2) OR m > 0",
           "SELECT COUNT(*) FROM t WHERE NOT (h = 1 AND (g = 'k3' OR d < 0.5))"):
     pm.make_instance_plan(parse(q), gs).next_block()
+# the compacted group-by outputs come back in one copy (runtime.cpp contiguous_out): the stub's gather pattern must
+# reach the result arrays unchanged (values i + 0.25, exact sums 1000 + i, registers 3 i + 1)
+import ctypes  # noqa: E402
+from pinot_amd.engine.plan import GpuCombineOperator as _GCO  # noqa: E402
+for q in ("SELECT h, COUNT(*), SUM(m), MAX(d) FROM t GROUP BY h LIMIT 100000",
+          "SELECT h, COUNT(*), SUM(m), DISTINCTCOUNTHLL(r) FROM t GROUP BY h LIMIT 100000"):
+    op = _GCO(parse(q), gs, 100000)
+    res = op.run_raw()
+    r = res.contents
+    ng, na = r.num_groups, r.num_aggregations
+    assert ng >= 1 and na == 3, (ng, na)
+    for i in range(ng * na):
+        assert r.values[i] == 0.25 + i and r.long_values[i] == 1000 + i, (q, i, r.values[i], r.long_values[i])
+    if r.num_hll:
+        for i in range(ng * r.num_hll * 256):
+            assert r.hll_registers[i] == (i * 3 + 1) & 0xFF, (q, i)
+    _lib.load().phip_result_free(res)
+    op.close()
 # filtered aggregations: several filter programs in one plan (per-entry staging, interleaved inverted words,
 # per-program statistics), and the descriptor checks of num_filter_programs / aggregation.program
 pm.make_instance_plan(parse("SELECT COUNT(*), SUM(m) FILTER(WHERE h IN (1, 2)), MIN(d) FILTER(WHERE h = 4 AND "
