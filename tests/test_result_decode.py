@@ -65,3 +65,24 @@ def test_fast_decode_leaves_hll_and_groups_to_the_general_path():
     assert GpuCombineOperator._aggregation_block(op, ctypes.pointer(r)) is None
     r, keep = _result([0.0], [5], [0], ngroups=3)
     assert GpuCombineOperator._aggregation_block(op, ctypes.pointer(r)) is None
+
+
+def test_dictionary_lookup_strings_and_numbers():
+    """Group keys' values from a result dictionary (plan._dictionary_lookup): NUL-padded fixed-width strings come
+    back without the padding (interior bytes kept), numbers as Python scalars, repeated and empty id lists."""
+    from pinot_amd.engine.plan import _dictionary_lookup
+    from pinot_amd.spi import DataType
+    words = ["", "a", "MFGR#1221", "héllo", "x y"]
+    w = max(len(s.encode()) for s in words)
+    blob = (ctypes.c_uint8 * (len(words) * w))(*b"".join(s.encode().ljust(w, b"\0") for s in words))
+    dv = _lib.DictionaryView(int(DataType.STRING), len(words), w, 0, ctypes.addressof(blob))
+    ids = [4, 0, 2, 2, 3, 1]
+    assert _dictionary_lookup(dv, ids) == [words[i] for i in ids]
+    assert _dictionary_lookup(dv, []) == []
+    nums = (ctypes.c_int64 * 4)(-5, 2 ** 40, 0, 7)
+    dv = _lib.DictionaryView(int(DataType.LONG), 4, 0, 0, ctypes.addressof(nums))
+    got = _dictionary_lookup(dv, [1, 3, 0])
+    assert got == [2 ** 40, 7, -5] and all(type(v) is int for v in got)
+    dbl = (ctypes.c_double * 2)(1.5, -0.25)
+    dv = _lib.DictionaryView(int(DataType.DOUBLE), 2, 0, 0, ctypes.addressof(dbl))
+    assert _dictionary_lookup(dv, [1, 0]) == [-0.25, 1.5]
