@@ -961,13 +961,12 @@ __global__ __launch_bounds__(256) void group_compact_kernel(const uint64_t *__re
 }
 
 // Gather the aggregates of the compacted groups. table = [1 + naggs][ndense], row 0 = counts.
-__global__ void group_gather_kernel(const int64_t *__restrict__ keys, int64_t ngroups, int64_t ndense,
-                                    int32_t naggs, int32_t own_count, const int32_t *__restrict__ kinds,
-                                    const uint64_t *__restrict__ table, const uint32_t *__restrict__ hll, int32_t nhll,
-                                    int32_t log2m, double *__restrict__ out_values, int64_t *__restrict__ out_longs,
-                                    uint8_t *__restrict__ out_hll) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ngroups; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t key = keys[i];
+__device__ __forceinline__ void gather_group(int64_t i, int64_t key, int64_t ndense, int32_t naggs, int32_t own_count,
+                                             const int32_t *__restrict__ kinds, const uint64_t *__restrict__ table,
+                                             const uint32_t *__restrict__ hll, int32_t nhll, int32_t log2m,
+                                             double *__restrict__ out_values, int64_t *__restrict__ out_longs,
+                                             uint8_t *__restrict__ out_hll) {
+  {
     for (int a = 0; a < naggs; a++) {
       const int kind = kinds[a];
       const uint64_t v = table[(int64_t)(1 + a) * ndense + key];
@@ -990,6 +989,32 @@ __global__ void group_gather_kernel(const int64_t *__restrict__ keys, int64_t ng
       uint8_t *dst = out_hll + (i * nhll + h) * m;
       for (int j = 0; j < m; j++) dst[j] = (uint8_t)src[j];
     }
+  }
+}
+
+__global__ void group_gather_kernel(const int64_t *__restrict__ keys, int64_t ngroups, int64_t ndense,
+                                    int32_t naggs, int32_t own_count, const int32_t *__restrict__ kinds,
+                                    const uint64_t *__restrict__ table, const uint32_t *__restrict__ hll, int32_t nhll,
+                                    int32_t log2m, double *__restrict__ out_values, int64_t *__restrict__ out_longs,
+                                    uint8_t *__restrict__ out_hll) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ngroups; i += (int64_t)gridDim.x * blockDim.x)
+    gather_group(i, keys[i], ndense, naggs, own_count, kinds, table, hll, nhll, log2m, out_values, out_longs, out_hll);
+}
+
+// The one-round-trip variant (runtime.cpp, group-by results without a host read of the group count): the count is
+// the scan's total on the device (`d_ngroups`, offsets[nchunks]), the grid covers the key space, and the count, the
+// keys, values and exact sums land in mapped host memory (vector stores), read by the host after its one wait.
+__global__ void group_gather_mapped_kernel(const int64_t *__restrict__ keys, const int64_t *__restrict__ d_ngroups,
+                                           int64_t ndense, int32_t naggs, int32_t own_count,
+                                           const int32_t *__restrict__ kinds, const uint64_t *__restrict__ table,
+                                           int64_t *__restrict__ out_count, int64_t *__restrict__ out_keys,
+                                           double *__restrict__ out_values, int64_t *__restrict__ out_longs) {
+  const int64_t ngroups = min(*d_ngroups, ndense);
+  if (blockIdx.x == 0 && threadIdx.x == 0) out_count[0] = ngroups;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ngroups; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t key = keys[i];
+    out_keys[i] = key;
+    gather_group(i, key, ndense, naggs, own_count, kinds, table, nullptr, 0, 0, out_values, out_longs, nullptr);
   }
 }
 
@@ -1100,6 +1125,16 @@ hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t nde
   if (ngroups <= 0) return hipSuccess;
   group_gather_kernel<<<grid_for(ngroups), 256, 0, s>>>(keys, ngroups, ndense, naggs, own_count, kinds, table, hll, nhll,
                                                        log2m, vals, longs, hll_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_gather_mapped(const int64_t *keys, const int64_t *d_ngroups, int64_t ndense, int32_t naggs,
+                                      int32_t own_count, const int32_t *kinds, const uint64_t *table,
+                                      int64_t *out_count, int64_t *out_keys, double *vals, int64_t *longs,
+                                      hipStream_t s) {
+  if (ndense <= 0) return hipErrorInvalidValue;
+  group_gather_mapped_kernel<<<grid_for(ndense), 256, 0, s>>>(keys, d_ngroups, ndense, naggs, own_count, kinds, table,
+                                                              out_count, out_keys, vals, longs);
   return hipGetLastError();
 }
 

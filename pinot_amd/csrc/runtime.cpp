@@ -72,6 +72,10 @@ hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t
 hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t ndense, int32_t naggs, int32_t own_count,
                                const int32_t *kinds, const uint64_t *table, const uint32_t *hll, int32_t nhll,
                                int32_t log2m, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
+hipError_t launch_group_gather_mapped(const int64_t *keys, const int64_t *d_ngroups, int64_t ndense, int32_t naggs,
+                                      int32_t own_count, const int32_t *kinds, const uint64_t *table,
+                                      int64_t *out_count, int64_t *out_keys, double *vals, int64_t *longs,
+                                      hipStream_t s);
 hipError_t launch_select_count(const DevSelQuery *q, int64_t total_work, int64_t *tile_cnt, hipStream_t s);
 hipError_t launch_select_scan(void *temp, size_t *temp_bytes, const int64_t *in, int64_t *out, int64_t n, hipStream_t s);
 hipError_t launch_select_bases(const DevSelQuery *q, int64_t *seg_base, int64_t *kept, int64_t *total, hipStream_t s);
@@ -1339,6 +1343,7 @@ struct Plan {
     for (void *p : allocs) (void)hipFree(p);
     if (pinned) (void)hipHostFree(pinned);
     if (pstage) (void)hipHostFree(pstage);
+    if (gb_pinned) (void)hipHostFree(gb_pinned);
   }
   // configuration
   DevAggQuery dq;
@@ -1380,6 +1385,9 @@ struct Plan {
   // pinned host landing area for the per-execution results: finals[64] | seg_matched[nmatch] | hll
   uint64_t *pinned = nullptr;
   uint64_t *pinned_dev = nullptr;  // the same memory as the device addresses it
+  // group-by results in one round trip (execute, group_gather_mapped_kernel): count | keys | values | exact sums
+  // for the whole key space, mapped; made on the first execution that takes that path
+  uint8_t *gb_pinned = nullptr, *gb_pinned_dev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   bool graph_failed = false;
   int executions = 0;
@@ -3515,10 +3523,49 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     rc = ws.get("gb_offsets", (size_t)(nchunks + 1) * 8, &offs);
     if (rc) return rc;
     HIP_TRY(launch_group_count((const uint64_t *)gtab, dq.num_groups, (int32_t *)cc, nchunks, (int64_t *)offs, st));
-    int64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    ngroups = total;
+    // One round trip when neither numGroupsLimit nor the trim can apply whatever the group count is (key space below
+    // both) and the key space's rows fit the mapped landing area: compaction, gather and the count run back to back
+    // and write the results into mapped host memory, so the host neither waits for the count nor copies the outputs
+    // (a wait + a copy command less per group-by query). Dense tables without HLL registers only (byte registers
+    // would cross PCIe one byte store at a time); PHIP_GB_ONE_TRIP_MAX = the landing area's bytes, 0 = off.
+    static const int64_t one_trip_max = [] {
+      const char *e = getenv("PHIP_GB_ONE_TRIP_MAX");
+      return e ? (int64_t)atoll(e) : (int64_t)16 << 20;
+    }();
+    const int64_t ndense = dq.num_groups;
+    const int64_t one_trip_bytes = 64 + ndense * (8 + 16 * (int64_t)naggs);
+    const bool one_trip = mode == EXEC_FULL && dq.mode != GB_HASH && nhll == 0 && ndense > 0 &&
+                          (P.num_groups_limit <= 0 || ndense < P.num_groups_limit) &&
+                          (P.trim_size <= 0 || ndense <= P.trim_size) && one_trip_bytes <= one_trip_max;
+    if (one_trip) {
+      if (!P.gb_pinned) {
+        void *h = nullptr, *dp = nullptr;
+        HIP_TRY(hipHostMalloc(&h, (size_t)one_trip_bytes, hipHostMallocMapped));
+        P.gb_pinned = (uint8_t *)h;
+        HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
+        P.gb_pinned_dev = (uint8_t *)dp;
+      }
+      void *dkeys;
+      if ((rc = ws.get("gb_keys", (size_t)ndense * 8, &dkeys))) return rc;
+      uint8_t *hd = P.gb_pinned_dev;
+      const size_t vb_max = (size_t)ndense * naggs * 8;
+      HIP_TRY(launch_group_compact((const uint64_t *)gtab, ndense, (const int64_t *)offs, nchunks, (int64_t *)dkeys, st));
+      HIP_TRY(launch_group_gather_mapped((const int64_t *)dkeys, (const int64_t *)offs + nchunks, ndense, naggs,
+                                         dq.own_count_rows, gather_kinds, (const uint64_t *)gtab, (int64_t *)hd,
+                                         (int64_t *)(hd + 64), (double *)(hd + 64 + ndense * 8),
+                                         (int64_t *)(hd + 64 + ndense * 8 + vb_max), st));
+      if (P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const uint8_t *h = P.gb_pinned;
+      memcpy(&ngroups, h, 8);
+      if (ngroups < 0 || ngroups > ndense)
+        return fail(PHIP_ERR_HIP, "group count %lld outside the key space %lld", (long long)ngroups, (long long)ndense);
+    } else {
+      int64_t total = 0;
+      HIP_TRY(hipMemcpyAsync(&total, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      ngroups = total;
+    }
     if (mode == EXEC_PARTIAL) {
       // per-segment numGroupsLimit needs the first-seen record pass of phip_plan_execute
       if (P.num_groups_limit > 0 && ngroups >= P.num_groups_limit)
@@ -3560,7 +3607,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       return PHIP_OK;
     };
     bool out_contig = false;
-    if (!limit_pass) {
+    if (!limit_pass && !one_trip) {
       rc = contiguous_out("gb_out", ngroups, &keys, &ov, &ol, &oh);
       if (rc) return rc;
       out_contig = true;
@@ -3628,7 +3675,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     impl->hll.resize((size_t)ngroups * nhll * m_regs);
     const size_t kb = (size_t)ngroups * 8, vb = (size_t)ngroups * naggs * 8, hb = impl->hll.size();
     std::vector<uint8_t> staged;
-    if (ngroups && out_contig) {  // one copy of the contiguous outputs (each small copy is its own command)
+    if (one_trip) {  // (already waited for: the outputs are in the mapped landing area)
+      const uint8_t *h = P.gb_pinned + 64;
+      memcpy(hkeys.data(), h, kb);
+      if (vb) {
+        memcpy(impl->values.data(), h + ndense * 8, vb);
+        memcpy(impl->longs.data(), h + ndense * 8 + (size_t)ndense * naggs * 8, vb);
+      }
+    } else if (ngroups && out_contig) {  // one copy of the contiguous outputs (each small copy is its own command)
       staged.resize(kb + 2 * vb + hb);
       HIP_TRY(hipMemcpyAsync(staged.data(), keys, staged.size(), hipMemcpyDeviceToHost, st));
     } else if (ngroups) {
@@ -3639,8 +3693,10 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       }
       if (nhll) HIP_TRY(hipMemcpyAsync(impl->hll.data(), oh, impl->hll.size(), hipMemcpyDeviceToHost, st));
     }
-    if (P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if (!one_trip) {
+      if (P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
+      HIP_TRY(hipStreamSynchronize(st));
+    }
     if (!staged.empty()) {
       memcpy(hkeys.data(), staged.data(), kb);
       if (vb) {
