@@ -3528,10 +3528,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     // and write the results into mapped host memory, so the host neither waits for the count nor copies the outputs
     // (a wait + a copy command less per group-by query). Dense tables without HLL registers only (byte registers
     // would cross PCIe one byte store at a time); PHIP_GB_ONE_TRIP_MAX = the landing area's bytes, 0 = off.
-    static const int64_t one_trip_max = [] {
-      const char *e = getenv("PHIP_GB_ONE_TRIP_MAX");
-      return e ? (int64_t)atoll(e) : (int64_t)16 << 20;
-    }();
+    const char *otm = getenv("PHIP_GB_ONE_TRIP_MAX");  // (read per execution: A/B inside one process)
+    const int64_t one_trip_max = otm ? (int64_t)atoll(otm) : (int64_t)16 << 20;
     const int64_t ndense = dq.num_groups;
     const int64_t one_trip_bytes = 64 + ndense * (8 + 16 * (int64_t)naggs);
     const bool one_trip = mode == EXEC_FULL && dq.mode != GB_HASH && nhll == 0 && ndense > 0 &&
