@@ -1008,13 +1008,25 @@ __global__ void group_gather_mapped_kernel(const int64_t *__restrict__ keys, con
                                            int64_t ndense, int32_t naggs, int32_t own_count,
                                            const int32_t *__restrict__ kinds, const uint64_t *__restrict__ table,
                                            int64_t *__restrict__ out_count, int64_t *__restrict__ out_keys,
-                                           double *__restrict__ out_values, int64_t *__restrict__ out_longs) {
+                                           double *__restrict__ out_values, int64_t *__restrict__ out_longs,
+                                           const uint32_t *__restrict__ hll, int32_t nhll, int32_t log2m,
+                                           uint32_t *__restrict__ out_hll) {
   const int64_t ngroups = min(*d_ngroups, ndense);
-  if (blockIdx.x == 0 && threadIdx.x == 0) out_count[0] = ngroups;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ngroups; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t0 == 0) out_count[0] = ngroups;
+  for (int64_t i = t0; i < ngroups; i += stride) {
     const int64_t key = keys[i];
     out_keys[i] = key;
     gather_group(i, key, ndense, naggs, own_count, kinds, table, nullptr, 0, 0, out_values, out_longs, nullptr);
+  }
+  // HLL registers (u32 per register in the table, < 64): four packed per 4-B store, one 16-B load each, so the
+  // registers cross to host memory a word, not a byte, at a time
+  const int64_t q = (int64_t)nhll << (log2m - 2);  // packed words per group
+  for (int64_t w = t0; w < ngroups * q; w += stride) {
+    const int64_t i = w / q, r = w - i * q;
+    const int64_t h = r >> (log2m - 2), j = (r & ((1 << (log2m - 2)) - 1)) << 2;
+    const uint4 v = *(const uint4 *)(hll + ((h * ndense + keys[i]) << log2m) + j);
+    out_hll[w] = (v.x & 0xFFu) | ((v.y & 0xFFu) << 8) | ((v.z & 0xFFu) << 16) | ((v.w & 0xFFu) << 24);
   }
 }
 
@@ -1131,10 +1143,13 @@ hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t nde
 hipError_t launch_group_gather_mapped(const int64_t *keys, const int64_t *d_ngroups, int64_t ndense, int32_t naggs,
                                       int32_t own_count, const int32_t *kinds, const uint64_t *table,
                                       int64_t *out_count, int64_t *out_keys, double *vals, int64_t *longs,
+                                      const uint32_t *hll, int32_t nhll, int32_t log2m, uint32_t *hll_out,
                                       hipStream_t s) {
-  if (ndense <= 0) return hipErrorInvalidValue;
-  group_gather_mapped_kernel<<<grid_for(ndense), 256, 0, s>>>(keys, d_ngroups, ndense, naggs, own_count, kinds, table,
-                                                              out_count, out_keys, vals, longs);
+  if (ndense <= 0 || (nhll > 0 && (log2m < 4 || log2m > 16))) return hipErrorInvalidValue;
+  const int64_t work = std::max<int64_t>(ndense, nhll > 0 ? ndense * ((int64_t)nhll << (log2m - 2)) : 0);
+  group_gather_mapped_kernel<<<grid_for(work), 256, 0, s>>>(keys, d_ngroups, ndense, naggs, own_count, kinds, table,
+                                                            out_count, out_keys, vals, longs, hll, nhll, log2m,
+                                                            hll_out);
   return hipGetLastError();
 }
 

@@ -75,6 +75,7 @@ hipError_t launch_group_gather(const int64_t *keys, int64_t ngroups, int64_t nde
 hipError_t launch_group_gather_mapped(const int64_t *keys, const int64_t *d_ngroups, int64_t ndense, int32_t naggs,
                                       int32_t own_count, const int32_t *kinds, const uint64_t *table,
                                       int64_t *out_count, int64_t *out_keys, double *vals, int64_t *longs,
+                                      const uint32_t *hll, int32_t nhll, int32_t log2m, uint32_t *hll_out,
                                       hipStream_t s);
 hipError_t launch_select_count(const DevSelQuery *q, int64_t total_work, int64_t *tile_cnt, hipStream_t s);
 hipError_t launch_select_scan(void *temp, size_t *temp_bytes, const int64_t *in, int64_t *out, int64_t n, hipStream_t s);
@@ -3526,13 +3527,16 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     // One round trip when neither numGroupsLimit nor the trim can apply whatever the group count is (key space below
     // both) and the key space's rows fit the mapped landing area: compaction, gather and the count run back to back
     // and write the results into mapped host memory, so the host neither waits for the count nor copies the outputs
-    // (a wait + a copy command less per group-by query). Dense tables without HLL registers only (byte registers
-    // would cross PCIe one byte store at a time); PHIP_GB_ONE_TRIP_MAX = the landing area's bytes, 0 = off.
+    // (a wait + a copy command less per group-by query). HLL registers cross packed four to a word
+    // (PHIP_GB_ONE_TRIP_HLL=0: those plans keep the two trips); PHIP_GB_ONE_TRIP_MAX = the landing area's bytes,
+    // 0 = off.
     const char *otm = getenv("PHIP_GB_ONE_TRIP_MAX");  // (read per execution: A/B inside one process)
     const int64_t one_trip_max = otm ? (int64_t)atoll(otm) : (int64_t)16 << 20;
     const int64_t ndense = dq.num_groups;
-    const int64_t one_trip_bytes = 64 + ndense * (8 + 16 * (int64_t)naggs);
-    const bool one_trip = mode == EXEC_FULL && dq.mode != GB_HASH && nhll == 0 && ndense > 0 &&
+    const char *oth = getenv("PHIP_GB_ONE_TRIP_HLL");
+    const bool one_trip_hll = !oth || atoi(oth) != 0;
+    const int64_t one_trip_bytes = 64 + ndense * (8 + 16 * (int64_t)naggs + (int64_t)nhll * m_regs);
+    const bool one_trip = mode == EXEC_FULL && dq.mode != GB_HASH && (nhll == 0 || one_trip_hll) && ndense > 0 &&
                           (P.num_groups_limit <= 0 || ndense < P.num_groups_limit) &&
                           (P.trim_size <= 0 || ndense <= P.trim_size) && one_trip_bytes <= one_trip_max;
     if (one_trip) {
@@ -3551,7 +3555,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       HIP_TRY(launch_group_gather_mapped((const int64_t *)dkeys, (const int64_t *)offs + nchunks, ndense, naggs,
                                          dq.own_count_rows, gather_kinds, (const uint64_t *)gtab, (int64_t *)hd,
                                          (int64_t *)(hd + 64), (double *)(hd + 64 + ndense * 8),
-                                         (int64_t *)(hd + 64 + ndense * 8 + vb_max), st));
+                                         (int64_t *)(hd + 64 + ndense * 8 + vb_max), (const uint32_t *)ghll, nhll,
+                                         log2m, (uint32_t *)(hd + 64 + ndense * 8 + 2 * vb_max), st));
       if (P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
       HIP_TRY(hipStreamSynchronize(st));
       const uint8_t *h = P.gb_pinned;
@@ -3680,6 +3685,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         memcpy(impl->values.data(), h + ndense * 8, vb);
         memcpy(impl->longs.data(), h + ndense * 8 + (size_t)ndense * naggs * 8, vb);
       }
+      if (hb) memcpy(impl->hll.data(), h + ndense * 8 + 2 * (size_t)ndense * naggs * 8, hb);
     } else if (ngroups && out_contig) {  // one copy of the contiguous outputs (each small copy is its own command)
       staged.resize(kb + 2 * vb + hb);
       HIP_TRY(hipMemcpyAsync(staged.data(), keys, staged.size(), hipMemcpyDeviceToHost, st));

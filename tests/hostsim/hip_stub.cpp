@@ -141,11 +141,14 @@ hipError_t launch_group_gather(const int64_t *, int64_t ng, int64_t, int32_t nag
 }
 hipError_t launch_group_gather_mapped(const int64_t *keys, const int64_t *d_ng, int64_t ndense, int32_t naggs, int32_t,
                                       const int32_t *, const uint64_t *, int64_t *count, int64_t *ok, double *v,
-                                      int64_t *l, hipStream_t) {
+                                      int64_t *l, const uint32_t *, int32_t nhll, int32_t log2m, uint32_t *hout,
+                                      hipStream_t) {
   const int64_t ng = *d_ng < ndense ? *d_ng : ndense;
   *count = ng;
   for (int64_t i = 0; i < ng; i++) ok[i] = keys[i];
   for (int64_t i = 0; i < ng * naggs; i++) { v[i] = 0.25 + (double)i; l[i] = 1000 + i; }  // the gather's pattern
+  uint8_t *h = (uint8_t *)hout;
+  if (nhll) for (int64_t i = 0; i < ng * nhll * (1 << log2m); i++) h[i] = (uint8_t)(i * 3 + 1);
   return hipSuccess;
 }
 hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hipStream_t) {

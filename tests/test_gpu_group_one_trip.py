@@ -1,7 +1,8 @@
 """Group-by results in one round trip (runtime.cpp one_trip / aggregate.hip group_gather_mapped_kernel): when neither
 numGroupsLimit nor the trim can apply and the key space's rows fit the mapped landing area, the group count, keys,
-values and exact sums come back through mapped host memory without a wait for the count. Both paths
-(PHIP_GB_ONE_TRIP_MAX=0 forces the two-trip one) must give the oracle's groups: every aggregation kind, several keys,
+values, exact sums and HLL registers come back through mapped host memory without a wait for the count. Both paths
+(PHIP_GB_ONE_TRIP_MAX=0 forces the two-trip one, PHIP_GB_ONE_TRIP_HLL=0 for plans with registers) must give the
+oracle's groups: every aggregation kind, registers bit-exact, several keys,
 an empty result, a key space right at the landing area's size limit, and a plan executed repeatedly (the landing
 area is reused)."""
 import numpy as np
@@ -20,6 +21,8 @@ QUERIES = [
     "SELECT s, SUM(d) FROM t WHERE f > 1000 GROUP BY s LIMIT 100",                     # nothing matches
     "SELECT g, SUM(v) FILTER (WHERE f < 10), COUNT(*) FROM t GROUP BY g LIMIT 1000",
     "SELECT g, s, MAX(d) FROM t WHERE s <> 'b3' GROUP BY g, s ORDER BY g, s DESC LIMIT 5",
+    "SELECT g, DISTINCTCOUNTHLL(v), SUM(d) FROM t WHERE f < 70 GROUP BY g LIMIT 1000",   # registers packed 4 a word
+    "SELECT g, s, DISTINCTCOUNTHLL(f, 4), DISTINCTCOUNTHLL(s, 4), COUNT(*) FROM t GROUP BY g, s LIMIT 100000",
 ]
 
 
@@ -44,8 +47,12 @@ def segs(gpu_lib):
 
 def _run(sql, segs, monkeypatch, max_bytes, reps=1):
     from pinot_amd.engine.plan import GpuInstancePlanMaker
+    monkeypatch.delenv("PHIP_GB_ONE_TRIP_HLL", raising=False)
     if max_bytes is None:
         monkeypatch.delenv("PHIP_GB_ONE_TRIP_MAX", raising=False)
+    elif max_bytes == "no-hll":
+        monkeypatch.delenv("PHIP_GB_ONE_TRIP_MAX", raising=False)
+        monkeypatch.setenv("PHIP_GB_ONE_TRIP_HLL", "0")
     else:
         monkeypatch.setenv("PHIP_GB_ONE_TRIP_MAX", str(max_bytes))
     raws, gs = segs
@@ -56,7 +63,7 @@ def _run(sql, segs, monkeypatch, max_bytes, reps=1):
     return qc, blks, executor.execute(qc, raws)
 
 
-@pytest.mark.parametrize("max_bytes", [None, 0])
+@pytest.mark.parametrize("max_bytes", [None, 0, "no-hll"])
 @pytest.mark.parametrize("sql", QUERIES)
 def test_gpu_group_one_trip(sql, max_bytes, segs, monkeypatch):
     from pinot_amd.engine.reduce import reduce_blocks
