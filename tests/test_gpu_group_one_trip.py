@@ -88,3 +88,33 @@ def test_gpu_group_one_trip_size_limit(slack, segs, monkeypatch):
     sql = "SELECT g, s, SUM(v), COUNT(*) FROM t GROUP BY g, s LIMIT 100000"
     qc, blks, (oblk, exact) = _run(sql, segs, monkeypatch, need + slack)
     _check(qc, blks[0], oblk, exact)
+
+
+@pytest.fixture(scope="module")
+def wide(gpu_lib):
+    from pinot_amd.engine.segment import GpuSegment
+    rng = np.random.default_rng(17)
+    n = 120_000
+    c = SegmentCreator("otw")
+    c.add_column("a", DataType.INT, rng.integers(0, 20_000, n))   # ~20K groups: above trimSize 5000, below 100K
+    c.add_column("m", DataType.LONG, rng.integers(-10 ** 9, 10 ** 9, n))
+    c.add_column("f", DataType.INT, rng.integers(0, 100, n))
+    raw = c.build()
+    g = GpuSegment(raw)
+    yield [raw], [g]
+    g.destroy()
+
+
+@pytest.mark.parametrize("max_bytes", [None, 0])
+@pytest.mark.parametrize("sql", ["SELECT a, SUM(m) FROM t WHERE f < 90 GROUP BY a ORDER BY SUM(m) DESC LIMIT 10",
+                                 "SELECT a, COUNT(*) FROM t GROUP BY a ORDER BY a DESC LIMIT 7"])
+def test_gpu_group_one_trip_trim_fallback(sql, max_bytes, wide, monkeypatch):
+    """A plan whose trim can apply goes one trip speculatively; with more groups than trimSize the compaction and
+    gather run again into device buffers and the device trim keeps its top 5000: the oracle's rows either way."""
+    from pinot_amd.engine.reduce import reduce_blocks, trim_groups
+    from tests import fixtures
+    qc, blks, (oblk, exact) = _run(sql, wide, monkeypatch, max_bytes, reps=2)
+    for blk in blks:
+        assert blk.num_groups_trimmed
+        o = trim_groups(qc, oblk)
+        assert fixtures.rows_match(reduce_blocks(qc, [blk]).rows, reduce_blocks(qc, [o]).rows)
