@@ -3536,10 +3536,11 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     const char *oth = getenv("PHIP_GB_ONE_TRIP_HLL");
     const bool one_trip_hll = !oth || atoi(oth) != 0;
     const int64_t one_trip_bytes = 64 + ndense * (8 + 16 * (int64_t)naggs + (int64_t)nhll * m_regs);
-    // (a plan whose trim can apply goes one trip too, speculatively: when the count then exceeds trimSize, the
-    // compaction and gather run again into device buffers for the trim below -- the table is still intact)
+    // (a plan whose numGroupsLimit or trim can apply goes one trip too, speculatively: when the count then reaches
+    // the limit or exceeds trimSize, the limit pass / the compaction and gather into device buffers for the trim run
+    // below as without it -- the table is still intact)
     bool one_trip = mode == EXEC_FULL && dq.mode != GB_HASH && (nhll == 0 || one_trip_hll) && ndense > 0 &&
-                    (P.num_groups_limit <= 0 || ndense < P.num_groups_limit) && one_trip_bytes <= one_trip_max;
+                    one_trip_bytes <= one_trip_max;
     if (one_trip) {
       if (!P.gb_pinned) {
         void *h = nullptr, *dp = nullptr;
@@ -3566,6 +3567,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         return fail(PHIP_ERR_HIP, "group count %lld outside the key space %lld", (long long)ngroups, (long long)ndense);
       if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0 || P.order_terms.num_terms > 0))
         one_trip = false;  // the trim needs the outputs on the device
+      if (P.num_groups_limit > 0 && ngroups >= P.num_groups_limit) one_trip = false;  // the limit pass decides
     } else {
       int64_t total = 0;
       HIP_TRY(hipMemcpyAsync(&total, (int64_t *)offs + nchunks, 8, hipMemcpyDeviceToHost, st));
