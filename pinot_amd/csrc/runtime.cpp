@@ -224,6 +224,7 @@ struct Workspace {
   };
   std::map<std::string, Buf> dev;
   std::map<std::string, Buf> host;  // pinned
+  std::map<std::string, std::pair<Buf, void *>> mapped;  // pinned, device-visible (+ its device address)
 
   int32_t get(const std::string &name, size_t bytes, void **out) {
     Buf &b = dev[name];
@@ -247,7 +248,25 @@ struct Workspace {
     *out = b.p;
     return PHIP_OK;
   }
+  int32_t get_mapped(const std::string &name, size_t bytes, void **host_out, void **dev_out) {
+    auto &e = mapped[name];
+    if (e.first.cap < bytes) {
+      if (e.first.p) (void)hipHostFree(e.first.p);
+      e.first.p = nullptr;
+      e.first.cap = 0;
+      size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
+      HIP_TRY(hipHostMalloc(&e.first.p, cap, hipHostMallocMapped));
+      e.first.cap = cap;
+      HIP_TRY(hipHostGetDevicePointer(&e.second, e.first.p, 0));
+    }
+    *host_out = e.first.p;
+    *dev_out = e.second;
+    return PHIP_OK;
+  }
   void release() {
+    for (auto &kv : mapped)
+      if (kv.second.first.p) (void)hipHostFree(kv.second.first.p);
+    mapped.clear();
     for (auto &kv : dev)
       if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto &kv : host)
@@ -1344,7 +1363,6 @@ struct Plan {
     for (void *p : allocs) (void)hipFree(p);
     if (pinned) (void)hipHostFree(pinned);
     if (pstage) (void)hipHostFree(pstage);
-    if (gb_pinned) (void)hipHostFree(gb_pinned);
   }
   // configuration
   DevAggQuery dq;
@@ -1386,9 +1404,6 @@ struct Plan {
   // pinned host landing area for the per-execution results: finals[64] | seg_matched[nmatch] | hll
   uint64_t *pinned = nullptr;
   uint64_t *pinned_dev = nullptr;  // the same memory as the device addresses it
-  // group-by results in one round trip (execute, group_gather_mapped_kernel): count | keys | values | exact sums
-  // for the whole key space, mapped; made on the first execution that takes that path
-  uint8_t *gb_pinned = nullptr, *gb_pinned_dev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   bool graph_failed = false;
   int executions = 0;
@@ -3524,14 +3539,13 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     rc = ws.get("gb_offsets", (size_t)(nchunks + 1) * 8, &offs);
     if (rc) return rc;
     HIP_TRY(launch_group_count((const uint64_t *)gtab, dq.num_groups, (int32_t *)cc, nchunks, (int64_t *)offs, st));
-    // One round trip when neither numGroupsLimit nor the trim can apply whatever the group count is (key space below
-    // both) and the key space's rows fit the mapped landing area: compaction, gather and the count run back to back
-    // and write the results into mapped host memory, so the host neither waits for the count nor copies the outputs
-    // (a wait + a copy command less per group-by query). HLL registers cross packed four to a word
-    // (PHIP_GB_ONE_TRIP_HLL=0: those plans keep the two trips); PHIP_GB_ONE_TRIP_MAX = the landing area's bytes,
-    // 0 = off.
+    // One round trip when the key space's rows fit the lane's mapped landing area (default up to 64 MiB): compaction,
+    // gather and the count run back to back and write the results into mapped host memory, so the host neither waits
+    // for the count nor copies the outputs (a wait + a copy command less per group-by query). HLL registers cross
+    // packed four to a word (PHIP_GB_ONE_TRIP_HLL=0: those plans keep the two trips); PHIP_GB_ONE_TRIP_MAX = the
+    // landing area's bytes, 0 = off.
     const char *otm = getenv("PHIP_GB_ONE_TRIP_MAX");  // (read per execution: A/B inside one process)
-    const int64_t one_trip_max = otm ? (int64_t)atoll(otm) : (int64_t)16 << 20;
+    const int64_t one_trip_max = otm ? (int64_t)atoll(otm) : (int64_t)64 << 20;
     const int64_t ndense = dq.num_groups;
     const char *oth = getenv("PHIP_GB_ONE_TRIP_HLL");
     const bool one_trip_hll = !oth || atoi(oth) != 0;
@@ -3541,17 +3555,16 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     // below as without it -- the table is still intact)
     bool one_trip = mode == EXEC_FULL && dq.mode != GB_HASH && (nhll == 0 || one_trip_hll) && ndense > 0 &&
                     one_trip_bytes <= one_trip_max;
+    const uint8_t *landing = nullptr;
     if (one_trip) {
-      if (!P.gb_pinned) {
-        void *h = nullptr, *dp = nullptr;
-        HIP_TRY(hipHostMalloc(&h, (size_t)one_trip_bytes, hipHostMallocMapped));
-        P.gb_pinned = (uint8_t *)h;
-        HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
-        P.gb_pinned_dev = (uint8_t *)dp;
-      }
+      // the lane's landing area (count | keys | values | exact sums | registers over the whole key space), grown on
+      // demand: read out below before the lane is released
+      void *lh = nullptr, *ld = nullptr;
+      if ((rc = ws.get_mapped("gb_landing", (size_t)one_trip_bytes, &lh, &ld))) return rc;
+      landing = (const uint8_t *)lh;
       void *dkeys;
       if ((rc = ws.get("gb_keys", (size_t)ndense * 8, &dkeys))) return rc;
-      uint8_t *hd = P.gb_pinned_dev;
+      uint8_t *hd = (uint8_t *)ld;
       const size_t vb_max = (size_t)ndense * naggs * 8;
       HIP_TRY(launch_group_compact((const uint64_t *)gtab, ndense, (const int64_t *)offs, nchunks, (int64_t *)dkeys, st));
       HIP_TRY(launch_group_gather_mapped((const int64_t *)dkeys, (const int64_t *)offs + nchunks, ndense, naggs,
@@ -3561,8 +3574,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
                                          log2m, (uint32_t *)(hd + 64 + ndense * 8 + 2 * vb_max), st));
       if (P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
       HIP_TRY(hipStreamSynchronize(st));
-      const uint8_t *h = P.gb_pinned;
-      memcpy(&ngroups, h, 8);
+      memcpy(&ngroups, landing, 8);
       if (ngroups < 0 || ngroups > ndense)
         return fail(PHIP_ERR_HIP, "group count %lld outside the key space %lld", (long long)ngroups, (long long)ndense);
       if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0 || P.order_terms.num_terms > 0))
@@ -3684,7 +3696,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     const size_t kb = (size_t)ngroups * 8, vb = (size_t)ngroups * naggs * 8, hb = impl->hll.size();
     std::vector<uint8_t> staged;
     if (one_trip) {  // (already waited for: the outputs are in the mapped landing area)
-      const uint8_t *h = P.gb_pinned + 64;
+      const uint8_t *h = landing + 64;
       memcpy(hkeys.data(), h, kb);
       if (vb) {
         memcpy(impl->values.data(), h + ndense * 8, vb);
