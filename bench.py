@@ -39,7 +39,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROUND = "r04"
+ROUND = "r05"
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def load_layout(ssb, seg_per_gpu, world, rank, cols, seed, layout, keep_host):
@@ -163,6 +168,148 @@ def check_parity(queries, qcs, answers, raws, dist, torch):
     return ok, detail
 
 
+GROUP_BY_LEGS = {"c3": ["Q2.1", "Q2.2", "Q2.3", "Q3.1", "Q3.2", "Q3.3", "Q3.4", "Q4.1", "Q4.2", "Q4.3"],
+                 "c5": ["C5"]}
+
+
+def _same_value(got, want):
+    """An exact int64 SUM intermediate (int) against the CPU's exact sum; a double one must equal it exactly too
+    (the sums here are integral and below 2^53, where the reference's double holder is exact)."""
+    if isinstance(got, (int, np.integer)):
+        return int(got) == want
+    return abs(want) < 2 ** 53 and float(got) == float(want)
+
+
+def compare_groups(blk, cpu_groups, sum_agg, hll_agg):
+    """A GPU GroupByResultsBlock against cpu_baseline.PreparedGroupBy.groups: the same key tuples, every SUM equal,
+    every HLL register equal. Returns (equal, first mismatch or None)."""
+    if set(blk.groups) != set(cpu_groups):
+        extra = sorted(set(blk.groups) - set(cpu_groups), key=str)[:2]
+        miss = sorted(set(cpu_groups) - set(blk.groups), key=str)[:2]
+        return False, f"group sets differ: {len(blk.groups)} vs {len(cpu_groups)}, gpu-only {extra}, cpu-only {miss}"
+    for k, (s, _, regs) in cpu_groups.items():
+        g = blk.groups[k]
+        if sum_agg is not None and not _same_value(g[sum_agg], s):
+            return False, f"SUM of {k}: {g[sum_agg]} vs {s}"
+        if hll_agg is not None and not np.array_equal(np.asarray(g[hll_agg], dtype=np.uint8), regs):
+            return False, f"HLL registers of {k} differ"
+    return True, None
+
+
+def check_merged_group_by(qc, blk, raws, dist):
+    """The cross-GPU merged group-by block (every rank holds it) against oracle/cpu_scan.c over ALL ranks'
+    segments: each rank runs the CPU group-by over its own segments, the value-keyed groups are gathered and merged
+    (sums and counts added, registers max-ed: the reference's combine merge), and each rank compares. Returns
+    "checked" when every rank's block equals the merged CPU answer (one MIN all-reduce), else the first mismatch."""
+    import torch
+    from oracle import cpu_baseline
+    p = cpu_baseline.PreparedGroupBy(qc, raws)
+    out = p.run(cpu_baseline.usable_cpus()[0])
+    mine = (p.groups(out), out[3])
+    parts = [mine]
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, mine)
+    merged, docs = {}, 0
+    for groups, d in parts:
+        docs += d
+        for k, (s, c, regs) in groups.items():
+            if k in merged:
+                s0, c0, r0 = merged[k]
+                merged[k] = (None if s is None else s0 + s, c0 + c, None if regs is None else np.maximum(r0, regs))
+            else:
+                merged[k] = (s, c, regs)
+    good, why = compare_groups(blk, merged, p.sum_agg, p.hll_agg)
+    if good and blk.stats.num_docs_scanned != docs:
+        good, why = False, f"numDocsScanned {blk.stats.num_docs_scanned} vs {docs}"
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([1 if good else 0], dtype=torch.int64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if good and not bool(t.item()):
+            good, why = False, "another rank's merged block differs"
+    return "checked" if good else f"MISMATCH: {why}"
+
+
+def run_group_by(args, dist, leg, gsegs, raws, torch, want_cpu):
+    """BASELINE C3 (SSB Q2.x-Q4.x, multi-column GROUP BY) / the C5 query over this rank's resident segments, each
+    query prepared once and run warmup + steps times; then one more execution per query, outside the timed region,
+    checked bit-exactly against oracle/cpu_scan.c's group-by over the same segments (group set, exact SUMs, HLL
+    registers, numDocsScanned). Per query: p50 latency, kernel times and each kernel's algorithmic-byte frac.
+    At N > 1 the queries run over the rank's own segments (the merged C5 is "c5_merged")."""
+    from oracle import cpu_baseline
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    from pinot_amd.query.sql import parse
+    from tools import ssb
+    queries = GROUP_BY_LEGS[leg]
+    qcs = {q: parse(ssb.SSB_QUERIES[q]) for q in queries}
+    pm = GpuInstancePlanMaker()
+    ops = {q: pm.make_instance_plan(qcs[q], gsegs) for q in queries}
+    for _ in range(args.warmup):
+        for q in queries:
+            ops[q].next_block()
+    lat = {q: [] for q in queries}
+    ks = {q: [] for q in queries}
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for q in queries:
+            ts = time.perf_counter()
+            blk = ops[q].next_block()
+            lat[q].append((time.perf_counter() - ts) * 1e3)
+            ks[q].append((blk.filter_kernel_ms, blk.agg_kernel_ms, blk.filter_bytes, blk.agg_bytes))
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    answers = {q: ops[q].next_block() for q in queries}
+    for op in ops.values():
+        op.close()
+    rows = sum(s.num_docs for s in gsegs)
+    threads = cpu_baseline.usable_cpus()[0]
+    per_q = {}
+    ok = True
+    for q in queries:
+        k = np.asarray(ks[q], dtype=np.float64)
+        fms, ams = float(k[:, 0].mean()), float(k[:, 1].mean())
+        fb, ab = float(k[:, 2].mean()), float(k[:, 3].mean())
+        blk = answers[q]
+        d = {"p50_ms": round(float(np.median(lat[q])), 4), "groups": len(blk.groups),
+             "docs_scanned": blk.stats.num_docs_scanned,
+             "filter_ms": round(fms, 4), "agg_ms": round(ams, 4),
+             "filter_frac": round(fb / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if fms > 0 else None,
+             "agg_frac": round(ab / (ams * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if ams > 0 else None,
+             "filter_bytes": int(fb), "agg_bytes": int(ab)}
+        if not args.no_parity:
+            p = cpu_baseline.PreparedGroupBy(qcs[q], raws)
+            out = p.run(threads)
+            good, why = compare_groups(blk, p.groups(out), p.sum_agg, p.hll_agg)
+            good = good and out[3] == blk.stats.num_docs_scanned
+            if why is None and not good:
+                why = f"numDocsScanned {blk.stats.num_docs_scanned} vs {out[3]}"
+            d["parity"] = "equal" if good else f"MISMATCH: {why}"
+            ok &= good
+        per_q[q] = d
+    res = {"queries": {q: ssb.SSB_QUERIES[q] for q in queries},
+           "rows_per_query": rows, "segments": len(gsegs),
+           "value": round(rows * len(queries) * args.steps / elapsed / 1e9, 3), "unit": "G rows/s",
+           "ms_per_pass": round(elapsed * 1e3 / args.steps, 4), "per_query": per_q}
+    if not args.no_parity:
+        if dist is not None:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int64,
+                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = bool(t.item())
+        res["parity"] = "checked" if ok else "MISMATCH"
+    if want_cpu:
+        v, th, reps, el = cpu_baseline.time_group_by([qcs[q] for q in queries], raws, threads,
+                                                     min_seconds=args.cpu_seconds)
+        res["cpu_baseline"] = {"value": round(v / 1e9, 4), "unit": "G rows/s", "cores": th, "kind": "port",
+                               "sample": f"restatement, not Pinot: oracle/cpu_scan.c cg_run (OpenMP dense group-by, "
+                                         f"{th} threads) running {'+'.join(queries)} over the same {len(raws)} "
+                                         f"segments, {reps} reps in {el:.1f} s"}
+    return res
+
+
 # kernel families of one query execution: a plain filter launch, a filter launch that aggregated its own tiles
 # (fused), and a separate aggregation launch.
 #
@@ -249,6 +396,10 @@ def main():
     ap.add_argument("--c5", default="auto", choices=["auto", "on", "off"],
                     help="also time the C5 query over all segments of all ranks (auto: at N > 1)")
     ap.add_argument("--queries", default="Q1.1,Q1.2,Q1.3")
+    ap.add_argument("--group-by", default="c3,c5",
+                    help="group-by legs over the headline layout's segments (BASELINE C3 = SSB Q2.x-Q4.x, C5's "
+                         "query), each parity-checked against oracle/cpu_scan.c; '' = none")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time per leg")
     ap.add_argument("--layout", default="both", choices=["sorted", "unsorted", "both"],
                     help="headline = sorted (SURVEY.md §8d C2); both also measures the unsorted layout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -285,7 +436,12 @@ def main():
     seg_per_gpu = args.segs_per_gpu or (100 if world == 1 else 125)
     head_segs = min(100, seg_per_gpu)  # C2's SF100 per GPU: weak scaling of the headline at exactly 100 per rank
     want_c5 = args.c5 == "on" or (args.c5 == "auto" and world > 1)
+    gb_legs = [g for g in args.group_by.split(",") if g]
+    for g in gb_legs:
+        if g not in GROUP_BY_LEGS:
+            raise SystemExit(f"unknown group-by leg {g}")
     cols = ssb.columns_for(queries + (["C5"] if want_c5 else []))
+    gb_cols = ssb.columns_for(queries + (["C5"] if want_c5 else []) + [q for g in gb_legs for q in GROUP_BY_LEGS[g]])
     qcs = {q: parse(ssb.SSB_QUERIES[q]) for q in queries}
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -310,17 +466,24 @@ def main():
     results = {}
     for li, layout in enumerate(layouts):
         t0 = time.time()
-        gsegs, raws = load_layout(ssb, seg_per_gpu, world, rank, cols, args.seed, layout,
-                                  keep_host=not args.no_parity or (want_cpu and li == 0))
+        gsegs, all_raws = load_layout(ssb, seg_per_gpu, world, rank, gb_cols if li == 0 else cols, args.seed, layout,
+                                      keep_host=not args.no_parity or (want_cpu and li == 0))
         load_s = time.time() - t0
+        log(f"rank {rank}: {layout} layout loaded ({len(gsegs)} segments, {len(gb_cols if li == 0 else cols)} "
+            f"columns) in {load_s:.1f} s")
         head = gsegs[:head_segs]
-        raws = raws[:head_segs]
+        raws = all_raws[:head_segs]
         rows_per_rank = sum(s.num_docs for s in head)
         elapsed, lat, kstats, answers = run_layout(args, dist, queries, qcs, head, torch)
         res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(head),
                "lat": lat, "roofline": roofline(kstats, queries, traffic, touched, layout, args.steps)}
         if not args.no_parity:
             res["parity"] = check_parity(queries, qcs, answers, raws, dist, torch)
+        log(f"rank {rank}: {layout} Q1.x timed, parity {res.get('parity', (None,))[0]}")
+        if li == 0:
+            for g in gb_legs:  # C3 / C5 over this rank's resident segments, parity-checked, own cpu_baseline
+                res[g] = run_group_by(args, dist, g, gsegs, all_raws, torch, want_cpu)
+                log(f"rank {rank}: group-by leg {g}: {res[g]['value']} G rows/s, parity {res[g].get('parity')}")
         if want_c5 and li == 0:
             qc5 = parse(ssb.SSB_QUERIES["C5"])
             el5, lat5, blk5 = run_c5(args, dist, qc5, gsegs, torch)
@@ -331,8 +494,11 @@ def main():
                          "p50_latency_ms": round(float(np.median(lat5)), 3), "groups": len(blk5.groups),
                          "merge": "distributed_block: node-global dictionaries, dense partial tables all-reduced "
                                   "in place over RCCL (int64 SUM + uint8 MAX for this query)"}
+            if not args.no_parity:
+                res["c5"]["parity"] = check_merged_group_by(qc5, blk5, all_raws, dist)
         for s in gsegs:
             s.destroy()
+        del all_raws
         if not (want_cpu and li == 0):
             del raws
         if want_cpu and li == 0:
@@ -383,14 +549,19 @@ def main():
     if "cpu" in head:
         out["cpu_baseline"] = head["cpu"]
     if not args.no_parity:
-        ok = all(results[l]["parity"][0] for l in layouts)
+        ok = all(results[l]["parity"][0] for l in layouts) and all(head[g].get("parity") == "checked" for g in gb_legs) \
+            and head.get("c5", {}).get("parity", "checked") == "checked"
         out["parity"] = "checked" if ok else "MISMATCH"
         out["parity_detail"] = {
             "against": "oracle/cpu_scan.c on the same segments, every rank, outside the timed region: exact int64 "
-                       "SUM == the CPU's (integer-valued) double SUM, numDocsScanned == its matched docs",
+                       "SUM == the CPU's (integer-valued) double SUM, numDocsScanned == its matched docs; group-by "
+                       "legs (c3, c5): the same group keys, exact SUMs and HLL registers as cpu_scan.c's dense "
+                       "group-by (per-query detail under each leg)",
             **{l: results[l]["parity"][1] for l in layouts}}
+    for g in gb_legs:
+        out[g] = head[g]
     if "c5" in head:
-        out["c5"] = head["c5"]
+        out["c5_merged" if "c5" in gb_legs else "c5"] = head["c5"]
     if len(layouts) > 1:
         r = results[layouts[1]]
         v2, ms2 = summary(r)
