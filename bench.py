@@ -493,7 +493,8 @@ def main():
                          "ms_per_query": round(el5 * 1e3 / args.steps, 3),
                          "p50_latency_ms": round(float(np.median(lat5)), 3), "groups": len(blk5.groups),
                          "merge": "distributed_block: node-global dictionaries, dense partial tables all-reduced "
-                                  "in place over RCCL (int64 SUM + uint8 MAX for this query)"}
+                                  f"in place over {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
+                                  "(int64 SUM + uint8 MAX for this query)"}
             if not args.no_parity:
                 res["c5"]["parity"] = check_merged_group_by(qc5, blk5, all_raws, dist)
         for s in gsegs:
