@@ -221,7 +221,9 @@ struct Workspace {
   struct Buf {
     void *p = nullptr;
     size_t cap = 0;
+    int32_t small_uses = 0;  // consecutive requests of < 1/4 of cap (mapped areas shrink after kShrinkAfter)
   };
+  static constexpr int32_t kShrinkAfter = 64;
   std::map<std::string, Buf> dev;
   std::map<std::string, Buf> host;  // pinned
   std::map<std::string, std::pair<Buf, void *>> mapped;  // pinned, device-visible (+ its device address)
@@ -248,8 +250,23 @@ struct Workspace {
     *out = b.p;
     return PHIP_OK;
   }
+  // A pinned, device-visible area (the group-by landing area): grown on demand, and given back to the allocator
+  // once kShrinkAfter consecutive executions on this lane needed less than a quarter of it (one large key space
+  // does not keep tens of MiB of pinned host memory per lane for the life of the process). The previous
+  // execution on the lane has been read out before the next one asks, so a reallocation never races a writer.
   int32_t get_mapped(const std::string &name, size_t bytes, void **host_out, void **dev_out) {
     auto &e = mapped[name];
+    const size_t big = (size_t)1 << 20;
+    if (e.first.cap > big && bytes < e.first.cap / 4) {
+      if (++e.first.small_uses >= kShrinkAfter) {
+        (void)hipHostFree(e.first.p);
+        e.first.p = nullptr;
+        e.first.cap = 0;
+        e.first.small_uses = 0;
+      }
+    } else {
+      e.first.small_uses = 0;
+    }
     if (e.first.cap < bytes) {
       if (e.first.p) (void)hipHostFree(e.first.p);
       e.first.p = nullptr;
@@ -1640,9 +1657,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
     if (integral && ag.function == PHIP_AGG_SUM) {
       // int64 accumulation is exact only while no partial can leave int64: bound sum |expr| over every doc
-      // from the columns' value ranges. Past 2^62 the SUM takes the reference's own double accumulation
+      // from the columns' value ranges. Past 2^58 the SUM takes the reference's own double accumulation
       // (SumAggregationFunction.java:76-101; MultiplicationTransformFunction computes 1.0*a*b in double),
-      // which cannot wrap.
+      // which cannot wrap. (2^58, not 2^62: the cross-GPU merge all-reduces the exact partials of up to
+      // kMaxExactRanks = 16 GPUs as int64 SUM, distributed.allreduce_*, and 16 x 2^58 = 2^62 cannot wrap either.)
       long double bound = 0;
       for (int s = 0; s < nseg && integral; s++) {
         const ColumnStore &ca = segs[s]->cols[colidx[s][ag.column_a]];
@@ -1656,7 +1674,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         }
         bound += e * (long double)segs[s]->num_docs;
       }
-      if (bound >= (long double)((int64_t)1 << 62)) integral = false;
+      if (bound >= (long double)((int64_t)1 << 58)) integral = false;
     }
     d.integral = integral;
     d.acc = acc_kind_for(ag, integral);
@@ -2733,8 +2751,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // their XCD's eighth of the work (its dictionaries then stay in that XCD's L2)
   int xcd_walk = fused_naggs > 0 ? 2 : 0;
   if (walk_env) xcd_walk = !strcmp(walk_env, "xcd") ? 1 : (!strcmp(walk_env, "xcdc") ? 2 : 0);
+  int64_t min_tiles_per_wave = 1;
+  if (const char *mt = getenv("PHIP_FILTER_MIN_TILES")) min_tiles_per_wave = std::max(1, atoi(mt));  // A/B
   int filter_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)dev->num_cus * fbpc,
-                                                                  ceil_div(total_work, kFilterWaves)));
+                                                                  ceil_div(total_work, kFilterWaves * min_tiles_per_wave)));
   if (xcd_walk) filter_blocks = (int)round_up(std::max(filter_blocks, 8), 8);
 
   // ---- aggregation kernel configuration (aggregate.hip) -----------------------------------------

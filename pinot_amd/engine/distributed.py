@@ -561,6 +561,9 @@ def allreduce_aggregation_partial(part, dist, group=None, any_f64=None):
     part.stats_dev = None  # (phip_plan_finish takes the host statistics)
 
 
+MAX_EXACT_RANKS = 16  # runtime.cpp: exact int64 SUMs are bounded by 2^58 per GPU, 16 x 2^58 = 2^62
+
+
 def distributed_block(op, dist=None, group=None, fallback_op=None):
     """This rank's share of a query merged with every other rank's; every rank returns the merged block.
 
@@ -590,7 +593,12 @@ def distributed_block(op, dist=None, group=None, fallback_op=None):
     dev = _device(dist, group)
     shape = [0, 0, 0] if part is None or not part.global_keys else [1, part.num_groups, part.num_rows]
     nrow = _lib.PARTIAL_MAX_ROWS
-    f64 = [1 if shape[0] and r < part.num_rows and part.row_kinds[r] == _lib.ROW_SUM_F64 else 0 for r in range(nrow)]
+    # an exact int64 partial is bounded by 2^58 per GPU (the library's plan-time bound), so the int64 SUM of up to
+    # MAX_EXACT_RANKS of them cannot wrap; past that every SUM row merges in double (the reference's own type)
+    wide = dist.get_world_size(group) > MAX_EXACT_RANKS
+    f64 = [1 if shape[0] and r < part.num_rows and (part.row_kinds[r] == _lib.ROW_SUM_F64 or
+                                                    (wide and part.row_kinds[r] == _lib.ROW_SUM_I64)) else 0
+           for r in range(nrow)]
     v = torch.tensor([1 if err is not None else 0, 1 - shape[0], shape[1], shape[2], -shape[1], -shape[2]] + f64,
                      dtype=torch.int64, device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)

@@ -259,6 +259,10 @@ def _three_valued(seg: GpuSegment, fc: FilterContext):
         if pred.type in ("IS_NULL", "IS_NOT_NULL") or not seg.has_null_vector(pred.column):
             return p, _fold_not(p), None
         n, nn = _null_leaf(seg, pred.column), _null_leaf(seg, pred.column, True)
+        if not seg.column_metadata(pred.column).has_dictionary:
+            # raw-value evaluators are never always-true / always-false (BaseRawValueBasedPredicateEvaluator.java:
+            # 37-44): the scan operator keeps the null bitmap as its nulls even when p folded to a constant here
+            return _fold_and([p, nn]), _fold_and([_fold_not(p), nn]), n
         if _is_const(p, _FALSE):
             return _FALSE, _TRUE, None
         if _is_const(p, _TRUE):
@@ -318,7 +322,10 @@ def compile_filter(seg: GpuSegment, fc: Optional[FilterContext], null_handling: 
     if fc.type == "OR":
         if any(_is_const(k, _TRUE) for k in kids):
             return _TRUE
-        kids = _merge_or_leaves([k for k in kids if not _is_const(k, _FALSE)])
+        # (only EQ / IN predicates merge: MergeEqInFilterOptimizer leaves ranges as separate scan operators)
+        eq_in = [c.type == "PREDICATE" and c.predicate.type in ("EQ", "IN") for c in fc.children]
+        kept = [(k, m) for k, m in zip(kids, eq_in) if not _is_const(k, _FALSE)]
+        kids = _merge_or_leaves([k for k, _ in kept], [m for _, m in kept])
         if not kids:
             return _FALSE
         if len(kids) == 1:
@@ -333,17 +340,19 @@ def _leaf_ids(leaf):
     return np.asarray(leaf.ids, dtype=np.int32)
 
 
-def _merge_or_leaves(kids):
-    """OR of EQ / IN / range leaves on one dictionary column -> one leaf over the union of their dict ids, as the
-    reference's broker rewrites an OR of EQ / IN predicates on one column into one IN (MergeEqInFilterOptimizer,
+def _merge_or_leaves(kids, mergeable=None):
+    """OR of EQ / IN leaves on one dictionary column -> one leaf over the union of their dict ids, as the reference's
+    broker rewrites an OR of EQ / IN predicates on one column into one IN (MergeEqInFilterOptimizer,
     pinot-core/.../query/optimizer/filter/MergeEqInFilterOptimizer.java:40-120): a scan leaf (DICT_SET; the library
     turns a contiguous id set into a range) when every merged leaf scans, an inverted leaf when every one reads the
-    inverted index. Exclusive (NOT_EQ / NOT_IN) leaves stay apart. The doc set is the OR's."""
+    inverted index. Exclusive (NOT_EQ / NOT_IN) leaves and leaves of other predicates (mergeable[i] False: ranges,
+    which the optimizer leaves alone, so numEntriesScannedInFilter counts one scan per range) stay apart. The doc set
+    is the OR's."""
     scan = (_lib.LEAF_DICT_RANGE, _lib.LEAF_DICT_SET)
     groups, order = {}, []
-    for k in kids:
+    for i, k in enumerate(kids):
         fam = None
-        if isinstance(k, _Leaf) and k.column is not None and not k.exclusive:
+        if isinstance(k, _Leaf) and k.column is not None and not k.exclusive and (mergeable is None or mergeable[i]):
             fam = "scan" if k.kind in scan else ("inv" if k.kind == _lib.LEAF_INVERTED else None)
         key = (k.column, fam) if fam else id(k)
         if key not in groups:
@@ -840,9 +849,11 @@ class GpuCombineOperator:
                 nk = r.num_group_by
                 keys = np.ctypeslib.as_array(r.group_keys, shape=(max(ng * nk, 1),))[:ng * nk].reshape(ng, nk) if ng else np.zeros((0, nk), np.int32)
                 cols = []  # per group-by column: the values of the groups' keys (only the ids that occur)
+                key_space = 1  # the query-global key space: the union of the segments' values per column
                 for k in range(nk):
                     dv = _lib.DictionaryView()
                     _lib.check(lib.phip_result_dictionary(res, k, ctypes.byref(dv)))
+                    key_space *= max(int(dv.cardinality), 1)
                     cols.append(_dictionary_lookup(dv, keys[:, k]) if ng else [])
                 # column-wise (one list per primitive, then per function), zipped into the groups' lists: the
                 # per-group Python work is a few list operations (280 groups: 0.25 -> ~0.05 ms)
@@ -862,6 +873,7 @@ class GpuCombineOperator:
                 blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
                                           bool(r.num_groups_limit_reached))
                 blk.num_groups_trimmed = bool(r.num_groups_trimmed)
+                blk.key_space = key_space
                 blk.key_types = self.key_types()
             blk.device_ms = r.device_ms
             blk.scan_kernel_ms = r.scan_kernel_ms
@@ -1542,12 +1554,21 @@ class GpuGroupByCombineOperator:
             docs = [s.num_docs for s in self.segments]
         return [min(int(d), ks, self.limit) for d, ks in zip(docs, self.key_space)]
 
-    def _check_threshold(self, records):
+    def _check_threshold(self, records, distinct=None, key_space=None):
+        """ConcurrentIndexedTable resizes once its map holds trimThreshold DISTINCT keys (ConcurrentIndexedTable.java:
+        63-67), so the combine's bound is the per-segment records' sum capped by the distinct keys of the merged
+        result (exact when the block is untrimmed) or by the query-global key space (the union of the segments'
+        dictionaries)."""
         nonempty = sum(1 for r in records if r > 0)
-        if nonempty >= 2 and sum(records) >= self.threshold:
+        bound = sum(records)
+        if distinct is not None:
+            bound = min(bound, distinct)
+        if key_space:
+            bound = min(bound, key_space)
+        if nonempty >= 2 and bound >= self.threshold:
             raise UnsupportedOnGpu(
-                f"the combine can reach its trim threshold ({self.threshold} records from {nonempty} segments): "
-                "which partial groups survive depends on the reference's thread interleaving")
+                f"the combine can reach its trim threshold ({self.threshold} distinct records from {nonempty} "
+                "segments): which partial groups survive depends on the reference's thread interleaving")
 
     def _run_per_segment(self):
         from .reduce import trim_groups
@@ -1558,7 +1579,6 @@ class GpuGroupByCombineOperator:
                 _set_segment_trim(op, self.min_seg)
                 self.per_segment.append(op)
         blocks = [op.next_block() for op in self.per_segment]
-        self._check_threshold([len(b.groups) for b in blocks])
         aggs = self.query.aggregations
         groups, stats, reached = {}, ExecutionStatistics(), False
         times = dict.fromkeys(GpuFilteredAggregationOperator._TIMES, 0)
@@ -1570,6 +1590,7 @@ class GpuGroupByCombineOperator:
             reached |= bool(b.num_groups_limit_reached)
             for k in times:
                 times[k] += getattr(b, k, 0) or 0
+        self._check_threshold([len(b.groups) for b in blocks], distinct=len(groups))
         out = GroupByResultsBlock(aggs, list(self.query.group_by), groups, stats, reached)
         out.key_types = getattr(blocks[0], "key_types", None) if blocks else None
         out.num_groups_trimmed = False
@@ -1586,7 +1607,8 @@ class GpuGroupByCombineOperator:
             return self._run_per_segment()
         if self.seg_trim is not None:
             bounds = [min(b, self.seg_trim) for b in bounds]
-        self._check_threshold(bounds)
+        distinct = None if getattr(blk, "num_groups_trimmed", True) else len(blk.groups)
+        self._check_threshold(bounds, distinct, getattr(blk, "key_space", None))
         return blk
 
     def close(self):

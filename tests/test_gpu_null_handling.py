@@ -58,6 +58,11 @@ AGG = [
     "SELECT COUNT(*), SUM(k) FROM t WHERE NOT (r BETWEEN 10 AND 500000)",
     "SELECT COUNT(*), MAX(f) FROM t WHERE NOT (t BETWEEN 3 AND 20) AND NOT (d <> 12345)",
     "SELECT SUM(k), COUNT(*) FROM t WHERE NOT (NOT (d = 7 OR l > 0) AND s <> 'v4')",
+    # raw column leaves that fold to a constant keep the null bitmap (BaseRawValueBasedPredicateEvaluator: never
+    # always-true / always-false): an empty range and a NOT IN left without integral values
+    "SELECT COUNT(*), SUM(k) FROM t WHERE NOT (r BETWEEN 500 AND 100)",
+    "SELECT COUNT(*), SUM(k) FROM t WHERE NOT (r NOT IN (1.5, 2.5))",
+    "SELECT COUNT(*), MAX(l) FROM t WHERE NOT (r IN (2.5) AND g < 4) OR k = 3",
 ]
 
 

@@ -48,7 +48,7 @@ def _assert_intermediates_equal(aggs, gpu_vals, ora_vals, ora_exact):
                 if abs(ex) < 2 ** 53:
                     assert float(g) == o
             elif ex is not None:
-                # integer inputs whose |sum| bound passed 2^62: the library summed in double, as
+                # integer inputs whose |sum| bound passed 2^58: the library summed in double, as
                 # SumAggregationFunction does -- within REL of both the exact sum and the reference's fold
                 assert isinstance(g, float), g
                 assert abs(g - ex) <= REL * max(abs(ex), 1.0), (g, ex)

@@ -122,3 +122,26 @@ def test_gpu_group_trim_threshold(trim_segments):
     gblk = _gpu().make_instance_plan(qc, segs).next_block()
     oblk, exact = executor.execute(qc, raws)
     _check(qc, gblk, trim_groups(qc, oblk), exact)
+
+
+@pytest.mark.gpu
+def test_gpu_default_threshold_overlapping_segments(gpu_lib):
+    """The default groupTrimThreshold (10^6) over 12 segments whose per-segment bounds (100K docs, numGroupsLimit
+    100K) sum to 1.2M records, but whose keys overlap (150K distinct values in all): the reference's combine never
+    holds 10^6 keys, so the GPU answers, equal to the oracle."""
+    rng = np.random.default_rng(11)
+    raws = []
+    for s in range(12):
+        c = SegmentCreator(f"ov{s}")
+        c.add_column("k", DataType.INT, rng.integers(0, 150_000, 100_000))
+        c.add_column("m", DataType.LONG, rng.integers(-10 ** 9, 10 ** 9, 100_000))
+        raws.append(c.build())
+    segs = _segs(raws)
+    try:
+        qc = parse("SELECT k, SUM(m) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 10")
+        gblk = _gpu().make_instance_plan(qc, segs).next_block()
+        oblk, exact = executor.execute(qc, raws)
+        _check(qc, gblk, trim_groups(qc, oblk), exact)
+    finally:
+        for g in segs:
+            g.destroy()

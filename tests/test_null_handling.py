@@ -212,7 +212,10 @@ WHERES = ["x = 5", "x <> 5", "NOT (x = 5)", "x IS NULL", "x IS NOT NULL", "NOT (
           "NOT (NOT (x = 5 AND y = 1))", "s = 'a' OR x > 6", "NOT (s = 'a' OR x > 6)", "s IS NULL OR x IS NULL",
           "NOT (s IN ('a', 'b') AND NOT (x BETWEEN 1 AND 7))", "y = 2 AND NOT (x = 7)",
           "o BETWEEN 1 AND 3", "NOT (o BETWEEN 1 AND 3)", "NOT (o > 2 OR s = 'c')", "o IS NULL OR s IS NULL",
-          "NOT (s = 'b')", "s <> 'zz'", "NOT (s <> 'zz')"]
+          "NOT (s = 'b')", "s <> 'zz'", "NOT (s <> 'zz')",
+          # raw leaves folded to constants keep the null bitmap as their nulls
+          "NOT (r BETWEEN 50 AND 10)", "NOT (r NOT IN (1.5, 2.5))", "NOT (r IN (2.5) AND x = 5)",
+          "r BETWEEN 50 AND 10 OR NOT (x = 5)"]
 
 
 @pytest.mark.parametrize("nh", [True, False])

@@ -196,3 +196,32 @@ def test_execution_time_refusal_goes_to_the_cpu_plan():
     cpu = _CpuMaker()
     op = GpuPlanWithCpuFallback(GpuGroupByCombineOperator(q, _Op(segs, [9000, 9000]), None), cpu, q, segs)
     assert op.next_block() == "cpu-block" and cpu.calls == [q]
+
+
+def test_combine_threshold_counts_distinct_keys():
+    """ConcurrentIndexedTable resizes on the number of DISTINCT keys in its map (ConcurrentIndexedTable.java:63-67):
+    per-segment bounds that sum past the threshold do not refuse the query when the merged result (untrimmed) or the
+    query-global key space holds fewer keys than the threshold."""
+    sql = "SET groupTrimThreshold = 10; SELECT k, COUNT(*) FROM t GROUP BY k ORDER BY COUNT(*) LIMIT 10"
+    q = _resolved(sql)
+    segs = [_Seg(100000, 8000), _Seg(100000, 8000)]
+
+    class _Untrimmed(_Op):
+        def __init__(self, segments, matched, groups, trimmed, key_space):
+            super().__init__(segments, matched, groups)
+            self.trimmed, self.key_space = trimmed, key_space
+
+        def next_block(self):
+            b = super().next_block()
+            b.num_groups_trimmed, b.key_space = self.trimmed, self.key_space
+            return b
+
+    few = {(k,): [1] for k in range(9000)}  # 9000 distinct keys < threshold 10000, bounds sum to 18000
+    GpuGroupByCombineOperator(q, _Untrimmed(segs, [9000, 9000], few, False, 20000), None).next_block()
+    # trimmed block: the distinct count is unknown, the key space (8000 < 10000) still bounds it
+    GpuGroupByCombineOperator(q, _Untrimmed(segs, [9000, 9000], few, True, 8000), None).next_block()
+    with pytest.raises(UnsupportedOnGpu):  # trimmed, key space 20000: the combine may resize
+        GpuGroupByCombineOperator(q, _Untrimmed(segs, [9000, 9000], few, True, 20000), None).next_block()
+    many = {(k,): [1] for k in range(12000)}
+    with pytest.raises(UnsupportedOnGpu):  # 12000 distinct keys >= 10000
+        GpuGroupByCombineOperator(q, _Untrimmed(segs, [9000, 9000], many, False, 20000), None).next_block()
