@@ -170,7 +170,7 @@ __device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc,
       if (c.hll_rows) {
         if (act) hll_row_each(c, doc, [&](int r, uint32_t rho) { __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_WG); });
       } else {
-        const uint32_t h = hll_entry(c, doc, q.log2m);
+        const uint32_t h = hll_entry(c, doc, ag.log2m);
         if (act) __hip_atomic_fetch_max(&regs[h >> 8], h & 0xffu, PHIP_RLX, PHIP_WG);
       }
     } else {
@@ -232,7 +232,7 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
         if (c.hll_rows) {
           hll_row_each(c, doc, [&](int r, uint32_t rho) { lds_hll_max(regs, (uint32_t)r, rho); });
         } else {
-          const uint32_t h = hll_entry(c, doc, q.log2m);
+          const uint32_t h = hll_entry(c, doc, ag.log2m);
           lds_hll_max(regs, h >> 8, h & 0xffu);
         }
         break;

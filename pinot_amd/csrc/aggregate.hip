@@ -63,7 +63,7 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
         for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
       } else if (!c.has_dict) {  // raw values, hashed per doc
 #pragma unroll
-        for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], q.log2m);
+        for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], ag.log2m);
       } else {
         uint32_t id[U];
         batch_ids<U>(c, d, sa, id);
@@ -135,11 +135,34 @@ __device__ __forceinline__ void batch_ids_hbm(ccol_t &c, const int32_t (&d)[U], 
   for (int u = 0; u < U; u++) id[u] = decode_bits(c.words, (uint64_t)(uint32_t)d[u] * b, b);
 }
 
+// one group-by column's contribution to the keys of a batch (ids, remap, stride)
+template <int U>
+__device__ __forceinline__ void batch_key_column(cquery_t &q, cseg_t &seg, int k, const int32_t (&d)[U],
+                                                 int32_t (&key)[U]) {
+  ccol_t &c = seg.cols[q.gb_cols[k]];
+  uint32_t id[U];
+  if (c.has_dict) {
+    batch_ids_hbm<U>(c, d, id);
+    if (c.remap) {
+#pragma unroll
+      for (int u = 0; u < U; u++) id[u] = (uint32_t)((const PHIP_GLB int32_t *)c.remap)[id[u]];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) id[u] = (uint32_t)(raw_i64(c, d[u]) - c.gb_base);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) key[u] += (int32_t)id[u] * (int32_t)q.gb_stride[k];
+}
+
+// The first kKeyFast columns' ids are issued together, then their remaps (two round trips for up to four columns);
+// columns past them (a GROUP BY of more than four columns) follow one at a time.
+constexpr int kKeyFast = 4;
 template <int U>
 __device__ __forceinline__ void batch_group_keys(cquery_t &q, cseg_t &seg, const int32_t (&d)[U], int32_t (&key)[U]) {
-  uint32_t id[kMaxGroupBy][U];
+  uint32_t id[kKeyFast][U];
 #pragma unroll
-  for (int k = 0; k < kMaxGroupBy; k++) {
+  for (int k = 0; k < kKeyFast; k++) {
 #pragma unroll
     for (int u = 0; u < U; u++) id[k][u] = 0;
     if (k < q.num_group_by) {
@@ -153,7 +176,7 @@ __device__ __forceinline__ void batch_group_keys(cquery_t &q, cseg_t &seg, const
     }
   }
 #pragma unroll
-  for (int k = 0; k < kMaxGroupBy; k++) {
+  for (int k = 0; k < kKeyFast; k++) {
     if (k < q.num_group_by) {
       ccol_t &c = seg.cols[q.gb_cols[k]];
       if (c.has_dict && c.remap) {
@@ -167,10 +190,12 @@ __device__ __forceinline__ void batch_group_keys(cquery_t &q, cseg_t &seg, const
   for (int u = 0; u < U; u++) {
     int32_t kk = 0;
 #pragma unroll
-    for (int k = 0; k < kMaxGroupBy; k++)
+    for (int k = 0; k < kKeyFast; k++)
       if (k < q.num_group_by) kk += (int32_t)id[k][u] * (int32_t)q.gb_stride[k];
     key[u] = kk;
   }
+#pragma unroll 1
+  for (int k = kKeyFast; k < q.num_group_by; k++) batch_key_column<U>(q, seg, k, d, key);
 }
 
 // Values of a batch from ids already loaded (dictionary columns) or from the raw column.
@@ -332,7 +357,7 @@ __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const
           for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
         } else {
 #pragma unroll
-          for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], q.log2m);
+          for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], ag.log2m);
         }
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -422,7 +447,7 @@ __device__ __forceinline__ void group_update_global(cquery_t &q, cseg_t &seg, in
             if (regs[r] < rho) __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_AG);
           });
         } else {
-          const uint32_t h = hll_entry(c, doc, q.log2m);
+          const uint32_t h = hll_entry(c, doc, ag.log2m);
           glb_u32 *r = regs + (h >> 8);
           if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
         }

@@ -10,7 +10,7 @@ constexpr int kMaxAggs = 8;           // aggregation slots per query
 constexpr int kMaxPrograms = 8;       // filter programs per query (filtered aggregations in one pass)
 constexpr int kDenseMin = 640;        // default DevAggQuery::dense_min
 constexpr int kMaxFilterStack = 6;    // postfix evaluation stack depth (host rejects deeper programs)
-constexpr int kMaxGroupBy = 4;
+constexpr int kMaxGroupBy = 8;  // GROUP BY columns (the mixed-radix key space stays below 2^62)
 constexpr int kWave = 64;             // CDNA wavefront
 constexpr int kTileGroups = 32;       // 64-doc groups per tile: bit (31-g) of lane l's mask word = doc 64g+l
 constexpr int kTileDocs = kTileGroups * 64;  // 2048 docs per tile
@@ -28,6 +28,9 @@ constexpr int kFusedRingTile = 512;   // fused aggregation, per-tile mode: u16 t
 #endif
 constexpr int kFusedRingDefer = PHIP_FUSED_RING_DEFER;  // fused aggregation, deferred mode: u32 segment doc ids per wave (one batch
                                       // + an eighth of a tile)
+// fused deferred tiles with at least this many matched docs (of 2048) are projected in place, lane-major
+// (filter.hip fused_dense_tile); PHIP_FUSED_DENSE_MIN overrides
+constexpr int kFusedDenseMin = 192;
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;
@@ -226,7 +229,9 @@ struct DevFilter {
   const struct DevAggQuery *agg;  // device copy of the aggregation descriptor, null = not fused
   uint64_t *agg_partials;         // [num_blocks][num_aggs]
   int32_t fring_bytes;            // per-wave matched-doc ring (fused): 4 * kFusedRingDefer when a segment defers,
-  int32_t pad_f;                  // else 2 * kFusedRingTile
+                                  // else 2 * kFusedRingTile
+  int32_t fused_dense_min;        // deferred fused tiles with >= this many matched docs are projected in place,
+                                  // lane-major (coalesced reads of every group), not through the ring; 0 = never
   const DevFinal *fin;            // non-null: this launch is the plan's last; its last workgroup finalizes
 };
 

@@ -1561,7 +1561,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     return fail(PHIP_ERR_INVALID, "query: need >=1 segment and <= %d columns", kMaxQueryColumns);
   if (q->num_aggregations < 0 || q->num_aggregations > kMaxAggs)
     return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d aggregations on the GPU path", kMaxAggs);
-  if (q->num_group_by < 0 || q->num_group_by > 4) return fail(PHIP_ERR_UNSUPPORTED, "query: at most 4 group-by columns");
+  if (q->num_group_by < 0 || q->num_group_by > kMaxGroupBy)
+    return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d group-by columns", kMaxGroupBy);
   if (q->num_segments > 1 && want_bitmap) return fail(PHIP_ERR_INVALID, "filter bitmap: one segment only");
   const int nprog = std::max(1, q->num_filter_programs);
   if (nprog > kMaxPrograms) return fail(PHIP_ERR_UNSUPPORTED, "query: at most %d filter programs", kMaxPrograms);
@@ -1681,8 +1682,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     kinds[a] = d.acc;
     if (d.acc == ACC_HLL) {
       if (ag.log2m < 4 || ag.log2m > 12) return fail(PHIP_ERR_UNSUPPORTED, "log2m %d outside [4,12]", ag.log2m);
-      if (nhll > 0 && ag.log2m != log2m) return fail(PHIP_ERR_UNSUPPORTED, "all HLL aggregations must share log2m");
-      log2m = ag.log2m;
+      // DISTINCTCOUNTHLL functions of different log2m share the plan's register tables at the largest one's stride:
+      // function a's registers are the first 2^log2m_a of its slot (its per-doc (register, rho) entries are computed
+      // with its own log2m, DistinctCountHLLAggregationFunction.java:105-145). One column per entry table, so two
+      // log2m over one column stay on the CPU path.
+      for (int b = 0; b < a; b++)
+        if (dq.aggs[b].acc == ACC_HLL && dq.aggs[b].col_a == ag.column_a && dq.aggs[b].log2m != ag.log2m)
+          return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL of column %d with two log2m (%d, %d)", ag.column_a,
+                      dq.aggs[b].log2m, ag.log2m);
+      log2m = std::max(log2m, ag.log2m);
       d.hll_slot = nhll++;
       d.log2m = ag.log2m;
     }
@@ -2839,6 +2847,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   fq.nbuf = nbuf;
   fq.fring_bytes = fring_bytes;
   fq.xcd_walk = xcd_walk;
+  {
+    const char *dm = getenv("PHIP_FUSED_DENSE_MIN");  // measurement override (0 = always through the ring)
+    fq.fused_dense_min = dm ? atoi(dm) : kFusedDenseMin;
+  }
   {
     const char *pe = getenv("PHIP_FILTER_PROBE");
     fq.probe = pe ? atoi(pe) : 0;

@@ -832,7 +832,7 @@ class GpuCombineOperator:
                     return int(longs[g][i]) if exact[i] else float(vals[g][i])
                 if f in (_lib.AGG_MIN, _lib.AGG_MAX):
                     return float(vals[g][i])
-                return hll[g, hll_slot[i]].copy()
+                return hll[g, hll_slot[i], :1 << self.prims[i][4]].copy()  # (slots hold 2^max-log2m bytes)
 
             def intermediates(g):
                 out = []
@@ -865,7 +865,8 @@ class GpuCombineOperator:
                     elif f in (_lib.AGG_SUM, _lib.AGG_MIN, _lib.AGG_MAX):
                         prim_cols.append(vals[:, i].tolist())
                     else:
-                        prim_cols.append([hll[g, hll_slot[i]].copy() for g in range(ng)])
+                        mi = 1 << self.prims[i][4]
+                        prim_cols.append([hll[g, hll_slot[i], :mi].copy() for g in range(ng)])
                 fcols = [list(zip(prim_cols[sl[0]], prim_cols[sl[1]])) if fn in ("avg", "minmaxrange") else prim_cols[sl]
                          for fn, sl in self.mapping]
                 gkeys = list(zip(*cols)) if nk else [()] * ng
@@ -1641,6 +1642,12 @@ class GpuPlanWithCpuFallback:
     def close(self):
         self.gpu_op.close()
 
+    def __getattr__(self, name):
+        # the GPU operator's surface (execute_partial / finish for a multi-GPU merge, run_raw, key_types, ...)
+        if name == "gpu_op":
+            raise AttributeError(name)
+        return getattr(self.gpu_op, name)
+
 
 def use_gpu_option(query: QueryContext, default: bool) -> bool:
     """The ``useGpu`` query option (``SET useGpu = true;`` / queryOptions), parsed as Java's
@@ -1860,9 +1867,9 @@ class GpuInstancePlanMaker:
             op = self._make_gpu_plan(query, segments)
         except UnsupportedOnGpu:
             return self.cpu_plan_maker.make_instance_plan(query, segments)
-        if query.group_by:  # (a group-by execution may still refuse: trim threshold, several infos at the limit)
-            return GpuPlanWithCpuFallback(op, self.cpu_plan_maker, query, segments)
-        return op
+        # (an execution may still refuse: the combine's trim threshold, several infos at the limit, or a shape the
+        # library only rejects when it prepares the plan on first execution)
+        return GpuPlanWithCpuFallback(op, self.cpu_plan_maker, query, segments)
 
     def _make_gpu_plan(self, query: QueryContext, segments: Sequence[GpuSegment]):
         query = self.apply_query_options(query)
