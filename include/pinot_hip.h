@@ -49,6 +49,9 @@
 #define PHIP_ERR_UNSUPPORTED 3 /* shape outside the GPU subset: caller falls back to the Java path */
 #define PHIP_ERR_NOT_FOUND 4   /* unknown segment handle or column */
 #define PHIP_ERR_NO_DEVICE 5   /* no usable GPU */
+#define PHIP_ERR_TIMEOUT 6     /* the plan's deadline passed (QueryTimeoutException: BaseSingleBlockCombineOperator
+                                  .java:137-144 checks QueryContext.getEndTimeMs) */
+#define PHIP_ERR_CANCELLED 7   /* phip_plan_cancel stopped the execution (QueryCancelledException) */
 
 /* ---- stored data types (FieldSpec.DataType, single-value) ---------------------------------- */
 #define PHIP_TYPE_INT 0
@@ -340,6 +343,14 @@ PHIP_API int32_t phip_query(const phip_query_desc *query, phip_result **out_resu
 PHIP_API int32_t phip_plan_create(const phip_query_desc *query, uint64_t *out_plan);
 PHIP_API int32_t phip_plan_execute(uint64_t plan, phip_result **out_result);
 PHIP_API int32_t phip_plan_destroy(uint64_t plan);
+/* Query deadline and cancellation (QueryContext.getEndTimeMs / the server's cancel of a running query,
+ * BaseSingleBlockCombineOperator.java:137-144, QueryScheduler cancel): an execution checks them between its launch
+ * phases -- before enqueuing, after the main kernels, before a numGroupsLimit pass and before the server trim -- and
+ * returns PHIP_ERR_TIMEOUT / PHIP_ERR_CANCELLED there (a launch in flight completes: kernels are not interrupted,
+ * as the reference's operators only check between blocks). deadline_ms: wall-clock milliseconds since the Unix
+ * epoch (System.currentTimeMillis), 0 = none. A cancel is sticky: the plan belongs to one query. */
+PHIP_API int32_t phip_plan_set_deadline(uint64_t plan, int64_t deadline_ms);
+PHIP_API int32_t phip_plan_cancel(uint64_t plan);
 PHIP_API int32_t phip_result_dictionary(const phip_result *result, int32_t group_by_index,
                                         phip_dictionary_view *out_view);
 PHIP_API void phip_result_free(phip_result *result);

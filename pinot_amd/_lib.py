@@ -16,6 +16,8 @@ PHIP_ERR_HIP = 2
 PHIP_ERR_UNSUPPORTED = 3
 PHIP_ERR_NOT_FOUND = 4
 PHIP_ERR_NO_DEVICE = 5
+PHIP_ERR_TIMEOUT = 6
+PHIP_ERR_CANCELLED = 7
 
 FWD_FIXED_BIT, FWD_SORTED, FWD_RAW_CHUNK, FWD_HLL_REGISTERS = 0, 1, 2, 3
 NODE_LEAF, NODE_AND, NODE_OR, NODE_NOT = 0, 1, 2, 3
@@ -38,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap", "phip_plan_create", "phip_plan_execute",
     "phip_plan_destroy", "phip_global_dictionary", "phip_plan_execute_partial", "phip_plan_finish",
     "phip_runtime_versions", "phip_plan_abandon_partial", "phip_result_select_dictionary",
+    "phip_plan_set_deadline", "phip_plan_cancel",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -148,6 +151,27 @@ class PhipError(RuntimeError):
         self.code = code
 
 
+class UnsupportedOnGpu(Exception):
+    """Query shape outside the GPU subset (the Java side would call super.makeInstancePlan)."""
+
+
+class PhipUnsupported(PhipError, UnsupportedOnGpu):
+    """PHIP_ERR_UNSUPPORTED from the library: the plan maker's CPU operator answers the query."""
+
+
+class QueryTimeoutError(PhipError):
+    """PHIP_ERR_TIMEOUT: the plan's deadline passed (QueryTimeoutException / QueryErrorCode.EXECUTION_TIMEOUT,
+    BaseSingleBlockCombineOperator.java:137-144)."""
+
+
+class QueryCancelledError(PhipError):
+    """PHIP_ERR_CANCELLED: phip_plan_cancel stopped the execution (QueryCancelledException)."""
+
+
+_ERRORS = {PHIP_ERR_UNSUPPORTED: PhipUnsupported, PHIP_ERR_TIMEOUT: QueryTimeoutError,
+           PHIP_ERR_CANCELLED: QueryCancelledError}
+
+
 _lib = None
 _torch_first = False  # torch's HIP runtime was in the process before the library bound to one
 
@@ -217,6 +241,10 @@ def load(with_torch: bool = False):
     lib.phip_plan_finish.restype = i32
     lib.phip_plan_abandon_partial.argtypes = [u64]
     lib.phip_plan_abandon_partial.restype = i32
+    lib.phip_plan_set_deadline.argtypes = [u64, i64]
+    lib.phip_plan_set_deadline.restype = i32
+    lib.phip_plan_cancel.argtypes = [u64]
+    lib.phip_plan_cancel.restype = i32
     built, runtime = ctypes.c_int32(0), ctypes.c_int32(0)
     rv = getattr(lib, "phip_runtime_versions", None)  # (absent from round-2 builds used in A/B runs)
     if rv is not None:
@@ -232,5 +260,5 @@ def load(with_torch: bool = False):
 
 def check(rc):
     if rc != PHIP_OK:
-        raise PhipError(rc, load().phip_last_error().decode(errors="replace"))
+        raise _ERRORS.get(rc, PhipError)(rc, load().phip_last_error().decode(errors="replace"))
     return rc

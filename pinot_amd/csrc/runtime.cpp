@@ -1363,6 +1363,8 @@ int acc_kind_for(const phip_aggregation &a, bool integral) {
 // same launch sequence (a captured hipGraph from the second execution on).
 struct Plan {
   Device *dev = nullptr;
+  std::atomic<int64_t> deadline_ms{0};  // phip_plan_set_deadline (0 = none)
+  std::atomic<int32_t> cancelled{0};    // phip_plan_cancel (sticky)
   std::vector<std::shared_ptr<Segment>> segs;  // keeps the segments' HBM alive while the plan exists
   std::vector<void *> allocs;
   int32_t alloc(size_t bytes, void **out) {
@@ -3134,6 +3136,20 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   return PHIP_OK;
 }
 
+// Deadline / cancel checkpoint between an execution's launch phases (include/pinot_hip.h phip_plan_set_deadline).
+static int32_t check_deadline(const Plan &P, const char *where) {
+  if (P.cancelled.load(std::memory_order_relaxed))
+    return fail(PHIP_ERR_CANCELLED, "query cancelled (%s)", where);
+  const int64_t d = P.deadline_ms.load(std::memory_order_relaxed);
+  if (d > 0) {
+    const int64_t now = std::chrono::duration_cast<std::chrono::milliseconds>(
+                            std::chrono::system_clock::now().time_since_epoch()).count();
+    if (now > d) return fail(PHIP_ERR_TIMEOUT, "query timed out %lld ms past its deadline (%s)", (long long)(now - d),
+                             where);
+  }
+  return PHIP_OK;
+}
+
 // The device work of one execution, on `st` (eager, or recorded into a graph by stream capture).
 static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   DevAggQuery &dq = P.dq;
@@ -3235,6 +3251,10 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
                            void **oh, int64_t *ngroups, int32_t *limit_reached, const int64_t *normal_offs) {
   const int32_t S = P.nseg, naggs = P.naggs, nhll = P.nhll, m_regs = P.m_regs;
   const int64_t limit = P.num_groups_limit;
+  {
+    int32_t drc = check_deadline(P, "before the numGroupsLimit pass");
+    if (drc) return drc;
+  }
   int64_t space = 1;
   for (auto &d : P.gb_dicts) space *= d->card;
   if ((double)space * (double)S >= (double)((int64_t)1 << 62))
@@ -3446,6 +3466,10 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   }
   if (mode != EXEC_FINISH && P.partial_pending)  // the caller still owns the table (it may be all-reducing it)
     return fail(PHIP_ERR_INVALID, "plan has a pending partial table: phip_plan_finish or phip_plan_abandon_partial first");
+  if (mode != EXEC_FINISH) {
+    int32_t drc = check_deadline(P, "before the launches");
+    if (drc) return drc;
+  }
   // measurement only (PHIP_HOST_TRACE=1): host microseconds per phase of this call, one stderr line per execution
   static const bool host_trace = getenv("PHIP_HOST_TRACE") != nullptr;
   using hclock = std::chrono::steady_clock;
@@ -3618,6 +3642,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       HIP_TRY(hipStreamSynchronize(st));
       ngroups = total;
     }
+    if ((rc = check_deadline(P, "after the group-by kernels"))) return rc;
     if (mode == EXEC_PARTIAL) {
       // per-segment numGroupsLimit needs the first-seen record pass of phip_plan_execute
       if (P.num_groups_limit > 0 && ngroups >= P.num_groups_limit)
@@ -3679,6 +3704,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       if (rc) return rc;
     }
     if (P.trim_size > 0 && ngroups > P.trim_size && (naggs > 0 || P.order_nkeys > 0 || P.order_terms.num_terms > 0)) {
+      if ((rc = check_deadline(P, "before the server trim"))) return rc;
       // ORDER BY <aggregation> with more groups than trimSize: keep the top trimSize on the device
       // (IndexedTable.finish -> TableResizer.getTopRecords), so only those records cross PCIe.
       size_t sbytes = 0;
@@ -4305,6 +4331,22 @@ static int32_t find_plan(uint64_t plan, Plan **out) {
   auto it = g_plans.find(plan);
   if (it == g_plans.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown plan handle %llu", (unsigned long long)plan);
   *out = it->second.get();
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_plan_set_deadline(uint64_t plan, int64_t deadline_ms) {
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  p->deadline_ms.store(deadline_ms > 0 ? deadline_ms : 0, std::memory_order_relaxed);
+  return PHIP_OK;
+}
+
+PHIP_API int32_t phip_plan_cancel(uint64_t plan) {
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  p->cancelled.store(1, std::memory_order_relaxed);
   return PHIP_OK;
 }
 

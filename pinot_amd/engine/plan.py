@@ -11,11 +11,13 @@
                          CombineOperator merge (…/operator/combine/BaseSingleBlockCombineOperator.java:58-162)
                          with one phip_query call.
 """
+import contextvars
 import ctypes
 import dataclasses
 import math
 import os
 import re
+import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Union
 
@@ -33,8 +35,7 @@ from .results import (AggregationResultsBlock, ExecutionStatistics, GroupByResul
 from .segment import GpuSegment
 
 
-class UnsupportedOnGpu(Exception):
-    """Query shape outside the GPU subset (the Java side would call super.makeInstancePlan)."""
+from .._lib import QueryCancelledError, QueryTimeoutError, UnsupportedOnGpu  # noqa: E402,F401 (re-exported)
 
 
 # ------------------------------------------------------------------------------ filter trees
@@ -645,9 +646,18 @@ class GpuCombineOperator:
             self._lib = lib
         if prepare_only:
             return None
+        self._apply_deadline(lib)
         res = ctypes.POINTER(_lib.Result)()
         _lib.check(lib.phip_plan_execute(self._plan, ctypes.byref(res)))
         return res
+
+    def _apply_deadline(self, lib):
+        """The running query's end time to the prepared plan (phip_plan_set_deadline; 0 = none), when it changed."""
+        end = _END_TIME_MS.get()
+        d = int(end) if end is not None else 0
+        if d != getattr(self, "_deadline_set", 0):
+            _lib.check(lib.phip_plan_set_deadline(self._plan, d))
+            self._deadline_set = d
 
     def close(self):
         """Release the prepared plan (and with it the last references to unloaded segments)."""
@@ -726,6 +736,7 @@ class GpuCombineOperator:
             return None
         lib = _lib.load()
         self.run_raw(prepare_only=True)
+        self._apply_deadline(lib)
         part = _lib.Partial()
         rc = lib.phip_plan_execute_partial(self._plan, ctypes.byref(part))
         if rc == _lib.PHIP_ERR_UNSUPPORTED:
@@ -1020,7 +1031,11 @@ def _run_parts(parts):
     after another too). Running them on concurrent execution lanes from a thread pool was measured slower on C1
     FILTERED_MIXED (0.48 -> 0.56 ms p50, profiles/r02c_configs_c1.jsonl): each info's device work is ~50 us and the
     host side of an execution does not overlap under the GIL."""
-    return [op.next_block() for _, op in parts]
+    out = []
+    for _, op in parts:
+        check_deadline("between filtered-aggregation plans")
+        out.append(op.next_block())
+    return out
 
 
 class GpuFilteredAggregationOperator:
@@ -1457,6 +1472,55 @@ def _int_option(options, key, min_value=None):
     return x
 
 
+def _long_option_positive(options, key):
+    """QueryOptionsUtils.checkedParseLongPositive (QueryOptionsUtils.java:410-430): Long.parseLong, at least 1."""
+    v = options.get(key)
+    if v is None:
+        return None
+    v = str(v)
+    if not _INT.match(v) or not 1 <= int(v) < (1 << 63):
+        raise QueryOptionError(f"{key} must be a number between 1 and 2^63-1, got: {v}")
+    return int(v)
+
+
+# The running query's end time (QueryContext.getEndTimeMs, wall-clock ms): set by the outermost operator for the
+# length of its next_block (_DeadlineOperator), read by every plan execution under it and by the multi-plan
+# operators between their plans (BaseSingleBlockCombineOperator.java:133-144 checks it between blocks).
+_END_TIME_MS = contextvars.ContextVar("pinot_amd_end_time_ms", default=None)
+
+
+def check_deadline(where: str):
+    """QueryTimeoutError when the running query's end time has passed (a no-op without timeoutMs)."""
+    end = _END_TIME_MS.get()
+    if end is not None and time.time() * 1000.0 > end:
+        raise QueryTimeoutError(_lib.PHIP_ERR_TIMEOUT, f"query timed out ({where})")
+
+
+class _DeadlineOperator:
+    """The outermost operator of a query with timeoutMs: each next_block runs under endTimeMs = its start +
+    timeoutMs (the server's QueryContext end time), which every library execution under it receives
+    (phip_plan_set_deadline) and the multi-plan operators check between plans."""
+
+    def __init__(self, op, timeout_ms):
+        self.op, self.timeout_ms = op, timeout_ms
+
+    def next_block(self):
+        token = _END_TIME_MS.set(time.time() * 1000.0 + self.timeout_ms)
+        try:
+            check_deadline("before execution")
+            return self.op.next_block()
+        finally:
+            _END_TIME_MS.reset(token)
+
+    def close(self):
+        self.op.close()
+
+    def __getattr__(self, name):
+        if name == "op":
+            raise AttributeError(name)
+        return getattr(self.op, name)
+
+
 def _bool_option(options, key) -> bool:
     """Boolean.parseBoolean of a query option (only a case-insensitive "true" is true)."""
     return str(options.get(key, "")).strip().lower() == "true"
@@ -1579,7 +1643,10 @@ class GpuGroupByCombineOperator:
                 op = self.make_op([seg])
                 _set_segment_trim(op, self.min_seg)
                 self.per_segment.append(op)
-        blocks = [op.next_block() for op in self.per_segment]
+        blocks = []
+        for op in self.per_segment:  # (the combine checks the query's end time between its segments' blocks)
+            check_deadline("between per-segment group-by plans")
+            blocks.append(op.next_block())
         aggs = self.query.aggregations
         groups, stats, reached = {}, ExecutionStatistics(), False
         times = dict.fromkeys(GpuFilteredAggregationOperator._TIMES, 0)
@@ -1838,6 +1905,7 @@ class GpuInstancePlanMaker:
         results). enableNullHandling is _make_operator's (GpuNullHandlingAggregationOperator)."""
         o = query.options
         _bool_option(o, "enableNullHandling")  # (validated: the operators read it, null_handling_enabled)
+        _long_option_positive(o, "timeoutMs")  # (validated: make_instance_plan applies it, _DeadlineOperator)
         for k in ("serverReturnFinalResult", "serverReturnFinalResultKeyUnpartitioned"):
             if _bool_option(o, k):
                 raise UnsupportedOnGpu(f"{k}: the GPU operators return intermediate results")
@@ -1857,6 +1925,11 @@ class GpuInstancePlanMaker:
     def make_instance_plan(self, query: Union[str, QueryContext], segments: Sequence[GpuSegment]):
         if isinstance(query, str):
             query = parse(query)
+        timeout = _long_option_positive(query.options, "timeoutMs")
+        op = self._make_instance_plan(query, segments)
+        return _DeadlineOperator(op, timeout) if timeout is not None else op
+
+    def _make_instance_plan(self, query: QueryContext, segments: Sequence[GpuSegment]):
         if not use_gpu_option(query, self.default_use_gpu):
             if self.cpu_plan_maker is None:
                 raise UnsupportedOnGpu("useGpu=false: the query belongs to the CPU plan maker")

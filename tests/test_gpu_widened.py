@@ -149,3 +149,34 @@ def test_gpu_refusals_reach_the_cpu_plan_maker(sql, wide_segments):
     op = GpuInstancePlanMaker(cpu_plan_maker=cpu).make_instance_plan(qc, segs)
     assert op.next_block() == "cpu" and cpu.calls == 1
     op.close()
+
+
+def test_gpu_plan_deadline_and_cancel(wide_segments):
+    """phip_plan_set_deadline / phip_plan_cancel (QueryContext.getEndTimeMs, BaseSingleBlockCombineOperator.java:
+    133-144): a past deadline fails the execution with PHIP_ERR_TIMEOUT, a far one runs it, a cancel is sticky; the
+    query option timeoutMs runs a query with time left."""
+    import ctypes
+    import time
+
+    from pinot_amd import _lib
+    from pinot_amd.engine.plan import QueryCancelledError, QueryTimeoutError
+    raws, segs = wide_segments
+    lib = _lib.load()
+    for sql in ("SELECT SUM(m), COUNT(*) FROM t WHERE f < 40", "SELECT c1, c2, SUM(m) FROM t GROUP BY c1, c2 LIMIT 100"):
+        op = GpuInstancePlanMaker().make_instance_plan(parse(sql), segs)
+        op.run_raw(prepare_only=True)
+        res = ctypes.POINTER(_lib.Result)()
+        _lib.check(lib.phip_plan_set_deadline(op._plan, 1))  # 1 ms after the epoch: long past
+        with pytest.raises(QueryTimeoutError):
+            _lib.check(lib.phip_plan_execute(op._plan, ctypes.byref(res)))
+        _lib.check(lib.phip_plan_set_deadline(op._plan, int(time.time() * 1000) + 60_000))
+        _lib.check(lib.phip_plan_execute(op._plan, ctypes.byref(res)))
+        lib.phip_result_free(res)
+        _lib.check(lib.phip_plan_cancel(op._plan))
+        with pytest.raises(QueryCancelledError):
+            _lib.check(lib.phip_plan_execute(op._plan, ctypes.byref(res)))
+        op.close()
+    qc = parse("SET timeoutMs = 60000; SELECT c1, SUM(m) FROM t WHERE f < 40 GROUP BY c1 LIMIT 100")
+    blk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
+    oblk, ex = executor.execute(qc, raws)
+    _check_groups(qc, blk, oblk, ex)

@@ -225,3 +225,30 @@ def test_combine_threshold_counts_distinct_keys():
     many = {(k,): [1] for k in range(12000)}
     with pytest.raises(UnsupportedOnGpu):  # 12000 distinct keys >= 10000
         GpuGroupByCombineOperator(q, _Untrimmed(segs, [9000, 9000], many, False, 20000), None).next_block()
+
+
+def test_timeout_option_validated_and_applied():
+    """timeoutMs is QueryOptionsUtils.getTimeoutMs (a positive long); a query whose end time passed raises
+    QueryTimeoutError before it runs, and one with time left runs its operator."""
+    import time as _time
+
+    from pinot_amd.engine import plan as _plan
+    from pinot_amd.engine.plan import QueryOptionError, QueryTimeoutError
+    for bad in ("0", "-5", "abc", "1.5"):
+        with pytest.raises(QueryOptionError):
+            GpuInstancePlanMaker().apply_query_options(parse(f"SET timeoutMs = {bad}; SELECT COUNT(*) FROM t"))
+
+    class _Inner:
+        def next_block(self):
+            _plan.check_deadline("inside")
+            return "ran"
+
+        def close(self):
+            pass
+
+    assert _plan._DeadlineOperator(_Inner(), 10_000).next_block() == "ran"
+    slow = _plan._DeadlineOperator(type("S", (), {"next_block": lambda s: (_time.sleep(0.02), _plan.check_deadline(
+        "after sleeping"))[1], "close": lambda s: None})(), 1)
+    with pytest.raises(QueryTimeoutError):
+        slow.next_block()
+    _plan.check_deadline("outside any query")  # no end time: no-op
