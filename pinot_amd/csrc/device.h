@@ -28,9 +28,6 @@ constexpr int kFusedRingTile = 512;   // fused aggregation, per-tile mode: u16 t
 #endif
 constexpr int kFusedRingDefer = PHIP_FUSED_RING_DEFER;  // fused aggregation, deferred mode: u32 segment doc ids per wave (one batch
                                       // + an eighth of a tile)
-// fused deferred tiles with at least this many matched docs (of 2048) are projected in place, lane-major
-// (filter.hip fused_dense_tile); PHIP_FUSED_DENSE_MIN overrides
-constexpr int kFusedDenseMin = 192;
 // aggregation kernel: 8 waves per workgroup
 constexpr int kAggBlock = 512;
 constexpr int kAggWaves = kAggBlock / kWave;
@@ -229,9 +226,7 @@ struct DevFilter {
   const struct DevAggQuery *agg;  // device copy of the aggregation descriptor, null = not fused
   uint64_t *agg_partials;         // [num_blocks][num_aggs]
   int32_t fring_bytes;            // per-wave matched-doc ring (fused): 4 * kFusedRingDefer when a segment defers,
-                                  // else 2 * kFusedRingTile
-  int32_t fused_dense_min;        // deferred fused tiles with >= this many matched docs are projected in place,
-                                  // lane-major (coalesced reads of every group), not through the ring; 0 = never
+  int32_t pad_f;                  // else 2 * kFusedRingTile
   const DevFinal *fin;            // non-null: this launch is the plan's last; its last workgroup finalizes
 };
 

@@ -1200,43 +1200,15 @@ __device__ __forceinline__ void fused_flush(cquery_t &aq, cseg_t &seg, const PHI
   fused_batch<NA, kFusedBatch, true>(aq, seg, tz, d, act, sda, sdb, acc);
 }
 
-// A dense tile projected in place: lane-major groups (lane l: doc 64g + l), kFusedDenseBatch groups per round trip,
-// every column read coalesced (a 4-B doc-order value column: 256 B per group and wave-instruction) instead of per-doc
-// gathers through the ring. When most 64-B lines of a value column hold a matched doc anyway (density >~ 8 %), the
-// gather moves the same lines with 64 distinct addresses per instruction; this moves them 4 lines per instruction.
-#ifndef PHIP_FUSED_DENSE_BATCH
-#define PHIP_FUSED_DENSE_BATCH 8
-#endif
-constexpr int kFusedDenseBatch = PHIP_FUSED_DENSE_BATCH;
-template <int NA>
-__device__ __forceinline__ void fused_dense_tile(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
-                                                 const SmallDict (&sda)[NA], const SmallDict (&sdb)[NA],
-                                                 uint64_t (&acc)[NA]) {
-  const int lane = lane_id();
-  const int32_t last = t.valid_docs - 1;
-#pragma unroll 1
-  for (int g0 = 0; g0 < kTileGroups; g0 += kFusedDenseBatch) {
-    // bit u of act = group g0 + u (bit 31 - g of the mask is doc 64g + lane)
-    const uint32_t act = __builtin_bitreverse32(mask << g0) & ((1u << kFusedDenseBatch) - 1u);
-    if (ballot(act != 0) == 0) continue;
-    int32_t td[kFusedDenseBatch];
-#pragma unroll
-    for (int u = 0; u < kFusedDenseBatch; u++) td[u] = min(64 * (g0 + u) + lane, last);
-    fused_batch<NA, kFusedDenseBatch, false>(aq, seg, t, td, act, sda, sdb, acc);
-  }
-}
-
-// deferred mode: append the tile's matched docs; a full batch is projected at once. A tile with at least
-// dense_min matched docs is projected in place instead (fused_dense_tile); the ring keeps its pending docs.
+// deferred mode: append the tile's matched docs; a full batch is projected at once
+// (Measured and not kept, round 5: dense tiles projected in place, lane-major, 8 groups per round trip -- sorted
+// Q1.1 0.180 -> 0.374 ms at >= 256 matched docs per tile: four dependent round trips per tile instead of one per
+// 256 deferred docs; profiles/r05e_dense.log.)
 template <int NA>
 __device__ __forceinline__ void fused_defer(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
                                             PHIP_LDS uint32_t *ring, int &head, int &tail, const SmallDict (&sda)[NA],
-                                            const SmallDict (&sdb)[NA], uint64_t (&acc)[NA], int dense_min) {
+                                            const SmallDict (&sdb)[NA], uint64_t (&acc)[NA]) {
   if (ballot(mask != 0) == 0) return;
-  if (dense_min > 0 && wave_sum_u32((uint32_t)__popc(mask)) >= (uint32_t)dense_min) {
-    fused_dense_tile<NA>(aq, seg, t, mask, sda, sdb, acc);
-    return;
-  }
   const TileRank r = rank_tile(mask);
   const int head0 = head;
   // the whole tile when the ring has room, else eighth tiles (8 lanes, <= 256 docs) each after draining the ring below
@@ -1468,8 +1440,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVE
       else *mo = mask;
     }
     if constexpr (NA > 0) {
-      if (seg.fused_defer)
-        fused_defer<NA>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail, sda, sdb, acc, q.fused_dense_min);
+      if (seg.fused_defer) fused_defer<NA>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail, sda, sdb, acc);
       else fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, docring, sda, sdb, acc);
     }
     slot = slot + 1 == nbuf ? 0 : slot + 1;

@@ -2850,10 +2850,6 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   fq.fring_bytes = fring_bytes;
   fq.xcd_walk = xcd_walk;
   {
-    const char *dm = getenv("PHIP_FUSED_DENSE_MIN");  // measurement override (0 = always through the ring)
-    fq.fused_dense_min = dm ? atoi(dm) : kFusedDenseMin;
-  }
-  {
     const char *pe = getenv("PHIP_FILTER_PROBE");
     fq.probe = pe ? atoi(pe) : 0;
     // range scans of the contiguous evaluator inline: the call's register save / restore through scratch cost

@@ -664,6 +664,7 @@ class GpuCombineOperator:
         if getattr(self, "_plan", None):
             self._lib.phip_plan_destroy(self._plan)
             self._plan = None
+        self._str_dicts = None  # (decoded entries of the destroyed plan's dictionaries)
 
     def __del__(self):
         try:
@@ -785,6 +786,15 @@ class GpuCombineOperator:
         blk.segment_docs_matched = None
         return blk
 
+    def _key_values(self, k, dv, ids):
+        """Values of group-by column k's keys (`ids` into the result's query-global dictionary) as an array."""
+        if DataType(dv.data_type) == DataType.STRING and dv.string_width > 0 and len(ids):
+            cache = self.__dict__.get("_str_dicts")
+            if cache is None:
+                cache = self._str_dicts = {}
+            return _string_cache_lookup(cache, k, dv, ids)
+        return _dictionary_array(dv, ids)
+
     def key_types(self):
         """Stored types of the group-by columns, from the column metadata (the group-by block's DataSchema)."""
         return [_STORED[self.segments[0].column_metadata(e.name).data_type] for e in self.query.group_by] \
@@ -859,31 +869,29 @@ class GpuCombineOperator:
             else:
                 nk = r.num_group_by
                 keys = np.ctypeslib.as_array(r.group_keys, shape=(max(ng * nk, 1),))[:ng * nk].reshape(ng, nk) if ng else np.zeros((0, nk), np.int32)
+                # The block is columnar (the reference's DataTable keeps dictionary-encoded columns too): per group-by
+                # column the groups' key values as one array, per primitive one value array -- copied out of the
+                # library's result here; the {key tuple: intermediates} view is built on first access
+                # (GroupByResultsBlock.groups), as one list per column zipped into the groups' lists.
                 cols = []  # per group-by column: the values of the groups' keys (only the ids that occur)
                 key_space = 1  # the query-global key space: the union of the segments' values per column
                 for k in range(nk):
                     dv = _lib.DictionaryView()
                     _lib.check(lib.phip_result_dictionary(res, k, ctypes.byref(dv)))
                     key_space *= max(int(dv.cardinality), 1)
-                    cols.append(_dictionary_lookup(dv, keys[:, k]) if ng else [])
-                # column-wise (one list per primitive, then per function), zipped into the groups' lists: the
-                # per-group Python work is a few list operations (280 groups: 0.25 -> ~0.05 ms)
-                prim_cols = []
+                    cols.append(self._key_values(k, dv, keys[:, k]) if ng else np.zeros(0, np.int64))
+                prim_arrays = []
                 for i, p in enumerate(self.prims):
                     f = p[0]
                     if f == _lib.AGG_COUNT or (f == _lib.AGG_SUM and exact[i]):
-                        prim_cols.append(longs[:, i].tolist())  # (Python ints / floats, as tolist() makes them)
+                        prim_arrays.append(longs[:, i].copy())
                     elif f in (_lib.AGG_SUM, _lib.AGG_MIN, _lib.AGG_MAX):
-                        prim_cols.append(vals[:, i].tolist())
+                        prim_arrays.append(vals[:, i].copy())
                     else:
-                        mi = 1 << self.prims[i][4]
-                        prim_cols.append([hll[g, hll_slot[i], :mi].copy() for g in range(ng)])
-                fcols = [list(zip(prim_cols[sl[0]], prim_cols[sl[1]])) if fn in ("avg", "minmaxrange") else prim_cols[sl]
-                         for fn, sl in self.mapping]
-                gkeys = list(zip(*cols)) if nk else [()] * ng
-                groups = dict(zip(gkeys, map(list, zip(*fcols)))) if fcols else {k: [] for k in gkeys}
-                blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
+                        prim_arrays.append(hll[:, hll_slot[i], :1 << self.prims[i][4]])  # (hll is a copy)
+                blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), None, stats,
                                           bool(r.num_groups_limit_reached))
+                blk.set_columns(cols, prim_arrays, self.mapping)
                 blk.num_groups_trimmed = bool(r.num_groups_trimmed)
                 blk.key_space = key_space
                 blk.key_types = self.key_types()
@@ -899,6 +907,38 @@ class GpuCombineOperator:
             return blk
         finally:
             lib.phip_result_free(res)
+
+
+def _string_cache_lookup(cache, k, dv, ids):
+    """STRING group keys through a per-operator cache of decoded dictionary entries: the query-global dictionary of
+    a dictionary column is the plan's own (stable while the plan lives), so each entry is decoded once per plan
+    (lazily: only the ids some execution's groups use), not once per group and execution (Q4.3's 800 groups over two
+    STRING keys: ~1600 decodes per query before)."""
+    card, w = int(dv.cardinality), int(dv.string_width)
+    key = (k, int(dv.values or 0), card, w)
+    arr = cache.get(key)
+    if arr is None:
+        arr = cache[key] = np.empty(card, dtype=object)
+    ids = np.asarray(ids, dtype=np.int64)
+    uniq = np.unique(ids)
+    todo = uniq[np.equal(arr[uniq], None)]
+    if len(todo):
+        raw = np.ctypeslib.as_array(ctypes.cast(dv.values, ctypes.POINTER(ctypes.c_uint8)), shape=(card * w,))
+        for i, v in zip(todo.tolist(), raw.view(f"S{w}")[todo].tolist()):
+            arr[i] = v.decode("utf-8")
+    return arr[ids]
+
+
+def _dictionary_array(dv, ids):
+    """_dictionary_lookup as a numpy array (object array for STRING)."""
+    if DataType(dv.data_type) == DataType.STRING:
+        return np.array(_dictionary_lookup(dv, ids), dtype=object)
+    ids = np.asarray(ids, dtype=np.int64)
+    t = DataType(dv.data_type)
+    dt = {DataType.INT: np.int32, DataType.LONG: np.int64, DataType.FLOAT: np.float32, DataType.DOUBLE: np.float64}[t]
+    arr = np.ctypeslib.as_array(ctypes.cast(dv.values, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                shape=(max(int(dv.cardinality), 1),))
+    return arr[ids]  # (fancy indexing copies: the result's dictionary may go with the result)
 
 
 def _dictionary_lookup(dv, ids):

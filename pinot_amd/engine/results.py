@@ -53,6 +53,33 @@ class GroupByResultsBlock:
     scan_kernel_ms: float = 0.0
     key_types: Optional[List[str]] = None  # stored types of the group-by columns (column metadata: INT / LONG / ...)
 
+    def set_columns(self, key_columns, prim_columns, mapping):
+        """A columnar block (the GPU decode): per group-by column an array of the groups' key values, per primitive
+        (plan_aggregations) an array of the groups' values (HLL: [groups][registers] u8), and the functions' mapping
+        onto primitives. `groups` -- the {key tuple: intermediates} view -- is built from them on first access."""
+        self.__dict__.pop("groups", None)
+        self.key_columns, self.prim_columns, self._mapping = key_columns, prim_columns, mapping
+
+    @property
+    def num_groups(self) -> int:
+        if "groups" in self.__dict__ or not hasattr(self, "key_columns"):
+            return len(self.groups)
+        return len(self.key_columns[0]) if self.key_columns else (len(self.prim_columns[0]) if self.prim_columns else 0)
+
+    def __getattr__(self, name):
+        # (only reached when `groups` is not set: a columnar block builds its dict view once)
+        if name != "groups" or "prim_columns" not in self.__dict__:
+            raise AttributeError(name)
+        prim = [[row.copy() for row in c] if c.ndim == 2 else c.tolist() for c in self.prim_columns]
+        fcols = [list(zip(prim[sl[0]], prim[sl[1]])) if fn in ("avg", "minmaxrange") else prim[sl]
+                 for fn, sl in self._mapping]
+        cols = [c.tolist() for c in self.key_columns]
+        n = self.num_groups
+        gkeys = list(zip(*cols)) if cols else [()] * n
+        g = dict(zip(gkeys, map(list, zip(*fcols)))) if fcols else {k: [] for k in gkeys}
+        self.groups = g
+        return g
+
 
 @dataclass
 class SelectionResultsBlock:
