@@ -888,7 +888,9 @@ class GpuCombineOperator:
                     elif f in (_lib.AGG_SUM, _lib.AGG_MIN, _lib.AGG_MAX):
                         prim_arrays.append(vals[:, i].copy())
                     else:
-                        prim_arrays.append(hll[:, hll_slot[i], :1 << self.prims[i][4]])  # (hll is a copy)
+                        mi = 1 << self.prims[i][4]
+                        prim_arrays.append(hll[:, hll_slot[i], :mi] if hll is not None  # (hll is a copy)
+                                           else np.zeros((0, mi), np.uint8))
                 blk = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), None, stats,
                                           bool(r.num_groups_limit_reached))
                 blk.set_columns(cols, prim_arrays, self.mapping)

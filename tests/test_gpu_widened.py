@@ -52,7 +52,9 @@ WIDE = [
     "SELECT c0, c1, c2, c3, c4, COUNT(*), SUM(m) FROM t GROUP BY c0, c1, c2, c3, c4 LIMIT 100000",
     "SELECT c0, c1, c2, c3, c4, c5, c6, c7, SUM(m), MAX(u) FROM t WHERE f < 60 "
     "GROUP BY c0, c1, c2, c3, c4, c5, c6, c7 LIMIT 100000",
-    "SELECT s, c1, c2, c4, c6, COUNT(*), DISTINCTCOUNTHLL(u) FROM t WHERE c3 = 33 "
+    "SELECT s, c1, c2, c4, c6, COUNT(*), DISTINCTCOUNTHLL(u) FROM t WHERE c3 = 13 "
+    "GROUP BY s, c1, c2, c4, c6 LIMIT 100000",
+    "SELECT s, c1, c2, c4, c6, COUNT(*), DISTINCTCOUNTHLL(u) FROM t WHERE c3 = 33 "  # no doc matches: no group
     "GROUP BY s, c1, c2, c4, c6 LIMIT 100000",
     "SELECT c0, c1, c2, c3, c4, u, SUM(m) FROM t WHERE f < 5 GROUP BY c0, c1, c2, c3, c4, u LIMIT 100000",  # hash
     "SELECT c0, c1, c2, c3, c4, c5, SUM(m) FROM t GROUP BY c0, c1, c2, c3, c4, c5 ORDER BY SUM(m) DESC LIMIT 10",
