@@ -1200,7 +1200,11 @@ __device__ __forceinline__ void fused_flush(cquery_t &aq, cseg_t &seg, const PHI
   fused_batch<NA, kFusedBatch, true>(aq, seg, tz, d, act, sda, sdb, acc);
 }
 
-// deferred mode: append the tile's matched docs; a full batch is projected at once
+// deferred mode: append the tile's matched docs; a full batch is projected at once. (Measured and not kept, round 5:
+// the batch's loads issued when it fills and consumed after the next tile's DMA wait and evaluation -- sorted Q1.1
+// 0.157 -> 0.153 ms against the same build's synchronous batches, but the batch held across the tile cost 136 B of
+// spills per lane and the build ran slower than this one, 0.138 ms; profiles/r05k_pipe_ab_sorted.log. Lane-major
+// dense tiles projected in place, 8 groups per round trip, ran 2x slower: profiles/r05e_dense.log.)
 // (Measured and not kept, round 5: dense tiles projected in place, lane-major, 8 groups per round trip -- sorted
 // Q1.1 0.180 -> 0.374 ms at >= 256 matched docs per tile: four dependent round trips per tile instead of one per
 // 256 deferred docs; profiles/r05e_dense.log.)
@@ -1287,7 +1291,8 @@ __device__ __forceinline__ void cursor_issue(StageCursor<kS> &c, uint32_t lbase,
 }
 
 #ifndef PHIP_FUSED_WAVES
-#define PHIP_FUSED_WAVES 6  // waves per SIMD the fused launches are compiled for (A/B builds override it)
+#define PHIP_FUSED_WAVES 5  // waves per SIMD the fused launches are compiled for: the LDS admits 5 workgroups (20 waves)
+                            // per CU, and 6 left 68 B of spills per lane (sorted Q1.1 -5 %, profiles/r05j_ablib_waves.log)
 #endif
 template <bool kConjOnly, int NA>
 __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVES : 6) : 4) void filter_kernel(DevFilter q) {
