@@ -2,14 +2,14 @@
 #include "agg_kernel.h"
 
 namespace phip {
-template hipError_t launch_agg_t<1, GB_LDS, true>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
+template hipError_t launch_agg_t<1, GB_LDS, true, kAggWaves>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
                                                   hipEvent_t);
-template hipError_t launch_agg_t<1, GB_LDS, false>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
+template hipError_t launch_agg_t<1, GB_LDS, false, kAggWaves>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
                                                   hipEvent_t);
-template hipError_t launch_agg_t<1, GB_GLOBAL, true>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
+template hipError_t launch_agg_t<1, GB_GLOBAL, true, kAggWaves>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
                                                   hipEvent_t);
-template hipError_t launch_agg_t<1, GB_GLOBAL, false>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
+template hipError_t launch_agg_t<1, GB_GLOBAL, false, kAggWaves>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
                                                   hipEvent_t);
-template hipError_t launch_agg_t<1, GB_HASH, false>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
+template hipError_t launch_agg_t<1, GB_HASH, false, kAggWaves>(const DevAggQuery *, int, size_t, hipStream_t, hipEvent_t,
                                                   hipEvent_t);
 }  // namespace phip

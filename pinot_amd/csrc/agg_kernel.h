@@ -488,9 +488,12 @@ __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, 
 // the per-64-doc ring walk alone -- its smaller code and register footprint measured 8-10 % faster on
 // the sparse SSB Q1.x aggregations than a kernel that merely skips the batched path at run time.
 // For GB_LDS / GB_GLOBAL, kDense selects the batched group-by walk (group_ring_batch) instead.
-template <int NA, int MODE, bool kDense>
-__global__ __launch_bounds__(kAggBlock, (MODE == GB_LDS || MODE == GB_GLOBAL) && kDense ? 6 : 1)
+// W: waves per workgroup (8; 16 for an LDS group table so large that one workgroup fills the CU's LDS -- twice the
+// waves share the one table, so the CU keeps 16 waves of gathers in flight instead of 8: DevAggQuery.wg_waves).
+template <int NA, int MODE, bool kDense, int W = kAggWaves>
+__global__ __launch_bounds__(W * kWave, (MODE == GB_LDS || MODE == GB_GLOBAL) && kDense ? 6 : 1)
 void agg_kernel(const DevAggQuery *qptr) {
+  constexpr int kBlock = W * kWave;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   cquery_t &q = *(cquery_t *)qptr;
   const int lane = lane_id();
@@ -500,27 +503,27 @@ void agg_kernel(const DevAggQuery *qptr) {
   constexpr bool kRingFill = MODE == GB_NONE || kGbBatch;  // matched docs enter the ring by a wave prefix scan
   constexpr int R = ring_entries(MODE, kGbBatch);
   lds_u32 *ring = (lds_u32 *)lds + wave * R;
-  PHIP_LDS unsigned char *stage = lds + kAggWaves * R * 4;  // GB_NONE dense-tile staging
+  PHIP_LDS unsigned char *stage = lds + W * R * 4;  // GB_NONE dense-tile staging
   PHIP_LDS unsigned char *stg = stage + wave * q.stage_bytes;
   const uint32_t stg_lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)stg);
-  PHIP_LDS unsigned char *rest = stage + kAggWaves * q.stage_bytes;
+  PHIP_LDS unsigned char *rest = stage + W * q.stage_bytes;
   lds_u32 *hll_lds = (lds_u32 *)rest;
   lds_u64 *tbl = (lds_u64 *)rest;
   lds_u32 *hll_packed = (lds_u32 *)(rest + (size_t)q.tbl_words * 8);
   int hll_words = 0;
   if (MODE == GB_NONE && q.num_hll > 0) {
     hll_words = q.num_hll << q.log2m;
-    for (int i = threadIdx.x; i < hll_words; i += kAggBlock) hll_lds[i] = 0;
+    for (int i = threadIdx.x; i < hll_words; i += kBlock) hll_lds[i] = 0;
   }
   if (MODE == GB_LDS) {
     const int G = (int)q.num_groups;
-    for (int i = threadIdx.x; i < q.tbl_words; i += kAggBlock) {
+    for (int i = threadIdx.x; i < q.tbl_words; i += kBlock) {
       const int row = i / G;
       uint64_t init = 0;
       if (row > 0 && q.aggs[row - 1].acc == ACC_MIN_F64) init = ~0ull;  // ordered(+inf) < ~0
       tbl[i] = init;
     }
-    for (int i = threadIdx.x; i < q.hll_words; i += kAggBlock) hll_packed[i] = 0;
+    for (int i = threadIdx.x; i < q.hll_words; i += kBlock) hll_packed[i] = 0;
   }
   __syncthreads();
 
@@ -530,8 +533,8 @@ void agg_kernel(const DevAggQuery *qptr) {
   const int gx = gridDim.x >> 3;
   const int xs = (int)((int64_t)q.total_work * x / 8);
   const int xe = (int)((int64_t)q.total_work * (x + 1) / 8);
-  const int wx = gx * kAggWaves;
-  const int wid = j * kAggWaves + wave;
+  const int wx = gx * W;
+  const int wid = j * W + wave;
 
   uint64_t acc[NA];
 #pragma unroll
@@ -705,7 +708,7 @@ void agg_kernel(const DevAggQuery *qptr) {
 
   // ---- workgroup epilogue --------------------------------------------------------------------
   if constexpr (MODE == GB_NONE) {
-    __shared__ uint64_t part[kAggWaves][kMaxAggs];
+    __shared__ uint64_t part[W][kMaxAggs];
 #pragma unroll
     for (int a = 0; a < NA; a++) {
       if (a >= q.num_aggs) break;
@@ -722,37 +725,37 @@ void agg_kernel(const DevAggQuery *qptr) {
         if (a >= q.num_aggs) break;
         const int kind = q.aggs[a].acc;
         uint64_t v = part[0][a];
-        for (int w = 1; w < kAggWaves; w++) v = acc_combine(kind, v, part[w][a]);
+        for (int w = 1; w < W; w++) v = acc_combine(kind, v, part[w][a]);
         coherent_store(q.partials + (size_t)blockIdx.x * q.num_aggs + a, v);  // (read by the finalizing workgroup)
       }
     }
-    for (int i = threadIdx.x; i < hll_words; i += kAggBlock)
+    for (int i = threadIdx.x; i < hll_words; i += kBlock)
       if (hll_lds[i]) __hip_atomic_fetch_max((glb_u32 *)q.hll_regs + i, (uint32_t)hll_lds[i], PHIP_RLX, PHIP_AG);
     if (q.fin != nullptr) finalize_tail(q.fin);
   } else if constexpr (MODE == GB_LDS) {
     __syncthreads();
     glb_u64 *slab = (glb_u64 *)q.gb_table + (size_t)blockIdx.x * q.tbl_words;
-    for (int i = threadIdx.x; i < q.tbl_words; i += kAggBlock) slab[i] = tbl[i];
+    for (int i = threadIdx.x; i < q.tbl_words; i += kBlock) slab[i] = tbl[i];
     glb_u32 *hs = (glb_u32 *)q.gb_hll + (size_t)blockIdx.x * q.hll_words;
-    for (int i = threadIdx.x; i < q.hll_words; i += kAggBlock) hs[i] = hll_packed[i];
+    for (int i = threadIdx.x; i < q.hll_words; i += kBlock) hs[i] = hll_packed[i];
   }
 }
 
-template <int NA, int MODE, bool D>
+template <int NA, int MODE, bool D, int W>
 hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1) {
   if (lds > 65536) {
     // once per instantiation (a magic static: thread-safe under concurrent queries)
     static const hipError_t configured =
-        hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+        hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D, W>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
     if (configured != hipSuccess) return configured;
   }
   if (e0 != nullptr) {  // timing carried by the dispatch packet itself (hipExtLaunchKernel)
     void *args[] = {(void *)&q};
-    return hipExtLaunchKernel((const void *)agg_kernel<NA, MODE, D>, dim3(nblocks), dim3(kAggBlock), args, lds, s, e0,
+    return hipExtLaunchKernel((const void *)agg_kernel<NA, MODE, D, W>, dim3(nblocks), dim3(W * kWave), args, lds, s, e0,
                               e1, 0);
   }
-  agg_kernel<NA, MODE, D><<<nblocks, kAggBlock, lds, s>>>(q);
+  agg_kernel<NA, MODE, D, W><<<nblocks, W * kWave, lds, s>>>(q);
   return hipGetLastError();
 }
 

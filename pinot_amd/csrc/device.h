@@ -287,6 +287,8 @@ struct DevAggQuery {
   int32_t own_count_rows;  // group-by over several filter programs (FILTER + GROUP BY): every COUNT counts its own
                            // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
   const DevFinal *fin;     // GB_NONE: non-null when this launch is the plan's last (agg_common.h finalize_tail)
+  int32_t wg_waves;        // waves per workgroup of the launch (kAggWaves; 16 for a batched GB_LDS table that leaves
+  int32_t pad_w;           // one 8-wave workgroup per CU)
 };
 
 // Selection (row-returning) queries (select.hip): SelectionOnlyOperator per segment + the combine's concatenation.

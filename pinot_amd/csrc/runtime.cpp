@@ -2816,11 +2816,22 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dq.hll_words = (int32_t)hll_words;
       agg_lds += (size_t)round_up(table_bytes, 16);
       agg_bpc = std::max(1, std::min(4, (int)((160 * 1024 - 1024) / agg_lds)));
+      // A table that leaves one 8-wave workgroup per CU (Q2.1's 7000 groups x 16 B = 112 KB): 16-wave workgroups share
+      // it, so the CU keeps 16 waves of gathers in flight instead of 8 (SQ: the 8-wave walk spent 76 % of its wave
+      // cycles in s_waitcnt, profiles/r05l_sq_gb.txt). PHIP_GB_WAVES=8 keeps 8-wave workgroups (A/B).
+      const char *gw = getenv("PHIP_GB_WAVES");
+      const size_t lds16 = (size_t)16 * ring_entries(GB_LDS, batched) * 4 + (size_t)16 * dq.stage_bytes +
+                           (size_t)round_up(table_bytes, 16);
+      if (batched && agg_bpc == 1 && lds16 <= (size_t)159 * 1024 && !(gw && atoi(gw) == 8)) {
+        dq.wg_waves = 16;
+        agg_lds = lds16;
+      }
     }
   } else if (nhll) {
     agg_lds += (size_t)nhll * m_regs * 4;
   }
-  int agg_blocks = (int)std::min<int64_t>((int64_t)dev->num_cus * agg_bpc, ceil_div(total_work, kAggWaves));
+  if (dq.wg_waves == 0) dq.wg_waves = kAggWaves;
+  int agg_blocks = (int)std::min<int64_t>((int64_t)dev->num_cus * agg_bpc, ceil_div(total_work, dq.wg_waves));
   agg_blocks = (int)round_up(std::max(agg_blocks, 8), 8);  // the XCD walk needs a multiple of 8 workgroups
 
   const size_t nodes_off = blob.reserve(std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));

@@ -17,6 +17,7 @@ import dataclasses
 import math
 import os
 import re
+import struct
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Union
@@ -722,7 +723,10 @@ class GpuCombineOperator:
         return AggregationResultsBlock(self.query.aggregations, results, stats)
 
     def next_block(self):
-        if self._non_scan_fit():
+        fit = self.__dict__.get("_non_scan")  # (a function of the query and the segments: decided once)
+        if fit is None:
+            fit = self._non_scan = self._non_scan_fit()
+        if fit:
             return self._non_scan_block()
         return self._block_from_result(self.run_raw())
 
@@ -766,17 +770,18 @@ class GpuCombineOperator:
         na, ng, nhll = f[7], f[8], f[10]
         if ng != 1 or nhll:
             return None
-        vals = list((ctypes.c_double * na).from_address(f[11])) if na else []
-        longs = list((ctypes.c_int64 * na).from_address(f[12])) if na else []
-        exact = list((ctypes.c_int32 * na).from_address(f[19])) if na else []
-        pv = []
-        for i, p in enumerate(self.prims):
-            k = p[0]
-            if k == _lib.AGG_COUNT or (k == _lib.AGG_SUM and exact[i]):
-                pv.append(int(longs[i]))
-            else:
-                pv.append(float(vals[i]))
-        out = [(pv[s[0]], pv[s[1]]) if fn in ("avg", "minmaxrange") else pv[s] for fn, s in self.mapping]
+        dec = self.__dict__.get("_agg_dec")
+        if dec is None or dec[0] != na:  # (per operator: the slots' structs and each primitive's kind)
+            kinds = [0 if p[0] == _lib.AGG_COUNT else (1 if p[0] == _lib.AGG_SUM else 2) for p in self.prims]
+            pairs = [fn in ("avg", "minmaxrange") for fn, _ in self.mapping]
+            dec = self._agg_dec = (na, struct.Struct(f"<{na}d"), struct.Struct(f"<{na}q"), struct.Struct(f"<{na}i"),
+                                   kinds, pairs)
+        _, sd, sq, si, kinds, pairs = dec
+        vals = sd.unpack(ctypes.string_at(f[11], 8 * na)) if na else ()
+        longs = sq.unpack(ctypes.string_at(f[12], 8 * na)) if na else ()
+        exact = si.unpack(ctypes.string_at(f[19], 4 * na)) if na else ()
+        pv = [longs[i] if k == 0 or (k == 1 and exact[i]) else vals[i] for i, k in enumerate(kinds)]
+        out = [(pv[s[0]], pv[s[1]]) if pr else pv[s] for pr, (_, s) in zip(pairs, self.mapping)]
         blk = AggregationResultsBlock(self.query.aggregations, out, ExecutionStatistics(*f[0:6]))
         blk.scan_kernel_ms, blk.device_ms = f[15], f[16]
         blk.fused = bool(f[18])
