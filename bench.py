@@ -139,9 +139,32 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
     # one more execution per query, outside the timed region: this rank's answers, checked against the CPU
     # restatement on the same segments (check_parity)
     answers = {q: ops[q].next_block() for q in queries}
+    concurrent = None
+    if dist is None:
+        # Outside the headline: the same queries as concurrent clients (one thread per query, each running its
+        # prepared plan `steps` times back to back on its own execution lane -- a server's worker threads, DESIGN.md
+        # §7); reported beside `value`, which stays the sequential step.
+        import threading
+        barrier = threading.Barrier(len(queries) + 1)
+
+        def client(q):
+            barrier.wait()
+            for _ in range(args.steps):
+                ops[q].next_block()
+
+        threads = [threading.Thread(target=client, args=(q,)) for q in queries]
+        for th in threads:
+            th.start()
+        torch.cuda.synchronize()
+        barrier.wait()
+        t0 = time.perf_counter()
+        for th in threads:
+            th.join()
+        torch.cuda.synchronize()
+        concurrent = time.perf_counter() - t0
     for op in ops.values():
         op.close()
-    return elapsed, lat, kstats, answers
+    return elapsed, lat, kstats, answers, concurrent
 
 
 def check_parity(queries, qcs, answers, raws, dist, torch):
@@ -474,9 +497,14 @@ def main():
         head = gsegs[:head_segs]
         raws = all_raws[:head_segs]
         rows_per_rank = sum(s.num_docs for s in head)
-        elapsed, lat, kstats, answers = run_layout(args, dist, queries, qcs, head, torch)
+        elapsed, lat, kstats, answers, concurrent = run_layout(args, dist, queries, qcs, head, torch)
         res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(head),
                "lat": lat, "roofline": roofline(kstats, queries, traffic, touched, layout, args.steps)}
+        if concurrent:
+            res["concurrent"] = {"value": round(rows_per_rank * len(queries) * args.steps / concurrent / 1e9, 3),
+                                 "unit": "G rows/s", "ms_per_step": round(concurrent * 1e3 / args.steps, 4),
+                                 "note": f"{'+'.join(queries)} as {len(queries)} concurrent client threads (one per "
+                                         f"query, own execution lane each), {args.steps} executions each; not `value`"}
         if not args.no_parity:
             res["parity"] = check_parity(queries, qcs, answers, raws, dist, torch)
         log(f"rank {rank}: {layout} Q1.x timed, parity {res.get('parity', (None,))[0]}")
@@ -549,6 +577,8 @@ def main():
     }
     if "cpu" in head:
         out["cpu_baseline"] = head["cpu"]
+    if "concurrent" in head:
+        out["concurrent_clients"] = head["concurrent"]
     if not args.no_parity:
         ok = all(results[l]["parity"][0] for l in layouts) and all(head[g].get("parity") == "checked" for g in gb_legs) \
             and head.get("c5", {}).get("parity", "checked") == "checked"

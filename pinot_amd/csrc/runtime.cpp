@@ -2754,6 +2754,19 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       }
     }
     if (nbuf < 2) return fail(PHIP_ERR_UNSUPPORTED, "filter needs %d bytes of LDS per ring slot", stage_stride);
+    // A small fused query (up to 8 tiles per wave at one workgroup per CU: sorted Q1.2's ~3.8K tiles) runs one
+    // workgroup per CU with the deepest ring: its waves get several tiles each with all their DMAs in flight at once,
+    // instead of 5x the waves with one tile each and a 2-slot ring (Q1.2 fused 39.8 -> 33.6 us, profiles/r05d_q1_small.log;
+    // PHIP_FUSED_SMALL=0 keeps the width rule)
+    const char *fs = getenv("PHIP_FUSED_SMALL");
+    if (!env && fused_naggs > 0 && !(fs && atoi(fs) == 0) &&
+        total_work <= (int64_t)dev->num_cus * kFilterWaves * 8 && fbpc > 1) {
+      const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024) - 256 - fring) / ((int64_t)kFilterWaves * stage_stride));
+      if (nb >= 2) {
+        nbuf = (int)nb;
+        fbpc = 1;
+      }
+    }
   }
   const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_naggs > 0 ? (size_t)kFilterWaves * fring_bytes : 0);
   const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "xcdc" / "contig"

@@ -7,3 +7,4 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 rc=$?; echo "rc=$rc" >> gpurun_out/r05m_tests.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 400 python -u tools/gb_ab.py --queries Q2.1,Q2.2,Q2.3,Q3.1,Q4.1,Q4.2,C5 --layout sorted --reps 20 \
   --set "" --set PHIP_GB_WAVES=8 > gpurun_out/r05m_gb16.log 2>&1 || exit $?
+bash tools/host_trace.sh > gpurun_out/r05m_host_trace.log 2>&1 || exit $?
