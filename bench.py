@@ -144,24 +144,27 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
         # Outside the headline: the same queries as concurrent clients (one thread per query, each running its
         # prepared plan `steps` times back to back on its own execution lane -- a server's worker threads, DESIGN.md
         # §7); reported beside `value`, which stays the sequential step.
+        # The warm-up runs concurrently too: the library creates an execution lane (stream + scratch, ~10-20 ms) the
+        # first time a query finds every lane busy.
         import threading
         barrier = threading.Barrier(len(queries) + 1)
 
-        def client(q):
+        def client(q, n):
             barrier.wait()
-            for _ in range(args.steps):
+            for _ in range(n):
                 ops[q].next_block()
 
-        threads = [threading.Thread(target=client, args=(q,)) for q in queries]
-        for th in threads:
-            th.start()
-        torch.cuda.synchronize()
-        barrier.wait()
-        t0 = time.perf_counter()
-        for th in threads:
-            th.join()
-        torch.cuda.synchronize()
-        concurrent = time.perf_counter() - t0
+        for n in (max(args.warmup, 1), args.steps):
+            threads = [threading.Thread(target=client, args=(q, n)) for q in queries]
+            for th in threads:
+                th.start()
+            torch.cuda.synchronize()
+            barrier.wait()
+            t0 = time.perf_counter()
+            for th in threads:
+                th.join()
+            torch.cuda.synchronize()
+            concurrent = time.perf_counter() - t0
     for op in ops.values():
         op.close()
     return elapsed, lat, kstats, answers, concurrent

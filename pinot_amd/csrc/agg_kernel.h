@@ -262,15 +262,26 @@ __device__ __forceinline__ void batch_expr2_f64(cseg_t &s, cagg_t &a, const int3
   }
 }
 
-// One table word update: LDS atomics for the workgroup's table, agent-scope atomics for the HBM table.
+// One table word update: LDS atomics for the workgroup's table, agent-scope atomics for the HBM table, and for the
+// XCD-private copies (GB_XCD) workgroup-scope atomics on the copy of the XCD the wave runs on: every wave that
+// touches a copy shares that XCD's L2, where the atomic is performed (an agent-scope one goes to the memory side,
+// which serialises hot rows); the kernel's end-of-launch release writes the L2 back for xcd_merge_kernel.
+__device__ __forceinline__ int64_t xcd_copy() {
+  return (int64_t)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcdCopies - 1));  // hwreg(HW_REG_XCC_ID, 0, 4)
+}
 template <int MODE>
 __device__ __forceinline__ void tbl_add_u64(cquery_t &q, lds_u64 *tbl, int64_t i, uint64_t v) {
   if constexpr (MODE == GB_LDS) __hip_atomic_fetch_add(&tbl[i], v, PHIP_RLX, PHIP_WG);
+  else if constexpr (MODE == GB_XCD)
+    __hip_atomic_fetch_add(&((glb_u64 *)q.gb_table)[xcd_copy() * q.xcd_words + i], v, PHIP_RLX, PHIP_WG);
   else __hip_atomic_fetch_add(&((glb_u64 *)q.gb_table)[i], v, PHIP_RLX, PHIP_AG);
 }
 template <int MODE>
 __device__ __forceinline__ void tbl_add_f64(cquery_t &q, lds_u64 *tbl, int64_t i, double v) {
   if constexpr (MODE == GB_LDS) __hip_atomic_fetch_add((PHIP_LDS double *)&tbl[i], v, PHIP_RLX, PHIP_WG);
+  else if constexpr (MODE == GB_XCD)
+    __hip_atomic_fetch_add((PHIP_GLB double *)&((glb_u64 *)q.gb_table)[xcd_copy() * q.xcd_words + i], v, PHIP_RLX,
+                           PHIP_WG);
   else __hip_atomic_fetch_add((PHIP_GLB double *)&((glb_u64 *)q.gb_table)[i], v, PHIP_RLX, PHIP_AG);
 }
 template <int MODE>
@@ -278,6 +289,10 @@ __device__ __forceinline__ void tbl_minmax(cquery_t &q, lds_u64 *tbl, int64_t i,
   if constexpr (MODE == GB_LDS) {
     if (is_min) __hip_atomic_fetch_min(&tbl[i], v, PHIP_RLX, PHIP_WG);
     else __hip_atomic_fetch_max(&tbl[i], v, PHIP_RLX, PHIP_WG);
+  } else if constexpr (MODE == GB_XCD) {
+    glb_u64 *p = &((glb_u64 *)q.gb_table)[xcd_copy() * q.xcd_words + i];
+    if (is_min) __hip_atomic_fetch_min(p, v, PHIP_RLX, PHIP_WG);
+    else __hip_atomic_fetch_max(p, v, PHIP_RLX, PHIP_WG);
   } else {
     glb_u64 *p = &((glb_u64 *)q.gb_table)[i];
     if (is_min) __hip_atomic_fetch_min(p, v, PHIP_RLX, PHIP_AG);
@@ -290,6 +305,9 @@ __device__ __forceinline__ void tbl_hll(cquery_t &q, lds_u32 *hll_packed, int sl
   const int64_t G = q.num_groups;
   if constexpr (MODE == GB_LDS) {
     lds_hll_max(hll_packed + ((((int64_t)slot * G + key) << q.log2m) >> 2), reg, rho);
+  } else if constexpr (MODE == GB_XCD) {
+    glb_u32 *r = (glb_u32 *)q.gb_hll + xcd_copy() * q.xcd_hll_words + (((int64_t)slot * G + key) << q.log2m) + reg;
+    if (*r < rho) __hip_atomic_fetch_max(r, rho, PHIP_RLX, PHIP_WG);  // (a stale read only costs an atomic)
   } else {
     glb_u32 *r = (glb_u32 *)q.gb_hll + (((int64_t)slot * G + key) << q.log2m) + reg;
     if (*r < rho) __hip_atomic_fetch_max(r, rho, PHIP_RLX, PHIP_AG);
@@ -298,17 +316,18 @@ __device__ __forceinline__ void tbl_hll(cquery_t &q, lds_u32 *hll_packed, int sl
 
 constexpr int kRingGB = kRingGroupBatch;
 
-template <int MODE>
+// (U chunks of 64 ring entries per round trip from a ring of RING entries; the fused group-by of filter_kernel.h uses
+// a smaller ring and batch than the aggregation kernel)
+template <int MODE, int U = kBatch, int RING = kRingGB>
 __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const lds_u32 *ring, int tail, int n,
                                                  lds_u64 *tbl, lds_u32 *hll_packed) {
-  constexpr int U = kBatch;
   const int lane = lane_id();
   int32_t d[U];
   uint32_t act = 0;
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const bool on = 64 * u + lane < n;
-    d[u] = on ? (int32_t)ring[(tail + 64 * u + lane) & (kRingGB - 1)] : 0;  // (doc 0: a valid doc, no effect)
+    d[u] = on ? (int32_t)ring[(tail + 64 * u + lane) & (RING - 1)] : 0;  // (doc 0: a valid doc, no effect)
     act |= on ? (1u << u) : 0u;
   }
   int32_t key[U];

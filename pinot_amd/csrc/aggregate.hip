@@ -182,6 +182,42 @@ __global__ void fill_u64_kernel(uint64_t *__restrict__ p, int64_t n, uint64_t v)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// GB_XCD (the fused group-by's XCD-private table copies): every copy's rows set to their identity (0; ~0 for a MIN
+// row of order-preserving images), and after the launch copies 1.. folded into copy 0 in copy order.
+__global__ void xcd_init_kernel(uint64_t *__restrict__ tab, int64_t words, int64_t G, const int32_t *__restrict__ kinds) {
+  const int64_t n = words * kXcdCopies;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)((i % words) / G);
+    tab[i] = (row > 0 && kinds[row - 1] == ACC_MIN_F64) ? ~0ull : 0ull;
+  }
+}
+__global__ void xcd_merge_kernel(uint64_t *__restrict__ tab, int64_t words, int64_t G, const int32_t *__restrict__ kinds,
+                                 uint32_t *__restrict__ hll, int64_t hll_words) {
+  const int64_t n = words > hll_words ? words : hll_words;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < words) {
+      const int row = (int)(i / G);
+      const int kind = row == 0 ? ACC_COUNT : kinds[row - 1];
+      uint64_t v = tab[i];
+#pragma unroll
+      for (int c = 1; c < kXcdCopies; c++) {
+        const uint64_t w = tab[(int64_t)c * words + i];
+        if (kind == ACC_SUM_F64) v = as_u64(as_f64(v) + as_f64(w));
+        else if (kind == ACC_MIN_F64) v = v < w ? v : w;
+        else if (kind == ACC_MAX_F64) v = v > w ? v : w;
+        else v += w;
+      }
+      tab[i] = v;
+    }
+    if (i < hll_words) {
+      uint32_t v = hll[i];
+#pragma unroll
+      for (int c = 1; c < kXcdCopies; c++) v = max(v, hll[(int64_t)c * hll_words + i]);
+      hll[i] = v;
+    }
+  }
+}
+
 // Per 1024-group chunk: number of non-empty groups.
 __global__ __launch_bounds__(256) void group_count_kernel(const uint64_t *__restrict__ counts, int64_t n,
                                                           int32_t *__restrict__ chunk_counts) {
@@ -395,6 +431,18 @@ hipError_t launch_finalize_all(const uint64_t *pa, int nba, int na, const int32_
                                const int32_t *kf, uint64_t *segm, int nseg, uint32_t *hll, int hll_words, uint64_t *out,
                                hipStream_t s) {
   finalize_all_kernel<<<na + 3, 64, 0, s>>>(pa, nba, na, ka, pf, nbf, kf, segm, nseg, hll, hll_words, out);
+  return hipGetLastError();
+}
+hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t G, const int32_t *kinds, hipStream_t s) {
+  if (words <= 0) return hipSuccess;
+  xcd_init_kernel<<<grid_for(words * kXcdCopies), 256, 0, s>>>(tab, words, G, kinds);
+  return hipGetLastError();
+}
+hipError_t launch_xcd_merge(uint64_t *tab, int64_t words, int64_t G, const int32_t *kinds, uint32_t *hll,
+                            int64_t hll_words, hipStream_t s) {
+  const int64_t n = std::max(words, hll_words);
+  if (n <= 0) return hipSuccess;
+  xcd_merge_kernel<<<grid_for(n), 256, 0, s>>>(tab, words, G, kinds, hll, hll_words);
   return hipGetLastError();
 }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s) {

@@ -42,6 +42,10 @@ constexpr int kRingGroup = 128;
 // the batched group-by walk (GB_LDS / GB_GLOBAL, DevAggQuery::dense_batch): kBatch chunks per gather round
 // trip like GB_NONE, a tile entering in eighth-tile pieces of <= 256 docs (its LDS goes to the table)
 constexpr int kRingGroupBatch = PHIP_KBATCH <= 4 ? 512 : 1024;  // power of two >= 64 * kBatch + 256
+// fused group-by (filter_kernel.h fused_defer_gb): u32 segment doc ids per wave, flushed 128 at a time; 1 KiB per wave
+// instead of the deferred aggregation's 2 KiB keeps a resident workgroup the LDS-DMA ring would otherwise lose
+constexpr int kFusedRingGB = 256;
+constexpr int kFusedBatchGB = 2;
 constexpr int ring_entries(int mode, bool batched = false) {
   return mode == 0 ? kRingAgg : (batched ? kRingGroupBatch : kRingGroup);
 }
@@ -71,7 +75,11 @@ enum GroupMode : int32_t {
   GB_GLOBAL = 2,  // one table in HBM, global atomics
   GB_HASH = 3,    // key space too large for a dense table: open-addressing hash in HBM (slot = group),
                   // IntMapBasedHolder's role (DictionaryBasedGroupKeyGenerator.java:416-495)
+  GB_XCD = 4,     // fused group-by only (filter_kernel.h): kXcdCopies XCD-private copies of the GB_GLOBAL table, each
+                  // updated by one XCD's waves with workgroup-scope atomics (performed in that XCD's L2, not at the
+                  // memory side), merged into copy 0 by xcd_merge_kernel; the plan's mode stays GB_GLOBAL
 };
+constexpr int kXcdCopies = 8;  // MI355X: 8 XCDs (HW_REG_XCC_ID & 7)
 constexpr uint64_t kHashEmpty = ~0ull;  // empty key slot (mixed-radix keys are < 2^62)
 
 // One column as seen by one segment of a query.
@@ -289,6 +297,8 @@ struct DevAggQuery {
   const DevFinal *fin;     // GB_NONE: non-null when this launch is the plan's last (agg_common.h finalize_tail)
   int32_t wg_waves;        // waves per workgroup of the launch (kAggWaves; 16 for a batched GB_LDS table that leaves
   int32_t pad_w;           // one 8-wave workgroup per CU)
+  int64_t xcd_words;       // GB_XCD: u64 words of one table copy ((1 + num_aggs) x num_groups)
+  int64_t xcd_hll_words;   // GB_XCD: u32 words of one copy's HLL registers (num_hll x num_groups x m)
 };
 
 // Selection (row-returning) queries (select.hip): SelectionOnlyOperator per segment + the combine's concatenation.

@@ -23,7 +23,7 @@
 // projects anything; COUNT-only queries stop here (FastFilteredCountOperator.java:66-78).
 #include <hip/hip_ext.h>
 
-#include "agg_common.h"
+#include "agg_kernel.h"  // (the fused group-by flushes through agg_kernel.h's group_ring_batch)
 
 namespace phip {
 
@@ -1230,6 +1230,43 @@ __device__ __forceinline__ void fused_defer(cquery_t &aq, cseg_t &seg, const Til
   }
 }
 
+// Fused group-by (NA == kFusedGroupBy: a dense key space in an HBM table, GB_GLOBAL): the tile's matched docs are
+// appended to the same deferred ring, and every full batch goes through the aggregation kernel's batched group-by
+// walk -- key ids and remaps, then per aggregation its inputs, agent-scope atomics into the table
+// (DictionaryBasedGroupKeyGenerator.java:285-414 keys, DefaultGroupByExecutor.java:116-140 holders). The tile masks
+// never reach HBM and the second launch with its mask walk is gone.
+// NA == kFusedGroupBy: one HBM table (agent-scope atomics); NA == kFusedGroupByXcd: its XCD-private copies (GB_XCD).
+constexpr int kFusedGroupBy = -1;
+constexpr int kFusedGroupByXcd = -2;
+constexpr int kGbFlush = 64 * kFusedBatchGB;
+static_assert(kFusedRingGB >= 2 * kGbFlush, "a piece of <= kGbFlush docs lands on < kGbFlush pending");
+
+template <int MODE>
+__device__ __forceinline__ void fused_flush_gb(cquery_t &aq, cseg_t &seg, const PHIP_LDS uint32_t *ring, int tail, int n) {
+  group_ring_batch<MODE, kFusedBatchGB, kFusedRingGB>(aq, seg, (const lds_u32 *)ring, tail, n, nullptr, nullptr);
+}
+
+template <int MODE>
+__device__ __forceinline__ void fused_defer_gb(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
+                                               PHIP_LDS uint32_t *ring, int &head, int &tail) {
+  if (ballot(mask != 0) == 0) return;
+  const TileRank r = rank_tile(mask);
+  const int head0 = head;
+  // the whole tile when the ring has room, else sixteenth tiles (4 lanes, <= 128 docs) each after draining the ring
+  // below one flush (< 128 pending + 128 <= kFusedRingGB)
+  const int npiece = head - tail + r.total <= kFusedRingGB ? 1 : 16;
+  const int lanes = 64 / npiece;
+  for (int p = 0; p < npiece; p++) {
+    const int e = __builtin_amdgcn_readlane((int)r.incl, lanes * p + lanes - 1);
+    write_ranked<uint32_t, kFusedRingGB>(r, lanes * p, lanes * (p + 1), -head0, t.doc0, ring);
+    head = head0 + e;
+    while (head - tail >= kGbFlush) {
+      fused_flush_gb<MODE>(aq, seg, ring, tail, kGbFlush);
+      tail += kGbFlush;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // the filter kernel
 // ------------------------------------------------------------------------------------------------
@@ -1295,7 +1332,7 @@ __device__ __forceinline__ void cursor_issue(StageCursor<kS> &c, uint32_t lbase,
                             // per CU, and 6 left 68 B of spills per lane (sorted Q1.1 -5 %, profiles/r05j_ablib_waves.log)
 #endif
 template <bool kConjOnly, int NA>
-__global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVES : 6) : 4) void filter_kernel(DevFilter q) {
+__global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA != 0 ? PHIP_FUSED_WAVES : 6) : 4) void filter_kernel(DevFilter q) {
   constexpr int kSConj = NA > 0 ? kMaxConj + kMaxAggStage : kMaxConj;
   constexpr int kS = kConjOnly ? (kSConj < kMaxStage ? kSConj : kMaxStage) : kMaxStage;  // (DevSeg.stage size)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1332,7 +1369,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVE
   PHIP_LDS uint8_t *ring = (PHIP_LDS uint8_t *)(smem + (size_t)wave * nbuf * stride);
   // fused aggregation: the wave's matched-doc ring sits after every wave's DMA ring
   PHIP_LDS uint8_t *docring_b = (PHIP_LDS uint8_t *)(smem + (size_t)kFilterWaves * nbuf * stride) +
-                                (NA > 0 ? (size_t)wave * q.fring_bytes : 0);
+                                (NA != 0 ? (size_t)wave * q.fring_bytes : 0);
   PHIP_LDS uint16_t *docring = (PHIP_LDS uint16_t *)docring_b;
   PHIP_LDS uint32_t *deferring = (PHIP_LDS uint32_t *)docring_b;
   int dhead = 0, dtail = 0;  // deferred ring cursors (wave-uniform)
@@ -1349,6 +1386,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVE
   const int nd = q.min_dma;
   const int st = q.mask_out != nullptr ? 1 : 0;
   constexpr int NAX = NA > 0 ? NA : 1;
+  constexpr int kGbMode = NA == kFusedGroupByXcd ? GB_XCD : GB_GLOBAL;  // (NA < 0: the fused group-by's table)
   uint64_t acc[NAX];
   SmallDict sda[NAX], sdb[NAX];
   if constexpr (NA > 0) {
@@ -1389,6 +1427,13 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVE
       if constexpr (NA > 0) {  // the previous segment's deferred docs, before its small dictionaries go
         if (si >= 0 && dhead > dtail)
           fused_flush<NA>(*(cquery_t *)q.agg, segs[si], deferring, dtail, dhead - dtail, sda, sdb, acc);
+        dhead = dtail = 0;
+      }
+      if constexpr (NA < 0) {  // (the group keys are the segment's: flushed before it ends)
+        while (si >= 0 && dhead > dtail) {
+          fused_flush_gb<kGbMode>(*(cquery_t *)q.agg, segs[si], deferring, dtail, min(dhead - dtail, kGbFlush));
+          dtail += kGbFlush;
+        }
         dhead = dtail = 0;
       }
       if (si >= 0) {
@@ -1448,11 +1493,18 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA > 0 ? PHIP_FUSED_WAVE
       if (seg.fused_defer) fused_defer<NA>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail, sda, sdb, acc);
       else fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, docring, sda, sdb, acc);
     }
+    if constexpr (NA < 0) fused_defer_gb<kGbMode>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail);
     slot = slot + 1 == nbuf ? 0 : slot + 1;
   }
 #undef PHIP_PREFETCH
   if constexpr (NA > 0) {
     if (si >= 0 && dhead > dtail) fused_flush<NA>(*(cquery_t *)q.agg, segs[si], deferring, dtail, dhead - dtail, sda, sdb, acc);
+  }
+  if constexpr (NA < 0) {
+    while (si >= 0 && dhead > dtail) {
+      fused_flush_gb<kGbMode>(*(cquery_t *)q.agg, segs[si], deferring, dtail, min(dhead - dtail, kGbFlush));
+      dtail += kGbFlush;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (si >= 0) {

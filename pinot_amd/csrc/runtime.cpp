@@ -48,6 +48,9 @@ size_t chunk_decode_extra_lds(int codec, int32_t out_cap);
 hipError_t launch_sorted_to_packed(const uint32_t *be_pairs, int32_t card, int32_t *ids_tmp, int64_t n, int32_t bits,
                                    uint32_t *words, int64_t nwords, hipStream_t s);
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t s);
+hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t G, const int32_t *kinds, hipStream_t s);
+hipError_t launch_xcd_merge(uint64_t *tab, int64_t words, int64_t G, const int32_t *kinds, uint32_t *hll,
+                            int64_t hll_words, hipStream_t s);
 hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *groups, int32_t ngroups, hipStream_t s);
 hipError_t launch_filter(const DevFilter &q, bool conj_only, int fused_naggs, int nblocks, size_t lds_bytes,
                          hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
@@ -1409,6 +1412,8 @@ struct Plan {
   std::vector<ProjCol> proj;
   bool has_filter = false, need_agg = false, need_mask = false, group_by = false, conj_only = false;
   int fused_naggs = 0;  // > 0: the filter kernel aggregates (fused_tile), no aggregation launch
+  bool fused_gb = false;  // the filter kernel runs the dense group-by into the HBM table (no aggregation launch)
+  bool gb_xcd = false;    // ... into kXcdCopies XCD-private copies of it (GB_XCD), merged after the launch
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
   int filter_blocks = 1, agg_blocks = 8;
@@ -2685,6 +2690,41 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       }
     }
   }
+  // Fused group-by (filter_kernel.h fused_defer_gb): a dense key space whose table lives in HBM -- the filter kernel
+  // collects its matched docs in a deferred ring (1 KiB per wave, kFusedRingGB: half the deferred aggregation's, so
+  // the LDS-DMA ring keeps its resident workgroups on most queries) and runs the batched group-by walk itself, so
+  // neither the tile masks (256 B per tile written and read back) nor the second launch's walk over every mask remain.
+  // Its table updates are HBM atomics, which serialise on hot rows: an LDS-sized table stays with the aggregation
+  // kernel's LDS tables unless few docs hit each key (<= kFuseGbMaxPerKey expected). With at least one doc per key the
+  // table is kept once per XCD (GB_XCD: workgroup-scope atomics in the XCD's L2, folded by xcd_merge_kernel) when the
+  // eight copies fit PHIP_FUSED_GB_XCD_MAX bytes each (default 16 MiB); sparser keys keep one table (the copies' init
+  // and merge would cost more than they save). Measured on SSB SF100 unsorted, p50 (tools/gb_ab.py,
+  // profiles/r05r_xcd_ab.log, two launches -> fused): Q2.3 0.449 -> 0.357 ms (XCD copies), Q3.2 0.711 -> 0.548 (XCD),
+  // Q3.3 0.517 -> 0.520, Q3.4 0.536 -> 0.518, Q4.3 0.616 -> 0.585; hot tables fused measured 1.3-40x slower (C5 0.90 ->
+  // 5.0 ms with XCD copies, 37 ms with one table; Q2.1 0.57 -> 1.02; profiles/r05p_fgb_ab.log). PHIP_FUSED_GB: "0" off,
+  // "2" every dense table into one HBM table, "3" every dense table with XCD copies up to the cap (measurement
+  // overrides).
+  bool fused_gb = false, gb_xcd = false;
+  if (group_by && dq.mode != GB_HASH && conj_all && any_filter_prog && nprog == 1 && !want_bitmap && nsel == 0) {
+    const char *fg = getenv("PHIP_FUSED_GB");
+    const int fgm = fg ? atoi(fg) : 1;
+    const int64_t m = nhll ? ((int64_t)1 << log2m) : 0;
+    const int64_t table_bytes = (int64_t)(1 + naggs) * dq.num_groups * 8 + (int64_t)nhll * dq.num_groups * m;
+    const char *force = getenv("PHIP_GB_MODE");
+    const bool lds_sized = table_bytes <= 128 * 1024 && !(force && !strcmp(force, "global"));
+    double est_docs = 0.0;
+    for (size_t i = 0; i < dsegs.size(); i++) est_docs += seg_est[i] * dsegs[i].num_docs;
+    const double per_key = est_docs / (double)std::max<int64_t>(1, dq.num_groups);
+    const double kFuseGbMaxPerKey = 40.0;
+    const char *fx = getenv("PHIP_FUSED_GB_XCD_MAX");
+    const int64_t xcd_max = fx ? atoll(fx) : (int64_t)16 << 20;
+    fused_gb = fgm == 2 || fgm == 3 || (fgm == 1 && (!lds_sized || per_key <= kFuseGbMaxPerKey));
+    gb_xcd = fused_gb && fgm != 2 && table_bytes <= xcd_max && (fgm == 3 || per_key >= 1.0);
+    if (fused_gb) {
+      any_defer = true;
+      for (DevSeg &ds : dsegs) ds.fused_defer = 1;
+    }
+  }
   stage_stride = (int32_t)round_up(std::max(stage_stride, 16), 16);
   for (const DevSeg &ds : dsegs) {
     int64_t per_tile = 0;
@@ -2725,12 +2765,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   }
   for (int s = 0; s < nseg; s++) P.seg_docs.push_back(segs[s]->num_docs);
   const bool conj_only = conj_all;
-  if (fused_naggs > 0) need_mask = false;  // the filter kernel aggregates its own tiles
+  if (fused_naggs > 0 || fused_gb) need_mask = false;  // the filter kernel aggregates its own tiles
+  const bool fused_any = fused_naggs > 0 || fused_gb;
   // ring depth: prefer 4 workgroups (16 waves) per CU for the VALU/LDS work of the leaves, and give
   // each wave the deepest ring that then fits the 160 KiB LDS (bytes in flight per CU =
   // blocks x 4 waves x (nbuf-1) x slot)
   int nbuf = 0, fbpc = 0;
-  const int32_t fring_bytes = any_defer ? 4 * kFusedRingDefer : 2 * kFusedRingTile;  // per wave (filter.hip)
+  const int32_t fring_bytes = fused_gb ? 4 * kFusedRingGB : (any_defer ? 4 * kFusedRingDefer : 2 * kFusedRingTile);  // per wave
   {
     const char *env = getenv("PHIP_FILTER_BPC");  // measurement override
     int want = env ? std::max(1, std::min(8, atoi(env))) : (conj_only ? 6 : 4);
@@ -2742,9 +2783,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const int64_t waves_at = (int64_t)dev->num_cus * want * kFilterWaves;
     // (a fused launch keeps the full width: its waves also wait on gathers -- sorted Q1.1 fused 0.201 -> 0.187 ms at
     // 6 instead of 3 workgroups per CU, profiles/r03p_fused_bpc_ab.log)
-    if (!env && total_work >= 4 * waves_at && fused_naggs == 0)
+    if (!env && total_work >= 4 * waves_at && !fused_any)
       while (want > 2 && total_work < kMinTilesPerWave * (int64_t)dev->num_cus * want * kFilterWaves) want--;
-    const int64_t fring = fused_naggs > 0 ? (int64_t)kFilterWaves * fring_bytes : 0;  // fused doc rings
+    const int64_t fring = fused_any ? (int64_t)kFilterWaves * fring_bytes : 0;  // fused doc rings
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
       // a workgroup's share of the CU's 160 KiB, less 256 B for the kernel's static LDS (block partials)
       const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024) / bpc - 256 - fring) / ((int64_t)kFilterWaves * stage_stride));
@@ -2759,7 +2800,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // instead of 5x the waves with one tile each and a 2-slot ring (Q1.2 fused 39.8 -> 33.6 us, profiles/r05d_q1_small.log;
     // PHIP_FUSED_SMALL=0 keeps the width rule)
     const char *fs = getenv("PHIP_FUSED_SMALL");
-    if (!env && fused_naggs > 0 && !(fs && atoi(fs) == 0) &&
+    if (!env && fused_any && !(fs && atoi(fs) == 0) &&
         total_work <= (int64_t)dev->num_cus * kFilterWaves * 8 && fbpc > 1) {
       const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024) - 256 - fring) / ((int64_t)kFilterWaves * stage_stride));
       if (nb >= 2) {
@@ -2768,11 +2809,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       }
     }
   }
-  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_naggs > 0 ? (size_t)kFilterWaves * fring_bytes : 0);
+  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_any ? (size_t)kFilterWaves * fring_bytes : 0);
   const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "xcdc" / "contig"
   // contiguous per-wave ranges measured fastest for the plain filter; a fused aggregation's waves stay inside
   // their XCD's eighth of the work (its dictionaries then stay in that XCD's L2)
-  int xcd_walk = fused_naggs > 0 ? 2 : 0;
+  int xcd_walk = fused_any ? 2 : 0;
   if (walk_env) xcd_walk = !strcmp(walk_env, "xcd") ? 1 : (!strcmp(walk_env, "xcdc") ? 2 : 0);
   int64_t min_tiles_per_wave = 1;
   if (const char *mt = getenv("PHIP_FILTER_MIN_TILES")) min_tiles_per_wave = std::max(1, atoi(mt));  // A/B
@@ -2804,9 +2845,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const int64_t hll_words = (int64_t)nhll * dq.num_groups * m_regs / 4;
     const int64_t table_bytes = tbl_words * 8 + hll_words * 4;
     const char *force = getenv("PHIP_GB_MODE");  // measurement override: "lds" / "global"
-    bool use_lds = table_bytes <= 128 * 1024;
+    bool use_lds = table_bytes <= 128 * 1024 && !fused_gb;
     if (force && !strcmp(force, "global")) use_lds = false;
-    if (force && !strcmp(force, "lds") && (int64_t)agg_lds + round_up(table_bytes, 16) <= 159 * 1024) use_lds = true;
+    if (force && !strcmp(force, "lds") && !fused_gb && (int64_t)agg_lds + round_up(table_bytes, 16) <= 159 * 1024)
+      use_lds = true;
     // The batched walk (aggregate.hip group_ring_batch: kBatch chunks per gather round trip) for LDS tables, the
     // one-chunk walk for HBM tables: measured on SSB SF100 (tools/gb_ab.py, profiles/r04b_gb_ab.log) the LDS
     // group-bys gain (Q2.1 aggregation 0.45 -> 0.34 ms, Q2.2 0.20 -> 0.19, Q4.1 0.63 -> 0.56) and the sparse HBM-table
@@ -2920,13 +2962,19 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       fq.agg = (const DevAggQuery *)(base + dq_off);
     }
   }
+  if (fused_gb) fq.agg = (const DevAggQuery *)(base + dq_off);
   void *gtab = nullptr, *ghll = nullptr, *slab = nullptr, *hslab = nullptr;
   if (group_by) {
-    rc = P.alloc((size_t)(1 + naggs) * dq.num_groups * 8, &gtab);
+    const size_t copies = gb_xcd ? kXcdCopies : 1;
+    rc = P.alloc(copies * (1 + naggs) * dq.num_groups * 8, &gtab);
     if (rc) return rc;
     if (nhll) {
-      rc = P.alloc((size_t)nhll * dq.num_groups * m_regs * 4, &ghll);
+      rc = P.alloc(copies * nhll * dq.num_groups * m_regs * 4, &ghll);
       if (rc) return rc;
+    }
+    if (gb_xcd) {
+      dq.xcd_words = (int64_t)(1 + naggs) * dq.num_groups;
+      dq.xcd_hll_words = (int64_t)nhll * dq.num_groups * m_regs;
     }
     if (dq.mode == GB_HASH) {
       void *hk = nullptr, *ho = nullptr;
@@ -3070,6 +3118,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.group_by = group_by;
   P.conj_only = conj_only;
   P.fused_naggs = fused_naggs;
+  P.fused_gb = fused_gb;
+  P.gb_xcd = gb_xcd;
   P.want_bitmap = want_bitmap;
   P.filter_nwords = filter_nwords;
   P.filter_blocks = filter_blocks;
@@ -3097,7 +3147,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.first_doc = (uint32_t *)first_doc;
   if (const char *te = getenv("PHIP_TOTAL_EVENTS")) P.total_events = atoi(te) != 0;
   // ev[4] only between two launches (selection plans time their gather with it, execute_select)
-  P.split_event = P.select || (P.has_filter && P.need_agg && P.fused_naggs == 0);
+  P.split_event = P.select || (P.has_filter && P.need_agg && P.fused_naggs == 0 && !P.fused_gb);
   if (const char *se = getenv("PHIP_SPLIT_EVENT")) P.split_event = P.split_event || atoi(se) != 0;  // A/B
   for (auto &e : P.ev) HIP_TRY(hipEventCreate(&e));
   {
@@ -3210,7 +3260,10 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     HIP_TRY(hipMemsetAsync(dq.hash_overflow, 0, 4, st));
     if (P.first_doc) HIP_TRY(hipMemsetAsync(P.first_doc, 0xff, (size_t)dq.num_groups * 4, st));
   }
-  if (group_by && (dq.mode == GB_GLOBAL || dq.mode == GB_HASH)) {
+  if (group_by && P.gb_xcd) {  // every XCD-private copy at its identity
+    HIP_TRY(launch_xcd_init((uint64_t *)gtab, dq.xcd_words, dq.num_groups, dev_kinds, st));
+    if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)kXcdCopies * dq.xcd_hll_words * 4, st));
+  } else if (group_by && (dq.mode == GB_GLOBAL || dq.mode == GB_HASH)) {
     HIP_TRY(hipMemsetAsync(gtab, 0, (size_t)dq.num_groups * 8, st));  // counts
     for (int a = 0; a < naggs; a++) {
       uint64_t init = 0;
@@ -3219,7 +3272,7 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     }
     if (nhll) HIP_TRY(hipMemsetAsync(ghll, 0, (size_t)nhll * dq.num_groups * m_regs * 4, st));
   }
-  const bool fused = P.fused_naggs > 0;
+  const bool fused = P.fused_naggs > 0 || P.fused_gb;
   // Opt-in (PHIP_EXT_EVENTS=1): a one-kernel plan's timing events recorded by the kernel's own dispatch packet
   // (hipExtLaunchKernel) instead of two barrier-packet markers. Measured on the sorted headline it costs more than it
   // saves: enqueue 7.0 -> 9.8 us per query, step 0.286 -> 0.304 ms (profiles/r04p_host_ab.log).
@@ -3229,12 +3282,16 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   hipEvent_t e0 = ext_events ? P.ev[1] : nullptr, e1 = ext_events ? P.ev[2] : nullptr;
   if (!ext_events) HIP_TRY(hipEventRecord(P.ev[1], st));
   if (has_filter && total_work > 0)
-    HIP_TRY(launch_filter(fq, conj_only, P.fused_naggs, filter_blocks, filter_lds, st, e0, e1));
+    HIP_TRY(launch_filter(fq, conj_only, P.fused_gb ? (P.gb_xcd ? -2 : -1) : P.fused_naggs, filter_blocks, filter_lds, st,
+                          e0, e1));
   // (a plan of one kernel -- fused, or a filter or aggregation alone -- needs no split event)
   if (P.split_event) HIP_TRY(hipEventRecord(P.ev[4], st));
   if (need_agg && total_work > 0 && !fused)
     HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st, e0, e1));
   if (!ext_events) HIP_TRY(hipEventRecord(P.ev[2], st));
+  if (group_by && P.gb_xcd && total_work > 0)  // the XCD-private copies folded into copy 0 (the plan's table)
+    HIP_TRY(launch_xcd_merge((uint64_t *)gtab, dq.xcd_words, dq.num_groups, dev_kinds, (uint32_t *)ghll,
+                             dq.xcd_hll_words, st));
   if (group_by && dq.mode == GB_LDS && total_work > 0)
     HIP_TRY(launch_slab_reduce((const uint64_t *)slab, agg_blocks, dq.tbl_words, dq.num_groups, dev_kinds,
                                (uint64_t *)gtab, (const uint32_t *)hslab, nhll ? dq.hll_words : 0, (uint32_t *)ghll, st));
@@ -3331,6 +3388,23 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
   for (int a = 0; a < naggs; a++)
     HIP_TRY(launch_fill_u64((uint64_t *)tab + (int64_t)(1 + a) * cap, cap, dq.aggs[a].acc == ACC_MIN_F64 ? ~0ull : 0ull, st));
   if (nhll) HIP_TRY(hipMemsetAsync(hll, 0, (size_t)nhll * cap * m_regs * 4, st));
+  if (P.fused_gb && P.total_work > 0) {
+    // the fused group-by left no tile masks: the plain conjunctive filter writes them into scratch (its matched-doc
+    // counts and partials into scratch too: the statistics were read after the normal pass)
+    void *lm, *lp, *ls;
+    if ((rc = ws.get("lim_masks", (size_t)P.total_work * 64 * 4, &lm))) return rc;
+    if ((rc = ws.get("lim_fpart", (size_t)P.filter_blocks * 2 * 8, &lp))) return rc;
+    if ((rc = ws.get("lim_segm", (size_t)std::max(P.nmatch, 1) * 8, &ls))) return rc;
+    HIP_TRY(hipMemsetAsync(ls, 0, (size_t)std::max(P.nmatch, 1) * 8, st));
+    DevFilter fq = P.fq;
+    fq.agg = nullptr;
+    fq.fin = nullptr;
+    fq.mask_out = (uint32_t *)lm;
+    fq.partials = (uint64_t *)lp;
+    fq.seg_matched = (uint64_t *)ls;
+    HIP_TRY(launch_filter(fq, true, 0, P.filter_blocks, P.filter_lds, st, nullptr, nullptr));
+    dq.mask = (const uint32_t *)lm;
+  }
   HIP_TRY(hipMemcpyAsync(ddq, &dq, sizeof(dq), hipMemcpyHostToDevice, st));
   if (P.total_work > 0)
     HIP_TRY(launch_agg(dq, (const DevAggQuery *)ddq, P.agg_blocks, (size_t)kAggWaves * kRingGroup * 4, st));
@@ -3895,7 +3969,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   if (P.split_event) {
     HIP_TRY(hipEventElapsedTime(&t_filter, P.ev[1], P.ev[4]));
     HIP_TRY(hipEventElapsedTime(&t_agg, P.ev[4], P.ev[2]));
-  } else if (has_filter && !(need_agg && !P.fused_naggs)) {
+  } else if (has_filter && !(need_agg && !P.fused_naggs && !P.fused_gb)) {
     t_filter = t_scan;  // the one kernel between ev[1] and ev[2] is the filter (fused or not)
   } else {
     t_agg = t_scan;
@@ -3918,7 +3992,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     }
     r.agg_bytes = ab;
   }
-  if (P.fused_naggs > 0) {  // one kernel filtered and aggregated: it owns both times and both byte counts
+  if (P.fused_naggs > 0 || P.fused_gb) {  // one kernel filtered and aggregated: it owns both times and both byte counts
     r.fused = 1;
     r.filter_kernel_ms = t_filter + t_agg;
     r.agg_kernel_ms = 0.0;

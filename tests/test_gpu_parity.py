@@ -339,6 +339,64 @@ def test_gpu_ssb_vs_oracle(name, ssb_segments):
             _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
 
 
+# ---- fused group-by (filter_kernel.h fused_defer_gb): the filter kernel runs the dense HBM-table walk ------
+GB_SSB = [n for n in SSB_NAMES if not n.startswith("Q1")]
+
+
+@pytest.mark.parametrize("mode", ["2", "3"], ids=["hbm_table", "xcd_copies"])
+@pytest.mark.parametrize("name", GB_SSB)
+def test_gpu_ssb_fused_group_by(name, mode, ssb_segments, monkeypatch):
+    """PHIP_FUSED_GB=2 fuses every dense group-by into one HBM table (the LDS-sized tables too), =3 into XCD-private
+    copies merged after the launch (tables up to PHIP_FUSED_GB_XCD_MAX): the same groups, sums and HLL registers as
+    the oracle, and the one launch reports itself fused. (Over the sorted layout a segment whose date predicate is an
+    OR of two doc ranges takes the general filter program, which does not fuse.)"""
+    from tools import ssb
+    monkeypatch.setenv("PHIP_FUSED_GB", mode)
+    raws, segs = ssb_segments
+    qc = parse(ssb.SSB_QUERIES[name])
+    gblk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
+    if not raws[0].columns["D_YEAR"].metadata.is_sorted:
+        assert gblk.fused
+    if gblk.fused:
+        assert gblk.agg_kernel_ms == 0.0
+    oblk, exact = executor.execute(qc, raws)
+    assert gblk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+    assert set(gblk.groups) == set(oblk.groups)
+    for k, v in oblk.groups.items():
+        _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
+
+
+@pytest.mark.parametrize("limit", [10 ** 9, 5000], ids=["no_limit", "limit_reached"])
+def test_gpu_fused_group_by_limit_pass(limit, gpu_lib):
+    """A 240K-key dense space (HBM table: fused by default) over 3 segments with different dictionaries. With
+    numGroupsLimit 5000 the limit pass runs, which first has the plain filter write the tile masks the fused launch
+    never produced; both ways every group equals the oracle's."""
+    rng = np.random.default_rng(43)
+    raws = []
+    for k in range(3):
+        n = 120_000 + 511 * k
+        c = SegmentCreator(f"fl{k}")
+        c.add_column("a", DataType.INT, rng.integers(0, 600, n))
+        c.add_column("b", DataType.LONG, rng.integers(0, 400, n) * 5 + 1)
+        c.add_column("f", DataType.INT, rng.integers(0, 100, n))
+        c.add_column("m", DataType.LONG, rng.integers(-10 ** 9, 10 ** 9, n))
+        raws.append(c.build())
+    segs = [GpuSegment(r) for r in raws]
+    try:
+        qc = parse("SELECT a, b, COUNT(*), SUM(m), MAX(m) FROM t WHERE f < 70 AND a >= 3 GROUP BY a, b LIMIT 10000000")
+        gblk = GpuInstancePlanMaker(num_groups_limit=limit).make_instance_plan(qc, segs).next_block()
+        oblk, exact = executor.execute(qc, raws, num_groups_limit=limit)
+        assert gblk.fused
+        assert gblk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+        assert gblk.num_groups_limit_reached == oblk.num_groups_limit_reached == (limit == 5000)
+        assert set(gblk.groups) == set(oblk.groups)
+        for k, v in oblk.groups.items():
+            _assert_intermediates_equal(qc.aggregations, gblk.groups[k], v, exact[k])
+    finally:
+        for s in segs:
+            s.destroy()
+
+
 # ---- dense tiles: batched lane-major aggregation walk vs per-64-doc chunks vs the oracle ------------
 DENSE_QUERIES = [
     "SELECT COUNT(*), SUM(a), SUM(r), SUM(d), MIN(d), MAX(a), MIN(r), DISTINCTCOUNTHLL(a) FROM t",
