@@ -115,7 +115,7 @@ hipError_t launch_roaring_or(const RoaringTask *tasks, const RoaringGroup *group
 }
 
 
-// the seven filter_kernel instantiations, one translation unit each (filter_k*.hip)
+// the eight filter_kernel instantiations, one translation unit each (filter_k*.hip)
 hipError_t launch_filter_general(const DevFilter &, int, size_t, hipStream_t, hipEvent_t, hipEvent_t);
 hipError_t launch_filter_conj(const DevFilter &, int, size_t, hipStream_t, hipEvent_t, hipEvent_t);
 hipError_t launch_filter_fused1(const DevFilter &, int, size_t, hipStream_t, hipEvent_t, hipEvent_t);
@@ -123,15 +123,17 @@ hipError_t launch_filter_fused2(const DevFilter &, int, size_t, hipStream_t, hip
 hipError_t launch_filter_fused4(const DevFilter &, int, size_t, hipStream_t, hipEvent_t, hipEvent_t);
 hipError_t launch_filter_fusedgb(const DevFilter &, int, size_t, hipStream_t, hipEvent_t, hipEvent_t);
 hipError_t launch_filter_fusedgbx(const DevFilter &, int, size_t, hipStream_t, hipEvent_t, hipEvent_t);
+hipError_t launch_filter_fusedgbl(const DevFilter &, int, size_t, hipStream_t, hipEvent_t, hipEvent_t);
 
 // conj_only: every segment's program takes the conjunctive fast path (the interpreter is compiled
 // out, which frees registers for more resident waves); fused_naggs > 0: the aggregation runs inside
 // (q.agg set, conj_only required); fused_naggs < 0: the dense group-by runs inside (q.agg set), -1 into the HBM
-// table, -2 into its XCD-private copies
+// table, -2 into its XCD-private copies, -3 into the workgroup's LDS table
 // (e0 / e1: optional start / stop events recorded by the kernel's own dispatch, hipExtLaunchKernel)
 hipError_t launch_filter(const DevFilter &q, bool conj_only, int fused_naggs, int nblocks, size_t lds_bytes,
                          hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (!conj_only) return launch_filter_general(q, nblocks, lds_bytes, s, e0, e1);
+  if (fused_naggs == -3) return launch_filter_fusedgbl(q, nblocks, lds_bytes, s, e0, e1);
   if (fused_naggs == -2) return launch_filter_fusedgbx(q, nblocks, lds_bytes, s, e0, e1);
   if (fused_naggs < 0) return launch_filter_fusedgb(q, nblocks, lds_bytes, s, e0, e1);
   if (fused_naggs == 0) return launch_filter_conj(q, nblocks, lds_bytes, s, e0, e1);

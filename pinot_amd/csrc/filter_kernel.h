@@ -1235,20 +1235,24 @@ __device__ __forceinline__ void fused_defer(cquery_t &aq, cseg_t &seg, const Til
 // walk -- key ids and remaps, then per aggregation its inputs, agent-scope atomics into the table
 // (DictionaryBasedGroupKeyGenerator.java:285-414 keys, DefaultGroupByExecutor.java:116-140 holders). The tile masks
 // never reach HBM and the second launch with its mask walk is gone.
-// NA == kFusedGroupBy: one HBM table (agent-scope atomics); NA == kFusedGroupByXcd: its XCD-private copies (GB_XCD).
+// NA == kFusedGroupBy: one HBM table (agent-scope atomics); NA == kFusedGroupByXcd: its XCD-private copies (GB_XCD);
+// NA == kFusedGroupByLds: the workgroup's table in LDS after the rings, written to its slab at the end (GB_LDS).
 constexpr int kFusedGroupBy = -1;
 constexpr int kFusedGroupByXcd = -2;
+constexpr int kFusedGroupByLds = -3;
 constexpr int kGbFlush = 64 * kFusedBatchGB;
 static_assert(kFusedRingGB >= 2 * kGbFlush, "a piece of <= kGbFlush docs lands on < kGbFlush pending");
 
 template <int MODE>
-__device__ __forceinline__ void fused_flush_gb(cquery_t &aq, cseg_t &seg, const PHIP_LDS uint32_t *ring, int tail, int n) {
-  group_ring_batch<MODE, kFusedBatchGB, kFusedRingGB>(aq, seg, (const lds_u32 *)ring, tail, n, nullptr, nullptr);
+__device__ __forceinline__ void fused_flush_gb(cquery_t &aq, cseg_t &seg, const PHIP_LDS uint32_t *ring, int tail, int n,
+                                               lds_u64 *tbl, lds_u32 *hll_packed) {
+  group_ring_batch<MODE, kFusedBatchGB, kFusedRingGB>(aq, seg, (const lds_u32 *)ring, tail, n, tbl, hll_packed);
 }
 
 template <int MODE>
 __device__ __forceinline__ void fused_defer_gb(cquery_t &aq, cseg_t &seg, const Tile &t, uint32_t mask,
-                                               PHIP_LDS uint32_t *ring, int &head, int &tail) {
+                                               PHIP_LDS uint32_t *ring, int &head, int &tail, lds_u64 *tbl,
+                                               lds_u32 *hll_packed) {
   if (ballot(mask != 0) == 0) return;
   const TileRank r = rank_tile(mask);
   const int head0 = head;
@@ -1261,7 +1265,7 @@ __device__ __forceinline__ void fused_defer_gb(cquery_t &aq, cseg_t &seg, const 
     write_ranked<uint32_t, kFusedRingGB>(r, lanes * p, lanes * (p + 1), -head0, t.doc0, ring);
     head = head0 + e;
     while (head - tail >= kGbFlush) {
-      fused_flush_gb<MODE>(aq, seg, ring, tail, kGbFlush);
+      fused_flush_gb<MODE>(aq, seg, ring, tail, kGbFlush, tbl, hll_packed);
       tail += kGbFlush;
     }
   }
@@ -1386,7 +1390,22 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA != 0 ? PHIP_FUSED_WAV
   const int nd = q.min_dma;
   const int st = q.mask_out != nullptr ? 1 : 0;
   constexpr int NAX = NA > 0 ? NA : 1;
-  constexpr int kGbMode = NA == kFusedGroupByXcd ? GB_XCD : GB_GLOBAL;  // (NA < 0: the fused group-by's table)
+  constexpr int kGbMode = NA == kFusedGroupByXcd ? GB_XCD : (NA == kFusedGroupByLds ? GB_LDS : GB_GLOBAL);
+  // (NA < 0: the fused group-by's table; GB_LDS: the workgroup's, after every wave's DMA and doc rings)
+  lds_u64 *gtbl = nullptr;
+  lds_u32 *ghll = nullptr;
+  if constexpr (NA == kFusedGroupByLds) {
+    cquery_t &aq = *(cquery_t *)q.agg;
+    gtbl = (lds_u64 *)(smem + (size_t)kFilterWaves * (nbuf * stride + q.fring_bytes));
+    ghll = (lds_u32 *)((PHIP_LDS uint8_t *)gtbl + (size_t)aq.tbl_words * 8);
+    const int G = (int)aq.num_groups;
+    for (int i = threadIdx.x; i < aq.tbl_words; i += kFilterBlock) {
+      const int row = i / G;
+      gtbl[i] = (row > 0 && aq.aggs[row - 1].acc == ACC_MIN_F64) ? ~0ull : 0ull;  // ordered(+inf) < ~0
+    }
+    for (int i = threadIdx.x; i < aq.hll_words; i += kFilterBlock) ghll[i] = 0;
+    __syncthreads();
+  }
   uint64_t acc[NAX];
   SmallDict sda[NAX], sdb[NAX];
   if constexpr (NA > 0) {
@@ -1431,7 +1450,8 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA != 0 ? PHIP_FUSED_WAV
       }
       if constexpr (NA < 0) {  // (the group keys are the segment's: flushed before it ends)
         while (si >= 0 && dhead > dtail) {
-          fused_flush_gb<kGbMode>(*(cquery_t *)q.agg, segs[si], deferring, dtail, min(dhead - dtail, kGbFlush));
+          fused_flush_gb<kGbMode>(*(cquery_t *)q.agg, segs[si], deferring, dtail, min(dhead - dtail, kGbFlush), gtbl,
+                                  ghll);
           dtail += kGbFlush;
         }
         dhead = dtail = 0;
@@ -1493,7 +1513,7 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA != 0 ? PHIP_FUSED_WAV
       if (seg.fused_defer) fused_defer<NA>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail, sda, sdb, acc);
       else fused_tile<NA>(*(cquery_t *)q.agg, seg, tl, mask, docring, sda, sdb, acc);
     }
-    if constexpr (NA < 0) fused_defer_gb<kGbMode>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail);
+    if constexpr (NA < 0) fused_defer_gb<kGbMode>(*(cquery_t *)q.agg, seg, tl, mask, deferring, dhead, dtail, gtbl, ghll);
     slot = slot + 1 == nbuf ? 0 : slot + 1;
   }
 #undef PHIP_PREFETCH
@@ -1502,7 +1522,8 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA != 0 ? PHIP_FUSED_WAV
   }
   if constexpr (NA < 0) {
     while (si >= 0 && dhead > dtail) {
-      fused_flush_gb<kGbMode>(*(cquery_t *)q.agg, segs[si], deferring, dtail, min(dhead - dtail, kGbFlush));
+      fused_flush_gb<kGbMode>(*(cquery_t *)q.agg, segs[si], deferring, dtail, min(dhead - dtail, kGbFlush), gtbl,
+                              ghll);
       dtail += kGbFlush;
     }
   }
@@ -1547,6 +1568,14 @@ __global__ __launch_bounds__(kFilterBlock, kConjOnly ? (NA != 0 ? PHIP_FUSED_WAV
         coherent_store(q.agg_partials + (size_t)blockIdx.x * aq.num_aggs + a, v);
       }
     }
+  }
+  if constexpr (NA == kFusedGroupByLds) {  // the workgroup's table -> its slab (slab_reduce_kernel folds them in order)
+    cquery_t &aq = *(cquery_t *)q.agg;
+    __syncthreads();
+    glb_u64 *slab = (glb_u64 *)aq.gb_table + (size_t)blockIdx.x * aq.tbl_words;
+    for (int i = threadIdx.x; i < aq.tbl_words; i += kFilterBlock) slab[i] = gtbl[i];
+    glb_u32 *hs = (glb_u32 *)aq.gb_hll + (size_t)blockIdx.x * aq.hll_words;
+    for (int i = threadIdx.x; i < aq.hll_words; i += kFilterBlock) hs[i] = ghll[i];
   }
   if (q.fin != nullptr) finalize_tail(q.fin);
 }

@@ -1414,6 +1414,7 @@ struct Plan {
   int fused_naggs = 0;  // > 0: the filter kernel aggregates (fused_tile), no aggregation launch
   bool fused_gb = false;  // the filter kernel runs the dense group-by into the HBM table (no aggregation launch)
   bool gb_xcd = false;    // ... into kXcdCopies XCD-private copies of it (GB_XCD), merged after the launch
+  bool gb_lds = false;    // ... into each workgroup's LDS table (GB_LDS), its slabs reduced after the launch
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
   int filter_blocks = 1, agg_blocks = 8;
@@ -2702,9 +2703,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // profiles/r05r_xcd_ab.log, two launches -> fused): Q2.3 0.449 -> 0.357 ms (XCD copies), Q3.2 0.711 -> 0.548 (XCD),
   // Q3.3 0.517 -> 0.520, Q3.4 0.536 -> 0.518, Q4.3 0.616 -> 0.585; hot tables fused measured 1.3-40x slower (C5 0.90 ->
   // 5.0 ms with XCD copies, 37 ms with one table; Q2.1 0.57 -> 1.02; profiles/r05p_fgb_ab.log). PHIP_FUSED_GB: "0" off,
-  // "2" every dense table into one HBM table, "3" every dense table with XCD copies up to the cap (measurement
-  // overrides).
-  bool fused_gb = false, gb_xcd = false;
+  // "2" every dense table into one HBM table, "3" every dense table with XCD copies up to the cap, "4" LDS-sized
+  // tables into the workgroup's LDS table (when the rings still fit beside it) (measurement overrides). The LDS table
+  // beside the filter's rings leaves 1-3 workgroups (4-12 waves) per CU for a walk that is latency-bound, so it
+  // measured slower than the separate aggregation kernel's LDS tables everywhere but Q4.1 (2.8 KB table): Q2.1 0.570 ->
+  // 0.985 ms, Q3.1 0.955 -> 1.670, Q4.2 0.628 -> 1.323, Q4.1 0.780 -> 0.765 (profiles/r05t_lds_ab.log) -- opt-in only.
+  bool fused_gb = false, gb_xcd = false, gb_lds = false;
+  int64_t gb_lds_bytes = 0;  // the fused LDS table per workgroup
   if (group_by && dq.mode != GB_HASH && conj_all && any_filter_prog && nprog == 1 && !want_bitmap && nsel == 0) {
     const char *fg = getenv("PHIP_FUSED_GB");
     const int fgm = fg ? atoi(fg) : 1;
@@ -2718,8 +2723,25 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const double kFuseGbMaxPerKey = 40.0;
     const char *fx = getenv("PHIP_FUSED_GB_XCD_MAX");
     const int64_t xcd_max = fx ? atoll(fx) : (int64_t)16 << 20;
-    fused_gb = fgm == 2 || fgm == 3 || (fgm == 1 && (!lds_sized || per_key <= kFuseGbMaxPerKey));
+    // A sorted group-by column hands each XCD's contiguous doc range a few keys at a time, so the per-key estimate
+    // (uniform keys) understates how hot its rows run: SSB Q2.3 over the layout sorted by date (D_YEAR a key) 0.454 ->
+    // 0.499 ms fused with XCD copies, against 0.457 -> 0.354 unsorted (profiles/r05w_sorted_ab.log).
+    bool sorted_key = false;
+    for (int k = 0; k < q->num_group_by; k++)
+      for (int s2 = 0; s2 < nseg; s2++)
+        sorted_key |= !segs[s2]->cols[colidx[s2][q->group_by_columns[k]]].sorted_pairs.empty();
+    fused_gb = fgm == 2 || fgm == 3 || (fgm == 1 && (!lds_sized || (per_key <= kFuseGbMaxPerKey && !sorted_key)));
     gb_xcd = fused_gb && fgm != 2 && table_bytes <= xcd_max && (fgm == 3 || per_key >= 1.0);
+    if (fgm == 4 && lds_sized) {
+      // (u64 rows, then the HLL registers packed four u8 to a u32 word: nhll x G x m bytes)
+      const int64_t lb = round_up((int64_t)(1 + naggs) * dq.num_groups * 8 + (int64_t)nhll * dq.num_groups * m, 16);
+      const int64_t ss = round_up(std::max(stage_stride, 16), 16);
+      if ((160 * 1024 - 256 - (int64_t)kFilterWaves * 4 * kFusedRingGB - lb) / ((int64_t)kFilterWaves * ss) >= 2) {
+        fused_gb = gb_lds = true;
+        gb_xcd = false;
+        gb_lds_bytes = lb;
+      }
+    }
     if (fused_gb) {
       any_defer = true;
       for (DevSeg &ds : dsegs) ds.fused_defer = 1;
@@ -2785,7 +2807,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // 6 instead of 3 workgroups per CU, profiles/r03p_fused_bpc_ab.log)
     if (!env && total_work >= 4 * waves_at && !fused_any)
       while (want > 2 && total_work < kMinTilesPerWave * (int64_t)dev->num_cus * want * kFilterWaves) want--;
-    const int64_t fring = fused_any ? (int64_t)kFilterWaves * fring_bytes : 0;  // fused doc rings
+    const int64_t fring = (fused_any ? (int64_t)kFilterWaves * fring_bytes : 0) + gb_lds_bytes;  // fused doc rings (+ table)
     for (int bpc = want; bpc >= 1 && nbuf < 2; bpc--) {
       // a workgroup's share of the CU's 160 KiB, less 256 B for the kernel's static LDS (block partials)
       const int64_t nb = std::min<int64_t>(kMaxRing, ((160 * 1024) / bpc - 256 - fring) / ((int64_t)kFilterWaves * stage_stride));
@@ -2809,7 +2831,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       }
     }
   }
-  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_any ? (size_t)kFilterWaves * fring_bytes : 0);
+  const size_t filter_lds = (size_t)kFilterWaves * nbuf * stage_stride + (fused_any ? (size_t)kFilterWaves * fring_bytes : 0) +
+                            (size_t)gb_lds_bytes;
   const char *walk_env = getenv("PHIP_FILTER_WALK");  // measurement override: "xcd" / "xcdc" / "contig"
   // contiguous per-wave ranges measured fastest for the plain filter; a fused aggregation's waves stay inside
   // their XCD's eighth of the work (its dictionaries then stay in that XCD's L2)
@@ -2845,7 +2868,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     const int64_t hll_words = (int64_t)nhll * dq.num_groups * m_regs / 4;
     const int64_t table_bytes = tbl_words * 8 + hll_words * 4;
     const char *force = getenv("PHIP_GB_MODE");  // measurement override: "lds" / "global"
-    bool use_lds = table_bytes <= 128 * 1024 && !fused_gb;
+    bool use_lds = table_bytes <= 128 * 1024 && (!fused_gb || gb_lds);
     if (force && !strcmp(force, "global")) use_lds = false;
     if (force && !strcmp(force, "lds") && !fused_gb && (int64_t)agg_lds + round_up(table_bytes, 16) <= 159 * 1024)
       use_lds = true;
@@ -2986,10 +3009,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dq.hash_overflow = (uint32_t *)ho;
     }
     if (dq.mode == GB_LDS) {
-      rc = P.alloc((size_t)agg_blocks * dq.tbl_words * 8 + 16, &slab);
+      const size_t nslabs = gb_lds ? filter_blocks : agg_blocks;  // (the fused LDS table: one slab per filter workgroup)
+      rc = P.alloc(nslabs * dq.tbl_words * 8 + 16, &slab);
       if (rc) return rc;
       if (nhll) {
-        rc = P.alloc((size_t)agg_blocks * dq.hll_words * 4 + 16, &hslab);
+        rc = P.alloc(nslabs * dq.hll_words * 4 + 16, &hslab);
         if (rc) return rc;
       }
       dq.gb_table = (uint64_t *)slab;
@@ -3120,6 +3144,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.fused_naggs = fused_naggs;
   P.fused_gb = fused_gb;
   P.gb_xcd = gb_xcd;
+  P.gb_lds = gb_lds;
   P.want_bitmap = want_bitmap;
   P.filter_nwords = filter_nwords;
   P.filter_blocks = filter_blocks;
@@ -3282,8 +3307,8 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   hipEvent_t e0 = ext_events ? P.ev[1] : nullptr, e1 = ext_events ? P.ev[2] : nullptr;
   if (!ext_events) HIP_TRY(hipEventRecord(P.ev[1], st));
   if (has_filter && total_work > 0)
-    HIP_TRY(launch_filter(fq, conj_only, P.fused_gb ? (P.gb_xcd ? -2 : -1) : P.fused_naggs, filter_blocks, filter_lds, st,
-                          e0, e1));
+    HIP_TRY(launch_filter(fq, conj_only, P.fused_gb ? (P.gb_lds ? -3 : (P.gb_xcd ? -2 : -1)) : P.fused_naggs, filter_blocks,
+                          filter_lds, st, e0, e1));
   // (a plan of one kernel -- fused, or a filter or aggregation alone -- needs no split event)
   if (P.split_event) HIP_TRY(hipEventRecord(P.ev[4], st));
   if (need_agg && total_work > 0 && !fused)
@@ -3293,7 +3318,8 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     HIP_TRY(launch_xcd_merge((uint64_t *)gtab, dq.xcd_words, dq.num_groups, dev_kinds, (uint32_t *)ghll,
                              dq.xcd_hll_words, st));
   if (group_by && dq.mode == GB_LDS && total_work > 0)
-    HIP_TRY(launch_slab_reduce((const uint64_t *)slab, agg_blocks, dq.tbl_words, dq.num_groups, dev_kinds,
+    HIP_TRY(launch_slab_reduce((const uint64_t *)slab, P.gb_lds ? filter_blocks : agg_blocks, dq.tbl_words, dq.num_groups,
+                               dev_kinds,
                                (uint64_t *)gtab, (const uint32_t *)hslab, nhll ? dq.hll_words : 0, (uint32_t *)ghll, st));
   if (group_by && dq.mode == GB_LDS && total_work == 0) {
     // nothing to reduce: the table holds every row's identity (a partial table is merged row by row)

@@ -343,19 +343,20 @@ def test_gpu_ssb_vs_oracle(name, ssb_segments):
 GB_SSB = [n for n in SSB_NAMES if not n.startswith("Q1")]
 
 
-@pytest.mark.parametrize("mode", ["2", "3"], ids=["hbm_table", "xcd_copies"])
+@pytest.mark.parametrize("mode", ["2", "3", "4"], ids=["hbm_table", "xcd_copies", "lds_table"])
 @pytest.mark.parametrize("name", GB_SSB)
 def test_gpu_ssb_fused_group_by(name, mode, ssb_segments, monkeypatch):
     """PHIP_FUSED_GB=2 fuses every dense group-by into one HBM table (the LDS-sized tables too), =3 into XCD-private
-    copies merged after the launch (tables up to PHIP_FUSED_GB_XCD_MAX): the same groups, sums and HLL registers as
-    the oracle, and the one launch reports itself fused. (Over the sorted layout a segment whose date predicate is an
-    OR of two doc ranges takes the general filter program, which does not fuse.)"""
+    copies merged after the launch (tables up to PHIP_FUSED_GB_XCD_MAX), =4 the LDS-sized tables into each workgroup's
+    LDS table (slabs reduced after the launch; other tables keep the two launches): the same groups, sums and HLL
+    registers as the oracle, and the one launch reports itself fused. (Over the sorted layout a segment whose date
+    predicate is an OR of two doc ranges takes the general filter program, which does not fuse.)"""
     from tools import ssb
     monkeypatch.setenv("PHIP_FUSED_GB", mode)
     raws, segs = ssb_segments
     qc = parse(ssb.SSB_QUERIES[name])
     gblk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
-    if not raws[0].columns["D_YEAR"].metadata.is_sorted:
+    if not raws[0].columns["D_YEAR"].metadata.is_sorted and mode != "4":
         assert gblk.fused
     if gblk.fused:
         assert gblk.agg_kernel_ms == 0.0
