@@ -198,7 +198,13 @@ typedef struct phip_query_desc {
   /* ORDER BY on group-by columns instead (takes precedence when > 0): entry j = k + 1 (ASC) or -(k + 1)
    * (DESC) for group-by column k; the query-global dictionaries are value-sorted, so id order is value order. */
   int32_t num_order_by_keys;
-  int32_t reserved0;
+  /* enableNullHandling group keys (NoDictionarySingleColumnGroupKeyGenerator.getKeyForNullValue /
+   * NoDictionaryMultiColumnGroupKeyGenerator, pinot-core/.../groupby/NoDictionary*GroupKeyGenerator.java): bit k =
+   * group-by column k's null docs (its null value vector) form one more key value, the null key -- group key id =
+   * the column's phip_dictionary_view.cardinality in phip_result.group_keys; it is counted toward numGroupsLimit in
+   * first-seen order like any key, sorts after every value in an ascending key trim and first in a descending one
+   * (the reference's default NULLS LAST / NULLS FIRST). 0 = the stored default values are the keys. */
+  int32_t null_group_by;
   const int32_t *order_by_keys;
   /* Any other ORDER BY (TableResizer, pinot-core/.../data/table/TableResizer.java:90-125,410-450): a list of
    * terms, each a group-by column or an aggregation's final result, mixed freely (takes precedence over both
@@ -307,6 +313,10 @@ typedef struct phip_result {
   /* The part of filter_bytes the filter launch STREAMS (the staged tiles' words, LDS-DMA); for a fused launch
    * filter_bytes also holds its gathers (agg_bytes folded in). The traffic calibration separates the two. */
   int64_t stream_bytes;
+  /* Per filter program (phip_query_desc.num_filter_programs entries, 1 for one program): the docs that passed it over
+   * all segments -- the reference's numDocsScanned when programs are the plan maker's own device (the null-handling
+   * group-by's IS NOT NULL programs), not FilteredGroupByOperator infos. For a phip_plan_finish result: this GPU's. */
+  const int64_t *program_docs_matched;
 } phip_result;
 
 typedef struct phip_dictionary_view {

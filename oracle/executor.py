@@ -513,19 +513,32 @@ def _agg_segment(os_, ag, docs, null_handling=False):
     raise NotImplementedError(f)
 
 
-def _group_segment(os_, query, docs, num_groups_limit):
+def _group_segment(os_, query, docs, num_groups_limit, null_handling=False):
     """One segment's GroupByOperator: first-seen group ids in doc order, capped at numGroupsLimit
     (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:1023-1048); per-doc holder updates in
     doc order (DoubleGroupByResultHolder.java:94-98, SumAggregationFunction.aggregateGroupBySV :160-180);
     HLL registers of the distinct matched values per group. Returns ({key: intermediates}, {key: exact sums},
-    limit reached)."""
+    limit reached).
+
+    null_handling (enableNullHandling: DefaultGroupByExecutor.java:106-116 takes the NoDictionary*GroupKeyGenerator
+    with null handling): a group-by column's null docs (its null value vector) key as None, one more key value that
+    joins the first-seen order like any other (NoDictionarySingleColumnGroupKeyGenerator.getKeyForNullValue,
+    :407-416); nullable functions skip null inputs per group (_group_aggregate_nullable)."""
     codes = np.zeros(len(docs), dtype=np.int64)
     uniq_vals = []
     stride = 1
     for e in query.group_by:
-        u, inv = np.unique(os_.values(e.name)[docs], return_inverse=True)
+        vals = os_.values(e.name)[docs]
+        nul = os_.nulls(e.name)[docs] if null_handling and os_.has_nulls(e.name) else None
+        if nul is not None and nul.any():
+            u, inv_nn = np.unique(vals[~nul], return_inverse=True)
+            inv = np.full(len(docs), len(u), dtype=np.int64)   # the null key: one code past the values
+            inv[~nul] = inv_nn
+            u = list(u.tolist()) + [None]
+        else:
+            u, inv = np.unique(vals, return_inverse=True)
         uniq_vals.append(u)
-        codes += inv.astype(np.int64) * stride
+        codes += np.asarray(inv).astype(np.int64) * stride
         stride *= max(len(u), 1)
     ukeys, first, inv = np.unique(codes, return_index=True, return_inverse=True)
     order = np.argsort(first, kind="stable")           # groups in first-seen (doc) order
@@ -547,7 +560,10 @@ def _group_segment(os_, query, docs, num_groups_limit):
         keys.append(tuple(k))
     per_agg, per_exact = [], []
     for ag in query.aggregations:
-        v, ex = _group_aggregate(os_, ag, docs, gid, ng)
+        if null_handling and ag.function in _NULLABLE and ag.argument is not None:
+            v, ex = _group_aggregate_nullable(os_, ag, docs, gid, ng)
+        else:
+            v, ex = _group_aggregate(os_, ag, docs, gid, ng)
         per_agg.append(v)
         per_exact.append(ex)
     groups, exact = {}, {}
@@ -596,6 +612,25 @@ def _group_aggregate(os_, ag, docs, gid, ng):
             v = mn.tolist() if f == "min" else (mx.tolist() if f == "max" else list(zip(mn.tolist(), mx.tolist())))
         else:
             raise NotImplementedError(f)
+    return v, ex
+
+
+def _group_aggregate_nullable(os_, ag, docs, gid, ng):
+    """enableNullHandling, a nullable function (NullableSingleInputAggregationFunction) per group: the docs where
+    any column of its argument is null are skipped (BaseTransformFunction's OR of the null bitmaps); a group left
+    with none is None (null), COUNT(col) counts the rest (CountAggregationFunction.java:44-160)."""
+    from pinot_amd.query.context import columns_of
+    keep = np.ones(len(docs), dtype=bool)
+    for c in columns_of(ag.argument):
+        if os_.has_nulls(c):
+            keep &= ~os_.nulls(c)[docs]
+    n_nn = np.bincount(gid[keep], minlength=ng)
+    if ag.function == "count":
+        return n_nn.tolist(), None
+    v, ex = _group_aggregate(os_, ag, docs[keep], gid[keep], ng)
+    v = [x if n_nn[g] else None for g, x in enumerate(v)]
+    if ex is not None:
+        ex = [x if n_nn[g] else None for g, x in enumerate(ex)]
     return v, ex
 
 
@@ -695,9 +730,9 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT, min_segm
                 cols.update(columns_of(ag.argument))
         for e in query.group_by:
             cols.update(columns_of(e))
-        if any(ag.filter is not None for ag in query.aggregations) or any(
+        if any(ag.filter is not None for ag in query.aggregations) and any(
                 os_.has_nulls(c) for os_, _ in per_seg for c in cols):
-            raise NotImplementedError("null group keys / per-group null results (not restated)")
+            raise NotImplementedError("FILTER + GROUP BY under null handling over columns with nulls (not restated)")
     if any(ag.filter is not None for ag in query.aggregations):
         if query.group_by:
             return _execute_filtered_group_by(query, segments, num_groups_limit)
@@ -719,7 +754,7 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT, min_segm
     for os_, docs in per_seg:
         if len(docs) == 0:
             continue
-        seg_groups, seg_exact, reached = _group_segment(os_, query, docs, num_groups_limit)
+        seg_groups, seg_exact, reached = _group_segment(os_, query, docs, num_groups_limit, nh)
         limit_reached |= reached
         if query.order_by and min_segment_group_trim_size is not None and min_segment_group_trim_size > 0:
             trim = max(5 * int(query.limit), min_segment_group_trim_size)  # GroupByUtils.getTableCapacity
@@ -727,9 +762,8 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT, min_segm
         for k, vals in seg_groups.items():
             exs = seg_exact[k]
             if k in groups:
+                exact_groups[k] = [_merge_exact(a, b, x, y) for a, b, x, y in zip(exact_groups[k], exs, groups[k], vals)]
                 groups[k] = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(query.aggregations, groups[k], vals)]
-                exact_groups[k] = [(a + b) if a is not None and b is not None else None
-                                   for a, b in zip(exact_groups[k], exs)]
             else:
                 groups[k] = vals
                 exact_groups[k] = exs

@@ -94,7 +94,7 @@ class QueryDesc(ctypes.Structure):
                 ("aggregations", ctypes.POINTER(Aggregation)), ("group_by_columns", ctypes.POINTER(ctypes.c_int32)),
                 ("num_groups_limit", ctypes.c_int64),
                 ("order_by_aggregation", ctypes.c_int32), ("order_by_desc", ctypes.c_int32),
-                ("trim_size", ctypes.c_int64), ("num_order_by_keys", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("trim_size", ctypes.c_int64), ("num_order_by_keys", ctypes.c_int32), ("null_group_by", ctypes.c_int32),
                 ("order_by_keys", ctypes.POINTER(ctypes.c_int32)),
                 ("num_order_terms", ctypes.c_int32), ("num_filter_programs", ctypes.c_int32),
                 ("order_terms", ctypes.POINTER(OrderTerm)),
@@ -117,12 +117,13 @@ class Result(ctypes.Structure):
                 ("filter_bytes", ctypes.c_int64), ("agg_bytes", ctypes.c_int64),
                 ("num_rows", ctypes.c_int64), ("num_select", ctypes.c_int32), ("reserved_select", ctypes.c_int32),
                 ("select_types", ctypes.POINTER(ctypes.c_int32)), ("select_values", ctypes.POINTER(ctypes.c_uint64)),
-                ("segment_docs_matched", ctypes.POINTER(ctypes.c_int64)), ("stream_bytes", ctypes.c_int64)]
+                ("segment_docs_matched", ctypes.POINTER(ctypes.c_int64)), ("stream_bytes", ctypes.c_int64),
+                ("program_docs_matched", ctypes.POINTER(ctypes.c_int64))]
 
 
 # phip_result's scalar image in one read (the aggregation-only fast path of plan._block_from_result): the fields in
 # declaration order, natural alignment (checked against ctypes below)
-RESULT_IMAGE = struct.Struct("<4q4iq2i4Q2d2iQ2d3q2i3Qq")
+RESULT_IMAGE = struct.Struct("<4q4iq2i4Q2d2iQ2d3q2i3QqQ")
 assert RESULT_IMAGE.size == ctypes.sizeof(Result)
 
 

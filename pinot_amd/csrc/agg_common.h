@@ -198,6 +198,7 @@ __device__ __forceinline__ int64_t group_key(cquery_t &q, cseg_t &seg, int32_t d
       const uint32_t id = col_dict_id(c, doc);
       gid = c.remap ? ((const PHIP_GLB int32_t *)c.remap)[id] : (int32_t)id;
     }
+    if (c.gb_nulls != nullptr && ((c.gb_nulls[doc >> 6] >> (doc & 63)) & 1ull)) gid = c.gb_null_id;  // the null key
     key += gid * q.gb_stride[k];
   }
   return key;

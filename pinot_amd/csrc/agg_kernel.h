@@ -121,6 +121,18 @@ __device__ __forceinline__ void batch_ids_hbm(ccol_t &c, const int32_t (&d)[U], 
   for (int u = 0; u < U; u++) id[u] = decode_bits(c.words, (uint64_t)(uint32_t)d[u] * b, b);
 }
 
+// enableNullHandling null keys: a null doc of a null-key column takes the column's null key id
+template <int U>
+__device__ __forceinline__ void batch_null_keys(ccol_t &c, const int32_t (&d)[U], uint32_t (&id)[U]) {
+  if (c.gb_nulls == nullptr) return;
+  uint64_t w[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) w[u] = c.gb_nulls[(uint32_t)d[u] >> 6];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if ((w[u] >> ((uint32_t)d[u] & 63u)) & 1ull) id[u] = (uint32_t)c.gb_null_id;
+}
+
 // one group-by column's contribution to the keys of a batch (ids, remap, stride)
 template <int U>
 __device__ __forceinline__ void batch_key_column(cquery_t &q, cseg_t &seg, int k, const int32_t (&d)[U],
@@ -137,6 +149,7 @@ __device__ __forceinline__ void batch_key_column(cquery_t &q, cseg_t &seg, int k
 #pragma unroll
     for (int u = 0; u < U; u++) id[u] = (uint32_t)(raw_i64(c, d[u]) - c.gb_base);
   }
+  batch_null_keys<U>(c, d, id);
 #pragma unroll
   for (int u = 0; u < U; u++) key[u] += (int32_t)id[u] * (int32_t)q.gb_stride[k];
 }
@@ -169,6 +182,7 @@ __device__ __forceinline__ void batch_group_keys(cquery_t &q, cseg_t &seg, const
 #pragma unroll
         for (int u = 0; u < U; u++) id[k][u] = (uint32_t)((const PHIP_GLB int32_t *)c.remap)[id[k][u]];
       }
+      batch_null_keys<U>(c, d, id[k]);
     }
   }
   // (GB_LDS / GB_GLOBAL key spaces are below 2^31: 32-bit keys and strides)

@@ -101,9 +101,12 @@ hipError_t launch_materialize(const uint32_t *words, int32_t bits, const void *d
 // Value range of a raw INT / LONG column (LE, resident), for the plan-time int64 overflow bound of
 // integer SUMs (SumAggregationFunction adds in double and never wraps, :76-101). out = {min, max},
 // preset to {INT64_MAX, INT64_MIN} by the caller.
-__global__ void minmax_i64_kernel(const void *__restrict__ raw, int32_t type, int64_t n, int64_t *__restrict__ out) {
+// (nulls: the null doc words -- those docs are skipped: the range of the non-null values -- or null)
+__global__ void minmax_i64_kernel(const void *__restrict__ raw, int32_t type, int64_t n, int64_t *__restrict__ out,
+                                  const uint64_t *__restrict__ nulls) {
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (nulls != nullptr && ((nulls[i >> 6] >> (i & 63)) & 1ull)) continue;
     const int64_t v = type == PHIP_TYPE_LONG ? ((const int64_t *)raw)[i] : (int64_t)((const int32_t *)raw)[i];
     lo = v < lo ? v : lo;
     hi = v > hi ? v : hi;
@@ -119,9 +122,9 @@ __global__ void minmax_i64_kernel(const void *__restrict__ raw, int32_t type, in
   }
 }
 
-hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s) {
+hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s, const uint64_t *nulls) {
   if (n <= 0) return hipSuccess;
-  minmax_i64_kernel<<<grid_for(n, 256, 1024), 256, 0, s>>>(raw, type, n, out);
+  minmax_i64_kernel<<<grid_for(n, 256, 1024), 256, 0, s>>>(raw, type, n, out, nulls);
   return hipGetLastError();
 }
 

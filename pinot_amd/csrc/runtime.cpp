@@ -99,7 +99,8 @@ hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t 
                                int64_t cap, int32_t naggs, int32_t own_count, const int32_t *kinds,
                                const uint64_t *table, const uint32_t *hll, int32_t nhll, int32_t log2m,
                                int64_t *keys_out, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
-hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s);
+hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s,
+                             const uint64_t *nulls = nullptr);
 hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
                                       int32_t *err, int32_t *sizes, uint8_t *lits, uint64_t lits_stride, hipStream_t s);
 hipError_t launch_bitslice(const uint32_t *words, int32_t bits, int64_t ntiles, uint32_t *planes, hipStream_t s);
@@ -366,6 +367,8 @@ struct ColumnStore {
   std::map<int, uint32_t *> hll_doc;  // per log2m: doc-order copy of hll (ensure_hll_doc), in the segment's allocations
   bool has_range = false;             // INT / LONG: value range (plan-time overflow bound of integer sums)
   int64_t vmin = 0, vmax = 0;
+  int64_t nn_vmin = 0, nn_vmax = 0;   // raw INT / LONG with a null vector: the non-null values' range (null keys);
+  bool nn_empty = false;              // nn_empty: every doc is null
   // inverted index
   uint8_t *inv_blob = nullptr;
   std::vector<int64_t> inv_begin;  // card+1 into inv_conts
@@ -983,6 +986,20 @@ static int32_t load_column(const phip_column_desc &c, Segment &seg, hipStream_t 
   if (c.null_vector != nullptr && c.null_vector_bytes > 0) {
     int32_t rc = load_null_vector(c, cs, seg, st);
     if (rc) return rc;
+    if (cs.has_range && cs.raw != nullptr && cs.nulls != nullptr && n > 0) {
+      // a raw key column's null docs hold the default null value: the null-key group-by keys the other values only
+      int64_t mm[2] = {INT64_MAX, INT64_MIN};
+      void *dmm;
+      HIP_TRY(hipMalloc(&dmm, 16));
+      temps.push_back(dmm);
+      HIP_TRY(hipMemcpyAsync(dmm, mm, 16, hipMemcpyHostToDevice, st));
+      HIP_TRY(launch_minmax_i64(cs.raw, c.data_type, n, (int64_t *)dmm, st, cs.nulls));
+      HIP_TRY(hipMemcpyAsync(mm, dmm, 16, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      cs.nn_empty = mm[0] > mm[1];
+      cs.nn_vmin = cs.nn_empty ? 0 : mm[0];
+      cs.nn_vmax = cs.nn_empty ? 0 : mm[1];
+    }
   }
   seg.by_name[cs.name] = (int)seg.cols.size();
   seg.cols.push_back(std::move(cs));
@@ -1021,6 +1038,7 @@ struct ResultImpl {
   std::vector<int32_t> sel_types;
   std::vector<std::shared_ptr<Device::Remap>> sel_dicts;  // per select column: query-global dictionary (STRING)
   std::vector<int64_t> seg_docs;  // per segment: matched docs summed over the filter programs
+  std::vector<int64_t> prog_docs;  // per filter program: matched docs summed over the segments
 };
 
 // validate a preorder subtree; returns index after it or -1
@@ -1143,11 +1161,13 @@ static int compare_value(int32_t type, const uint8_t *a, const uint8_t *b, int w
 // node-global dictionary registered for the column (phip_global_dictionary, multi-GPU servers), else the
 // sorted union of the segments' dictionaries. Per segment a dict-id -> global-id map in HBM (nullptr when
 // the segment's dictionary IS the global one).
+// (skip_nulls: a null-key column -- a raw column's id range then covers its non-null values only)
 int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
-                    const std::string &name, std::shared_ptr<Device::Remap> &out) {
+                    const std::string &name, std::shared_ptr<Device::Remap> &out, bool skip_nulls = false) {
   auto git = dev.globals.find(name);
   const Device::GlobalDict *gd = git == dev.globals.end() ? nullptr : &git->second;
   std::string key = name;
+  if (skip_nulls) key += "#nn";
   if (gd) key += "@g" + std::to_string(gd->gen);
   for (auto *s : segs) key += ":" + std::to_string(s->handle);
   auto it = dev.remaps.find(key);
@@ -1174,6 +1194,12 @@ int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::
         return fail(PHIP_ERR_UNSUPPORTED, "group-by on column %s: raw in some segments only", name.c_str());
       if (!c.has_range) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s without a value range", name.c_str());
       if (segs[i]->num_docs == 0) continue;
+      if (skip_nulls && c.nulls != nullptr) {  // (the non-null values' range)
+        if (c.nn_empty) continue;
+        lo = std::min(lo, c.nn_vmin);
+        hi = std::max(hi, c.nn_vmax);
+        continue;
+      }
       lo = std::min(lo, c.vmin);
       hi = std::max(hi, c.vmax);
     }
@@ -1392,6 +1418,7 @@ struct Plan {
   std::vector<DevSeg> dsegs;
   std::vector<RoaringTask> tasks;
   std::vector<std::shared_ptr<Device::Remap>> gb_dicts;
+  std::vector<int64_t> gb_radix;  // per group-by column: key ids (its dictionary's, + 1 for the null key)
   int nseg = 0, naggs = 0, nhll = 0, log2m = 0, m_regs = 0, num_group_by = 0, num_projected = 0;
   int nprog = 1;   // filter programs (phip_query_desc.num_filter_programs)
   int nmatch = 0;  // seg_matched slots = nprog * nseg
@@ -1917,15 +1944,22 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       int c = q->group_by_columns[k];
       std::vector<int> ci(nseg);
       for (int s = 0; s < nseg; s++) ci[s] = colidx[s][c];
+      // the null key (phip_query_desc.null_group_by): one more id, after the dictionary's, when some segment's
+      // column holds a null doc
+      bool null_key = false;
+      if ((q->null_group_by >> k) & 1)
+        for (int s = 0; s < nseg; s++) null_key |= segs[s]->cols[ci[s]].nulls != nullptr;
       std::shared_ptr<Device::Remap> r;
-      int32_t rc = build_remap(*dev, segs, ci, q->columns[c], r);
+      int32_t rc = build_remap(*dev, segs, ci, q->columns[c], r, null_key);
       if (rc) return rc;
       gb_dicts.push_back(r);
+      const int64_t radix = (int64_t)r->card + (null_key ? 1 : 0);
+      P.gb_radix.push_back(radix);
       dq.gb_cols[k] = c;
       dq.gb_stride[k] = stride;
-      if ((double)stride * (double)r->card > (double)((int64_t)1 << 62))
+      if ((double)stride * (double)radix > (double)((int64_t)1 << 62))
         return fail(PHIP_ERR_UNSUPPORTED, "group-by key space exceeds 2^62");
-      stride *= r->card;
+      stride *= radix;
     }
     // Dense table (ArrayBasedHolder's role) while the key space is small, or not much larger than the
     // docs that can create groups; above that an open-addressing hash over the keys (IntMapBasedHolder's
@@ -2019,8 +2053,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       }
     }
     for (int k = 0; k < q->num_group_by; k++) {
-      ds.cols[q->group_by_columns[k]].remap = gb_dicts[k]->dev[s];
-      if (gb_dicts[k]->raw) ds.cols[q->group_by_columns[k]].gb_base = gb_dicts[k]->raw_base;
+      DevCol &gc = ds.cols[q->group_by_columns[k]];
+      gc.remap = gb_dicts[k]->dev[s];
+      if (gb_dicts[k]->raw) gc.gb_base = gb_dicts[k]->raw_base;
+      if (P.gb_radix[k] > gb_dicts[k]->card) {  // a null-key column: its null docs (if this segment has any)
+        gc.gb_nulls = segs[s]->cols[colidx[s][q->group_by_columns[k]]].nulls;
+        gc.gb_null_id = gb_dicts[k]->card;
+      }
     }
     for (int c = 0; c < ncols; c++)
       if (col_remap[c]) ds.cols[c].remap = col_remap[c]->dev[s];
@@ -3359,7 +3398,7 @@ static int32_t group_limit(Plan &P, Workspace &ws, hipStream_t st, int64_t match
     if (drc) return drc;
   }
   int64_t space = 1;
-  for (auto &d : P.gb_dicts) space *= d->card;
+  for (int64_t r : P.gb_radix) space *= r;
   if ((double)space * (double)S >= (double)((int64_t)1 << 62))
     return fail(PHIP_ERR_UNSUPPORTED, "numGroupsLimit pass: key space x %d segments exceeds 2^62", S);
   {  // first-seen positions are program * num_docs + doc in 32 bits (aggregate.hip group_chunk_hash)
@@ -3832,14 +3871,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       KeyOrder ko{};
       ko.num_group_by = P.num_group_by;
       ko.num_keys = P.order_nkeys;
-      for (int k = 0; k < P.num_group_by; k++) ko.card[k] = gb_dicts[k]->card;
+      for (int k = 0; k < P.num_group_by; k++) ko.card[k] = P.gb_radix[k];  // (a null key sorts last ascending)
       for (int j = 0; j < P.order_nkeys; j++) {
         ko.gb[j] = (P.order_keys[j] > 0 ? P.order_keys[j] : -P.order_keys[j]) - 1;
         ko.desc[j] = P.order_keys[j] < 0;
       }
       const KeyOrder *kop = P.order_nkeys > 0 ? &ko : nullptr;
       OrderTerms ot = P.order_terms;
-      for (int k = 0; k < P.num_group_by; k++) ot.card[k] = gb_dicts[k]->card;
+      for (int k = 0; k < P.num_group_by; k++) ot.card[k] = P.gb_radix[k];
       const bool terms = ot.num_terms > 0;
       if (terms)
         HIP_TRY(launch_trim_order_terms(nullptr, nullptr, &ot, ngroups, naggs, nullptr, &sbytes, &order, st));
@@ -3909,8 +3948,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     for (int64_t g = 0; g < ngroups; g++) {
       int64_t key = hkeys[g];
       for (int k = 0; k < P.num_group_by; k++) {
-        impl->keys[g * P.num_group_by + k] = (int32_t)(key % gb_dicts[k]->card);
-        key /= gb_dicts[k]->card;
+        impl->keys[g * P.num_group_by + k] = (int32_t)(key % P.gb_radix[k]);  // (== card: the null key)
+        key /= P.gb_radix[k];
       }
     }
     impl->dicts = gb_dicts;  // (num_groups_limit_reached was set by group_limit, before any trim)
@@ -3919,7 +3958,9 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       // a raw column's result dictionary: the values its groups use, ascending; group keys re-pointed at it
       std::vector<int32_t> used;
       used.reserve(ngroups);
-      for (int64_t g = 0; g < ngroups; g++) used.push_back(impl->keys[g * P.num_group_by + k]);
+      const int32_t null_id = P.gb_radix[k] > gb_dicts[k]->card ? gb_dicts[k]->card : -1;
+      for (int64_t g = 0; g < ngroups; g++)
+        if (impl->keys[g * P.num_group_by + k] != null_id) used.push_back(impl->keys[g * P.num_group_by + k]);
       std::sort(used.begin(), used.end());
       used.erase(std::unique(used.begin(), used.end()), used.end());
       auto rd = std::make_shared<Device::Remap>();
@@ -3936,9 +3977,9 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
           memcpy(rd->values.data() + 8 * i, &v, 8);
         }
       }
-      for (int64_t g = 0; g < ngroups; g++) {
+      for (int64_t g = 0; g < ngroups; g++) {  // (the null key stays one past the values: rd->card)
         int32_t &id = impl->keys[g * P.num_group_by + k];
-        id = (int32_t)(std::lower_bound(used.begin(), used.end(), id) - used.begin());
+        id = id == null_id ? rd->card : (int32_t)(std::lower_bound(used.begin(), used.end(), id) - used.begin());
       }
       impl->dicts[k] = rd;
     }
@@ -4042,6 +4083,11 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     for (int p = 0; p < P.nprog; p++)
       impl->seg_docs[s] += has_filter ? (int64_t)segm[p * nseg + s] : P.slot_docs[p * nseg + s];
   r.segment_docs_matched = impl->seg_docs.data();
+  impl->prog_docs.assign(std::max(P.nprog, 1), 0);
+  for (int p = 0; p < P.nprog; p++)
+    for (int s = 0; s < nseg; s++)
+      impl->prog_docs[p] += has_filter ? (int64_t)segm[p * nseg + s] : P.slot_docs[p * nseg + s];
+  r.program_docs_matched = impl->prog_docs.data();
   r.num_aggregations = naggs;
   r.num_groups = group_by ? ngroups : 1;
   r.num_group_by = P.num_group_by;
@@ -4251,6 +4297,8 @@ static int32_t finish_agg_partial(Plan &P, const phip_partial *merged, phip_resu
   }
   impl->hll.assign((const uint8_t *)(h + rows + 6), (const uint8_t *)(h + rows + 6) + hbytes);
   impl->seg_docs.assign(1, 0);
+  impl->prog_docs.assign(1, 0);
+  r.program_docs_matched = impl->prog_docs.data();
   r.num_aggregations = na;
   r.num_groups = 1;
   r.num_hll = P.nhll;

@@ -468,6 +468,8 @@ def plan_aggregations(aggs: Sequence[AggregationInfo], programs: Optional[Sequen
 class GpuCombineOperator:
     """One operator over all segments of the query (the all-segment GPU variant of SURVEY.md §8b)."""
 
+    null_keys = 0  # phip_query_desc.null_group_by (set per instance under enableNullHandling)
+
     def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int,
                  segment_filters=None, programs=None):
         """segment_filters: optional per-segment (FilterContext or None, inclusive doc ranges or None) replacing
@@ -485,6 +487,14 @@ class GpuCombineOperator:
         self.stats_programs = 0  # phip_query_desc.stats_programs: 0 = every program's scans count
         self.prims, self.mapping = plan_aggregations(query.aggregations, programs[1] if programs is not None else None)
         nh = null_handling_enabled(query)
+        # enableNullHandling: the group-by columns whose null docs key as the null key (phip_query_desc.null_group_by;
+        # NoDictionary*GroupKeyGenerator with null handling, DefaultGroupByExecutor.java:106-116)
+        self.null_keys = 0
+        if nh:
+            for k, e in enumerate(query.group_by):
+                if isinstance(e, Identifier) and any(s.has_column(e.name) and s.has_null_vector(e.name)
+                                                     for s in self.segments):
+                    self.null_keys |= 1 << k
         if programs is not None:
             # program-major, as filter_offsets lays them out: program p of segment s at p * nseg + s
             self.trees = [compile_filter(s, f, nh) for f in programs[0] for s in self.segments]
@@ -558,6 +568,7 @@ class GpuCombineOperator:
         q.num_group_by = len(self.query.group_by)
         q.group_by_columns = gb
         q.num_groups_limit = self.num_groups_limit
+        q.null_group_by = self.null_keys
         q.order_by_aggregation, q.order_by_desc, q.trim_size, okeys, terms = self._trim_spec()
         if okeys:
             arr = (ctypes.c_int32 * len(okeys))(*okeys)
@@ -597,6 +608,12 @@ class GpuCombineOperator:
         gb = [str(e) for e in q.group_by]
         if len(q.order_by) > 8 or len(gb) > 8:
             return none
+        for ob in q.order_by:
+            # the device orders a null key after every value (its id is the dictionary's cardinality): the reference's
+            # default; an explicit NULLS FIRST ascending / NULLS LAST descending is left to the host's trim
+            if str(ob.expression) in gb and (self.null_keys >> gb.index(str(ob.expression))) & 1 and \
+                    ob.nulls_last is not None and ob.nulls_last != ob.ascending:
+                return none
         if all(str(ob.expression) in gb for ob in q.order_by):
             keys = [(gb.index(str(ob.expression)) + 1) * (1 if ob.ascending else -1) for ob in q.order_by]
             return -1, 0, trim, keys, []
@@ -792,7 +809,22 @@ class GpuCombineOperator:
         return blk
 
     def _key_values(self, k, dv, ids):
-        """Values of group-by column k's keys (`ids` into the result's query-global dictionary) as an array."""
+        """Values of group-by column k's keys (`ids` into the result's query-global dictionary) as an array; under
+        enableNullHandling the null key (id == the dictionary's cardinality) is None."""
+        if (self.null_keys >> k) & 1:
+            ids = np.asarray(ids)
+            isnull = ids >= dv.cardinality
+            if isnull.any():
+                out = np.empty(len(ids), dtype=object)
+                nn = ~isnull
+                if nn.any():
+                    vals = self._key_values_plain(k, dv, ids[nn])
+                    out[nn] = [v.item() if hasattr(v, "item") else v for v in vals]
+                out[isnull] = None
+                return out
+        return self._key_values_plain(k, dv, ids)
+
+    def _key_values_plain(self, k, dv, ids):
         if DataType(dv.data_type) == DataType.STRING and dv.string_width > 0 and len(ids):
             cache = self.__dict__.get("_str_dicts")
             if cache is None:
@@ -883,7 +915,7 @@ class GpuCombineOperator:
                 for k in range(nk):
                     dv = _lib.DictionaryView()
                     _lib.check(lib.phip_result_dictionary(res, k, ctypes.byref(dv)))
-                    key_space *= max(int(dv.cardinality), 1)
+                    key_space *= max(int(dv.cardinality) + ((self.null_keys >> k) & 1), 1)
                     cols.append(self._key_values(k, dv, keys[:, k]) if ng else np.zeros(0, np.int64))
                 prim_arrays = []
                 for i, p in enumerate(self.prims):
@@ -907,6 +939,8 @@ class GpuCombineOperator:
             nseg = r.num_segments_processed
             blk.segment_docs_matched = ((np.ctypeslib.as_array(r.segment_docs_matched, shape=(nseg,)).tolist() if nseg
                                          else []) if self.query.group_by and r.segment_docs_matched else None)
+            blk.program_docs_matched = ([int(r.program_docs_matched[p]) for p in range(self.num_programs)]
+                                        if self.query.group_by and r.program_docs_matched else None)
             blk.filter_kernel_ms, blk.agg_kernel_ms = r.filter_kernel_ms, r.agg_kernel_ms
             blk.filter_bytes, blk.agg_bytes = int(r.filter_bytes), int(r.agg_bytes)
             blk.stream_bytes = int(r.stream_bytes)
@@ -1802,12 +1836,12 @@ _NULLABLE = ("sum", "min", "max", "avg", "minmaxrange", "count")  # NullableSing
 
 def _null_handling_operator(query: QueryContext, segments, limit):
     """enableNullHandling (QueryContext.isNullHandlingEnabled). The filter side needs nothing here: every
-    GpuCombineOperator compiles its programs three-valued (_three_valued). This picks the aggregation side:
+    GpuCombineOperator compiles its programs three-valued (_three_valued) and keys null group-by docs as the null key
+    (GpuCombineOperator.null_keys). This picks the aggregation side:
       * aggregation only -> GpuNullHandlingAggregationOperator;
-      * group-by: the GPU operators when no group-by column and no nullable function's column has a null vector in
-        any segment (every group then holds docs with non-null values: the results are the plain ones); else the
-        null group keys (DefaultGroupByExecutor's no-dictionary generators) and per-group null results are not
-        on the GPU path: UnsupportedOnGpu. FILTER clauses and CASE with GROUP BY likewise;
+      * group-by: GpuNullHandlingGroupByOperator when a nullable function's column has a null vector in some segment
+        (per-group null results); else the regular operators (null keys, if any, come from the library). FILTER
+        clauses and CASE with GROUP BY stay UnsupportedOnGpu;
       * selection: the selected columns must be null-free (the reference returns nulls for null values);
     None = the regular operators apply."""
     def null_cols(exprs):
@@ -1826,10 +1860,121 @@ def _null_handling_operator(query: QueryContext, segments, limit):
     if query.group_by:
         if any(ag.filter is not None for ag in query.aggregations):
             raise UnsupportedOnGpu("enableNullHandling with FILTER clauses and GROUP BY")
-        if null_cols(list(query.group_by)) or null_cols(nullable_args):
-            raise UnsupportedOnGpu("enableNullHandling: group-by / aggregated columns with null values")
+        if null_cols(nullable_args):
+            return GpuNullHandlingGroupByOperator(query, segments, limit, null_cols(nullable_args))
         return None
     return GpuNullHandlingAggregationOperator(query, segments, limit, null_cols(nullable_args))
+
+
+class GpuNullHandlingGroupByOperator:
+    """GROUP BY under enableNullHandling with nullable functions over columns that hold nulls (DefaultGroupByExecutor
+    with null handling, DefaultGroupByExecutor.java:106-116: NoDictionary*GroupKeyGenerator keys the matched docs --
+    null group-by docs as the null key -- and every NullableSingleInputAggregationFunction skips the docs where its
+    argument is null, its group result null when none was left: SumAggregationFunction.aggregateGroupBySV under null
+    handling, CountAggregationFunction for COUNT(col)).
+
+    One GPU plan of filter programs over one shared key space: program 0 is the query's filter (every matched doc: it
+    generates the groups and numbers them first-seen in doc order for numGroupsLimit, the library's limit pass
+    ordering (segment, key) by (program, doc)), program p > 0 is ``filter AND c IS NOT NULL ...`` for one set of
+    null-holding argument columns, carrying the functions over them plus a hidden COUNT(*) (their non-null docs per
+    group: 0 = a null result; COUNT(col) is that count). Every program's docs are program 0's, so the groups are
+    program 0's. The statistics are the reference's single pass: numDocsScanned = program 0's matched docs
+    (phip_result.program_docs_matched), post-filter entries = those x the distinct projected columns, filter scans of
+    program 0 only. The server-level trim runs on the host after the nulls are restored (the device would order a
+    null result by its holder default)."""
+
+    _MAX_PROGRAMS = 8
+
+    def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int, null_cols):
+        self.query = query
+        self.segments = list(segments)
+        keys = [None]  # program 0: the query's filter (its docs: every group)
+        aggs, progs = [], []
+        counts = {}
+
+        def program_of(cols):
+            k = tuple(sorted(cols))
+            if k not in keys:
+                keys.append(k)
+            return keys.index(k)
+
+        def count_for(p):
+            if p not in counts:
+                counts[p] = len(aggs)
+                aggs.append(AggregationInfo("count", None))
+                progs.append(p)
+            return counts[p]
+
+        self.slots = []  # per original aggregation: (value index, non-null count index or None)
+        for ag in query.aggregations:
+            cols = [c for c in columns_of(ag.argument) if c in null_cols] if ag.argument is not None else []
+            if ag.function not in _NULLABLE or not cols:
+                self.slots.append((len(aggs), None))
+                aggs.append(ag)
+                progs.append(0)
+                continue
+            p = program_of(cols)
+            if ag.function == "count":
+                self.slots.append((count_for(p), None))
+                continue
+            if ag.function == "avg":  # (its own count is the non-null count)
+                self.slots.append((len(aggs), "avg"))
+                aggs.append(ag)
+                progs.append(p)
+                continue
+            ci = count_for(p)
+            self.slots.append((len(aggs), ci))
+            aggs.append(ag)
+            progs.append(p)
+        if len(keys) > self._MAX_PROGRAMS:
+            raise UnsupportedOnGpu("enableNullHandling GROUP BY: more than 8 sets of null-holding argument columns")
+        filters = []
+        for k in keys:
+            if k is None:
+                filters.append(query.filter)
+                continue
+            nn = [FilterContext.PRED(Predicate("IS_NOT_NULL", Identifier(c))) for c in k]
+            parts = ([query.filter] if query.filter is not None else []) + nn
+            filters.append(parts[0] if len(parts) == 1 else FilterContext.AND(*parts))
+        sub = QueryContext(query.table, [], aggs, None, list(query.group_by), [], limit=query.limit,
+                           options=dict(query.options))
+        self.op = GpuCombineOperator(sub, self.segments, num_groups_limit, programs=(filters, progs))
+        if len(self.op.prims) > 8:  # (device.h kMaxAggs primitive slots: the functions plus their non-null counts)
+            self.op.close()
+            raise UnsupportedOnGpu("enableNullHandling GROUP BY: more than 8 aggregation slots with the non-null counts")
+        self.op.stats_programs = 1  # (program 0's filter scans: the reference's one pass)
+        self.op.device_trim = False
+        proj = set()
+        for e in query.group_by:
+            proj.update(columns_of(e))
+        for ag in query.aggregations:
+            if ag.argument is not None:
+                proj.update(c for c in columns_of(ag.argument) if c != "*")
+        self.num_projected = len(proj)
+
+    def next_block(self):
+        from .reduce import trim_groups
+        blk = self.op.next_block()
+        groups = {}
+        for key, vals in blk.groups.items():
+            groups[key] = [None if (ci == "avg" and vals[vi][1] == 0) or (isinstance(ci, int) and vals[ci] == 0)
+                           else vals[vi] for vi, ci in self.slots]
+        stats = dataclasses.replace(blk.stats)
+        docs0 = blk.program_docs_matched[0] if blk.program_docs_matched else stats.num_docs_scanned
+        stats.num_docs_scanned = docs0
+        stats.num_entries_scanned_post_filter = docs0 * self.num_projected
+        out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
+                                  blk.num_groups_limit_reached)
+        out.key_types = getattr(blk, "key_types", None)
+        for k in GpuFilteredAggregationOperator._TIMES + ("fused",):
+            setattr(out, k, getattr(blk, k, 0))
+        out.segment_docs_matched = None
+        if self.query.order_by:
+            out = trim_groups(self.query, out)
+        return out
+
+    def close(self):
+        self.op.close()
 
 
 class GpuNullHandlingAggregationOperator:

@@ -43,6 +43,18 @@ def hll_cardinality(regs: np.ndarray) -> int:
     return int(math.floor(est + 0.5))
 
 
+def order_key(ob, value):
+    """Sort key of one ORDER BY expression over records (used with reverse = DESC): a null (None) value -- a null
+    group key or a null aggregation result under enableNullHandling -- goes last or first as ob.is_nulls_last says
+    (OrderByExpressionContext.isNullsLast; the comparator of TableResizer / the broker's reduce)."""
+    high = ob.is_nulls_last != (not ob.ascending)  # where nulls sit before the DESC reversal
+
+    def key(rec):
+        v = value(rec)
+        return ((v is None) if high else (v is not None), v)
+    return key
+
+
 def final_result(function: str, v):
     """AggregationFunction.extractFinalResult (a null intermediate stays null)."""
     if v is None:
@@ -145,7 +157,7 @@ def reduce_blocks(query: QueryContext, blocks) -> ResultTable:
         return finals[i]
 
     for ob in reversed(query.order_by):
-        records.sort(key=lambda rec: value_of(ob.expression, rec), reverse=not ob.ascending)
+        records.sort(key=order_key(ob, lambda rec: value_of(ob.expression, rec)), reverse=not ob.ascending)
     records = records[:query.limit]
     rows = [[value_of(e, rec) for e, _ in query.select] for rec in records]
     return ResultTable(names, rows, stats, limit_reached)
@@ -194,7 +206,7 @@ def trim_groups(query: QueryContext, block, min_trim=None):
         return block
     gb_index = {str(e): i for i, e in enumerate(query.group_by)}
     recs = [(key, [final_result(a.function, x) for a, x in zip(query.aggregations, v)]) for key, v in block.groups.items()]
-    recs.sort(key=lambda r: r[0])
+    recs.sort(key=lambda r: tuple((x is None, x) for x in r[0]))  # (a null key after the values)
 
     def value_of(expr, rec):
         if str(expr) in gb_index:
@@ -202,7 +214,7 @@ def trim_groups(query: QueryContext, block, min_trim=None):
         return rec[1][_agg_index(query, expr)]
 
     for ob in reversed(query.order_by):
-        recs.sort(key=lambda r: value_of(ob.expression, r), reverse=not ob.ascending)
+        recs.sort(key=order_key(ob, lambda r: value_of(ob.expression, r)), reverse=not ob.ascending)
     keep = {r[0] for r in recs[:k]}
     block.groups = {key: v for key, v in block.groups.items() if key in keep}
     block.num_groups_trimmed = True

@@ -164,6 +164,13 @@ class AggregationInfo:
 class OrderByExpression:
     expression: Expression
     ascending: bool = True
+    nulls_last: Optional[bool] = None  # NULLS FIRST / LAST; None = the default
+
+    @property
+    def is_nulls_last(self) -> bool:
+        """OrderByExpressionContext.isNullsLast (pinot-core/.../request/context/OrderByExpressionContext.java:53-61):
+        nulls sort as if larger than every value unless NULLS FIRST / LAST says otherwise."""
+        return self.ascending if self.nulls_last is None else self.nulls_last
 
 
 @dataclass

@@ -326,7 +326,15 @@ class _Parser:
             asc = False
         else:
             self.accept("kw", "asc")
-        return OrderByExpression(e, asc)
+        nulls_last = None
+        t = self.peek()
+        if t[0] == "ident" and str(t[1]).lower() == "nulls":  # NULLS FIRST | NULLS LAST
+            self.i += 1
+            w = self.expect("ident")[1].lower()
+            if w not in ("first", "last"):
+                raise SqlError(f"NULLS {w}: expected FIRST or LAST")
+            nulls_last = w == "last"
+        return OrderByExpression(e, asc, nulls_last)
 
 
 def _collect_aggs(expr, out, flt=None, null_handling=False):
@@ -394,7 +402,7 @@ def parse(sql: str) -> QueryContext:
         if isinstance(e, Identifier) and e.name in alias_map:
             e = alias_map[e.name]
         _collect_aggs(e, aggs, None, nh)
-        resolved_order.append(OrderByExpression(e, ob.ascending))
+        resolved_order.append(OrderByExpression(e, ob.ascending, ob.nulls_last))
     for e, _ in select:
         if isinstance(e, FilterClause):
             continue

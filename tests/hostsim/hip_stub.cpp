@@ -76,6 +76,11 @@ hipError_t launch_varbyte_copy(const uint8_t *, const uint64_t *, const int32_t 
 size_t chunk_decode_extra_lds(int, int32_t) { return 0; }
 hipError_t launch_sorted_to_packed(const uint32_t *, int32_t, int32_t *, int64_t, int32_t, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_fill_u64(uint64_t *p, int64_t n, uint64_t v, hipStream_t) { for (int64_t i = 0; i < n; i++) p[i] = v; return hipSuccess; }
+hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t, const int32_t *, hipStream_t) {
+  memset(tab, 0, (size_t)words * kXcdCopies * 8);
+  return hipSuccess;
+}
+hipError_t launch_xcd_merge(uint64_t *, int64_t, int64_t, const int32_t *, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_roaring_or(const RoaringTask *, const RoaringGroup *, int32_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_filter(const DevFilter &q, bool, int fused_naggs, int nblocks, size_t, hipStream_t, hipEvent_t,
                          hipEvent_t) {
@@ -155,7 +160,7 @@ hipError_t launch_hash_keys(int64_t *slots, int64_t n, const uint64_t *keys, hip
   for (int64_t i = 0; i < n; i++) slots[i] = (int64_t)keys[slots[i]];
   return hipSuccess;
 }
-hipError_t launch_minmax_i64(const void *, int32_t, int64_t, int64_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_minmax_i64(const void *, int32_t, int64_t, int64_t *, hipStream_t, const uint64_t *) { return hipSuccess; }
 hipError_t launch_limit_prepare(const int64_t *, int64_t, const uint64_t *, const uint32_t *, int32_t, uint64_t *,
                                 int32_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_limit_bounds(const uint64_t *, int64_t, int64_t *, int64_t *, hipStream_t) { return hipSuccess; }

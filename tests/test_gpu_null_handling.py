@@ -1,8 +1,9 @@
 """Null value vectors on the GPU (PHIP_LEAF_NULL over the resident null doc words) and enableNullHandling: three-valued
 filters (the plan's trees, plan._three_valued), null-skipping aggregations with null results
 (GpuNullHandlingAggregationOperator), COUNT(col), IS [NOT] NULL with and without null handling, and the shapes that
-stay on the CPU (null group keys, per-group nulls) -- every block against the oracle (eval_filter3, the oracle's
-null-skipping _agg_segment), including numDocsScanned and the post-filter entries."""
+stay on the CPU; GROUP BY with null keys and per-group null results (GpuNullHandlingGroupByOperator,
+phip_query_desc.null_group_by) -- every block against the oracle (eval_filter3, the oracle's null-skipping
+_agg_segment and null-aware _group_segment), including numDocsScanned and the post-filter entries."""
 import numpy as np
 import pytest
 
@@ -114,9 +115,9 @@ def test_gpu_null_handling_group_by_over_null_free_columns(sql, null_segments):
 
 
 @pytest.mark.parametrize("sql", [
-    "SELECT g, SUM(d) FROM t GROUP BY g LIMIT 10",              # per-group null results
-    "SELECT s, COUNT(*) FROM t GROUP BY s LIMIT 10",            # a null group key
     "SELECT g, SUM(k) FILTER (WHERE d > 3) FROM t GROUP BY g LIMIT 10",
+    # nine primitive slots once the non-null counts are added (device kMaxAggs = 8): the CPU plan maker's
+    "SELECT g, SUM(d), MIN(l), MAX(f), COUNT(*), AVG(r) FROM t GROUP BY g LIMIT 10",
     "SELECT d, k FROM t WHERE g = 1 LIMIT 10",                  # selected null values
 ])
 def test_gpu_null_handling_refusals(sql, null_segments):
@@ -155,3 +156,127 @@ def test_gpu_null_enabled_known_answers(dt, base, gpu_lib):
     finally:
         for g in segs:
             g.destroy()
+
+
+# ---- GROUP BY under enableNullHandling: null keys, per-group null results -----------------------------------------
+GB = [
+    "SELECT s, COUNT(*) FROM t GROUP BY s LIMIT 100",                                    # a null STRING key
+    "SELECT d, g, COUNT(*), SUM(k) FROM t WHERE g < 6 GROUP BY d, g LIMIT 100000",      # INT key, nulls in 2 segments
+    "SELECT r, COUNT(*) FROM t WHERE k > 40 GROUP BY r LIMIT 100000",                   # a raw LONG key with nulls
+    "SELECT g, SUM(d), MIN(l), COUNT(d), COUNT(*), AVG(r) FROM t GROUP BY g LIMIT 100",  # null results
+    "SELECT s, g, SUM(d * k), MINMAXRANGE(f), COUNT(l) FROM t WHERE NOT (d > 150) GROUP BY s, g LIMIT 1000",
+    "SELECT z, SUM(z), COUNT(z), COUNT(*) FROM t GROUP BY z LIMIT 10",                  # all-null key and values
+    "SELECT t, s, DISTINCTCOUNTHLL(d), SUM(l) FROM t WHERE s IS NOT NULL OR d IS NULL GROUP BY t, s LIMIT 10000",
+    "SELECT k, s, SUM(f), COUNT(*) FROM t WHERE k = -999 GROUP BY k, s LIMIT 10",       # nothing matches
+]
+
+
+def _check_nullable_groups(qc, blk, oblk, ex):
+    from tests.test_gpu_parity import _assert_intermediates_equal
+    assert blk.stats.num_docs_scanned == oblk.stats.num_docs_scanned
+    assert blk.stats.num_entries_scanned_post_filter == oblk.stats.num_entries_scanned_post_filter
+    assert blk.num_groups_limit_reached == oblk.num_groups_limit_reached
+    assert set(blk.groups) == set(oblk.groups)
+    for key, ov in oblk.groups.items():
+        gv = blk.groups[key]
+        for ag, g, o, e in zip(qc.aggregations, gv, ov, ex[key]):
+            assert (g is None) == (o is None), (key, ag, g, o)
+            if o is not None:
+                _assert_intermediates_equal([ag], [g], [o], [e])
+
+
+@pytest.mark.parametrize("sql", GB)
+def test_gpu_null_handling_group_by(sql, null_segments):
+    """Null keys (the library's null key id) and per-group null results (IS NOT NULL programs beside the query's
+    own) against the oracle's null-aware GroupByOperator: keys, every intermediate, numDocsScanned, post-filter
+    entries."""
+    qc, blk, oblk, ex = _run(NH + sql, null_segments)
+    _check_nullable_groups(qc, blk, oblk, ex)
+
+
+@pytest.mark.parametrize("mode", ["hash", "fused_xcd", "fused_hbm"])
+@pytest.mark.parametrize("sql", [GB[1], GB[3], GB[4]])
+def test_gpu_null_handling_group_by_table_modes(sql, mode, null_segments, monkeypatch):
+    """The same null keys / null results through the hash table, and fused into the filter (XCD copies, one HBM
+    table) where the program is conjunctive."""
+    monkeypatch.setenv(*{"hash": ("PHIP_GB_HASH", "1"), "fused_xcd": ("PHIP_FUSED_GB", "3"),
+                         "fused_hbm": ("PHIP_FUSED_GB", "2")}[mode])
+    qc, blk, oblk, ex = _run(NH + sql, null_segments)
+    _check_nullable_groups(qc, blk, oblk, ex)
+
+
+@pytest.mark.parametrize("limit", [40, 150])
+def test_gpu_null_handling_group_by_num_groups_limit(limit, null_segments):
+    """numGroupsLimit counts the null key in first-seen order (getKeyForNullValue) over the query's matched docs --
+    program 0 -- per segment; the kept groups and their null results equal the oracle's."""
+    raws, segs = null_segments
+    for sql in ("SELECT d, COUNT(*), SUM(l) FROM t GROUP BY d LIMIT 100000",
+                "SELECT d, g, COUNT(d), MAX(f) FROM t WHERE k > 0 GROUP BY d, g LIMIT 100000"):
+        qc = parse(NH + sql)
+        op = GpuInstancePlanMaker(num_groups_limit=limit).make_instance_plan(qc, segs)
+        blk = op.next_block()
+        op.close()
+        oblk, ex = executor.execute(qc, raws, num_groups_limit=limit)
+        assert oblk.num_groups_limit_reached
+        _check_nullable_groups(qc, blk, oblk, ex)
+
+
+@pytest.mark.parametrize("order", ["d ASC", "d DESC", "d ASC NULLS FIRST", "d DESC NULLS LAST", "SUM(l) DESC",
+                                   "SUM(l) ASC NULLS FIRST"])
+def test_gpu_null_handling_group_by_order_by(order, null_segments):
+    """Broker rows ordered with the reference's null placement (OrderByExpressionContext.isNullsLast: nulls as the
+    largest value unless NULLS FIRST / LAST says otherwise), for keys and null results alike; trimmed on the device
+    or the host, the rows equal the oracle's."""
+    raws, segs = null_segments
+    qc = parse(NH + f"SELECT d, SUM(l), COUNT(*) FROM t WHERE g < 3 GROUP BY d ORDER BY {order} LIMIT 30")
+    blk = GpuInstancePlanMaker().make_instance_plan(qc, segs).next_block()
+    oblk, _ = executor.execute(qc, raws)
+    got, want = reduce_blocks(qc, [blk]).rows, reduce_blocks(qc, [oblk]).rows
+    assert [r[0] for r in got] == [r[0] for r in want]
+    for a, b in zip(got, want):
+        assert (a[1] is None) == (b[1] is None) and a[2] == b[2]
+        if b[1] is not None:
+            assert abs(a[1] - b[1]) <= 1e-9 * max(1.0, abs(b[1]))
+
+
+NULL_GB_KATS = [
+    ("SELECT column1, COUNT(*) FROM testTable GROUP BY column1",
+     {"column1": [None, None, None, 1, 2, 2]}, {(2,): [8], (1,): [4], (None,): [12]}),
+    ("SELECT column1, COUNT(column2) FROM testTable GROUP BY column1",
+     {"column1": [1, None, None], "column2": [1, 1, 1]}, {(None,): [8], (1,): [4]}),
+    ("SELECT count(*), column1, column2 FROM testTable GROUP BY column1, column2",
+     {"column1": [None, None, None, 1, 1, 1], "column2": [None, 1, 1, 1, None, -2 ** 31]},
+     {(None, None): [4], (None, 1): [8], (1, 1): [4], (1, None): [4], (1, -2 ** 31): [4]}),
+    ("SELECT count(*), column1 FROM testTable GROUP BY column1",
+     {"column1": [None, 1, 1, 2, 3]}, {(1,): [8], (2,): [4], (3,): [4], (None,): [4]}),
+]
+
+
+@pytest.mark.parametrize("sql,cols,expect", NULL_GB_KATS, ids=[k[0][:48] for k in NULL_GB_KATS])
+def test_gpu_null_group_keys_known_answers(sql, cols, expect, gpu_lib):
+    """NullHandlingEnabledQueriesTest's GROUP BY cases (testGroupByOrderByNullsLastUsingOrdinal :153-176,
+    testHavingFilterIsNull :178-199, testMultiColumnGroupBy :778-806, testGroupByOrderBy :834-858): one segment
+    queried as 2 servers x 2 segments, every count x 4; a stored Integer.MIN_VALUE is a value, a null doc the null
+    key."""
+    from pinot_amd.engine.results import merge_intermediate
+    from pinot_amd.engine.segment import GpuSegment
+    c = SegmentCreator("kat")
+    for name, vals in cols.items():
+        nulls = [v is None for v in vals]
+        c.add_column(name, DataType.INT, [0 if v is None else v for v in vals], nulls=nulls if any(nulls) else None)
+    seg = GpuSegment(c.build())
+    try:
+        qc = parse(NH + sql)
+        blk = GpuInstancePlanMaker().make_instance_plan(qc, [seg, seg]).next_block()
+        merged = {}
+        for _ in range(2):
+            for k, v in blk.groups.items():
+                merged[k] = [merge_intermediate(a.function, x, y) for a, x, y in zip(qc.aggregations, merged[k], v)] \
+                    if k in merged else list(v)
+        assert merged == expect
+        if sql.startswith("SELECT column1, COUNT(*)"):  # the test's own ORDER BY 1 DESC NULLS LAST: 2, 1, null
+            q2 = parse(NH + sql + " ORDER BY column1 DESC NULLS LAST")
+            b2 = GpuInstancePlanMaker().make_instance_plan(q2, [seg, seg]).next_block()
+            assert reduce_blocks(q2, [b2, b2]).rows == [[2, 8], [1, 4], [None, 12]]
+    finally:
+        seg.destroy()

@@ -226,3 +226,71 @@ def test_plan_three_valued_trees_match_the_oracle(where, nh):
     tree = plan.compile_filter(_HostSeg(seg), fc, nh)
     os_ = executor.OracleSegment(seg)
     assert _docs(_eval_tree(os_, tree)) == _docs(executor.eval_filter(os_, fc, nh)), where
+
+
+# ---- GROUP BY under enableNullHandling: null keys and per-group null results --------------------------------------
+# NullHandlingEnabledQueriesTest (pinot-core/src/test/java/org/apache/pinot/queries/NullHandlingEnabledQueriesTest
+# .java): one segment queried as 2 servers x 2 segments (NUM_OF_SEGMENT_COPIES = 4 in every count), INT dimensions
+# whose null docs store Integer.MIN_VALUE -- which a non-null row may hold too (testMultiColumnGroupBy).
+NULL_GB_KATS = [
+    # testGroupByOrderByNullsLastUsingOrdinal (:153-176): column1 = null x3, 1, 2, 2
+    ("SELECT column1, COUNT(*) FROM testTable GROUP BY column1",
+     {"column1": ([None, None, None, 1, 2, 2], None)},
+     {(2,): [2 * 4], (1,): [4], (None,): [3 * 4]}),
+    # testHavingFilterIsNull / IsNotNull (:178-222): (1, 1), (null, 1), (null, 1); COUNT(column2) per column1
+    ("SELECT column1, COUNT(column2) FROM testTable GROUP BY column1",
+     {"column1": ([1, None, None], None), "column2": ([1, 1, 1], None)},
+     {(None,): [2 * 4], (1,): [4]}),
+    # testMultiColumnGroupBy (:778-806): a stored Integer.MIN_VALUE is a value, a null doc the null key
+    ("SELECT count(*), column1, column2 FROM testTable GROUP BY column1, column2",
+     {"column1": ([None, None, None, 1, 1, 1], None),
+      "column2": ([None, 1, 1, 1, None, -2 ** 31], None)},
+     {(None, None): [4], (None, 1): [2 * 4], (1, 1): [4], (1, None): [4], (1, -2 ** 31): [4]}),
+    # testGroupByOrderBy (:834-858): null, 1, 1, 2, 3
+    ("SELECT count(*), column1 FROM testTable GROUP BY column1",
+     {"column1": ([None, 1, 1, 2, 3], None)},
+     {(1,): [2 * 4], (2,): [4], (3,): [4], (None,): [4]}),
+]
+
+
+def _kat_segment(cols):
+    c = SegmentCreator("kat")
+    for name, (vals, _) in cols.items():
+        nulls = [v is None for v in vals]
+        c.add_column(name, DataType.INT, [0 if v is None else v for v in vals], nulls=nulls if any(nulls) else None)
+    return c.build()
+
+
+@pytest.mark.parametrize("sql,cols,expect", NULL_GB_KATS, ids=[k[0][:48] for k in NULL_GB_KATS])
+def test_oracle_null_group_keys_known_answers(sql, cols, expect):
+    """The oracle's null-aware GROUP BY reproduces the reference's rows: the null docs of a group-by column form the
+    None key, COUNT(col) skips null inputs (the blocks of 2 x 2 segment copies merged as the broker would)."""
+    from pinot_amd.engine.results import merge_intermediate
+    seg = _kat_segment(cols)
+    qc = parse("SET enableNullHandling = true; " + sql)
+    blk, _ = executor.execute(qc, [seg, seg])
+    merged = {}
+    for _ in range(2):  # two servers, each the same two segments
+        for k, v in blk.groups.items():
+            merged[k] = [merge_intermediate(a.function, x, y) for a, x, y in zip(qc.aggregations, merged[k], v)] \
+                if k in merged else list(v)
+    assert merged == expect
+
+
+def test_oracle_per_group_null_results_hand_derived():
+    """SUM / MIN / MAX / AVG over a group whose inputs are all null are None; COUNT(col) is 0; a null key and null
+    results together; numGroupsLimit counts the null key in first-seen order."""
+    c = SegmentCreator("g")
+    c.add_column("k", DataType.INT, [1, 1, 2, 0, 2, 3, 0], nulls=[0, 0, 0, 1, 0, 0, 1])
+    c.add_column("v", DataType.LONG, [10, 0, 0, 5, 0, 7, 0], nulls=[0, 1, 1, 0, 1, 0, 1])
+    seg = c.build()
+    qc = parse("SET enableNullHandling = true; SELECT k, SUM(v), MIN(v), COUNT(v), COUNT(*), AVG(v) FROM t GROUP BY k")
+    blk, ex = executor.execute(qc, [seg])
+    assert blk.groups[(1,)] == [10.0, 10.0, 1, 2, (10.0, 1)]
+    assert blk.groups[(2,)] == [None, None, 0, 2, None]
+    assert blk.groups[(None,)] == [5.0, 5.0, 1, 2, (5.0, 1)]
+    assert blk.groups[(3,)] == [7.0, 7.0, 1, 1, (7.0, 1)]
+    assert ex[(1,)][0] == 10 and ex[(2,)][0] is None
+    # numGroupsLimit 2: first seen are 1 (doc 0) and 2 (doc 2); the null key (doc 3) is the third -- dropped
+    blk2, _ = executor.execute(qc, [seg], num_groups_limit=2)
+    assert set(blk2.groups) == {(1,), (2,)} and blk2.num_groups_limit_reached
