@@ -243,10 +243,18 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
     keys = list(block.groups.keys())
     nk = len(block.group_by)
     world = dist.get_world_size(group)
-    local_vals = [sorted({k[c] for k in keys}) for c in range(nk)]
+    # An upper bound of the merged key space first (the sum over ranks of each column's distinct values): a large one
+    # goes straight to the record merge, without all-gathering every distinct value as Python objects
+    local_sets = [{k[c] for k in keys} for c in range(nk)]
+    bound = _reduce(dist, group, np.array([len(x) for x in local_sets] + [0], dtype=np.int64), dist.ReduceOp.SUM)[:nk]
+    if nk and float(np.prod(np.maximum(bound, 1).astype(np.float64))) > max_dense_groups:
+        merged = _merge_records_columnar(block, dist, group)
+        if merged is not None:
+            return merged
+    local_vals = [sorted(x, key=lambda v: (v is None, v)) for x in local_sets]
     gathered = [None] * world
     dist.all_gather_object(gathered, (local_vals, _hll_width(aggs, list(block.groups.values()))), group=group)
-    gdict = [sorted(set().union(*[g[0][c] for g in gathered])) for c in range(nk)]
+    gdict = [sorted(set().union(*[g[0][c] for g in gathered]), key=lambda v: (v is None, v)) for c in range(nk)]
     hll_m = max(g[1] for g in gathered)
     cards = [max(len(d), 1) for d in gdict]
     ndense = int(np.prod(cards, dtype=np.int64)) if nk else 1
@@ -288,6 +296,152 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
         groups[tuple(key)] = lay.get(srows[d, 1:], mrows[d])
     out = GroupByResultsBlock(aggs, block.group_by, groups, _stats_from(sv[:6]), bool(mv[0]))
     out.key_types = getattr(block, "key_types", None)
+    return out
+
+
+_NUMERIC_KEYS = ("INT", "LONG", "FLOAT", "DOUBLE")
+
+
+def _merge_records_columnar(block, dist, group):
+    """The record merge of a large key space as columns over the communicator (GroupByCombineOperator's upsert by
+    key, GroupByCombineOperator.java:138-147, across GPUs): every rank packs its groups into an int64 key matrix
+    (per group-by column the value -- a FLOAT / DOUBLE as its bits -- and a null-key flag), an int64 value matrix
+    (COUNTs and exact SUMs as integers, double results as their bits, a presence flag per function for null
+    intermediates) and a u8 HLL register matrix; three all_gathers (RCCL on the GPUs) bring every rank's rows, and
+    the rows merge by key in rank order (np.unique + np.add / minimum / maximum.at: the same answer on every rank,
+    independent of arrival order). None when a group-by column is not numeric (STRING keys keep the object merge);
+    every rank decides the same way."""
+    aggs = block.aggregations
+    nk = len(block.group_by)
+    kt = getattr(block, "key_types", None)
+    ok = kt is not None and len(kt) == nk and all(t in _NUMERIC_KEYS for t in kt)
+    keys = list(block.groups.keys())
+    vals = list(block.groups.values())
+    n = len(keys)
+    # per SUM / AVG: does any rank hold a double (the exact integer column then carries doubles for everyone)
+    any_f = [1 if ag.function in ("sum", "avg") and any(
+        v[a] is not None and not isinstance(v[a][0] if ag.function == "avg" else v[a], (int, np.integer))
+        for v in vals) else 0 for a, ag in enumerate(aggs)]
+    flags = _reduce(dist, group, np.array([0 if ok else 1] + any_f, dtype=np.int64), dist.ReduceOp.MAX)
+    if flags[0]:
+        return None
+    any_f = [int(x) for x in flags[1:]]
+    floats = [t in ("FLOAT", "DOUBLE") for t in kt]
+    K = np.zeros((n, 2 * nk), dtype=np.int64)
+    for c in range(nk):
+        col = [k[c] for k in keys]
+        K[:, nk + c] = [v is None for v in col]
+        if floats[c]:
+            x = np.array([0.0 if v is None else float(v) for v in col], dtype=np.float64)
+            x[x == 0] = 0.0  # (-0.0 keys the same group as 0.0, as the value-keyed dict of the object merge does)
+            K[:, c] = x.view(np.int64)
+        else:
+            K[:, c] = [0 if v is None else int(v) for v in col]
+    # value columns: (kind, agg, part) with kind I (int64) / F (double bits) / P (presence)
+    cols = []
+    for a, ag in enumerate(aggs):
+        f = ag.function
+        if f == "count":
+            cols.append(("I", a, None))
+        elif f == "sum":
+            cols.append(("F" if any_f[a] else "I", a, None))
+        elif f in ("min", "max"):
+            cols.append(("F", a, None))
+        elif f in ("avg", "minmaxrange"):
+            cols.append(("F", a, 0))
+            cols.append(("I" if f == "avg" else "F", a, 1))
+        cols.append(("P", a, None))
+    V = np.zeros((n, len(cols)), dtype=np.int64)
+    for j, (kind, a, part) in enumerate(cols):
+        f = aggs[a].function
+        if f in _HLL_FUNCS:
+            if kind == "P":
+                V[:, j] = 1
+            continue
+        col = [v[a] for v in vals]
+        if kind == "P":
+            V[:, j] = [x is not None for x in col]
+            continue
+        ident = {"min": float("inf"), "max": float("-inf")}.get(f, 0)
+        if part is not None:
+            ident = (float("inf"), float("-inf"))[part] if f == "minmaxrange" else 0
+            col = [ident if x is None else x[part] for x in col]
+        else:
+            col = [ident if x is None else x for x in col]
+        if kind == "F":
+            V[:, j] = np.array(col, dtype=np.float64).view(np.int64)
+        else:
+            V[:, j] = np.array([int(x) for x in col], dtype=np.int64)
+    # HLL registers: each function's 2^log2m (the query's, the same on every rank) side by side
+    hoff, width = {}, 0
+    for a, ag in enumerate(aggs):
+        if ag.function in _HLL_FUNCS:
+            hoff[a] = (width, 1 << ag.log2m)
+            width += 1 << ag.log2m
+    H = np.zeros((n, max(width, 1)), dtype=np.uint8)
+    for a, (o, m) in hoff.items():
+        for i, v in enumerate(vals):
+            H[i, o:o + m] = np.asarray(v[a], dtype=np.uint8)[:m]
+    Ka = _all_gather_rows(dist, group, K.reshape(-1)).reshape(-1, 2 * nk) if nk else np.zeros((0, 0), np.int64)
+    Va = _all_gather_rows(dist, group, V.reshape(-1)).reshape(-1, len(cols))
+    Ha = _all_gather_rows(dist, group, H)
+    st = _reduce(dist, group, np.concatenate([_stats_vector(block.stats), [0]]), dist.ReduceOp.SUM)[:6]
+    lim = _reduce(dist, group, np.array([int(block.num_groups_limit_reached)], np.int64), dist.ReduceOp.MAX)[0]
+    uniq, inv = np.unique(Ka, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    G = len(uniq)
+    merged_cols = []
+    for j, (kind, a, part) in enumerate(cols):
+        f = aggs[a].function
+        if kind == "P":
+            acc = np.zeros(G, dtype=np.int64)
+            np.maximum.at(acc, inv, Va[:, j])
+        elif kind == "I":
+            acc = np.zeros(G, dtype=np.int64)
+            np.add.at(acc, inv, Va[:, j])
+        else:
+            x = Va[:, j].view(np.float64)
+            op = "min" if (f == "min" or (f == "minmaxrange" and part == 0)) else \
+                ("max" if (f == "max" or (f == "minmaxrange" and part == 1)) else "sum")
+            acc = np.full(G, {"min": np.inf, "max": -np.inf, "sum": 0.0}[op])
+            {"min": np.minimum, "max": np.maximum, "sum": np.add}[op].at(acc, inv, x)
+        merged_cols.append(acc)
+    Hm = np.zeros((G, Ha.shape[1]), dtype=np.uint8)
+    np.maximum.at(Hm, inv, Ha)
+    groups = {}
+    col_of = {}
+    for j, (kind, a, part) in enumerate(cols):
+        col_of[(kind == "P", a, part)] = j
+    for g in range(G):
+        key = []
+        for c in range(nk):
+            if uniq[g, nk + c]:
+                key.append(None)
+            elif floats[c]:
+                key.append(float(np.int64(uniq[g, c]).view(np.float64)))
+            else:
+                key.append(int(uniq[g, c]))
+        row = []
+        for a, ag in enumerate(aggs):
+            f = ag.function
+            present = merged_cols[col_of[(True, a, None)]][g]
+            if f in _HLL_FUNCS:
+                o, m = hoff[a]
+                row.append(Hm[g, o:o + m].copy())
+                continue
+            if not present:
+                row.append(None)
+                continue
+            if f in ("avg", "minmaxrange"):
+                x0 = merged_cols[col_of[(False, a, 0)]][g]
+                x1 = merged_cols[col_of[(False, a, 1)]][g]
+                row.append((float(x0), int(x1)) if f == "avg" else (float(x0), float(x1)))
+            else:
+                x = merged_cols[col_of[(False, a, None)]][g]
+                row.append(int(x) if cols[col_of[(False, a, None)]][0] == "I" else float(x))
+        groups[tuple(key)] = row
+    out = GroupByResultsBlock(aggs, block.group_by, groups, _stats_from(st), bool(lim))
+    out.key_types = kt
     return out
 
 
