@@ -192,7 +192,9 @@ __device__ __forceinline__ int64_t group_key(cquery_t &q, cseg_t &seg, int32_t d
   for (int k = 0; k < q.num_group_by; k++) {
     ccol_t &c = seg.cols[q.gb_cols[k]];
     int64_t gid;
-    if (!c.has_dict) {
+    if (c.gb_ids != nullptr) {
+      gid = c.gb_ids[doc];
+    } else if (!c.has_dict) {
       gid = raw_i64(c, doc) - c.gb_base;
     } else {
       const uint32_t id = col_dict_id(c, doc);

@@ -139,7 +139,10 @@ __device__ __forceinline__ void batch_key_column(cquery_t &q, cseg_t &seg, int k
                                                  int32_t (&key)[U]) {
   ccol_t &c = seg.cols[q.gb_cols[k]];
   uint32_t id[U];
-  if (c.has_dict) {
+  if (c.gb_ids != nullptr) {
+#pragma unroll
+    for (int u = 0; u < U; u++) id[u] = (uint32_t)c.gb_ids[d[u]];
+  } else if (c.has_dict) {
     batch_ids_hbm<U>(c, d, id);
     if (c.remap) {
 #pragma unroll
@@ -166,7 +169,10 @@ __device__ __forceinline__ void batch_group_keys(cquery_t &q, cseg_t &seg, const
     for (int u = 0; u < U; u++) id[k][u] = 0;
     if (k < q.num_group_by) {
       ccol_t &c = seg.cols[q.gb_cols[k]];
-      if (c.has_dict) {
+      if (c.gb_ids != nullptr) {  // raw FLOAT / DOUBLE: the doc's id column
+#pragma unroll
+        for (int u = 0; u < U; u++) id[k][u] = (uint32_t)c.gb_ids[d[u]];
+      } else if (c.has_dict) {
         batch_ids_hbm<U>(c, d, id[k]);
       } else {  // raw INT / LONG: value - gb_base (below 2^31 here: an LDS / HBM table's key space)
 #pragma unroll

@@ -103,6 +103,7 @@ struct DevCol {
   const uint64_t *gb_nulls; // null-key group-by column (phip_query_desc.null_group_by): its null doc words (bit d % 64
                             // of word d / 64); a null doc's key id is gb_null_id. null = no null key
   int64_t gb_null_id;
+  const int32_t *gb_ids;    // raw FLOAT / DOUBLE group-by column: doc-order key ids (keys.hip), or null
 };
 constexpr int kBitSliceMaxBits = 12;
 

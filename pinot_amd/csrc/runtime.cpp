@@ -99,6 +99,11 @@ hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t 
                                int64_t cap, int32_t naggs, int32_t own_count, const int32_t *kinds,
                                const uint64_t *table, const uint32_t *hll, int32_t nhll, int32_t log2m,
                                int64_t *keys_out, double *vals, int64_t *longs, uint8_t *hll_out, hipStream_t s);
+hipError_t launch_raw_images(const void *raw, int32_t type, int64_t n, uint64_t *out, hipStream_t s);
+hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *in, uint64_t *sorted, uint64_t *out,
+                                  int64_t *num_out, int64_t n, hipStream_t s);
+hipError_t launch_raw_key_ids(const void *raw, int32_t type, int64_t n, const uint64_t *uniq, int64_t u, int32_t *ids,
+                              hipStream_t s);
 hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s,
                              const uint64_t *nulls = nullptr);
 hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
@@ -327,8 +332,11 @@ struct Device {
     bool raw = false;             // a raw INT / LONG column: id = value - raw_base (values not materialised)
     int64_t raw_base = 0;
     std::vector<uint8_t> values;  // LE typed or fixed-width strings
+    std::vector<int32_t *> ids;   // raw FLOAT / DOUBLE column: per segment its docs' ids into `values` (keys.hip)
     ~Remap() {
       for (auto *p : dev)
+        if (p) (void)hipFree(p);
+      for (auto *p : ids)
         if (p) (void)hipFree(p);
     }
   };
@@ -1157,6 +1165,100 @@ static int compare_value(int32_t type, const uint8_t *a, const uint8_t *b, int w
   }
 }
 
+// A raw FLOAT / DOUBLE group-by column (keys.hip): the sorted distinct values over the segments become the remap's
+// dictionary (values, card) and each segment gets a doc-order int32 id column (Remap.ids -> DevCol.gb_ids). Built on
+// the device's setup stream once per (column, segments), cached with the other remaps.
+static int32_t raw_real_key_ids(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
+                                const std::string &name, int32_t type, Device::Remap &r) {
+  hipStream_t st = dev.stream;
+  std::vector<void *> tmp;  // freed on every return
+  struct Free {
+    std::vector<void *> &v;
+    ~Free() {
+      for (void *p : v) (void)hipFree(p);
+    }
+  } free_tmp{tmp};
+  auto alloc = [&](size_t bytes, void **p) -> int32_t {
+    HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    tmp.push_back(*p);
+    return PHIP_OK;
+  };
+  std::vector<uint64_t *> seg_uniq(segs.size(), nullptr);
+  std::vector<int64_t> seg_u(segs.size(), 0);
+  int64_t total = 0;
+  for (size_t i = 0; i < segs.size(); i++) {
+    const ColumnStore &c = segs[i]->cols[colidx[i]];
+    if (!no_dict(c) || c.fwd_kind != PHIP_FWD_RAW_CHUNK || c.type != type)
+      return fail(PHIP_ERR_UNSUPPORTED, "group-by on column %s: raw in some segments only", name.c_str());
+    const int64_t n = segs[i]->num_docs;
+    if (n <= 0) continue;
+    if (n > INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s: segment over 2^31 docs", name.c_str());
+    void *img, *srt, *uq, *cnt, *scratch;
+    size_t sb = 0;
+    int32_t rc;
+    if ((rc = alloc((size_t)n * 8, &img)) || (rc = alloc((size_t)n * 8, &srt)) || (rc = alloc((size_t)n * 8, &uq)) ||
+        (rc = alloc(8, &cnt)))
+      return rc;
+    HIP_TRY(launch_sort_unique_u64(nullptr, &sb, nullptr, nullptr, nullptr, nullptr, n, st));
+    if ((rc = alloc(sb, &scratch))) return rc;
+    HIP_TRY(launch_raw_images(c.raw, type, n, (uint64_t *)img, st));
+    HIP_TRY(launch_sort_unique_u64(scratch, &sb, (uint64_t *)img, (uint64_t *)srt, (uint64_t *)uq, (int64_t *)cnt, n, st));
+    HIP_TRY(hipMemcpyAsync(&seg_u[i], cnt, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    seg_uniq[i] = (uint64_t *)uq;
+    total += seg_u[i];
+  }
+  void *all, *srt, *guniq, *cnt, *scratch;
+  size_t sb = 0;
+  int32_t rc;
+  if ((rc = alloc((size_t)total * 8, &all)) || (rc = alloc((size_t)total * 8, &srt)) ||
+      (rc = alloc((size_t)total * 8, &guniq)) || (rc = alloc(8, &cnt)))
+    return rc;
+  int64_t off = 0;
+  for (size_t i = 0; i < segs.size(); i++) {
+    if (!seg_u[i]) continue;
+    HIP_TRY(hipMemcpyAsync((uint64_t *)all + off, seg_uniq[i], (size_t)seg_u[i] * 8, hipMemcpyDeviceToDevice, st));
+    off += seg_u[i];
+  }
+  HIP_TRY(launch_sort_unique_u64(nullptr, &sb, nullptr, nullptr, nullptr, nullptr, total, st));
+  if ((rc = alloc(sb, &scratch))) return rc;
+  int64_t u = 0;
+  HIP_TRY(launch_sort_unique_u64(scratch, &sb, (uint64_t *)all, (uint64_t *)srt, (uint64_t *)guniq, (int64_t *)cnt, total, st));
+  HIP_TRY(hipMemcpyAsync(&u, cnt, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (u > INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s: %lld distinct values", name.c_str(), (long long)u);
+  r.ids.assign(segs.size(), nullptr);
+  for (size_t i = 0; i < segs.size(); i++) {
+    const int64_t n = segs[i]->num_docs;
+    void *p;
+    HIP_TRY(hipMalloc(&p, std::max<size_t>((size_t)n * 4, 16)));
+    r.ids[i] = (int32_t *)p;  // owned by r from here
+    HIP_TRY(launch_raw_key_ids(segs[i]->cols[colidx[i]].raw, type, n, (const uint64_t *)guniq, u, (int32_t *)p, st));
+  }
+  std::vector<uint64_t> img((size_t)u);
+  if (u) HIP_TRY(hipMemcpyAsync(img.data(), guniq, (size_t)u * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int w = type_width(type);
+  r.values.assign((size_t)u * w, 0);
+  for (int64_t i = 0; i < u; i++) {  // the images back to values (keys.hip f64_order_image inverted)
+    const uint64_t k = img[(size_t)i];
+    const uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    double d;
+    memcpy(&d, &b, 8);
+    if (w == 4) {
+      const float f = (float)d;
+      memcpy(r.values.data() + 4 * i, &f, 4);
+    } else {
+      memcpy(r.values.data() + 8 * i, &d, 8);
+    }
+  }
+  r.type = type;
+  r.width = w;
+  r.card = (int32_t)u;
+  r.dev.assign(segs.size(), nullptr);
+  return PHIP_OK;
+}
+
 // Query-global dictionary of one group-by column across the query's segments: the
 // node-global dictionary registered for the column (phip_global_dictionary, multi-GPU servers), else the
 // sorted union of the segments' dictionaries. Per segment a dict-id -> global-id map in HBM (nullptr when
@@ -1210,6 +1312,14 @@ int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::
     r->raw_base = lo;
     r->card = (int32_t)(hi - lo + 1);
     r->dev.assign(segs.size(), nullptr);
+    dev.remaps[key] = r;
+    out = r;
+    return PHIP_OK;
+  }
+  if (no_dict(c0) && c0.fwd_kind == PHIP_FWD_RAW_CHUNK && (type == PHIP_TYPE_FLOAT || type == PHIP_TYPE_DOUBLE)) {
+    if (gd) return fail(PHIP_ERR_INVALID, "column %s is raw: it has no global dictionary", name.c_str());
+    int32_t rc = raw_real_key_ids(dev, segs, colidx, name, type, *r);
+    if (rc) return rc;
     dev.remaps[key] = r;
     out = r;
     return PHIP_OK;
@@ -2056,6 +2166,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       DevCol &gc = ds.cols[q->group_by_columns[k]];
       gc.remap = gb_dicts[k]->dev[s];
       if (gb_dicts[k]->raw) gc.gb_base = gb_dicts[k]->raw_base;
+      if (!gb_dicts[k]->ids.empty()) gc.gb_ids = gb_dicts[k]->ids[s];  // a raw FLOAT / DOUBLE key: its id column
       if (P.gb_radix[k] > gb_dicts[k]->card) {  // a null-key column: its null docs (if this segment has any)
         gc.gb_nulls = segs[s]->cols[colidx[s][q->group_by_columns[k]]].nulls;
         gc.gb_null_id = gb_dicts[k]->card;

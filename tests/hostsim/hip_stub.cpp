@@ -80,6 +80,16 @@ hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t, const int32_t 
   memset(tab, 0, (size_t)words * kXcdCopies * 8);
   return hipSuccess;
 }
+hipError_t launch_raw_images(const void *, int32_t, int64_t, uint64_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *, uint64_t *, uint64_t *, int64_t *num_out,
+                                  int64_t, hipStream_t) {
+  if (!temp) *temp_bytes = 64;
+  else *num_out = 0;
+  return hipSuccess;
+}
+hipError_t launch_raw_key_ids(const void *, int32_t, int64_t, const uint64_t *, int64_t, int32_t *, hipStream_t) {
+  return hipSuccess;
+}
 hipError_t launch_xcd_merge(uint64_t *, int64_t, int64_t, const int32_t *, uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_roaring_or(const RoaringTask *, const RoaringGroup *, int32_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_filter(const DevFilter &q, bool, int fused_naggs, int nblocks, size_t, hipStream_t, hipEvent_t,

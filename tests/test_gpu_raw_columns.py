@@ -3,7 +3,8 @@
   group-by   NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator
              (DefaultGroupByExecutor.java:106-116): a raw INT / LONG column keys by its values; on the GPU the key
              dimension is value - min over the query's segments (value order = key order), mixed with dictionary
-             columns' global ids, and a result's dictionary holds only the values its groups use.
+             columns' global ids, and a result's dictionary holds only the values its groups use. A raw FLOAT / DOUBLE
+             column keys through the sorted distinct values over the segments (keys.hip, a doc-order id column).
   HLL        DistinctCountHLLAggregationFunction over raw INT / LONG / FLOAT / DOUBLE values (:106-145): every matched
              doc's value hashed on the device (clearspring MurmurHash.hashLong, the dictionary path's mapping).
 
@@ -32,8 +33,10 @@ def raw_segments(gpu_lib):
         c = SegmentCreator(f"raw{s}", no_dictionary_columns=["ri", "rl", "rf", "rd", "rm"])
         c.add_column("ri", DataType.INT, rng.integers(-50 + 7 * s, 60 + 3 * s, n).astype(np.int32))
         c.add_column("rl", DataType.LONG, rng.integers(-3_000_000_000, -2_999_990_000, n) + 1_000_000 * s)
-        c.add_column("rf", DataType.FLOAT, np.round(rng.normal(0, 5, n), 1).astype(np.float32))
-        c.add_column("rd", DataType.DOUBLE, np.round(rng.normal(0, 50, n), 2))
+        # (+ 0.0: no -0.0 -- the reference keys it apart from 0.0 by its bits, Double2IntOpenHashMap, and so does the
+        # GPU, but value-keyed Python dicts and the oracle's np.unique fold the two)
+        c.add_column("rf", DataType.FLOAT, (np.round(rng.normal(0, 5, n), 1) + 0.0).astype(np.float32))
+        c.add_column("rd", DataType.DOUBLE, np.round(rng.normal(0, 50, n), 2) + 0.0)
         c.add_column("rm", DataType.LONG, rng.integers(-10 ** 9, 10 ** 9, n))
         c.add_column("dk", DataType.STRING, np.array([f"k{x}" for x in rng.integers(0, 9 + s, n)]))
         c.add_column("f", DataType.INT, rng.integers(0, 100, n))
@@ -50,6 +53,11 @@ RAW_GROUP_BY = [
     "SELECT dk, ri, SUM(rm), DISTINCTCOUNTHLL(rl) FROM t WHERE f >= 10 GROUP BY dk, ri LIMIT 100000",
     "SELECT ri, dk, COUNT(*) FROM t GROUP BY ri, dk ORDER BY COUNT(*) DESC, ri, dk LIMIT 7",  # device trim
     "SELECT ri, SUM(rm) FROM t GROUP BY ri ORDER BY ri DESC LIMIT 5",  # key-order trim over raw values
+    # raw FLOAT / DOUBLE keys (keys.hip: the sorted distinct values over the segments, a doc-order id column each)
+    "SELECT rf, COUNT(*), SUM(rm) FROM t GROUP BY rf LIMIT 100000",
+    "SELECT rd, dk, COUNT(*), MIN(ri), DISTINCTCOUNTHLL(rf) FROM t WHERE f < 50 GROUP BY rd, dk LIMIT 100000",
+    "SELECT rf, rd, COUNT(*) FROM t WHERE f < 20 GROUP BY rf, rd ORDER BY rf DESC, rd LIMIT 9",  # key-order trim
+    "SELECT rf, SUM(rd), MAX(rf) FROM t WHERE rf > 1.5 GROUP BY rf LIMIT 100000",  # key column also filtered / aggregated
 ]
 
 
