@@ -464,11 +464,21 @@ def _distinct_values(vals, t):
     return np.unique(vals, return_inverse=True)
 
 
-def _hll_registers(os_, col, docs, log2m):
+def _hll_inputs(os_, arg, docs):
+    """(values, stored type) DISTINCTCOUNTHLL offers: a column's values, or an expression's -- the arithmetic transform
+    functions' DOUBLE results, offered as java.lang.Double (hashLong of the bits, DistinctCountHLLAggregationFunction
+    .java:106-145 DOUBLE case)."""
+    from pinot_amd.query.context import Identifier
+    if isinstance(arg, Identifier):
+        return os_.values(arg.name)[docs], int(os_.meta(arg.name).data_type)
+    return np.asarray(_expr_values(os_, arg, docs), dtype=np.float64), 3
+
+
+def _hll_registers(os_, arg, docs, log2m):
     L = _oracle_lib()
     regs = np.zeros(1 << log2m, dtype=np.uint8)
-    t = int(os_.meta(col).data_type)
-    for v in _distinct_values(os_.values(col)[docs], t)[0].tolist():  # (each distinct value once: order-free max)
+    vals, t = _hll_inputs(os_, arg, docs)
+    for v in _distinct_values(vals, t)[0].tolist():  # (each distinct value once: order-free max)
         L.oracle_hll_offer_hashed(regs.ctypes.data, log2m, _hll_hash(L, v, t))
     return regs
 
@@ -494,7 +504,7 @@ def _agg_segment(os_, ag, docs, null_handling=False):
     if f == "count":
         return len(docs), None
     if f in ("distinctcounthll", "distinctcountrawhll"):
-        return _hll_registers(os_, ag.argument.name, docs, ag.log2m), None
+        return _hll_registers(os_, ag.argument, docs, ag.log2m), None
     vals = _expr_values(os_, ag.argument, docs).astype(np.float64)
     if f == "sum":
         s = _oracle_lib().oracle_block_sum_f64(np.ascontiguousarray(vals).ctypes.data, len(vals), MAX_DOC_PER_CALL)
@@ -583,7 +593,7 @@ def _group_aggregate(os_, ag, docs, gid, ng):
     if f == "count":
         v = np.bincount(gid, minlength=ng).tolist()
     elif f in ("distinctcounthll", "distinctcountrawhll"):
-        v = _hll_group_registers(os_, ag.argument.name, docs, gid, ng, ag.log2m)
+        v = _hll_group_registers(os_, ag.argument, docs, gid, ng, ag.log2m)
     else:
         vals = _expr_values(os_, ag.argument, docs).astype(np.float64)
         if f in ("sum", "avg"):
@@ -634,11 +644,11 @@ def _group_aggregate_nullable(os_, ag, docs, gid, ng):
     return v, ex
 
 
-def _hll_group_registers(os_, col, docs, gid, ng, log2m):
+def _hll_group_registers(os_, arg, docs, gid, ng, log2m):
     """Registers per group: every distinct matched value offered once (order-free max)."""
     L = _oracle_lib()
-    t = int(os_.meta(col).data_type)
-    uval, uinv = _distinct_values(os_.values(col)[docs], t)
+    vals, t = _hll_inputs(os_, arg, docs)
+    uval, uinv = _distinct_values(vals, t)
     reg_of = np.empty(len(uval), dtype=np.int64)
     rho_of = np.empty(len(uval), dtype=np.uint8)
     one = np.zeros(1 << log2m, dtype=np.uint8)

@@ -126,6 +126,12 @@ __device__ __forceinline__ int32_t murmur_hash_long_dev(int64_t data) {
   h ^= h >> 15;
   return (int32_t)h;
 }
+__device__ __forceinline__ uint32_t hll_entry_bits(int64_t x, int log2m) {
+  const uint32_t ux = (uint32_t)murmur_hash_long_dev(x);
+  const uint32_t j = ux >> (32 - log2m);
+  const uint32_t w = (ux << log2m) | ((1u << (log2m - 1)) + 1u);
+  return (j << 8) | ((uint32_t)__builtin_clz(w) + 1u);
+}
 __device__ __forceinline__ uint32_t hll_entry_raw(ccol_t &c, int32_t doc, int log2m) {
   int64_t x;
   switch (c.type) {
@@ -134,16 +140,19 @@ __device__ __forceinline__ uint32_t hll_entry_raw(ccol_t &c, int32_t doc, int lo
     case PHIP_TYPE_FLOAT: x = ((const PHIP_GLB int32_t *)c.raw)[doc]; break;
     default: x = ((const PHIP_GLB int64_t *)c.raw)[doc]; break;
   }
-  const uint32_t ux = (uint32_t)murmur_hash_long_dev(x);
-  const uint32_t j = ux >> (32 - log2m);
-  const uint32_t w = (ux << log2m) | ((1u << (log2m - 1)) + 1u);
-  return (j << 8) | ((uint32_t)__builtin_clz(w) + 1u);
+  return hll_entry_bits(x, log2m);
 }
 // the entry of doc's value in column c: the per-dictionary-id table, or hashed from the raw value
 __device__ __forceinline__ uint32_t hll_entry(ccol_t &c, int32_t doc, int log2m) {
   if (c.hll_doc != nullptr) return ((const PHIP_GLB uint32_t *)c.hll_doc)[doc];
   if (!c.has_dict) return hll_entry_raw(c, doc, log2m);
   return ((const PHIP_GLB uint32_t *)c.hll)[col_dict_id(c, doc)];
+}
+// a DISTINCTCOUNTHLL's entry at doc: of its column, or of its expression's double value (hashLong of the bits: the
+// reference offers a transform function's DOUBLE result as java.lang.Double)
+__device__ __forceinline__ uint32_t hll_entry_agg(cseg_t &seg, cagg_t &ag, int32_t doc) {
+  if (ag.expr != PHIP_EXPR_COLUMN) return hll_entry_bits(__double_as_longlong(expr_f64(seg, ag, doc)), ag.log2m);
+  return hll_entry(seg.cols[ag.col_a], doc, ag.log2m);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -170,7 +179,7 @@ __device__ __forceinline__ void agg_chunk(cquery_t &q, cseg_t &seg, int32_t doc,
       if (c.hll_rows) {
         if (act) hll_row_each(c, doc, [&](int r, uint32_t rho) { __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_WG); });
       } else {
-        const uint32_t h = hll_entry(c, doc, ag.log2m);
+        const uint32_t h = hll_entry_agg(seg, ag, doc);
         if (act) __hip_atomic_fetch_max(&regs[h >> 8], h & 0xffu, PHIP_RLX, PHIP_WG);
       }
     } else {
@@ -235,7 +244,7 @@ __device__ __forceinline__ void group_chunk_lds(cquery_t &q, cseg_t &seg, int32_
         if (c.hll_rows) {
           hll_row_each(c, doc, [&](int r, uint32_t rho) { lds_hll_max(regs, (uint32_t)r, rho); });
         } else {
-          const uint32_t h = hll_entry(c, doc, ag.log2m);
+          const uint32_t h = hll_entry_agg(seg, ag, doc);
           lds_hll_max(regs, h >> 8, h & 0xffu);
         }
         break;

@@ -44,7 +44,12 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
     } else if (kind == ACC_HLL) {
       ccol_t &c = seg.cols[ag.col_a];
       uint32_t h[U];
-      if (c.hll_doc != nullptr) {  // doc-order entries
+      if (ag.expr != PHIP_EXPR_COLUMN) {  // an expression's double values, hashed per doc
+        double x[U];
+        batch_expr_f64<U>(seg, ag, d, sa, sb, x);
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = hll_entry_bits(__double_as_longlong(x[u]), ag.log2m);
+      } else if (c.hll_doc != nullptr) {  // doc-order entries
 #pragma unroll
         for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
       } else if (!c.has_dict) {  // raw values, hashed per doc
@@ -375,9 +380,15 @@ __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const
         for (int u = 0; u < U; u++)
           if ((act >> u) & 1u)
             hll_row_each(c, d[u], [&](int r, uint32_t rho) { tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], r, rho); });
-      } else if (c.hll_doc != nullptr || !c.has_dict) {  // doc-order entries, or raw values hashed per doc
+      } else if (ag.expr != PHIP_EXPR_COLUMN || c.hll_doc != nullptr || !c.has_dict) {
+        // an expression's double values or raw values hashed per doc, or doc-order entries
         uint32_t h[U];
-        if (c.hll_doc != nullptr) {
+        if (ag.expr != PHIP_EXPR_COLUMN) {
+          double x[U];
+          batch_expr2_f64<U>(seg, ag, d, x);
+#pragma unroll
+          for (int u = 0; u < U; u++) h[u] = hll_entry_bits(__double_as_longlong(x[u]), ag.log2m);
+        } else if (c.hll_doc != nullptr) {
 #pragma unroll
           for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
         } else {
@@ -472,7 +483,7 @@ __device__ __forceinline__ void group_update_global(cquery_t &q, cseg_t &seg, in
             if (regs[r] < rho) __hip_atomic_fetch_max(&regs[r], rho, PHIP_RLX, PHIP_AG);
           });
         } else {
-          const uint32_t h = hll_entry(c, doc, ag.log2m);
+          const uint32_t h = hll_entry_agg(seg, ag, doc);
           glb_u32 *r = regs + (h >> 8);
           if (*r < (h & 0xffu)) __hip_atomic_fetch_max(r, h & 0xffu, PHIP_RLX, PHIP_AG);
         }

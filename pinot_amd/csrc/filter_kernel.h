@@ -1200,6 +1200,17 @@ __device__ __forceinline__ void fused_flush(cquery_t &aq, cseg_t &seg, const PHI
   fused_batch<NA, kFusedBatch, true>(aq, seg, tz, d, act, sda, sdb, acc);
 }
 
+constexpr int defer_piece_lanes(int room) {  // the largest power of two <= room / 32 lanes (at most 64)
+  int l = 64;
+  while (l > 1 && l * 32 > room) l >>= 1;
+  return l;
+}
+constexpr int kDeferPieceLanes = defer_piece_lanes(kFusedRingDefer - 64 * kFusedBatch);
+static_assert(kFusedRingDefer - 64 * kFusedBatch >= 32 * kDeferPieceLanes, "a piece fits the ring beside a batch");
+
+// (Measured and not kept, round 5: a 256-entry ring flushed 128 docs at a time -- 1 KiB per wave, as the fused group-by
+// uses -- sorted Q1.1 0.136 -> 0.231 ms, unsorted Q1.3 0.352 -> 0.431: half the loads in flight per wave costs more than
+// the resident workgroup it frees; profiles/r05za_ring256_ab_*.log.)
 // deferred mode: append the tile's matched docs; a full batch is projected at once. (Measured and not kept, round 5:
 // the batch's loads issued when it fills and consumed after the next tile's DMA wait and evaluation -- sorted Q1.1
 // 0.157 -> 0.153 ms against the same build's synchronous batches, but the batch held across the tile cost 136 B of
@@ -1215,9 +1226,10 @@ __device__ __forceinline__ void fused_defer(cquery_t &aq, cseg_t &seg, const Til
   if (ballot(mask != 0) == 0) return;
   const TileRank r = rank_tile(mask);
   const int head0 = head;
-  // the whole tile when the ring has room, else eighth tiles (8 lanes, <= 256 docs) each after draining the ring below
-  // one batch (< 256 pending + 256 <= kFusedRingDefer)
-  const int npiece = head - tail + r.total <= kFusedRingDefer ? 1 : 8;
+  // the whole tile when the ring has room, else pieces of kDeferPieceLanes lanes (<= 32 docs a lane) each after
+  // draining the ring below one batch (< 64 x kFusedBatch pending + the piece <= kFusedRingDefer): eighth tiles for
+  // the default 512-entry ring and 4-chunk batch
+  const int npiece = head - tail + r.total <= kFusedRingDefer ? 1 : 64 / kDeferPieceLanes;
   const int lanes = 64 / npiece;
   for (int p = 0; p < npiece; p++) {
     const int e = __builtin_amdgcn_readlane((int)r.incl, lanes * p + lanes - 1);

@@ -1767,8 +1767,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       if (ag.column_a < 0 || ag.column_a >= ncols) return fail(PHIP_ERR_INVALID, "aggregation column out of range");
       projected[ag.column_a] = true;
       proj_progs[ag.column_a] |= 1u << ag.program;
-      if (ag.expr != PHIP_EXPR_COLUMN) {
-        if (ag.function == PHIP_AGG_HLL) return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over expressions");
+      if (ag.expr != PHIP_EXPR_COLUMN) {  // (DISTINCTCOUNTHLL over a col op col: its double values hashed per doc)
         if (ag.column_b < 0 || ag.column_b >= ncols) return fail(PHIP_ERR_INVALID, "aggregation column out of range");
         projected[ag.column_b] = true;
         proj_progs[ag.column_b] |= 1u << ag.program;
@@ -1790,6 +1789,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         }
         // raw numeric columns offer their values directly (DistinctCountHLLAggregationFunction.java:106-145): the
         // kernels hash each matched doc's value (agg_common.h hll_entry_raw); raw STRING values stay on the CPU
+        if (ag.function == PHIP_AGG_HLL && ag.expr != PHIP_EXPR_COLUMN && ca.type == PHIP_TYPE_STRING)
+          return fail(PHIP_ERR_INVALID, "numeric expression over STRING column");
         if (ag.function == PHIP_AGG_HLL && ca.fwd_kind == PHIP_FWD_RAW_CHUNK && ca.type == PHIP_TYPE_STRING)
           return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over raw STRING column %s", ca.name.c_str());
         if (ag.expr != PHIP_EXPR_COLUMN) {
@@ -1832,7 +1833,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       // with its own log2m, DistinctCountHLLAggregationFunction.java:105-145). One column per entry table, so two
       // log2m over one column stay on the CPU path.
       for (int b = 0; b < a; b++)
-        if (dq.aggs[b].acc == ACC_HLL && dq.aggs[b].col_a == ag.column_a && dq.aggs[b].log2m != ag.log2m)
+        if (dq.aggs[b].acc == ACC_HLL && dq.aggs[b].expr == PHIP_EXPR_COLUMN && ag.expr == PHIP_EXPR_COLUMN &&
+            dq.aggs[b].col_a == ag.column_a && dq.aggs[b].log2m != ag.log2m)
           return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL of column %d with two log2m (%d, %d)", ag.column_a,
                       dq.aggs[b].log2m, ag.log2m);
       log2m = std::max(log2m, ag.log2m);
@@ -2146,7 +2148,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dc.lds_off = -1;
     }
     for (int a = 0; a < naggs; a++) {
-      if (dq.aggs[a].acc != ACC_HLL) continue;
+      if (dq.aggs[a].acc != ACC_HLL || dq.aggs[a].expr != PHIP_EXPR_COLUMN) continue;  // (an expression: hashed per doc)
       ColumnStore &cs = sg.cols[colidx[s][dq.aggs[a].col_a]];
       if (cs.fwd_kind == PHIP_FWD_HLL_REGISTERS) continue;  // the register rows are the column's raw values
       if (no_dict(cs)) continue;  // raw values: hashed per doc on the device

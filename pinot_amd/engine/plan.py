@@ -456,8 +456,7 @@ def plan_aggregations(aggs: Sequence[AggregationInfo], programs: Optional[Sequen
         elif f == "minmaxrange":
             mapping.append(("minmaxrange", (slot((_lib.AGG_MIN,) + expr + (0,)), slot((_lib.AGG_MAX,) + expr + (0,)))))
         elif f in ("distinctcounthll", "distinctcountrawhll"):
-            if expr[0] != _lib.EXPR_COLUMN:
-                raise UnsupportedOnGpu("DISTINCTCOUNTHLL over an expression")
+            # (over an expression: its DOUBLE values hashed on the device, as the reference offers a transform's result)
             mapping.append((f, slot((_lib.AGG_HLL,) + expr + (ag.log2m,))))
         else:
             raise UnsupportedOnGpu(f"aggregation {f} is not on the GPU path")

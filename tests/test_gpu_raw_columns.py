@@ -99,6 +99,9 @@ RAW_HLL = [
     "SELECT DISTINCTCOUNTHLL(rm), COUNT(*) FROM t WHERE f < 40",
     "SELECT dk, DISTINCTCOUNTHLL(rd), DISTINCTCOUNTHLL(ri) FROM t GROUP BY dk LIMIT 100000",
     "SELECT DISTINCTCOUNTHLL(rl, 12), SUM(ri) FROM t WHERE f BETWEEN 20 AND 80",
+    # over expressions: the transform's DOUBLE values offered as java.lang.Double (hashLong of the bits)
+    "SELECT DISTINCTCOUNTHLL(ri * f), DISTINCTCOUNTHLL(rd - rf), COUNT(*) FROM t WHERE f < 60",
+    "SELECT dk, DISTINCTCOUNTHLL(ri + f), SUM(rm) FROM t GROUP BY dk LIMIT 100000",
 ]
 
 

@@ -11,7 +11,7 @@ SRCS=${3:-$(cd "$C" && ls filter_k_*.hip)}
 B=/tmp/abbuild/$NAME
 mkdir -p "$B" "$ROOT/tools/ablib"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -munsafe-fp-atomics -fvisibility=hidden"
-(cd "$C" && make -s)
+(cd "$C" && make -s -j8)
 OBJS=""
 for o in $(cd "$C" && ls *.o); do
   src=""
