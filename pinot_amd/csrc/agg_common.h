@@ -142,9 +142,17 @@ __device__ __forceinline__ uint32_t hll_entry_raw(ccol_t &c, int32_t doc, int lo
   }
   return hll_entry_bits(x, log2m);
 }
+// a doc-order entry as (register << 8) | rho: the 32-bit copy, or the 16-bit one unpacked
+__device__ __forceinline__ uint32_t hll_doc_entry(ccol_t &c, int32_t doc) {
+  if (c.hll_doc16 != nullptr) {
+    const uint32_t e = ((const PHIP_GLB uint16_t *)c.hll_doc16)[doc];
+    return ((e >> 5) << 8) | (e & 31u);
+  }
+  return ((const PHIP_GLB uint32_t *)c.hll_doc)[doc];
+}
 // the entry of doc's value in column c: the per-dictionary-id table, or hashed from the raw value
 __device__ __forceinline__ uint32_t hll_entry(ccol_t &c, int32_t doc, int log2m) {
-  if (c.hll_doc != nullptr) return ((const PHIP_GLB uint32_t *)c.hll_doc)[doc];
+  if (c.hll_doc != nullptr || c.hll_doc16 != nullptr) return hll_doc_entry(c, doc);
   if (!c.has_dict) return hll_entry_raw(c, doc, log2m);
   return ((const PHIP_GLB uint32_t *)c.hll)[col_dict_id(c, doc)];
 }

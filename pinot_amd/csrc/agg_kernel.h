@@ -49,9 +49,9 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
         batch_expr_f64<U>(seg, ag, d, sa, sb, x);
 #pragma unroll
         for (int u = 0; u < U; u++) h[u] = hll_entry_bits(__double_as_longlong(x[u]), ag.log2m);
-      } else if (c.hll_doc != nullptr) {  // doc-order entries
+      } else if (c.hll_doc != nullptr || c.hll_doc16 != nullptr) {  // doc-order entries
 #pragma unroll
-        for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
+        for (int u = 0; u < U; u++) h[u] = hll_doc_entry(c, d[u]);
       } else if (!c.has_dict) {  // raw values, hashed per doc
 #pragma unroll
         for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], ag.log2m);
@@ -380,7 +380,7 @@ __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const
         for (int u = 0; u < U; u++)
           if ((act >> u) & 1u)
             hll_row_each(c, d[u], [&](int r, uint32_t rho) { tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key[u], r, rho); });
-      } else if (ag.expr != PHIP_EXPR_COLUMN || c.hll_doc != nullptr || !c.has_dict) {
+      } else if (ag.expr != PHIP_EXPR_COLUMN || c.hll_doc != nullptr || c.hll_doc16 != nullptr || !c.has_dict) {
         // an expression's double values or raw values hashed per doc, or doc-order entries
         uint32_t h[U];
         if (ag.expr != PHIP_EXPR_COLUMN) {
@@ -388,9 +388,9 @@ __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const
           batch_expr2_f64<U>(seg, ag, d, x);
 #pragma unroll
           for (int u = 0; u < U; u++) h[u] = hll_entry_bits(__double_as_longlong(x[u]), ag.log2m);
-        } else if (c.hll_doc != nullptr) {
+        } else if (c.hll_doc != nullptr || c.hll_doc16 != nullptr) {
 #pragma unroll
-          for (int u = 0; u < U; u++) h[u] = ((const glb_u32 *)c.hll_doc)[d[u]];
+          for (int u = 0; u < U; u++) h[u] = hll_doc_entry(c, d[u]);
         } else {
 #pragma unroll
           for (int u = 0; u < U; u++) h[u] = hll_entry_raw(c, d[u], ag.log2m);

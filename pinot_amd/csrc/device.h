@@ -100,6 +100,7 @@ struct DevCol {
                             // plane k (bit bits-1-k of the id) as 64 lane words, bit 31-g of lane l = doc 64g + l
   int64_t gb_base;          // raw INT / LONG group-by column: its key id = value - gb_base
   const uint32_t *hll_doc;  // DISTINCTCOUNTHLL: doc-order copy of `hll` (entry of doc d = hll[id(d)]), or null
+  const uint16_t *hll_doc16;  // ... packed to 16 bits, (register << 5) | rho (log2m <= 11), when hll_doc is null
   const uint64_t *gb_nulls; // null-key group-by column (phip_query_desc.null_group_by): its null doc words (bit d % 64
                             // of word d / 64); a null doc's key id is gb_null_id. null = no null key
   int64_t gb_null_id;

@@ -86,6 +86,21 @@ __global__ void materialize_kernel(const uint32_t *__restrict__ words, int32_t b
   for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x)
     vals[d] = dict[decode_bits(words, (uint64_t)d * (uint32_t)bits, (uint32_t)bits)];
 }
+// Doc-order DISTINCTCOUNTHLL entries packed to 16 bits for log2m <= 11: (register << 5) | rho (rho <= 33 - log2m < 32)
+// from the per-id (register << 8) | rho table -- half the bytes a matched doc's HLL update reads.
+__global__ void materialize_hll16_kernel(const uint32_t *__restrict__ words, int32_t bits, const uint32_t *__restrict__ table,
+                                         int64_t n, uint16_t *__restrict__ out) {
+  for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = table[decode_bits(words, (uint64_t)d * (uint32_t)bits, (uint32_t)bits)];
+    out[d] = (uint16_t)(((e >> 8) << 5) | (e & 31u));
+  }
+}
+hipError_t launch_materialize_hll16(const uint32_t *words, int32_t bits, const uint32_t *table, int64_t n, uint16_t *out,
+                                    hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  materialize_hll16_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(words, bits, table, n, out);
+  return hipGetLastError();
+}
 hipError_t launch_materialize(const uint32_t *words, int32_t bits, const void *dict, int32_t width, int64_t n,
                               void *vals, hipStream_t s) {
   if (n <= 0) return hipSuccess;

@@ -104,6 +104,8 @@ hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *in, 
                                   int64_t *num_out, int64_t n, hipStream_t s);
 hipError_t launch_raw_key_ids(const void *raw, int32_t type, int64_t n, const uint64_t *uniq, int64_t u, int32_t *ids,
                               hipStream_t s);
+hipError_t launch_materialize_hll16(const uint32_t *words, int32_t bits, const uint32_t *table, int64_t n, uint16_t *out,
+                                    hipStream_t s);
 hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s,
                              const uint64_t *nulls = nullptr);
 hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
@@ -373,6 +375,7 @@ struct ColumnStore {
   std::vector<int32_t> sorted_pairs;  // sorted columns: (start,end) per dict id
   std::map<int, uint32_t *> hll;      // per log2m
   std::map<int, uint32_t *> hll_doc;  // per log2m: doc-order copy of hll (ensure_hll_doc), in the segment's allocations
+  std::map<int, uint16_t *> hll_doc16;  // per log2m <= 11: the same entries packed to 16 bits
   bool has_range = false;             // INT / LONG: value range (plan-time overflow bound of integer sums)
   int64_t vmin = 0, vmax = 0;
   int64_t nn_vmin = 0, nn_vmax = 0;   // raw INT / LONG with a null vector: the non-null values' range (null keys);
@@ -1470,6 +1473,23 @@ static int32_t ensure_hll_doc(Segment &sg, ColumnStore &c, int log2m, const uint
   *made = true;
   return PHIP_OK;
 }
+// ... packed to 16 bits when log2m <= 11 ((register << 5) | rho): half the bytes per matched doc
+static int32_t ensure_hll_doc16(Segment &sg, ColumnStore &c, int log2m, const uint32_t *table, hipStream_t st,
+                                bool *made, uint16_t **out) {
+  auto it = c.hll_doc16.find(log2m);
+  if (it != c.hll_doc16.end()) {
+    *out = it->second;
+    return PHIP_OK;
+  }
+  void *p;
+  int32_t rc = dev_alloc(sg, (size_t)std::max<int32_t>(sg.num_docs, 1) * 2, &p);
+  if (rc) return rc;
+  HIP_TRY(launch_materialize_hll16(c.words, c.bits, table, sg.num_docs, (uint16_t *)p, st));
+  c.hll_doc16[log2m] = (uint16_t *)p;
+  *out = (uint16_t *)p;
+  *made = true;
+  return PHIP_OK;
+}
 
 static int32_t ensure_vals(Segment &sg, ColumnStore &c, hipStream_t st, bool *made) {
   if (c.vals != nullptr) return PHIP_OK;
@@ -2117,6 +2137,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   dsegs.reserve((size_t)nseg * nprog);
   bool hll_made = false;
   std::vector<bool> hll_doc_used((size_t)nseg * ncols, false);  // (segment, column): HLL entries read by doc
+  std::vector<bool> hll_doc16_used((size_t)nseg * ncols, false);  // ... 16-bit ones
   const char *hde = getenv("PHIP_HLL_DOC");  // measurement override: "0" = gather the per-id table
   const char *mze = getenv("PHIP_MATERIALIZE");
   const bool hll_doc_on = !(hde && atoi(hde) == 0) && !(mze && atoi(mze) == 0) && !want_bitmap;
@@ -2157,10 +2178,21 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       if (rc) return rc;
       ds.cols[dq.aggs[a].col_a].hll = h;
       if (hll_doc_on && cs.words != nullptr && (int64_t)cs.card * 4 >= vals_min && vals_min >= 0) {
-        uint32_t *hd;
-        rc = ensure_hll_doc(sg, cs, dq.aggs[a].log2m, h, st, &hll_made, &hd);
-        if (rc) return rc;
-        ds.cols[dq.aggs[a].col_a].hll_doc = hd;
+        // 16-bit entries where log2m <= 11 (PHIP_HLL_DOC16=0: the 32-bit ones, A/B)
+        const char *h16 = getenv("PHIP_HLL_DOC16");
+        const bool doc16 = !(h16 && atoi(h16) == 0);
+        if (doc16 && dq.aggs[a].log2m <= 11) {
+          uint16_t *hd;
+          rc = ensure_hll_doc16(sg, cs, dq.aggs[a].log2m, h, st, &hll_made, &hd);
+          if (rc) return rc;
+          ds.cols[dq.aggs[a].col_a].hll_doc16 = hd;
+          hll_doc16_used[(size_t)s * ncols + dq.aggs[a].col_a] = true;
+        } else {
+          uint32_t *hd;
+          rc = ensure_hll_doc(sg, cs, dq.aggs[a].log2m, h, st, &hll_made, &hd);
+          if (rc) return rc;
+          ds.cols[dq.aggs[a].col_a].hll_doc = hd;
+        }
         hll_doc_used[(size_t)s * ncols + dq.aggs[a].col_a] = true;
       }
     }
@@ -2933,7 +2965,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       const bool raw = (as_raw(s, c) && !ids_streamed[(size_t)s * ncols + c]) || hll_doc_used[(size_t)s * ncols + c];
       pc.bits.push_back(raw ? 0 : cs.bits);
       pc.card.push_back(raw ? 0 : cs.card);
-      pc.width.push_back(cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type));  // STRING: remap / HLL entry
+      pc.width.push_back(hll_doc16_used[(size_t)s * ncols + c] ? 2 : (cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type)));  // STRING: remap / HLL entry
     }
     P.proj.push_back(pc);
   }

@@ -80,6 +80,9 @@ hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t, const int32_t 
   memset(tab, 0, (size_t)words * kXcdCopies * 8);
   return hipSuccess;
 }
+hipError_t launch_materialize_hll16(const uint32_t *, int32_t, const uint32_t *, int64_t, uint16_t *, hipStream_t) {
+  return hipSuccess;
+}
 hipError_t launch_raw_images(const void *, int32_t, int64_t, uint64_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *, uint64_t *, uint64_t *, int64_t *num_out,
                                   int64_t, hipStream_t) {
