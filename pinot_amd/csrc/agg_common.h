@@ -26,7 +26,12 @@ __device__ __forceinline__ double dict_f64(ccol_t &c, uint32_t id) {
     default: return ((const PHIP_GLB double *)c.dict)[id];
   }
 }
+// doc-order values bit-packed at the column's range width (DevCol.vpack): one window load, like a dictionary id
+__device__ __forceinline__ int64_t packed_i64(ccol_t &c, int32_t doc) {
+  return c.vbase + (int64_t)decode_bits(c.vpack, (uint64_t)(uint32_t)doc * (uint32_t)c.vbits, (uint32_t)c.vbits);
+}
 __device__ __forceinline__ int64_t raw_i64(ccol_t &c, int32_t doc) {
+  if (c.vpack != nullptr) return packed_i64(c, doc);
   switch (c.type) {
     case PHIP_TYPE_INT: return ((const PHIP_GLB int32_t *)c.raw)[doc];
     case PHIP_TYPE_LONG: return ((const PHIP_GLB int64_t *)c.raw)[doc];
@@ -35,6 +40,7 @@ __device__ __forceinline__ int64_t raw_i64(ccol_t &c, int32_t doc) {
   }
 }
 __device__ __forceinline__ double raw_f64(ccol_t &c, int32_t doc) {
+  if (c.vpack != nullptr) return (double)packed_i64(c, doc);
   switch (c.type) {
     case PHIP_TYPE_INT: return (double)((const PHIP_GLB int32_t *)c.raw)[doc];
     case PHIP_TYPE_LONG: return (double)((const PHIP_GLB int64_t *)c.raw)[doc];
@@ -337,6 +343,9 @@ __device__ __forceinline__ void batch_i64(ccol_t &c, const int32_t (&d)[U], cons
         for (int u = 0; u < U; u++) v[u] = dict_i64(c, id[u]);
         break;
     }
+  } else if (c.vpack != nullptr) {
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = packed_i64(c, d[u]);
   } else {
     switch (c.type) {
       case PHIP_TYPE_INT:

@@ -105,6 +105,10 @@ struct DevCol {
                             // of word d / 64); a null doc's key id is gb_null_id. null = no null key
   int64_t gb_null_id;
   const int32_t *gb_ids;    // raw FLOAT / DOUBLE group-by column: doc-order key ids (keys.hip), or null
+  const uint32_t *vpack;    // has_dict == 0, INT / LONG: doc-order values bit-packed (value - vbase in vbits bits,
+  int64_t vbase;            // the forward index's layout), or null: `raw` holds them typed
+  int32_t vbits;
+  int32_t vpad;
 };
 constexpr int kBitSliceMaxBits = 12;
 

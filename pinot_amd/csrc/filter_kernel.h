@@ -973,6 +973,12 @@ __device__ __forceinline__ uint32_t fused_id(ccol_t &c, const Tile &t, int32_t t
   return decode_bits(c.words, (uint64_t)(uint32_t)(t.doc0 + td) * b, b);
 }
 
+// a packed doc-order value (DevCol.vpack) streamed with the tile (the runtime stages the packed words like ids)
+__device__ __forceinline__ int64_t fused_packed(ccol_t &c, const Tile &t, int32_t td) {
+  const uint32_t b = (uint32_t)c.vbits;
+  return c.vbase + (int64_t)(window_at((const PHIP_LDS uint32_t *)(t.stage + c.lds_off), td * (int32_t)b) >> (32 - b));
+}
+
 __device__ __forceinline__ uint64_t small_dict_bits(const SmallDict &sd, uint32_t id, bool wide) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(id << 2), (int)sd.lo);
   if (!wide) return lo;
@@ -984,6 +990,11 @@ template <int U, bool kHbm>
 __device__ __forceinline__ void fused_f64_u(ccol_t &c, const SmallDict &sd, const Tile &t, const int32_t (&td)[U],
                                             double (&v)[U]) {
   if (!c.has_dict) {
+    if (!kHbm && c.lds_off >= 0) {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = (double)fused_packed(c, t, td[u]);
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < U; u++) v[u] = raw_f64(c, t.doc0 + td[u]);
     return;
@@ -1023,6 +1034,11 @@ template <int U, bool kHbm>
 __device__ __forceinline__ void fused_i64_u(ccol_t &c, const SmallDict &sd, const Tile &t, const int32_t (&td)[U],
                                             int64_t (&v)[U]) {
   if (!c.has_dict) {
+    if (!kHbm && c.lds_off >= 0) {
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = fused_packed(c, t, td[u]);
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < U; u++) v[u] = raw_i64(c, t.doc0 + td[u]);
     return;

@@ -101,6 +101,37 @@ hipError_t launch_materialize_hll16(const uint32_t *words, int32_t bits, const u
   materialize_hll16_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(words, bits, table, n, out);
   return hipGetLastError();
 }
+// Doc-order values of an INT / LONG dictionary column bit-packed at the width of its value range: doc d's value - base
+// as vbits stream bits at d * vbits (the forward index's own layout, bit 31 of word k = stream bit 32k), read back
+// with decode_bits. One thread assembles one output word from the <= 3 docs overlapping it, so nothing is shared.
+template <typename T>
+__global__ void materialize_packed_kernel(const uint32_t *__restrict__ words, int32_t bits, const T *__restrict__ dict,
+                                          int64_t n, int64_t base, int32_t vbits, int64_t nwords,
+                                          uint32_t *__restrict__ out) {
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t first = 32 * w;
+    const int64_t d0 = first / vbits;
+    const int64_t d1 = std::min<int64_t>(n - 1, (first + 31) / vbits);
+    uint32_t acc = 0;
+    for (int64_t d = d0; d <= d1; d++) {
+      const uint64_t v = (uint64_t)((int64_t)dict[decode_bits(words, (uint64_t)d * (uint32_t)bits, (uint32_t)bits)] - base);
+      const int64_t sh = 32 - (d * vbits - first) - vbits;  // in [1 - vbits, 31]
+      acc |= sh >= 0 ? (uint32_t)(v << sh) : (uint32_t)(v >> -sh);
+    }
+    out[w] = acc;
+  }
+}
+hipError_t launch_materialize_packed(const uint32_t *words, int32_t bits, const void *dict, int32_t width, int64_t n,
+                                     int64_t base, int32_t vbits, int64_t nwords, uint32_t *out, hipStream_t s) {
+  if (nwords <= 0) return hipSuccess;
+  if (width == 4)
+    materialize_packed_kernel<int32_t><<<grid_for(nwords, 256, 8192), 256, 0, s>>>(words, bits, (const int32_t *)dict,
+                                                                                    n, base, vbits, nwords, out);
+  else
+    materialize_packed_kernel<int64_t><<<grid_for(nwords, 256, 8192), 256, 0, s>>>(words, bits, (const int64_t *)dict,
+                                                                                    n, base, vbits, nwords, out);
+  return hipGetLastError();
+}
 hipError_t launch_materialize(const uint32_t *words, int32_t bits, const void *dict, int32_t width, int64_t n,
                               void *vals, hipStream_t s) {
   if (n <= 0) return hipSuccess;

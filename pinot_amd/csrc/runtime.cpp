@@ -111,6 +111,8 @@ hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *
 hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
                                       int32_t *err, int32_t *sizes, uint8_t *lits, uint64_t lits_stride, hipStream_t s);
 hipError_t launch_bitslice(const uint32_t *words, int32_t bits, int64_t ntiles, uint32_t *planes, hipStream_t s);
+hipError_t launch_materialize_packed(const uint32_t *words, int32_t bits, const void *dict, int32_t width, int64_t n,
+                                     int64_t base, int32_t vbits, int64_t nwords, uint32_t *out, hipStream_t s);
 hipError_t launch_materialize(const uint32_t *words, int32_t bits, const void *dict, int32_t width, int64_t n,
                               void *vals, hipStream_t s);
 hipError_t launch_varbyte_offsets(const uint8_t *stage, const uint64_t *chunk_base, const int32_t *chunk_size,
@@ -369,6 +371,8 @@ struct ColumnStore {
   uint64_t str_total = 0;       // raw STRING: bytes of all values
   uint32_t *planes = nullptr;   // bit-sliced copy of words (fixed-bit columns of <= kBitSliceMaxBits bits)
   void *vals = nullptr;         // numeric dictionary column: doc-order LE values (ensure_vals), made on first use
+  uint32_t *vpack = nullptr;    // ... INT / LONG: the same values bit-packed at the range's width (value - vmin)
+  int32_t vbits = 0;
   uint64_t *nulls = nullptr;    // null value vector as dense doc words (load_null_vector), or null: no null doc
   int64_t null_count = 0;
   std::vector<uint8_t> host_dict;  // dictionary bytes as given (BE / padded strings)
@@ -1491,7 +1495,35 @@ static int32_t ensure_hll_doc16(Segment &sg, ColumnStore &c, int log2m, const ui
   return PHIP_OK;
 }
 
-static int32_t ensure_vals(Segment &sg, ColumnStore &c, hipStream_t st, bool *made) {
+// Bits per doc of an INT / LONG column's values packed relative to its minimum (the dictionary's first entry), or 0
+// when packing saves nothing (the range needs the type's width, or more than decode_bits' 32).
+static int32_t packed_value_bits(const ColumnStore &c) {
+  if (!c.has_range || (c.type != PHIP_TYPE_INT && c.type != PHIP_TYPE_LONG)) return 0;
+  const uint64_t r = (uint64_t)c.vmax - (uint64_t)c.vmin;
+  const int32_t b = r == 0 ? 1 : 64 - __builtin_clzll(r);
+  return b <= 32 && b < 8 * type_width(c.type) ? b : 0;
+}
+static bool vpack_enabled() {
+  const char *e = getenv("PHIP_VPACK");  // measurement override: "0" = typed doc-order values
+  return !(e && atoi(e) == 0);
+}
+// (packed when the range allows and vpack_enabled(): e.g. LO_EXTENDEDPRICE in 24 bits, LO_SUPPLYCOST in 17)
+static int32_t ensure_vals(Segment &sg, ColumnStore &c, hipStream_t st, bool *made, bool pack) {
+  if (pack && packed_value_bits(c) > 0) {
+    if (c.vpack != nullptr) return PHIP_OK;
+    const int32_t vb = packed_value_bits(c);
+    // whole tiles (the filter kernel may stream them like ids) + 4 guard words, like the forward index's words
+    const int64_t nwords = round_up(std::max<int64_t>(sg.num_docs, 1), kTileDocs) * vb / 32 + 4;
+    void *p;
+    int32_t rc = dev_alloc(sg, (size_t)nwords * 4, &p);
+    if (rc) return rc;
+    HIP_TRY(launch_materialize_packed(c.words, c.bits, c.dict, type_width(c.type), sg.num_docs, c.vmin, vb, nwords,
+                                      (uint32_t *)p, st));
+    c.vpack = (uint32_t *)p;
+    c.vbits = vb;
+    *made = true;
+    return PHIP_OK;
+  }
   if (c.vals != nullptr) return PHIP_OK;
   const int w = type_width(c.type);
   void *p;
@@ -1869,6 +1901,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   // from the Infinity Cache). The kernels take such a column as a raw one (DevCol.has_dict = 0).
   std::vector<bool> use_vals(ncols, false);
   const int64_t vals_min = materialize_min_dict();
+  const bool vpack_on = vpack_enabled();
   {
     const char *me = getenv("PHIP_MATERIALIZE");  // measurement override: "0" = ids + dictionary gathers
     if (!(me && atoi(me) == 0) && !want_bitmap && vals_min >= 0) {
@@ -1895,16 +1928,17 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       for (int s = 0; s < nseg; s++) {
         ColumnStore &cs = segs[s]->cols[colidx[s][c]];
         if (!vals_eligible(cs, vals_min)) continue;
-        int32_t rc = ensure_vals(*segs[s], cs, st, &made);
+        int32_t rc = ensure_vals(*segs[s], cs, st, &made, vpack_on);
         if (rc) return rc;
       }
     }
     if (made) HIP_TRY(hipStreamSynchronize(st));
   }
-  // column c of segment s read as raw values (no dictionary, or its doc-order values above)
+  // column c of segment s read as raw values (no dictionary, or its doc-order values above, packed or typed)
+  auto packed_vals = [&](const ColumnStore &cs) -> bool { return vpack_on && cs.vpack != nullptr; };
   auto as_raw = [&](int s, int c) -> bool {
     const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
-    return no_dict(cs) || (use_vals[c] && cs.vals != nullptr && vals_eligible(cs, vals_min));
+    return no_dict(cs) || (use_vals[c] && (packed_vals(cs) || cs.vals != nullptr) && vals_eligible(cs, vals_min));
   };
   // Batched dense-tile walk (aggregate.hip agg_batch) only when every dictionary the aggregations
   // gather from is small enough to stay cache-resident. Gathers from a large dictionary (~1M distinct
@@ -2160,8 +2194,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dc.type = cs.type;
       dc.has_dict = !no_dict(cs);
       if (dc.has_dict && as_raw(s, c)) {  // doc-order values of a value-only column
-        dc.raw = cs.vals;
         dc.has_dict = 0;
+        if (packed_vals(cs)) {
+          dc.raw = nullptr;
+          dc.vpack = cs.vpack;
+          dc.vbase = cs.vmin;
+          dc.vbits = cs.vbits;
+        } else {
+          dc.raw = cs.vals;
+        }
       }
       dc.hll_rows = cs.hll_log2m;
       dc.str_off = cs.str_off;
@@ -2831,6 +2872,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     if (fuse && any_value) {
       fused_naggs = naggs;
       const char *sv = getenv("PHIP_STREAM_VALUES");  // measurement override: "0" never, "1" always
+      const char *sp = getenv("PHIP_STREAM_PACKED");  // measurement override: "0" = stream ids + dictionary instead
       const double kStreamValueMin = 0.5;
       for (size_t i = 0; i < dsegs.size(); i++) {
         DevSeg &ds = dsegs[i];
@@ -2849,20 +2891,24 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
             const ColumnStore &cs = segs[sidx]->cols[colidx[sidx][c]];
             const bool via_vals = !dc.has_dict && !no_dict(cs);
             if (!dc.has_dict && !via_vals) continue;
-            const int32_t bits = via_vals ? cs.bits : dc.bits;
+            // packed values stream as they are (vbits per doc, no dictionary gather after): fused_i64_u / fused_f64_u
+            const bool via_packed = via_vals && dc.vpack != nullptr && !(sp && atoi(sp) == 0);
+            const int32_t bits = via_packed ? dc.vbits : via_vals ? cs.bits : dc.bits;
             const bool dense = seg_est[i] * (1024.0 / std::max(1, bits)) >= kStreamValueMin;
             if (!(sv ? atoi(sv) != 0 : (dense && !big))) continue;
             const int32_t bytes = 256 * bits;
             // (DevSeg.stage holds kMaxStage sources; the fused kernel's cursor takes up to kMaxConj + kMaxAggStage)
             if (ds.num_stage >= std::min(kMaxStage, kMaxConj + kMaxAggStage) || off + bytes + 2 * kStagePad > kSlotBudget)
               continue;
-            if (via_vals) {
+            if (via_vals && !via_packed) {
               dc.has_dict = 1;
               dc.raw = cs.raw;
+              dc.vpack = nullptr;
+              dc.vbits = 0;
               ids_streamed[(size_t)sidx * ncols + c] = true;
             }
             dc.lds_off = off + kStagePad;
-            ds.stage[ds.num_stage++] = {(const uint8_t *)dc.words, bytes, dc.lds_off};
+            ds.stage[ds.num_stage++] = {(const uint8_t *)(via_packed ? dc.vpack : dc.words), bytes, dc.lds_off};
             ds.num_dma += (int32_t)ceil_div(bytes, 1024);
             off += bytes + 2 * kStagePad;
           }
@@ -2963,7 +3009,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     for (int s = 0; s < nseg; s++) {
       const ColumnStore &cs = segs[s]->cols[colidx[s][c]];
       const bool raw = (as_raw(s, c) && !ids_streamed[(size_t)s * ncols + c]) || hll_doc_used[(size_t)s * ncols + c];
-      pc.bits.push_back(raw ? 0 : cs.bits);
+      // (packed doc-order values: vbits per doc and no dictionary)
+      const bool packed = raw && !no_dict(cs) && !hll_doc_used[(size_t)s * ncols + c] && packed_vals(cs);
+      pc.bits.push_back(packed ? cs.vbits : raw ? 0 : cs.bits);
       pc.card.push_back(raw ? 0 : cs.card);
       pc.width.push_back(hll_doc16_used[(size_t)s * ncols + c] ? 2 : (cs.type == PHIP_TYPE_STRING ? 4 : type_width(cs.type)));  // STRING: remap / HLL entry
     }

@@ -83,6 +83,10 @@ hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t, const int32_t 
 hipError_t launch_materialize_hll16(const uint32_t *, int32_t, const uint32_t *, int64_t, uint16_t *, hipStream_t) {
   return hipSuccess;
 }
+hipError_t launch_materialize_packed(const uint32_t *, int32_t, const void *, int32_t, int64_t, int64_t, int32_t, int64_t,
+                                     uint32_t *, hipStream_t) {
+  return hipSuccess;
+}
 hipError_t launch_raw_images(const void *, int32_t, int64_t, uint64_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *, uint64_t *, uint64_t *, int64_t *num_out,
                                   int64_t, hipStream_t) {

@@ -4,7 +4,9 @@ gather. Every path that projects values (fused filter+aggregation, the aggregati
 LDS / HBM / hash group-by tables, filtered aggregations) must give the oracle's answers with the values on
 (PHIP_MATERIALIZE_MIN_DICT=0: every numeric dictionary), at the default threshold, and off (PHIP_MATERIALIZE=0);
 columns a filter or group-by also reads keep their ids. DISTINCTCOUNTHLL over a large dictionary reads doc-order
-registers entries (ensure_hll_doc) the same way: registers bit-exact."""
+registers entries (ensure_hll_doc) the same way: registers bit-exact. INT / LONG values whose range fits fewer bits
+than the type are bit-packed at that width relative to the dictionary's minimum (DevCol.vpack; "typed" mode turns
+that off): negative values, ranges of 1 value, LONG columns around 2^40 and a 32-bit range are all exact."""
 import numpy as np
 import pytest
 
@@ -17,7 +19,8 @@ from tests import fixtures
 
 pytestmark = pytest.mark.gpu
 
-MODES = {"all": {"PHIP_MATERIALIZE_MIN_DICT": "0"}, "default": {}, "off": {"PHIP_MATERIALIZE": "0"}}
+MODES = {"all": {"PHIP_MATERIALIZE_MIN_DICT": "0"}, "default": {}, "off": {"PHIP_MATERIALIZE": "0"},
+         "typed": {"PHIP_MATERIALIZE_MIN_DICT": "0", "PHIP_VPACK": "0"}}
 
 
 @pytest.fixture(scope="module")
@@ -34,6 +37,11 @@ def mat_segments(gpu_lib):
         c.add_column("l", DataType.LONG, rng.integers(-10 ** 15, 10 ** 15, n))
         c.add_column("d", DataType.DOUBLE, np.round(rng.normal(0, 1e4, n), 2))
         c.add_column("fl", DataType.FLOAT, np.round(rng.normal(0, 50, n), 1).astype(np.float32))
+        c.add_column("ni", DataType.INT, rng.integers(-70_000, 60_000, n))                  # negative, 17 bits
+        c.add_column("nl", DataType.LONG, (1 << 40) + rng.integers(-5_000_000, 5_000_000, n))  # LONG in 24 bits
+        c.add_column("w", DataType.INT, rng.integers(-2 ** 31, 2 ** 31 - 1, n))            # 32-bit range: typed
+        c.add_column("lw", DataType.LONG, rng.integers(0, 2 ** 32, n) - 2 ** 31)            # LONG in 32 bits
+        c.add_column("one", DataType.INT, np.full(n, -17 + k))                              # one value: 1 bit
         raws.append(c.build())
     segs = [GpuSegment(r) for r in raws]
     yield raws, segs
@@ -50,6 +58,10 @@ AGG = [
     "SELECT SUM(p) FILTER (WHERE f < 10), MAX(l) FILTER (WHERE g = 3), COUNT(*) FROM t WHERE q > 5",
     "SELECT DISTINCTCOUNTHLL(p), COUNT(*) FROM t WHERE f < 30",                # doc-order HLL entries
     "SELECT DISTINCTCOUNTHLL(l, 10), DISTINCTCOUNTHLL(q, 10), SUM(p) FROM t WHERE g <> 4",
+    "SELECT SUM(ni), MIN(ni), MAX(nl), SUM(nl), SUM(one), MIN(lw) FROM t WHERE f < 30 AND g BETWEEN 1 AND 4",
+    "SELECT SUM(ni * q), MAX(w), MIN(w), SUM(lw), SUM(w) FROM t WHERE f >= 2",
+    "SELECT SUM(nl - ni), MIN(one), MAX(lw), SUM(one * ni) FROM t WHERE f = 7",
+    "SELECT SUM(ni), SUM(nl), SUM(lw), MAX(one) FROM t",
 ]
 GROUP_BY = [
     "SELECT g, SUM(p), MAX(d), COUNT(*) FROM t WHERE f < 50 GROUP BY g LIMIT 1000",
@@ -58,6 +70,8 @@ GROUP_BY = [
     "SELECT p, COUNT(*) FROM t WHERE f < 3 GROUP BY p LIMIT 100000",               # p a key: ids
     "SELECT g, DISTINCTCOUNTHLL(p), SUM(l) FROM t WHERE f < 60 GROUP BY g LIMIT 100",  # HLL in an LDS table
     "SELECT g, q, DISTINCTCOUNTHLL(l) FROM t GROUP BY g, q LIMIT 100000",
+    "SELECT g, SUM(ni), MIN(nl), MAX(lw), SUM(one * ni) FROM t WHERE f < 50 GROUP BY g LIMIT 1000",
+    "SELECT g, q, SUM(nl), MAX(ni), SUM(w) FROM t GROUP BY g, q LIMIT 100000",
 ]
 
 
@@ -108,3 +122,14 @@ def test_gpu_materialized_values_memory(mat_segments, monkeypatch):
     assert again == after
     for r, b, a in zip(raws, before, after):
         assert a - b in (0, 8 * r.num_docs)  # (0: an earlier test of this module made them)
+
+
+def test_gpu_packed_values_memory(mat_segments, monkeypatch):
+    """Packed values take whole 2048-doc tiles x bits / 32 + 4 guard words: ni's range needs 17 bits, nl's 24."""
+    raws, segs = mat_segments
+    for col, bits in (("ni", 17), ("nl", 24)):
+        before = [s.device_bytes() for s in segs]
+        _run(f"SELECT SUM({col}) FROM t WHERE f < 40", "all", mat_segments, monkeypatch)
+        after = [s.device_bytes() for s in segs]
+        for r, b, a in zip(raws, before, after):
+            assert a - b in (0, 4 * (-(-r.num_docs // 2048) * 2048 * bits // 32 + 4))
