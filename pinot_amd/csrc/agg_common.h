@@ -132,15 +132,48 @@ __device__ __forceinline__ int32_t murmur_hash_long_dev(int64_t data) {
   h ^= h >> 15;
   return (int32_t)h;
 }
-__device__ __forceinline__ uint32_t hll_entry_bits(int64_t x, int log2m) {
-  const uint32_t ux = (uint32_t)murmur_hash_long_dev(x);
+// clearspring MurmurHash.hash(byte[]) with seed -1, as HyperLogLog.offer hashes a String's bytes (the same function
+// ensure_hll applies to STRING dictionary entries): a raw STRING doc's UTF-8 bytes, read a byte at a time (unaligned)
+__device__ __forceinline__ uint32_t murmur_hash_bytes_dev(const PHIP_GLB uint8_t *d, int32_t len) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = 0xffffffffu ^ (uint32_t)len;
+  const int32_t n4 = len >> 2;
+  for (int32_t i = 0; i < n4; i++) {
+    uint32_t k = (uint32_t)d[4 * i] | ((uint32_t)d[4 * i + 1] << 8) | ((uint32_t)d[4 * i + 2] << 16) |
+                 ((uint32_t)d[4 * i + 3] << 24);
+    k *= m;
+    k ^= k >> 24;
+    k *= m;
+    h *= m;
+    h ^= k;
+  }
+  const int32_t left = len - (n4 << 2);
+  if (left) {  // (Java bytes are signed: each tail byte sign-extends)
+    if (left >= 3) h ^= (uint32_t)((int32_t)(int8_t)d[len - 3] << 16);
+    if (left >= 2) h ^= (uint32_t)((int32_t)(int8_t)d[len - 2] << 8);
+    h ^= (uint32_t)(int32_t)(int8_t)d[len - 1];
+    h *= m;
+  }
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return h;
+}
+__device__ __forceinline__ uint32_t hll_entry_hash(uint32_t ux, int log2m) {
   const uint32_t j = ux >> (32 - log2m);
   const uint32_t w = (ux << log2m) | ((1u << (log2m - 1)) + 1u);
   return (j << 8) | ((uint32_t)__builtin_clz(w) + 1u);
 }
+__device__ __forceinline__ uint32_t hll_entry_bits(int64_t x, int log2m) {
+  return hll_entry_hash((uint32_t)murmur_hash_long_dev(x), log2m);
+}
 __device__ __forceinline__ uint32_t hll_entry_raw(ccol_t &c, int32_t doc, int log2m) {
   int64_t x;
   switch (c.type) {
+    case PHIP_TYPE_STRING: {
+      const uint64_t b = c.str_off[doc], e = c.str_off[doc + 1];
+      return hll_entry_hash(murmur_hash_bytes_dev((const PHIP_GLB uint8_t *)c.raw + b, (int32_t)(e - b)), log2m);
+    }
     case PHIP_TYPE_INT: x = ((const PHIP_GLB int32_t *)c.raw)[doc]; break;
     case PHIP_TYPE_LONG: x = ((const PHIP_GLB int64_t *)c.raw)[doc]; break;
     case PHIP_TYPE_FLOAT: x = ((const PHIP_GLB int32_t *)c.raw)[doc]; break;

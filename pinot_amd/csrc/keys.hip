@@ -44,6 +44,73 @@ __global__ void raw_key_ids_kernel(const void *__restrict__ raw, int32_t type, i
   }
 }
 
+// Raw STRING keys: the same scheme over a 64-bit hash of each doc's UTF-8 bytes (FNV-1a with a final avalanche).
+// Per segment the (hash, doc) pairs are sorted and made unique by hash, keeping a representative doc per hash; every
+// doc's bytes are compared with its representative's (a hash collision inside a segment sets *collided), the host
+// compares representatives across segments, sorts the distinct strings bytewise (the STRING dictionaries' order) and
+// hands back a segment-hash-index -> global-id map for raw_str_ids_kernel.
+__device__ __forceinline__ uint64_t str_hash64(const uint8_t *p, int64_t len) {
+  uint64_t h = 0xcbf29ce484222325ull ^ (uint64_t)len;
+  for (int64_t i = 0; i < len; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
+}
+
+__global__ void str_hash_kernel(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off, int64_t n,
+                                uint64_t *__restrict__ hash, int32_t *__restrict__ docs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    hash[i] = str_hash64(bytes + off[i], (int64_t)(off[i + 1] - off[i]));
+    docs[i] = (int32_t)i;
+  }
+}
+
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t *a, int64_t u, uint64_t k) {
+  int64_t lo = 0, hi = u;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void str_verify_kernel(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off, int64_t n,
+                                  const uint64_t *__restrict__ uniq, const int32_t *__restrict__ rep, int64_t u,
+                                  int32_t *__restrict__ collided) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t len = (int64_t)(off[i + 1] - off[i]);
+    const int64_t r = rep[lower_bound_u64(uniq, u, str_hash64(bytes + off[i], len))];
+    bool same = (int64_t)(off[r + 1] - off[r]) == len;
+    for (int64_t b = 0; same && b < len; b++) same = bytes[off[i] + b] == bytes[off[r] + b];
+    if (!same) *collided = 1;  // (vector store; any colliding doc's lane may write it)
+  }
+}
+
+// the representatives' lengths, then (dst offsets from the host) their bytes back to back
+__global__ void str_rep_lens_kernel(const uint64_t *__restrict__ off, const int32_t *__restrict__ rep, int64_t u,
+                                    uint32_t *__restrict__ lens) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < u; j += (int64_t)gridDim.x * blockDim.x)
+    lens[j] = (uint32_t)(off[rep[j] + 1] - off[rep[j]]);
+}
+__global__ void str_rep_bytes_kernel(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off,
+                                     const int32_t *__restrict__ rep, int64_t u, const uint64_t *__restrict__ dst_off,
+                                     uint8_t *__restrict__ dst) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < u; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t s = off[rep[j]], len = off[rep[j] + 1] - s;
+    for (uint64_t b = 0; b < len; b++) dst[dst_off[j] + b] = bytes[s + b];
+  }
+}
+
+__global__ void raw_str_ids_kernel(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off, int64_t n,
+                                   const uint64_t *__restrict__ uniq, int64_t u, const int32_t *__restrict__ map,
+                                   int32_t *__restrict__ ids) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ids[i] = map[lower_bound_u64(uniq, u, str_hash64(bytes + off[i], (int64_t)(off[i + 1] - off[i])))];
+}
+
 static inline int keys_grid(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -77,6 +144,58 @@ hipError_t launch_raw_key_ids(const void *raw, int32_t type, int64_t n, const ui
                               hipStream_t s) {
   if (n <= 0) return hipSuccess;
   raw_key_ids_kernel<<<keys_grid(n), 256, 0, s>>>(raw, type, n, uniq, u, ids);
+  return hipGetLastError();
+}
+
+// (pairs sorted by hash, unique by hash with the first doc of each run; temp == nullptr: the scratch bytes)
+hipError_t launch_str_hash_unique(void *temp, size_t *temp_bytes, const uint8_t *bytes, const uint64_t *off, int64_t n,
+                                  uint64_t *hash, int32_t *docs, uint64_t *hash_sorted, int32_t *docs_sorted,
+                                  uint64_t *uniq, int32_t *rep, int64_t *num_out, hipStream_t s) {
+  size_t a = 0, b = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint64_t *)hash, hash_sorted, (const int32_t *)docs,
+                                                    docs_sorted, (int)n, 0, 64, s);
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceSelect::UniqueByKey(nullptr, b, (const uint64_t *)hash_sorted, (const int32_t *)docs_sorted, uniq, rep,
+                                        num_out, (int)n, s);
+  if (e != hipSuccess) return e;
+  if (temp == nullptr) {
+    *temp_bytes = a > b ? a : b;
+    return hipSuccess;
+  }
+  if (n <= 0) return hipMemsetAsync(num_out, 0, 8, s);
+  str_hash_kernel<<<keys_grid(n), 256, 0, s>>>(bytes, off, n, hash, docs);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  e = hipcub::DeviceRadixSort::SortPairs(temp, a, (const uint64_t *)hash, hash_sorted, (const int32_t *)docs, docs_sorted,
+                                         (int)n, 0, 64, s);
+  if (e != hipSuccess) return e;
+  return hipcub::DeviceSelect::UniqueByKey(temp, b, (const uint64_t *)hash_sorted, (const int32_t *)docs_sorted, uniq, rep,
+                                           num_out, (int)n, s);
+}
+
+hipError_t launch_str_verify(const uint8_t *bytes, const uint64_t *off, int64_t n, const uint64_t *uniq, const int32_t *rep,
+                             int64_t u, int32_t *collided, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  str_verify_kernel<<<keys_grid(n), 256, 0, s>>>(bytes, off, n, uniq, rep, u, collided);
+  return hipGetLastError();
+}
+
+hipError_t launch_str_rep_lens(const uint64_t *off, const int32_t *rep, int64_t u, uint32_t *lens, hipStream_t s) {
+  if (u <= 0) return hipSuccess;
+  str_rep_lens_kernel<<<keys_grid(u), 256, 0, s>>>(off, rep, u, lens);
+  return hipGetLastError();
+}
+
+hipError_t launch_str_rep_bytes(const uint8_t *bytes, const uint64_t *off, const int32_t *rep, int64_t u,
+                                const uint64_t *dst_off, uint8_t *dst, hipStream_t s) {
+  if (u <= 0) return hipSuccess;
+  str_rep_bytes_kernel<<<keys_grid(u), 256, 0, s>>>(bytes, off, rep, u, dst_off, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_raw_str_ids(const uint8_t *bytes, const uint64_t *off, int64_t n, const uint64_t *uniq, int64_t u,
+                              const int32_t *map, int32_t *ids, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  raw_str_ids_kernel<<<keys_grid(n), 256, 0, s>>>(bytes, off, n, uniq, u, map, ids);
   return hipGetLastError();
 }
 

@@ -102,6 +102,16 @@ hipError_t launch_limit_reduce(const uint64_t *k, const int64_t *slot2, int64_t 
 hipError_t launch_raw_images(const void *raw, int32_t type, int64_t n, uint64_t *out, hipStream_t s);
 hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *in, uint64_t *sorted, uint64_t *out,
                                   int64_t *num_out, int64_t n, hipStream_t s);
+hipError_t launch_str_hash_unique(void *temp, size_t *temp_bytes, const uint8_t *bytes, const uint64_t *off, int64_t n,
+                                  uint64_t *hash, int32_t *docs, uint64_t *hash_sorted, int32_t *docs_sorted,
+                                  uint64_t *uniq, int32_t *rep, int64_t *num_out, hipStream_t s);
+hipError_t launch_str_verify(const uint8_t *bytes, const uint64_t *off, int64_t n, const uint64_t *uniq, const int32_t *rep,
+                             int64_t u, int32_t *collided, hipStream_t s);
+hipError_t launch_str_rep_lens(const uint64_t *off, const int32_t *rep, int64_t u, uint32_t *lens, hipStream_t s);
+hipError_t launch_str_rep_bytes(const uint8_t *bytes, const uint64_t *off, const int32_t *rep, int64_t u,
+                                const uint64_t *dst_off, uint8_t *dst, hipStream_t s);
+hipError_t launch_raw_str_ids(const uint8_t *bytes, const uint64_t *off, int64_t n, const uint64_t *uniq, int64_t u,
+                              const int32_t *map, int32_t *ids, hipStream_t s);
 hipError_t launch_raw_key_ids(const void *raw, int32_t type, int64_t n, const uint64_t *uniq, int64_t u, int32_t *ids,
                               hipStream_t s);
 hipError_t launch_materialize_hll16(const uint32_t *words, int32_t bits, const uint32_t *table, int64_t n, uint16_t *out,
@@ -336,7 +346,7 @@ struct Device {
     bool raw = false;             // a raw INT / LONG column: id = value - raw_base (values not materialised)
     int64_t raw_base = 0;
     std::vector<uint8_t> values;  // LE typed or fixed-width strings
-    std::vector<int32_t *> ids;   // raw FLOAT / DOUBLE column: per segment its docs' ids into `values` (keys.hip)
+    std::vector<int32_t *> ids;   // raw FLOAT / DOUBLE / STRING column: per segment its docs' ids into `values` (keys.hip)
     ~Remap() {
       for (auto *p : dev)
         if (p) (void)hipFree(p);
@@ -1266,6 +1276,131 @@ static int32_t raw_real_key_ids(Device &dev, const std::vector<Segment *> &segs,
   return PHIP_OK;
 }
 
+// Raw STRING keys (the no-dictionary generators key a String by its value): per segment the docs' 64-bit hashes are
+// sorted and made unique on the device with a representative doc each, every doc is compared with its representative
+// (keys.hip), the representatives' bytes come to the host, which checks equal hashes across segments hold equal
+// strings, sorts the distinct strings bytewise (the STRING dictionaries' padded order) and maps each segment's hashes
+// to global ids for the doc-order id column. A hash collision refuses the plan (PHIP_ERR_UNSUPPORTED).
+static int32_t raw_string_key_ids(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
+                                  const std::string &name, Device::Remap &r) {
+  hipStream_t st = dev.stream;
+  std::vector<void *> tmp;
+  struct Free {
+    std::vector<void *> &v;
+    ~Free() {
+      for (void *p : v) (void)hipFree(p);
+    }
+  } free_tmp{tmp};
+  auto alloc = [&](size_t bytes, void **p) -> int32_t {
+    HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    tmp.push_back(*p);
+    return PHIP_OK;
+  };
+  void *flag;
+  int32_t rc;
+  if ((rc = alloc(8, &flag))) return rc;
+  HIP_TRY(hipMemsetAsync(flag, 0, 8, st));
+  std::vector<uint64_t *> seg_uniq(segs.size(), nullptr);
+  std::vector<int64_t> seg_u(segs.size(), 0);
+  std::vector<std::vector<uint64_t>> seg_hash(segs.size());
+  std::vector<std::vector<std::string>> seg_str(segs.size());
+  for (size_t i = 0; i < segs.size(); i++) {
+    const ColumnStore &c = segs[i]->cols[colidx[i]];
+    if (!no_dict(c) || c.fwd_kind != PHIP_FWD_RAW_CHUNK || c.type != PHIP_TYPE_STRING || c.str_off == nullptr)
+      return fail(PHIP_ERR_UNSUPPORTED, "group-by on column %s: raw in some segments only", name.c_str());
+    const int64_t n = segs[i]->num_docs;
+    if (n <= 0) continue;
+    if (n > INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s: segment over 2^31 docs", name.c_str());
+    const uint8_t *bytes = (const uint8_t *)c.raw;
+    void *h, *d, *hs, *ds, *uq, *rp, *cnt, *scratch;
+    size_t sb = 0;
+    if ((rc = alloc((size_t)n * 8, &h)) || (rc = alloc((size_t)n * 4, &d)) || (rc = alloc((size_t)n * 8, &hs)) ||
+        (rc = alloc((size_t)n * 4, &ds)) || (rc = alloc((size_t)n * 8, &uq)) || (rc = alloc((size_t)n * 4, &rp)) ||
+        (rc = alloc(8, &cnt)))
+      return rc;
+    HIP_TRY(launch_str_hash_unique(nullptr, &sb, bytes, c.str_off, n, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                   nullptr, st));
+    if ((rc = alloc(sb, &scratch))) return rc;
+    HIP_TRY(launch_str_hash_unique(scratch, &sb, bytes, c.str_off, n, (uint64_t *)h, (int32_t *)d, (uint64_t *)hs,
+                                   (int32_t *)ds, (uint64_t *)uq, (int32_t *)rp, (int64_t *)cnt, st));
+    int64_t u = 0;
+    HIP_TRY(hipMemcpyAsync(&u, cnt, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(launch_str_verify(bytes, c.str_off, n, (const uint64_t *)uq, (const int32_t *)rp, u, (int32_t *)flag, st));
+    void *lens, *doff;
+    if ((rc = alloc((size_t)u * 4, &lens)) || (rc = alloc((size_t)u * 8, &doff))) return rc;
+    HIP_TRY(launch_str_rep_lens(c.str_off, (const int32_t *)rp, u, (uint32_t *)lens, st));
+    std::vector<uint32_t> hl((size_t)u);
+    std::vector<uint64_t> ho((size_t)u + 1, 0);
+    seg_hash[i].resize((size_t)u);
+    HIP_TRY(hipMemcpyAsync(hl.data(), lens, (size_t)u * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(seg_hash[i].data(), uq, (size_t)u * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int64_t j = 0; j < u; j++) ho[(size_t)j + 1] = ho[(size_t)j] + hl[(size_t)j];
+    void *dst;
+    if ((rc = alloc(ho[(size_t)u], &dst))) return rc;
+    HIP_TRY(hipMemcpyAsync(doff, ho.data(), (size_t)u * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_str_rep_bytes(bytes, c.str_off, (const int32_t *)rp, u, (const uint64_t *)doff, (uint8_t *)dst, st));
+    std::vector<uint8_t> hb(ho[(size_t)u]);
+    int32_t collided = 0;
+    if (!hb.empty()) HIP_TRY(hipMemcpyAsync(hb.data(), dst, hb.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&collided, flag, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (collided) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw STRING column %s: 64-bit hash collision", name.c_str());
+    seg_str[i].resize((size_t)u);
+    for (int64_t j = 0; j < u; j++)
+      seg_str[i][(size_t)j].assign((const char *)hb.data() + ho[(size_t)j], hl[(size_t)j]);
+    seg_uniq[i] = (uint64_t *)uq;
+    seg_u[i] = u;
+  }
+  // equal hashes hold equal strings across segments; the distinct strings sorted bytewise are the key space
+  std::unordered_map<uint64_t, const std::string *> by_hash;
+  std::vector<const std::string *> distinct;
+  for (size_t i = 0; i < segs.size(); i++)
+    for (size_t j = 0; j < seg_str[i].size(); j++) {
+      auto ins = by_hash.emplace(seg_hash[i][j], &seg_str[i][j]);
+      if (!ins.second) {
+        if (*ins.first->second != seg_str[i][j])
+          return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw STRING column %s: 64-bit hash collision", name.c_str());
+      } else {
+        distinct.push_back(&seg_str[i][j]);
+      }
+    }
+  if ((int64_t)distinct.size() > INT32_MAX)
+    return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s: %zu distinct values", name.c_str(), distinct.size());
+  std::sort(distinct.begin(), distinct.end(), [](const std::string *a, const std::string *b) { return *a < *b; });
+  std::unordered_map<const std::string *, int32_t> rank;
+  size_t width = 1;
+  for (size_t g = 0; g < distinct.size(); g++) {
+    rank[distinct[g]] = (int32_t)g;
+    width = std::max(width, distinct[g]->size());
+  }
+  r.values.assign(distinct.size() * width, 0);
+  for (size_t g = 0; g < distinct.size(); g++) memcpy(r.values.data() + g * width, distinct[g]->data(), distinct[g]->size());
+  r.ids.assign(segs.size(), nullptr);
+  for (size_t i = 0; i < segs.size(); i++) {
+    const int64_t n = segs[i]->num_docs;
+    void *p;
+    HIP_TRY(hipMalloc(&p, std::max<size_t>((size_t)n * 4, 16)));
+    r.ids[i] = (int32_t *)p;  // owned by r from here
+    if (n <= 0) continue;
+    std::vector<int32_t> map(seg_str[i].size());
+    for (size_t j = 0; j < map.size(); j++) map[j] = rank.at(by_hash.at(seg_hash[i][j]));
+    void *dm;
+    if ((rc = alloc(map.size() * 4, &dm))) return rc;
+    HIP_TRY(hipMemcpyAsync(dm, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    const ColumnStore &c = segs[i]->cols[colidx[i]];
+    HIP_TRY(launch_raw_str_ids((const uint8_t *)c.raw, c.str_off, n, seg_uniq[i], seg_u[i], (const int32_t *)dm,
+                               (int32_t *)p, st));
+    HIP_TRY(hipStreamSynchronize(st));  // (map freed with tmp after the launch completes)
+  }
+  r.type = PHIP_TYPE_STRING;
+  r.width = (int32_t)width;
+  r.card = (int32_t)distinct.size();
+  r.dev.assign(segs.size(), nullptr);
+  return PHIP_OK;
+}
+
 // Query-global dictionary of one group-by column across the query's segments: the
 // node-global dictionary registered for the column (phip_global_dictionary, multi-GPU servers), else the
 // sorted union of the segments' dictionaries. Per segment a dict-id -> global-id map in HBM (nullptr when
@@ -1326,6 +1461,14 @@ int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::
   if (no_dict(c0) && c0.fwd_kind == PHIP_FWD_RAW_CHUNK && (type == PHIP_TYPE_FLOAT || type == PHIP_TYPE_DOUBLE)) {
     if (gd) return fail(PHIP_ERR_INVALID, "column %s is raw: it has no global dictionary", name.c_str());
     int32_t rc = raw_real_key_ids(dev, segs, colidx, name, type, *r);
+    if (rc) return rc;
+    dev.remaps[key] = r;
+    out = r;
+    return PHIP_OK;
+  }
+  if (no_dict(c0) && c0.fwd_kind == PHIP_FWD_RAW_CHUNK && type == PHIP_TYPE_STRING) {
+    if (gd) return fail(PHIP_ERR_INVALID, "column %s is raw: it has no global dictionary", name.c_str());
+    int32_t rc = raw_string_key_ids(dev, segs, colidx, name, *r);
     if (rc) return rc;
     dev.remaps[key] = r;
     out = r;
@@ -1840,11 +1983,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
                         ca.hll_log2m);
         }
         // raw numeric columns offer their values directly (DistinctCountHLLAggregationFunction.java:106-145): the
-        // kernels hash each matched doc's value (agg_common.h hll_entry_raw); raw STRING values stay on the CPU
+        // kernels hash each matched doc's value (agg_common.h hll_entry_raw), a raw STRING doc's UTF-8 bytes too
         if (ag.function == PHIP_AGG_HLL && ag.expr != PHIP_EXPR_COLUMN && ca.type == PHIP_TYPE_STRING)
           return fail(PHIP_ERR_INVALID, "numeric expression over STRING column");
-        if (ag.function == PHIP_AGG_HLL && ca.fwd_kind == PHIP_FWD_RAW_CHUNK && ca.type == PHIP_TYPE_STRING)
-          return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL over raw STRING column %s", ca.name.c_str());
         if (ag.expr != PHIP_EXPR_COLUMN) {
           const ColumnStore &cb = segs[s]->cols[colidx[s][ag.column_b]];
           if (!(cb.type == PHIP_TYPE_INT || cb.type == PHIP_TYPE_LONG)) integral = false;
@@ -1883,8 +2024,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       // DISTINCTCOUNTHLL functions of different log2m share the plan's register tables at the largest one's stride:
       // function a's registers are the first 2^log2m_a of its slot (its per-doc (register, rho) entries are computed
       // with its own log2m, DistinctCountHLLAggregationFunction.java:105-145). One column per entry table, so two
-      // log2m over one column stay on the CPU path.
-      for (int b = 0; b < a; b++)
+      // log2m over one dictionary column stay on the CPU path (a raw column's values are hashed per function).
+      bool raw_everywhere = ag.expr == PHIP_EXPR_COLUMN;
+      for (int s = 0; s < nseg && raw_everywhere; s++) {
+        const ColumnStore &cs = segs[s]->cols[colidx[s][ag.column_a]];
+        raw_everywhere = cs.fwd_kind == PHIP_FWD_RAW_CHUNK;
+      }
+      for (int b = 0; b < a && !raw_everywhere; b++)
         if (dq.aggs[b].acc == ACC_HLL && dq.aggs[b].expr == PHIP_EXPR_COLUMN && ag.expr == PHIP_EXPR_COLUMN &&
             dq.aggs[b].col_a == ag.column_a && dq.aggs[b].log2m != ag.log2m)
           return fail(PHIP_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL of column %d with two log2m (%d, %d)", ag.column_a,

@@ -88,6 +88,19 @@ hipError_t launch_materialize_packed(const uint32_t *, int32_t, const void *, in
   return hipSuccess;
 }
 hipError_t launch_raw_images(const void *, int32_t, int64_t, uint64_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_str_hash_unique(void *temp, size_t *temp_bytes, const uint8_t *, const uint64_t *, int64_t, uint64_t *,
+                                  int32_t *, uint64_t *, int32_t *, uint64_t *, int32_t *, int64_t *num_out, hipStream_t) {
+  if (!temp) *temp_bytes = 64;
+  else *num_out = 0;
+  return hipSuccess;
+}
+hipError_t launch_str_verify(const uint8_t *, const uint64_t *, int64_t, const uint64_t *, const int32_t *, int64_t, int32_t *,
+                             hipStream_t) { return hipSuccess; }
+hipError_t launch_str_rep_lens(const uint64_t *, const int32_t *, int64_t, uint32_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_str_rep_bytes(const uint8_t *, const uint64_t *, const int32_t *, int64_t, const uint64_t *, uint8_t *,
+                                hipStream_t) { return hipSuccess; }
+hipError_t launch_raw_str_ids(const uint8_t *, const uint64_t *, int64_t, const uint64_t *, int64_t, const int32_t *, int32_t *,
+                              hipStream_t) { return hipSuccess; }
 hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *, uint64_t *, uint64_t *, int64_t *num_out,
                                   int64_t, hipStream_t) {
   if (!temp) *temp_bytes = 64;

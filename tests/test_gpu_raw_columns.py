@@ -4,9 +4,12 @@
              (DefaultGroupByExecutor.java:106-116): a raw INT / LONG column keys by its values; on the GPU the key
              dimension is value - min over the query's segments (value order = key order), mixed with dictionary
              columns' global ids, and a result's dictionary holds only the values its groups use. A raw FLOAT / DOUBLE
-             column keys through the sorted distinct values over the segments (keys.hip, a doc-order id column).
+             column keys through the sorted distinct values over the segments (keys.hip, a doc-order id column); a raw
+             STRING column through its distinct strings sorted bytewise (64-bit hashes sorted and verified on the device,
+             the representatives' bytes merged on the host).
   HLL        DistinctCountHLLAggregationFunction over raw INT / LONG / FLOAT / DOUBLE values (:106-145): every matched
-             doc's value hashed on the device (clearspring MurmurHash.hashLong, the dictionary path's mapping).
+             doc's value hashed on the device (clearspring MurmurHash.hashLong, the dictionary path's mapping); raw
+             STRING values by MurmurHash.hash of their UTF-8 bytes (seed -1, HyperLogLog.offer of a String).
 
 Every block equals the oracle's (values read from the raw chunks: an independent route)."""
 import numpy as np
@@ -30,7 +33,7 @@ def raw_segments(gpu_lib):
     rng = np.random.default_rng(31)
     raws = []
     for s, n in enumerate((20_000, 33_333, 4097)):
-        c = SegmentCreator(f"raw{s}", no_dictionary_columns=["ri", "rl", "rf", "rd", "rm"])
+        c = SegmentCreator(f"raw{s}", no_dictionary_columns=["ri", "rl", "rf", "rd", "rm", "rs"])
         c.add_column("ri", DataType.INT, rng.integers(-50 + 7 * s, 60 + 3 * s, n).astype(np.int32))
         c.add_column("rl", DataType.LONG, rng.integers(-3_000_000_000, -2_999_990_000, n) + 1_000_000 * s)
         # (+ 0.0: no -0.0 -- the reference keys it apart from 0.0 by its bits, Double2IntOpenHashMap, and so does the
@@ -40,6 +43,10 @@ def raw_segments(gpu_lib):
         c.add_column("rm", DataType.LONG, rng.integers(-10 ** 9, 10 ** 9, n))
         c.add_column("dk", DataType.STRING, np.array([f"k{x}" for x in rng.integers(0, 9 + s, n)]))
         c.add_column("f", DataType.INT, rng.integers(0, 100, n))
+        # raw STRING: lengths 0-14 (every murmur tail), multi-byte UTF-8, values shared across segments or not
+        words = ["", "a", "ab", "abc", "abcd", "zé", "ÿÿÿ", "日本語", "naïve-x", "k" * 13, "Z", "mid", "abcde"] + \
+            [f"s{s}-{j}" for j in range(5 + 40 * s)]
+        c.add_column("rs", DataType.STRING, np.array(words, dtype=object)[rng.integers(0, len(words), n)])
         raws.append(c.build())
     segs = _segs(raws)
     yield raws, segs
@@ -58,6 +65,11 @@ RAW_GROUP_BY = [
     "SELECT rd, dk, COUNT(*), MIN(ri), DISTINCTCOUNTHLL(rf) FROM t WHERE f < 50 GROUP BY rd, dk LIMIT 100000",
     "SELECT rf, rd, COUNT(*) FROM t WHERE f < 20 GROUP BY rf, rd ORDER BY rf DESC, rd LIMIT 9",  # key-order trim
     "SELECT rf, SUM(rd), MAX(rf) FROM t WHERE rf > 1.5 GROUP BY rf LIMIT 100000",  # key column also filtered / aggregated
+    # raw STRING keys (distinct strings over the segments sorted bytewise, a doc-order id column each)
+    "SELECT rs, COUNT(*), SUM(rm) FROM t GROUP BY rs LIMIT 100000",
+    "SELECT rs, dk, ri, COUNT(*), DISTINCTCOUNTHLL(rs) FROM t WHERE f < 50 GROUP BY rs, dk, ri LIMIT 100000",
+    "SELECT rs, SUM(ri) FROM t WHERE f < 70 GROUP BY rs ORDER BY rs DESC LIMIT 6",  # key-order trim
+    "SELECT rs, COUNT(*) FROM t WHERE rs >= 'abc' AND rs < 'zz' GROUP BY rs LIMIT 100000",  # raw STRING leaf too
 ]
 
 
@@ -102,6 +114,9 @@ RAW_HLL = [
     # over expressions: the transform's DOUBLE values offered as java.lang.Double (hashLong of the bits)
     "SELECT DISTINCTCOUNTHLL(ri * f), DISTINCTCOUNTHLL(rd - rf), COUNT(*) FROM t WHERE f < 60",
     "SELECT dk, DISTINCTCOUNTHLL(ri + f), SUM(rm) FROM t GROUP BY dk LIMIT 100000",
+    # raw STRING values: MurmurHash.hash(bytes) on the device
+    "SELECT DISTINCTCOUNTHLL(rs), DISTINCTCOUNTHLL(rs, 10), COUNT(*) FROM t WHERE f < 70",
+    "SELECT dk, DISTINCTCOUNTHLL(rs, 6), SUM(ri) FROM t GROUP BY dk LIMIT 100000",
 ]
 
 
