@@ -112,6 +112,29 @@ struct DevCol {
 };
 constexpr int kBitSliceMaxBits = 12;
 
+// One group-by column's key id source for the tuple packing of key spaces above 2^62 (keys.hip tuple_words_kernel).
+constexpr int kMaxTupleCols = 8;
+constexpr int kMaxTupleWords = 4;
+struct TupleCol {
+  const uint32_t *words;  // dictionary ids (null: raw INT / LONG values in `raw`, or `ids`)
+  const int32_t *remap;   // segment dict id -> query-global id, null = identity
+  const int32_t *ids;     // doc-order global ids (raw FLOAT / DOUBLE / STRING keys), or null
+  const void *raw;
+  const uint64_t *nulls;  // null docs (their id = null_id), or null
+  int64_t base;           // raw INT / LONG: id = value - base
+  int64_t null_id;
+  uint64_t stride;        // the column's place in its word's mixed radix
+  int32_t bits;
+  int32_t type;
+  int32_t word;
+  int32_t pad;
+};
+struct TupleCols {
+  TupleCol cols[kMaxTupleCols];
+  int32_t k;  // columns
+  int32_t w;  // words
+};
+
 // One source the filter wave copies into its LDS stage slot for every tile (LDS-DMA, 1 KiB per
 // wave-instruction): a fixed-bit filter column (256*b bytes per 2048-doc tile) or the dense doc words of
 // an inverted leaf (256 bytes per tile).

@@ -111,6 +111,67 @@ __global__ void raw_str_ids_kernel(const uint8_t *__restrict__ bytes, const uint
     ids[i] = map[lower_bound_u64(uniq, u, str_hash64(bytes + off[i], (int64_t)(off[i + 1] - off[i])))];
 }
 
+// Group-by key spaces above 2^62 (the reference's LongMapBasedHolder / ArrayMapBasedHolder role,
+// DictionaryBasedGroupKeyGenerator.java:150-185): each doc's tuple of query-global key ids is packed into W <= 4 u64
+// words (mixed radix per word, the columns split so no word's radix product leaves u64), the segment's tuples are
+// ranked (LSD: a stable radix sort of the permutation per word, last word first), and the distinct tuples of all
+// segments ranked the same way become one virtual key column of doc-order ids (DevCol.gb_ids).
+__global__ void tuple_words_kernel(TupleCols tc, int64_t n, uint64_t *__restrict__ out) {
+  for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t w[kMaxTupleWords] = {0, 0, 0, 0};
+    for (int k = 0; k < tc.k; k++) {
+      const TupleCol &c = tc.cols[k];
+      int64_t gid;
+      if (c.ids != nullptr) {
+        gid = c.ids[d];
+      } else if (c.words == nullptr) {  // raw INT / LONG: value - base
+        gid = (c.type == PHIP_TYPE_LONG ? ((const int64_t *)c.raw)[d] : (int64_t)((const int32_t *)c.raw)[d]) - c.base;
+      } else {
+        const uint32_t id = decode_bits(c.words, (uint64_t)d * (uint32_t)c.bits, (uint32_t)c.bits);
+        gid = c.remap ? c.remap[id] : (int64_t)id;
+      }
+      if (c.nulls != nullptr && ((c.nulls[d >> 6] >> (d & 63)) & 1ull)) gid = c.null_id;
+#pragma unroll
+      for (int j = 0; j < kMaxTupleWords; j++)
+        if (j == c.word) w[j] += (uint64_t)gid * c.stride;
+    }
+    for (int j = 0; j < tc.w; j++) out[j * n + d] = w[j];
+  }
+}
+
+__global__ void iota_kernel(int32_t *__restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = (int32_t)i;
+}
+__global__ void gather_word_kernel(const uint64_t *__restrict__ w, const int32_t *__restrict__ perm, int64_t n,
+                                   uint64_t *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = w[perm[i]];
+}
+__global__ void tuple_heads_kernel(const uint64_t *__restrict__ words, int32_t nw, const int32_t *__restrict__ perm,
+                                   int64_t n, int32_t *__restrict__ head) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int32_t h = i == 0;
+    for (int j = 0; j < nw && !h; j++) h = words[j * n + perm[i]] != words[j * n + perm[i - 1]];
+    head[i] = h;
+  }
+}
+__global__ void tuple_scatter_kernel(const uint64_t *__restrict__ words, int32_t nw, const int32_t *__restrict__ perm,
+                                     const int32_t *__restrict__ head, const int32_t *__restrict__ rank1, int64_t n,
+                                     int32_t *__restrict__ ids, uint64_t *__restrict__ uniq, int64_t ucap) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = rank1[i] - 1;
+    ids[perm[i]] = r;
+    if (head[i])
+      for (int j = 0; j < nw; j++) uniq[j * ucap + r] = words[j * n + perm[i]];
+  }
+}
+__global__ void gather_ids_kernel(const int32_t *__restrict__ local, const int32_t *__restrict__ map, int64_t n,
+                                  int32_t *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = map[local[i]];
+}
+
 static inline int keys_grid(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -196,6 +257,63 @@ hipError_t launch_raw_str_ids(const uint8_t *bytes, const uint64_t *off, int64_t
                               const int32_t *map, int32_t *ids, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   raw_str_ids_kernel<<<keys_grid(n), 256, 0, s>>>(bytes, off, n, uniq, u, map, ids);
+  return hipGetLastError();
+}
+
+hipError_t launch_tuple_words(const TupleCols &tc, int64_t n, uint64_t *out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  tuple_words_kernel<<<keys_grid(n), 256, 0, s>>>(tc, n, out);
+  return hipGetLastError();
+}
+
+// Rank the n tuples of words (nw x n, word-major): ids[i] = rank of tuple i among the distinct tuples (ordered by word
+// 0, then 1, ...), uniq (nw x ucap) = the distinct tuples, *num_out = their count. temp == nullptr: scratch bytes.
+hipError_t launch_tuple_rank(void *temp, size_t *temp_bytes, const uint64_t *words, int32_t nw, int64_t n, int32_t *ids,
+                             uint64_t *uniq, int64_t ucap, int64_t *num_out, hipStream_t s) {
+  // scratch: key, key_sorted (8n each), perm, perm_sorted, head, rank1 (4n each), then the library's temp
+  const size_t fixed = (size_t)n * 32 + 256;
+  size_t a = 0, b = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                                    (const int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0, 64, s);
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceScan::InclusiveSum(nullptr, b, (const int32_t *)nullptr, (int32_t *)nullptr, (int)n, s);
+  if (e != hipSuccess) return e;
+  if (temp == nullptr) {
+    *temp_bytes = fixed + (a > b ? a : b);
+    return hipSuccess;
+  }
+  *num_out = 0;
+  if (n <= 0) return hipSuccess;
+  uint8_t *t = (uint8_t *)temp;
+  uint64_t *key = (uint64_t *)t, *key2 = key + n;
+  int32_t *perm = (int32_t *)(key2 + n), *perm2 = perm + n, *head = perm2 + n, *rank1 = head + n;
+  void *lib = (void *)(((uintptr_t)(rank1 + n) + 255) & ~(uintptr_t)255);
+  const int g = keys_grid(n);
+  iota_kernel<<<g, 256, 0, s>>>(perm, n);
+  for (int j = nw - 1; j >= 0; j--) {
+    gather_word_kernel<<<g, 256, 0, s>>>(words + (int64_t)j * n, perm, n, key);
+    e = hipcub::DeviceRadixSort::SortPairs(lib, a, (const uint64_t *)key, key2, (const int32_t *)perm, perm2, (int)n, 0, 64, s);
+    if (e != hipSuccess) return e;
+    int32_t *x = perm;
+    perm = perm2;
+    perm2 = x;
+  }
+  tuple_heads_kernel<<<g, 256, 0, s>>>(words, nw, perm, n, head);
+  e = hipcub::DeviceScan::InclusiveSum(lib, b, (const int32_t *)head, rank1, (int)n, s);
+  if (e != hipSuccess) return e;
+  tuple_scatter_kernel<<<g, 256, 0, s>>>(words, nw, perm, head, rank1, n, ids, uniq, ucap);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  int32_t u = 0;
+  e = hipMemcpyAsync(&u, rank1 + n - 1, 4, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  *num_out = u;
+  return e;
+}
+
+hipError_t launch_gather_ids(const int32_t *local, const int32_t *map, int64_t n, int32_t *out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  gather_ids_kernel<<<keys_grid(n), 256, 0, s>>>(local, map, n, out);
   return hipGetLastError();
 }
 

@@ -112,6 +112,10 @@ hipError_t launch_str_rep_bytes(const uint8_t *bytes, const uint64_t *off, const
                                 const uint64_t *dst_off, uint8_t *dst, hipStream_t s);
 hipError_t launch_raw_str_ids(const uint8_t *bytes, const uint64_t *off, int64_t n, const uint64_t *uniq, int64_t u,
                               const int32_t *map, int32_t *ids, hipStream_t s);
+hipError_t launch_tuple_words(const TupleCols &tc, int64_t n, uint64_t *out, hipStream_t s);
+hipError_t launch_tuple_rank(void *temp, size_t *temp_bytes, const uint64_t *words, int32_t nw, int64_t n, int32_t *ids,
+                             uint64_t *uniq, int64_t ucap, int64_t *num_out, hipStream_t s);
+hipError_t launch_gather_ids(const int32_t *local, const int32_t *map, int64_t n, int32_t *out, hipStream_t s);
 hipError_t launch_raw_key_ids(const void *raw, int32_t type, int64_t n, const uint64_t *uniq, int64_t u, int32_t *ids,
                               hipStream_t s);
 hipError_t launch_materialize_hll16(const uint32_t *words, int32_t bits, const uint32_t *table, int64_t n, uint16_t *out,
@@ -347,6 +351,8 @@ struct Device {
     int64_t raw_base = 0;
     std::vector<uint8_t> values;  // LE typed or fixed-width strings
     std::vector<int32_t *> ids;   // raw FLOAT / DOUBLE / STRING column: per segment its docs' ids into `values` (keys.hip)
+    std::vector<uint64_t> tuples; // tuple keys (key spaces above 2^62): tuple_w x card packed words, word-major
+    int32_t tuple_w = 0;
     ~Remap() {
       for (auto *p : dev)
         if (p) (void)hipFree(p);
@@ -1401,6 +1407,145 @@ static int32_t raw_string_key_ids(Device &dev, const std::vector<Segment *> &seg
   return PHIP_OK;
 }
 
+// Tuple keys for a group-by whose mixed-radix key space exceeds 2^62: the columns' query-global ids (nulls as the
+// column's null id) packed into <= 4 u64 words per doc, ranked per segment and then across segments (keys.hip), as
+// one virtual column: card = the distinct tuples, doc-order ids per segment, the tuples' words kept for decoding.
+static int32_t build_tuple_keys(Device &dev, const std::vector<Segment *> &segs,
+                                const std::vector<std::vector<int>> &colidx, const int32_t *gb_cols, int K,
+                                const std::vector<std::shared_ptr<Device::Remap>> &dicts,
+                                const std::vector<int64_t> &radix, std::vector<int32_t> &word,
+                                std::vector<uint64_t> &stride, std::shared_ptr<Device::Remap> &out) {
+  // columns into words: mixed radix per word while the product fits u64
+  word.assign(K, 0);
+  stride.assign(K, 1);
+  int W = 1;
+  long double prod = 1;
+  for (int k = 0; k < K; k++) {
+    if (prod * (long double)radix[k] > 18446744073709551615.0L) {
+      W++;
+      prod = 1;
+    }
+    word[k] = W - 1;
+    stride[k] = (uint64_t)prod;
+    prod *= (long double)radix[k];
+  }
+  if (W > kMaxTupleWords || K > kMaxTupleCols)
+    return fail(PHIP_ERR_UNSUPPORTED, "group-by tuple keys: %d words over %d columns", W, K);
+  std::string key = "tuple";
+  for (int k = 0; k < K; k++) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "|%d@%p#%lld", gb_cols[k], (const void *)dicts[k].get(), (long long)radix[k]);
+    key += buf;
+  }
+  for (auto *sg : segs) key += ":" + std::to_string(sg->handle);
+  auto it = dev.remaps.find(key);
+  if (it != dev.remaps.end()) {
+    out = it->second;
+    return PHIP_OK;
+  }
+  hipStream_t st = dev.stream;
+  std::vector<void *> tmp;
+  struct Free {
+    std::vector<void *> &v;
+    ~Free() {
+      for (void *p : v) (void)hipFree(p);
+    }
+  } free_tmp{tmp};
+  auto alloc = [&](size_t bytes, void **p) -> int32_t {
+    HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    tmp.push_back(*p);
+    return PHIP_OK;
+  };
+  auto r = std::make_shared<Device::Remap>();
+  const size_t S = segs.size();
+  std::vector<int32_t *> local(S, nullptr);
+  std::vector<uint64_t *> seg_uniq(S, nullptr);
+  std::vector<int64_t> seg_u(S, 0);
+  int64_t total = 0;
+  int32_t rc;
+  for (size_t i = 0; i < S; i++) {
+    const int64_t n = segs[i]->num_docs;
+    if (n <= 0) continue;
+    if (n > INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "group-by tuple keys: segment over 2^31 docs");
+    TupleCols tc{};
+    tc.k = K;
+    tc.w = W;
+    for (int k = 0; k < K; k++) {
+      const ColumnStore &c = segs[i]->cols[colidx[i][gb_cols[k]]];
+      const Device::Remap &d = *dicts[k];
+      TupleCol &t = tc.cols[k];
+      t.word = word[k];
+      t.stride = stride[k];
+      t.null_id = d.card;
+      t.nulls = radix[k] > d.card ? c.nulls : nullptr;
+      if (!d.ids.empty()) {
+        t.ids = d.ids[i];
+      } else if (d.raw) {
+        t.raw = c.raw;
+        t.type = c.type;
+        t.base = d.raw_base;
+      } else {
+        t.words = c.words;
+        t.bits = c.bits;
+        t.remap = d.dev[i];
+      }
+    }
+    void *w, *ids, *uq, *scratch;
+    size_t sb = 0;
+    if ((rc = alloc((size_t)n * 8 * W, &w)) || (rc = alloc((size_t)n * 4, &ids)) || (rc = alloc((size_t)n * 8 * W, &uq)))
+      return rc;
+    HIP_TRY(launch_tuple_words(tc, n, (uint64_t *)w, st));
+    HIP_TRY(launch_tuple_rank(nullptr, &sb, nullptr, W, n, nullptr, nullptr, 0, nullptr, st));
+    if ((rc = alloc(sb, &scratch))) return rc;
+    int64_t u = 0;
+    HIP_TRY(launch_tuple_rank(scratch, &sb, (const uint64_t *)w, W, n, (int32_t *)ids, (uint64_t *)uq, n, &u, st));
+    local[i] = (int32_t *)ids;
+    seg_uniq[i] = (uint64_t *)uq;
+    seg_u[i] = u;
+    total += u;
+  }
+  // the segments' distinct tuples, ranked together
+  void *all, *gids, *guniq, *scratch;
+  size_t sb = 0;
+  if ((rc = alloc((size_t)std::max<int64_t>(total, 1) * 8 * W, &all)) || (rc = alloc((size_t)total * 4, &gids)) ||
+      (rc = alloc((size_t)std::max<int64_t>(total, 1) * 8 * W, &guniq)))
+    return rc;
+  int64_t off = 0;
+  for (size_t i = 0; i < S; i++) {
+    for (int j = 0; j < W && seg_u[i]; j++)
+      HIP_TRY(hipMemcpyAsync((uint64_t *)all + (int64_t)j * total + off, seg_uniq[i] + (int64_t)j * segs[i]->num_docs,
+                             (size_t)seg_u[i] * 8, hipMemcpyDeviceToDevice, st));
+    off += seg_u[i];
+  }
+  HIP_TRY(launch_tuple_rank(nullptr, &sb, nullptr, W, total, nullptr, nullptr, 0, nullptr, st));
+  if ((rc = alloc(sb, &scratch))) return rc;
+  int64_t U = 0;
+  HIP_TRY(launch_tuple_rank(scratch, &sb, (const uint64_t *)all, W, total, (int32_t *)gids, (uint64_t *)guniq, total, &U, st));
+  if (U > INT32_MAX) return fail(PHIP_ERR_UNSUPPORTED, "group-by tuple keys: %lld distinct tuples", (long long)U);
+  r->ids.assign(S, nullptr);
+  off = 0;
+  for (size_t i = 0; i < S; i++) {
+    const int64_t n = segs[i]->num_docs;
+    void *p;
+    HIP_TRY(hipMalloc(&p, std::max<size_t>((size_t)std::max<int64_t>(n, 0) * 4, 16)));
+    r->ids[i] = (int32_t *)p;  // owned by r from here
+    if (n > 0) HIP_TRY(launch_gather_ids(local[i], (const int32_t *)gids + off, n, (int32_t *)p, st));
+    off += seg_u[i];
+  }
+  r->tuples.resize((size_t)U * W);
+  for (int j = 0; j < W && U; j++)
+    HIP_TRY(hipMemcpyAsync(r->tuples.data() + (size_t)j * U, (const uint64_t *)guniq + (int64_t)j * total, (size_t)U * 8,
+                           hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  r->tuple_w = W;
+  r->type = PHIP_TYPE_INT;
+  r->card = (int32_t)U;
+  r->dev.assign(S, nullptr);
+  dev.remaps[key] = r;
+  out = r;
+  return PHIP_OK;
+}
+
 // Query-global dictionary of one group-by column across the query's segments: the
 // node-global dictionary registered for the column (phip_global_dictionary, multi-GPU servers), else the
 // sorted union of the segments' dictionaries. Per segment a dict-id -> global-id map in HBM (nullptr when
@@ -1724,6 +1869,16 @@ struct Plan {
   std::vector<RoaringTask> tasks;
   std::vector<std::shared_ptr<Device::Remap>> gb_dicts;
   std::vector<int64_t> gb_radix;  // per group-by column: key ids (its dictionary's, + 1 for the null key)
+  // tuple keys (key space above 2^62): the device groups by one virtual column (tuple_remap's doc-order ids); the
+  // result's keys expand back to the query's columns (tuple_dicts / tuple_radix, packed per tuple_word / tuple_stride)
+  bool tuple_keys = false;
+  std::shared_ptr<Device::Remap> tuple_remap;
+  std::vector<std::shared_ptr<Device::Remap>> tuple_dicts;
+  std::vector<int64_t> tuple_radix;
+  std::vector<int32_t> tuple_word;
+  std::vector<uint64_t> tuple_stride;
+  int32_t tuple_gb_col[1] = {0};
+  std::vector<int32_t> tuple_cols;  // the query's group-by columns
   int nseg = 0, naggs = 0, nhll = 0, log2m = 0, m_regs = 0, num_group_by = 0, num_projected = 0;
   int nprog = 1;   // filter programs (phip_query_desc.num_filter_programs)
   int nmatch = 0;  // seg_matched slots = nprog * nseg
@@ -1938,6 +2093,54 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         return fail(PHIP_ERR_NOT_FOUND, "segment %s has no column %s", segs[s]->name.c_str(), q->columns[c]);
       colidx[s][c] = it->second;
     }
+
+  // A group-by whose mixed-radix key space exceeds 2^62 groups by tuple keys (build_tuple_keys): the plan is made for
+  // one virtual key column (the first group-by column's slot carries its ids) and execute_plan expands the keys.
+  // Device trims that order by a group key need the columns' order, so such a plan returns every group instead.
+  phip_query_desc qv;
+  if (q->num_group_by > 1 && q->group_by_columns) {
+    std::vector<std::shared_ptr<Device::Remap>> dicts;
+    std::vector<int64_t> radix;
+    long double space = 1;
+    for (int k = 0; k < q->num_group_by; k++) {
+      const int c = q->group_by_columns[k];
+      if (c < 0 || c >= ncols) return fail(PHIP_ERR_INVALID, "group_by_columns[%d] = %d out of range", k, c);
+      std::vector<int> ci(nseg);
+      for (int s = 0; s < nseg; s++) ci[s] = colidx[s][c];
+      bool null_key = false;
+      if ((q->null_group_by >> k) & 1)
+        for (int s = 0; s < nseg; s++) null_key |= segs[s]->cols[ci[s]].nulls != nullptr;
+      std::shared_ptr<Device::Remap> r;
+      int32_t rc = build_remap(*dev, segs, ci, q->columns[c], r, null_key);
+      if (rc) return rc;
+      dicts.push_back(r);
+      radix.push_back((int64_t)r->card + (null_key ? 1 : 0));
+      space *= (long double)radix.back();
+    }
+    const char *tk = getenv("PHIP_TUPLE_KEYS");  // test override: "1" = tuple keys for any multi-column group-by
+    if (space > (long double)((int64_t)1 << 62) || (tk && atoi(tk) != 0)) {
+      int32_t rc = build_tuple_keys(*dev, segs, colidx, q->group_by_columns, q->num_group_by, dicts, radix,
+                                    P.tuple_word, P.tuple_stride, P.tuple_remap);
+      if (rc) return rc;
+      P.tuple_keys = true;
+      P.tuple_dicts = dicts;
+      P.tuple_radix = radix;
+      P.tuple_gb_col[0] = q->group_by_columns[0];
+      P.tuple_cols.assign(q->group_by_columns, q->group_by_columns + q->num_group_by);
+      qv = *q;
+      qv.num_group_by = 1;
+      qv.group_by_columns = P.tuple_gb_col;
+      qv.null_group_by = 0;
+      bool key_terms = qv.num_order_by_keys > 0;
+      for (int j = 0; j < qv.num_order_terms && qv.order_terms; j++) key_terms |= qv.order_terms[j].kind == PHIP_ORDER_GROUP_KEY;
+      if (key_terms) {
+        qv.trim_size = 0;
+        qv.num_order_by_keys = 0;
+        qv.num_order_terms = 0;
+      }
+      q = &qv;
+    }
+  }
 
   // aggregations
   DevAggQuery dq;
@@ -2240,7 +2443,12 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   sq.num_select = nsel;
   sq.limit = std::max<int64_t>(0, q->select_limit);
   int num_projected = 0;
-  for (bool p : projected) num_projected += p ? 1 : 0;
+  {
+    std::vector<bool> counted = projected;  // (tuple keys: the query's own group-by columns are the projected ones)
+    if (P.tuple_keys)
+      for (int k = 0; k < (int)P.tuple_dicts.size(); k++) counted[P.tuple_cols[k]] = true;
+    for (bool p : counted) num_projected += p ? 1 : 0;
+  }
 
   // group-by key space
   const bool group_by = q->num_group_by > 0;
@@ -2262,8 +2470,12 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       if ((q->null_group_by >> k) & 1)
         for (int s = 0; s < nseg; s++) null_key |= segs[s]->cols[ci[s]].nulls != nullptr;
       std::shared_ptr<Device::Remap> r;
-      int32_t rc = build_remap(*dev, segs, ci, q->columns[c], r, null_key);
-      if (rc) return rc;
+      if (P.tuple_keys) {
+        r = P.tuple_remap;
+      } else {
+        int32_t rc = build_remap(*dev, segs, ci, q->columns[c], r, null_key);
+        if (rc) return rc;
+      }
       gb_dicts.push_back(r);
       const int64_t radix = (int64_t)r->card + (null_key ? 1 : 0);
       P.gb_radix.push_back(radix);
@@ -4157,7 +4369,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       part->row_kinds[0] = PHIP_ROW_COUNT;
       for (int a = 0; a < naggs; a++) part->row_kinds[1 + a] = dq.aggs[a].acc;  // ACC_* == PHIP_ROW_*
       local_stats(part->stats);
-      part->global_keys = 1;
+      part->global_keys = 1;  // (tuple keys: this device's own virtual ids, so the record merge)
       for (const auto &d : gb_dicts) part->global_keys &= d->global ? 1 : 0;
       P.partial_pending = true;
       P.clean = true;
@@ -4291,24 +4503,39 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         key /= P.gb_radix[k];
       }
     }
-    impl->dicts = gb_dicts;  // (num_groups_limit_reached was set by group_limit, before any trim)
-    for (int k = 0; k < P.num_group_by; k++) {
-      if (!gb_dicts[k]->raw) continue;
+    // tuple keys: each group's virtual id back to the query's columns' ids
+    const int KO = P.tuple_keys ? (int)P.tuple_dicts.size() : P.num_group_by;
+    const auto &DO = P.tuple_keys ? P.tuple_dicts : gb_dicts;
+    const auto &RO = P.tuple_keys ? P.tuple_radix : P.gb_radix;
+    if (P.tuple_keys) {
+      const Device::Remap &tr = *P.tuple_remap;
+      const int64_t U = tr.card;
+      std::vector<int32_t> ek((size_t)ngroups * KO);
+      for (int64_t g = 0; g < ngroups; g++) {
+        const int64_t v = impl->keys[g];
+        for (int k = 0; k < KO; k++)
+          ek[g * KO + k] = (int32_t)((tr.tuples[(size_t)P.tuple_word[k] * U + v] / P.tuple_stride[k]) % (uint64_t)RO[k]);
+      }
+      impl->keys.swap(ek);
+    }
+    impl->dicts = DO;  // (num_groups_limit_reached was set by group_limit, before any trim)
+    for (int k = 0; k < KO; k++) {
+      if (!DO[k]->raw) continue;
       // a raw column's result dictionary: the values its groups use, ascending; group keys re-pointed at it
       std::vector<int32_t> used;
       used.reserve(ngroups);
-      const int32_t null_id = P.gb_radix[k] > gb_dicts[k]->card ? gb_dicts[k]->card : -1;
+      const int32_t null_id = RO[k] > DO[k]->card ? DO[k]->card : -1;
       for (int64_t g = 0; g < ngroups; g++)
-        if (impl->keys[g * P.num_group_by + k] != null_id) used.push_back(impl->keys[g * P.num_group_by + k]);
+        if (impl->keys[g * KO + k] != null_id) used.push_back(impl->keys[g * KO + k]);
       std::sort(used.begin(), used.end());
       used.erase(std::unique(used.begin(), used.end()), used.end());
       auto rd = std::make_shared<Device::Remap>();
-      rd->type = gb_dicts[k]->type;
+      rd->type = DO[k]->type;
       rd->card = (int32_t)used.size();
       const int w = type_width(rd->type);
       rd->values.resize(used.size() * w);
       for (size_t i = 0; i < used.size(); i++) {
-        const int64_t v = gb_dicts[k]->raw_base + used[i];
+        const int64_t v = DO[k]->raw_base + used[i];
         if (w == 4) {
           const int32_t v4 = (int32_t)v;
           memcpy(rd->values.data() + 4 * i, &v4, 4);
@@ -4317,7 +4544,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
         }
       }
       for (int64_t g = 0; g < ngroups; g++) {  // (the null key stays one past the values: rd->card)
-        int32_t &id = impl->keys[g * P.num_group_by + k];
+        int32_t &id = impl->keys[g * KO + k];
         id = id == null_id ? rd->card : (int32_t)(std::lower_bound(used.begin(), used.end(), id) - used.begin());
       }
       impl->dicts[k] = rd;
@@ -4429,7 +4656,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   r.program_docs_matched = impl->prog_docs.data();
   r.num_aggregations = naggs;
   r.num_groups = group_by ? ngroups : 1;
-  r.num_group_by = P.num_group_by;
+  r.num_group_by = P.tuple_keys ? (int32_t)P.tuple_dicts.size() : P.num_group_by;
   r.num_hll = nhll;
   r.values = impl->values.data();
   r.long_values = impl->longs.data();

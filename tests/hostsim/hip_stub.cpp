@@ -107,6 +107,14 @@ hipError_t launch_sort_unique_u64(void *temp, size_t *temp_bytes, uint64_t *, ui
   else *num_out = 0;
   return hipSuccess;
 }
+hipError_t launch_tuple_words(const TupleCols &, int64_t, uint64_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_tuple_rank(void *temp, size_t *temp_bytes, const uint64_t *, int32_t, int64_t, int32_t *, uint64_t *, int64_t,
+                             int64_t *num_out, hipStream_t) {
+  if (!temp) *temp_bytes = 64;
+  else *num_out = 0;
+  return hipSuccess;
+}
+hipError_t launch_gather_ids(const int32_t *, const int32_t *, int64_t, int32_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_raw_key_ids(const void *, int32_t, int64_t, const uint64_t *, int64_t, int32_t *, hipStream_t) {
   return hipSuccess;
 }

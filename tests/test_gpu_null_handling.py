@@ -194,13 +194,13 @@ def test_gpu_null_handling_group_by(sql, null_segments):
     _check_nullable_groups(qc, blk, oblk, ex)
 
 
-@pytest.mark.parametrize("mode", ["hash", "fused_xcd", "fused_hbm"])
+@pytest.mark.parametrize("mode", ["hash", "fused_xcd", "fused_hbm", "tuple"])
 @pytest.mark.parametrize("sql", [GB[1], GB[3], GB[4]])
 def test_gpu_null_handling_group_by_table_modes(sql, mode, null_segments, monkeypatch):
-    """The same null keys / null results through the hash table, and fused into the filter (XCD copies, one HBM
-    table) where the program is conjunctive."""
+    """The same null keys / null results through the hash table, fused into the filter (XCD copies, one HBM
+    table) where the program is conjunctive, and as tuple keys (a null key's id inside the packed tuple)."""
     monkeypatch.setenv(*{"hash": ("PHIP_GB_HASH", "1"), "fused_xcd": ("PHIP_FUSED_GB", "3"),
-                         "fused_hbm": ("PHIP_FUSED_GB", "2")}[mode])
+                         "fused_hbm": ("PHIP_FUSED_GB", "2"), "tuple": ("PHIP_TUPLE_KEYS", "1")}[mode])
     qc, blk, oblk, ex = _run(NH + sql, null_segments)
     _check_nullable_groups(qc, blk, oblk, ex)
 
