@@ -740,12 +740,9 @@ def execute(query, segments, num_groups_limit=DEFAULT_NUM_GROUPS_LIMIT, min_segm
                 cols.update(columns_of(ag.argument))
         for e in query.group_by:
             cols.update(columns_of(e))
-        if any(ag.filter is not None for ag in query.aggregations) and any(
-                os_.has_nulls(c) for os_, _ in per_seg for c in cols):
-            raise NotImplementedError("FILTER + GROUP BY under null handling over columns with nulls (not restated)")
     if any(ag.filter is not None for ag in query.aggregations):
         if query.group_by:
-            return _execute_filtered_group_by(query, segments, num_groups_limit)
+            return _execute_filtered_group_by(query, segments, num_groups_limit, nh)
         return _execute_filtered(query, segments, nh)
     if not query.group_by:
         results, exact = None, None
@@ -904,12 +901,17 @@ def _filter_infos(query):
     return out
 
 
-def _execute_filtered_group_by(query, segments, num_groups_limit):
+def _execute_filtered_group_by(query, segments, num_groups_limit, null_handling=False):
     """FilteredGroupByOperator.getNextBlock (pinot-core/.../operator/query/FilteredGroupByOperator.java:110-176):
     the infos share ONE group key generator, so a group's id is first-seen over info 0's docs, then info 1's, ...
     (numGroupsLimit counts the union); holders of functions whose filter never reached a group keep their
     defaults (ensureCapacity); numDocsScanned / post-filter entries are summed over the infos, each info
-    projecting the group-by columns plus its functions' arguments."""
+    projecting the group-by columns plus its functions' arguments.
+
+    null_handling: the filters are three-valued (a doc passes where they are TRUE), a group-by column's null docs key
+    as None (as _group_segment), and a nullable function skips null inputs; under null handling its holder is an
+    ObjectGroupByResultHolder (SumAggregationFunction.createGroupByResultHolder :62-67), so a group its info never
+    reached -- or reached with null inputs only -- is None, COUNT(col) 0."""
     from pinot_amd.engine.results import ExecutionStatistics, GroupByResultsBlock, merge_intermediate
     from pinot_amd.query.context import columns_of
     infos = _filter_infos(query)
@@ -922,11 +924,11 @@ def _execute_filtered_group_by(query, segments, num_groups_limit):
         gb_cols.update(columns_of(e))
     for seg in segments:
         os_ = OracleSegment(seg)
-        base = eval_filter(os_, query.filter)
+        base = eval_filter(os_, query.filter, null_handling)
         parts = []
         scanned = 0
         for flt, idxs in infos:
-            mask = base if flt is None else (base & eval_filter(os_, flt))
+            mask = base if flt is None else (base & eval_filter(os_, flt, null_handling))
             docs = np.nonzero(mask)[0]
             proj = set(gb_cols)
             for i in idxs:
@@ -946,9 +948,17 @@ def _execute_filtered_group_by(query, segments, num_groups_limit):
         uniq_vals = []
         stride = 1
         for e in query.group_by:
-            u, inv = np.unique(os_.values(e.name)[alldocs], return_inverse=True)
+            vals = os_.values(e.name)[alldocs]
+            nul = os_.nulls(e.name)[alldocs] if null_handling and os_.has_nulls(e.name) else None
+            if nul is not None and nul.any():
+                u, inv_nn = np.unique(vals[~nul], return_inverse=True)
+                inv = np.full(len(alldocs), len(u), dtype=np.int64)   # the null key: one code past the values
+                inv[~nul] = inv_nn
+                u = list(u.tolist()) + [None]
+            else:
+                u, inv = np.unique(vals, return_inverse=True)
             uniq_vals.append(u)
-            codes += inv.astype(np.int64) * stride
+            codes += np.asarray(inv).astype(np.int64) * stride
             stride *= max(len(u), 1)
         ukeys, first, inv = np.unique(codes, return_index=True, return_inverse=True)
         order = np.argsort(first, kind="stable")       # first seen over info 0, info 1, ...
@@ -972,14 +982,17 @@ def _execute_filtered_group_by(query, segments, num_groups_limit):
             off += len(docs)
             keep = gid < ng                             # INVALID_ID past the limit: doc dropped
             for i in idxs:
-                per_agg[i], per_exact[i] = _group_aggregate(os_, query.aggregations[i], docs[keep], gid[keep], ng)
+                ag = query.aggregations[i]
+                if null_handling and ag.function in _NULLABLE and ag.argument is not None:
+                    per_agg[i], per_exact[i] = _group_aggregate_nullable(os_, ag, docs[keep], gid[keep], ng)
+                else:
+                    per_agg[i], per_exact[i] = _group_aggregate(os_, ag, docs[keep], gid[keep], ng)
         for g, k in enumerate(keys):
             vals = [per_agg[a][g] for a in range(na)]
             exs = [per_exact[a][g] if per_exact[a] is not None else None for a in range(na)]
             if k in groups:
+                exact_groups[k] = [_merge_exact(a, b, x, y) for a, b, x, y in zip(exact_groups[k], exs, groups[k], vals)]
                 groups[k] = [merge_intermediate(ag.function, a, b) for ag, a, b in zip(query.aggregations, groups[k], vals)]
-                exact_groups[k] = [(a + b) if a is not None and b is not None else None
-                                   for a, b in zip(exact_groups[k], exs)]
             else:
                 groups[k] = vals
                 exact_groups[k] = exs

@@ -340,6 +340,7 @@ enum SelKind : int32_t {
   SEL_F64 = 1,  // FLOAT / DOUBLE column, or an arithmetic expression (evaluated in double, as the transform
                 // functions do): the value as double bits
   SEL_ID = 2,   // STRING column: the id in the query-global dictionary (DevCol.remap)
+  SEL_STR = 3,  // raw STRING column: the row's locator (segment entry << 32 | doc); its bytes are gathered after
 };
 struct DevSelect {
   int32_t expr;  // PHIP_EXPR_*

@@ -83,6 +83,10 @@ hipError_t launch_group_gather_mapped(const int64_t *keys, const int64_t *d_ngro
 hipError_t launch_select_count(const DevSelQuery *q, int64_t total_work, int64_t *tile_cnt, hipStream_t s);
 hipError_t launch_select_scan(void *temp, size_t *temp_bytes, const int64_t *in, int64_t *out, int64_t n, hipStream_t s);
 hipError_t launch_select_bases(const DevSelQuery *q, int64_t *seg_base, int64_t *kept, int64_t *total, hipStream_t s);
+hipError_t launch_select_str_lens(const uint64_t *loc, int64_t rows, const uint64_t *const *offs, uint32_t *lens,
+                                  hipStream_t s);
+hipError_t launch_select_str_bytes(const uint64_t *loc, int64_t rows, const uint8_t *const *strs,
+                                   const uint64_t *const *offs, const uint64_t *dst_off, uint8_t *dst, hipStream_t s);
 hipError_t launch_select_gather(const DevSelQuery *q, int64_t total_work, uint64_t *out, int64_t num_rows,
                                 hipStream_t s);
 hipError_t launch_limit_prepare(const int64_t *slots, int64_t n, const uint64_t *hkeys, const uint32_t *first_doc,
@@ -1944,6 +1948,7 @@ struct Plan {
           *sel_total = nullptr;
   std::vector<int32_t> sel_types;
   std::vector<std::shared_ptr<Device::Remap>> sel_dicts;
+  std::vector<std::vector<const void *>> sel_str_ptrs;  // per SEL_STR expression: its segments' bytes, then offsets
   std::vector<int32_t> sel_bits, sel_width;  // per select column's projected bytes (algorithmic bytes)
   float sel_filter_ms = 0.f;
   // record ev[0] / ev[3] around the whole sequence (phip_result.device_ms): off by default -- every timing marker is a
@@ -2416,15 +2421,21 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
         if (cs.type != t0) return fail(PHIP_ERR_UNSUPPORTED, "selection: column %s changes type across segments", q->columns[c]);
         if (cs.fwd_kind == PHIP_FWD_HLL_REGISTERS)
           return fail(PHIP_ERR_INVALID, "selection of the HLL register column %s", q->columns[c]);
-        if (cs.type == PHIP_TYPE_STRING && (e.expr != PHIP_EXPR_COLUMN || cs.fwd_kind == PHIP_FWD_RAW_CHUNK))
-          return fail(PHIP_ERR_UNSUPPORTED, "selection: STRING column %s outside a dictionary-encoded projection",
-                      q->columns[c]);
+        if (cs.type == PHIP_TYPE_STRING && e.expr != PHIP_EXPR_COLUMN)
+          return fail(PHIP_ERR_INVALID, "selection: numeric expression over STRING column %s", q->columns[c]);
+        if (cs.type == PHIP_TYPE_STRING && (cs.fwd_kind == PHIP_FWD_RAW_CHUNK) !=
+                                               (segs[0]->cols[colidx[0][c]].fwd_kind == PHIP_FWD_RAW_CHUNK))
+          return fail(PHIP_ERR_UNSUPPORTED, "selection: STRING column %s raw in some segments only", q->columns[c]);
       }
     }
     const int t = segs[0]->cols[colidx[0][e.column_a]].type;
     if (e.expr != PHIP_EXPR_COLUMN) {
       d.kind = SEL_F64;
       sel_types[k] = PHIP_TYPE_DOUBLE;
+    } else if (t == PHIP_TYPE_STRING && segs[0]->cols[colidx[0][e.column_a]].fwd_kind == PHIP_FWD_RAW_CHUNK) {
+      // a raw STRING column: the rows' locators, their bytes gathered after the rows are known (execute_select)
+      d.kind = SEL_STR;
+      sel_types[k] = PHIP_TYPE_STRING;
     } else if (t == PHIP_TYPE_STRING) {
       d.kind = SEL_ID;
       sel_types[k] = PHIP_TYPE_STRING;
@@ -3642,6 +3653,17 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     P.sq_off = sq_off;
     P.sel_types = sel_types;
     P.sel_dicts = sel_dicts;
+    P.sel_str_ptrs.assign(nsel, {});
+    for (int k = 0; k < nsel; k++) {
+      if (sq.sel[k].kind != SEL_STR) continue;
+      std::vector<const void *> &v = P.sel_str_ptrs[k];
+      v.resize(2 * (size_t)nseg);
+      for (int s = 0; s < nseg; s++) {
+        const ColumnStore &cs = segs[s]->cols[colidx[s][sq.sel[k].col_a]];
+        v[s] = cs.raw;
+        v[nseg + s] = cs.str_off;
+      }
+    }
     for (int k = 0; k < nsel; k++) {  // bytes one row reads per expression (first segment's widths)
       for (int c : {sq.sel[k].col_a, sq.sel[k].expr != PHIP_EXPR_COLUMN ? sq.sel[k].col_b : -1}) {
         if (c < 0) continue;
@@ -4120,6 +4142,7 @@ static int32_t execute_select(Plan &P, Workspace &ws, hipStream_t st, ResultImpl
   kept.assign(nent, 0);
   *num_rows = 0;
   *gather_ms = 0.f;
+  impl.sel_dicts = P.sel_dicts;  // (a raw STRING expression's own dictionary replaces its entry below)
   if (tw > 0) {
     size_t tb = 0;
     HIP_TRY(launch_select_scan(nullptr, &tb, nullptr, nullptr, tw + 1, st));
@@ -4143,6 +4166,49 @@ static int32_t execute_select(Plan &P, Workspace &ws, hipStream_t st, ResultImpl
     HIP_TRY(hipMemcpyAsync(impl.sel_values.data(), out, (size_t)rows * P.nsel * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipEventElapsedTime(gather_ms, P.ev[4], P.ev[2]));
+    // raw STRING expressions: the rows' bytes gathered by locator, then the distinct row values (bytewise order) as
+    // this result's dictionary of the column, the rows pointing into it
+    for (int k = 0; k < P.nsel; k++) {
+      if (P.sel_str_ptrs[k].empty()) continue;
+      const std::vector<const void *> &ptrs = P.sel_str_ptrs[k];
+      const size_t ns = ptrs.size() / 2;
+      void *tab, *lens, *doff, *dst;
+      if ((rc = ws.get("sel_str_tab", ptrs.size() * 8, &tab)) || (rc = ws.get("sel_str_lens", (size_t)rows * 4, &lens)) ||
+          (rc = ws.get("sel_str_off", (size_t)rows * 8, &doff)))
+        return rc;
+      const uint64_t *loc = (const uint64_t *)out + (size_t)k * rows;
+      HIP_TRY(hipMemcpyAsync(tab, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(launch_select_str_lens(loc, rows, (const uint64_t *const *)tab + ns, (uint32_t *)lens, st));
+      std::vector<uint32_t> hl((size_t)rows);
+      HIP_TRY(hipMemcpyAsync(hl.data(), lens, (size_t)rows * 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      std::vector<uint64_t> ho((size_t)rows + 1, 0);
+      for (int64_t r = 0; r < rows; r++) ho[(size_t)r + 1] = ho[(size_t)r] + hl[(size_t)r];
+      if ((rc = ws.get("sel_str_bytes", std::max<uint64_t>(ho[(size_t)rows], 16), &dst))) return rc;
+      HIP_TRY(hipMemcpyAsync(doff, ho.data(), (size_t)rows * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(launch_select_str_bytes(loc, rows, (const uint8_t *const *)tab, (const uint64_t *const *)tab + ns,
+                                      (const uint64_t *)doff, (uint8_t *)dst, st));
+      std::vector<uint8_t> hb(ho[(size_t)rows]);
+      if (!hb.empty()) HIP_TRY(hipMemcpyAsync(hb.data(), dst, hb.size(), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      std::vector<std::string> vals((size_t)rows);
+      for (int64_t r = 0; r < rows; r++) vals[(size_t)r].assign((const char *)hb.data() + ho[(size_t)r], hl[(size_t)r]);
+      std::vector<std::string> uniq = vals;
+      std::sort(uniq.begin(), uniq.end());
+      uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+      size_t width = 1;
+      for (const auto &u : uniq) width = std::max(width, u.size());
+      auto rd = std::make_shared<Device::Remap>();
+      rd->type = PHIP_TYPE_STRING;
+      rd->width = (int32_t)width;
+      rd->card = (int32_t)uniq.size();
+      rd->values.assign(uniq.size() * width, 0);
+      for (size_t i = 0; i < uniq.size(); i++) memcpy(rd->values.data() + i * width, uniq[i].data(), uniq[i].size());
+      for (int64_t r = 0; r < rows; r++)
+        impl.sel_values[(size_t)k * rows + r] =
+            (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), vals[(size_t)r]) - uniq.begin());
+      impl.sel_dicts[k] = rd;
+    }
   }
   *num_rows = rows;
   return PHIP_OK;
@@ -4684,7 +4750,6 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     r.num_rows = sel_rows;
     r.num_select = P.nsel;
     impl->sel_types = P.sel_types;
-    impl->sel_dicts = P.sel_dicts;
     r.select_types = impl->sel_types.data();
     r.select_values = impl->sel_values.data();
     r.filter_kernel_ms = has_filter ? P.sel_filter_ms : 0.0;

@@ -71,6 +71,7 @@ __device__ __forceinline__ uint64_t sel_value(cseg_t &seg, const PHIP_CAS DevSel
       const uint32_t id = col_dict_id(a, doc);
       return (uint64_t)(int64_t)(a.remap ? ((const PHIP_GLB int32_t *)a.remap)[id] : (int32_t)id);
     }
+    if (s.kind == SEL_STR) return ((uint64_t)(uint32_t)seg.seg_index << 32) | (uint32_t)doc;
     if (s.kind == SEL_I64) return (uint64_t)col_i64(a, doc);
     return as_u64(col_f64(a, doc));
   }
@@ -142,6 +143,40 @@ hipError_t launch_select_scan(void *temp, size_t *temp_bytes, const int64_t *in,
 
 hipError_t launch_select_bases(const DevSelQuery *q, int64_t *seg_base, int64_t *kept, int64_t *total, hipStream_t s) {
   select_bases_kernel<<<1, 64, 0, s>>>(q, seg_base, kept, total);
+  return hipGetLastError();
+}
+
+// Raw STRING rows (SEL_STR): each row's locator -> its byte length, then (offsets from the host) its bytes back to
+// back. strs[i] / offs[i]: segment entry i's UTF-8 bytes and num_docs + 1 offsets.
+__global__ void select_str_lens_kernel(const uint64_t *__restrict__ loc, int64_t rows, const uint64_t *const *offs,
+                                       uint32_t *__restrict__ lens) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t *o = offs[loc[r] >> 32];
+    const uint32_t d = (uint32_t)loc[r];
+    lens[r] = (uint32_t)(o[d + 1] - o[d]);
+  }
+}
+__global__ void select_str_bytes_kernel(const uint64_t *__restrict__ loc, int64_t rows, const uint8_t *const *strs,
+                                        const uint64_t *const *offs, const uint64_t *__restrict__ dst_off,
+                                        uint8_t *__restrict__ dst) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = loc[r] >> 32;
+    const uint32_t d = (uint32_t)loc[r];
+    const uint64_t s = offs[e][d], n = offs[e][d + 1] - s;
+    for (uint64_t b = 0; b < n; b++) dst[dst_off[r] + b] = strs[e][s + b];
+  }
+}
+hipError_t launch_select_str_lens(const uint64_t *loc, int64_t rows, const uint64_t *const *offs, uint32_t *lens,
+                                  hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  select_str_lens_kernel<<<(int)std::min<int64_t>(4096, (rows + 255) / 256), 256, 0, s>>>(loc, rows, offs, lens);
+  return hipGetLastError();
+}
+hipError_t launch_select_str_bytes(const uint64_t *loc, int64_t rows, const uint8_t *const *strs,
+                                   const uint64_t *const *offs, const uint64_t *dst_off, uint8_t *dst, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  select_str_bytes_kernel<<<(int)std::min<int64_t>(4096, (rows + 255) / 256), 256, 0, s>>>(loc, rows, strs, offs,
+                                                                                             dst_off, dst);
   return hipGetLastError();
 }
 

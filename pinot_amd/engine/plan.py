@@ -1839,8 +1839,8 @@ def _null_handling_operator(query: QueryContext, segments, limit):
     (GpuCombineOperator.null_keys). This picks the aggregation side:
       * aggregation only -> GpuNullHandlingAggregationOperator;
       * group-by: GpuNullHandlingGroupByOperator when a nullable function's column has a null vector in some segment
-        (per-group null results); else the regular operators (null keys, if any, come from the library). FILTER
-        clauses and CASE with GROUP BY stay UnsupportedOnGpu;
+        (per-group null results) or a function has a FILTER (a group its info never reached is null); else the
+        regular operators (null keys, if any, come from the library). CASE with GROUP BY stays UnsupportedOnGpu;
       * selection: the selected columns must be null-free (the reference returns nulls for null values);
     None = the regular operators apply."""
     def null_cols(exprs):
@@ -1857,8 +1857,8 @@ def _null_handling_operator(query: QueryContext, segments, limit):
         return None
     nullable_args = [ag.argument for ag in query.aggregations if ag.function in _NULLABLE and ag.argument is not None]
     if query.group_by:
-        if any(ag.filter is not None for ag in query.aggregations):
-            raise UnsupportedOnGpu("enableNullHandling with FILTER clauses and GROUP BY")
+        if any(ag.filter is not None for ag in query.aggregations):  # (unreached groups: null holders)
+            return GpuNullHandlingGroupByOperator(query, segments, limit, null_cols(nullable_args))
         if null_cols(nullable_args):
             return GpuNullHandlingGroupByOperator(query, segments, limit, null_cols(nullable_args))
         return None
@@ -1880,19 +1880,41 @@ class GpuNullHandlingGroupByOperator:
     program 0's. The statistics are the reference's single pass: numDocsScanned = program 0's matched docs
     (phip_result.program_docs_matched), post-filter entries = those x the distinct projected columns, filter scans of
     program 0 only. The server-level trim runs on the host after the nulls are restored (the device would order a
-    null result by its holder default)."""
+    null result by its holder default).
+
+    With FILTER clauses (FilteredGroupByOperator.java:110-176 under null handling) the infos of
+    GpuFilteredGroupByOperator -- one per distinct FILTER, then the main filter's -- are programs 0..I-1 in that
+    order (first-seen over info 0's docs, then info 1's, ...), each IS NOT NULL set a program ``info filter AND c IS
+    NOT NULL ...`` after them, and every nullable function carries the non-null count of its own program: its holder
+    is an ObjectGroupByResultHolder (SumAggregationFunction.createGroupByResultHolder :62-67), so a group its info
+    never reached is null too. Statistics sum over the infos (each projecting the group-by columns plus its
+    functions' arguments)."""
 
     _MAX_PROGRAMS = 8
 
     def __init__(self, query: QueryContext, segments: Sequence[GpuSegment], num_groups_limit: int, null_cols):
         self.query = query
         self.segments = list(segments)
-        keys = [None]  # program 0: the query's filter (its docs: every group)
+        main, by_filter = [], {}
+        for i, ag in enumerate(query.aggregations):
+            if ag.filter is None:
+                main.append(i)
+            else:
+                by_filter.setdefault(ag.filter, []).append(i)
+        order = list(by_filter.items())
+        self.num_filtered_infos = len(order)
+        skip = str(query.options.get("filteredAggregationsSkipEmptyGroups", "false")).lower() == "true"
+        if main or not skip or not order:
+            order.append((None, main))
+        filtered = self.num_filtered_infos > 0
+        info_filters = [query.filter if flt is None else _and(query.filter, flt) for flt, _ in order]
+        info_of = {i: p for p, (_, idxs) in enumerate(order) for i in idxs}
+        keys = [(p, ()) for p in range(len(order))]  # programs 0..I-1: the infos (their docs: every group)
         aggs, progs = [], []
         counts = {}
 
-        def program_of(cols):
-            k = tuple(sorted(cols))
+        def program_of(p, cols):
+            k = (p, tuple(sorted(cols)))
             if k not in keys:
                 keys.append(k)
             return keys.index(k)
@@ -1905,63 +1927,76 @@ class GpuNullHandlingGroupByOperator:
             return counts[p]
 
         self.slots = []  # per original aggregation: (value index, non-null count index or None)
-        for ag in query.aggregations:
+        for i, ag0 in enumerate(query.aggregations):
+            ag = ag0.unfiltered()
+            p = info_of[i]
             cols = [c for c in columns_of(ag.argument) if c in null_cols] if ag.argument is not None else []
-            if ag.function not in _NULLABLE or not cols:
+            nullable = ag.function in _NULLABLE and ag.argument is not None
+            if not nullable or (not cols and not filtered):
                 self.slots.append((len(aggs), None))
                 aggs.append(ag)
-                progs.append(0)
+                progs.append(p)
                 continue
-            p = program_of(cols)
+            q = program_of(p, cols) if cols else p
             if ag.function == "count":
-                self.slots.append((count_for(p), None))
+                self.slots.append((count_for(q), None))
                 continue
             if ag.function == "avg":  # (its own count is the non-null count)
                 self.slots.append((len(aggs), "avg"))
                 aggs.append(ag)
-                progs.append(p)
+                progs.append(q)
                 continue
-            ci = count_for(p)
+            ci = count_for(q)
             self.slots.append((len(aggs), ci))
             aggs.append(ag)
-            progs.append(p)
+            progs.append(q)
         if len(keys) > self._MAX_PROGRAMS:
-            raise UnsupportedOnGpu("enableNullHandling GROUP BY: more than 8 sets of null-holding argument columns")
+            raise UnsupportedOnGpu("enableNullHandling GROUP BY: more than 8 infos and sets of null-holding argument "
+                                   "columns")
         filters = []
-        for k in keys:
-            if k is None:
-                filters.append(query.filter)
-                continue
-            nn = [FilterContext.PRED(Predicate("IS_NOT_NULL", Identifier(c))) for c in k]
-            parts = ([query.filter] if query.filter is not None else []) + nn
-            filters.append(parts[0] if len(parts) == 1 else FilterContext.AND(*parts))
+        for p, cols in keys:
+            nn = [FilterContext.PRED(Predicate("IS_NOT_NULL", Identifier(c))) for c in cols]
+            parts = ([info_filters[p]] if info_filters[p] is not None else []) + nn
+            filters.append(None if not parts else parts[0] if len(parts) == 1 else FilterContext.AND(*parts))
         sub = QueryContext(query.table, [], aggs, None, list(query.group_by), [], limit=query.limit,
                            options=dict(query.options))
         self.op = GpuCombineOperator(sub, self.segments, num_groups_limit, programs=(filters, progs))
         if len(self.op.prims) > 8:  # (device.h kMaxAggs primitive slots: the functions plus their non-null counts)
             self.op.close()
             raise UnsupportedOnGpu("enableNullHandling GROUP BY: more than 8 aggregation slots with the non-null counts")
-        self.op.stats_programs = 1  # (program 0's filter scans: the reference's one pass)
+        self.num_infos = len(order)
+        self.op.stats_programs = (1 << len(order)) - 1  # (the infos' filter scans: the reference's passes)
         self.op.device_trim = False
-        proj = set()
+        gb = set()
         for e in query.group_by:
-            proj.update(columns_of(e))
-        for ag in query.aggregations:
-            if ag.argument is not None:
-                proj.update(c for c in columns_of(ag.argument) if c != "*")
-        self.num_projected = len(proj)
+            gb.update(columns_of(e))
+        self.info_projected = []  # per info: the group-by columns plus its functions' arguments
+        for _, idxs in order:
+            proj = set(gb)
+            for i in (idxs if filtered else range(len(query.aggregations))):
+                ag = query.aggregations[i]
+                if ag.argument is not None:
+                    proj.update(c for c in columns_of(ag.argument) if c != "*")
+            self.info_projected.append(len(proj))
+        self.num_projected = self.info_projected[-1]
 
     def next_block(self):
         from .reduce import trim_groups
         blk = self.op.next_block()
+        if blk.num_groups_limit_reached and self.num_filtered_infos >= 2:
+            raise UnsupportedOnGpu("numGroupsLimit reached by a FILTER + GROUP BY query with two or more filtered "
+                                   "infos (the reference's info order is HashMap order)")
         groups = {}
         for key, vals in blk.groups.items():
             groups[key] = [None if (ci == "avg" and vals[vi][1] == 0) or (isinstance(ci, int) and vals[ci] == 0)
                            else vals[vi] for vi, ci in self.slots]
         stats = dataclasses.replace(blk.stats)
-        docs0 = blk.program_docs_matched[0] if blk.program_docs_matched else stats.num_docs_scanned
-        stats.num_docs_scanned = docs0
-        stats.num_entries_scanned_post_filter = docs0 * self.num_projected
+        if blk.program_docs_matched:
+            docs = [int(blk.program_docs_matched[p]) for p in range(self.num_infos)]
+        else:
+            docs = [stats.num_docs_scanned]
+        stats.num_docs_scanned = sum(docs)
+        stats.num_entries_scanned_post_filter = sum(d * n for d, n in zip(docs, self.info_projected))
         out = GroupByResultsBlock(self.query.aggregations, list(self.query.group_by), groups, stats,
                                   blk.num_groups_limit_reached)
         out.key_types = getattr(blk, "key_types", None)

@@ -221,4 +221,7 @@ hipError_t launch_select_bases(const DevSelQuery *q, int64_t *, int64_t *kept, i
   total[0] = total[1] = 0; return hipSuccess;
 }
 hipError_t launch_select_gather(const DevSelQuery *, int64_t, uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
+hipError_t launch_select_str_lens(const uint64_t *, int64_t, const uint64_t *const *, uint32_t *, hipStream_t) { return hipSuccess; }
+hipError_t launch_select_str_bytes(const uint64_t *, int64_t, const uint8_t *const *, const uint64_t *const *, const uint64_t *, uint8_t *,
+                                   hipStream_t) { return hipSuccess; }
 }  // namespace phip

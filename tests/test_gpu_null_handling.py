@@ -115,7 +115,6 @@ def test_gpu_null_handling_group_by_over_null_free_columns(sql, null_segments):
 
 
 @pytest.mark.parametrize("sql", [
-    "SELECT g, SUM(k) FILTER (WHERE d > 3) FROM t GROUP BY g LIMIT 10",
     # nine primitive slots once the non-null counts are added (device kMaxAggs = 8): the CPU plan maker's
     "SELECT g, SUM(d), MIN(l), MAX(f), COUNT(*), AVG(r) FROM t GROUP BY g LIMIT 10",
     "SELECT d, k FROM t WHERE g = 1 LIMIT 10",                  # selected null values
@@ -201,6 +200,29 @@ def test_gpu_null_handling_group_by_table_modes(sql, mode, null_segments, monkey
     table) where the program is conjunctive, and as tuple keys (a null key's id inside the packed tuple)."""
     monkeypatch.setenv(*{"hash": ("PHIP_GB_HASH", "1"), "fused_xcd": ("PHIP_FUSED_GB", "3"),
                          "fused_hbm": ("PHIP_FUSED_GB", "2"), "tuple": ("PHIP_TUPLE_KEYS", "1")}[mode])
+    qc, blk, oblk, ex = _run(NH + sql, null_segments)
+    _check_nullable_groups(qc, blk, oblk, ex)
+
+
+NH_FILTER_GB = [
+    "SELECT g, SUM(k) FILTER (WHERE d > 3), COUNT(*) FROM t GROUP BY g LIMIT 100",
+    "SELECT d, g, SUM(l) FILTER (WHERE k > 40), MIN(f) FILTER (WHERE s IS NULL), COUNT(d) FILTER (WHERE g < 3), "
+    "AVG(r) FROM t WHERE g < 6 GROUP BY d, g LIMIT 100000",
+    # every function filtered: the main info still generates the groups (functions none of whose docs reached a group
+    # are null, COUNT 0)
+    "SELECT s, MAX(f) FILTER (WHERE d IS NOT NULL), COUNT(*) FILTER (WHERE d > 190) FROM t GROUP BY s LIMIT 100",
+    "SELECT z, SUM(z) FILTER (WHERE g = 1), COUNT(*) FROM t GROUP BY z LIMIT 10",
+    "SET filteredAggregationsSkipEmptyGroups = true; SELECT g, t, SUM(k) FILTER (WHERE d > 150), "
+    "MINMAXRANGE(l) FILTER (WHERE d > 150) FROM t GROUP BY g, t LIMIT 100000",
+]
+
+
+@pytest.mark.parametrize("sql", NH_FILTER_GB)
+def test_gpu_null_handling_filtered_group_by(sql, null_segments):
+    """FILTER + GROUP BY under enableNullHandling (FilteredGroupByOperator's infos over the null-aware generator):
+    programs = the infos, then their IS NOT NULL sets; a nullable function is null where its own program's docs
+    never reached the group (ObjectGroupByResultHolder). Keys, every intermediate and the summed statistics equal the
+    oracle's."""
     qc, blk, oblk, ex = _run(NH + sql, null_segments)
     _check_nullable_groups(qc, blk, oblk, ex)
 

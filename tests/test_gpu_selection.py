@@ -41,7 +41,7 @@ def _segments():
     out = []
     for k in range(3):
         n = 70_000 + 12_345 * k  # ragged last tiles
-        c = SegmentCreator(f"gs{k}", no_dictionary_columns=["r", "rd"], inverted_index_columns=["h"])
+        c = SegmentCreator(f"gs{k}", no_dictionary_columns=["r", "rd", "rs"], inverted_index_columns=["h"])
         c.add_column("s", DataType.STRING, np.array([f"name{x:04d}" for x in rng.integers(50 * k, 400 + 60 * k, n)]))
         c.add_column("h", DataType.INT, rng.integers(0, 9 + k, n))
         c.add_column("i", DataType.INT, rng.integers(-10 ** 6, 10 ** 6, n))
@@ -51,6 +51,10 @@ def _segments():
         c.add_column("r", DataType.LONG, rng.integers(0, 10 ** 9, n))
         c.add_column("rd", DataType.DOUBLE, rng.random(n))
         c.add_column("srt", DataType.INT, np.sort(rng.integers(0, 5000, n)))
+        # raw STRING (rows' bytes gathered by locator on the device): empty, multi-byte and long values
+        words = np.array(["", "é", "zz-top", "naïve", "日本", "x" * 40] + [f"w{j}" for j in range(300 + 50 * k)],
+                         dtype=object)
+        c.add_column("rs", DataType.STRING, words[rng.integers(0, len(words), n)])
         out.append(c.build())
     return out
 
@@ -81,6 +85,8 @@ QUERIES = [
     "SELECT i, s FROM t WHERE i > 0 LIMIT 3000",                                # cuts inside a tile of segment 0
     "SELECT i, s FROM t WHERE i > 900000 LIMIT 7000",                           # ends inside segment 1
     "SELECT i, i, s FROM t WHERE f < 1.5 LIMIT 1000000",                        # a repeated expression
+    "SELECT rs, i, s, rs FROM t WHERE h = 2 LIMIT 1000000",                     # raw STRING values
+    "SELECT rs FROM t WHERE rs >= 'w2' AND rs < 'x' LIMIT 5000",                # raw STRING leaf and values
 ]
 
 

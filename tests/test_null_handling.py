@@ -294,3 +294,23 @@ def test_oracle_per_group_null_results_hand_derived():
     # numGroupsLimit 2: first seen are 1 (doc 0) and 2 (doc 2); the null key (doc 3) is the third -- dropped
     blk2, _ = executor.execute(qc, [seg], num_groups_limit=2)
     assert set(blk2.groups) == {(1,), (2,)} and blk2.num_groups_limit_reached
+
+
+def test_oracle_filtered_group_by_null_handling_hand_derived():
+    """FILTER + GROUP BY under null handling (FilteredGroupByOperator over the null-aware generator): a FILTER passes
+    the docs where it is TRUE (a null comparison is not), the infos share the generator (the main info's docs make
+    every group), a nullable function whose info never reached a group -- or reached it with null inputs only -- is
+    None (ObjectGroupByResultHolder), COUNT 0; numDocsScanned sums the infos' docs."""
+    c = SegmentCreator("fg")
+    c.add_column("g", DataType.INT, [1, 1, 2, 0, 3], nulls=[0, 0, 0, 1, 0])
+    c.add_column("k", DataType.INT, [5, 0, 7, 9, 0], nulls=[0, 1, 0, 0, 1])
+    c.add_column("d", DataType.INT, [10, 1, 0, 8, 6], nulls=[0, 0, 1, 0, 0])
+    seg = c.build()
+    qc = parse("SET enableNullHandling = true; SELECT g, SUM(k) FILTER (WHERE d > 3), COUNT(k) FILTER (WHERE d > 3), "
+               "COUNT(*) FROM t GROUP BY g")
+    blk, ex = executor.execute(qc, [seg])
+    # info d > 3: docs 0 (g 1, k 5), 3 (g null, k 9), 4 (g 3, k null); the main info: every doc
+    assert blk.groups == {(1,): [5.0, 1, 2], (2,): [None, 0, 1], (None,): [9.0, 1, 1], (3,): [None, 0, 1]}
+    assert ex[(1,)][0] == 5 and ex[(2,)][0] is None
+    assert blk.stats.num_docs_scanned == 3 + 5
+    assert blk.stats.num_entries_scanned_post_filter == 3 * 2 + 5 * 1  # (g, k) per filtered doc; g per main doc
