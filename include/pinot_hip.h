@@ -246,6 +246,7 @@ typedef struct phip_select_expr {
 #define PHIP_ORDER_VALUE 1     /* aggregations[a] as double: SUM / MIN / MAX / COUNT (AggregationFunctionExtractor) */
 #define PHIP_ORDER_AVG 2       /* aggregations[a] (SUM) / aggregations[b] (COUNT); -inf when the count is 0 */
 #define PHIP_ORDER_RANGE 3     /* aggregations[b] (MAX) - aggregations[a] (MIN): MINMAXRANGE */
+#define PHIP_ORDER_HLL 4       /* aggregations[a] (DISTINCTCOUNTHLL): its registers' cardinality estimate */
 
 typedef struct phip_order_term {
   int32_t kind; /* PHIP_ORDER_* */

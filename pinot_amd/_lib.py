@@ -78,7 +78,7 @@ class OrderTerm(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("a", ctypes.c_int32), ("b", ctypes.c_int32), ("desc", ctypes.c_int32)]
 
 
-ORDER_GROUP_KEY, ORDER_VALUE, ORDER_AVG, ORDER_RANGE = 0, 1, 2, 3
+ORDER_GROUP_KEY, ORDER_VALUE, ORDER_AVG, ORDER_RANGE, ORDER_HLL = 0, 1, 2, 3, 4
 
 
 class SelectExpr(ctypes.Structure):

@@ -374,14 +374,14 @@ struct KeyOrder {
 // General ORDER BY for the device trim (trim.hip, launch_trim_order_terms): up to kMaxOrderKeys terms, each a
 // group-by column or the final result of an aggregation (TableResizer's GroupByExpressionExtractor /
 // AggregationFunctionExtractor), sorted least significant term first with stable radix passes.
-enum OrderTermKind : int32_t { TERM_GROUP_KEY = 0, TERM_VALUE = 1, TERM_AVG = 2, TERM_RANGE = 3 };
+enum OrderTermKind : int32_t { TERM_GROUP_KEY = 0, TERM_VALUE = 1, TERM_AVG = 2, TERM_RANGE = 3, TERM_HLL = 4 };
 struct OrderTerms {
   int32_t num_group_by;
   int32_t num_terms;
   int64_t card[kMaxOrderKeys];   // query-global cardinality of group-by column k
   int32_t kind[kMaxOrderKeys];   // OrderTermKind
   int32_t a[kMaxOrderKeys];      // group-by index (GROUP_KEY), value slot (VALUE), SUM / MIN slot (AVG / RANGE)
-  int32_t b[kMaxOrderKeys];      // COUNT slot (AVG), MAX slot (RANGE)
+  int32_t b[kMaxOrderKeys];      // COUNT slot (AVG), MAX slot (RANGE); HLL: a = register block, b = log2m
   int32_t desc[kMaxOrderKeys];
 };
 

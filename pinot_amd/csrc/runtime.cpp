@@ -36,8 +36,8 @@ hipError_t launch_trim_order(const double *vals, const int64_t *keys, const KeyO
                              int32_t agg, int32_t desc, void *scratch, size_t *scratch_bytes, const int32_t **order_out,
                              hipStream_t s);
 hipError_t launch_trim_order_terms(const double *vals, const int64_t *keys, const OrderTerms *ot, int64_t n,
-                                   int32_t naggs, void *scratch, size_t *scratch_bytes, const int32_t **order_out,
-                                   hipStream_t s);
+                                   int32_t naggs, const uint8_t *hll, int64_t hll_bytes, int32_t m_regs, void *scratch,
+                                   size_t *scratch_bytes, const int32_t **order_out, hipStream_t s);
 hipError_t launch_trim_gather(const int32_t *order, int64_t k, int32_t naggs, int64_t hll_bytes, const int64_t *keys,
                               const double *vals, const int64_t *longs, const uint8_t *hll, int64_t *keys_out,
                               double *vals_out, int64_t *longs_out, uint8_t *hll_out, hipStream_t s);
@@ -3714,12 +3714,17 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
           ok = agg_ok(t.a, false) && agg_ok(t.b, false) && q->aggregations[t.a].function == PHIP_AGG_MIN &&
                q->aggregations[t.b].function == PHIP_AGG_MAX;
           break;
+        case PHIP_ORDER_HLL: ok = t.a >= 0 && t.a < q->num_aggregations && q->aggregations[t.a].function == PHIP_AGG_HLL; break;
         default: ok = false;
       }
       if (!ok) return fail(PHIP_ERR_INVALID, "order_terms[%d] (kind %d, a %d, b %d) invalid", j, t.kind, t.a, t.b);
       ot.kind[j] = t.kind;
       ot.a[j] = t.a;
       ot.b[j] = t.b;
+      if (t.kind == PHIP_ORDER_HLL) {  // (the function's register block and its own log2m)
+        ot.a[j] = dq.aggs[t.a].hll_slot;
+        ot.b[j] = dq.aggs[t.a].log2m;
+      }
       ot.desc[j] = t.desc ? 1 : 0;
     }
     P.trim_size = q->trim_size;
@@ -4498,7 +4503,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       for (int k = 0; k < P.num_group_by; k++) ot.card[k] = P.gb_radix[k];
       const bool terms = ot.num_terms > 0;
       if (terms)
-        HIP_TRY(launch_trim_order_terms(nullptr, nullptr, &ot, ngroups, naggs, nullptr, &sbytes, &order, st));
+        HIP_TRY(launch_trim_order_terms(nullptr, nullptr, &ot, ngroups, naggs, nullptr, 0, 0, nullptr, &sbytes, &order,
+                                        st));
       else
         HIP_TRY(launch_trim_order(nullptr, nullptr, kop, ngroups, naggs, P.order_agg, P.order_desc, nullptr, &sbytes,
                                   &order, st));
@@ -4507,7 +4513,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       if ((rc = ws.get("trim_scratch", sbytes, &scratch))) return rc;
       if ((rc = contiguous_out("trim_out", k, &k2, &v2, &l2, &h2))) return rc;
       if (terms)
-        HIP_TRY(launch_trim_order_terms((const double *)ov, (const int64_t *)keys, &ot, ngroups, naggs, scratch, &sbytes,
+        HIP_TRY(launch_trim_order_terms((const double *)ov, (const int64_t *)keys, &ot, ngroups, naggs, (const uint8_t *)oh,
+                                        nhll ? (int64_t)nhll * m_regs : 0, m_regs, scratch, &sbytes,
                                         &order, st));
       else
         HIP_TRY(launch_trim_order((const double *)ov, (const int64_t *)keys, kop, ngroups, naggs, P.order_agg,

@@ -66,8 +66,34 @@ __device__ __forceinline__ uint64_t double_order(double d) {
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);  // Double.compare order: -0.0 < 0.0, NaN last
 }
 
+// clearspring HyperLogLog.cardinality() (stream-lib 2.9.8, DistinctCountHLLAggregationFunction.extractFinalResult;
+// engine/reduce.py hll_cardinality): alpha * m^2 / sum 2^-reg, linear counting below 2.5 m (Long.MAX_VALUE when no
+// register is zero), rounded half up. The sum of dyadic terms is exact in any order.
+__device__ double hll_estimate(const uint8_t *regs, int32_t log2m) {
+  const int32_t m = 1 << log2m;
+  const double md = (double)m;
+  double alpha_mm;
+  if (log2m == 4) alpha_mm = 0.673 * md * md;
+  else if (log2m == 5) alpha_mm = 0.697 * md * md;
+  else if (log2m == 6) alpha_mm = 0.709 * md * md;
+  else alpha_mm = (0.7213 / (1.0 + 1.079 / md)) * md * md;
+  double s = 0.0;
+  int32_t zeros = 0;
+  for (int32_t r = 0; r < m; r++) {
+    s += 1.0 / (double)(1ull << regs[r]);
+    zeros += regs[r] == 0;
+  }
+  const double est = alpha_mm * (1.0 / s);
+  if (est <= 2.5 * md) {
+    if (zeros == 0) return 9223372036854775807.0;
+    return floor(md * log(md / (double)zeros) + 0.5);
+  }
+  return floor(est + 0.5);
+}
+
 __global__ void term_keys_kernel(const double *__restrict__ vals, const int64_t *__restrict__ keys, int64_t n,
                                  int32_t naggs, OrderTerms ot, int32_t j, const int32_t *__restrict__ perm,
+                                 const uint8_t *__restrict__ hll, int64_t hll_bytes, int32_t m_regs,
                                  uint64_t *__restrict__ ukeys, int32_t *__restrict__ idx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t g = perm ? perm[i] : i;
@@ -79,6 +105,9 @@ __global__ void term_keys_kernel(const double *__restrict__ vals, const int64_t 
         key /= ot.card[k];
       }
       u = (uint64_t)(ot.desc[j] ? ot.card[ot.a[j]] - 1 - id : id);
+    } else if (ot.kind[j] == TERM_HLL) {
+      u = double_order(hll_estimate(hll + g * hll_bytes + (int64_t)ot.a[j] * m_regs, ot.b[j]));
+      if (ot.desc[j]) u = ~u;
     } else {
       const double *v = vals + g * naggs;
       double d;
@@ -139,8 +168,8 @@ static inline int key_bits(int64_t card) {
 // General ORDER BY: one stable radix pass per term, least significant term first (LSD over terms), so ties
 // on every term keep the lowest group index. Same scratch layout as launch_trim_order.
 hipError_t launch_trim_order_terms(const double *vals, const int64_t *keys, const OrderTerms *ot, int64_t n,
-                                   int32_t naggs, void *scratch, size_t *scratch_bytes, const int32_t **order_out,
-                                   hipStream_t s) {
+                                   int32_t naggs, const uint8_t *hll, int64_t hll_bytes, int32_t m_regs, void *scratch,
+                                   size_t *scratch_bytes, const int32_t **order_out, hipStream_t s) {
   size_t sort_bytes = 0;
   hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
                                                     (const int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0, 64, s);
@@ -155,7 +184,7 @@ hipError_t launch_trim_order_terms(const double *vals, const int64_t *keys, cons
   void *tmp = (uint8_t *)scratch + keys_bytes + idx_bytes;
   const int32_t *perm = nullptr;
   for (int j = ot->num_terms - 1; j >= 0; j--) {
-    term_keys_kernel<<<trim_grid(n), 256, 0, s>>>(vals, keys, n, naggs, *ot, j, perm, k0, i0);
+    term_keys_kernel<<<trim_grid(n), 256, 0, s>>>(vals, keys, n, naggs, *ot, j, perm, hll, hll_bytes, m_regs, k0, i0);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int end_bit = ot->kind[j] == TERM_GROUP_KEY ? key_bits(ot->card[ot->a[j]]) : 64;

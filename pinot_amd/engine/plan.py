@@ -589,8 +589,9 @@ class GpuCombineOperator:
         group-by values, or aggregations' final results). Returns (order_by_aggregation, desc, trimSize,
         group-key order, general terms): a single SUM/MIN/MAX/COUNT or only group-by columns use the one-pass
         device orders, any other mix of group-by columns and SUM/MIN/MAX/COUNT/AVG/MINMAXRANGE goes as
-        PHIP_ORDER_* terms; an ORDER BY outside that (HLL, post-aggregation expressions) returns every group
-        (the broker's ORDER BY + LIMIT gives the same final rows)."""
+        PHIP_ORDER_* terms (DISTINCTCOUNTHLL by its cardinality estimate, PHIP_ORDER_HLL); an ORDER BY outside that
+        (DISTINCTCOUNTRAWHLL, post-aggregation expressions) returns every group (the broker's ORDER BY + LIMIT gives
+        the same final rows)."""
         from .reduce import _agg_index
         q = getattr(self, "trim_query", None) or self.query
         none = (-1, 0, 0, [], [])
@@ -632,6 +633,8 @@ class GpuCombineOperator:
                 terms.append((_lib.ORDER_AVG, int(sl[0]), int(sl[1]), desc))
             elif f == "minmaxrange":
                 terms.append((_lib.ORDER_RANGE, int(sl[0]), int(sl[1]), desc))
+            elif f == "distinctcounthll":  # (its cardinality estimate, computed from the registers on the device)
+                terms.append((_lib.ORDER_HLL, int(sl), 0, desc))
             else:
                 return none
         if len(terms) == 1 and terms[0][0] == _lib.ORDER_VALUE:

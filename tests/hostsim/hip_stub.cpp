@@ -50,7 +50,7 @@ hipError_t launch_trim_order(const double *, const int64_t *, const KeyOrder *, 
   return hipSuccess;
 }
 hipError_t launch_trim_order_terms(const double *, const int64_t *, const OrderTerms *, int64_t n, int32_t,
-                                   void *scratch, size_t *scratch_bytes, const int32_t **order_out, hipStream_t) {
+                                   const uint8_t *, int64_t, int32_t, void *scratch, size_t *scratch_bytes, const int32_t **order_out, hipStream_t) {
   if (!scratch) {
     *scratch_bytes = (size_t)n * 4 + 64;
     return hipSuccess;

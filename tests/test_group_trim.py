@@ -48,9 +48,14 @@ def test_trim_spec_rules():
                      (_lib.ORDER_AVG, s_avg[0], s_avg[1], 1)]
     (_a, _d, _t, _k, terms), op = _spec("SELECT k, MINMAXRANGE(m) FROM t GROUP BY k ORDER BY MINMAXRANGE(m) LIMIT 10")
     assert terms == [(_lib.ORDER_RANGE, op.mapping[0][1][0], op.mapping[0][1][1], 0)]
-    # no trim: disabled, HLL, no ORDER BY
+    # DISTINCTCOUNTHLL: its cardinality estimate, computed from the registers on the device
+    (_a, _d, _t, _k, terms), op = _spec("SELECT k, DISTINCTCOUNTHLL(m) FROM t GROUP BY k ORDER BY DISTINCTCOUNTHLL(m), "
+                                        "k LIMIT 10")
+    assert terms == [(_lib.ORDER_HLL, op.mapping[0][1], 0, 0), (_lib.ORDER_GROUP_KEY, 0, 0, 0)]
+    # no trim: disabled, a serialized HLL (DISTINCTCOUNTRAWHLL), no ORDER BY
     for sql, opts in (("SELECT k, SUM(m) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 10", {"minServerGroupTrimSize": 0}),
-                      ("SELECT k, DISTINCTCOUNTHLL(m) FROM t GROUP BY k ORDER BY DISTINCTCOUNTHLL(m), k LIMIT 10", {}),
+                      ("SELECT k, DISTINCTCOUNTRAWHLL(m) FROM t GROUP BY k ORDER BY DISTINCTCOUNTRAWHLL(m), k LIMIT 10",
+                       {}),
                       ("SELECT k, SUM(m) FROM t GROUP BY k LIMIT 10", {})):
         assert _spec(sql, **opts)[0] == (-1, 0, 0, [], []), sql
 
@@ -122,6 +127,10 @@ def test_gpu_device_trim(gpu_lib, sql, exact_set):
     "SELECT k, k2, AVG(m) FROM t WHERE q < 45 GROUP BY k, k2 ORDER BY AVG(m) DESC, k2 LIMIT 100",  # hash table
     "SELECT q, k, SUM(m), MIN(m) FROM t GROUP BY q, k ORDER BY q DESC, SUM(m) LIMIT 1200",
     "SELECT k, MINMAXRANGE(m), MAX(m) FROM t GROUP BY k ORDER BY MINMAXRANGE(m), MAX(m) DESC, k LIMIT 10",
+    # the registers' cardinality estimate (clearspring HyperLogLog.cardinality) on the device
+    "SELECT k, DISTINCTCOUNTHLL(k2), COUNT(*) FROM t GROUP BY k ORDER BY DISTINCTCOUNTHLL(k2) DESC, k LIMIT 10",
+    "SELECT k, DISTINCTCOUNTHLL(m, 5), SUM(m) FROM t WHERE q < 30 GROUP BY k ORDER BY DISTINCTCOUNTHLL(m, 5), k DESC "
+    "LIMIT 1100",
 ])
 def test_gpu_device_trim_mixed_order(gpu_lib, sql):
     """Mixed ORDER BY (GroupByUtils.java:108,161 -> TableResizer over group values and final results): the kept
@@ -155,7 +164,9 @@ def test_gpu_device_trim_mixed_order(gpu_lib, sql):
         assert set(blk.groups) == {k for k, _ in recs[:trim]}
         for k, v in blk.groups.items():
             for g, o in zip(v, oblk.groups[k]):
-                if isinstance(o, tuple):
+                if isinstance(o, np.ndarray):
+                    assert np.array_equal(g, o)
+                elif isinstance(o, tuple):
                     assert all(x == y or abs(x - y) <= 1e-9 * max(abs(x), abs(y)) for x, y in zip(g, o))
                 else:
                     assert g == o or abs(g - o) <= 1e-9 * max(abs(g), abs(o))

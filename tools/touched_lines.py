@@ -91,8 +91,14 @@ def main():
                             if (args.materialize_min >= 0 and m.cardinality * w >= args.materialize_min
                                     and c.upper() not in where):
                                 # a value-only column with a large dictionary also has doc-order values (runtime.cpp
-                                # ensure_vals): the floor is the cheaper of the two routes
-                                via_vals = 64 * lines_of(docs, 8 * w)
+                                # ensure_vals), INT / LONG ones bit-packed at their range's width (packed_value_bits):
+                                # the floor is the cheaper of the two routes
+                                vb = 8 * w
+                                if int(m.data_type) in (0, 1):
+                                    dv = np.frombuffer(raw.columns[c].dictionary, dtype=">i4" if w == 4 else ">i8")
+                                    rb = max(1, int(dv[-1]) - int(dv[0])).bit_length()
+                                    vb = rb if rb <= 32 and rb < 8 * w else vb
+                                via_vals = 64 * lines_of(docs, vb)
                                 res[q]["value_line_bytes"] = res[q].get("value_line_bytes", 0) + via_vals
                                 res[q]["ids_dict_line_bytes"] = res[q].get("ids_dict_line_bytes", 0) + via_ids
                                 res[q]["id_line_bytes"] += min(via_vals, via_ids)
