@@ -1758,7 +1758,8 @@ class GpuGroupByCombineOperator:
             return self._run_per_segment()
         if self.seg_trim is not None:
             bounds = [min(b, self.seg_trim) for b in bounds]
-        distinct = None if getattr(blk, "num_groups_trimmed", True) else len(blk.groups)
+        # (num_groups: a columnar block's count without building its {key: intermediates} view, ~0.1 ms at 800 groups)
+        distinct = None if getattr(blk, "num_groups_trimmed", True) else blk.num_groups
         self._check_threshold(bounds, distinct, getattr(blk, "key_space", None))
         return blk
 
