@@ -4148,6 +4148,13 @@ static int32_t execute_select(Plan &P, Workspace &ws, hipStream_t st, ResultImpl
   *num_rows = 0;
   *gather_ms = 0.f;
   impl.sel_dicts = P.sel_dicts;  // (a raw STRING expression's own dictionary replaces its entry below)
+  for (int k = 0; k < P.nsel; k++) {
+    if (P.sel_str_ptrs[k].empty()) continue;
+    auto rd = std::make_shared<Device::Remap>();  // (no row: an empty dictionary)
+    rd->type = PHIP_TYPE_STRING;
+    rd->width = 1;
+    impl.sel_dicts[k] = rd;
+  }
   if (tw > 0) {
     size_t tb = 0;
     HIP_TRY(launch_select_scan(nullptr, &tb, nullptr, nullptr, tw + 1, st));

@@ -115,6 +115,23 @@ try:
 except _lib.PhipError:
     pass
 op.close()
+# round 5: raw STRING keys / HLL / selection (device hashing and the host merge of representatives), tuple keys
+# (forced on a small key space), the HLL-ordered trim, packed doc-order values
+for q in ("SELECT s, h, COUNT(*) FROM t GROUP BY s, h LIMIT 1000",
+          "SELECT h, DISTINCTCOUNTHLL(s), DISTINCTCOUNTHLL(s, 10) FROM t GROUP BY h LIMIT 100",
+          "SELECT s, h FROM t WHERE h > 1 LIMIT 50"):
+    pm.make_instance_plan(parse(q), rs).next_block()
+os.environ["PHIP_TUPLE_KEYS"] = "1"
+pm.make_instance_plan(parse("SELECT g, h, COUNT(*), SUM(m) FROM t GROUP BY g, h ORDER BY SUM(m) DESC LIMIT 5"),
+                      gs).next_block()
+pm.make_instance_plan(parse("SELECT g, h, r, COUNT(*) FROM t GROUP BY g, h, r ORDER BY g, h LIMIT 5"), gs).next_block()
+del os.environ["PHIP_TUPLE_KEYS"]
+hq = parse("SELECT g, DISTINCTCOUNTHLL(m), COUNT(*) FROM t GROUP BY g ORDER BY DISTINCTCOUNTHLL(m) DESC, g LIMIT 2")
+hq.options["minServerGroupTrimSize"] = "3"
+pm.make_instance_plan(hq, gs).next_block()
+os.environ["PHIP_MATERIALIZE_MIN_DICT"] = "0"
+pm.make_instance_plan(parse("SELECT SUM(m), MAX(h), SUM(r) FROM t WHERE d < 0.5"), gs).next_block()
+del os.environ["PHIP_MATERIALIZE_MIN_DICT"]
 for g in rs:
     g.destroy()
 for g in gs:

@@ -87,6 +87,7 @@ QUERIES = [
     "SELECT i, i, s FROM t WHERE f < 1.5 LIMIT 1000000",                        # a repeated expression
     "SELECT rs, i, s, rs FROM t WHERE h = 2 LIMIT 1000000",                     # raw STRING values
     "SELECT rs FROM t WHERE rs >= 'w2' AND rs < 'x' LIMIT 5000",                # raw STRING leaf and values
+    "SELECT rs, i FROM t WHERE h = 100 LIMIT 50",                               # raw STRING, nothing matches
 ]
 
 
