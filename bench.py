@@ -39,7 +39,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROUND = "r05"
+ROUND = "r06"
+
+
+def latest_profile(kind):
+    """profiles/<round>_<kind>.json of this round, else the newest earlier round's (rNN sorts by name)."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{kind}.json")))
+    mine = os.path.join(ROOT, "profiles", f"{ROUND}_{kind}.json")
+    return mine if os.path.exists(mine) else (cands[-1] if cands else mine)
 
 
 def log(msg):
@@ -140,7 +148,7 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
     # restatement on the same segments (check_parity)
     answers = {q: ops[q].next_block() for q in queries}
     concurrent = None
-    if dist is None:
+    if dist is None and not args.no_concurrent:
         # Outside the headline: the same queries as concurrent clients (one thread per query, each running its
         # prepared plan `steps` times back to back on its own execution lane -- a server's worker threads, DESIGN.md
         # §7); reported beside `value`, which stays the sequential step.
@@ -410,9 +418,45 @@ def roofline(kstats, queries, traffic, touched, layout, steps):
                      "touched_floor = streamed bytes + the 64-B lines a launch's gathers must move"}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without torchrun: N rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set as torch.distributed.run sets them, rendezvous on 127.0.0.1), started before this process touches
+    the GPU. Rank 0's stdout (the JSON line) passes through; every rank's stderr is inherited. Returns the exit
+    code: the first non-zero one (the other ranks are then stopped), else 0."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr, start_new_session=False))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"rank {procs.index(p)} exited with {code}: stopping the other ranks")
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks. Under torchrun it must equal WORLD_SIZE; without torchrun, N > 1 starts N rank "
+                         "processes here (one per GPU, before any GPU call) and prints rank 0's line")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--segs-per-gpu", type=int, default=0,
@@ -431,14 +475,22 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the check of every query's answer against oracle/cpu_scan.c on the same segments")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", f"{ROUND}_traffic.json"),
+    ap.add_argument("--no-concurrent", action="store_true",
+                    help="skip the concurrent-client leg (profiling runs: every kernel launch is then sequential, so "
+                         "rocprof averages equal the timed leg's)")
+    ap.add_argument("--traffic-json", default=latest_profile("traffic"),
                     help="HBM bytes per launch per kernel and layout from rocprofv3 --pmc passes (tools/traffic.py)")
-    ap.add_argument("--touched-json", default=os.path.join(ROOT, "profiles", f"{ROUND}_touched.json"),
+    ap.add_argument("--touched-json", default=latest_profile("touched"),
                     help="64-B lines the gathers touch per query and layout (tools/touched_lines.py)")
     ap.add_argument("--seed", type=int, default=42)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        raise SystemExit(spawn_ranks(args.gpus))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -519,15 +571,16 @@ def main():
             qc5 = parse(ssb.SSB_QUERIES["C5"])
             el5, lat5, blk5 = run_c5(args, dist, qc5, gsegs, torch)
             rows5 = sum(s.num_docs for s in gsegs) * world
-            res["c5"] = {"query": ssb.SSB_QUERIES["C5"], "rows": rows5, "segments": len(gsegs) * world,
+            res["c5_merged"] = {"query": ssb.SSB_QUERIES["C5"], "rows": rows5, "segments": len(gsegs) * world,
                          "value": round(rows5 * args.steps / el5 / 1e9, 3), "unit": "G rows/s",
                          "ms_per_query": round(el5 * 1e3 / args.steps, 3),
                          "p50_latency_ms": round(float(np.median(lat5)), 3), "groups": len(blk5.groups),
-                         "merge": "distributed_block: node-global dictionaries, dense partial tables all-reduced "
-                                  f"in place over {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
-                                  "(int64 SUM + uint8 MAX for this query)"}
+                         "merge": ("distributed_block: node-global dictionaries, dense partial tables all-reduced "
+                                   f"in place over {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
+                                   "(int64 SUM + uint8 MAX for this query)") if dist is not None
+                         else "one GPU: no exchange"}
             if not args.no_parity:
-                res["c5"]["parity"] = check_merged_group_by(qc5, blk5, all_raws, dist)
+                res["c5_merged"]["parity"] = check_merged_group_by(qc5, blk5, all_raws, dist)
         for s in gsegs:
             s.destroy()
         del all_raws
@@ -573,7 +626,10 @@ def main():
                                + (f" (each rank holds {seg_per_gpu} segments of an SF{seg_per_gpu * world} table; "
                                   f"C5 runs over all of them)" if want_c5 else ""),
                    "layout": f"{layouts[0]}" + (" by LO_ORDERDATE (SURVEY.md §8d C2)" if layouts[0] == "sorted" else ""),
-                   "rows_per_gpu": head["rows_per_rank"], "parallelism": f"segment-sharded x{world}, RCCL all-reduce"},
+                   "rows_per_gpu": head["rows_per_rank"],
+                   "parallelism": (f"segment-sharded x{world}, partial tables all-reduced over "
+                                   f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}") if world > 1
+                   else "one GPU (no collective)"},
         "p50_latency_ms": {q: round(float(np.median(head["lat"][q])), 3) for q in queries},
         "roofline": head["roofline"],
         "load_s": round(head["load_s"], 1),
@@ -584,7 +640,7 @@ def main():
         out["concurrent_clients"] = head["concurrent"]
     if not args.no_parity:
         ok = all(results[l]["parity"][0] for l in layouts) and all(head[g].get("parity") == "checked" for g in gb_legs) \
-            and head.get("c5", {}).get("parity", "checked") == "checked"
+            and head.get("c5_merged", {}).get("parity", "checked") == "checked"
         out["parity"] = "checked" if ok else "MISMATCH"
         out["parity_detail"] = {
             "against": "oracle/cpu_scan.c on the same segments, every rank, outside the timed region: exact int64 "
@@ -594,8 +650,8 @@ def main():
             **{l: results[l]["parity"][1] for l in layouts}}
     for g in gb_legs:
         out[g] = head[g]
-    if "c5" in head:
-        out["c5_merged" if "c5" in gb_legs else "c5"] = head["c5"]
+    if "c5_merged" in head:  # the C5 query over every rank's segments, merged across ranks (N > 1 / --c5 on)
+        out["c5_merged"] = head["c5_merged"]
     if len(layouts) > 1:
         r = results[layouts[1]]
         v2, ms2 = summary(r)

@@ -24,6 +24,51 @@ import numpy as np
 from . import lib as _oracle_lib
 
 _BE = {0: ">i4", 1: ">i8", 2: ">f4", 3: ">f8"}
+
+
+class _JavaRealKey(float):
+    """A FLOAT / DOUBLE group key -0.0 or NaN, equal and hashed as Java's Double.equals / doubleToLongBits keys it
+    (NoDictionarySingleColumnGroupKeyGenerator's Double2IntOpenHashMap / Float2IntOpenHashMap compare the bits: -0.0
+    and 0.0 are two groups, every NaN one). The oracle's own restatement (same equality and hash as the product's
+    results.JavaDoubleKey, so the two sides' dictionaries compare)."""
+    __slots__ = ()
+
+    def __eq__(self, o):
+        if not isinstance(o, float):
+            return NotImplemented
+        x = float(o)
+        if float(self) != float(self):
+            return x != x
+        return x == 0.0 and bool(np.signbit(x))
+
+    def __ne__(self, o):
+        r = self.__eq__(o)
+        return r if r is NotImplemented else not r
+
+    def __hash__(self):
+        return hash(0x7FF8000000000000) if float(self) != float(self) else hash(-0x8000000000000000)
+
+    def __reduce__(self):
+        return (_JavaRealKey, (float(self),))
+
+
+def _jkey(x):
+    if isinstance(x, float) and (x != x or (x == 0.0 and np.signbit(x))):
+        return _JavaRealKey(x)
+    return x
+
+
+def _unique_keys(vals):
+    """np.unique(vals, return_inverse=True) with Java's key equality for reals: by the bits (doubleToLongBits: NaN
+    canonical), so -0.0 and 0.0 stay two key values (np.unique on floats would merge them)."""
+    vals = np.asarray(vals)
+    if vals.dtype.kind != "f":
+        return np.unique(vals, return_inverse=True)
+    v = vals.astype(np.float64)
+    b = v.view(np.int64).copy()
+    b[np.isnan(v)] = 0x7FF8000000000000
+    ub, inv = np.unique(b, return_inverse=True)
+    return ub.view(np.float64), inv
 _NATIVE = {0: np.int64, 1: np.int64, 2: np.float64, 3: np.float64}
 MAX_DOC_PER_CALL = 10_000
 
@@ -541,12 +586,12 @@ def _group_segment(os_, query, docs, num_groups_limit, null_handling=False):
         vals = os_.values(e.name)[docs]
         nul = os_.nulls(e.name)[docs] if null_handling and os_.has_nulls(e.name) else None
         if nul is not None and nul.any():
-            u, inv_nn = np.unique(vals[~nul], return_inverse=True)
+            u, inv_nn = _unique_keys(vals[~nul])
             inv = np.full(len(docs), len(u), dtype=np.int64)   # the null key: one code past the values
             inv[~nul] = inv_nn
             u = list(u.tolist()) + [None]
         else:
-            u, inv = np.unique(vals, return_inverse=True)
+            u, inv = _unique_keys(vals)
         uniq_vals.append(u)
         codes += np.asarray(inv).astype(np.int64) * stride
         stride *= max(len(u), 1)
@@ -565,7 +610,7 @@ def _group_segment(os_, query, docs, num_groups_limit, null_handling=False):
     for code in key_codes.tolist():
         k = []
         for u in uniq_vals:
-            k.append(u[code % len(u)].item() if hasattr(u[code % len(u)], "item") else u[code % len(u)])
+            k.append(_jkey(u[code % len(u)].item() if hasattr(u[code % len(u)], "item") else u[code % len(u)]))
             code //= len(u)
         keys.append(tuple(k))
     per_agg, per_exact = [], []
@@ -951,12 +996,12 @@ def _execute_filtered_group_by(query, segments, num_groups_limit, null_handling=
             vals = os_.values(e.name)[alldocs]
             nul = os_.nulls(e.name)[alldocs] if null_handling and os_.has_nulls(e.name) else None
             if nul is not None and nul.any():
-                u, inv_nn = np.unique(vals[~nul], return_inverse=True)
+                u, inv_nn = _unique_keys(vals[~nul])
                 inv = np.full(len(alldocs), len(u), dtype=np.int64)   # the null key: one code past the values
                 inv[~nul] = inv_nn
                 u = list(u.tolist()) + [None]
             else:
-                u, inv = np.unique(vals, return_inverse=True)
+                u, inv = _unique_keys(vals)
             uniq_vals.append(u)
             codes += np.asarray(inv).astype(np.int64) * stride
             stride *= max(len(u), 1)
@@ -971,7 +1016,7 @@ def _execute_filtered_group_by(query, segments, num_groups_limit, null_handling=
         for code in ukeys[order[:ng]].tolist():
             k = []
             for u in uniq_vals:
-                k.append(u[code % len(u)].item() if hasattr(u[code % len(u)], "item") else u[code % len(u)])
+                k.append(_jkey(u[code % len(u)].item() if hasattr(u[code % len(u)], "item") else u[code % len(u)]))
                 code //= len(u)
             keys.append(tuple(k))
         per_agg = [None] * na

@@ -335,6 +335,7 @@ struct Lane {
 struct Device {
   int ordinal = 0;
   int num_cus = 256;
+  int num_xcc = 8;  // XCDs (L2 domains) of this device: the GB_XCD copies need at most kXcdCopies of them
   hipStream_t stream = nullptr;  // setup stream: segment load, plan preparation (under mu)
   hipEvent_t ev[4] = {};
   std::mutex mu;                 // guards setup work and the remap cache
@@ -442,6 +443,18 @@ static std::atomic<uint64_t> g_next_handle{1};
 
 static void init_lanes(Device *d);
 
+// XCDs of a device (hipDeviceAttributeNumberOfXccs; 8 on an MI355X in SPX mode, 1 per device in CPX). The fused
+// group-by's GB_XCD mode picks a table copy by HW_REG_XCC_ID & 7 and updates it with workgroup-scope atomics in that
+// XCD's L2, correct only while no two L2 domains of the device share a copy: with at most kXcdCopies XCDs the ids
+// are distinct mod 8 (a partition's XCC ids are a contiguous run). A device reporting more XCDs, or no count at all,
+// keeps the one agent-scope table (prepare_plan).
+static hipError_t device_xcc_count(int ordinal, int *out) {
+  int x = 0;
+  if (hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, ordinal) != hipSuccess || x <= 0) x = 1 << 30;
+  *out = x;
+  return hipSuccess;
+}
+
 static int32_t ensure_devices_locked() {
   if (!g_devices.empty()) return PHIP_OK;
   int n = 0;
@@ -452,6 +465,7 @@ static int32_t ensure_devices_locked() {
   d->ordinal = cur;
   HIP_TRY(hipSetDevice(cur));
   HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, cur));
+  HIP_TRY(device_xcc_count(cur, &d->num_xcc));
   HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
   init_lanes(d.get());
@@ -3330,7 +3344,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       for (int s2 = 0; s2 < nseg; s2++)
         sorted_key |= !segs[s2]->cols[colidx[s2][q->group_by_columns[k]]].sorted_pairs.empty();
     fused_gb = fgm == 2 || fgm == 3 || (fgm == 1 && (!lds_sized || (per_key <= kFuseGbMaxPerKey && !sorted_key)));
-    gb_xcd = fused_gb && fgm != 2 && table_bytes <= xcd_max && (fgm == 3 || per_key >= 1.0);
+    gb_xcd = fused_gb && fgm != 2 && table_bytes <= xcd_max && (fgm == 3 || per_key >= 1.0) &&
+             dev->num_xcc <= kXcdCopies;  // (XCC ids distinct mod kXcdCopies: device_xcc_count)
     if (fgm == 4 && lds_sized) {
       // (u64 rows, then the HLL registers packed four u8 to a u32 word: nhll x G x m bytes)
       const int64_t lb = round_up((int64_t)(1 + naggs) * dq.num_groups * 8 + (int64_t)nhll * dq.num_groups * m, 16);
@@ -5001,6 +5016,7 @@ PHIP_API int32_t phip_init(const int32_t *devices, int32_t num_devices) {
     d->ordinal = devices[i];
     HIP_TRY(hipSetDevice(d->ordinal));
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, d->ordinal));
+    HIP_TRY(device_xcc_count(d->ordinal, &d->num_xcc));
     HIP_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     for (auto &e : d->ev) HIP_TRY(hipEventCreate(&e));
     init_lanes(d.get());

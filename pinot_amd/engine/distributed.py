@@ -22,7 +22,8 @@ from typing import List, Optional
 
 import numpy as np
 
-from .results import AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock, merge_intermediate
+from .results import (AggregationResultsBlock, ExecutionStatistics, GroupByResultsBlock, java_double_key,
+                      merge_intermediate)
 
 _HLL_FUNCS = ("distinctcounthll", "distinctcountrawhll")
 
@@ -77,7 +78,7 @@ def _f64_from_key(k: int) -> float:
 class _Layout:
     """Where each function's intermediate lives in the SUM (float64) and MAX (int64) parts of a row."""
 
-    def __init__(self, aggregations, hll_m):
+    def __init__(self, aggregations):
         self.plan = []
         self.nsum = 0
         self.nmax = 0
@@ -96,7 +97,7 @@ class _Layout:
             elif f == "minmaxrange":
                 self.plan.append(("range", self._m(1), self._m(1)))
             elif f in _HLL_FUNCS:
-                m = hll_m or (1 << a.log2m)
+                m = 1 << a.log2m  # each function's own width (DISTINCTCOUNTHLL log2m may differ per function)
                 self.plan.append(("hll", self._m(m), m))
             else:
                 raise NotImplementedError(f)
@@ -149,6 +150,8 @@ class _Layout:
                 mv[p[2]] = _f64_key(float(v[1]))
             else:
                 r = np.asarray(v, dtype=np.int64)
+                if len(r) != p[2]:
+                    raise ValueError(f"HLL intermediate of {len(r)} registers where log2m gives {p[2]}")
                 mv[p[1]:p[1] + p[2]] = r
 
     def empty_max(self, rows):
@@ -204,11 +207,13 @@ def _sum_max(dist, group, sv: np.ndarray, mv: np.ndarray):
     return out[:ns].reshape(sv.shape), out[ns:].view(np.int64).reshape(mv.shape)
 
 
-def _hll_width(aggregations, rows):
-    for i, a in enumerate(aggregations):
-        if a.function in _HLL_FUNCS:
-            return len(rows[0][i]) if rows else 1 << a.log2m
-    return 0
+def _key_order(v):
+    """A total order of one column's key values for the node-global dictionaries: None (null) last, NaN before it,
+    -0.0 beside 0.0 (two keys: results.JavaDoubleKey)."""
+    if not isinstance(v, float):
+        return (v is None, False, 0 if v is None else v, False)
+    x = float(v)  # (plain float comparisons, whatever the wrapper's equality)
+    return (False, x != x, 0.0 if x != x else x, x == 0.0 and not np.signbit(x))
 
 
 def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 22):
@@ -225,7 +230,7 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
         return block
     aggs = block.aggregations
     if isinstance(block, AggregationResultsBlock):
-        lay = _Layout(aggs, _hll_width(aggs, [block.results]))
+        lay = _Layout(aggs)
         sv = np.zeros(6 + lay.nsum)
         mv = lay.empty_max(1)[0]
         sv[:6] = _stats_vector(block.stats)
@@ -251,11 +256,10 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
         merged = _merge_records_columnar(block, dist, group)
         if merged is not None:
             return merged
-    local_vals = [sorted(x, key=lambda v: (v is None, v)) for x in local_sets]
+    local_vals = [sorted(x, key=_key_order) for x in local_sets]
     gathered = [None] * world
-    dist.all_gather_object(gathered, (local_vals, _hll_width(aggs, list(block.groups.values()))), group=group)
-    gdict = [sorted(set().union(*[g[0][c] for g in gathered]), key=lambda v: (v is None, v)) for c in range(nk)]
-    hll_m = max(g[1] for g in gathered)
+    dist.all_gather_object(gathered, local_vals, group=group)
+    gdict = [sorted(set().union(*[g[c] for g in gathered]), key=_key_order) for c in range(nk)]
     cards = [max(len(d), 1) for d in gdict]
     ndense = int(np.prod(cards, dtype=np.int64)) if nk else 1
     if ndense > max_dense_groups:
@@ -273,27 +277,35 @@ def allreduce_block(block, dist=None, group=None, max_dense_groups: int = 1 << 2
         return out
     index = [{v: i for i, v in enumerate(d)} for d in gdict]
     strides = np.cumprod([1] + cards[:-1]).astype(np.int64)
-    lay = _Layout(aggs, hll_m)
-    # SUM rows: [stats | presence count | row SUM parts]; MAX: [limit flag | row MAX parts]
+    lay = _Layout(aggs)
+    na = len(aggs)
+    # SUM rows: [stats | presence count | row SUM parts]; MAX: [limit flag | row MAX parts | per-function presence]
+    # (a null intermediate -- enableNullHandling, nothing non-null aggregated into that group -- contributes the
+    # function's identity and presence 0; the merged group's function is null when no rank had a value)
+    w = lay.nmax + na
     sv = np.zeros(6 + ndense * (1 + lay.nsum))
-    mv = np.concatenate([np.array([int(block.num_groups_limit_reached)], np.int64), lay.empty_max(ndense).ravel()])
+    mrows = np.zeros((ndense, w), np.int64)
+    mrows[:, :lay.nmax] = lay.empty_max(ndense)
     sv[:6] = _stats_vector(block.stats)
     srows = sv[6:].reshape(ndense, 1 + lay.nsum)
-    mrows = mv[1:].reshape(ndense, lay.nmax)
+    ident = lay.get(np.zeros(lay.nsum), lay.empty_max(1)[0])
     for k, v in block.groups.items():
         d = int(sum(index[c][k[c]] * strides[c] for c in range(nk)))
         srows[d, 0] = 1.0
-        lay.put(srows[d, 1:], mrows[d], v)
+        lay.put(srows[d, 1:], mrows[d, :lay.nmax], [ident[i] if x is None else x for i, x in enumerate(v)])
+        mrows[d, lay.nmax:] = [x is not None for x in v]
+    mv = np.concatenate([np.array([int(block.num_groups_limit_reached)], np.int64), mrows.ravel()])
     sv, mv = _sum_max(dist, group, sv, mv)
     srows = sv[6:].reshape(ndense, 1 + lay.nsum)
-    mrows = mv[1:].reshape(ndense, lay.nmax)
+    mrows = mv[1:].reshape(ndense, w)
     groups = {}
     for d in np.nonzero(srows[:, 0])[0]:
         key, rem = [], int(d)
         for c in range(nk):
             key.append(gdict[c][rem % cards[c]])
             rem //= cards[c]
-        groups[tuple(key)] = lay.get(srows[d, 1:], mrows[d])
+        vals = lay.get(srows[d, 1:], mrows[d, :lay.nmax])
+        groups[tuple(key)] = [x if mrows[d, lay.nmax + i] else None for i, x in enumerate(vals)]
     out = GroupByResultsBlock(aggs, block.group_by, groups, _stats_from(sv[:6]), bool(mv[0]))
     out.key_types = getattr(block, "key_types", None)
     return out
@@ -333,8 +345,9 @@ def _merge_records_columnar(block, dist, group):
         K[:, nk + c] = [v is None for v in col]
         if floats[c]:
             x = np.array([0.0 if v is None else float(v) for v in col], dtype=np.float64)
-            x[x == 0] = 0.0  # (-0.0 keys the same group as 0.0, as the value-keyed dict of the object merge does)
-            K[:, c] = x.view(np.int64)
+            b = x.view(np.int64).copy()  # keyed by the bits, as the reference (doubleToLongBits): -0.0 and 0.0
+            b[np.isnan(x)] = 0x7FF8000000000000  # two groups, every NaN one (results.JavaDoubleKey)
+            K[:, c] = b
         else:
             K[:, c] = [0 if v is None else int(v) for v in col]
     # value columns: (kind, agg, part) with kind I (int64) / F (double bits) / P (presence)
@@ -418,7 +431,7 @@ def _merge_records_columnar(block, dist, group):
             if uniq[g, nk + c]:
                 key.append(None)
             elif floats[c]:
-                key.append(float(np.int64(uniq[g, c]).view(np.float64)))
+                key.append(java_double_key(float(np.int64(uniq[g, c]).view(np.float64))))
             else:
                 key.append(int(uniq[g, c]))
         row = []

@@ -9,10 +9,58 @@ Intermediate results follow each function's intermediate type:
   count -> int, sum -> float (int when every input is INT/LONG: exact), min/max ->
   float, avg -> (sum, count), minmaxrange -> (min, max), distinctcounthll -> uint8 registers.
 """
+import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
+
+
+class JavaDoubleKey(float):
+    """A FLOAT / DOUBLE group-key value that Python's float equality would merge with another: -0.0 (== 0.0 in
+    Python) and NaN (!= itself). The reference keys raw real group values by their bits (Double2IntOpenHashMap /
+    Float2IntOpenHashMap hash and compare doubleToLongBits / floatToIntBits, the Key's Double.equals in the
+    IndexedTable), so -0.0 and 0.0 are two groups and every NaN is one; so do the device tables (keys.hip) and so
+    does this wrapper: equal only to a -0.0 (resp. a NaN), hashed by the bits. Every other key stays a plain float."""
+    __slots__ = ()
+
+    def __eq__(self, o):
+        if not isinstance(o, float):
+            return NotImplemented
+        x = float(o)  # (plain float comparisons: o may be a JavaDoubleKey too)
+        if math.isnan(self):
+            return math.isnan(x)
+        return x == 0.0 and math.copysign(1.0, x) < 0
+
+    def __ne__(self, o):
+        r = self.__eq__(o)
+        return r if r is NotImplemented else not r
+
+    def __hash__(self):
+        return hash(0x7FF8000000000000) if math.isnan(self) else hash(-0x8000000000000000)
+
+    def __reduce__(self):
+        return (JavaDoubleKey, (float(self),))
+
+
+def java_double_key(x):
+    """x as a group-key value with Java's Double.equals semantics (JavaDoubleKey for -0.0 and NaN)."""
+    if isinstance(x, float) and (x != x or (x == 0.0 and math.copysign(1.0, x) < 0)):
+        return JavaDoubleKey(x)
+    return x
+
+
+def key_column_list(col, key_type=None):
+    """A key column (numpy array) as a list of group-key values: real columns (a float array, or an object array
+    of floats and None null keys when `key_type` is FLOAT / DOUBLE) wrap their -0.0 / NaN entries."""
+    out = col.tolist() if isinstance(col, np.ndarray) else list(col)
+    if isinstance(col, np.ndarray) and col.dtype.kind == "f":
+        odd = np.nonzero(np.isnan(col) | ((col == 0) & np.signbit(col)))[0]
+        for i in odd.tolist():
+            out[i] = JavaDoubleKey(out[i])
+    elif key_type in ("FLOAT", "DOUBLE"):
+        out = [java_double_key(v) for v in out]
+    return out
 
 
 @dataclass
@@ -73,7 +121,8 @@ class GroupByResultsBlock:
         prim = [[row.copy() for row in c] if c.ndim == 2 else c.tolist() for c in self.prim_columns]
         fcols = [list(zip(prim[sl[0]], prim[sl[1]])) if fn in ("avg", "minmaxrange") else prim[sl]
                  for fn, sl in self._mapping]
-        cols = [c.tolist() for c in self.key_columns]
+        kt = self.__dict__.get("key_types") or [None] * len(self.key_columns)
+        cols = [key_column_list(c, t) for c, t in zip(self.key_columns, kt)]
         n = self.num_groups
         gkeys = list(zip(*cols)) if cols else [()] * n
         g = dict(zip(gkeys, map(list, zip(*fcols)))) if fcols else {k: [] for k in gkeys}

@@ -33,7 +33,7 @@ def raw_segments(gpu_lib):
     rng = np.random.default_rng(31)
     raws = []
     for s, n in enumerate((20_000, 33_333, 4097)):
-        c = SegmentCreator(f"raw{s}", no_dictionary_columns=["ri", "rl", "rf", "rd", "rm", "rs"])
+        c = SegmentCreator(f"raw{s}", no_dictionary_columns=["ri", "rl", "rf", "rd", "rm", "rs", "rz"])
         c.add_column("ri", DataType.INT, rng.integers(-50 + 7 * s, 60 + 3 * s, n).astype(np.int32))
         c.add_column("rl", DataType.LONG, rng.integers(-3_000_000_000, -2_999_990_000, n) + 1_000_000 * s)
         # (+ 0.0: no -0.0 -- the reference keys it apart from 0.0 by its bits, Double2IntOpenHashMap, and so does the
@@ -41,6 +41,9 @@ def raw_segments(gpu_lib):
         c.add_column("rf", DataType.FLOAT, (np.round(rng.normal(0, 5, n), 1) + 0.0).astype(np.float32))
         c.add_column("rd", DataType.DOUBLE, np.round(rng.normal(0, 50, n), 2) + 0.0)
         c.add_column("rm", DataType.LONG, rng.integers(-10 ** 9, 10 ** 9, n))
+        # -0.0 and 0.0 (and values around them): two keys by their bits on the device, in the oracle and in the
+        # block's {key: intermediates} view (results.JavaDoubleKey)
+        c.add_column("rz", DataType.DOUBLE, np.array([-0.0, 0.0, 0.5, -0.25, 3.0])[rng.integers(0, 5 - (s == 2), n)])
         c.add_column("dk", DataType.STRING, np.array([f"k{x}" for x in rng.integers(0, 9 + s, n)]))
         c.add_column("f", DataType.INT, rng.integers(0, 100, n))
         # raw STRING: lengths 0-14 (every murmur tail), multi-byte UTF-8, values shared across segments or not
@@ -65,6 +68,8 @@ RAW_GROUP_BY = [
     "SELECT rd, dk, COUNT(*), MIN(ri), DISTINCTCOUNTHLL(rf) FROM t WHERE f < 50 GROUP BY rd, dk LIMIT 100000",
     "SELECT rf, rd, COUNT(*) FROM t WHERE f < 20 GROUP BY rf, rd ORDER BY rf DESC, rd LIMIT 9",  # key-order trim
     "SELECT rf, SUM(rd), MAX(rf) FROM t WHERE rf > 1.5 GROUP BY rf LIMIT 100000",  # key column also filtered / aggregated
+    "SELECT rz, COUNT(*), SUM(rm) FROM t GROUP BY rz LIMIT 100000",  # -0.0 and 0.0: two groups
+    "SELECT dk, rz, COUNT(*), MIN(rd) FROM t WHERE f < 70 GROUP BY dk, rz LIMIT 100000",
     # raw STRING keys (distinct strings over the segments sorted bytewise, a doc-order id column each)
     "SELECT rs, COUNT(*), SUM(rm) FROM t GROUP BY rs LIMIT 100000",
     "SELECT rs, dk, ri, COUNT(*), DISTINCTCOUNTHLL(rs) FROM t WHERE f < 50 GROUP BY rs, dk, ri LIMIT 100000",
@@ -88,6 +93,10 @@ def test_gpu_group_by_raw_columns(sql, mode, raw_segments, monkeypatch):
         oblk = trim_groups(qc, oblk)
     _check(qc, gblk, oblk, exact)
     assert gblk.key_types == oblk.key_types
+    if " rz," in sql:
+        z = [e.name for e in qc.group_by].index("rz")
+        zeros = {bool(np.signbit(k[z])) for k in gblk.groups if float(k[z]) == 0.0}
+        assert zeros == {True, False}, "-0.0 and 0.0 must be two groups"
     got, want = reduce_blocks(qc, [gblk]).rows, reduce_blocks(qc, [oblk]).rows
     if not qc.order_by:
         got, want = sorted(got), sorted(want)

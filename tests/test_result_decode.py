@@ -86,3 +86,40 @@ def test_dictionary_lookup_strings_and_numbers():
     dbl = (ctypes.c_double * 2)(1.5, -0.25)
     dv = _lib.DictionaryView(int(DataType.DOUBLE), 2, 0, 0, ctypes.addressof(dbl))
     assert _dictionary_lookup(dv, [1, 0]) == [-0.25, 1.5]
+
+
+def test_columnar_block_real_keys_by_bits():
+    """The {key: intermediates} view of a columnar group-by block keeps raw DOUBLE keys -0.0 and 0.0 as two groups
+    (the device keys reals by their bits, as the reference's Double2IntOpenHashMap does) and NaN as one; a plain
+    dict over Python floats would merge -0.0 into 0.0 and overwrite that group's values."""
+    import numpy as np
+
+    from pinot_amd.engine.results import GroupByResultsBlock, JavaDoubleKey
+    qc = parse("SELECT z, COUNT(*) FROM t GROUP BY z")
+    blk = GroupByResultsBlock(qc.aggregations, list(qc.group_by), None)
+    blk.key_types = ["DOUBLE"]
+    keys = np.array([0.0, -0.0, 1.5, np.nan], dtype=np.float64)
+    blk.set_columns([keys], [np.array([3, 5, 7, 11], np.int64)], [("count", 0)])
+    g = blk.groups
+    assert len(g) == 4
+    assert g[(0.0,)] == [3] and g[(JavaDoubleKey(-0.0),)] == [5] and g[(1.5,)] == [7]
+    assert g[(JavaDoubleKey(float("nan")),)] == [11]
+    # object key columns (null keys beside reals) wrap the same way
+    blk2 = GroupByResultsBlock(qc.aggregations, list(qc.group_by), None)
+    blk2.key_types = ["DOUBLE"]
+    blk2.set_columns([np.array([-0.0, None, 0.0], dtype=object)], [np.array([1, 2, 3], np.int64)], [("count", 0)])
+    assert len(blk2.groups) == 3 and blk2.groups[(JavaDoubleKey(-0.0),)] == [1] and blk2.groups[(None,)] == [2]
+
+
+def test_oracle_real_keys_by_bits():
+    """The oracle keys raw DOUBLE group values by their bits too: -0.0 and 0.0 two groups with their own counts."""
+    import numpy as np
+
+    from oracle import executor
+    from pinot_amd.segment.creator import SegmentCreator
+    from pinot_amd.spi import DataType
+    c = SegmentCreator("z", no_dictionary_columns=["z"])
+    c.add_column("z", DataType.DOUBLE, np.array([-0.0, 0.0, 0.0, -0.0, -0.0, 2.5]))
+    blk, _ = executor.execute(parse("SELECT z, COUNT(*) FROM t GROUP BY z"), [c.build()])
+    got = {(float(k[0]), bool(np.signbit(k[0]))): v[0] for k, v in blk.groups.items()}
+    assert got == {(0.0, True): 3, (0.0, False): 2, (2.5, False): 1}

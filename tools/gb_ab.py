@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layout", default="unsorted")
+    ap.add_argument("--gap", type=float, default=0.0,
+                    help="seconds of idle GPU before each (query, setting): tools/trace_summary.py splits a rocprofv3 "
+                         "kernel trace of this run into the queries at these gaps")
     args = ap.parse_args()
     sets = args.set if args.set is not None else [""]
     from pinot_amd import _lib
@@ -68,6 +71,8 @@ def main():
                 k, v = kv.split("=", 1)
                 os.environ[k] = v
             op = GpuInstancePlanMaker().make_instance_plan(qc, gsegs)
+            if args.gap:
+                time.sleep(args.gap)
             wall, fk, ak = [], [], []
             blk = None
             for i in range(args.warmup + args.reps):
