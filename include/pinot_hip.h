@@ -444,4 +444,41 @@ PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phi
  * partial is pending, phip_plan_execute / phip_plan_execute_partial on the plan return PHIP_ERR_INVALID. */
 PHIP_API int32_t phip_plan_abandon_partial(uint64_t plan);
 
+/* ---- multi-GPU servers in ONE process: node plans ------------------------------------------------------
+ * A Pinot server is one JVM that owns every GPU of its node: BaseCombineOperator fans a query's segments out over
+ * worker threads (pinot-core/.../operator/combine/BaseCombineOperator.java:98-143) and merges their blocks in that
+ * process (BaseSingleBlockCombineOperator.java:129-162, GroupByCombineOperator.java:138-147). phip_plan_create /
+ * phip_query over segments loaded on SEVERAL devices (phip_segment_desc.device) returns a node plan -- no other call
+ * changes, so the Java binding needs nothing beyond this header:
+ *   - each device's segments form one single-device sub-plan; the group-by columns of every sub-plan are keyed by the
+ *     node plan's own node-global dictionaries (the sorted union of the column's values over all its segments, built
+ *     at plan creation -- no phip_global_dictionary registration needed), so the devices' dense partial tables have
+ *     the same shape and key order;
+ *   - phip_plan_execute runs the sub-plans concurrently, one host thread and one execution lane per device, up to
+ *     their dense partial tables (phip_plan_execute_partial's), then merges them ON THE DEVICES: one RCCL reduce to
+ *     the root device (the first device in query order) over the node's communicator (ncclCommInitAll over the
+ *     node plan's devices, created once per device set, librccl loaded on first use; xGMI peer-to-peer) -- int64 SUM
+ *     for counts and exact sums, f64 SUM, unsigned MIN / MAX of the order-preserving images, MAX of the HLL registers
+ *     -- and finishes the merged table on the root (compaction, server trim, copy-out) exactly as phip_plan_finish;
+ *   - where the devices cannot share a communicator (two parts on one device, no loadable librccl) the non-root
+ *     tables are copied to the root device (hipMemcpyPeerAsync) and folded in by the library's merge kernel, the same
+ *     operators;
+ *   - aggregation-only queries (one group) and group-bys without a dense partial table (hash-table key spaces, a
+ *     device reaching numGroupsLimit -- the per-segment first-seen limit --, raw group-by keys, tuple keys) run each
+ *     sub-plan to its records and merge them on the host by key VALUE, as the reference's combine does (untrimmed:
+ *     the broker's ORDER BY / LIMIT applies to exact groups).
+ * Statistics are summed over the devices; segment_docs_matched covers every segment in query order; kernel times
+ * are the slowest device's. Selection queries over several devices return PHIP_ERR_UNSUPPORTED. The deadline and
+ * cancel calls apply to every sub-plan. phip_plan_execute_partial / phip_plan_finish / phip_plan_abandon_partial on
+ * a node plan return PHIP_ERR_INVALID (it merges internally).
+ * PHIP_NODE_SPLIT=k (environment, read at plan creation) splits a query whose segments share one device into k parts
+ * on that device -- a rehearsal of the node path on a one-GPU box (the peer-merge exchange; k = 1: one part and a
+ * one-rank RCCL communicator). PHIP_NODE_EXCHANGE=peer forces the merge kernel, =rccl refuses the fallback. */
+#define PHIP_EXCHANGE_NONE 0    /* a single-device plan */
+#define PHIP_EXCHANGE_RCCL 1    /* the last execution reduced the partial tables with RCCL */
+#define PHIP_EXCHANGE_PEER 2    /* ... copied them to the root device and merged them with the merge kernel */
+#define PHIP_EXCHANGE_RECORDS 3 /* ... merged the sub-plans' records on the host */
+/* Devices (sub-plans) of a plan and the exchange its last execution used (PHIP_EXCHANGE_*; NONE before the first). */
+PHIP_API int32_t phip_plan_exchange(uint64_t plan, int32_t *out_parts, int32_t *out_kind);
+
 #endif /* PINOT_HIP_H_ */

@@ -40,8 +40,14 @@ EXPORTED_SYMBOLS = (
     "phip_result_dictionary", "phip_result_free", "phip_filter_bitmap", "phip_plan_create", "phip_plan_execute",
     "phip_plan_destroy", "phip_global_dictionary", "phip_plan_execute_partial", "phip_plan_finish",
     "phip_runtime_versions", "phip_plan_abandon_partial", "phip_result_select_dictionary",
-    "phip_plan_set_deadline", "phip_plan_cancel",
+    "phip_plan_set_deadline", "phip_plan_cancel", "phip_plan_exchange",
 )
+
+# phip_plan_exchange kinds (include/pinot_hip.h "node plans")
+EXCHANGE_NONE = 0
+EXCHANGE_RCCL = 1
+EXCHANGE_PEER = 2
+EXCHANGE_RECORDS = 3
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 
@@ -234,6 +240,8 @@ def load(with_torch: bool = False):
     lib.phip_plan_execute.restype = i32
     lib.phip_plan_destroy.argtypes = [u64]
     lib.phip_plan_destroy.restype = i32
+    lib.phip_plan_exchange.argtypes = [u64, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    lib.phip_plan_exchange.restype = i32
     lib.phip_global_dictionary.argtypes = [i32, ctypes.c_char_p, i32, i32, i32, ctypes.c_void_p]
     lib.phip_global_dictionary.restype = i32
     lib.phip_plan_execute_partial.argtypes = [u64, ctypes.POINTER(Partial)]

@@ -28,6 +28,7 @@
 
 #include "../../include/pinot_hip.h"
 #include "device.h"
+#include "node.h"
 
 namespace phip {
 hipError_t launch_bswap32(uint32_t *p, int64_t n, hipStream_t s);
@@ -1569,13 +1570,28 @@ static int32_t build_tuple_keys(Device &dev, const std::vector<Segment *> &segs,
 // sorted union of the segments' dictionaries. Per segment a dict-id -> global-id map in HBM (nullptr when
 // the segment's dictionary IS the global one).
 // (skip_nulls: a null-key column -- a raw column's id range then covers its non-null values only)
+// The node plan being prepared on this thread (node_plan_create): its group-by columns' node-global dictionaries.
+static thread_local const NodeDicts *tl_node_dicts = nullptr;
+
 int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
                     const std::string &name, std::shared_ptr<Device::Remap> &out, bool skip_nulls = false) {
   auto git = dev.globals.find(name);
   const Device::GlobalDict *gd = git == dev.globals.end() ? nullptr : &git->second;
+  // a node plan's part (node_plan_create): the column keyed by the node plan's own union dictionary
+  Device::GlobalDict node_gd;
+  const bool node = tl_node_dicts != nullptr && tl_node_dicts->count(name) > 0;
+  if (node) {
+    const NodeDict &nd = tl_node_dicts->at(name);
+    node_gd.type = nd.type;
+    node_gd.card = nd.card;
+    node_gd.width = nd.width;
+    node_gd.gen = nd.gen;
+    node_gd.values = nd.values;
+    gd = &node_gd;
+  }
   std::string key = name;
   if (skip_nulls) key += "#nn";
-  if (gd) key += "@g" + std::to_string(gd->gen);
+  if (gd) key += (node ? "@n" : "@g") + std::to_string(gd->gen);
   for (auto *s : segs) key += ":" + std::to_string(s->handle);
   auto it = dev.remaps.find(key);
   if (it != dev.remaps.end()) {
@@ -5029,6 +5045,7 @@ static std::unordered_map<uint64_t, std::unique_ptr<Plan>> g_plans;  // guarded 
 static std::atomic<uint64_t> g_next_plan{1};
 
 PHIP_API int32_t phip_shutdown(void) {
+  node_shutdown();  // (its sub-plans and communicators first)
   std::lock_guard<std::mutex> g(g_mu);
   g_plans.clear();
   g_segments.clear();
@@ -5123,14 +5140,30 @@ PHIP_API int32_t phip_segment_device_bytes(uint64_t handle, uint64_t *out_bytes)
 PHIP_API int32_t phip_query(const phip_query_desc *query, phip_result **out_result) {
   if (!out_result) return fail(PHIP_ERR_INVALID, "null result pointer");
   *out_result = nullptr;
+  if (query && node_wanted(query)) {  // segments on several devices: a node plan, run once
+    uint64_t h = 0;
+    int32_t rc = node_create(query, &h);
+    if (rc) return rc;
+    rc = node_execute(h, out_result);
+    (void)node_destroy(h);
+    return rc;
+  }
   Plan plan;
   int32_t rc = prepare_plan(query, false, 0, plan);
   if (rc) return rc;
   return execute_plan(plan, out_result, nullptr);
 }
 
+static int32_t create_single_plan(const phip_query_desc *query, uint64_t *out_plan);
+
 PHIP_API int32_t phip_plan_create(const phip_query_desc *query, uint64_t *out_plan) {
   if (!out_plan) return fail(PHIP_ERR_INVALID, "null plan pointer");
+  *out_plan = 0;
+  if (query && node_wanted(query)) return node_create(query, out_plan);
+  return create_single_plan(query, out_plan);
+}
+
+static int32_t create_single_plan(const phip_query_desc *query, uint64_t *out_plan) {
   *out_plan = 0;
   auto plan = std::make_unique<Plan>();
   int32_t rc = prepare_plan(query, false, 0, *plan);
@@ -5145,6 +5178,7 @@ PHIP_API int32_t phip_plan_create(const phip_query_desc *query, uint64_t *out_pl
 PHIP_API int32_t phip_plan_execute(uint64_t plan, phip_result **out_result) {
   if (!out_result) return fail(PHIP_ERR_INVALID, "null result pointer");
   *out_result = nullptr;
+  if (is_node_plan(plan)) return node_execute(plan, out_result);
   Plan *p;
   {
     std::lock_guard<std::mutex> g(g_mu);
@@ -5164,6 +5198,7 @@ static int32_t find_plan(uint64_t plan, Plan **out) {
 }
 
 PHIP_API int32_t phip_plan_set_deadline(uint64_t plan, int64_t deadline_ms) {
+  if (is_node_plan(plan)) return node_set_deadline(plan, deadline_ms);
   Plan *p;
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
@@ -5172,6 +5207,7 @@ PHIP_API int32_t phip_plan_set_deadline(uint64_t plan, int64_t deadline_ms) {
 }
 
 PHIP_API int32_t phip_plan_cancel(uint64_t plan) {
+  if (is_node_plan(plan)) return node_cancel(plan);
   Plan *p;
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
@@ -5181,6 +5217,7 @@ PHIP_API int32_t phip_plan_cancel(uint64_t plan) {
 
 PHIP_API int32_t phip_plan_execute_partial(uint64_t plan, phip_partial *out_partial) {
   if (!out_partial) return fail(PHIP_ERR_INVALID, "null partial pointer");
+  if (is_node_plan(plan)) return fail(PHIP_ERR_INVALID, "a node plan merges its devices' partials itself");
   Plan *p;
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
@@ -5191,6 +5228,7 @@ PHIP_API int32_t phip_plan_execute_partial(uint64_t plan, phip_partial *out_part
 PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phip_result **out_result) {
   if (!merged || !out_result) return fail(PHIP_ERR_INVALID, "null argument");
   *out_result = nullptr;
+  if (is_node_plan(plan)) return fail(PHIP_ERR_INVALID, "a node plan merges its devices' partials itself");
   Plan *p;
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
@@ -5199,6 +5237,7 @@ PHIP_API int32_t phip_plan_finish(uint64_t plan, const phip_partial *merged, phi
 }
 
 PHIP_API int32_t phip_plan_abandon_partial(uint64_t plan) {
+  if (is_node_plan(plan)) return fail(PHIP_ERR_INVALID, "a node plan merges its devices' partials itself");
   Plan *p;
   int32_t rc = find_plan(plan, &p);
   if (rc) return rc;
@@ -5247,7 +5286,19 @@ PHIP_API int32_t phip_global_dictionary(int32_t device, const char *column, int3
   return PHIP_OK;
 }
 
+PHIP_API int32_t phip_plan_exchange(uint64_t plan, int32_t *out_parts, int32_t *out_kind) {
+  if (!out_parts || !out_kind) return fail(PHIP_ERR_INVALID, "null argument");
+  if (is_node_plan(plan)) return node_exchange_info(plan, out_parts, out_kind);
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  *out_parts = 1;
+  *out_kind = PHIP_EXCHANGE_NONE;
+  return PHIP_OK;
+}
+
 PHIP_API int32_t phip_plan_destroy(uint64_t plan) {
+  if (is_node_plan(plan)) return node_destroy(plan);
   std::unique_ptr<Plan> p;
   {
     std::lock_guard<std::mutex> g(g_mu);
@@ -5319,3 +5370,177 @@ PHIP_API int32_t phip_filter_bitmap(const phip_query_desc *query, uint64_t *word
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Node plans (node.cpp): hooks over the single-device machinery above
+// ------------------------------------------------------------------------------------------------
+
+int32_t phip::node_fail(int32_t code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int32_t phip::node_segment_device(uint64_t handle, int *ordinal) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_segments.find(handle);
+  if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle %llu", (unsigned long long)handle);
+  *ordinal = it->second->device;
+  return PHIP_OK;
+}
+
+int32_t phip::node_union_dictionary(const std::vector<uint64_t> &handles, const std::string &column, NodeDict *out,
+                                    bool *ok) {
+  *ok = false;
+  std::vector<std::shared_ptr<Segment>> segs;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (uint64_t h : handles) {
+      auto it = g_segments.find(h);
+      if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle %llu", (unsigned long long)h);
+      segs.push_back(it->second);
+    }
+  }
+  int32_t type = -1, width = 0;
+  std::vector<const ColumnStore *> cols;
+  for (auto &sp : segs) {
+    auto ci = sp->by_name.find(column);
+    if (ci == sp->by_name.end()) return PHIP_OK;  // (prepare_plan reports the missing column)
+    const ColumnStore &c = sp->cols[ci->second];
+    if (no_dict(c) || (type >= 0 && c.type != type)) return PHIP_OK;  // raw keys / mixed types: the record path
+    type = c.type;
+    width = std::max(width, type == PHIP_TYPE_STRING ? c.string_width : type_width(type));
+    cols.push_back(&c);
+  }
+  if (type < 0) return PHIP_OK;
+  // every segment's values in the comparable form (LE numbers, '\0'-padded strings), sorted, distinct (build_remap's)
+  std::vector<uint8_t> all;
+  for (const ColumnStore *c : cols) {
+    const int sw = type == PHIP_TYPE_STRING ? c->string_width : width;
+    for (int32_t id = 0; id < c->card; id++) {
+      const size_t at = all.size();
+      all.resize(at + width, 0);
+      const uint8_t *p = c->host_dict.data() + (size_t)id * sw;
+      if (type == PHIP_TYPE_STRING) memcpy(all.data() + at, p, sw);
+      else
+        for (int b = 0; b < width; b++) all[at + b] = p[width - 1 - b];
+    }
+  }
+  const int64_t total = width ? (int64_t)(all.size() / width) : 0;
+  std::vector<int64_t> order(total);
+  for (int64_t i = 0; i < total; i++) order[i] = i;
+  const uint8_t *A = all.data();
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int64_t x, int64_t y) { return compare_value(type, A + x * width, A + y * width, width) < 0; });
+  out->values.clear();
+  int64_t n = 0;
+  for (int64_t k = 0; k < total; k++) {
+    const uint8_t *v = A + order[k] * width;
+    if (n > 0 && compare_value(type, out->values.data() + (n - 1) * width, v, width) == 0) continue;
+    out->values.insert(out->values.end(), v, v + width);
+    n++;
+  }
+  if (n > INT32_MAX) return PHIP_OK;
+  out->type = type;
+  out->card = (int32_t)n;
+  out->width = type == PHIP_TYPE_STRING ? width : 0;
+  *ok = true;
+  return PHIP_OK;
+}
+
+int32_t phip::node_plan_create(const phip_query_desc *q, const NodeDicts *dicts, uint64_t *out_plan) {
+  tl_node_dicts = dicts;
+  const int32_t rc = create_single_plan(q, out_plan);
+  tl_node_dicts = nullptr;
+  return rc;
+}
+
+int32_t phip::node_plan_docs(uint64_t plan, std::vector<int64_t> *seg_docs, std::vector<int64_t> *prog_docs) {
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  const int nseg = p->nseg;
+  const uint64_t *segm = p->pinned + 64;
+  seg_docs->assign(std::max(nseg, 1), 0);
+  prog_docs->assign(std::max(p->nprog, 1), 0);
+  for (int pr = 0; pr < p->nprog; pr++)
+    for (int s = 0; s < nseg; s++) {
+      const int64_t d = p->has_filter ? (int64_t)segm[pr * nseg + s] : p->slot_docs[pr * nseg + s];
+      (*seg_docs)[s] += d;
+      (*prog_docs)[pr] += d;
+    }
+  return PHIP_OK;
+}
+
+int32_t phip::node_make_result(NodeResultData &&d, phip_result **out) {
+  auto impl = std::make_unique<ResultImpl>();
+  phip_result &r = impl->pub;
+  memset(&r, 0, sizeof(r));
+  r.num_docs_scanned = d.stats[0];
+  r.num_entries_scanned_in_filter = d.stats[1];
+  r.num_entries_scanned_post_filter = d.stats[2];
+  r.num_total_docs = d.stats[3];
+  r.num_segments_processed = (int32_t)d.stats[4];
+  r.num_segments_matched = (int32_t)d.stats[5];
+  r.num_groups_limit_reached = d.limit_reached;
+  r.num_aggregations = d.naggs;
+  r.num_groups = d.ngroups;
+  r.num_group_by = d.ngb;
+  r.num_hll = d.nhll;
+  impl->values = std::move(d.values);
+  impl->longs = std::move(d.longs);
+  impl->exact = std::move(d.exact);
+  impl->hll = std::move(d.hll);
+  impl->keys = std::move(d.keys);
+  impl->seg_docs = std::move(d.seg_docs);
+  impl->prog_docs = std::move(d.prog_docs);
+  if (impl->values.empty()) impl->values.resize(1);
+  if (impl->longs.empty()) impl->longs.resize(1);
+  if (impl->exact.empty()) impl->exact.resize(1);
+  if (impl->seg_docs.empty()) impl->seg_docs.resize(1);
+  if (impl->prog_docs.empty()) impl->prog_docs.resize(1);
+  for (auto &nd : d.dicts) {
+    auto rm = std::make_shared<Device::Remap>();
+    rm->type = nd.type;
+    rm->card = nd.card;
+    rm->width = nd.width;
+    rm->values = std::move(nd.values);
+    impl->dicts.push_back(rm);
+  }
+  r.values = impl->values.data();
+  r.long_values = impl->longs.data();
+  r.long_exact = impl->exact.data();
+  r.hll_registers = impl->hll.data();
+  r.group_keys = impl->keys.data();
+  r.segment_docs_matched = impl->seg_docs.data();
+  r.program_docs_matched = impl->prog_docs.data();
+  r.scan_kernel_ms = d.scan_ms;
+  r.device_ms = d.device_ms;
+  r.filter_kernel_ms = d.filter_ms;
+  r.agg_kernel_ms = d.agg_ms;
+  r.filter_bytes = d.filter_bytes;
+  r.agg_bytes = d.agg_bytes;
+  r.stream_bytes = d.stream_bytes;
+  r.fused = d.fused;
+  *out = &impl.release()->pub;
+  return PHIP_OK;
+}
+
+void phip::node_result_set_docs(phip_result *res, std::vector<int64_t> seg_docs, std::vector<int64_t> prog_docs) {
+  ResultImpl *impl = reinterpret_cast<ResultImpl *>(res);
+  impl->seg_docs = std::move(seg_docs);
+  impl->prog_docs = std::move(prog_docs);
+  if (impl->seg_docs.empty()) impl->seg_docs.resize(1);
+  if (impl->prog_docs.empty()) impl->prog_docs.resize(1);
+  impl->pub.segment_docs_matched = impl->seg_docs.data();
+  impl->pub.program_docs_matched = impl->prog_docs.data();
+}
+
+int phip::node_compare_value(int32_t type, const uint8_t *a, const uint8_t *b, int width) {
+  return compare_value(type, a, b, width);
+}
+int phip::node_type_width(int32_t type) { return type_width(type); }

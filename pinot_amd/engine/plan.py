@@ -679,6 +679,16 @@ class GpuCombineOperator:
             _lib.check(lib.phip_plan_set_deadline(self._plan, d))
             self._deadline_set = d
 
+    def exchange(self):
+        """(devices, exchange kind) of the prepared plan (phip_plan_exchange): a plan over segments on several devices
+        is a node plan whose sub-plans' partials meet in an RCCL reduce (_lib.EXCHANGE_RCCL), a peer merge
+        (EXCHANGE_PEER) or the host record merge (EXCHANGE_RECORDS); (1, EXCHANGE_NONE) for one device."""
+        if getattr(self, "_plan", None) is None:
+            return 1, _lib.EXCHANGE_NONE
+        parts, kind = ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(_lib.load().phip_plan_exchange(self._plan, ctypes.byref(parts), ctypes.byref(kind)))
+        return parts.value, kind.value
+
     def close(self):
         """Release the prepared plan (and with it the last references to unloaded segments)."""
         if getattr(self, "_plan", None):

@@ -8,7 +8,12 @@
 #include <cstdint>
 
 extern "C" {
-hipError_t hipGetDeviceCount(int *n) { *n = 1; return hipSuccess; }
+hipError_t hipGetDeviceCount(int *n) {  // HOSTSIM_DEVICES: stand-in devices for the node-plan paths
+  const char *e = getenv("HOSTSIM_DEVICES");
+  *n = e ? atoi(e) : 1;
+  return hipSuccess;
+}
+hipError_t hipMemcpyPeerAsync(void *d, int, const void *s, int, size_t n, hipStream_t) { memmove(d, s, n); return hipSuccess; }
 hipError_t hipGetDevice(int *d) { *d = 0; return hipSuccess; }
 hipError_t hipSetDevice(int) { return hipSuccess; }
 hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t, int) { *v = 256; return hipSuccess; }
@@ -40,7 +45,43 @@ const char *hipGetErrorString(hipError_t) { return "stub"; }
 }
 
 #include "../../pinot_amd/csrc/device.h"
+#include "../../pinot_amd/csrc/node.h"
 namespace phip {
+// node_merge.hip on the host (device memory is host memory here): the merges really run, so a node plan's merged
+// table can be checked
+hipError_t launch_partial_merge_rows(uint64_t *dst, const uint64_t *src, const int32_t *kinds, int rows, int64_t groups,
+                                     hipStream_t) {
+  for (int r = 0; r < rows; r++)
+    for (int64_t g = 0; g < groups; g++) {
+      uint64_t &a = dst[r * groups + g];
+      const uint64_t b = src[r * groups + g];
+      double x, y;
+      switch (kinds[r]) {
+        case PHIP_ROW_COUNT:
+        case PHIP_ROW_SUM_I64: a = (uint64_t)((int64_t)a + (int64_t)b); break;
+        case PHIP_ROW_SUM_F64: memcpy(&x, &a, 8); memcpy(&y, &b, 8); x += y; memcpy(&a, &x, 8); break;
+        case PHIP_ROW_MIN: a = a < b ? a : b; break;
+        case PHIP_ROW_MAX: a = a > b ? a : b; break;
+        default: break;
+      }
+    }
+  return hipSuccess;
+}
+hipError_t launch_max_u32(uint32_t *dst, const uint32_t *src, int64_t n, hipStream_t) {
+  for (int64_t i = 0; i < n; i++) dst[i] = dst[i] > src[i] ? dst[i] : src[i];
+  return hipSuccess;
+}
+hipError_t launch_max_u8(uint8_t *dst, const uint8_t *src, int64_t n, hipStream_t) {
+  for (int64_t i = 0; i < n; i++) dst[i] = dst[i] > src[i] ? dst[i] : src[i];
+  return hipSuccess;
+}
+hipError_t launch_i64_row_to_f64(uint64_t *row, int64_t n, hipStream_t) {
+  for (int64_t i = 0; i < n; i++) {
+    const double d = (double)(int64_t)row[i];
+    memcpy(&row[i], &d, 8);
+  }
+  return hipSuccess;
+}
 hipError_t launch_bswap32(uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_bswap64(uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_trim_order(const double *, const int64_t *, const KeyOrder *, int64_t n, int32_t, int32_t, int32_t, void *scratch,
