@@ -344,6 +344,154 @@ def run_group_by(args, dist, leg, gsegs, raws, torch, want_cpu):
     return res
 
 
+def _intermediate_equal(ag, g, o, ex):
+    """One function's GPU intermediate against the oracle's (exact integers; doubles 1e-9 relative, the north star's
+    DOUBLE tolerance; HLL registers bit-exact)."""
+    rel = 1e-9
+    f = ag.function
+    if f in ("distinctcounthll", "distinctcountrawhll"):
+        return np.array_equal(np.asarray(g), np.asarray(o))
+    if f == "count":
+        return g == o
+    if f == "sum":
+        if ex is not None and isinstance(g, (int, np.integer)):
+            return int(g) == ex
+        ref = ex if ex is not None else o
+        return g == o or abs(g - ref) <= rel * max(abs(ref), 1.0)
+    if f in ("min", "max"):
+        return g == o
+    if f == "avg":
+        return g[1] == o[1] and (float(g[0]) == o[0] or abs(g[0] - o[0]) <= rel * abs(o[0]))
+    if f == "minmaxrange":
+        return tuple(map(float, g)) == tuple(o)
+    return g == o
+
+
+def compare_blocks(qc, gblk, oblk, exact, scale=1):
+    """A GPU results block against oracle/executor.py's over the same segments (`scale` copies of them: counts, sums
+    and docs multiply; MIN / MAX / HLL do not change). Returns None when equal, else the first difference."""
+    from pinot_amd.engine.reduce import trim_groups
+    if gblk.stats.num_docs_scanned != oblk.stats.num_docs_scanned * scale:
+        return f"numDocsScanned {gblk.stats.num_docs_scanned} vs {oblk.stats.num_docs_scanned * scale}"
+
+    def scaled(ag, v, ex):
+        if scale == 1 or ag.function not in ("count", "sum"):
+            return v, ex
+        return v * scale, (ex * scale if ex is not None else None)
+
+    if not qc.group_by:
+        for ag, g, o, ex in zip(qc.aggregations, gblk.results, oblk.results, exact):
+            o, ex = scaled(ag, o, ex)
+            if not _intermediate_equal(ag, g, o, ex):
+                return f"{ag.function}: {g} vs {o} (exact {ex})"
+        return None
+    if getattr(gblk, "num_groups_trimmed", False):
+        oblk = trim_groups(qc, oblk)
+    if gblk.num_groups_limit_reached != oblk.num_groups_limit_reached:
+        return "numGroupsLimitReached differs"
+    if set(gblk.groups) != set(oblk.groups):
+        return f"group sets differ: {len(gblk.groups)} vs {len(oblk.groups)}"
+    for k, v in oblk.groups.items():
+        for ag, g, o, ex in zip(qc.aggregations, gblk.groups[k], v, exact[k]):
+            o, ex = scaled(ag, o, ex)
+            if not _intermediate_equal(ag, g, o, ex):
+                return f"group {k} {ag.function}: {g} vs {o}"
+    return None
+
+
+def time_config_queries(args, named, gsegs, oracle_segs, scale, rows_label):
+    """The queries of one config over its resident segments: each prepared once, `warmup` + `steps` executions (p50
+    wall, kernel times and algorithmic bytes per kernel from the library's HIP events), then the last block checked
+    against oracle/executor.py over `oracle_segs` (x `scale` copies) outside the timed region; the oracle's own run
+    time is the config's CPU baseline (numpy restatement, one thread)."""
+    from oracle import executor
+    from pinot_amd.engine.plan import GpuInstancePlanMaker
+    from pinot_amd.query.sql import parse
+    pm = GpuInstancePlanMaker()
+    rows = sum(s.num_docs for s in gsegs)
+    per_q, ok, t_total, cpu_rows, cpu_s = {}, True, 0.0, 0, 0.0
+    for name, sql in named.items():
+        qc = parse(sql)
+        op = pm.make_instance_plan(qc, gsegs)
+        for _ in range(args.warmup):
+            op.next_block()
+        lat, fk, ak = [], [], []
+        blk = None
+        for _ in range(args.steps):
+            ts = time.perf_counter()
+            blk = op.next_block()
+            lat.append((time.perf_counter() - ts) * 1e3)
+            fk.append(getattr(blk, "filter_kernel_ms", 0.0) or 0.0)
+            ak.append(getattr(blk, "agg_kernel_ms", 0.0) or 0.0)
+        if hasattr(op, "close"):
+            op.close()
+        p50 = float(np.median(lat))
+        t_total += float(np.sum(lat)) / 1e3
+        fms, ams = float(np.mean(fk)), float(np.mean(ak))
+        fb, ab = int(getattr(blk, "filter_bytes", 0) or 0), int(getattr(blk, "agg_bytes", 0) or 0)
+        d = {"p50_ms": round(p50, 4), "G_rows_per_s": round(rows / (p50 * 1e-3) / 1e9, 2),
+             "docs_scanned": blk.stats.num_docs_scanned, "filter_ms": round(fms, 4), "agg_ms": round(ams, 4),
+             "filter_bytes": fb, "agg_bytes": ab,
+             "filter_frac": round(fb / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if fms > 0 else None,
+             "agg_frac": round(ab / (ams * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if ams > 0 else None,
+             "fused": bool(getattr(blk, "fused", False))}
+        if qc.group_by:
+            d["groups"] = len(blk.groups)
+        if not args.no_parity:
+            t0 = time.perf_counter()
+            oblk, exact = executor.execute(qc, oracle_segs)
+            cpu_s += time.perf_counter() - t0
+            cpu_rows += sum(s.num_docs for s in oracle_segs)
+            why = compare_blocks(qc, blk, oblk, exact, scale)
+            d["parity"] = "equal" if why is None else f"MISMATCH: {why}"
+            ok &= why is None
+        per_q[name] = d
+    res = {"rows_per_query": rows, "segments": len(gsegs), "unit": "G rows/s",
+           "value": round(rows * len(named) * args.steps / t_total / 1e9, 3) if t_total else None,
+           "ms_per_pass": round(t_total * 1e3 / args.steps, 4), "per_query": per_q, "layout": rows_label}
+    if not args.no_parity:
+        res["parity"] = "checked" if ok else "MISMATCH"
+        res["cpu_baseline"] = {"value": round(cpu_rows / cpu_s / 1e9, 4) if cpu_s else None, "unit": "G rows/s",
+                               "cores": 1, "kind": "port",
+                               "sample": f"oracle/executor.py (numpy restatement of the CPU server path, one thread): "
+                                         f"each query once over {len(oracle_segs)} segment(s) of the same data "
+                                         f"({cpu_rows // max(len(named), 1)} rows per query), {cpu_s:.1f} s"}
+    return res
+
+
+def run_c1(args):
+    """BASELINE configs[0]: the BenchmarkQueries segment (P/BenchmarkQueries.java:81-137; 10M rows,
+    EXP(0.001), tools/bq.py), every query of the GPU subset, one GPU; parity against oracle/executor.py on the segment."""
+    from pinot_amd.engine.segment import GpuSegment
+    from tools import bq
+    raws = bq.make_segments(args.c1_rows, 1, "EXP(0.001)")
+    gsegs = [GpuSegment(r) for r in raws]
+    try:
+        res = time_config_queries(args, bq.QUERIES, gsegs, raws, 1, f"{args.c1_rows} rows, 1 segment, EXP(0.001)")
+    finally:
+        for g in gsegs:
+            g.destroy()
+    return res
+
+
+def run_c4(args):
+    """BASELINE configs[3]: 5-predicate AND / OR / NOT over Roaring inverted indexes, 100 x 10M = 1B
+    rows (10 distinct generated segments each resident 10 times), selectivity 0.01 %-50 %, COUNT(*) and SUM(M);
+    parity against oracle/executor.py over the 10 distinct segments (counts, sums and docs x 10)."""
+    from pinot_amd.engine.segment import GpuSegment
+    from tools import c4
+    distinct = [c4.make_segment(i, num_rows=args.c4_rows) for i in range(args.c4_distinct)]
+    gsegs = [GpuSegment(r) for _ in range(args.c4_copies) for r in distinct]
+    named = {f"sel={sel} {agg}": c4.query(sel, agg) for sel in c4.SELECTIVITIES for agg in ("COUNT(*)", "SUM(M)")}
+    try:
+        res = time_config_queries(args, named, gsegs, distinct, args.c4_copies,
+                                  f"{len(gsegs)} x {args.c4_rows} rows ({args.c4_distinct} distinct x {args.c4_copies})")
+    finally:
+        for g in gsegs:
+            g.destroy()
+    return res
+
+
 # kernel families of one query execution: a plain filter launch, a filter launch that aggregated its own tiles
 # (fused), and a separate aggregation launch.
 #
@@ -470,6 +618,13 @@ def main():
                     help="group-by legs over the headline layout's segments (BASELINE C3 = SSB Q2.x-Q4.x, C5's "
                          "query), each parity-checked against oracle/cpu_scan.c; '' = none")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time per leg")
+    ap.add_argument("--configs", default="c1,c4",
+                    help="the other BASELINE configs as legs at N = 1 (c1: BenchmarkQueries 10M rows; c4: 1B-row "
+                         "inverted-index sweep), each parity-checked against oracle/executor.py; '' = none")
+    ap.add_argument("--c1-rows", type=int, default=10_000_000)
+    ap.add_argument("--c4-rows", type=int, default=10_000_000)
+    ap.add_argument("--c4-distinct", type=int, default=10)
+    ap.add_argument("--c4-copies", type=int, default=10)
     ap.add_argument("--layout", default="both", choices=["sorted", "unsorted", "both"],
                     help="headline = sorted (SURVEY.md §8d C2); both also measures the unsorted layout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -598,6 +753,13 @@ def main():
             del raws
         results[layout] = res
 
+    cfg_legs = {}
+    if world == 1:
+        for leg in [c for c in args.configs.split(",") if c]:
+            t0 = time.time()
+            cfg_legs[leg] = {"c1": run_c1, "c4": run_c4}[leg](args)
+            log(f"config leg {leg}: {cfg_legs[leg]['value']} G rows/s, parity {cfg_legs[leg].get('parity')} "
+                f"({time.time() - t0:.0f} s)")
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -650,6 +812,10 @@ def main():
             **{l: results[l]["parity"][1] for l in layouts}}
     for g in gb_legs:
         out[g] = head[g]
+    for leg, r in cfg_legs.items():
+        out[leg] = r
+        if not args.no_parity and r.get("parity") != "checked":
+            out["parity"] = "MISMATCH"
     if "c5_merged" in head:  # the C5 query over every rank's segments, merged across ranks (N > 1 / --c5 on)
         out["c5_merged"] = head["c5_merged"]
     if len(layouts) > 1:
