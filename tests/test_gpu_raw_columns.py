@@ -100,7 +100,7 @@ def test_gpu_group_by_raw_columns(sql, mode, raw_segments, monkeypatch):
     got, want = reduce_blocks(qc, [gblk]).rows, reduce_blocks(qc, [oblk]).rows
     if not qc.order_by:  # (-0.0 before 0.0, as Double.compare orders them: Python's sort would tie the two)
         def order(r):
-            return [(x, bool(np.signbit(x)) is False) if isinstance(x, float) else x for x in r]
+            return [(float(x), not np.signbit(x)) if isinstance(x, float) else x for x in r]
         got, want = sorted(got, key=order), sorted(want, key=order)
     assert fixtures.rows_match(got, want)
 
