@@ -2389,7 +2389,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dq.stage_off[k] = off + kStagePad;
       off += 256 * maxbits[k] + 2 * kStagePad;
     }
-    // dictionaries of at most kAggLdsDict bytes (in every segment) are read from LDS as well
+    // dictionaries of at most kAggLdsDict bytes (in every segment) are read from LDS as well. (Round 6 measured 8 KiB
+    // dictionaries in LDS too, the per-wave copies within 8 KiB more of LDS per wave: C4 SUM(M) over a 1000-entry
+    // dictionary got slower at every selectivity -- 50 %: aggregation 1.33 -> 1.96 ms, 0.01 %: 0.16 -> 0.27 ms,
+    // profiles/r06d_c4_lds_dict_ab.log -- the larger stage area halves the resident workgroups of a latency-bound walk)
     for (size_t k = 0; k < cols.size() && ok; k++) {
       dq.stage_dict_off[k] = -1;
       int64_t bytes = 0;
@@ -3260,12 +3263,18 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // (profiles/r03n_fuse_large_ab.log). Their value columns are gathered, not streamed with every tile (streaming
     // LO_EXTENDEDPRICE over 293K tiles: 1.4 ms). PHIP_FUSE_LARGE=0 restores the size rule alone.
     const bool big = total_work > kFuseMaxTiles;
+    // A small query whose tiles are mostly matched (estimated >= kFuseDenseSplit docs per 2048-doc tile) splits: the
+    // aggregation kernel's dense-tile walk projects a tile's matched docs four groups per gather round trip, where the
+    // fused tile drains them through its deferred ring 128 at a time, one round trip each (C1 on 10M rows,
+    // profiles/r06d_c1_ab.log: FILTERED_QUERY, 88 % matched, p50 0.199 -> 0.113 ms split).
+    const double kFuseDenseSplit = 1024.0;
+    const bool dense_small = !big && per_tile >= kFuseDenseSplit;
     const char *fl = getenv("PHIP_FUSE_LARGE");  // measurement override
     bool bs_all = true;  // (the P-layout conjunction's heavier evaluation keeps the size rule)
     for (const DevSeg &ds : dsegs) bs_all &= ds.conj == 0 || ds.conj_bs != 0;
     const bool fuse_large = (fl ? atoi(fl) != 0 : true) && bs_all;
     bool fuse = conj_all && any_filter_prog && !group_by && nprog == 1 && nhll == 0 && naggs > 0 && naggs <= 4 && !want_bitmap &&
-                (fe ? atoi(fe) != 0 : (!big || fuse_large || (fuse_per_tile > 0 && per_tile <= fuse_per_tile)));
+                (fe ? atoi(fe) != 0 : (!dense_small && (!big || fuse_large || (fuse_per_tile > 0 && per_tile <= fuse_per_tile))));
     bool any_value = false;
     for (int a = 0; a < naggs; a++) any_value |= dq.aggs[a].acc != ACC_COUNT;
     if (fuse && any_value) {
