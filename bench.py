@@ -1,7 +1,8 @@
 """Headline benchmark: SSB SF100 flattened lineorder, Q1.1-Q1.3 (scan filter + SUM), per GPU.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; N>1 is launched by
-torch.distributed.run with one rank per GPU. A step = Q1.1 + Q1.2 + Q1.3, each one query over 100 segments
+torch.distributed.run with one rank per GPU, or, without it, by this script itself (spawn_ranks: N rank processes
+started before any GPU call, rank 0's line printed). A step = Q1.1 + Q1.2 + Q1.3, each one query over 100 segments
 x 6M rows per GPU (SF100 per GPU, weak scaling). At N = 1 the rank holds exactly those 100 (BASELINE C2); at
 N > 1 each rank holds 125 segments of an SF(125N) table (N = 8: SF1000, BASELINE C5) and the step runs over
 the first 100 of them, while the C5 query (DISTINCTCOUNTHLL + GROUP BY) runs over all 125 per rank and is
@@ -16,10 +17,11 @@ sorted forward indexes and their predicates are doc ranges (SortedIndexBasedFilt
 Pinot's CPU path would use them. The same queries over the unsorted layout (every row scanned: the
 scan-bound case) are measured in the same run and reported under "unsorted_layout".
 
-Roofline (per kernel, from the library's own HIP events on the stream the kernels run on): achieved =
-the kernel's algorithmic bytes per launch (phip_result.filter_bytes / agg_bytes, SURVEY.md §8d, computed by
-libpinot_hip from the tiles it must stream and the docs it must project) / its mean launch time; the
-dominant kernel (largest time share) is the headline `roofline`. `traffic` = HBM bytes per launch of that
+Roofline (per kernel, from the library's own HIP events on the stream the kernels run on -- recorded by each launch's
+dispatch packet in a repeat of the timed executions, so they time the kernel itself): achieved = the kernel's
+algorithmic bytes per launch (phip_result.filter_bytes / agg_bytes, SURVEY.md §8d, computed by libpinot_hip from the
+tiles it must stream and the docs it must project) / its mean launch time; the dominant kernel (largest time share)
+is the headline `roofline`. `traffic` = HBM bytes per launch of that
 kernel from this round's rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes
 (profiles/<round>_traffic.json, tools/traffic.py), or null.
 
@@ -147,6 +149,22 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
     # one more execution per query, outside the timed region: this rank's answers, checked against the CPU
     # restatement on the same segments (check_parity)
     answers = {q: ops[q].next_block() for q in queries}
+    # Kernel durations for the roofline, outside the timed region: the same executions again with each one-kernel
+    # plan's HIP events recorded by its dispatch packet (PHIP_EXT_EVENTS=1: hipExtLaunchKernel on the library's
+    # stream), which time the kernel itself; the timed steps' barrier-marker events also hold the ~5 us dispatch
+    # latency of the kernel behind the first marker (sorted Q1.x: 131.8 / 35.3 / 21.4 us vs rocprofv3's 126.3 / 30.0 /
+    # 16.0, profiles/r06f_trace_sorted.json). The extra dispatch work is why the timed steps do not use it
+    # (profiles/r04p_host_ab.log: step 0.286 -> 0.304 ms).
+    kstats_ext = {q: [] for q in queries}
+    os.environ["PHIP_EXT_EVENTS"] = "1"
+    try:
+        for _ in range(args.steps):
+            for q in queries:
+                blk = ops[q].next_block()
+                kstats_ext[q].append((blk.filter_kernel_ms, blk.agg_kernel_ms, blk.filter_bytes, blk.agg_bytes,
+                                      bool(getattr(blk, "fused", False)), int(getattr(blk, "stream_bytes", 0) or 0)))
+    finally:
+        del os.environ["PHIP_EXT_EVENTS"]
     concurrent = None
     if dist is None and not args.no_concurrent:
         # Outside the headline: the same queries as concurrent clients (one thread per query, each running its
@@ -175,7 +193,7 @@ def run_layout(args, dist, queries, qcs, gsegs, torch):
             concurrent = time.perf_counter() - t0
     for op in ops.values():
         op.close()
-    return elapsed, lat, kstats, answers, concurrent
+    return elapsed, lat, kstats, answers, concurrent, kstats_ext
 
 
 def check_parity(queries, qcs, answers, raws, dist, torch):
@@ -707,9 +725,17 @@ def main():
         head = gsegs[:head_segs]
         raws = all_raws[:head_segs]
         rows_per_rank = sum(s.num_docs for s in head)
-        elapsed, lat, kstats, answers, concurrent = run_layout(args, dist, queries, qcs, head, torch)
+        elapsed, lat, kstats, answers, concurrent, kstats_ext = run_layout(args, dist, queries, qcs, head, torch)
+        rf = roofline(kstats_ext, queries, traffic, touched, layout, args.steps)
+        rb = roofline(kstats, queries, traffic, touched, layout, args.steps)
+        rf["timing"] = ("kernel durations from HIP events recorded by each launch's dispatch packet (PHIP_EXT_EVENTS=1, "
+                        "the timed steps' executions repeated outside the timed region)")
+        rf["bracket_events"] = {"kernel": rb["kernel"], "frac": rb["frac"],
+                                "ms_per_launch": rb["kernels"][rb["kernel"]]["ms_per_launch"],
+                                "note": "the timed steps' own barrier-marker events (include the kernel's dispatch "
+                                        "latency)"}
         res = {"elapsed": elapsed, "rows_per_rank": rows_per_rank, "load_s": load_s, "nseg": len(head),
-               "lat": lat, "roofline": roofline(kstats, queries, traffic, touched, layout, args.steps)}
+               "lat": lat, "roofline": rf}
         if concurrent:
             res["concurrent"] = {"value": round(rows_per_rank * len(queries) * args.steps / concurrent / 1e9, 3),
                                  "unit": "G rows/s", "ms_per_step": round(concurrent * 1e3 / args.steps, 4),

@@ -64,7 +64,8 @@ def cycle(a):
     if a.bench:
         line = [l for l in open(a.bench) if l.lstrip().startswith("{")][-1]
         j = json.loads(line)
-        rf = j["roofline"] if a.layout in (None, "sorted") else j["unsorted_layout"]["roofline"]
+        # (a run with --layout unsorted reports the unsorted layout at the top level)
+        rf = j["unsorted_layout"]["roofline"] if a.layout == "unsorted" and "unsorted_layout" in j else j["roofline"]
         k = rf["kernels"][a.family]
         mean_s = sum(alld) / len(alld) * 1e-9
         ach = k["alg_bytes_per_launch"] / mean_s / 1e9
