@@ -43,7 +43,7 @@ n2)
   tail -c 1500 gpurun_out/${TAG}_n2.log
   ;;
 trace)
-  B="--no-cpu-baseline --no-parity --no-concurrent --group-by= --steps 10 --warmup 3"
+  B="--no-cpu-baseline --no-parity --no-concurrent --group-by= --configs= --steps 10 --warmup 3"
   for L in sorted unsorted; do
     step trace_$L 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
     python3 tools/trace_summary.py cycle gpurun_out/prof_${TAG}_$L/run_kernel_trace.csv --queries Q1.1,Q1.2,Q1.3 \
@@ -55,7 +55,7 @@ trace)
     -o gpurun_out/trace_${TAG}_gb.json > /dev/null 2> gpurun_out/trace_${TAG}_gb.err || cat gpurun_out/trace_${TAG}_gb.err
   ;;
 traffic)
-  B="--no-cpu-baseline --no-parity --no-concurrent --group-by= --steps 10 --warmup 3"
+  B="--no-cpu-baseline --no-parity --no-concurrent --group-by= --configs= --steps 10 --warmup 3"
   for L in sorted unsorted; do
     step pmcf_$L 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
     step pmcw_$L 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_${TAG}_$L -o run -- python3 -u bench.py $B --layout $L
@@ -79,7 +79,7 @@ gbpmc)
     step gbfetch_$Q 200 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/gbfetch_${TAG}_$Q -o run -- python3 -u tools/gb_ab.py --queries $Q $G
     step gbwrite_$Q 200 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/gbwrite_${TAG}_$Q -o run -- python3 -u tools/gb_ab.py --queries $Q $G
   done
-  B1="--no-cpu-baseline --no-parity --no-concurrent --group-by= --steps 5 --warmup 2 --layout sorted --queries Q1.1"
+  B1="--no-cpu-baseline --no-parity --no-concurrent --group-by= --configs= --steps 5 --warmup 2 --layout sorted --queries Q1.1"
   step q11sq 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT --output-format csv -d gpurun_out/q11sq_$TAG -o run -- python3 -u bench.py $B1
   for x in gpurun_out/gbsq_${TAG}_* gpurun_out/gbtcc_${TAG}_* gpurun_out/gbfetch_${TAG}_* gpurun_out/gbwrite_${TAG}_* gpurun_out/q11sq_$TAG; do
     [ -d "$x" ] && python3 tools/pmc_summary.py "$x" > "$x.txt" 2>&1
