@@ -141,10 +141,37 @@ __global__ void finalize_partials2_kernel(const uint64_t *__restrict__ pa, int n
 // docs, entries scanned) -> out[32 + i], the last block copies the per-segment matched counts -> out[64 + s]
 // and the HLL registers -> (u32) out[64 + nseg ...], zeroing both device arrays for the next execution (so no
 // memset launch precedes the query kernels).
+__device__ __forceinline__ void finalize_all_body(const uint64_t *__restrict__ pa, int nba, int na,
+                                                  const int32_t *__restrict__ ka, const uint64_t *__restrict__ pf,
+                                                  int nbf, const int32_t *__restrict__ kf, uint64_t *__restrict__ segm,
+                                                  int nseg, uint32_t *__restrict__ hll, int hll_words, uint64_t *out);
+
+// ticket != null: completion published to the host -- every block fences its writes to the mapped result area at
+// system scope and takes a ticket; the last one resets the ticket and stores `seq` into out[kDoneSlot] with a
+// system-scope release, so a host that polls that word (execute_plan, PHIP_POLL_DONE) may read the results without
+// waiting for the kernel's completion signal (the end-of-kernel release and the signal write behind it).
 __global__ void finalize_all_kernel(const uint64_t *__restrict__ pa, int nba, int na, const int32_t *__restrict__ ka,
                                     const uint64_t *__restrict__ pf, int nbf, const int32_t *__restrict__ kf,
                                     uint64_t *__restrict__ segm, int nseg, uint32_t *__restrict__ hll, int hll_words,
-                                    uint64_t *out) {
+                                    uint64_t *out, uint32_t *ticket, uint64_t seq) {
+  finalize_all_body(pa, nba, na, ka, pf, nbf, kf, segm, nseg, hll, hll_words, out);
+  if (ticket == nullptr) return;
+  __threadfence_system();  // (every thread's result stores, at system scope, before the block's ticket)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(out + kDoneSlot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+__device__ __forceinline__ void finalize_all_body(const uint64_t *__restrict__ pa, int nba, int na,
+                                                  const int32_t *__restrict__ ka, const uint64_t *__restrict__ pf,
+                                                  int nbf, const int32_t *__restrict__ kf, uint64_t *__restrict__ segm,
+                                                  int nseg, uint32_t *__restrict__ hll, int hll_words, uint64_t *out) {
   const int i = blockIdx.x;
   if (i < na) {
     finalize_slot(pa, nba, na, ka, out, i);
@@ -429,8 +456,8 @@ hipError_t launch_finalize_partials2(const uint64_t *pa, int nba, int na, const 
 }
 hipError_t launch_finalize_all(const uint64_t *pa, int nba, int na, const int32_t *ka, const uint64_t *pf, int nbf,
                                const int32_t *kf, uint64_t *segm, int nseg, uint32_t *hll, int hll_words, uint64_t *out,
-                               hipStream_t s) {
-  finalize_all_kernel<<<na + 3, 64, 0, s>>>(pa, nba, na, ka, pf, nbf, kf, segm, nseg, hll, hll_words, out);
+                               hipStream_t s, uint32_t *ticket, uint64_t seq) {
+  finalize_all_kernel<<<na + 3, 64, 0, s>>>(pa, nba, na, ka, pf, nbf, kf, segm, nseg, hll, hll_words, out, ticket, seq);
   return hipGetLastError();
 }
 hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t G, const int32_t *kinds, hipStream_t s) {

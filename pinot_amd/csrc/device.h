@@ -9,6 +9,7 @@ constexpr int kMaxQueryColumns = 16;  // distinct columns one query may referenc
 constexpr int kMaxAggs = 8;           // aggregation slots per query
 constexpr int kMaxPrograms = 8;       // filter programs per query (filtered aggregations in one pass)
 constexpr int kDenseMin = 640;        // default DevAggQuery::dense_min
+constexpr int kDoneSlot = 63;         // finals[kDoneSlot] of a plan's mapped result area: the execution's completion word
 constexpr int kMaxFilterStack = 6;    // postfix evaluation stack depth (host rejects deeper programs)
 constexpr int kMaxGroupBy = 8;  // GROUP BY columns (the mixed-radix key space stays below 2^62)
 constexpr int kWave = 64;             // CDNA wavefront

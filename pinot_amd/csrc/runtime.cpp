@@ -68,7 +68,7 @@ hipError_t launch_finalize_partials(const uint64_t *partials, int nblocks, int n
                                     uint64_t *out, hipStream_t s);
 hipError_t launch_finalize_all(const uint64_t *pa, int nba, int na, const int32_t *ka, const uint64_t *pf, int nbf,
                                const int32_t *kf, uint64_t *segm, int nseg, uint32_t *hll, int hll_words, uint64_t *out,
-                               hipStream_t s);
+                               hipStream_t s, uint32_t *ticket = nullptr, uint64_t seq = 0);
 hipError_t launch_group_count(const uint64_t *counts, int64_t n, int32_t *chunk_counts, int64_t nchunks,
                               int64_t *offsets, hipStream_t s);
 hipError_t launch_group_compact(const uint64_t *counts, int64_t n, const int64_t *offsets, int64_t nchunks,
@@ -1987,6 +1987,15 @@ struct Plan {
   bool split_event = true;   // record ev[4] between a filter and a separate aggregation launch
   bool fold_final = false;   // the last kernel's last workgroup finalizes (no finalize_all launch)
   uint32_t *fin_counter = nullptr;  // its ticket counter (device)
+  // Completion by polling (aggregation-only plans, PHIP_POLL_DONE, default on): finalize_all publishes the execution's
+  // sequence number in the mapped result area after its results (aggregate.hip finalize_all_kernel), and the host spins
+  // on that word instead of waiting for the stream -- the kernel's end-of-pipe release and completion signal are not
+  // on the query's path. done_seq = the number this execution waits for (0: wait for the stream).
+  uint32_t *done_ticket = nullptr;
+  uint64_t done_counter = 0, done_seq = 0;
+  // PHIP_KERNEL_TIMING=0 (read per execution; aggregation-only plans): no timing markers around the kernels -- two
+  // barrier packets the command processor waits on per query -- and kernel times reported as 0
+  bool timed = true;
 };
 
 // String.compareTo order (UTF-16 code units) over UTF-8 bytes: the lead bytes 0xEE / 0xEF (U+E000..U+FFFF) rank
@@ -3843,6 +3852,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
     P.pinned_dev = (uint64_t *)dp;
   }
+  if (!group_by && !P.select && !want_bitmap) {
+    void *tk = nullptr;
+    const int32_t trc = P.alloc(64, &tk);
+    if (trc) return trc;
+    HIP_TRY(hipMemsetAsync(tk, 0, 64, st));
+    P.done_ticket = (uint32_t *)tk;
+  }
   // Finalize in the last workgroup of the plan's last kernel (agg_common.h finalize_tail) for aggregation-only plans:
   // the finalize_all launch and its dispatch gap go. With one device-scope ticket counter the workgroups' atomics
   // serialised at the memory side (the fused kernel grew 13-50 us, step 0.346 -> 0.421 ms, profiles/r04f_host_ab.log);
@@ -3960,17 +3976,19 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   // saves: enqueue 7.0 -> 9.8 us per query, step 0.286 -> 0.304 ms (profiles/r04p_host_ab.log).
   const int nkern = (has_filter ? 1 : 0) + (need_agg && !fused ? 1 : 0);
   const char *xe = getenv("PHIP_EXT_EVENTS");
-  const bool ext_events = total_work > 0 && nkern == 1 && !P.split_event && xe && atoi(xe) != 0;
+  const char *kt = getenv("PHIP_KERNEL_TIMING");  // "0": no timing markers (aggregation-only plans; times read 0)
+  P.timed = group_by || P.select || !(kt && atoi(kt) == 0);
+  const bool ext_events = P.timed && total_work > 0 && nkern == 1 && !P.split_event && xe && atoi(xe) != 0;
   hipEvent_t e0 = ext_events ? P.ev[1] : nullptr, e1 = ext_events ? P.ev[2] : nullptr;
-  if (!ext_events) HIP_TRY(hipEventRecord(P.ev[1], st));
+  if (!ext_events && P.timed) HIP_TRY(hipEventRecord(P.ev[1], st));
   if (has_filter && total_work > 0)
     HIP_TRY(launch_filter(fq, conj_only, P.fused_gb ? (P.gb_lds ? -3 : (P.gb_xcd ? -2 : -1)) : P.fused_naggs, filter_blocks,
                           filter_lds, st, e0, e1));
   // (a plan of one kernel -- fused, or a filter or aggregation alone -- needs no split event)
-  if (P.split_event) HIP_TRY(hipEventRecord(P.ev[4], st));
+  if (P.split_event && P.timed) HIP_TRY(hipEventRecord(P.ev[4], st));
   if (need_agg && total_work > 0 && !fused)
     HIP_TRY(launch_agg(dq, (const DevAggQuery *)(base + dq_off), agg_blocks, agg_lds, st, e0, e1));
-  if (!ext_events) HIP_TRY(hipEventRecord(P.ev[2], st));
+  if (!ext_events && P.timed) HIP_TRY(hipEventRecord(P.ev[2], st));
   if (group_by && P.gb_xcd && total_work > 0)  // the XCD-private copies folded into copy 0 (the plan's table)
     HIP_TRY(launch_xcd_merge((uint64_t *)gtab, dq.xcd_words, dq.num_groups, dev_kinds, (uint32_t *)ghll,
                              dq.xcd_hll_words, st));
@@ -3990,12 +4008,16 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
     HIP_TRY(launch_masks_to_words((const uint32_t *)masks, dsegs[0].tile0, dsegs[0].num_work, (uint64_t *)fo,
                                   filter_nwords, st));
   // every result lands in the plan's pinned buffer, written by the device: finals[64] | seg_matched[nmatch] | HLL
+  P.done_seq = 0;
   if (total_work > 0 && !P.fold_final) {
     const bool aggs_here = need_agg && !group_by && naggs > 0;
+    const char *pd = getenv("PHIP_POLL_DONE");  // measurement override: "0" waits for the stream
+    const bool poll = P.done_ticket != nullptr && !(pd && atoi(pd) == 0) && !P.total_events;
+    if (poll) P.done_seq = ++P.done_counter;
     HIP_TRY(launch_finalize_all(aggs_here ? (const uint64_t *)apart : nullptr, fused ? filter_blocks : agg_blocks,
                                 aggs_here ? naggs : 0, dev_kinds, has_filter ? (const uint64_t *)fpart : nullptr,
                                 filter_blocks, dev_kinds + naggs, (uint64_t *)seg_matched, P.nmatch, dq.hll_regs,
-                                (int)hll_words, P.pinned_dev, st));
+                                (int)hll_words, P.pinned_dev, st, poll ? P.done_ticket : nullptr, P.done_seq));
   }
   if (!group_by && P.total_events) HIP_TRY(hipEventRecord(P.ev[3], st));
   (void)fin_agg;
@@ -4669,6 +4691,22 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       }
       impl->dicts[k] = rd;
     }
+  } else if (P.done_seq != 0 && !P.graph_exec && !P.select && !filter_words) {
+    // the finalize kernel's completion word (Plan::done_seq): spin on the mapped result area; a kernel that has
+    // not published within the bound is waited for on the stream (which also reports a failed launch)
+    volatile const uint64_t *done = P.pinned + kDoneSlot;
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false;
+    for (uint32_t spin = 0;; spin++) {
+      if (*done == P.done_seq) {
+        seen = true;
+        break;
+      }
+      if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (!seen) HIP_TRY(hipStreamSynchronize(st));
   } else {
     HIP_TRY(hipStreamSynchronize(st));
   }
@@ -4716,10 +4754,12 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     if (nhll) for (size_t i = 0; i < ((size_t)nhll << log2m); i++) impl->hll[i] = (uint8_t)hll_host[i];
   }
   float t_all = 0.f, t_scan = 0.f, t_filter = 0.f, t_agg = 0.f;
-  HIP_TRY(hipEventElapsedTime(&t_scan, P.ev[1], P.ev[2]));
+  if (P.timed && total_work > 0) HIP_TRY(hipEventElapsedTime(&t_scan, P.ev[1], P.ev[2]));
   if (P.total_events) HIP_TRY(hipEventElapsedTime(&t_all, P.ev[0], P.ev[3]));
   else t_all = t_scan;
-  if (P.split_event) {
+  if (!P.timed || total_work == 0) {
+    // (no markers were recorded: the kernel times read 0)
+  } else if (P.split_event) {
     HIP_TRY(hipEventElapsedTime(&t_filter, P.ev[1], P.ev[4]));
     HIP_TRY(hipEventElapsedTime(&t_agg, P.ev[4], P.ev[2]));
   } else if (has_filter && !(need_agg && !P.fused_naggs && !P.fused_gb)) {

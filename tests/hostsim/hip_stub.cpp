@@ -194,7 +194,9 @@ hipError_t launch_finalize_partials2(const uint64_t *, int, int na, const int32_
   return hipSuccess;
 }
 hipError_t launch_finalize_all(const uint64_t *, int, int na, const int32_t *, const uint64_t *, int, const int32_t *,
-                               uint64_t *segm, int nseg, uint32_t *hll, int hll_words, uint64_t *out, hipStream_t) {
+                               uint64_t *segm, int nseg, uint32_t *hll, int hll_words, uint64_t *out, hipStream_t,
+                               uint32_t *ticket, uint64_t seq) {
+  if (ticket) out[kDoneSlot] = seq;  // (published below with the results: the host's poll sees it at once)
   memset(out, 0, 64 * 8);
   memcpy(out + 64, segm, (size_t)nseg * 8);
   memset(segm, 0, (size_t)nseg * 8);
