@@ -1987,7 +1987,8 @@ struct Plan {
   bool split_event = true;   // record ev[4] between a filter and a separate aggregation launch
   bool fold_final = false;   // the last kernel's last workgroup finalizes (no finalize_all launch)
   uint32_t *fin_counter = nullptr;  // its ticket counter (device)
-  // Completion by polling (aggregation-only plans, PHIP_POLL_DONE, default on): finalize_all publishes the execution's
+  // Completion by polling (aggregation-only plans run without timing markers, PHIP_POLL_DONE, default on): finalize_all
+  // publishes the execution's
   // sequence number in the mapped result area after its results (aggregate.hip finalize_all_kernel), and the host spins
   // on that word instead of waiting for the stream -- the kernel's end-of-pipe release and completion signal are not
   // on the query's path. done_seq = the number this execution waits for (0: wait for the stream).
@@ -4012,7 +4013,9 @@ static int32_t enqueue_plan(Plan &P, hipStream_t st) {
   if (total_work > 0 && !P.fold_final) {
     const bool aggs_here = need_agg && !group_by && naggs > 0;
     const char *pd = getenv("PHIP_POLL_DONE");  // measurement override: "0" waits for the stream
-    const bool poll = P.done_ticket != nullptr && !(pd && atoi(pd) == 0) && !P.total_events;
+    // (only without timing markers: an event's elapsed time is readable once the runtime has seen its command
+    // complete, which a poll that returns early does not wait for -- "device not ready" under concurrent lanes)
+    const bool poll = P.done_ticket != nullptr && !(pd && atoi(pd) == 0) && !P.total_events && !P.timed;
     if (poll) P.done_seq = ++P.done_counter;
     HIP_TRY(launch_finalize_all(aggs_here ? (const uint64_t *)apart : nullptr, fused ? filter_blocks : agg_blocks,
                                 aggs_here ? naggs : 0, dev_kinds, has_filter ? (const uint64_t *)fpart : nullptr,
