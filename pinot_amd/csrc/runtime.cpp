@@ -1987,11 +1987,11 @@ struct Plan {
   bool split_event = true;   // record ev[4] between a filter and a separate aggregation launch
   bool fold_final = false;   // the last kernel's last workgroup finalizes (no finalize_all launch)
   uint32_t *fin_counter = nullptr;  // its ticket counter (device)
-  // Completion by polling (aggregation-only plans run without timing markers, PHIP_POLL_DONE, default on): finalize_all
-  // publishes the execution's
-  // sequence number in the mapped result area after its results (aggregate.hip finalize_all_kernel), and the host spins
-  // on that word instead of waiting for the stream -- the kernel's end-of-pipe release and completion signal are not
-  // on the query's path. done_seq = the number this execution waits for (0: wait for the stream).
+  // Completion by polling (aggregation-only plans run without timing markers, PHIP_POLL_DONE, default on):
+  // finalize_all publishes the execution's sequence number in the mapped result area after its results
+  // (aggregate.hip finalize_all_kernel), and the host spins on that word instead of waiting for the stream -- the
+  // kernel's end-of-pipe release and completion signal are not on the query's path. done_seq = the number this
+  // execution waits for (0: wait for the stream).
   uint32_t *done_ticket = nullptr;
   uint64_t done_counter = 0, done_seq = 0;
   // PHIP_KERNEL_TIMING=0 (read per execution; aggregation-only plans): no timing markers around the kernels -- two
