@@ -2553,6 +2553,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(stride, docs));
       int64_t cap = 1024;
       while (cap < 2 * bound) cap <<= 1;
+      if (const char *hc = getenv("PHIP_GB_HASH_CAP"))  // test override: a smaller table, so it must grow and rerun
+        cap = std::max<int64_t>(64, std::min<int64_t>(cap, (int64_t)1 << (63 - __builtin_clzll((uint64_t)std::max(2LL, atoll(hc))))));
       const int64_t per_slot = 8 + 8 * (1 + (int64_t)naggs);
       if (cap * per_slot > ((int64_t)24 << 30))
         return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table of %lld slots exceeds the memory budget", (long long)cap);
@@ -2943,6 +2945,8 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       const int64_t bound = std::max<int64_t>(1, std::min<int64_t>(gb_key_space, work_docs));
       int64_t cap = 1024;
       while (cap < 2 * bound) cap <<= 1;
+      if (const char *hc = getenv("PHIP_GB_HASH_CAP"))
+        cap = std::max<int64_t>(64, std::min<int64_t>(cap, (int64_t)1 << (63 - __builtin_clzll((uint64_t)std::max(2LL, atoll(hc))))));
       if (dq.mode != GB_HASH || cap < dq.num_groups) {
         const int64_t per_slot = 8 + 8 * (1 + (int64_t)naggs);
         if (cap * per_slot > ((int64_t)24 << 30))
@@ -4295,6 +4299,7 @@ static int32_t execute_select(Plan &P, Workspace &ws, hipStream_t st, ResultImpl
 // group table, handed to the caller (phip_plan_execute_partial). EXEC_FINISH: compaction / trim / copy-out
 // of the caller-merged table (phip_plan_finish).
 enum { EXEC_FULL = 0, EXEC_PARTIAL = 1, EXEC_FINISH = 2 };
+constexpr int32_t kGrowHash = -100;  // execute_plan: the hash table overflowed (internal status: execute_growing)
 static_assert(ACC_COUNT == PHIP_ROW_COUNT && ACC_SUM_I64 == PHIP_ROW_SUM_I64 && ACC_SUM_F64 == PHIP_ROW_SUM_F64 &&
                   ACC_MIN_F64 == PHIP_ROW_MIN && ACC_MAX_F64 == PHIP_ROW_MAX && ACC_HLL == PHIP_ROW_HLL,
               "partial row kinds are the accumulator kinds");
@@ -4550,7 +4555,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
     if (dq.mode == GB_HASH) HIP_TRY(hipMemcpyAsync(&overflow, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
     if (limit_pass) {
       HIP_TRY(hipStreamSynchronize(st));
-      if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
+      if (overflow) return kGrowHash;  // (execute_growing: a table twice the size, and the execution again)
       const int64_t matched_docs = has_filter ? (int64_t)fin[32] : docs_in_work;
       rc = group_limit(P, ws, st, matched_docs, &keys, &ov, &ol, &oh, &ngroups, &r.num_groups_limit_reached,
                        (const int64_t *)offs);
@@ -4639,7 +4644,7 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       }
       if (hb) memcpy(impl->hll.data(), staged.data() + kb + 2 * vb, hb);
     }
-    if (overflow) return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table overflow (%lld slots)", (long long)dq.num_groups);
+    if (overflow) return kGrowHash;
     impl->keys.resize(ngroups * P.num_group_by);
     for (int64_t g = 0; g < ngroups; g++) {
       int64_t key = hkeys[g];
@@ -5049,6 +5054,54 @@ static int32_t finish_agg_partial(Plan &P, const phip_partial *merged, phip_resu
   return PHIP_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Hash-table growth (DictionaryBasedGroupKeyGenerator's holders grow with their maps,
+// DictionaryBasedGroupKeyGenerator.java:150-185, instead of refusing). The open-addressing table is sized at plan
+// creation to twice the groups possible, so a full table takes a capacity override (PHIP_GB_HASH_CAP) or a bound
+// that did not hold; then the execution reports kGrowHash, the table is reallocated at twice the slots (new
+// plan-owned buffers, the device descriptor updated) and the execution runs again -- every kernel from the filter on,
+// the tables reset as on any execution. Up to kMaxHashGrowth doublings per execution.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMaxHashGrowth = 8;
+
+static int32_t grow_hash_table(Plan &P) {
+  DevAggQuery &dq = P.dq;
+  const int64_t cap = dq.num_groups * 2;
+  const int64_t per_slot = 8 + 8 * (1 + (int64_t)P.naggs) + (int64_t)P.nhll * P.m_regs * 4 + (P.first_doc ? 4 : 0);
+  if (cap * per_slot > ((int64_t)24 << 30))
+    return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table of %lld slots exceeds the memory budget", (long long)cap);
+  HIP_TRY(hipSetDevice(P.dev->ordinal));
+  void *tab = nullptr, *hll = nullptr, *hk = nullptr, *fd = nullptr;
+  int32_t rc = P.alloc((size_t)(1 + P.naggs) * cap * 8, &tab);
+  if (rc == PHIP_OK && P.nhll) rc = P.alloc((size_t)P.nhll * cap * P.m_regs * 4, &hll);
+  if (rc == PHIP_OK) rc = P.alloc((size_t)cap * 8, &hk);
+  if (rc == PHIP_OK && P.first_doc) rc = P.alloc((size_t)cap * 4, &fd);
+  if (rc) return rc;
+  P.gtab = tab;
+  P.ghll = hll;
+  dq.gb_table = (uint64_t *)tab;
+  dq.gb_hll = (uint32_t *)hll;
+  dq.gb_keys = (uint64_t *)hk;
+  if (P.first_doc) {
+    P.first_doc = (uint32_t *)fd;
+    dq.first_doc = (uint32_t *)fd;
+  }
+  dq.num_groups = cap;
+  HIP_TRY(hipMemcpy(P.base + P.dq_off, &dq, sizeof(DevAggQuery), hipMemcpyHostToDevice));
+  return PHIP_OK;
+}
+
+static int32_t execute_growing(Plan &P, phip_result **out_result, uint64_t *filter_words) {
+  for (int g = 0;; g++) {
+    const int32_t rc = execute_plan(P, out_result, filter_words);
+    if (rc != kGrowHash) return rc;
+    if (g == kMaxHashGrowth)
+      return fail(PHIP_ERR_UNSUPPORTED, "group-by hash table still full after %d doublings", kMaxHashGrowth);
+    const int32_t grc = grow_hash_table(P);
+    if (grc) return grc;
+  }
+}
+
 // ================================================================================================
 // C ABI
 // ================================================================================================
@@ -5203,7 +5256,7 @@ PHIP_API int32_t phip_query(const phip_query_desc *query, phip_result **out_resu
   Plan plan;
   int32_t rc = prepare_plan(query, false, 0, plan);
   if (rc) return rc;
-  return execute_plan(plan, out_result, nullptr);
+  return execute_growing(plan, out_result, nullptr);
 }
 
 static int32_t create_single_plan(const phip_query_desc *query, uint64_t *out_plan);
@@ -5238,7 +5291,7 @@ PHIP_API int32_t phip_plan_execute(uint64_t plan, phip_result **out_result) {
     if (it == g_plans.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown plan handle %llu", (unsigned long long)plan);
     p = it->second.get();
   }
-  return execute_plan(*p, out_result, nullptr);
+  return execute_growing(*p, out_result, nullptr);
 }
 
 static int32_t find_plan(uint64_t plan, Plan **out) {
