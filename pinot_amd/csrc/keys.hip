@@ -49,6 +49,10 @@ __global__ void raw_key_ids_kernel(const void *__restrict__ raw, int32_t type, i
 // doc's bytes are compared with its representative's (a hash collision inside a segment sets *collided), the host
 // compares representatives across segments, sorts the distinct strings bytewise (the STRING dictionaries' order) and
 // hands back a segment-hash-index -> global-id map for raw_str_ids_kernel.
+// (a test hook narrows the hash -- PHIP_STR_HASH_BITS, set_str_hash_bits -- so collisions occur and the exact host path
+// that resolves them is exercised; all 64 bits otherwise)
+__device__ uint64_t g_str_hash_mask = ~0ull;
+
 __device__ __forceinline__ uint64_t str_hash64(const uint8_t *p, int64_t len) {
   uint64_t h = 0xcbf29ce484222325ull ^ (uint64_t)len;
   for (int64_t i = 0; i < len; i++) h = (h ^ p[i]) * 0x100000001b3ull;
@@ -56,7 +60,12 @@ __device__ __forceinline__ uint64_t str_hash64(const uint8_t *p, int64_t len) {
   h *= 0xff51afd7ed558ccdull;
   h ^= h >> 33;
   h *= 0xc4ceb9fe1a85ec53ull;
-  return h ^ (h >> 33);
+  return (h ^ (h >> 33)) & g_str_hash_mask;
+}
+
+hipError_t set_str_hash_bits(int bits) {
+  const uint64_t m = bits >= 64 || bits <= 0 ? ~0ull : ((1ull << bits) - 1ull);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_str_hash_mask), &m, sizeof(m));
 }
 
 __global__ void str_hash_kernel(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off, int64_t n,

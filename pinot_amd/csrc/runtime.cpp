@@ -115,6 +115,7 @@ hipError_t launch_str_verify(const uint8_t *bytes, const uint64_t *off, int64_t 
 hipError_t launch_str_rep_lens(const uint64_t *off, const int32_t *rep, int64_t u, uint32_t *lens, hipStream_t s);
 hipError_t launch_str_rep_bytes(const uint8_t *bytes, const uint64_t *off, const int32_t *rep, int64_t u,
                                 const uint64_t *dst_off, uint8_t *dst, hipStream_t s);
+hipError_t set_str_hash_bits(int bits);
 hipError_t launch_raw_str_ids(const uint8_t *bytes, const uint64_t *off, int64_t n, const uint64_t *uniq, int64_t u,
                               const int32_t *map, int32_t *ids, hipStream_t s);
 hipError_t launch_tuple_words(const TupleCols &tc, int64_t n, uint64_t *out, hipStream_t s);
@@ -1305,9 +1306,99 @@ static int32_t raw_real_key_ids(Device &dev, const std::vector<Segment *> &segs,
 // sorted and made unique on the device with a representative doc each, every doc is compared with its representative
 // (keys.hip), the representatives' bytes come to the host, which checks equal hashes across segments hold equal
 // strings, sorts the distinct strings bytewise (the STRING dictionaries' padded order) and maps each segment's hashes
-// to global ids for the doc-order id column. A hash collision refuses the plan (PHIP_ERR_UNSUPPORTED).
+// to global ids for the doc-order id column. A hash collision (two distinct strings, one 64-bit hash -- inside a segment
+// or across segments) takes raw_string_key_ids_exact instead.
+static int32_t raw_string_key_ids_exact(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
+                                        const std::string &name, Device::Remap &r);
+static constexpr int32_t kStrCollision = -101;  // raw_string_key_ids_hashed: the exact path decides
+
+static int32_t raw_string_key_ids_hashed(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
+                                         const std::string &name, Device::Remap &r);
+
 static int32_t raw_string_key_ids(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
                                   const std::string &name, Device::Remap &r) {
+  static int hash_bits_set = 64;  // (under the device mutex, as every remap build)
+  const char *hb = getenv("PHIP_STR_HASH_BITS");  // test hook: fewer hash bits, so collisions occur
+  const int hash_bits = hb ? atoi(hb) : 64;
+  if (hash_bits != hash_bits_set) {
+    HIP_TRY(set_str_hash_bits(hash_bits));
+    hash_bits_set = hash_bits;
+  }
+  const char *ex = getenv("PHIP_STR_KEYS_EXACT");  // test override: the exact path always
+  int32_t rc = ex && atoi(ex) != 0 ? kStrCollision : raw_string_key_ids_hashed(dev, segs, colidx, name, r);
+  if (rc == kStrCollision) {
+    r.ids.clear();
+    r.values.clear();
+    rc = raw_string_key_ids_exact(dev, segs, colidx, name, r);
+  }
+  return rc;
+}
+
+// Exact raw STRING keys on the host: every segment's values and offsets copied out, the distinct strings found with a
+// hash map of the bytes themselves (no fixed-width hash to collide), sorted bytewise, each doc's id copied back as the
+// doc-order id column. A host pass over the column's bytes -- taken only when the device hashes collided.
+static int32_t raw_string_key_ids_exact(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
+                                        const std::string &name, Device::Remap &r) {
+  hipStream_t st = dev.stream;
+  std::unordered_map<std::string, int32_t> first;  // string -> index in `distinct`
+  std::vector<const std::string *> distinct;
+  std::vector<std::vector<int32_t>> doc_ids(segs.size());
+  for (size_t i = 0; i < segs.size(); i++) {
+    const ColumnStore &c = segs[i]->cols[colidx[i]];
+    if (!no_dict(c) || c.fwd_kind != PHIP_FWD_RAW_CHUNK || c.type != PHIP_TYPE_STRING || c.str_off == nullptr)
+      return fail(PHIP_ERR_UNSUPPORTED, "group-by on column %s: raw in some segments only", name.c_str());
+    const int64_t n = segs[i]->num_docs;
+    if (n <= 0) continue;
+    std::vector<uint64_t> off((size_t)n + 1);
+    HIP_TRY(hipMemcpyAsync(off.data(), c.str_off, off.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint8_t> bytes(off[(size_t)n]);
+    if (!bytes.empty()) HIP_TRY(hipMemcpyAsync(bytes.data(), c.raw, bytes.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    doc_ids[i].resize((size_t)n);
+    for (int64_t d = 0; d < n; d++) {
+      std::string v((const char *)bytes.data() + off[(size_t)d], (size_t)(off[(size_t)d + 1] - off[(size_t)d]));
+      auto ins = first.emplace(std::move(v), (int32_t)distinct.size());
+      if (ins.second) {
+        if (distinct.size() >= (size_t)INT32_MAX)
+          return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw column %s: over 2^31 distinct values", name.c_str());
+        distinct.push_back(&ins.first->first);
+      }
+      doc_ids[i][(size_t)d] = ins.first->second;
+    }
+  }
+  std::vector<int32_t> order(distinct.size());
+  for (size_t g = 0; g < order.size(); g++) order[g] = (int32_t)g;
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return *distinct[a] < *distinct[b]; });
+  std::vector<int32_t> rank(distinct.size());
+  size_t width = 1;
+  for (size_t g = 0; g < order.size(); g++) {
+    rank[(size_t)order[g]] = (int32_t)g;
+    width = std::max(width, distinct[(size_t)order[g]]->size());
+  }
+  r.values.assign(distinct.size() * width, 0);
+  for (size_t g = 0; g < order.size(); g++)
+    memcpy(r.values.data() + g * width, distinct[(size_t)order[g]]->data(), distinct[(size_t)order[g]]->size());
+  r.ids.assign(segs.size(), nullptr);
+  for (size_t i = 0; i < segs.size(); i++) {
+    const int64_t n = segs[i]->num_docs;
+    void *p;
+    HIP_TRY(hipMalloc(&p, std::max<size_t>((size_t)n * 4, 16)));
+    r.ids[i] = (int32_t *)p;  // owned by r from here
+    if (n <= 0) continue;
+    for (auto &id : doc_ids[i]) id = rank[(size_t)id];
+    HIP_TRY(hipMemcpyAsync(p, doc_ids[i].data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  r.type = PHIP_TYPE_STRING;
+  r.width = (int32_t)width;
+  r.card = (int32_t)distinct.size();
+  r.dev.assign(segs.size(), nullptr);
+  return PHIP_OK;
+}
+
+static int32_t raw_string_key_ids_hashed(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
+                                         const std::string &name, Device::Remap &r) {
   hipStream_t st = dev.stream;
   std::vector<void *> tmp;
   struct Free {
@@ -1371,7 +1462,7 @@ static int32_t raw_string_key_ids(Device &dev, const std::vector<Segment *> &seg
     if (!hb.empty()) HIP_TRY(hipMemcpyAsync(hb.data(), dst, hb.size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(&collided, flag, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (collided) return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw STRING column %s: 64-bit hash collision", name.c_str());
+    if (collided) return kStrCollision;  // (two strings of this segment share a hash)
     seg_str[i].resize((size_t)u);
     for (int64_t j = 0; j < u; j++)
       seg_str[i][(size_t)j].assign((const char *)hb.data() + ho[(size_t)j], hl[(size_t)j]);
@@ -1385,8 +1476,7 @@ static int32_t raw_string_key_ids(Device &dev, const std::vector<Segment *> &seg
     for (size_t j = 0; j < seg_str[i].size(); j++) {
       auto ins = by_hash.emplace(seg_hash[i][j], &seg_str[i][j]);
       if (!ins.second) {
-        if (*ins.first->second != seg_str[i][j])
-          return fail(PHIP_ERR_UNSUPPORTED, "group-by on raw STRING column %s: 64-bit hash collision", name.c_str());
+        if (*ins.first->second != seg_str[i][j]) return kStrCollision;  // (two segments' strings share a hash)
       } else {
         distinct.push_back(&seg_str[i][j]);
       }

@@ -129,6 +129,7 @@ hipError_t launch_materialize_packed(const uint32_t *, int32_t, const void *, in
   return hipSuccess;
 }
 hipError_t launch_raw_images(const void *, int32_t, int64_t, uint64_t *, hipStream_t) { return hipSuccess; }
+hipError_t set_str_hash_bits(int) { return hipSuccess; }
 hipError_t launch_str_hash_unique(void *temp, size_t *temp_bytes, const uint8_t *, const uint64_t *, int64_t, uint64_t *,
                                   int32_t *, uint64_t *, int32_t *, uint64_t *, int32_t *, int64_t *num_out, hipStream_t) {
   if (!temp) *temp_bytes = 64;

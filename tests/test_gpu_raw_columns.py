@@ -147,3 +147,36 @@ def test_gpu_distinctcounthll_raw_columns(sql, raw_segments):
     if not qc.order_by:  # (no ORDER BY: the broker's rows come in table order; compare as sets)
         got, want = sorted(got), sorted(want)
     assert got == want
+
+
+@pytest.mark.parametrize("how", ["collide", "exact"])
+def test_gpu_raw_string_keys_hash_collisions(how, gpu_lib, monkeypatch):
+    """Raw STRING group keys whose 64-bit device hashes collide take the exact host path (every doc's bytes keyed by
+    themselves) instead of refusing the plan (round 5: PHIP_ERR_UNSUPPORTED). PHIP_STR_HASH_BITS=6 narrows the hash to
+    64 values for ~300 distinct strings, so collisions occur inside and across segments; PHIP_STR_KEYS_EXACT=1 takes
+    the exact path outright. Both equal the oracle."""
+    if how == "collide":
+        monkeypatch.setenv("PHIP_STR_HASH_BITS", "6")
+    else:
+        monkeypatch.setenv("PHIP_STR_KEYS_EXACT", "1")
+    rng = np.random.default_rng(71 if how == "collide" else 72)
+    raws = []
+    for s in range(3):
+        n = 9000 + 101 * s
+        c = SegmentCreator(f"sc{how}{s}", no_dictionary_columns=["rs"])
+        words = np.array([f"w{j}-{'x' * (j % 7)}" for j in range(80 * s, 80 * s + 150)] + ["", "zé", "日本"], dtype=object)
+        c.add_column("rs", DataType.STRING, words[rng.integers(0, len(words), n)])
+        c.add_column("m", DataType.LONG, rng.integers(-10 ** 6, 10 ** 6, n))
+        c.add_column("f", DataType.INT, rng.integers(0, 100, n))
+        raws.append(c.build())
+    segs = _segs(raws)
+    try:
+        for sql in ("SELECT rs, COUNT(*), SUM(m) FROM t GROUP BY rs LIMIT 100000",
+                    "SELECT rs, f, MAX(m) FROM t WHERE f < 20 GROUP BY rs, f LIMIT 100000"):
+            qc = parse(sql)
+            gblk = _gpu().make_instance_plan(qc, segs).next_block()
+            oblk, exact = executor.execute(qc, raws)
+            _check(qc, gblk, oblk, exact)
+    finally:
+        for g in segs:
+            g.destroy()
