@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6: completion polling + timing markers off -- correctness subset, then a host A/B of the sorted headline step
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused.py tests/test_gpu_concurrency.py tests/test_gpu_query_options.py tests/test_gpu_filter_programs.py tests/test_gpu_poll_done.py tests/test_gpu_hash_growth.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r06i_pytest.log 2>&1 || { tail -30 gpurun_out/r06i_pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused.py tests/test_gpu_concurrency.py tests/test_gpu_query_options.py tests/test_gpu_filter_programs.py tests/test_gpu_poll_done.py tests/test_gpu_hash_growth.py tests/test_gpu_raw_columns.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r06i_pytest.log 2>&1 || { tail -30 gpurun_out/r06i_pytest.log; exit 1; }
 tail -2 gpurun_out/r06i_pytest.log
 B="--group-by= --configs= --layout sorted --no-cpu-baseline --no-parity --no-concurrent --steps 30 --warmup 5"
 : > gpurun_out/r06i_ab.log
