@@ -463,10 +463,13 @@ PHIP_API int32_t phip_plan_abandon_partial(uint64_t plan);
  *   - where the devices cannot share a communicator (two parts on one device, no loadable librccl) the non-root
  *     tables are copied to the root device (hipMemcpyPeerAsync) and folded in by the library's merge kernel, the same
  *     operators;
- *   - aggregation-only queries (one group) and group-bys without a dense partial table (hash-table key spaces, a
- *     device reaching numGroupsLimit -- the per-segment first-seen limit --, raw group-by keys, tuple keys) run each
- *     sub-plan to its records and merge them on the host by key VALUE, as the reference's combine does (untrimmed:
- *     the broker's ORDER BY / LIMIT applies to exact groups).
+ *   - hash-table key spaces (node-global keys, each part's table sized for every doc of the node): the non-root
+ *     parts' keys, rows and registers are copied to the root device and inserted into the root's table by key
+ *     (PHIP_EXCHANGE_HASH), then finished as above;
+ *   - aggregation-only queries (one group) and group-bys without a mergeable partial table (a device reaching
+ *     numGroupsLimit -- the per-segment first-seen limit --, a full hash table, raw group-by keys, tuple keys, parts
+ *     whose null keys differ) run each sub-plan to its records and merge them on the host by key VALUE, as the
+ *     reference's combine does (untrimmed: the broker's ORDER BY / LIMIT applies to exact groups).
  * Statistics are summed over the devices; segment_docs_matched covers every segment in query order; kernel times
  * are the slowest device's. Selection queries over several devices return PHIP_ERR_UNSUPPORTED. The deadline and
  * cancel calls apply to every sub-plan. phip_plan_execute_partial / phip_plan_finish / phip_plan_abandon_partial on
@@ -478,6 +481,7 @@ PHIP_API int32_t phip_plan_abandon_partial(uint64_t plan);
 #define PHIP_EXCHANGE_RCCL 1    /* the last execution reduced the partial tables with RCCL */
 #define PHIP_EXCHANGE_PEER 2    /* ... copied them to the root device and merged them with the merge kernel */
 #define PHIP_EXCHANGE_RECORDS 3 /* ... merged the sub-plans' records on the host */
+#define PHIP_EXCHANGE_HASH 4    /* ... inserted the other sub-plans' hash-table groups into the root's table on the root device */
 /* Devices (sub-plans) of a plan and the exchange its last execution used (PHIP_EXCHANGE_*; NONE before the first). */
 PHIP_API int32_t phip_plan_exchange(uint64_t plan, int32_t *out_parts, int32_t *out_kind);
 

@@ -48,6 +48,7 @@ EXCHANGE_NONE = 0
 EXCHANGE_RCCL = 1
 EXCHANGE_PEER = 2
 EXCHANGE_RECORDS = 3
+EXCHANGE_HASH = 4
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 

@@ -411,8 +411,9 @@ hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream
 // q: host copy (for the variant choice); dq: the same descriptor in device memory.
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0,
                       hipEvent_t e1) {
-  if (q.mode == GB_LDS && q.wg_waves == 16 && q.dense_batch)
-    return launch_agg_t<1, GB_LDS, true, 16>(dq, nblocks, lds, s, e0, e1);
+  if (q.mode == GB_LDS && q.wg_waves == 16)
+    return q.dense_batch ? launch_agg_t<1, GB_LDS, true, 16>(dq, nblocks, lds, s, e0, e1)
+                         : launch_agg_t<1, GB_LDS, false, 16>(dq, nblocks, lds, s, e0, e1);
   if (q.mode == GB_LDS)
     return q.dense_batch ? launch_agg_t<1, GB_LDS, true>(dq, nblocks, lds, s, e0, e1) : launch_agg_t<1, GB_LDS>(dq, nblocks, lds, s, e0, e1);
   if (q.mode == GB_GLOBAL)

@@ -328,8 +328,8 @@ struct DevAggQuery {
   int32_t own_count_rows;  // group-by over several filter programs (FILTER + GROUP BY): every COUNT counts its own
                            // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
   const DevFinal *fin;     // GB_NONE: non-null when this launch is the plan's last (agg_common.h finalize_tail)
-  int32_t wg_waves;        // waves per workgroup of the launch (kAggWaves; 16 for a batched GB_LDS table that leaves
-  int32_t pad_w;           // one 8-wave workgroup per CU)
+  int32_t wg_waves;        // waves per workgroup of the launch (kAggWaves; 16 for a GB_LDS table that leaves fewer
+  int32_t pad_w;           // 8-wave workgroups per CU than it leaves 16-wave ones x 2)
   int64_t xcd_words;       // GB_XCD: u64 words of one table copy ((1 + num_aggs) x num_groups)
   int64_t xcd_hll_words;   // GB_XCD: u32 words of one copy's HLL registers (num_hll x num_groups x m)
 };

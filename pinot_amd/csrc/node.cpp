@@ -461,6 +461,61 @@ int32_t exchange_peer(NodePlan &np, std::vector<phip_partial> &pa, const int32_t
   return PHIP_OK;
 }
 
+// Hash-table parts: each non-root part's keys, rows and registers (copied to the root device over xGMI when they live on
+// another GPU) are inserted into the root part's table by key (node_merge.hip hash_merge_*). The root's table was sized
+// for every doc of the node (node_plan_create), so it holds the union unless a capacity override shrank it (*full).
+int32_t exchange_hash(NodePlan &np, std::vector<phip_partial> &pa, const std::vector<NodeGroupInfo> &gi,
+                      const int32_t *kinds, bool *full) {
+  *full = false;
+  const Part &root = np.parts[0];
+  const int rows = pa[0].num_rows, nhll = pa[0].num_hll, log2m = pa[0].log2m;
+  int64_t smax = 0;
+  bool remote = false;
+  for (size_t i = 1; i < np.parts.size(); i++) {
+    smax = std::max<int64_t>(smax, pa[i].num_groups);
+    remote |= np.parts[i].ordinal != root.ordinal;
+  }
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t kb = al((size_t)smax * 8), tb = al((size_t)rows * smax * 8),
+               hb = al(nhll ? ((size_t)nhll * smax << log2m) * 4 : 0);
+  const size_t head = 256 + kb;  // overflow flag | slot map
+  const size_t need = head + (remote ? kb + tb + hb : 0);
+  NODE_HIP(hipSetDevice(root.ordinal));
+  if (np.stage_bytes < need) {
+    if (np.stage) NODE_HIP(hipFree(np.stage));
+    np.stage = nullptr;
+    np.stage_bytes = 0;
+    NODE_HIP(hipMalloc(&np.stage, need));
+    np.stage_bytes = need;
+  }
+  uint8_t *st = (uint8_t *)np.stage;
+  uint32_t *ovf = (uint32_t *)st;
+  int64_t *map = (int64_t *)(st + 256);
+  NODE_HIP(hipMemsetAsync(ovf, 0, 4, root.stream));
+  for (size_t i = 1; i < np.parts.size(); i++) {
+    const int64_t sg = pa[i].num_groups;
+    const uint64_t *skeys = gi[i].keys, *stab = pa[i].table;
+    const uint32_t *shll = pa[i].hll;
+    if (np.parts[i].ordinal != root.ordinal) {
+      uint8_t *c = st + head;
+      const int o = np.parts[i].ordinal;
+      NODE_HIP(hipMemcpyPeerAsync(c, root.ordinal, skeys, o, (size_t)sg * 8, root.stream));
+      NODE_HIP(hipMemcpyPeerAsync(c + kb, root.ordinal, stab, o, (size_t)rows * sg * 8, root.stream));
+      if (nhll) NODE_HIP(hipMemcpyPeerAsync(c + kb + tb, root.ordinal, shll, o, ((size_t)nhll * sg << log2m) * 4, root.stream));
+      skeys = (const uint64_t *)c;
+      stab = (const uint64_t *)(c + kb);
+      shll = (const uint32_t *)(c + kb + tb);
+    }
+    NODE_HIP(launch_hash_merge(const_cast<uint64_t *>(gi[0].keys), pa[0].table, pa[0].hll, pa[0].num_groups, skeys, stab,
+                               shll, sg, kinds, rows, nhll, log2m, map, ovf, root.stream));
+  }
+  uint32_t h_ovf = 0;
+  NODE_HIP(hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, root.stream));
+  NODE_HIP(hipStreamSynchronize(root.stream));
+  *full = h_ovf != 0;
+  return PHIP_OK;
+}
+
 int32_t execute_dense(NodePlan &np, phip_result **out, bool *fell_back) {
   *fell_back = false;
   const size_t n = np.parts.size();
@@ -479,14 +534,28 @@ int32_t execute_dense(NodePlan &np, phip_result **out, bool *fell_back) {
   };
   bool records = false;
   for (size_t i = 0; i < n; i++) {
-    if (runs[i].rc == PHIP_ERR_UNSUPPORTED) records = true;  // hash table / numGroupsLimit reached on a device
+    if (runs[i].rc == PHIP_ERR_UNSUPPORTED) records = true;  // full hash table / numGroupsLimit reached on a device
     else if (runs[i].rc) {
       abandon(0);
       return node_fail(runs[i].rc, "%s", runs[i].err.c_str());
-    } else if (!pa[i].global_keys || pa[i].num_groups != pa[0].num_groups || pa[i].num_rows != pa[0].num_rows) {
-      records = true;  // raw / tuple keys: the devices' key orders differ
     }
   }
+  // The parts' keys must mean the same groups: node-global dictionaries (raw / tuple keys: each device's own ids, the
+  // record path) and one mixed radix (a null key adds a dimension value only where some segment holds nulls). Dense
+  // tables then align slot for slot; hash tables hold the same keys in different slots (exchange_hash).
+  std::vector<NodeGroupInfo> gi(n);
+  for (size_t i = 0; i < n && !records; i++) {
+    int32_t rc = node_plan_group_info(np.parts[i].plan, &gi[i]);
+    if (rc) {
+      abandon(0);
+      return rc;
+    }
+  }
+  const bool hash = !records && gi[0].hash;
+  for (size_t i = 0; i < n && !records; i++)
+    if (!pa[i].global_keys || gi[i].tuple || gi[i].hash != hash || gi[i].radix != gi[0].radix ||
+        pa[i].num_rows != pa[0].num_rows || (!hash && pa[i].num_groups != pa[0].num_groups) || (hash && !gi[i].keys))
+      records = true;
   if (records) {
     abandon(0);
     *fell_back = true;
@@ -512,7 +581,16 @@ int32_t execute_dense(NodePlan &np, phip_result **out, bool *fell_back) {
       }
   int32_t rc = PHIP_OK;
   int32_t kind = PHIP_EXCHANGE_NONE;
-  if (n > 1 || env_int("PHIP_NODE_SPLIT", 0) > 0) {
+  if (hash && n > 1) {
+    bool full = false;
+    rc = exchange_hash(np, pa, gi, kinds, &full);
+    kind = PHIP_EXCHANGE_HASH;
+    if (rc == PHIP_OK && full) {  // the root's table cannot take every group (a capacity override): the record path
+      abandon(0);
+      *fell_back = true;
+      return PHIP_OK;
+    }
+  } else if (n > 1 || env_int("PHIP_NODE_SPLIT", 0) > 0) {
     const char *force = getenv("PHIP_NODE_EXCHANGE");
     const bool want_peer = force && !strcmp(force, "peer");
     const bool need_rccl = force && !strcmp(force, "rccl");
@@ -667,18 +745,26 @@ int32_t node_create(const phip_query_desc *q, uint64_t *out_plan) {
     nd.gen = g_dict_gen++;
     dicts[name] = std::move(nd);
   }
+  int64_t node_docs = 0;
+  for (int i = 0; i < q->num_segments; i++) {
+    int d = 0;
+    int64_t nd = 0;
+    int32_t rc = node_segment_device(q->segments[i], &d, &nd);
+    if (rc) return rc;
+    node_docs += nd;
+  }
   const bool trims = np->group_by && (q->trim_size > 0 || q->num_order_terms > 0 || q->num_order_by_keys > 0 ||
                                       q->order_by_aggregation >= 0);
   for (auto &p : np->parts) {
     SubDesc sd;
     make_sub(q, p, false, sd);
-    int32_t rc = node_plan_create(&sd.q, &dicts, &p.plan);
+    int32_t rc = node_plan_create(&sd.q, &dicts, node_docs, &p.plan);
     if (rc) return rc;
     p.rplan = p.plan;
     if (trims) {
       SubDesc rd;
       make_sub(q, p, true, rd);
-      if ((rc = node_plan_create(&rd.q, &dicts, &p.rplan))) return rc;
+      if ((rc = node_plan_create(&rd.q, &dicts, node_docs, &p.rplan))) return rc;
     }
     NODE_HIP(hipSetDevice(p.ordinal));
     NODE_HIP(hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));

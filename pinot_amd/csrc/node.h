@@ -50,12 +50,21 @@ struct NodeResultData {
 
 // ---- runtime.cpp hooks -------------------------------------------------------------------------------------------
 int32_t node_fail(int32_t code, const char *fmt, ...);
-int32_t node_segment_device(uint64_t handle, int *ordinal);
+int32_t node_segment_device(uint64_t handle, int *ordinal, int64_t *docs = nullptr);
 // The sorted union of `column`'s dictionary values over the segments; *ok = false when some segment holds the column
 // without a dictionary (raw keys: the record path) or the types differ.
 int32_t node_union_dictionary(const std::vector<uint64_t> &handles, const std::string &column, NodeDict *out, bool *ok);
-// phip_plan_create of one device's part, its group-by columns keyed by `dicts` (nullptr: as phip_plan_create).
-int32_t node_plan_create(const phip_query_desc *q, const NodeDicts *dicts, uint64_t *out_plan);
+// phip_plan_create of one device's part, its group-by columns keyed by `dicts` (nullptr: as phip_plan_create);
+// node_docs = the docs of every segment of the node plan (a hash table is sized for all of them).
+int32_t node_plan_create(const phip_query_desc *q, const NodeDicts *dicts, int64_t node_docs, uint64_t *out_plan);
+// A part's group keys: the mixed radix per key column (tuple keys: per tuple dimension) and, for a hash table, its
+// device key array ([capacity] u64, kHashEmpty = free slot).
+struct NodeGroupInfo {
+  bool hash = false, tuple = false;
+  std::vector<int64_t> radix;
+  const uint64_t *keys = nullptr;
+};
+int32_t node_plan_group_info(uint64_t plan, NodeGroupInfo *out);
 // The per-segment / per-program matched docs of the plan's last execution (valid after execute / execute_partial).
 int32_t node_plan_docs(uint64_t plan, std::vector<int64_t> *seg_docs, std::vector<int64_t> *prog_docs);
 int32_t node_make_result(NodeResultData &&d, phip_result **out);
@@ -85,6 +94,12 @@ hipError_t launch_partial_merge_rows(uint64_t *dst, const uint64_t *src, const i
 hipError_t launch_max_u32(uint32_t *dst, const uint32_t *src, int64_t n, hipStream_t s);
 hipError_t launch_max_u8(uint8_t *dst, const uint8_t *src, int64_t n, hipStream_t s);
 hipError_t launch_i64_row_to_f64(uint64_t *row, int64_t n, hipStream_t s);
+// Inserts every occupied slot of a source hash table (keys [sg], rows [rows][sg], HLL u32 [nhll][sg][m]) into the
+// destination table (the root part's: [dg] ...), combining the rows by kind and the registers by max. map[sg] receives
+// each source slot's destination slot (-1: free); *overflow is set when the destination has no free slot left.
+hipError_t launch_hash_merge(uint64_t *dkeys, uint64_t *dtab, uint32_t *dhll, int64_t dg, const uint64_t *skeys,
+                             const uint64_t *stab, const uint32_t *shll, int64_t sg, const int32_t *kinds, int rows,
+                             int nhll, int log2m, int64_t *map, uint32_t *overflow, hipStream_t s);
 
 }  // namespace phip
 

@@ -1662,6 +1662,9 @@ static int32_t build_tuple_keys(Device &dev, const std::vector<Segment *> &segs,
 // (skip_nulls: a null-key column -- a raw column's id range then covers its non-null values only)
 // The node plan being prepared on this thread (node_plan_create): its group-by columns' node-global dictionaries.
 static thread_local const NodeDicts *tl_node_dicts = nullptr;
+// ... and the docs of the whole node plan (0: not a part). A part sizes a hash table for every doc of the node, so the
+// root's table can take the other parts' groups (node.cpp exchange_hash) and every part decides dense vs hash alike.
+static thread_local int64_t tl_node_docs = 0;
 
 int32_t build_remap(Device &dev, const std::vector<Segment *> &segs, const std::vector<int> &colidx,
                     const std::string &name, std::shared_ptr<Device::Remap> &out, bool skip_nulls = false) {
@@ -2026,6 +2029,7 @@ struct Plan {
   bool fused_gb = false;  // the filter kernel runs the dense group-by into the HBM table (no aggregation launch)
   bool gb_xcd = false;    // ... into kXcdCopies XCD-private copies of it (GB_XCD), merged after the launch
   bool gb_lds = false;    // ... into each workgroup's LDS table (GB_LDS), its slabs reduced after the launch
+  bool node_part = false;  // a node plan's part (node_plan_create): a hash table may go out as a partial table
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
   int filter_blocks = 1, agg_blocks = 8;
@@ -2635,6 +2639,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     // number of groups possible (min of key space and docs), so probe sequences stay short.
     int64_t docs = 0;
     for (int s = 0; s < nseg; s++) docs += segs[s]->num_docs;
+    if (tl_node_docs > 0) docs = tl_node_docs;  // a node plan's part: the node's docs bound the groups
     const char *hm = getenv("PHIP_GB_HASH");  // measurement override: "1" forces the hash table
     const bool force_hash = hm && atoi(hm) != 0;
     gb_key_space = stride;
@@ -3026,7 +3031,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   if (hll_made) HIP_TRY(hipStreamSynchronize(st));
   if (total_work > INT32_MAX / 2) return fail(PHIP_ERR_UNSUPPORTED, "too many tiles in one query");
   dq.total_work = (int32_t)total_work;
-  if (group_by && gb_key_space > ((int64_t)1 << 22)) {
+  if (group_by && gb_key_space > ((int64_t)1 << 22) && tl_node_docs == 0) {  // (node parts: sized by the node's docs)
     // Re-size a large group table from the docs of the work tiles (sorted-index pruning already cut them):
     // only those docs can create groups, and the table is cleared and compacted on every execution
     // (BenchmarkQueries STARTREE_FILTER_QUERY: one candidate tile, yet 2 x 10M hash slots before).
@@ -3639,15 +3644,19 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dq.hll_words = (int32_t)hll_words;
       agg_lds += (size_t)round_up(table_bytes, 16);
       agg_bpc = std::max(1, std::min(4, (int)((160 * 1024 - 1024) / agg_lds)));
-      // A table that leaves one 8-wave workgroup per CU (Q2.1's 7000 groups x 16 B = 112 KB): 16-wave workgroups share
-      // it, so the CU keeps 16 waves of gathers in flight instead of 8 (SQ: the 8-wave walk spent 76 % of its wave
-      // cycles in s_waitcnt, profiles/r05l_sq_gb.txt). PHIP_GB_WAVES=8 keeps 8-wave workgroups (A/B).
+      // A table that leaves fewer than four 8-wave workgroups per CU (Q2.1's 7000 groups x 16 B = 112 KB: one; C5's
+      // 175 keys x (24 B + 256 HLL registers) = 49 KB: three): 16-wave workgroups share it, so the CU keeps more waves
+      // of gathers in flight (Q2.1: 16 instead of 8 -- SQ: the 8-wave walk spent 76 % of its wave cycles in s_waitcnt,
+      // profiles/r05l_sq_gb.txt; C5: 32 instead of 24). PHIP_GB_WAVES=8 / 16 forces either (A/B).
       const char *gw = getenv("PHIP_GB_WAVES");
       const size_t lds16 = (size_t)16 * ring_entries(GB_LDS, batched) * 4 + (size_t)16 * dq.stage_bytes +
                            (size_t)round_up(table_bytes, 16);
-      if (batched && agg_bpc == 1 && lds16 <= (size_t)159 * 1024 && !(gw && atoi(gw) == 8)) {
+      const int bpc16 = lds16 <= (size_t)159 * 1024 ? std::max(1, std::min(2, (int)((160 * 1024 - 1024) / lds16))) : 0;
+      const bool want16 = gw ? atoi(gw) == 16 : 16 * bpc16 > kAggWaves * agg_bpc;
+      if (want16 && bpc16 > 0) {
         dq.wg_waves = 16;
         agg_lds = lds16;
+        agg_bpc = bpc16;
       }
     }
   } else if (nhll) {
@@ -3901,6 +3910,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.need_agg = need_agg;
   P.need_mask = need_mask;
   P.group_by = group_by;
+  P.node_part = tl_node_docs > 0;
   P.conj_only = conj_only;
   P.fused_naggs = fused_naggs;
   P.fused_gb = fused_gb;
@@ -4399,7 +4409,8 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
                             phip_partial *part = nullptr, const phip_partial *merged = nullptr) {
   Device *dev = P.dev;
   std::lock_guard<std::mutex> xlock(P.exec_mu);
-  if (mode != EXEC_FULL && (!P.group_by || P.dq.mode == GB_HASH))
+  // (a node part's hash table goes out too: node.cpp inserts the other parts' groups into the root's table)
+  if (mode != EXEC_FULL && (!P.group_by || (P.dq.mode == GB_HASH && !P.node_part)))
     return fail(PHIP_ERR_UNSUPPORTED, "partial tables: dense group-by and aggregation plans only (this plan: %s)",
                 P.group_by ? "hash-table key space" : "selection");
   if (mode == EXEC_FINISH) {
@@ -4596,6 +4607,12 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
       if (P.num_groups_limit > 0 && ngroups >= P.num_groups_limit)
         return fail(PHIP_ERR_UNSUPPORTED, "partial table: %lld groups reach numGroupsLimit %lld", (long long)ngroups,
                     (long long)P.num_groups_limit);
+      if (dq.mode == GB_HASH) {  // a full table cannot go out: the node plan takes the record path (which grows it)
+        uint32_t ovf = 0;
+        HIP_TRY(hipMemcpyAsync(&ovf, dq.hash_overflow, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (ovf) return fail(PHIP_ERR_UNSUPPORTED, "partial table: the group-by hash table is full");
+      }
       memset(part, 0, sizeof(*part));
       part->num_groups = dq.num_groups;
       part->num_rows = 1 + naggs;
@@ -5580,11 +5597,12 @@ int32_t phip::node_fail(int32_t code, const char *fmt, ...) {
   return code;
 }
 
-int32_t phip::node_segment_device(uint64_t handle, int *ordinal) {
+int32_t phip::node_segment_device(uint64_t handle, int *ordinal, int64_t *docs) {
   std::lock_guard<std::mutex> g(g_mu);
   auto it = g_segments.find(handle);
   if (it == g_segments.end()) return fail(PHIP_ERR_NOT_FOUND, "unknown segment handle %llu", (unsigned long long)handle);
   *ordinal = it->second->device;
+  if (docs) *docs = it->second->num_docs;
   return PHIP_OK;
 }
 
@@ -5647,11 +5665,24 @@ int32_t phip::node_union_dictionary(const std::vector<uint64_t> &handles, const 
   return PHIP_OK;
 }
 
-int32_t phip::node_plan_create(const phip_query_desc *q, const NodeDicts *dicts, uint64_t *out_plan) {
+int32_t phip::node_plan_create(const phip_query_desc *q, const NodeDicts *dicts, int64_t node_docs, uint64_t *out_plan) {
   tl_node_dicts = dicts;
+  tl_node_docs = std::max<int64_t>(node_docs, 1);
   const int32_t rc = create_single_plan(q, out_plan);
   tl_node_dicts = nullptr;
+  tl_node_docs = 0;
   return rc;
+}
+
+int32_t phip::node_plan_group_info(uint64_t plan, NodeGroupInfo *out) {
+  Plan *p;
+  int32_t rc = find_plan(plan, &p);
+  if (rc) return rc;
+  out->hash = p->group_by && p->dq.mode == GB_HASH;
+  out->tuple = p->tuple_keys;
+  out->radix = p->tuple_keys ? p->tuple_radix : p->gb_radix;
+  out->keys = out->hash ? p->dq.gb_keys : nullptr;
+  return PHIP_OK;
 }
 
 int32_t phip::node_plan_docs(uint64_t plan, std::vector<int64_t> *seg_docs, std::vector<int64_t> *prog_docs) {

@@ -682,7 +682,8 @@ class GpuCombineOperator:
     def exchange(self):
         """(devices, exchange kind) of the prepared plan (phip_plan_exchange): a plan over segments on several devices
         is a node plan whose sub-plans' partials meet in an RCCL reduce (_lib.EXCHANGE_RCCL), a peer merge
-        (EXCHANGE_PEER) or the host record merge (EXCHANGE_RECORDS); (1, EXCHANGE_NONE) for one device."""
+        (EXCHANGE_PEER), a hash-table insert on the root device (EXCHANGE_HASH) or the host record merge
+        (EXCHANGE_RECORDS); (1, EXCHANGE_NONE) for one device."""
         if getattr(self, "_plan", None) is None:
             return 1, _lib.EXCHANGE_NONE
         parts, kind = ctypes.c_int32(0), ctypes.c_int32(0)

@@ -82,6 +82,35 @@ hipError_t launch_i64_row_to_f64(uint64_t *row, int64_t n, hipStream_t) {
   }
   return hipSuccess;
 }
+hipError_t launch_hash_merge(uint64_t *dkeys, uint64_t *dtab, uint32_t *dhll, int64_t dg, const uint64_t *skeys,
+                             const uint64_t *stab, const uint32_t *shll, int64_t sg, const int32_t *kinds, int rows,
+                             int nhll, int log2m, int64_t *map, uint32_t *overflow, hipStream_t) {
+  if (dg <= 0 || (dg & (dg - 1)) || sg <= 0) return hipErrorInvalidValue;
+  const uint64_t mask = (uint64_t)dg - 1;
+  for (int64_t s = 0; s < sg; s++) {
+    map[s] = -1;
+    if (skeys[s] == kHashEmpty) continue;
+    uint64_t i = (skeys[s] * 0x9e3779b97f4a7c15ull) & mask;
+    for (uint64_t p = 0; p <= mask; p++, i = (i + 1) & mask) {
+      if (dkeys[i] == kHashEmpty) dkeys[i] = skeys[s];
+      if (dkeys[i] == skeys[s]) {
+        map[s] = (int64_t)i;
+        break;
+      }
+    }
+    if (map[s] < 0) {
+      *overflow = 1;
+      continue;
+    }
+    for (int r = 0; r < rows; r++) {
+      const int32_t k[1] = {kinds[r]};
+      launch_partial_merge_rows(dtab + r * dg + map[s], stab + r * sg + s, k, 1, 1, nullptr);
+    }
+    for (int h = 0; h < nhll; h++)
+      launch_max_u32(dhll + ((h * dg + map[s]) << log2m), shll + ((h * sg + s) << log2m), (int64_t)1 << log2m, nullptr);
+  }
+  return hipSuccess;
+}
 hipError_t launch_bswap32(uint32_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_bswap64(uint64_t *, int64_t, hipStream_t) { return hipSuccess; }
 hipError_t launch_trim_order(const double *, const int64_t *, const KeyOrder *, int64_t n, int32_t, int32_t, int32_t, void *scratch,

@@ -44,6 +44,14 @@ assert len(blk.groups) == 1, blk.groups  # key 0, marked in every part's table
 assert len(blk.segment_docs_matched) == len(segs), blk.segment_docs_matched
 assert blk.stats.num_segments_processed == len(segs), blk.stats
 dense.close()
+# hash-table key space (forced): the parts' tables are inserted into the root's by key (node_merge.hip hash_merge_*)
+os.environ["PHIP_GB_HASH"] = "1"
+hashed = GpuCombineOperator(parse("SELECT h, g, COUNT(*), SUM(m), MAX(m) FROM t GROUP BY h, g LIMIT 1000"), segs, 100000)
+hashed.next_block()
+parts, kind = hashed.exchange()
+assert parts == ndev and kind == _lib.EXCHANGE_HASH, (parts, kind)
+hashed.close()
+del os.environ["PHIP_GB_HASH"]
 for q in ("SELECT COUNT(*), SUM(m), MIN(m), DISTINCTCOUNTHLL(h) FROM t WHERE h < 3",  # one group: the host merge
           "SELECT r, COUNT(*), SUM(m) FROM t GROUP BY r LIMIT 1000",  # raw key: each device its own ids -> records
           "SELECT g, h, SUM(m) FROM t GROUP BY g, h ORDER BY SUM(m) DESC LIMIT 3"):  # trim: the record sub-plans

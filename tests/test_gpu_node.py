@@ -206,3 +206,57 @@ def test_gpu_node_repeated_executions(ssb_sf1, monkeypatch):
             for a, b in zip(again.groups[k], v):
                 assert np.array_equal(np.asarray(a), np.asarray(b))
     op.close()
+
+
+HASHED = [MIXED[0][0], MIXED[1][0], MIXED[2][0], MIXED[3][0],
+          "SELECT h, l, COUNT(*), SUM(d), MIN(m) FROM t WHERE d > 20 GROUP BY h, l LIMIT 100000"]
+
+
+@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("sql", HASHED, ids=[f"h{i}" for i in range(len(HASHED))])
+def test_gpu_node_hash_tables(sql, split, mixed, monkeypatch):
+    """Hash-table group-bys (PHIP_GB_HASH=1 forces the open-addressing table, as a key space above 2^26 does): each part's
+    table holds the same node-global keys in its own slots, so the exchange inserts the non-root parts' groups into the
+    root's table by key (node_merge.hip hash_merge_*) and the root finishes it -- groups, sums, MIN / MAX, HLL registers
+    and the trimmed ORDER BY equal the oracle's."""
+    raws, segs = mixed
+    monkeypatch.setenv("PHIP_GB_HASH", "1")
+    qc, blk, parts, kind = _run(sql, segs, monkeypatch, split)
+    assert parts == split and kind == _lib.EXCHANGE_HASH, (parts, kind)
+    _check(qc, blk, raws)
+    got, want = reduce_blocks(qc, [blk]).rows, reduce_blocks(qc, [executor.execute(qc, raws)[0]]).rows
+    if not qc.order_by:
+        got, want = sorted(got, key=str), sorted(want, key=str)
+    assert fixtures.rows_match(got, want)
+
+
+@pytest.mark.parametrize("name", ["C5", "Q3.1"])
+def test_gpu_node_hash_ssb(name, ssb_sf1, monkeypatch):
+    """SSB group-bys over three hash-table parts, executed three times (the tables are reset in between): the oracle's
+    groups each time, and the single-device plan's blocks bit for bit."""
+    from tools import ssb
+    raws, segs = ssb_sf1
+    monkeypatch.setenv("PHIP_GB_HASH", "1")
+    monkeypatch.setenv("PHIP_NODE_SPLIT", "3")
+    qc = parse(ssb.SSB_QUERIES[name])
+    op = GpuCombineOperator(qc, segs, 100_000)
+    blocks = [op.next_block() for _ in range(3)]
+    assert op.exchange() == (3, _lib.EXCHANGE_HASH)
+    op.close()
+    _check(qc, blocks[0], raws)
+    for b in blocks[1:]:
+        assert set(b.groups) == set(blocks[0].groups)
+        for k, v in blocks[0].groups.items():
+            for a, c in zip(b.groups[k], v):
+                assert np.array_equal(np.asarray(a), np.asarray(c)), (k, a, c)
+
+
+def test_gpu_node_hash_full_falls_back(mixed, monkeypatch):
+    """A part whose hash table is too small for its groups (PHIP_GB_HASH_CAP) hands no partial: the parts run to their
+    records (each growing its table) and merge on the host."""
+    raws, segs = mixed
+    monkeypatch.setenv("PHIP_GB_HASH", "1")
+    monkeypatch.setenv("PHIP_GB_HASH_CAP", "64")
+    qc, blk, parts, kind = _run("SELECT h, g, COUNT(*), SUM(m) FROM t GROUP BY h, g LIMIT 100000", segs, monkeypatch, 2)
+    assert kind == _lib.EXCHANGE_RECORDS
+    _check(qc, blk, raws)
