@@ -2030,6 +2030,17 @@ struct Plan {
   bool gb_xcd = false;    // ... into kXcdCopies XCD-private copies of it (GB_XCD), merged after the launch
   bool gb_lds = false;    // ... into each workgroup's LDS table (GB_LDS), its slabs reduced after the launch
   bool node_part = false;  // a node plan's part (node_plan_create): a hash table may go out as a partial table
+  // GB_LDS walks: [0] the one-chunk walk, [1] the batched one (agg_kernel kDense) -- LDS bytes, workgroups and waves
+  // per workgroup of each; walk_cur's is the launch's (agg_lds / agg_blocks / dq.dense_batch / dq.wg_waves), re-chosen
+  // after every execution from its matched docs when walk_adaptive (the device descriptor reads neither field)
+  struct GbWalk {
+    size_t lds = 0;
+    int blocks = 0, waves = 0;
+    bool batched = false, ok = false;
+  };
+  GbWalk walk[2];
+  int walk_cur = -1;
+  bool walk_adaptive = false;
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
   int filter_blocks = 1, agg_blocks = 8;
@@ -3642,22 +3653,46 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dq.mode = GB_LDS;
       dq.tbl_words = (int32_t)tbl_words;
       dq.hll_words = (int32_t)hll_words;
-      agg_lds += (size_t)round_up(table_bytes, 16);
-      agg_bpc = std::max(1, std::min(4, (int)((160 * 1024 - 1024) / agg_lds)));
-      // A table that leaves fewer than four 8-wave workgroups per CU (Q2.1's 7000 groups x 16 B = 112 KB: one; C5's
-      // 175 keys x (24 B + 256 HLL registers) = 49 KB: three): 16-wave workgroups share it, so the CU keeps more waves
-      // of gathers in flight (Q2.1: 16 instead of 8 -- SQ: the 8-wave walk spent 76 % of its wave cycles in s_waitcnt,
-      // profiles/r05l_sq_gb.txt; C5: 32 instead of 24). PHIP_GB_WAVES=8 / 16 forces either (A/B).
+      // A table that leaves one 8-wave workgroup per CU (Q2.1's 7000 groups x 16 B = 112 KB): 16-wave workgroups share
+      // it, so the CU keeps 16 waves of gathers in flight instead of 8 (SQ: the 8-wave walk spent 76 % of its wave
+      // cycles in s_waitcnt, profiles/r05l_sq_gb.txt). Not where 8-wave workgroups already keep 16-24 waves: C5's
+      // 49 KB table (three per CU) went 0.77 -> 0.87 ms in 16-wave pairs, Q3.1 0.60 -> 0.62 (profiles/r06l_waves_ab.log).
+      // PHIP_GB_WAVES=8 / 16 forces either (A/B).
       const char *gw = getenv("PHIP_GB_WAVES");
-      const size_t lds16 = (size_t)16 * ring_entries(GB_LDS, batched) * 4 + (size_t)16 * dq.stage_bytes +
-                           (size_t)round_up(table_bytes, 16);
-      const int bpc16 = lds16 <= (size_t)159 * 1024 ? std::max(1, std::min(2, (int)((160 * 1024 - 1024) / lds16))) : 0;
-      const bool want16 = gw ? atoi(gw) == 16 : 16 * bpc16 > kAggWaves * agg_bpc;
-      if (want16 && bpc16 > 0) {
-        dq.wg_waves = 16;
-        agg_lds = lds16;
-        agg_bpc = bpc16;
-      }
+      auto walk_of = [&](bool b) {
+        Plan::GbWalk w;
+        w.batched = b;
+        w.lds = (size_t)kAggWaves * ring_entries(GB_LDS, b) * 4 + (size_t)kAggWaves * dq.stage_bytes +
+                (size_t)round_up(table_bytes, 16);
+        int bpc = std::max(1, std::min(4, (int)((160 * 1024 - 1024) / w.lds)));
+        w.waves = kAggWaves;
+        const size_t lds16 = (size_t)16 * ring_entries(GB_LDS, b) * 4 + (size_t)16 * dq.stage_bytes +
+                             (size_t)round_up(table_bytes, 16);
+        const int bpc16 = lds16 <= (size_t)159 * 1024 ? std::max(1, std::min(2, (int)((160 * 1024 - 1024) / lds16))) : 0;
+        const bool want16 = gw ? atoi(gw) == 16 : bpc == 1;
+        if (want16 && bpc16 > 0) {
+          w.waves = 16;
+          w.lds = lds16;
+          bpc = bpc16;
+        }
+        w.blocks = (int)std::min<int64_t>((int64_t)dev->num_cus * bpc, ceil_div(total_work, w.waves));
+        w.blocks = (int)round_up(std::max(w.blocks, 8), 8);  // the XCD walk needs a multiple of 8 workgroups
+        w.ok = w.lds <= (size_t)159 * 1024;
+        return w;
+      };
+      P.walk[0] = walk_of(false);
+      P.walk[1] = walk_of(true);
+      const Plan::GbWalk &w = P.walk[batched ? 1 : 0];
+      agg_lds = w.lds;
+      dq.wg_waves = w.waves;
+      agg_bpc = std::max(1, (int)((w.blocks + dev->num_cus - 1) / dev->num_cus));
+      // Which walk runs follows the matched docs (the one-chunk walk for sparse matches, the batched one above
+      // kWalkBatchDocsPerCu per CU): the plan starts with the rule above and re-chooses after every execution.
+      // Measured (profiles/r06l_waves_ab.log, SSB SF100 sorted): Q3.1 21.9M docs 0.61 -> 0.47 ms batched, Q2.1 4.7M
+      // 0.27 -> 0.24, Q4.2 2.3M 0.146 -> 0.131; Q2.2 0.96M 0.161 -> 0.146 one-chunk, Q2.3 0.12M 0.135 -> 0.119, Q4.3
+      // 0.46M 0.065 -> 0.035. HLL tables keep the rule (C5 23.8M docs: batched 0.83 ms vs 0.77).
+      P.walk_adaptive = nhll == 0 && !gbb && !gw && !fused_gb && P.walk[0].ok && P.walk[1].ok;
+      P.walk_cur = batched ? 1 : 0;
     }
   } else if (nhll) {
     agg_lds += (size_t)nhll * m_regs * 4;
@@ -3665,6 +3700,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   if (dq.wg_waves == 0) dq.wg_waves = kAggWaves;
   int agg_blocks = (int)std::min<int64_t>((int64_t)dev->num_cus * agg_bpc, ceil_div(total_work, dq.wg_waves));
   agg_blocks = (int)round_up(std::max(agg_blocks, 8), 8);  // the XCD walk needs a multiple of 8 workgroups
+  if (P.walk_cur >= 0) agg_blocks = P.walk[P.walk_cur].blocks;
 
   const size_t nodes_off = blob.reserve(std::max<size_t>(nodes.size(), 1) * sizeof(DevNode));
   kinds[naggs] = ACC_COUNT;
@@ -3763,7 +3799,9 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       dq.hash_overflow = (uint32_t *)ho;
     }
     if (dq.mode == GB_LDS) {
-      const size_t nslabs = gb_lds ? filter_blocks : agg_blocks;  // (the fused LDS table: one slab per filter workgroup)
+      // (the fused LDS table: one slab per filter workgroup; an adaptive walk: the larger grid of the two)
+      const size_t nslabs = gb_lds ? filter_blocks
+                                   : std::max<int>(agg_blocks, P.walk_adaptive ? std::max(P.walk[0].blocks, P.walk[1].blocks) : 0);
       rc = P.alloc(nslabs * dq.tbl_words * 8 + 16, &slab);
       if (rc) return rc;
       if (nhll) {
@@ -4399,6 +4437,7 @@ static int32_t execute_select(Plan &P, Workspace &ws, hipStream_t st, ResultImpl
 // group table, handed to the caller (phip_plan_execute_partial). EXEC_FINISH: compaction / trim / copy-out
 // of the caller-merged table (phip_plan_finish).
 enum { EXEC_FULL = 0, EXEC_PARTIAL = 1, EXEC_FINISH = 2 };
+constexpr int64_t kWalkBatchDocsPerCu = 6144;  // Plan::walk_adaptive: matched docs per CU from which the batched walk runs
 constexpr int32_t kGrowHash = -100;  // execute_plan: the hash table overflowed (internal status: execute_growing)
 static_assert(ACC_COUNT == PHIP_ROW_COUNT && ACC_SUM_I64 == PHIP_ROW_SUM_I64 && ACC_SUM_F64 == PHIP_ROW_SUM_F64 &&
                   ACC_MIN_F64 == PHIP_ROW_MIN && ACC_MAX_F64 == PHIP_ROW_MAX && ACC_HLL == PHIP_ROW_HLL,
@@ -4970,6 +5009,17 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   P.clean = true;
   P.partial_pending = false;
   lg.done = true;
+  if (P.walk_adaptive && group_by) {  // the next execution's group-by walk, from this one's matched docs
+    const int64_t m = has_filter ? (int64_t)fin[32] : docs_in_work;
+    const int want = m >= kWalkBatchDocsPerCu * (int64_t)dev->num_cus ? 1 : 0;
+    if (want != P.walk_cur) {
+      P.walk_cur = want;
+      P.dq.dense_batch = P.walk[want].batched ? 1 : 0;
+      P.dq.wg_waves = P.walk[want].waves;
+      P.agg_blocks = P.walk[want].blocks;
+      P.agg_lds = P.walk[want].lds;
+    }
+  }
   if (out_result) {
     *out_result = &impl.release()->pub;
   }
