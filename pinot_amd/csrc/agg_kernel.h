@@ -525,6 +525,10 @@ template <int NA, int MODE>
 __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, bool act, uint64_t (&acc)[NA],
                                          lds_u32 *hll_lds, lds_u64 *tbl, lds_u32 *hll_packed) {
   if constexpr (MODE == GB_NONE) agg_chunk<NA>(q, seg, doc, act, acc, hll_lds);
+  // (Round 6 tried a prefetched chunk here: every column's load issued straight-line before any decode, then every
+  // dictionary / remap gather -- two round trips per chunk instead of one per load. It was slower: C5 aggregation 0.77
+  // -> 0.82 ms, Q3.1 one-chunk 0.61 -> 0.67, Q4.3 0.050 -> 0.054 (profiles/r06o_pf_ab.log): the walk is bound by the
+  // gathers' per-lane line requests, not by their round trips, and the straight-line form issued more of them.)
   else if constexpr (MODE == GB_LDS) group_chunk_lds(q, seg, doc, act, tbl, hll_packed);
   else if constexpr (MODE == GB_HASH) group_chunk_hash(q, seg, doc, act);
   else group_chunk_global(q, seg, doc, act);

@@ -5,7 +5,7 @@ the library reads at plan creation, e.g. PHIP_GB_BATCH=0 / PHIP_GB_MODE=global).
 setting returns the same groups and values (exact for integer results, 1e-9 relative for doubles).
 
 usage: python tools/gb_ab.py --queries Q2.1,Q3.1,C5 --set "" --set PHIP_GB_BATCH=0 [--sf 100] [--reps 20]
-       [--layout sorted]   (the Q1.x configs too: any SSB query name works)"""
+       [--layout sorted]   (the Q1.x configs too: any SSB query name works; --sql NAME::SQL adds one)"""
 import argparse
 import ctypes
 import json
@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layout", default="unsorted")
+    ap.add_argument("--sql", action="append", default=[],
+                    help="NAME::SQL -- an extra query over the SSB columns (e.g. a C5 variant without its HLL), usable "
+                         "in --queries by NAME")
     ap.add_argument("--gap", type=float, default=0.0,
                     help="seconds of idle GPU before each (query, setting): tools/trace_summary.py splits a rocprofv3 "
                          "kernel trace of this run into the queries at these gaps")
@@ -46,6 +49,9 @@ def main():
     from pinot_amd.engine.segment import GpuSegment
     from pinot_amd.query.sql import parse
     from tools import ssb
+    for spec in args.sql:
+        name, sql = spec.split("::", 1)
+        ssb.SSB_QUERIES[name] = sql
     _lib.check(_lib.load().phip_init((ctypes.c_int32 * 1)(0), 1))
     queries = args.queries.split(",")
     cols = ssb.columns_for(queries)
