@@ -586,6 +586,10 @@ def roofline(kstats, queries, traffic, touched, layout, steps):
     tot = sum(k["ms_per_step"] for k in kernels.values()) or 1.0
     for k in kernels.values():
         k["time_share"] = round(k["ms_per_step"] / tot, 3)
+    if not kernels:  # every tile of this rank's segments pruned (a sorted-layout shard outside the dates): no launch
+        return {"bound": "hbm", "kernel": None, "achieved": 0.0, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": 0.0,
+                "traffic": None, "kernels": {}, "bytes": "no kernel launched on this rank: its segments' tiles were "
+                                                         "all pruned by the sorted index"}
     dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
     d = kernels[dom]
     return {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -745,8 +749,8 @@ def main():
         rf["timing"] = ("kernel durations from HIP events recorded by each launch's dispatch packet (PHIP_EXT_EVENTS=1, "
                         "the timed steps' executions repeated outside the timed region, whose own steps ran without "
                         "timing markers)")
-        if args.timed_markers:
-            rb = roofline(kstats, queries, traffic, touched, layout, args.steps)
+        rb = roofline(kstats, queries, traffic, touched, layout, args.steps) if args.timed_markers else None
+        if rb and rb["kernel"]:
             rf["bracket_events"] = {"kernel": rb["kernel"], "frac": rb["frac"],
                                     "ms_per_launch": rb["kernels"][rb["kernel"]]["ms_per_launch"],
                                     "note": "the timed steps' own barrier-marker events"}

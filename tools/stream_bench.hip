@@ -3,6 +3,8 @@
 //   B  same with non-temporal loads
 //   C  LDS-DMA (global_load_lds_dwordx4) of `chunk` bytes per step per wave from a contiguous per-wave range,
 //      `nbuf` ring slots (nbuf-1 in flight), `wpc` waves per CU -- the filter kernel's staging shape
+//   D  the same ring, each step gathering `ncols` column slices of `cb` bytes from `ncols` separate regions (the
+//      filter's tile: every scan column's 256 x bits bytes, the last 1 KiB instruction partly masked)
 // usage: stream_bench [GiB=1]
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -62,6 +64,42 @@ __global__ __launch_bounds__(256) void read_dma(const uint8_t *__restrict__ p, s
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+template <int NBUF>
+__global__ __launch_bounds__(256) void read_dma_cols(const uint8_t *__restrict__ p, size_t bytes, int ncols, int cb,
+                                                     uint32_t *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + wave;
+  const size_t region = bytes / ncols;
+  const int64_t ntiles = region / cb;
+  const int64_t b = ntiles * gw / waves, e = ntiles * (gw + 1) / waves;
+  const int slot = ((ncols * cb + 1023) / 1024) * 1024;  // ring slot bytes
+  unsigned char *ring = smem + (size_t)wave * NBUF * slot;
+  const uint32_t rl = (uint32_t)(uintptr_t)ring;
+  const int per = (cb + 1023) / 1024;  // instructions per column
+  auto issue = [&](int64_t t) {
+    const uint32_t dst = rl + (uint32_t)(((t - b) % NBUF) * slot);
+    for (int c = 0; c < ncols; c++)
+      for (int k = 0; k < per; k++)
+        if (k * 1024 + lane * 16 < cb)
+          dma16(p + c * region + t * cb + k * 1024 + lane * 16, dst + (uint32_t)(c * cb + k * 1024));  // (uniform base: lane i lands at +16 i)
+  };
+  int64_t pf = b;
+  for (int i = 0; i < NBUF - 1 && pf < e; i++, pf++) issue(pf);
+  uint32_t acc = 0;
+  for (int64_t t = b; t < e; t++) {
+    if (pf < e) {
+      issue(pf);
+      pf++;
+      wait_vm(ncols * per * (NBUF - 1));
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    acc ^= ((volatile uint32_t *)(ring + ((t - b) % NBUF) * slot))[lane];
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char **argv) {
   const double gib = argc > 1 ? atof(argv[1]) : 1.0;
   const size_t bytes = (size_t)(gib * (1 << 30)) & ~(size_t)0xffff;
@@ -115,6 +153,30 @@ int main(int argc, char **argv) {
       CHECK(hipFuncSetAttribute((const void *)read_dma<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       CHECK(hipFuncSetAttribute((const void *)read_dma<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
+    time(go, nm);
+  }
+  // the filter's multi-column tiles (D): column slice bytes x columns, ring slots, waves per CU
+  struct ColCfg { int ncols, cb, bpc, nbuf; };
+  const ColCfg ccfgs[] = {{3, 1536, 4, 4}, {3, 1536, 6, 3}, {3, 1536, 2, 8}, {3, 768, 4, 6}, {4, 1024, 4, 4},
+                          {1, 4096, 4, 4}, {3, 2048, 4, 3}, {3, 1536, 8, 2}};
+  for (const ColCfg &c : ccfgs) {
+    const int slot = ((c.ncols * c.cb + 1023) / 1024) * 1024;
+    const size_t lds = (size_t)4 * c.nbuf * slot;
+    if (lds * c.bpc > 160 * 1024) continue;
+    char nm[96];
+    snprintf(nm, sizeof nm, "cols   %dx%5d B waves/CU=%2d nbuf=%d (%3zu KB)", c.ncols, c.cb, 4 * c.bpc, c.nbuf, lds * c.bpc / 1024);
+    auto go = [&] {
+      switch (c.nbuf) {
+        case 2: read_dma_cols<2><<<cus * c.bpc, 256, lds>>>(p, bytes, c.ncols, c.cb, out); break;
+        case 3: read_dma_cols<3><<<cus * c.bpc, 256, lds>>>(p, bytes, c.ncols, c.cb, out); break;
+        case 4: read_dma_cols<4><<<cus * c.bpc, 256, lds>>>(p, bytes, c.ncols, c.cb, out); break;
+        case 6: read_dma_cols<6><<<cus * c.bpc, 256, lds>>>(p, bytes, c.ncols, c.cb, out); break;
+        default: read_dma_cols<8><<<cus * c.bpc, 256, lds>>>(p, bytes, c.ncols, c.cb, out); break;
+      }
+    };
+    for (auto f : {(const void *)read_dma_cols<2>, (const void *)read_dma_cols<3>, (const void *)read_dma_cols<4>,
+                   (const void *)read_dma_cols<6>, (const void *)read_dma_cols<8>})
+      CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     time(go, nm);
   }
   CHECK(hipFree(p));
