@@ -157,8 +157,9 @@ int main(int argc, char **argv) {
   }
   // the filter's multi-column tiles (D): column slice bytes x columns, ring slots, waves per CU
   struct ColCfg { int ncols, cb, bpc, nbuf; };
-  const ColCfg ccfgs[] = {{3, 1536, 4, 4}, {3, 1536, 6, 3}, {3, 1536, 2, 8}, {3, 768, 4, 6}, {4, 1024, 4, 4},
-                          {1, 4096, 4, 4}, {3, 2048, 4, 3}, {3, 1536, 8, 2}};
+  const ColCfg ccfgs[] = {{3, 1536, 4, 2}, {3, 1536, 3, 2}, {3, 1536, 2, 4}, {3, 1536, 1, 8}, {3, 768, 4, 4},
+                          {4, 1024, 4, 2}, {1, 4096, 4, 2}, {1, 4096, 2, 4}, {3, 2048, 2, 3}, {6, 768, 2, 4},
+                          {2, 2048, 4, 2}, {3, 512, 4, 6}};
   for (const ColCfg &c : ccfgs) {
     const int slot = ((c.ncols * c.cb + 1023) / 1024) * 1024;
     const size_t lds = (size_t)4 * c.nbuf * slot;
