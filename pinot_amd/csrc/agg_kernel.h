@@ -339,6 +339,123 @@ __device__ __forceinline__ void tbl_hll(cquery_t &q, lds_u32 *hll_packed, int sl
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Group-by records (DevSeg.rec, runtime.cpp build_records): a matched doc's key ids, value fields and HLL entry come
+// from ONE 16-byte load of its record instead of one gather per column. Every gathered column touched nearly every
+// line of itself (C5: five columns at 4 % density, ~4.3 GB of lines per launch at ~5.6 TB/s); the record's lines
+// hold every field, so the launch touches fewer of them. Records are W <= 4 u32; the load always reads 16 bytes (the
+// allocation has the slack), so it is one instruction whatever W is.
+// ------------------------------------------------------------------------------------------------
+struct RecW {
+  uint32_t w0, w1, w2, w3;
+};
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ RecW rec_load(cseg_t &seg, int32_t doc) {
+  const PHIP_GLB u32x4_a4 *p =
+      (const PHIP_GLB u32x4_a4 *)((const PHIP_GLB uint32_t *)seg.rec + (int64_t)doc * seg.rec_words);
+  const u32x4_a4 v = __builtin_nontemporal_load(p);
+  return RecW{v.x, v.y, v.z, v.w};
+}
+// field f of a record (offset and width wave-uniform)
+__device__ __forceinline__ uint32_t rec_field(cseg_t &seg, const RecW &r, int f) {
+  const int off = seg.rec_off[f], bits = seg.rec_bits[f];
+  const int i = off >> 5, sh = off & 31;
+  const uint32_t lo = i == 0 ? r.w0 : (i == 1 ? r.w1 : (i == 2 ? r.w2 : r.w3));
+  const uint32_t hi = i == 0 ? r.w1 : (i == 1 ? r.w2 : (i == 2 ? r.w3 : 0u));
+  const uint64_t v = ((((uint64_t)hi) << 32) | lo) >> sh;
+  return bits >= 32 ? (uint32_t)v : (uint32_t)v & ((1u << bits) - 1u);
+}
+// the group key of a record (key fields 0 .. num_group_by - 1: dictionary ids, remapped)
+__device__ __forceinline__ int32_t rec_key(cquery_t &q, cseg_t &seg, const RecW &r) {
+  int32_t key = 0;
+  for (int k = 0; k < kRecKeys; k++) {
+    if (k >= q.num_group_by) break;
+    ccol_t &c = seg.cols[q.gb_cols[k]];
+    uint32_t id = rec_field(seg, r, k);
+    if (c.remap) id = (uint32_t)((const PHIP_GLB int32_t *)c.remap)[id];
+    key += (int32_t)id * (int32_t)q.gb_stride[k];
+  }
+  return key;
+}
+// a value input of an aggregation from its field: packed value (vbase + bits) or dictionary id (gathered)
+__device__ __forceinline__ int64_t rec_i64(ccol_t &c, uint32_t x) {
+  return c.vpack != nullptr ? c.vbase + (int64_t)x : dict_i64(c, x);
+}
+__device__ __forceinline__ double rec_f64(ccol_t &c, uint32_t x) {
+  return c.vpack != nullptr ? (double)(c.vbase + (int64_t)x) : dict_f64(c, x);
+}
+// the updates of one matched doc's record (act: the lane holds a matched doc)
+template <int MODE>
+__device__ __forceinline__ void rec_update(cquery_t &q, cseg_t &seg, const RecW &r, int32_t key, bool act, lds_u64 *tbl,
+                                           lds_u32 *hll_packed) {
+  const int64_t G = q.num_groups;
+  if (act) tbl_add_u64<MODE>(q, tbl, key, 1ull);
+  for (int a = 0; a < kMaxAggs; a++) {
+    if (a >= q.num_aggs) break;
+    cagg_t &ag = q.aggs[a];
+    if (ag.program != seg.program) continue;  // another filter program's function (wave-uniform)
+    const int64_t at = (int64_t)(1 + a) * G + key;
+    const int kind = ag.acc;
+    if (kind == ACC_COUNT) {
+      if (q.own_count_rows && act) tbl_add_u64<MODE>(q, tbl, at, 1ull);
+    } else if (kind == ACC_HLL) {
+      const uint32_t x = rec_field(seg, r, q.rec_fa[a]);
+      const uint32_t h = seg.cols[ag.col_a].hll_doc16 != nullptr ? (((x >> 5) << 8) | (x & 31u)) : x;
+      if (act) tbl_hll<MODE>(q, hll_packed, ag.hll_slot, key, h >> 8, h & 0xffu);
+    } else {
+      ccol_t &ca = seg.cols[ag.col_a];
+      const uint32_t xa = rec_field(seg, r, q.rec_fa[a]);
+      const bool two = ag.expr != PHIP_EXPR_COLUMN;
+      if (kind == ACC_SUM_I64) {
+        int64_t x = rec_i64(ca, xa);
+        if (two) {
+          const int64_t y = rec_i64(seg.cols[ag.col_b], rec_field(seg, r, q.rec_fb[a]));
+          x = ag.expr == PHIP_EXPR_ADD ? x + y : (ag.expr == PHIP_EXPR_SUB ? x - y : x * y);
+        }
+        if (act) tbl_add_u64<MODE>(q, tbl, at, (uint64_t)x);
+      } else {
+        double x = rec_f64(ca, xa);
+        if (two) {
+          const double y = rec_f64(seg.cols[ag.col_b], rec_field(seg, r, q.rec_fb[a]));
+          x = ag.expr == PHIP_EXPR_ADD ? x + y : (ag.expr == PHIP_EXPR_SUB ? x - y : x * y);
+        }
+        if (act) {
+          if (kind == ACC_SUM_F64) tbl_add_f64<MODE>(q, tbl, at, x);
+          else tbl_minmax<MODE>(q, tbl, at, f64_ordered(x), kind == ACC_MIN_F64);
+        }
+      }
+    }
+  }
+}
+// one-chunk walk: 64 ring docs (inactive lanes carry doc 0, a valid doc)
+template <int MODE>
+__device__ __forceinline__ void group_chunk_rec(cquery_t &q, cseg_t &seg, int32_t doc, bool act, lds_u64 *tbl,
+                                                lds_u32 *hll_packed) {
+  const RecW r = rec_load(seg, doc);
+  const int32_t key = rec_key(q, seg, r);
+  rec_update<MODE>(q, seg, r, key, act, tbl, hll_packed);
+}
+// batched walk: U chunks of ring entries, every record load issued before the first is decoded
+template <int MODE, int U, int RING>
+__device__ __forceinline__ void group_ring_batch_rec(cquery_t &q, cseg_t &seg, const lds_u32 *ring, int tail, int n,
+                                                     lds_u64 *tbl, lds_u32 *hll_packed) {
+  const int lane = lane_id();
+  RecW r[U];
+  uint32_t act = 0;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const bool on = 64 * u + lane < n;
+    const int32_t d = on ? (int32_t)ring[(tail + 64 * u + lane) & (RING - 1)] : 0;
+    act |= on ? (1u << u) : 0u;
+    r[u] = rec_load(seg, d);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int32_t key = rec_key(q, seg, r[u]);
+    rec_update<MODE>(q, seg, r[u], key, ((act >> u) & 1u) != 0, tbl, hll_packed);
+  }
+}
+
 constexpr int kRingGB = kRingGroupBatch;
 
 // (U chunks of 64 ring entries per round trip from a ring of RING entries; the fused group-by of filter_kernel.h uses
@@ -346,6 +463,10 @@ constexpr int kRingGB = kRingGroupBatch;
 template <int MODE, int U = kBatch, int RING = kRingGB>
 __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const lds_u32 *ring, int tail, int n,
                                                  lds_u64 *tbl, lds_u32 *hll_packed) {
+  if (seg.rec != nullptr) {
+    group_ring_batch_rec<MODE, U, RING>(q, seg, ring, tail, n, tbl, hll_packed);
+    return;
+  }
   const int lane = lane_id();
   int32_t d[U];
   uint32_t act = 0;
@@ -529,9 +650,15 @@ __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, 
   // dictionary / remap gather -- two round trips per chunk instead of one per load. It was slower: C5 aggregation 0.77
   // -> 0.82 ms, Q3.1 one-chunk 0.61 -> 0.67, Q4.3 0.050 -> 0.054 (profiles/r06o_pf_ab.log): the walk is bound by the
   // gathers' per-lane line requests, not by their round trips, and the straight-line form issued more of them.)
-  else if constexpr (MODE == GB_LDS) group_chunk_lds(q, seg, doc, act, tbl, hll_packed);
-  else if constexpr (MODE == GB_HASH) group_chunk_hash(q, seg, doc, act);
-  else group_chunk_global(q, seg, doc, act);
+  else if constexpr (MODE == GB_LDS) {
+    if (seg.rec != nullptr) group_chunk_rec<GB_LDS>(q, seg, doc, act, tbl, hll_packed);
+    else group_chunk_lds(q, seg, doc, act, tbl, hll_packed);
+  } else if constexpr (MODE == GB_HASH) {
+    group_chunk_hash(q, seg, doc, act);
+  } else {
+    if (seg.rec != nullptr) group_chunk_rec<MODE>(q, seg, doc, act, tbl, hll_packed);
+    else group_chunk_global(q, seg, doc, act);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -7,6 +7,18 @@ namespace phip {
 
 constexpr int kMaxQueryColumns = 16;  // distinct columns one query may reference
 constexpr int kMaxAggs = 8;           // aggregation slots per query
+constexpr int kRecKeys = 4;            // group-by record: key fields (DevSeg.rec)
+constexpr int kRecFields = kRecKeys + 2 * kMaxAggs;  // ... and up to two inputs per aggregation
+// One field's source for materialize_record_kernel: a fixed-bit stream (dictionary ids / packed values, `bits` per
+// doc), or doc-order u16 / u32 entries (HLL); placed at bit `off` of the doc's record.
+enum { REC_BITS = 0, REC_U16 = 1, REC_U32 = 2 };
+struct RecSrc {
+  const void *p;
+  int32_t kind, bits, off, pad;
+};
+struct RecSrcs {
+  RecSrc f[kRecFields];
+};
 constexpr int kMaxPrograms = 8;       // filter programs per query (filtered aggregations in one pass)
 constexpr int kDenseMin = 640;        // default DevAggQuery::dense_min
 constexpr int kDoneSlot = 63;         // finals[kDoneSlot] of a plan's mapped result area: the execution's completion word
@@ -200,6 +212,15 @@ struct DevSeg {
                         // the lane-major tile layout directly
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
+  // Group-by record (Segment::records, materialize_record_kernel): every field a matched doc's group-by update reads
+  // -- its key ids, its aggregations' packed values / value ids, its HLL entries -- packed into rec_words u32 per doc
+  // (field f at bits [rec_off[f], rec_off[f] + rec_bits[f]) of the doc's record, LSB first), so a doc costs one
+  // gather instead of one per column. null = the columns' own layouts.
+  const uint32_t *rec;
+  int32_t rec_words;
+  int32_t rec_nf;
+  uint8_t rec_off[kRecFields];
+  uint8_t rec_bits[kRecFields];
   DevCol cols[kMaxQueryColumns];
 };
 
@@ -328,8 +349,10 @@ struct DevAggQuery {
   int32_t own_count_rows;  // group-by over several filter programs (FILTER + GROUP BY): every COUNT counts its own
                            // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
   const DevFinal *fin;     // GB_NONE: non-null when this launch is the plan's last (agg_common.h finalize_tail)
-  int32_t wg_waves;        // waves per workgroup of the launch (kAggWaves; 16 for a GB_LDS table that leaves fewer
-  int32_t pad_w;           // 8-wave workgroups per CU than it leaves 16-wave ones x 2)
+  int32_t wg_waves;        // waves per workgroup of the launch (kAggWaves; 16 for a GB_LDS table that leaves one
+  int32_t pad_w;           // 8-wave workgroup per CU)
+  int8_t rec_fa[kMaxAggs];  // group-by record (DevSeg.rec): the field of aggregation a's input a / b / HLL entry
+  int8_t rec_fb[kMaxAggs];  // (-1: none; the key columns are fields 0 .. num_group_by - 1)
   int64_t xcd_words;       // GB_XCD: u64 words of one table copy ((1 + num_aggs) x num_groups)
   int64_t xcd_hll_words;   // GB_XCD: u32 words of one copy's HLL registers (num_hll x num_groups x m)
 };

@@ -144,6 +144,38 @@ hipError_t launch_materialize(const uint32_t *words, int32_t bits, const void *d
   return hipGetLastError();
 }
 
+// Group-by records (DevSeg.rec): doc d's fields packed LSB first into W u32 (one thread per doc, no word shared).
+__device__ __forceinline__ void rec_or(uint32_t (&r)[4], int i, uint32_t x) {
+  switch (i) {  // (uniform: a field's offset is the same for every doc)
+    case 0: r[0] |= x; break;
+    case 1: r[1] |= x; break;
+    case 2: r[2] |= x; break;
+    default: r[3] |= x; break;
+  }
+}
+__global__ void materialize_record_kernel(RecSrcs fs, int nf, int64_t n, int W, uint32_t *__restrict__ out) {
+  for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t r[4] = {0u, 0u, 0u, 0u};
+    for (int f = 0; f < nf; f++) {
+      const RecSrc &src = fs.f[f];
+      uint32_t v;
+      if (src.kind == REC_BITS) v = decode_bits((const uint32_t *)src.p, (uint64_t)d * (uint32_t)src.bits, (uint32_t)src.bits);
+      else if (src.kind == REC_U16) v = ((const uint16_t *)src.p)[d];
+      else v = ((const uint32_t *)src.p)[d];
+      if (src.bits < 32) v &= (1u << src.bits) - 1u;
+      const int i = src.off >> 5, sh = src.off & 31;
+      rec_or(r, i, v << sh);
+      if (sh + src.bits > 32) rec_or(r, i + 1, v >> (32 - sh));
+    }
+    for (int i = 0; i < W; i++) out[d * W + i] = r[i];
+  }
+}
+hipError_t launch_materialize_record(const RecSrcs &fs, int nf, int64_t n, int W, uint32_t *out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  materialize_record_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(fs, nf, n, W, out);
+  return hipGetLastError();
+}
+
 // Value range of a raw INT / LONG column (LE, resident), for the plan-time int64 overflow bound of
 // integer SUMs (SumAggregationFunction adds in double and never wraps, :76-101). out = {min, max},
 // preset to {INT64_MAX, INT64_MIN} by the caller.

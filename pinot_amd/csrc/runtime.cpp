@@ -126,6 +126,7 @@ hipError_t launch_raw_key_ids(const void *raw, int32_t type, int64_t n, const ui
                               hipStream_t s);
 hipError_t launch_materialize_hll16(const uint32_t *words, int32_t bits, const uint32_t *table, int64_t n, uint16_t *out,
                                     hipStream_t s);
+hipError_t launch_materialize_record(const RecSrcs &fs, int nf, int64_t n, int W, uint32_t *out, hipStream_t s);
 hipError_t launch_minmax_i64(const void *raw, int32_t type, int64_t n, int64_t *out, hipStream_t s,
                              const uint64_t *nulls = nullptr);
 hipError_t launch_chunk_decode_global(int codec, const uint8_t *blob, const RawChunk *chunks, int32_t nchunks, uint8_t *out,
@@ -418,6 +419,10 @@ static inline bool no_dict(const ColumnStore &c) {
 }
 
 
+// HBM held by group-by records per device (build_records' budget)
+constexpr int kMaxRecordDevices = 64;
+static std::atomic<uint64_t> g_record_bytes[kMaxRecordDevices];
+
 struct Segment {
   uint64_t handle = 0;
   int device = 0;
@@ -427,7 +432,15 @@ struct Segment {
   std::unordered_map<std::string, int> by_name;
   uint64_t device_bytes = 0;
   std::vector<void *> allocations;
+  // group-by records (DevSeg.rec) by field signature: words, u32 per doc (build_records; in `allocations`)
+  struct Record {
+    uint32_t *words = nullptr;
+    int32_t width = 0;
+  };
+  std::map<std::string, Record> records;
+  uint64_t record_bytes = 0;
   ~Segment() {
+    if (device >= 0 && device < kMaxRecordDevices) g_record_bytes[device] -= record_bytes;
     (void)hipSetDevice(device);
     for (void *p : allocations) (void)hipFree(p);
     for (auto &c : cols)
@@ -2200,6 +2213,112 @@ static int32_t raw_string_leaf(const phip_filter_node &fn, DevNode &dn, Blob &bl
   return PHIP_OK;
 }
 
+// Group-by records (DevSeg.rec): the fields a matched doc's group-by update reads -- the key columns' dictionary ids,
+// each aggregation's packed values or value ids, its doc-order HLL entries -- packed into W <= 4 u32 per doc, made on
+// first use for a field signature and kept with the segment (at most kMaxRecordSets per segment). The aggregation
+// kernel then reads one 16-byte record per matched doc instead of one line per column (agg_kernel.h rec_load).
+// A segment whose columns do not all fit (raw / null / FLOAT-id keys, raw typed values, HLL without doc-order entries)
+// keeps its columns' layouts: the kernel decides per segment.
+constexpr int kRecMinFields = 3;   // fewer fields: the per-column gathers already touch few lines
+constexpr double kRecMaxRatio = 0.8;  // a record's touched bytes must stay below this fraction of the columns'
+constexpr int kMaxRecordSets = 16;                       // record signatures kept per segment
+constexpr uint64_t kRecordBudget = (uint64_t)64 << 30;  // record bytes per device (PHIP_GB_RECORD_GIB overrides)
+// Lines a gather of bpd bytes per doc touches over n docs at match density p: each 128-B line holds 128 / bpd docs
+// and is touched unless none of them matched.
+static double touched_bytes(double bpd, double p, int64_t n) {
+  const double per_line = std::max(1.0, 128.0 / bpd);
+  return (double)n * bpd * (1.0 - std::pow(1.0 - std::min(1.0, std::max(0.0, p)), per_line));
+}
+static int32_t build_records(Segment &sg, const phip_query_desc *q, DevAggQuery &dq, DevSeg &ds,
+                             const std::vector<int> &colidx, int min_fields, double density, hipStream_t st,
+                             bool *made) {
+  RecSrcs fs;
+  memset(&fs, 0, sizeof(fs));
+  int nf = 0, off = 0;
+  bool ok = true;
+  std::string sig;
+  int8_t fa[kMaxAggs], fb[kMaxAggs];
+  auto add = [&](const void *p, int kind, int bits, int col) -> int8_t {
+    if (!ok || p == nullptr || bits <= 0 || bits > 32 || nf == kRecFields) {
+      ok = false;
+      return -1;
+    }
+    fs.f[nf] = RecSrc{p, kind, bits, off, 0};
+    off += bits;
+    sig += std::to_string(colidx[col]) + "/" + std::to_string(kind) + "/" + std::to_string(bits) + ";";
+    return (int8_t)nf++;
+  };
+  auto value_field = [&](int col) -> int8_t {
+    const DevCol &c = ds.cols[col];
+    if (c.vpack != nullptr) return add(c.vpack, REC_BITS, c.vbits, col);
+    if (c.has_dict && c.words != nullptr && c.type != PHIP_TYPE_STRING) return add(c.words, REC_BITS, c.bits, col);
+    ok = false;
+    return -1;
+  };
+  for (int k = 0; k < q->num_group_by && ok; k++) {
+    const int col = q->group_by_columns[k];
+    const DevCol &c = ds.cols[col];
+    if (!c.has_dict || c.words == nullptr || c.gb_nulls != nullptr || c.gb_ids != nullptr) ok = false;
+    else add(c.words, REC_BITS, c.bits, col);
+  }
+  for (int a = 0; a < kMaxAggs; a++) fa[a] = fb[a] = -1;
+  for (int a = 0; a < dq.num_aggs && ok; a++) {
+    const DevAgg &ag = dq.aggs[a];
+    if (ag.acc == ACC_COUNT) continue;
+    if (ag.acc == ACC_HLL) {
+      const DevCol &c = ds.cols[ag.col_a];
+      if (ag.expr != PHIP_EXPR_COLUMN || c.hll_rows) ok = false;
+      // (a 16-bit entry is (register << 5) | rho: log2m + 5 significant bits -- C5's five fields fit 8 bytes)
+      else if (c.hll_doc16 != nullptr) fa[a] = add(c.hll_doc16, REC_U16, std::min(16, (int)ag.log2m + 5), ag.col_a);
+      else if (c.hll_doc != nullptr) fa[a] = add(c.hll_doc, REC_U32, 32, ag.col_a);
+      else ok = false;
+      continue;
+    }
+    fa[a] = value_field(ag.col_a);
+    if (ag.expr != PHIP_EXPR_COLUMN) fb[a] = value_field(ag.col_b);
+  }
+  if (!ok || nf < min_fields || off > 128) return PHIP_OK;
+  const int W = (off + 31) / 32;
+  // Worth it when the record's touched lines are clearly fewer than the columns' at the estimated density (a general
+  // program estimates 1: no record). SSB SF100 (profiles/r06x_rec_ab.log): Q4.1 (density 1.6 %: 2.3 GB of column
+  // lines vs 1.1 GB of records) 0.50 -> 0.37 ms, C5 0.77 -> 0.61, Q2.1 0.25 -> 0.21; Q3.1 (3.4 %, three narrow keys
+  // whose lines are all touched anyway: 2.4 vs 2.0 GB) 0.51 -> 0.53, so it keeps its columns.
+  if (min_fields > 1) {
+    double cols = 0;
+    for (int f = 0; f < nf; f++) cols += touched_bytes(fs.f[f].bits / 8.0, density, sg.num_docs);
+    if (touched_bytes(4.0 * W, density, sg.num_docs) > kRecMaxRatio * cols) return PHIP_OK;
+  }
+  auto it = sg.records.find(sig);
+  if (it == sg.records.end()) {
+    if ((int)sg.records.size() >= kMaxRecordSets) return PHIP_OK;
+    const char *gib = getenv("PHIP_GB_RECORD_GIB");
+    const uint64_t budget = gib ? (uint64_t)atoll(gib) << 30 : kRecordBudget;
+    const uint64_t bytes = (uint64_t)sg.num_docs * W * 4 + 16;
+    if (sg.device < 0 || sg.device >= kMaxRecordDevices || g_record_bytes[sg.device] + bytes > budget) return PHIP_OK;
+    void *p;
+    // (+ 16 bytes: rec_load reads 16 bytes whatever W is)
+    int32_t rc = dev_alloc(sg, (size_t)sg.num_docs * W * 4 + 16, &p);
+    if (rc) return rc;
+    HIP_TRY(launch_materialize_record(fs, nf, sg.num_docs, W, (uint32_t *)p, st));
+    it = sg.records.emplace(sig, Segment::Record{(uint32_t *)p, W}).first;
+    sg.record_bytes += bytes;
+    g_record_bytes[sg.device] += bytes;
+    *made = true;
+  }
+  ds.rec = it->second.words;
+  ds.rec_words = W;
+  ds.rec_nf = nf;
+  for (int f = 0; f < nf; f++) {
+    ds.rec_off[f] = (uint8_t)fs.f[f].off;
+    ds.rec_bits[f] = (uint8_t)fs.f[f].bits;
+  }
+  for (int a = 0; a < kMaxAggs; a++) {  // (the same for every segment that has a record: the query fixes the order)
+    dq.rec_fa[a] = fa[a];
+    dq.rec_fb[a] = fb[a];
+  }
+  return PHIP_OK;
+}
+
 static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t filter_nwords, Plan &P) {
 
   if (!q || q->num_segments <= 0 || q->num_columns < 0 || q->num_columns > kMaxQueryColumns)
@@ -2692,6 +2811,13 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   bool hll_made = false;
   std::vector<bool> hll_doc_used((size_t)nseg * ncols, false);  // (segment, column): HLL entries read by doc
   std::vector<bool> hll_doc16_used((size_t)nseg * ncols, false);  // ... 16-bit ones
+  // group-by records (build_records): dense key spaces of dictionary keys, for every group-by the aggregation kernel
+  // walks (PHIP_GB_RECORD=0: the columns' own layouts; =1: a record for any number of fields, else from kRecMinFields)
+  const char *gre = getenv("PHIP_GB_RECORD");
+  const bool rec_want = group_by && dq.mode != GB_HASH && gb_key_space <= ((int64_t)1 << 22) && !want_bitmap &&
+                        q->num_group_by <= kRecKeys && !(gre && atoi(gre) == 0);
+  const int rec_min_fields = gre && atoi(gre) == 1 ? 1 : kRecMinFields;
+  for (int a = 0; a < kMaxAggs; a++) dq.rec_fa[a] = dq.rec_fb[a] = -1;
   const char *hde = getenv("PHIP_HLL_DOC");  // measurement override: "0" = gather the per-id table
   const char *mze = getenv("PHIP_MATERIALIZE");
   const bool hll_doc_on = !(hde && atoi(hde) == 0) && !(mze && atoi(mze) == 0) && !want_bitmap;
@@ -3348,6 +3474,16 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     }
     seg_off[&ds - dsegs.data()] = off;
   }
+  // group-by records, from each entry's estimated selectivity (build_records' touched-lines model)
+  if (rec_want) {
+    bool made = false;
+    for (size_t i = 0; i < dsegs.size(); i++) {
+      const int s = dsegs[i].seg_index % nseg;
+      int32_t rc = build_records(*segs[s], q, dq, dsegs[i], colidx[s], rec_min_fields, seg_est[i], st, &made);
+      if (rc) return rc;
+    }
+    if (made) HIP_TRY(hipStreamSynchronize(st));
+  }
   // Fused aggregation (filter.hip fused_tile): every segment on the conjunctive path, aggregation only
   // (no group-by, no HLL), at most 4 slots, a filter to fuse into. Value columns are then streamed with
   // the tile (one more LDS-DMA region) when the expected matches per 128-byte line of the column reach
@@ -3690,8 +3826,11 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       // kWalkBatchDocsPerCu per CU): the plan starts with the rule above and re-chooses after every execution.
       // Measured (profiles/r06l_waves_ab.log, SSB SF100 sorted): Q3.1 21.9M docs 0.61 -> 0.47 ms batched, Q2.1 4.7M
       // 0.27 -> 0.24, Q4.2 2.3M 0.146 -> 0.131; Q2.2 0.96M 0.161 -> 0.146 one-chunk, Q2.3 0.12M 0.135 -> 0.119, Q4.3
-      // 0.46M 0.065 -> 0.035. HLL tables keep the rule (C5 23.8M docs: batched 0.83 ms vs 0.77).
-      P.walk_adaptive = nhll == 0 && !gbb && !gw && !fused_gb && P.walk[0].ok && P.walk[1].ok;
+      // 0.46M 0.065 -> 0.035. HLL tables keep the rule when they gather per column (C5 23.8M docs: batched 0.83 ms
+      // vs 0.77); with group-by records the batched walk wins there too (C5 0.63 -> 0.61, profiles/r06w_rec_ab.log).
+      bool any_rec = false;
+      for (const DevSeg &d : dsegs) any_rec |= d.rec != nullptr;
+      P.walk_adaptive = (nhll == 0 || any_rec) && !gbb && !gw && !fused_gb && P.walk[0].ok && P.walk[1].ok;
       P.walk_cur = batched ? 1 : 0;
     }
   } else if (nhll) {

@@ -153,6 +153,7 @@ hipError_t launch_xcd_init(uint64_t *tab, int64_t words, int64_t, const int32_t 
 hipError_t launch_materialize_hll16(const uint32_t *, int32_t, const uint32_t *, int64_t, uint16_t *, hipStream_t) {
   return hipSuccess;
 }
+hipError_t launch_materialize_record(const RecSrcs &, int, int64_t, int, uint32_t *, hipStream_t) { return hipSuccess; }
 hipError_t launch_materialize_packed(const uint32_t *, int32_t, const void *, int32_t, int64_t, int64_t, int32_t, int64_t,
                                      uint32_t *, hipStream_t) {
   return hipSuccess;
