@@ -460,12 +460,14 @@ constexpr int kRingGB = kRingGroupBatch;
 
 // (U chunks of 64 ring entries per round trip from a ring of RING entries; the fused group-by of filter_kernel.h uses
 // a smaller ring and batch than the aggregation kernel)
-template <int MODE, int U = kBatch, int RING = kRingGB>
+template <int MODE, int U = kBatch, int RING = kRingGB, bool kRec = false>
 __device__ __forceinline__ void group_ring_batch(cquery_t &q, cseg_t &seg, const lds_u32 *ring, int tail, int n,
                                                  lds_u64 *tbl, lds_u32 *hll_packed) {
-  if (seg.rec != nullptr) {
-    group_ring_batch_rec<MODE, U, RING>(q, seg, ring, tail, n, tbl, hll_packed);
-    return;
+  if constexpr (kRec) {  // (the record variant only: the other kernels keep their code size)
+    if (seg.rec != nullptr) {
+      group_ring_batch_rec<MODE, U, RING>(q, seg, ring, tail, n, tbl, hll_packed);
+      return;
+    }
   }
   const int lane = lane_id();
   int32_t d[U];
@@ -642,7 +644,7 @@ __device__ __forceinline__ void group_chunk_hash(cquery_t &q, cseg_t &seg, int32
   group_update_global(q, seg, doc, slot);
 }
 
-template <int NA, int MODE>
+template <int NA, int MODE, bool kRec = false>
 __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, bool act, uint64_t (&acc)[NA],
                                          lds_u32 *hll_lds, lds_u64 *tbl, lds_u32 *hll_packed) {
   if constexpr (MODE == GB_NONE) agg_chunk<NA>(q, seg, doc, act, acc, hll_lds);
@@ -651,13 +653,12 @@ __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, 
   // -> 0.82 ms, Q3.1 one-chunk 0.61 -> 0.67, Q4.3 0.050 -> 0.054 (profiles/r06o_pf_ab.log): the walk is bound by the
   // gathers' per-lane line requests, not by their round trips, and the straight-line form issued more of them.)
   else if constexpr (MODE == GB_LDS) {
-    if (seg.rec != nullptr) group_chunk_rec<GB_LDS>(q, seg, doc, act, tbl, hll_packed);
+    if (kRec && seg.rec != nullptr) group_chunk_rec<GB_LDS>(q, seg, doc, act, tbl, hll_packed);
     else group_chunk_lds(q, seg, doc, act, tbl, hll_packed);
   } else if constexpr (MODE == GB_HASH) {
     group_chunk_hash(q, seg, doc, act);
   } else {
-    if (seg.rec != nullptr) group_chunk_rec<MODE>(q, seg, doc, act, tbl, hll_packed);
-    else group_chunk_global(q, seg, doc, act);
+    group_chunk_global(q, seg, doc, act);
   }
 }
 
@@ -671,7 +672,8 @@ __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, 
 // For GB_LDS / GB_GLOBAL, kDense selects the batched group-by walk (group_ring_batch) instead.
 // W: waves per workgroup (8; 16 for an LDS group table so large that one workgroup fills the CU's LDS -- twice the
 // waves share the one table, so the CU keeps 16 waves of gathers in flight instead of 8: DevAggQuery.wg_waves).
-template <int NA, int MODE, bool kDense, int W = kAggWaves>
+// kRec: the group-by record variant (DevAggQuery.rec_on: some segment has a DevSeg.rec; GB_LDS only).
+template <int NA, int MODE, bool kDense, int W = kAggWaves, bool kRec = false>
 __global__ __launch_bounds__(W * kWave, (MODE == GB_LDS || MODE == GB_GLOBAL) && kDense ? 6 : 1)
 void agg_kernel(const DevAggQuery *qptr) {
   constexpr int kBlock = W * kWave;
@@ -746,11 +748,11 @@ void agg_kernel(const DevAggQuery *qptr) {
       if constexpr (MODE == GB_NONE) {
         if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
       } else if constexpr (kGbBatch) {
-        if (head > tail) group_ring_batch<MODE>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
+        if (head > tail) group_ring_batch<MODE, kBatch, kRingGB, kRec>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
       } else if (head > tail) {  // leftover (< 64) matched docs of the previous segment
         const bool act = lane < head - tail;
         const int32_t doc = act ? (int32_t)ring[(tail + lane) & (R - 1)] : 0;
-        do_chunk<NA, MODE>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
+        do_chunk<NA, MODE, kRec>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
       }
       head = tail = 0;
       while (si + 1 < q.num_segs && segs[si + 1].work_begin <= t) si++;
@@ -847,7 +849,7 @@ void agg_kernel(const DevAggQuery *qptr) {
         }
         head = head0 + pend;
         while (head - tail >= 64 * kBatch) {
-          if constexpr (kGbBatch) group_ring_batch<MODE>(q, seg, ring, tail, 64 * kBatch, tbl, hll_packed);
+          if constexpr (kGbBatch) group_ring_batch<MODE, kBatch, kRingGB, kRec>(q, seg, ring, tail, 64 * kBatch, tbl, hll_packed);
           else agg_ring_batch<NA>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0);
           tail += 64 * kBatch;
         }
@@ -858,7 +860,7 @@ void agg_kernel(const DevAggQuery *qptr) {
       // every doc of the tile matched: consecutive chunks, coalesced column reads
       for (int c = 0; c < nvalid; c += 64) {
         const bool act = c + lane < nvalid;
-        do_chunk<NA, MODE>(q, seg, act ? doc0 + c + lane : 0, act, acc, hll_lds, tbl, hll_packed);
+        do_chunk<NA, MODE, kRec>(q, seg, act ? doc0 + c + lane : 0, act, acc, hll_lds, tbl, hll_packed);
       }
     } else {
       uint32_t any = wave_or32(m);
@@ -872,7 +874,7 @@ void agg_kernel(const DevAggQuery *qptr) {
         if (head - tail >= 64) {
           const int32_t doc = (int32_t)ring[(tail + lane) & (R - 1)];
           tail += 64;
-          do_chunk<NA, MODE>(q, seg, doc, true, acc, hll_lds, tbl, hll_packed);
+          do_chunk<NA, MODE, kRec>(q, seg, doc, true, acc, hll_lds, tbl, hll_packed);
         }
       }
     }
@@ -880,11 +882,11 @@ void agg_kernel(const DevAggQuery *qptr) {
   if constexpr (MODE == GB_NONE) {
     if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
   } else if constexpr (kGbBatch) {
-    if (head > tail) group_ring_batch<MODE>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
+    if (head > tail) group_ring_batch<MODE, kBatch, kRingGB, kRec>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
   } else if (head > tail) {
     const bool act = lane < head - tail;
     const int32_t doc = act ? (int32_t)ring[(tail + lane) & (R - 1)] : 0;
-    do_chunk<NA, MODE>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
+    do_chunk<NA, MODE, kRec>(q, segs[si], doc, act, acc, hll_lds, tbl, hll_packed);
   }
 
   // ---- workgroup epilogue --------------------------------------------------------------------
@@ -922,21 +924,21 @@ void agg_kernel(const DevAggQuery *qptr) {
   }
 }
 
-template <int NA, int MODE, bool D, int W>
+template <int NA, int MODE, bool D, int W, bool R = false>
 hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1) {
   if (lds > 65536) {
     // once per instantiation (a magic static: thread-safe under concurrent queries)
     static const hipError_t configured =
-        hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D, W>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+        hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D, W, R>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
     if (configured != hipSuccess) return configured;
   }
   if (e0 != nullptr) {  // timing carried by the dispatch packet itself (hipExtLaunchKernel)
     void *args[] = {(void *)&q};
-    return hipExtLaunchKernel((const void *)agg_kernel<NA, MODE, D, W>, dim3(nblocks), dim3(W * kWave), args, lds, s, e0,
+    return hipExtLaunchKernel((const void *)agg_kernel<NA, MODE, D, W, R>, dim3(nblocks), dim3(W * kWave), args, lds, s, e0,
                               e1, 0);
   }
-  agg_kernel<NA, MODE, D, W><<<nblocks, W * kWave, lds, s>>>(q);
+  agg_kernel<NA, MODE, D, W, R><<<nblocks, W * kWave, lds, s>>>(q);
   return hipGetLastError();
 }
 

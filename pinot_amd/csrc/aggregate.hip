@@ -405,12 +405,19 @@ static inline int grid_for(int64_t n, int per_block = 256, int cap = 4096) {
 }
 
 // the agg_kernel variants, instantiated in agg_k_*.hip (one translation unit per group)
-template <int NA, int MODE, bool D = false, int W = kAggWaves>
+template <int NA, int MODE, bool D = false, int W = kAggWaves, bool R = false>
 hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 
 // q: host copy (for the variant choice); dq: the same descriptor in device memory.
 hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0,
                       hipEvent_t e1) {
+  if (q.mode == GB_LDS && q.rec_on) {  // (group-by records: the variants that read them)
+    if (q.wg_waves == 16)
+      return q.dense_batch ? launch_agg_t<1, GB_LDS, true, 16, true>(dq, nblocks, lds, s, e0, e1)
+                           : launch_agg_t<1, GB_LDS, false, 16, true>(dq, nblocks, lds, s, e0, e1);
+    return q.dense_batch ? launch_agg_t<1, GB_LDS, true, kAggWaves, true>(dq, nblocks, lds, s, e0, e1)
+                         : launch_agg_t<1, GB_LDS, false, kAggWaves, true>(dq, nblocks, lds, s, e0, e1);
+  }
   if (q.mode == GB_LDS && q.wg_waves == 16)
     return q.dense_batch ? launch_agg_t<1, GB_LDS, true, 16>(dq, nblocks, lds, s, e0, e1)
                          : launch_agg_t<1, GB_LDS, false, 16>(dq, nblocks, lds, s, e0, e1);

@@ -212,6 +212,9 @@ struct DevSeg {
                         // the lane-major tile layout directly
   ConjLeaf conj_leaf[kMaxConj];
   StageSrc stage[kMaxStage];
+  DevCol cols[kMaxQueryColumns];
+  // (after the columns: the hot walks' column descriptors keep their scalar-cache alignment -- with these fields
+  // ahead of them, Q3.1's batched walk, which reads no record, ran 0.47 -> 0.53 ms)
   // Group-by record (Segment::records, materialize_record_kernel): every field a matched doc's group-by update reads
   // -- its key ids, its aggregations' packed values / value ids, its HLL entries -- packed into rec_words u32 per doc
   // (field f at bits [rec_off[f], rec_off[f] + rec_bits[f]) of the doc's record, LSB first), so a doc costs one
@@ -221,7 +224,6 @@ struct DevSeg {
   int32_t rec_nf;
   uint8_t rec_off[kRecFields];
   uint8_t rec_bits[kRecFields];
-  DevCol cols[kMaxQueryColumns];
 };
 
 struct DevNode {
@@ -350,11 +352,11 @@ struct DevAggQuery {
                            // program's docs in its own row 1 + a (row 0 counts the docs of every program: presence)
   const DevFinal *fin;     // GB_NONE: non-null when this launch is the plan's last (agg_common.h finalize_tail)
   int32_t wg_waves;        // waves per workgroup of the launch (kAggWaves; 16 for a GB_LDS table that leaves one
-  int32_t pad_w;           // 8-wave workgroup per CU)
-  int8_t rec_fa[kMaxAggs];  // group-by record (DevSeg.rec): the field of aggregation a's input a / b / HLL entry
-  int8_t rec_fb[kMaxAggs];  // (-1: none; the key columns are fields 0 .. num_group_by - 1)
+  int32_t rec_on;          // 8-wave workgroup per CU) | 1: some segment has a group-by record (agg_kernel R variant)
   int64_t xcd_words;       // GB_XCD: u64 words of one table copy ((1 + num_aggs) x num_groups)
   int64_t xcd_hll_words;   // GB_XCD: u32 words of one copy's HLL registers (num_hll x num_groups x m)
+  int8_t rec_fa[kMaxAggs];  // group-by record (DevSeg.rec): the field of aggregation a's input a / b / HLL entry
+  int8_t rec_fb[kMaxAggs];  // (-1: none; the key columns are fields 0 .. num_group_by - 1)
 };
 
 // Selection (row-returning) queries (select.hip): SelectionOnlyOperator per segment + the combine's concatenation.

@@ -3830,6 +3830,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       // vs 0.77); with group-by records the batched walk wins there too (C5 0.63 -> 0.61, profiles/r06w_rec_ab.log).
       bool any_rec = false;
       for (const DevSeg &d : dsegs) any_rec |= d.rec != nullptr;
+      dq.rec_on = any_rec ? 1 : 0;  // (the agg_kernel variant that reads them)
       P.walk_adaptive = (nhll == 0 || any_rec) && !gbb && !gw && !fused_gb && P.walk[0].ok && P.walk[1].ok;
       P.walk_cur = batched ? 1 : 0;
     }
@@ -3837,6 +3838,10 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     agg_lds += (size_t)nhll * m_regs * 4;
   }
   if (dq.wg_waves == 0) dq.wg_waves = kAggWaves;
+  if (dq.mode != GB_LDS || fused_gb) {  // only the LDS-table walks read group-by records (the segments keep theirs)
+    dq.rec_on = 0;
+    for (DevSeg &d : dsegs) d.rec = nullptr;
+  }
   int agg_blocks = (int)std::min<int64_t>((int64_t)dev->num_cus * agg_bpc, ceil_div(total_work, dq.wg_waves));
   agg_blocks = (int)round_up(std::max(agg_blocks, 8), 8);  // the XCD walk needs a multiple of 8 workgroups
   if (P.walk_cur >= 0) agg_blocks = P.walk[P.walk_cur].blocks;
