@@ -3483,6 +3483,15 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
       if (rc) return rc;
     }
     if (made) HIP_TRY(hipStreamSynchronize(st));
+    // A few record segments do not pay for the record variant's larger kernel on all the others (Q3.1: records on
+    // its sparse edge segments only ran 0.47 -> 0.52 ms, profiles/r06zj_trace.log): records for most docs, or none.
+    int64_t rec_docs = 0, all_docs = 0;
+    for (const DevSeg &d : dsegs) {
+      all_docs += d.num_docs;
+      rec_docs += d.rec != nullptr ? d.num_docs : 0;
+    }
+    if (rec_min_fields > 1 && 2 * rec_docs < all_docs)
+      for (DevSeg &d : dsegs) d.rec = nullptr;
   }
   // Fused aggregation (filter.hip fused_tile): every segment on the conjunctive path, aggregation only
   // (no group-by, no HLL), at most 4 slots, a filter to fuse into. Value columns are then streamed with
@@ -5156,6 +5165,11 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   if (P.walk_adaptive && group_by) {  // the next execution's group-by walk, from this one's matched docs
     const int64_t m = has_filter ? (int64_t)fin[32] : docs_in_work;
     const int want = m >= kWalkBatchDocsPerCu * (int64_t)dev->num_cus ? 1 : 0;
+    static const bool walk_trace = getenv("PHIP_WALK_TRACE") != nullptr;  // measurement: the walk switches
+    if (walk_trace)
+      fprintf(stderr, "phip_walk matched %lld cur %d want %d blocks %d/%d lds %zu/%zu waves %d/%d rec %d\n",
+              (long long)m, P.walk_cur, want, P.walk[0].blocks, P.walk[1].blocks, P.walk[0].lds, P.walk[1].lds,
+              P.walk[0].waves, P.walk[1].waves, P.dq.rec_on);
     if (want != P.walk_cur) {
       P.walk_cur = want;
       P.dq.dense_batch = P.walk[want].batched ? 1 : 0;

@@ -39,6 +39,10 @@ def main():
     ap.add_argument("--sql", action="append", default=[],
                     help="NAME::SQL -- an extra query over the SSB columns (e.g. a C5 variant without its HLL), usable "
                          "in --queries by NAME")
+    ap.add_argument("--hog-gib", type=float, default=0.0,
+                    help="allocate (and zero) this many GiB of HBM beside the segments first: does resident memory the "
+                         "queries never touch slow them (the group-by records' residency effect)?")
+    ap.add_argument("--hog-chunk-mib", type=int, default=1024, help="size of each --hog-gib allocation")
     ap.add_argument("--gap", type=float, default=0.0,
                     help="seconds of idle GPU before each (query, setting): tools/trace_summary.py splits a rocprofv3 "
                          "kernel trace of this run into the queries at these gaps")
@@ -66,6 +70,19 @@ def main():
                 if not ci.metadata.is_sorted:
                     ci.forward = b""
     print(json.dumps({"loaded_segments": len(gsegs), "load_s": round(time.time() - t0, 1)}), flush=True)
+    hogs = []
+    if args.hog_gib > 0:
+        hip = ctypes.CDLL("libamdhip64.so")
+        left = int(args.hog_gib * (1 << 30))
+        while left > 0:
+            n = min(left, args.hog_chunk_mib << 20)
+            p = ctypes.c_void_p()
+            if hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n)) != 0:
+                raise SystemExit("hipMalloc failed")
+            hip.hipMemset(p, 0, ctypes.c_size_t(n))
+            hogs.append(p)
+            left -= n
+        hip.hipDeviceSynchronize()
     base_env = dict(os.environ)
     for q in queries:
         qc = parse(ssb.SSB_QUERIES[q])
