@@ -656,7 +656,7 @@ class GpuCombineOperator:
     def run_raw(self, prepare_only=False):
         """One execution of the prepared plan (phip_plan_create once per operator, then phip_plan_execute:
         InstancePlanMakerImplV2's Plan run by GlobalPlanImplV0.execute)."""
-        lib = _lib.load()
+        lib = getattr(self, "_lib", None) or _lib.load()  # (the loaded library, kept once the plan exists)
         if getattr(self, "_plan", None) is None:
             keep = []
             q = self._desc(keep)
@@ -851,7 +851,7 @@ class GpuCombineOperator:
             if self.segments else None
 
     def _block_from_result(self, res):
-        lib = _lib.load()
+        lib = getattr(self, "_lib", None) or _lib.load()
         if not self.query.group_by:
             blk = self._aggregation_block(res)
             if blk is not None:
