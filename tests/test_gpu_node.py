@@ -260,3 +260,16 @@ def test_gpu_node_hash_full_falls_back(mixed, monkeypatch):
     qc, blk, parts, kind = _run("SELECT h, g, COUNT(*), SUM(m) FROM t GROUP BY h, g LIMIT 100000", segs, monkeypatch, 2)
     assert kind == _lib.EXCHANGE_RECORDS
     _check(qc, blk, raws)
+
+
+@pytest.mark.parametrize("split", [2, 3])
+@pytest.mark.parametrize("sql", [MIXED[0][0], MIXED[1][0], MIXED[3][0]], ids=["r0", "r1", "r3"])
+def test_gpu_node_with_group_records(sql, split, mixed, monkeypatch):
+    """Node parts whose aggregation walks read group-by records (PHIP_GB_RECORD=1, values materialized): the dense
+    partial tables still merge on the devices and equal the oracle."""
+    raws, segs = mixed
+    monkeypatch.setenv("PHIP_GB_RECORD", "1")
+    monkeypatch.setenv("PHIP_MATERIALIZE_MIN_DICT", "0")
+    qc, blk, parts, kind = _run(sql, segs, monkeypatch, split)
+    assert parts == split and kind == _lib.EXCHANGE_PEER, (parts, kind)
+    _check(qc, blk, raws)
