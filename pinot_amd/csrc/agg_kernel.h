@@ -8,13 +8,51 @@
 
 namespace phip {
 
+// GB_NONE id histogram (DevAggQuery.hist_aggs, the kHist variants): per-wave LDS bins of two u16 counts per word,
+// indexed by the segment's dictionary id of hist_col; n = an upper bound of the docs counted since the last flush, so
+// no count passes 65535.
+struct HistCtx {
+  lds_u32 *bins;
+  int n;
+};
+// The bins folded into the accumulators (the segment's dictionary values: sum += count x value, min / max over the
+// ids that occurred) and cleared. Wave-local: the wave's own LDS operations complete in order.
+template <int NA>
+__device__ __forceinline__ void hist_flush(cquery_t &q, cseg_t &seg, uint64_t (&acc)[NA], HistCtx &hc) {
+  const int lane = lane_id();
+  ccol_t &c = seg.cols[q.hist_col];
+#pragma unroll
+  for (int a = 0; a < NA; a++) {
+    if (a >= q.num_aggs) break;
+    if (!((q.hist_aggs >> a) & 1u)) continue;
+    const int kind = q.aggs[a].acc;
+    if (kind == ACC_SUM_I64) {
+      for (int i = lane; i < c.card; i += 64) {
+        const uint32_t cnt = (hc.bins[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+        if (cnt) acc[a] += (uint64_t)cnt * (uint64_t)dict_i64(c, (uint32_t)i);
+      }
+    } else {
+      double cur = as_f64(acc[a]);
+      for (int i = lane; i < c.card; i += 64) {
+        const uint32_t cnt = (hc.bins[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+        if (!cnt) continue;
+        const double v = dict_f64(c, (uint32_t)i);
+        cur = kind == ACC_MIN_F64 ? fmin(cur, v) : fmax(cur, v);
+      }
+      acc[a] = as_u64(cur);
+    }
+  }
+  for (int i = lane; i < q.hist_words; i += 64) hc.bins[i] = 0;
+  hc.n = 0;
+}
+
 // U docs per lane (d[u], act bit u = doc d[u] matched; inactive entries hold a valid doc and contribute the
 // identity): every load of the U docs is issued before the first use. staged: dict ids of the stage slots
 // come from the wave's LDS stage at tile-relative doc td + 64u (the dense-tile walk); otherwise from HBM.
-template <int NA, int U>
+template <int NA, int U, bool H = false>
 __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t (&d)[U], uint32_t act,
                                          const PHIP_LDS uint8_t *stg, int32_t td, bool staged, uint64_t (&acc)[NA],
-                                         lds_u32 *hll_lds) {
+                                         lds_u32 *hll_lds, HistCtx *hc = nullptr) {
 #pragma unroll
   for (int a = 0; a < NA; a++) {
     if (a >= q.num_aggs) break;
@@ -25,6 +63,18 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
     const int ja = ka < 0 ? 0 : ka, jb = kb < 0 ? 0 : kb;
     const BatchSrc sa{ka >= 0 ? (const PHIP_LDS uint32_t *)(stg + q.stage_off[ja]) : nullptr, td, act,
                       ka >= 0 && q.stage_dict_off[ja] >= 0 ? stg + q.stage_dict_off[ja] : nullptr};
+    if constexpr (H) {
+      if ((q.hist_aggs >> a) & 1u) {  // counted per id (the first such aggregation; the others share its bins)
+        if (a == __builtin_ctz(q.hist_aggs)) {
+          uint32_t id[U];
+          batch_ids<U>(seg.cols[ag.col_a], d, sa, id);
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if ((act >> u) & 1u) __hip_atomic_fetch_add(&hc->bins[id[u] >> 1], 1u << ((id[u] & 1u) * 16), PHIP_RLX, PHIP_WG);
+        }
+        continue;
+      }
+    }
     const BatchSrc sb{kb >= 0 ? (const PHIP_LDS uint32_t *)(stg + q.stage_off[jb]) : nullptr, td, act,
                       kb >= 0 && q.stage_dict_off[jb] >= 0 ? stg + q.stage_dict_off[jb] : nullptr};
     if (kind == ACC_COUNT) {
@@ -79,17 +129,21 @@ __device__ __forceinline__ void agg_docs(cquery_t &q, cseg_t &seg, const int32_t
       acc[a] = as_u64(cur);
     }
   }
+  if constexpr (H) {
+    hc->n += 64 * U;
+    if (hc->n > 65535 - 64 * U) hist_flush<NA>(q, seg, acc, *hc);
+  }
 }
 
 // Groups [g0, g0 + U) of a tile; act bit u = doc 64(g0 + u) + lane matched. Accumulation order per
 // lane is the doc order, as in agg_chunk.
-template <int NA, int U>
+template <int NA, int U, bool H = false>
 __device__ __forceinline__ void agg_batch(cquery_t &q, cseg_t &seg, int32_t doc, uint32_t act, int32_t safe,
                                           const PHIP_LDS uint8_t *stg, int32_t td, uint64_t (&acc)[NA],
-                                          lds_u32 *hll_lds) {
+                                          lds_u32 *hll_lds, HistCtx *hc = nullptr) {
   int32_t d[U];
   batch_docs<U>(doc, act, safe, d);
-  agg_docs<NA, U>(q, seg, d, act, stg, td, true, acc, hll_lds);
+  agg_docs<NA, U, H>(q, seg, d, act, stg, td, true, acc, hll_lds, hc);
 }
 
 // Up to kBatch chunks of 64 ring entries at once (GB_NONE): chunk u holds ring[tail + 64u + lane] while
@@ -97,9 +151,10 @@ __device__ __forceinline__ void agg_batch(cquery_t &q, cseg_t &seg, int32_t doc,
 // per 64. Per lane the docs stay in ring (= doc) order.
 constexpr int kRing = kRingAgg;  // agg_ring_batch runs in GB_NONE only
 
-template <int NA>
+template <int NA, bool H = false>
 __device__ __forceinline__ void agg_ring_batch(cquery_t &q, cseg_t &seg, const lds_u32 *ring, int tail, int n,
-                                               uint64_t (&acc)[NA], lds_u32 *hll_lds, int32_t safe) {
+                                               uint64_t (&acc)[NA], lds_u32 *hll_lds, int32_t safe,
+                                               HistCtx *hc = nullptr) {
   const int lane = lane_id();
   int32_t d[kBatch];
   uint32_t act = 0;
@@ -109,7 +164,7 @@ __device__ __forceinline__ void agg_ring_batch(cquery_t &q, cseg_t &seg, const l
     d[u] = on ? (int32_t)ring[(tail + 64 * u + lane) & (kRing - 1)] : safe;
     act |= on ? (1u << u) : 0u;
   }
-  agg_docs<NA, kBatch>(q, seg, d, act, nullptr, 0, false, acc, hll_lds);
+  agg_docs<NA, kBatch, H>(q, seg, d, act, nullptr, 0, false, acc, hll_lds, hc);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -673,7 +728,7 @@ __device__ __forceinline__ void do_chunk(cquery_t &q, cseg_t &seg, int32_t doc, 
 // W: waves per workgroup (8; 16 for an LDS group table so large that one workgroup fills the CU's LDS -- twice the
 // waves share the one table, so the CU keeps 16 waves of gathers in flight instead of 8: DevAggQuery.wg_waves).
 // kRec: the group-by record variant (DevAggQuery.rec_on: some segment has a DevSeg.rec; GB_LDS only).
-template <int NA, int MODE, bool kDense, int W = kAggWaves, bool kRec = false>
+template <int NA, int MODE, bool kDense, int W = kAggWaves, bool kRec = false, bool kHist = false>
 __global__ __launch_bounds__(W * kWave, (MODE == GB_LDS || MODE == GB_GLOBAL) && kDense ? 6 : 1)
 void agg_kernel(const DevAggQuery *qptr) {
   constexpr int kBlock = W * kWave;
@@ -697,6 +752,11 @@ void agg_kernel(const DevAggQuery *qptr) {
   if (MODE == GB_NONE && q.num_hll > 0) {
     hll_words = q.num_hll << q.log2m;
     for (int i = threadIdx.x; i < hll_words; i += kBlock) hll_lds[i] = 0;
+  }
+  HistCtx hc{nullptr, 0};  // (kHist: the wave's id bins after the HLL registers)
+  if constexpr (kHist) {
+    hc.bins = (lds_u32 *)rest + (size_t)hll_words + (size_t)wave * q.hist_words;
+    for (int i = lane; i < q.hist_words; i += 64) hc.bins[i] = 0;
   }
   if (MODE == GB_LDS) {
     const int G = (int)q.num_groups;
@@ -746,7 +806,8 @@ void agg_kernel(const DevAggQuery *qptr) {
     }
     if (segs[si].work_begin + segs[si].num_work <= t) {
       if constexpr (MODE == GB_NONE) {
-        if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
+        if (head > tail) agg_ring_batch<NA, kHist>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0, &hc);
+        if constexpr (kHist) hist_flush<NA>(q, segs[si], acc, hc);  // (the segment's dictionary goes)
       } else if constexpr (kGbBatch) {
         if (head > tail) group_ring_batch<MODE, kBatch, kRingGB, kRec>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
       } else if (head > tail) {  // leftover (< 64) matched docs of the previous segment
@@ -802,7 +863,7 @@ void agg_kernel(const DevAggQuery *qptr) {
       for (int g0 = 0; g0 < kTileGroups; g0 += kBatch) {
         const uint32_t act = __builtin_bitreverse32(m << g0) & ((1u << kBatch) - 1u);
         if (ballot(act != 0) == 0) continue;
-        agg_batch<NA, kBatch>(q, seg, doc0 + 64 * g0 + lane, act, doc0, stg, 64 * g0 + lane, acc, hll_lds);
+        agg_batch<NA, kBatch, kHist>(q, seg, doc0 + 64 * g0 + lane, act, doc0, stg, 64 * g0 + lane, acc, hll_lds, &hc);
       }
       if (q.num_stage > 0) __builtin_amdgcn_wave_barrier();  // LDS reads done before the next tile's DMA
       continue;
@@ -850,7 +911,7 @@ void agg_kernel(const DevAggQuery *qptr) {
         head = head0 + pend;
         while (head - tail >= 64 * kBatch) {
           if constexpr (kGbBatch) group_ring_batch<MODE, kBatch, kRingGB, kRec>(q, seg, ring, tail, 64 * kBatch, tbl, hll_packed);
-          else agg_ring_batch<NA>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0);
+          else agg_ring_batch<NA, kHist>(q, seg, ring, tail, 64 * kBatch, acc, hll_lds, 0, &hc);
           tail += 64 * kBatch;
         }
       }
@@ -880,7 +941,8 @@ void agg_kernel(const DevAggQuery *qptr) {
     }
   }
   if constexpr (MODE == GB_NONE) {
-    if (head > tail) agg_ring_batch<NA>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0);
+    if (head > tail) agg_ring_batch<NA, kHist>(q, segs[si], ring, tail, head - tail, acc, hll_lds, 0, &hc);
+    if constexpr (kHist) hist_flush<NA>(q, segs[si], acc, hc);
   } else if constexpr (kGbBatch) {
     if (head > tail) group_ring_batch<MODE, kBatch, kRingGB, kRec>(q, segs[si], ring, tail, head - tail, tbl, hll_packed);
   } else if (head > tail) {
@@ -924,21 +986,21 @@ void agg_kernel(const DevAggQuery *qptr) {
   }
 }
 
-template <int NA, int MODE, bool D, int W, bool R = false>
+template <int NA, int MODE, bool D, int W, bool R = false, bool Hs = false>
 hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1) {
   if (lds > 65536) {
     // once per instantiation (a magic static: thread-safe under concurrent queries)
     static const hipError_t configured =
-        hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D, W, R>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
+        hipFuncSetAttribute((const void *)agg_kernel<NA, MODE, D, W, R, Hs>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840 - 1024);
     if (configured != hipSuccess) return configured;
   }
   if (e0 != nullptr) {  // timing carried by the dispatch packet itself (hipExtLaunchKernel)
     void *args[] = {(void *)&q};
-    return hipExtLaunchKernel((const void *)agg_kernel<NA, MODE, D, W, R>, dim3(nblocks), dim3(W * kWave), args, lds, s, e0,
+    return hipExtLaunchKernel((const void *)agg_kernel<NA, MODE, D, W, R, Hs>, dim3(nblocks), dim3(W * kWave), args, lds, s, e0,
                               e1, 0);
   }
-  agg_kernel<NA, MODE, D, W, R><<<nblocks, W * kWave, lds, s>>>(q);
+  agg_kernel<NA, MODE, D, W, R, Hs><<<nblocks, W * kWave, lds, s>>>(q);
   return hipGetLastError();
 }
 

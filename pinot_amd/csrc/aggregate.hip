@@ -405,7 +405,7 @@ static inline int grid_for(int64_t n, int per_block = 256, int cap = 4096) {
 }
 
 // the agg_kernel variants, instantiated in agg_k_*.hip (one translation unit per group)
-template <int NA, int MODE, bool D = false, int W = kAggWaves, bool R = false>
+template <int NA, int MODE, bool D = false, int W = kAggWaves, bool R = false, bool H = false>
 hipError_t launch_agg_t(const DevAggQuery *q, int nblocks, size_t lds, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 
 // q: host copy (for the variant choice); dq: the same descriptor in device memory.
@@ -427,6 +427,10 @@ hipError_t launch_agg(const DevAggQuery &q, const DevAggQuery *dq, int nblocks, 
     return q.dense_batch ? launch_agg_t<1, GB_GLOBAL, true>(dq, nblocks, lds, s, e0, e1)
                          : launch_agg_t<1, GB_GLOBAL>(dq, nblocks, lds, s, e0, e1);
   if (q.mode == GB_HASH) return launch_agg_t<1, GB_HASH>(dq, nblocks, lds, s, e0, e1);
+  if (q.dense_batch && q.hist_aggs) {  // (the id-histogram variants: one or two aggregations)
+    if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE, true, kAggWaves, false, true>(dq, nblocks, lds, s, e0, e1);
+    return launch_agg_t<2, GB_NONE, true, kAggWaves, false, true>(dq, nblocks, lds, s, e0, e1);
+  }
   if (q.dense_batch) {
     if (q.num_aggs <= 1) return launch_agg_t<1, GB_NONE, true>(dq, nblocks, lds, s, e0, e1);
     if (q.num_aggs <= 2) return launch_agg_t<2, GB_NONE, true>(dq, nblocks, lds, s, e0, e1);

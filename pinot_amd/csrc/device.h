@@ -357,6 +357,13 @@ struct DevAggQuery {
   int64_t xcd_hll_words;   // GB_XCD: u32 words of one copy's HLL registers (num_hll x num_groups x m)
   int8_t rec_fa[kMaxAggs];  // group-by record (DevSeg.rec): the field of aggregation a's input a / b / HLL entry
   int8_t rec_fb[kMaxAggs];  // (-1: none; the key columns are fields 0 .. num_group_by - 1)
+  // GB_NONE id histogram (agg_kernel kHist): the aggregations in hist_aggs (SUM / MIN / MAX of one small-dictionary
+  // INT / LONG column, hist_col) count the docs per dictionary id in per-wave LDS bins (two u16 per u32 word,
+  // hist_words per wave) and fold count x value into their accumulators when a segment ends -- no dictionary gather
+  uint32_t hist_aggs;
+  int32_t hist_col;
+  int32_t hist_words;
+  int32_t hist_pad;
 };
 
 // Selection (row-returning) queries (select.hip): SelectionOnlyOperator per segment + the combine's concatenation.

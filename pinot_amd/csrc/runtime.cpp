@@ -2054,6 +2054,9 @@ struct Plan {
   GbWalk walk[2];
   int walk_cur = -1;
   bool walk_adaptive = false;
+  // GB_NONE id histogram (DevAggQuery.hist_aggs): its aggregations, and the launch's LDS with / without the bins
+  uint32_t hist_mask = 0;
+  size_t agg_lds_hist = 0, agg_lds_plain = 0;
   bool want_bitmap = false;
   int64_t filter_nwords = 0;
   int filter_blocks = 1, agg_blocks = 8;
@@ -2219,6 +2222,7 @@ static int32_t raw_string_leaf(const phip_filter_node &fn, DevNode &dn, Blob &bl
 // kernel then reads one 16-byte record per matched doc instead of one line per column (agg_kernel.h rec_load).
 // A segment whose columns do not all fit (raw / null / FLOAT-id keys, raw typed values, HLL without doc-order entries)
 // keeps its columns' layouts: the kernel decides per segment.
+constexpr int kHistCard = 2048;    // agg_kernel kHist: dictionary ids per LDS bin set (two u16 counts per word)
 constexpr int kRecMinFields = 3;   // fewer fields: the per-column gathers already touch few lines
 constexpr double kRecMaxRatio = 0.8;  // a record's touched bytes must stay below this fraction of the columns'
 constexpr int kMaxRecordSets = 16;                       // record signatures kept per segment
@@ -2584,6 +2588,43 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
     dq.dense_min = kDenseMin;
     const char *dm = getenv("PHIP_DENSE_MIN");  // measurement override
     if (dm) dq.dense_min = std::max(1, atoi(dm));
+    // Id histogram (agg_kernel kHist): SUM / MIN / MAX of one INT / LONG column whose dictionary has at most kHistCard
+    // ids in every segment count the docs per id in LDS and fold count x value in at each segment's end -- the
+    // per-doc dictionary gather goes (C4 SUM(M), 1000 ids). Integer sums stay exact (count x value wraps as the
+    // repeated sum does); MIN / MAX do not depend on order. COUNTs beside them keep their own path.
+    dq.hist_aggs = 0;
+    dq.hist_col = -1;
+    dq.hist_words = 0;
+    {
+      const char *he = getenv("PHIP_AGG_HIST");  // measurement override: "0" = gather the values
+      bool ok = q->num_group_by == 0 && dq.dense_batch && nhll == 0 && nprog == 1 && naggs <= 2 && !(he && atoi(he) == 0);
+      int col = -1, max_card = 0;
+      uint32_t mask = 0;
+      for (int a = 0; a < naggs && ok; a++) {
+        const phip_aggregation &ag = q->aggregations[a];
+        if (dq.aggs[a].acc == ACC_COUNT) continue;
+        const int k = dq.aggs[a].acc;
+        if ((k != ACC_SUM_I64 && k != ACC_MIN_F64 && k != ACC_MAX_F64) || ag.expr != PHIP_EXPR_COLUMN ||
+            (col >= 0 && ag.column_a != col)) {
+          ok = false;
+          break;
+        }
+        col = ag.column_a;
+        mask |= 1u << a;
+        for (int s = 0; s < nseg && ok; s++) {
+          const ColumnStore &cs = segs[s]->cols[colidx[s][col]];
+          if (as_raw(s, col) || no_dict(cs) || (cs.type != PHIP_TYPE_INT && cs.type != PHIP_TYPE_LONG) ||
+              cs.card < 1 || cs.card > kHistCard)
+            ok = false;
+          else max_card = std::max(max_card, cs.card);
+        }
+      }
+      if (ok && mask) {
+        dq.hist_aggs = mask;
+        dq.hist_col = col;
+        dq.hist_words = (max_card + 1) / 2;
+      }
+    }
     // Stage the fixed-bit words of the gathered dictionary columns of a dense tile in LDS (one region
     // per distinct column, sized for its widest segment), when they fit kAggStageBudget per wave.
     for (int a = 0; a < kMaxAggs; a++) dq.stage_slot_a[a] = dq.stage_slot_b[a] = -1;
@@ -3846,6 +3887,7 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   } else if (nhll) {
     agg_lds += (size_t)nhll * m_regs * 4;
   }
+  if (!group_by && dq.hist_aggs) agg_lds += (size_t)kAggWaves * dq.hist_words * 4;  // (the waves' id bins)
   if (dq.wg_waves == 0) dq.wg_waves = kAggWaves;
   if (dq.mode != GB_LDS || fused_gb) {  // only the LDS-table walks read group-by records (the segments keep theirs)
     dq.rec_on = 0;
@@ -4113,6 +4155,17 @@ static int32_t prepare_plan(const phip_query_desc *q, bool want_bitmap, int64_t 
   P.agg_blocks = agg_blocks;
   P.filter_lds = filter_lds;
   P.agg_lds = agg_lds;
+  if (P.dq.hist_aggs) {
+    // The id histogram pays for its per-segment flush and LDS only when most docs match (C4 SUM(M): 50 % 1.33 ->
+    // 1.09 ms; 0.01-10 % slower, profiles/r06zt_hist_ab.log): the plan starts with the value gathers and takes the
+    // histogram from the execution after one whose matched docs reached kHistMinMatch of its docs. The device
+    // descriptor keeps hist_aggs; the host copy's decides which variant launches.
+    P.hist_mask = P.dq.hist_aggs;
+    P.agg_lds_hist = agg_lds;
+    P.agg_lds_plain = agg_lds - (size_t)kAggWaves * P.dq.hist_words * 4;
+    P.dq.hist_aggs = 0;
+    P.agg_lds = P.agg_lds_plain;
+  }
   P.base = base;
   P.tasks_off = tasks_off;
   P.rgroups_off = rgroups_off;
@@ -4590,6 +4643,7 @@ static int32_t execute_select(Plan &P, Workspace &ws, hipStream_t st, ResultImpl
 // group table, handed to the caller (phip_plan_execute_partial). EXEC_FINISH: compaction / trim / copy-out
 // of the caller-merged table (phip_plan_finish).
 enum { EXEC_FULL = 0, EXEC_PARTIAL = 1, EXEC_FINISH = 2 };
+constexpr int64_t kHistMinMatchNum = 3, kHistMinMatchDen = 10;  // Plan::hist_mask: matched >= 30 % of the docs
 constexpr int64_t kWalkBatchDocsPerCu = 6144;  // Plan::walk_adaptive: matched docs per CU from which the batched walk runs
 constexpr int32_t kGrowHash = -100;  // execute_plan: the hash table overflowed (internal status: execute_growing)
 static_assert(ACC_COUNT == PHIP_ROW_COUNT && ACC_SUM_I64 == PHIP_ROW_SUM_I64 && ACC_SUM_F64 == PHIP_ROW_SUM_F64 &&
@@ -5162,6 +5216,14 @@ static int32_t execute_plan(Plan &P, phip_result **out_result, uint64_t *filter_
   P.clean = true;
   P.partial_pending = false;
   lg.done = true;
+  if (P.hist_mask && !group_by) {  // the next execution's aggregation walk: the id histogram when most docs match
+    const int64_t m = has_filter ? (int64_t)fin[32] : docs_in_work;
+    const bool on = m * kHistMinMatchDen >= docs_in_work * kHistMinMatchNum;
+    P.dq.hist_aggs = on ? P.hist_mask : 0;
+    P.agg_lds = on ? P.agg_lds_hist : P.agg_lds_plain;
+    static const bool hist_trace = getenv("PHIP_WALK_TRACE") != nullptr;  // measurement: the walk switches
+    if (hist_trace) fprintf(stderr, "phip_hist matched %lld of %lld: %s\n", (long long)m, (long long)docs_in_work, on ? "on" : "off");
+  }
   if (P.walk_adaptive && group_by) {  // the next execution's group-by walk, from this one's matched docs
     const int64_t m = has_filter ? (int64_t)fin[32] : docs_in_work;
     const int want = m >= kWalkBatchDocsPerCu * (int64_t)dev->num_cus ? 1 : 0;
